@@ -1,0 +1,102 @@
+"""ctypes mirror of include/fddp_hip.h (structs, constants, prototypes).
+
+Shared by the product binding (crocoddyl_amd._lib, libfddp_hip.so) and the
+test harness binding of the CPU oracle (tests/oracle_lib.py, liboracle.so),
+which exports the same functions with an ``oracle_`` prefix.
+"""
+import ctypes as C
+
+FDDP_OK = 0
+FDDP_ERR_INVALID_ARG = -1
+FDDP_ERR_RUNTIME = -2
+FDDP_ERR_UNSUPPORTED = -3
+FDDP_ERR_NO_DEVICE = -4
+
+STATUS_RUNNING, STATUS_CONVERGED, STATUS_REGMAX = 0, 1, 2
+
+KNOT_LQR, KNOT_UNICYCLE, KNOT_EULER_DIFFLQR = 1, 2, 3
+PARAM_HEADER = 4
+
+Q_FX, Q_FU, Q_LXX, Q_LXU, Q_LUU, Q_LX, Q_LU, Q_XNEXT, Q_FS, Q_K, Q_KV = range(11)
+Q_VXX, Q_VX, Q_QXX, Q_QXU, Q_QUU, Q_QX, Q_QU = range(11, 18)
+
+
+class Dims(C.Structure):
+    _fields_ = [("nx", C.c_int32), ("ndx", C.c_int32), ("nu_max", C.c_int32), ("T", C.c_int32), ("B", C.c_int32)]
+
+
+class KnotDesc(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("nu", C.c_int32), ("param_offset", C.c_int64), ("param_stride", C.c_int64)]
+
+
+class Params(C.Structure):
+    _fields_ = [("th_acceptstep", C.c_double), ("th_stop", C.c_double), ("th_grad", C.c_double),
+                ("th_stepdec", C.c_double), ("th_stepinc", C.c_double), ("th_acceptnegstep", C.c_double),
+                ("regfactor", C.c_double), ("regmin", C.c_double), ("regmax", C.c_double),
+                ("n_alphas", C.c_int32), ("pad_", C.c_int32), ("alphas", C.c_double * 16)]
+
+
+class Result(C.Structure):
+    _fields_ = [("status", C.c_int32), ("iter", C.c_int32), ("is_feasible", C.c_int32), ("n_iter_run", C.c_int32),
+                ("cost", C.c_double), ("stop", C.c_double), ("xreg", C.c_double), ("ureg", C.c_double),
+                ("steplength", C.c_double), ("dV", C.c_double), ("dVexp", C.c_double), ("d0", C.c_double),
+                ("d1", C.c_double)]
+
+
+P = C.c_void_p
+D = C.POINTER(C.c_double)
+I32 = C.POINTER(C.c_int32)
+
+# name -> (restype, argtypes); `h` is an opaque handle pointer
+PROTOS = {
+    "default_params": (None, [C.POINTER(Params)]),
+    "destroy": (None, [P]),
+    "last_error": (C.c_char_p, []),
+    "set_x0": (C.c_int, [P, D]),
+    "set_params": (C.c_int, [P, C.POINTER(Params)]),
+    "set_candidate": (C.c_int, [P, D, D, C.c_int]),
+    "solve": (C.c_int, [P, C.c_int, C.c_int, C.c_double, C.POINTER(Result)]),
+    "get_results": (C.c_int, [P, C.POINTER(Result)]),
+    "problem_calc": (C.c_int, [P, D]),
+    "problem_calc_diff": (C.c_int, [P, D]),
+    "compute_direction": (C.c_int, [P, C.c_int, I32]),
+    "update_expected_improvement": (C.c_int, [P]),
+    "try_step": (C.c_int, [P, C.c_double, D, I32]),
+    "expected_improvement": (C.c_int, [P, D]),
+    "stopping_criteria": (C.c_int, [P, D]),
+    "set_solver_state": (C.c_int, [P, C.c_int, C.c_double, C.c_double, C.c_int]),
+    "get_quantity": (C.c_int, [P, C.c_int, D]),
+    "mpc_shift": (C.c_int, [P]),
+}
+
+# product-only entry points (libfddp_hip)
+PROTOS_GPU = {
+    "create": (C.c_int, [C.POINTER(Dims), C.POINTER(KnotDesc), D, C.c_int64, C.c_int, C.POINTER(P)]),
+    "set_model_params": (C.c_int, [P, D, C.c_int64]),
+    "get_x0": (C.c_int, [P, D]),
+    "get_params": (C.c_int, [P, C.POINTER(Params)]),
+    "get_xs": (C.c_int, [P, D, C.c_int]),
+    "get_us": (C.c_int, [P, D, C.c_int]),
+    "get_xs_try": (C.c_int, [P, D]),
+    "get_us_try": (C.c_int, [P, D]),
+    "set_debug": (C.c_int, [P, C.c_int]),
+    "synchronize": (C.c_int, [P]),
+    "get_stream": (C.c_int, [P, C.POINTER(P)]),
+    "get_timing": (C.c_int, [P, D, C.POINTER(C.c_int64)]),
+    "set_timing": (C.c_int, [P, C.c_int]),
+    "device_bytes": (C.c_int64, [P]),
+}
+
+
+def bind(lib, prefix, protos):
+    for name, (res, args) in protos.items():
+        fn = getattr(lib, prefix + name)
+        fn.restype = res
+        fn.argtypes = args
+
+
+def dptr(a):
+    """double* of a C-contiguous float64 numpy array (or None)."""
+    if a is None:
+        return None
+    return a.ctypes.data_as(D)

@@ -1,0 +1,45 @@
+"""Loader of the in-tree HIP library (crocoddyl_amd/lib/libfddp_hip.so).
+
+There is no CPU fallback: if the library is missing or no gfx950 device is
+usable, every solver entry point raises. Build it with
+``python -c "import __graft_entry__ as g; g.build()"`` or ``make -C crocoddyl_amd/csrc``.
+"""
+import ctypes as C
+import os
+
+from . import _abi
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libfddp_hip.so")
+
+_lib = None
+
+
+class FDDPError(RuntimeError):
+    """Raised for argument errors (the reference's throw_pretty) and runtime failures."""
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"crocoddyl_amd: HIP library not built ({LIB_PATH} missing); "
+                              "run __graft_entry__.build() — there is no CPU fallback")
+        L = C.CDLL(LIB_PATH)
+        _abi.bind(L, "fddp_", _abi.PROTOS)
+        _abi.bind(L, "fddp_", _abi.PROTOS_GPU)
+        _lib = L
+    return _lib
+
+
+def check(rc):
+    if rc != _abi.FDDP_OK:
+        msg = lib().fddp_last_error().decode(errors="replace")
+        raise FDDPError(f"libfddp_hip error {rc}: {msg}")
+    return rc
+
+
+def default_params():
+    p = _abi.Params()
+    lib().fddp_default_params(C.byref(p))
+    return p

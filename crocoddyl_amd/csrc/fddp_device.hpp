@@ -1,0 +1,143 @@
+// Device-side data layout, per-element solver state and workgroup helpers
+// shared by the libfddp_hip kernels (gfx950, wave64).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/fddp_hip.h"
+
+namespace fddp {
+
+constexpr int kWave = 64;
+
+// Per-element FDDP state machine (SolverAbstract/SolverDDP/SolverFDDP members,
+// solver-base.hpp:230-276, ddp.hpp:270-306, fddp.hpp:95-101).
+struct ElemState {
+  double cost;        // cost_
+  double cost_try;    // cost_try_
+  double stop;        // stop_
+  double xreg, ureg;  // xreg_, ureg_
+  double steplength;  // steplength_
+  double dV, dVexp;   // dV_, dVexp_
+  double dg, dq, dv;  // dg_, dq_, dv_
+  double d0, d1;      // d_
+  int32_t is_feasible, was_feasible;
+  int32_t recalc;      // recalcDiff
+  int32_t iter;        // iter_
+  int32_t status;      // FDDP_STATUS_*
+  int32_t active;      // still iterating inside fddp_solve
+  int32_t cur;         // which of the two trajectory buffers holds xs_/us_
+  int32_t n_iter_run;  // loop bodies executed
+  int32_t bwd_fail;    // last backward pass raised backward_error
+  int32_t fwd_fail;    // last trial raised forward_error
+};
+
+static_assert(sizeof(ElemState) % 8 == 0, "ElemState alignment");
+
+__host__ __device__ inline int64_t pad2(int64_t v) { return (v + 1) & ~int64_t(1); }
+
+// All device buffers of one handle. Every per-knot array is [b][t][...] with
+// the per-knot stride padded to an even number of doubles (16-B aligned rows).
+struct Dev {
+  int nx, n, m, T, B;  // n = ndx, m = nu_max
+  int64_t sX, sN, sM, sNN, sNM, sMM;
+  const fddp_knot_desc* knots;  // T+1
+  const double* params;
+  double* x0;                // [B][sX]
+  double* xs[2];             // [B][T+1][sX]
+  double* us[2];             // [B][T][sM]
+  double* xnext[2];          // [B][T][sX]   data[t].xnext of that trajectory
+  double* kcost[2];          // [B][T+1]     data[t].cost of that trajectory
+  double *Fx, *Fu, *Lxx, *Lxu, *Luu, *Lx, *Lu;  // [B][T+1][...]
+  double* fs;                // [B][T+1][sN]
+  double* K;                 // [B][T][sNM]  (nu x ndx, ld = m)
+  double* k;                 // [B][T][sM]
+  double* Vxxfs;             // [B][T+1][sN] Vxx[t] * fs[t]
+  double* part;              // [B][T+1][8]  per-knot reduction terms
+  double* dvp;               // [B][T+1]     per-knot expectedImprovement terms
+  // debug per-knot stores (null unless fddp_set_debug)
+  double *dVxx, *dVx, *dQxx, *dQxu, *dQuu, *dQx, *dQu;
+  ElemState* st;             // [B]
+
+  __device__ __host__ int64_t knot(int b, int t) const { return (int64_t)b * (T + 1) + t; }
+  __device__ __host__ int64_t run(int b, int t) const { return (int64_t)b * T + t; }
+  __device__ __host__ const double* pblock(int b, int t) const {
+    return params + knots[t].param_offset + (int64_t)b * knots[t].param_stride;
+  }
+};
+
+// Solver thresholds (fddp_params) passed by value.
+struct Prm {
+  double th_acceptstep, th_stop, th_grad, th_stepdec, th_stepinc, th_acceptnegstep;
+  double regfactor, regmin, regmax;
+  int n_alphas;
+  double alphas[16];
+};
+
+// raiseIfNaN — src/core/solver-base.cpp:175-181
+__device__ inline bool raise_if_nan(double v) { return isnan(v) || isinf(v) || v >= 1e30; }
+// |x| value that trips raiseIfNaN(lpNorm<Infinity>) for an element of a vector
+__device__ inline bool bad_entry(double v) {
+  const double a = fabs(v);
+  return isnan(a) || isinf(a) || a >= 1e30;
+}
+
+// ---------------------------------------------------------------------------
+// Workgroup reductions (wave64 shuffles + LDS).
+// ---------------------------------------------------------------------------
+__device__ inline double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
+
+// Sum of v over the workgroup; `red` is LDS scratch of >= 2*nwaves doubles.
+// Ends with every thread holding the total; contains two barriers.
+template <int NT>
+__device__ inline double wg_sum(double v, double* red) {
+  constexpr int NW = NT / kWave;
+  v = wave_sum(v);
+  const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  double s = 0.;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) s += red[i];
+  __syncthreads();
+  return s;
+}
+
+// Several sums at once (same structure; red >= NV*NW doubles).
+template <int NT, int NV>
+__device__ inline void wg_sums(double (&v)[NV], double* red) {
+  constexpr int NW = NT / kWave;
+  const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    double x = wave_sum(v[j]);
+    if (lane == 0) red[j * NW + w] = x;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    double s = 0.;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) s += red[j * NW + i];
+    v[j] = s;
+  }
+  __syncthreads();
+}
+
+// OR of a predicate over the workgroup.
+__device__ inline bool wg_any(bool p, int* flag) {
+  if (threadIdx.x == 0) *flag = 0;
+  __syncthreads();
+  if (p) *flag = 1;
+  __syncthreads();
+  const bool r = *flag != 0;
+  __syncthreads();
+  return r;
+}
+
+}  // namespace fddp

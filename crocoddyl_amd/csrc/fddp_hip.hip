@@ -1,0 +1,810 @@
+// libfddp_hip — C ABI implementation (see include/fddp_hip.h).
+//
+// One handle = one ShootingProblem replicated over B batch elements (each
+// element with its own x0, warm start and optionally its own model
+// parameters) + one SolverFDDP state machine per element, all resident on one
+// gfx950 device. fddp_solve enqueues, per FDDP iteration:
+//   [iter 0] calc_kernel + cost_sum      ShootingProblem::calc (ddp.cpp:158)
+//   calc_diff_kernel (+gaps)             SolverDDP::calcDiff (ddp.cpp:157-178)
+//   backward_kernel (reg retries)        computeDirection loop (fddp.cpp:35-48)
+//   forward_kernel (line search, update) fddp.cpp:49-103
+// Elements that converge or abort drop out (masked); the host only reads one
+// counter per iteration to stop early.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/fddp_hip.h"
+#include "fddp_device.hpp"
+#include "fddp_kernels.hpp"
+
+using namespace fddp;
+
+namespace {
+
+thread_local std::string g_err;
+
+constexpr int kNT = 256;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                           \
+  do {                                                                                          \
+    hipError_t e_ = (expr);                                                                     \
+    if (e_ != hipSuccess)                                                                       \
+      return fail(FDDP_ERR_RUNTIME, std::string(#expr) + ": " + hipGetErrorString(e_));         \
+  } while (0)
+
+#define LAUNCH_CHECK()                                                                          \
+  do {                                                                                          \
+    hipError_t e_ = hipGetLastError();                                                          \
+    if (e_ != hipSuccess) return fail(FDDP_ERR_RUNTIME, std::string("launch: ") + hipGetErrorString(e_)); \
+  } while (0)
+
+int64_t block_doubles(int kind, int nx, int nu) {
+  switch (kind) {
+    case FDDP_KNOT_LQR:
+      return FDDP_PARAM_HEADER + 2LL * nx * nx + 2LL * nx * nu + (int64_t)nu * nu + 2LL * nx + nu;
+    case FDDP_KNOT_UNICYCLE:
+      return FDDP_PARAM_HEADER;
+    case FDDP_KNOT_EULER_DIFFLQR: {
+      const int64_t nq = nx / 2;
+      return FDDP_PARAM_HEADER + 2 * nq * nq + nq * nu + nq + (int64_t)nx * nx + (int64_t)nx * nu +
+             (int64_t)nu * nu + nx + nu;
+    }
+  }
+  return -1;
+}
+
+}  // namespace
+
+struct fddp_handle_s {
+  fddp_dims dims;
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::vector<fddp_knot_desc> knots;
+  int64_t n_params = 0;
+  fddp_params prm;
+  Dev D;
+  std::vector<void*> allocs;
+  double* staging = nullptr;
+  int64_t staging_len = 0;
+  double* d_out = nullptr;  // B doubles
+  int* d_count = nullptr;
+  int* h_count = nullptr;   // pinned
+  bool debug = false;
+  double* dbg[7] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  int64_t bytes = 0;
+  size_t bwd_smem = 0, fwd_smem = 0, calc_smem = 0, cdiff_smem = 0;
+  // timing
+  bool timing = false;
+  std::vector<hipEvent_t> ev_pool;
+  std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> ev_rec;
+  double t_ms[4] = {0, 0, 0, 0};
+  int64_t t_cnt[4] = {0, 0, 0, 0};
+};
+
+namespace {
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+int dalloc(fddp_handle* h, double** p, int64_t n) {
+  void* q = nullptr;
+  const size_t bytes = sizeof(double) * (size_t)(n > 0 ? n : 1);
+  HIP_TRY(hipMalloc(&q, bytes));
+  HIP_TRY(hipMemsetAsync(q, 0, bytes, h->stream));
+  h->allocs.push_back(q);
+  h->bytes += (int64_t)bytes;
+  *p = (double*)q;
+  return FDDP_OK;
+}
+
+hipEvent_t take_event(fddp_handle* h) {
+  if (!h->ev_pool.empty()) {
+    hipEvent_t e = h->ev_pool.back();
+    h->ev_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+
+struct Timed {
+  fddp_handle* h;
+  int cls;
+  hipEvent_t a = nullptr, b = nullptr;
+  Timed(fddp_handle* hh, int c) : h(hh), cls(c) {
+    if (h->timing) {
+      a = take_event(h);
+      b = take_event(h);
+      if (a) (void)hipEventRecord(a, h->stream);
+    }
+  }
+  ~Timed() {
+    if (h->timing && a && b) {
+      (void)hipEventRecord(b, h->stream);
+      h->ev_rec.push_back({cls, {a, b}});
+    }
+  }
+};
+
+Prm to_prm(const fddp_params& p) {
+  Prm q;
+  q.th_acceptstep = p.th_acceptstep;
+  q.th_stop = p.th_stop;
+  q.th_grad = p.th_grad;
+  q.th_stepdec = p.th_stepdec;
+  q.th_stepinc = p.th_stepinc;
+  q.th_acceptnegstep = p.th_acceptnegstep;
+  q.regfactor = p.regfactor;
+  q.regmin = p.regmin;
+  q.regmax = p.regmax;
+  q.n_alphas = p.n_alphas;
+  for (int i = 0; i < 16; ++i) q.alphas[i] = p.alphas[i];
+  return q;
+}
+
+// ---- kernel launchers ------------------------------------------------------
+int launch_calc(fddp_handle* h, int sel) {
+  Timed tm(h, 0);
+  const Dev& D = h->D;
+  hipLaunchKernelGGL(calc_kernel<kNT>, dim3(D.T + 1, D.B), dim3(kNT), h->calc_smem, h->stream, D, sel);
+  LAUNCH_CHECK();
+  return FDDP_OK;
+}
+int launch_cost_sum(fddp_handle* h, int sel, double* out) {
+  const Dev& D = h->D;
+  hipLaunchKernelGGL(cost_sum_kernel, dim3((D.B + 255) / 256), dim3(256), 0, h->stream, D, sel, out);
+  LAUNCH_CHECK();
+  return FDDP_OK;
+}
+int launch_calc_diff(fddp_handle* h, int sel, int gaps) {
+  Timed tm(h, 1);
+  const Dev& D = h->D;
+  hipLaunchKernelGGL(calc_diff_kernel<kNT>, dim3(D.T + 1, D.B), dim3(kNT), h->cdiff_smem, h->stream, D, sel, gaps);
+  LAUNCH_CHECK();
+  return FDDP_OK;
+}
+int launch_backward(fddp_handle* h, int mode) {
+  Timed tm(h, 2);
+  const Dev& D = h->D;
+  hipLaunchKernelGGL(backward_kernel<kNT>, dim3(D.B), dim3(kNT), h->bwd_smem, h->stream, D, to_prm(h->prm), mode);
+  LAUNCH_CHECK();
+  return FDDP_OK;
+}
+int launch_forward(fddp_handle* h, int mode, double alpha, int* count) {
+  Timed tm(h, 3);
+  const Dev& D = h->D;
+  hipLaunchKernelGGL(forward_kernel<kNT>, dim3(D.B), dim3(kNT), h->fwd_smem, h->stream, D, to_prm(h->prm), mode,
+                     alpha, count);
+  LAUNCH_CHECK();
+  return FDDP_OK;
+}
+
+__global__ void set_feasible_kernel(Dev D, int is_feasible) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < D.B) D.st[b].is_feasible = is_feasible;
+}
+__global__ void ei_kernel(Dev D, double* out) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= D.B) return;
+  ElemState& s = D.st[b];
+  s.d0 = s.dg + s.dv;
+  s.d1 = s.dq - 2 * s.dv;
+  out[2 * b] = s.d0;
+  out[2 * b + 1] = s.d1;
+}
+__global__ void step_state_kernel(Dev D, int iter, double xreg, double ureg, int was_feasible) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= D.B) return;
+  ElemState& s = D.st[b];
+  s.iter = iter;
+  s.xreg = xreg;
+  s.ureg = ureg;
+  s.was_feasible = was_feasible;
+}
+
+int download_states(fddp_handle* h, std::vector<ElemState>& v) {
+  v.resize(h->dims.B);
+  HIP_TRY(hipMemcpyAsync(v.data(), h->D.st, sizeof(ElemState) * h->dims.B, hipMemcpyDeviceToHost, h->stream));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  return FDDP_OK;
+}
+
+void fill_result(const ElemState& s, fddp_result* r) {
+  r->status = s.status;
+  r->iter = s.iter;
+  r->is_feasible = s.is_feasible;
+  r->n_iter_run = s.n_iter_run;
+  r->cost = s.cost;
+  r->stop = s.stop;
+  r->xreg = s.xreg;
+  r->ureg = s.ureg;
+  r->steplength = s.steplength;
+  r->dV = s.dV;
+  r->dVexp = s.dVexp;
+  r->d0 = s.d0;
+  r->d1 = s.d1;
+}
+
+int gather_traj(fddp_handle* h, int which, int other_buf, double* out, int on_device) {
+  const Dev& D0 = h->D;
+  Dev D = D0;
+  if (other_buf) {  // view the trial buffer as current: swap the pointers
+    std::swap(D.xs[0], D.xs[1]);
+    std::swap(D.us[0], D.us[1]);
+  }
+  const int64_t len = which == 0 ? (int64_t)D.B * (D.T + 1) * D.nx : (int64_t)D.B * D.T * D.m;
+  double* dst = on_device ? out : h->staging;
+  hipLaunchKernelGGL(gather_traj_kernel, dim3(8, D.B), dim3(256), 0, h->stream, D, which, dst);
+  LAUNCH_CHECK();
+  if (!on_device) {
+    HIP_TRY(hipMemcpyAsync(out, h->staging, sizeof(double) * len, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+  }
+  return FDDP_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* fddp_last_error(void) { return g_err.c_str(); }
+
+void fddp_default_params(fddp_params* p) {
+  // ddp.cpp:15-37 ; fddp.cpp:14-15 ; solver-base.cpp:24-25
+  p->th_acceptstep = 0.1;
+  p->th_stop = 1e-9;
+  p->th_grad = 1e-12;
+  p->th_stepdec = 0.5;
+  p->th_stepinc = 0.01;
+  p->th_acceptnegstep = 2.;
+  p->regfactor = 10.;
+  p->regmin = 1e-9;
+  p->regmax = 1e9;
+  p->n_alphas = 10;
+  p->pad_ = 0;
+  for (int i = 0; i < 16; ++i) p->alphas[i] = i < 10 ? 1. / std::pow(2., (double)i) : 0.;
+}
+
+int fddp_create(const fddp_dims* dims, const fddp_knot_desc* knots, const double* params, int64_t n_params,
+                int device, fddp_handle** out) {
+  g_err.clear();
+  if (!dims || !knots || !params || !out) return fail(FDDP_ERR_INVALID_ARG, "fddp_create: null argument");
+  *out = nullptr;
+  const fddp_dims d = *dims;
+  if (d.T < 1 || d.B < 1 || d.nx < 1 || d.nu_max < 0)
+    return fail(FDDP_ERR_INVALID_ARG, "fddp_create: T, B, nx must be positive");
+  if (d.nx != d.ndx) return fail(FDDP_ERR_UNSUPPORTED, "fddp_create: only Euclidean states (nx == ndx) are supported");
+  if (d.B > 65535) return fail(FDDP_ERR_INVALID_ARG, "fddp_create: B > 65535 per handle");
+  int nu_max = 0;
+  for (int t = 0; t <= d.T; ++t) {
+    const fddp_knot_desc& k = knots[t];
+    if (k.nu < 0) return fail(FDDP_ERR_INVALID_ARG, "fddp_create: negative nu");
+    if (t < d.T && k.nu > nu_max) nu_max = k.nu;
+    if (k.kind == FDDP_KNOT_UNICYCLE && (d.nx != 3 || k.nu != 2))
+      return fail(FDDP_ERR_INVALID_ARG, "fddp_create: unicycle knots need nx=3, nu=2");
+    if (k.kind == FDDP_KNOT_EULER_DIFFLQR && (d.nx % 2))
+      return fail(FDDP_ERR_INVALID_ARG, "fddp_create: Euler(DiffLQR) knots need an even nx");
+    const int64_t sz = block_doubles(k.kind, d.nx, k.nu);
+    if (sz < 0) return fail(FDDP_ERR_UNSUPPORTED, "fddp_create: unknown knot kind " + std::to_string(k.kind));
+    if (k.param_offset < 0 || k.param_stride < 0 ||
+        k.param_offset + (int64_t)(d.B - 1) * k.param_stride + sz > n_params)
+      return fail(FDDP_ERR_INVALID_ARG, "fddp_create: knot " + std::to_string(t) + " parameter block out of range");
+  }
+  if (nu_max != d.nu_max)
+    return fail(FDDP_ERR_INVALID_ARG, "fddp_create: nu_max must equal the max nu over the running knots");
+  if (knots[d.T].nu > d.nu_max)
+    return fail(FDDP_ERR_INVALID_ARG, "fddp_create: terminal nu exceeds nu_max");
+
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+    return fail(FDDP_ERR_NO_DEVICE, "fddp_create: no HIP device visible");
+  if (device < 0 || device >= ndev) return fail(FDDP_ERR_INVALID_ARG, "fddp_create: bad device index");
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, device));
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(FDDP_ERR_UNSUPPORTED, std::string("fddp_create: device is ") + prop.gcnArchName +
+                                          ", libfddp_hip is built for gfx950 (MI355X) only");
+
+  DeviceGuard g(device);
+  auto* h = new fddp_handle_s();
+  h->dims = d;
+  h->device = device;
+  h->knots.assign(knots, knots + d.T + 1);
+  h->n_params = n_params;
+  fddp_default_params(&h->prm);
+  int rc;
+  auto bail = [&](int code) {
+    fddp_destroy(h);
+    return code;
+  };
+  if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess)
+    return bail(fail(FDDP_ERR_RUNTIME, "hipStreamCreate failed"));
+
+  Dev& D = h->D;
+  std::memset(&D, 0, sizeof(D));
+  D.nx = d.nx;
+  D.n = d.ndx;
+  D.m = d.nu_max;
+  D.T = d.T;
+  D.B = d.B;
+  D.sX = pad2(d.nx);
+  D.sN = pad2(d.ndx);
+  D.sM = pad2(d.nu_max > 0 ? d.nu_max : 1);
+  D.sNN = pad2((int64_t)d.ndx * d.ndx);
+  D.sNM = pad2((int64_t)d.ndx * (d.nu_max > 0 ? d.nu_max : 1));
+  D.sMM = pad2((int64_t)d.nu_max * d.nu_max > 0 ? (int64_t)d.nu_max * d.nu_max : 1);
+  const int64_t B = d.B, K1 = (int64_t)d.T + 1, K0 = d.T;
+
+  h->bwd_smem = BwdSmem::bytes(D.n, D.m);
+  if (h->bwd_smem > 160 * 1024)
+    return bail(fail(FDDP_ERR_UNSUPPORTED, "fddp_create: (ndx, nu_max) too large for the LDS-resident Riccati sweep"));
+  h->fwd_smem = sizeof(double) * (2 * D.sX + D.sM + 5 * (kNT / kWave) + 16);
+  h->calc_smem = h->fwd_smem;
+  h->cdiff_smem = sizeof(double) * (D.sX + D.sM);
+
+  double* p = nullptr;
+  if ((rc = dalloc(h, &p, n_params))) return bail(rc);
+  D.params = p;
+  if (hipMemcpyAsync(p, params, sizeof(double) * n_params, hipMemcpyHostToDevice, h->stream) != hipSuccess)
+    return bail(fail(FDDP_ERR_RUNTIME, "upload params"));
+  fddp_knot_desc* kd = nullptr;
+  if ((rc = dalloc(h, (double**)&kd, (sizeof(fddp_knot_desc) * K1 + 7) / 8))) return bail(rc);
+  D.knots = kd;
+  if (hipMemcpyAsync(kd, knots, sizeof(fddp_knot_desc) * K1, hipMemcpyHostToDevice, h->stream) != hipSuccess)
+    return bail(fail(FDDP_ERR_RUNTIME, "upload knots"));
+
+  struct A {
+    double** p;
+    int64_t n;
+  } plan[] = {
+      {&D.x0, B * D.sX},          {&D.xs[0], B * K1 * D.sX}, {&D.xs[1], B * K1 * D.sX}, {&D.us[0], B * K0 * D.sM},
+      {&D.us[1], B * K0 * D.sM},  {&D.xnext[0], B * K0 * D.sX}, {&D.xnext[1], B * K0 * D.sX},
+      {&D.kcost[0], B * K1},      {&D.kcost[1], B * K1},     {&D.Fx, B * K1 * D.sNN},   {&D.Fu, B * K1 * D.sNM},
+      {&D.Lxx, B * K1 * D.sNN},   {&D.Lxu, B * K1 * D.sNM},  {&D.Luu, B * K1 * D.sMM},  {&D.Lx, B * K1 * D.sN},
+      {&D.Lu, B * K1 * D.sM},     {&D.fs, B * K1 * D.sN},    {&D.K, B * K0 * D.sNM},    {&D.k, B * K0 * D.sM},
+      {&D.Vxxfs, B * K1 * D.sN},  {&D.part, B * K1 * 8},     {&D.dvp, B * K1},
+  };
+  for (auto& a : plan)
+    if ((rc = dalloc(h, a.p, a.n))) return bail(rc);
+  double* stp = nullptr;
+  if ((rc = dalloc(h, &stp, (int64_t)(sizeof(ElemState) / 8) * B))) return bail(rc);
+  D.st = (ElemState*)stp;
+  h->staging_len = std::max<int64_t>(std::max<int64_t>(B * K1 * d.nx, B * K0 * D.sM), B * K1);
+  if ((rc = dalloc(h, &h->staging, h->staging_len))) return bail(rc);
+  if ((rc = dalloc(h, &h->d_out, 2 * B))) return bail(rc);
+  double* cnt = nullptr;
+  if ((rc = dalloc(h, &cnt, 1))) return bail(rc);
+  h->d_count = (int*)cnt;
+  if (hipHostMalloc((void**)&h->h_count, sizeof(int)) != hipSuccess)
+    return bail(fail(FDDP_ERR_RUNTIME, "hipHostMalloc"));
+
+  // SolverAbstract constructor state (solver-base.cpp:14-26): xreg = ureg = NaN
+  std::vector<ElemState> st0(B);
+  for (auto& s : st0) {
+    std::memset(&s, 0, sizeof(s));
+    s.xreg = NAN;
+    s.ureg = NAN;
+    s.steplength = 1.;
+  }
+  if (hipMemcpyAsync(D.st, st0.data(), sizeof(ElemState) * B, hipMemcpyHostToDevice, h->stream) != hipSuccess)
+    return bail(fail(FDDP_ERR_RUNTIME, "upload state"));
+  if (hipFuncSetAttribute((const void*)backward_kernel<kNT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)h->bwd_smem) != hipSuccess)
+    return bail(fail(FDDP_ERR_RUNTIME, "hipFuncSetAttribute(backward_kernel)"));
+  if (hipStreamSynchronize(h->stream) != hipSuccess) return bail(fail(FDDP_ERR_RUNTIME, "sync after create"));
+  *out = h;
+  return FDDP_OK;
+}
+
+void fddp_destroy(fddp_handle* h) {
+  if (!h) return;
+  DeviceGuard g(h->device);
+  if (h->stream) (void)hipStreamSynchronize(h->stream);
+  for (void* p : h->allocs) (void)hipFree(p);
+  for (auto& r : h->ev_rec) {
+    (void)hipEventDestroy(r.second.first);
+    (void)hipEventDestroy(r.second.second);
+  }
+  for (auto e : h->ev_pool) (void)hipEventDestroy(e);
+  if (h->h_count) (void)hipHostFree(h->h_count);
+  if (h->stream) (void)hipStreamDestroy(h->stream);
+  delete h;
+}
+
+int fddp_set_model_params(fddp_handle* h, const double* params, int64_t n_params) {
+  if (!h || !params || n_params != h->n_params) return fail(FDDP_ERR_INVALID_ARG, "fddp_set_model_params: size");
+  DeviceGuard g(h->device);
+  HIP_TRY(hipMemcpyAsync((void*)h->D.params, params, sizeof(double) * n_params, hipMemcpyHostToDevice, h->stream));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  return FDDP_OK;
+}
+
+int fddp_set_x0(fddp_handle* h, const double* x0) {
+  if (!h || !x0) return fail(FDDP_ERR_INVALID_ARG, "fddp_set_x0: null");
+  DeviceGuard g(h->device);
+  const Dev& D = h->D;
+  HIP_TRY(hipMemcpy2DAsync(D.x0, sizeof(double) * D.sX, x0, sizeof(double) * D.nx, sizeof(double) * D.nx, D.B,
+                           hipMemcpyHostToDevice, h->stream));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  return FDDP_OK;
+}
+
+int fddp_get_x0(fddp_handle* h, double* x0) {
+  if (!h || !x0) return fail(FDDP_ERR_INVALID_ARG, "fddp_get_x0: null");
+  DeviceGuard g(h->device);
+  const Dev& D = h->D;
+  HIP_TRY(hipMemcpy2DAsync(x0, sizeof(double) * D.nx, D.x0, sizeof(double) * D.sX, sizeof(double) * D.nx, D.B,
+                           hipMemcpyDeviceToHost, h->stream));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  return FDDP_OK;
+}
+
+int fddp_set_params(fddp_handle* h, const fddp_params* p) {
+  if (!h || !p) return fail(FDDP_ERR_INVALID_ARG, "fddp_set_params: null");
+  // validation as the reference setters
+  if (0. >= p->th_acceptstep || p->th_acceptstep > 1)
+    return fail(FDDP_ERR_INVALID_ARG, "th_acceptstep value should between 0 and 1.");  // solver-base.cpp:159-165
+  if (p->th_stop <= 0.) return fail(FDDP_ERR_INVALID_ARG, "th_stop value has to higher than 0.");  // :167-173
+  if (0. > p->th_grad) return fail(FDDP_ERR_INVALID_ARG, "th_grad value has to be positive.");    // ddp.cpp:480-486
+  if (0. >= p->th_stepdec || p->th_stepdec > 1.)
+    return fail(FDDP_ERR_INVALID_ARG, "th_stepdec value should between 0 and 1.");  // ddp.cpp:464-470
+  if (0. >= p->th_stepinc || p->th_stepinc > 1.)
+    return fail(FDDP_ERR_INVALID_ARG, "th_stepinc value should between 0 and 1.");  // ddp.cpp:472-478
+  if (0. > p->th_acceptnegstep)
+    return fail(FDDP_ERR_INVALID_ARG, "th_acceptnegstep value has to be positive.");  // fddp.cpp:229-235
+  if (p->regfactor <= 1.) return fail(FDDP_ERR_INVALID_ARG, "regfactor value is higher than 1.");  // ddp.cpp:420-426
+  if (0. > p->regmin) return fail(FDDP_ERR_INVALID_ARG, "regmin value has to be positive.");
+  if (0. > p->regmax) return fail(FDDP_ERR_INVALID_ARG, "regmax value has to be positive.");
+  if (p->n_alphas < 1 || p->n_alphas > 16) return fail(FDDP_ERR_INVALID_ARG, "n_alphas must be in [1, 16]");
+  for (int i = 1; i < p->n_alphas; ++i) {  // ddp.cpp:444-462
+    if (0. >= p->alphas[i]) return fail(FDDP_ERR_INVALID_ARG, "alpha values has to be positive.");
+    if (p->alphas[i] >= p->alphas[i - 1])
+      return fail(FDDP_ERR_INVALID_ARG, "alpha values are monotonously decreasing.");
+  }
+  h->prm = *p;
+  return FDDP_OK;
+}
+
+int fddp_get_params(fddp_handle* h, fddp_params* p) {
+  if (!h || !p) return fail(FDDP_ERR_INVALID_ARG, "fddp_get_params: null");
+  *p = h->prm;
+  return FDDP_OK;
+}
+
+int fddp_set_candidate(fddp_handle* h, const double* xs, const double* us, int is_feasible) {
+  if (!h) return fail(FDDP_ERR_INVALID_ARG, "fddp_set_candidate: null handle");
+  DeviceGuard g(h->device);
+  const Dev& D = h->D;
+  const int64_t lx = (int64_t)D.B * (D.T + 1) * D.nx, lu = (int64_t)D.B * D.T * D.m;
+  if (xs) HIP_TRY(hipMemcpyAsync(h->staging, xs, sizeof(double) * lx, hipMemcpyHostToDevice, h->stream));
+  hipLaunchKernelGGL(scatter_traj_kernel, dim3(8, D.B), dim3(256), 0, h->stream, D, 0, h->staging, xs ? 0 : 1);
+  LAUNCH_CHECK();
+  if (D.m > 0) {
+    if (us) HIP_TRY(hipMemcpyAsync(h->staging, us, sizeof(double) * lu, hipMemcpyHostToDevice, h->stream));
+    hipLaunchKernelGGL(scatter_traj_kernel, dim3(8, D.B), dim3(256), 0, h->stream, D, 1, h->staging, us ? 0 : 1);
+    LAUNCH_CHECK();
+  }
+  hipLaunchKernelGGL(set_feasible_kernel, dim3((D.B + 255) / 256), dim3(256), 0, h->stream, D, is_feasible ? 1 : 0);
+  LAUNCH_CHECK();
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  return FDDP_OK;
+}
+
+int fddp_solve(fddp_handle* h, int maxiter, int is_feasible, double reg_init, fddp_result* out) {
+  if (!h) return fail(FDDP_ERR_INVALID_ARG, "fddp_solve: null handle");
+  if (maxiter < 0) return fail(FDDP_ERR_INVALID_ARG, "fddp_solve: maxiter < 0");
+  DeviceGuard g(h->device);
+  const Dev& D = h->D;
+  const double xreg0 = std::isnan(reg_init) ? h->prm.regmin : reg_init;
+  hipLaunchKernelGGL(init_state_kernel, dim3((D.B + 255) / 256), dim3(256), 0, h->stream, D, is_feasible ? 1 : 0,
+                     xreg0);
+  LAUNCH_CHECK();
+  int rc;
+  for (int it = 0; it < maxiter; ++it) {
+    if (it == 0) {
+      if ((rc = launch_calc(h, SEL_ACTIVE))) return rc;
+      if ((rc = launch_cost_sum(h, SEL_ACTIVE, nullptr))) return rc;
+    }
+    if ((rc = launch_calc_diff(h, SEL_RECALC, 1))) return rc;
+    if ((rc = launch_backward(h, 0))) return rc;
+    HIP_TRY(hipMemsetAsync(h->d_count, 0, sizeof(int), h->stream));
+    if ((rc = launch_forward(h, 0, 1., h->d_count))) return rc;
+    if (it + 1 < maxiter) {
+      HIP_TRY(hipMemcpyAsync(h->h_count, h->d_count, sizeof(int), hipMemcpyDeviceToHost, h->stream));
+      HIP_TRY(hipStreamSynchronize(h->stream));
+      if (*h->h_count == 0) break;
+    }
+  }
+  if (out) {
+    std::vector<ElemState> st;
+    if ((rc = download_states(h, st))) return rc;
+    for (int b = 0; b < D.B; ++b) fill_result(st[b], &out[b]);
+  } else {
+    HIP_TRY(hipStreamSynchronize(h->stream));
+  }
+  return FDDP_OK;
+}
+
+int fddp_get_results(fddp_handle* h, fddp_result* out) {
+  if (!h || !out) return fail(FDDP_ERR_INVALID_ARG, "fddp_get_results: null");
+  DeviceGuard g(h->device);
+  std::vector<ElemState> st;
+  int rc;
+  if ((rc = download_states(h, st))) return rc;
+  for (int b = 0; b < h->dims.B; ++b) fill_result(st[b], &out[b]);
+  return FDDP_OK;
+}
+
+int fddp_get_xs(fddp_handle* h, double* out, int on_device) {
+  if (!h || !out) return fail(FDDP_ERR_INVALID_ARG, "fddp_get_xs: null");
+  DeviceGuard g(h->device);
+  return gather_traj(h, 0, 0, out, on_device);
+}
+int fddp_get_us(fddp_handle* h, double* out, int on_device) {
+  if (!h || !out) return fail(FDDP_ERR_INVALID_ARG, "fddp_get_us: null");
+  DeviceGuard g(h->device);
+  if (h->D.m == 0) return FDDP_OK;
+  return gather_traj(h, 1, 0, out, on_device);
+}
+int fddp_get_xs_try(fddp_handle* h, double* out) {
+  if (!h || !out) return fail(FDDP_ERR_INVALID_ARG, "fddp_get_xs_try: null");
+  DeviceGuard g(h->device);
+  return gather_traj(h, 0, 1, out, 0);
+}
+int fddp_get_us_try(fddp_handle* h, double* out) {
+  if (!h || !out) return fail(FDDP_ERR_INVALID_ARG, "fddp_get_us_try: null");
+  DeviceGuard g(h->device);
+  if (h->D.m == 0) return FDDP_OK;
+  return gather_traj(h, 1, 1, out, 0);
+}
+
+// ---- step API ---------------------------------------------------------------
+int fddp_problem_calc(fddp_handle* h, double* cost) {
+  if (!h) return fail(FDDP_ERR_INVALID_ARG, "null handle");
+  DeviceGuard g(h->device);
+  int rc;
+  if ((rc = launch_calc(h, SEL_ALL))) return rc;
+  if ((rc = launch_cost_sum(h, SEL_ALL, h->d_out))) return rc;
+  if (cost) HIP_TRY(hipMemcpyAsync(cost, h->d_out, sizeof(double) * h->dims.B, hipMemcpyDeviceToHost, h->stream));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  return FDDP_OK;
+}
+
+int fddp_problem_calc_diff(fddp_handle* h, double* cost) {
+  if (!h) return fail(FDDP_ERR_INVALID_ARG, "null handle");
+  DeviceGuard g(h->device);
+  int rc;
+  if ((rc = launch_calc_diff(h, SEL_ALL, 0))) return rc;
+  if ((rc = launch_cost_sum(h, SEL_ALL, h->d_out))) return rc;
+  if (cost) HIP_TRY(hipMemcpyAsync(cost, h->d_out, sizeof(double) * h->dims.B, hipMemcpyDeviceToHost, h->stream));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  return FDDP_OK;
+}
+
+int fddp_compute_direction(fddp_handle* h, int recalc, int32_t* status) {
+  if (!h) return fail(FDDP_ERR_INVALID_ARG, "null handle");
+  DeviceGuard g(h->device);
+  int rc;
+  if (recalc) {
+    if ((rc = launch_calc(h, SEL_ITER0))) return rc;
+    if ((rc = launch_cost_sum(h, SEL_ITER0, nullptr))) return rc;
+    if ((rc = launch_calc_diff(h, SEL_ALL, 1))) return rc;
+    if ((rc = launch_cost_sum(h, SEL_ALL, nullptr))) return rc;
+  }
+  if ((rc = launch_backward(h, 1))) return rc;
+  if (status) {
+    std::vector<ElemState> st;
+    if ((rc = download_states(h, st))) return rc;
+    for (int b = 0; b < h->dims.B; ++b) status[b] = st[b].bwd_fail;
+  } else {
+    HIP_TRY(hipStreamSynchronize(h->stream));
+  }
+  return FDDP_OK;
+}
+
+int fddp_update_expected_improvement(fddp_handle* h) {
+  // dg/dq are reduced inside the backward kernel (same terms, same order).
+  if (!h) return fail(FDDP_ERR_INVALID_ARG, "null handle");
+  return FDDP_OK;
+}
+
+int fddp_try_step(fddp_handle* h, double alpha, double* dV, int32_t* status) {
+  if (!h) return fail(FDDP_ERR_INVALID_ARG, "null handle");
+  if (alpha > 1. || alpha < 0.)
+    return fail(FDDP_ERR_INVALID_ARG, "invalid step length, value is between 0. to 1.");  // fddp.cpp:150-153
+  DeviceGuard g(h->device);
+  int rc;
+  if ((rc = launch_forward(h, 1, alpha, nullptr))) return rc;
+  std::vector<ElemState> st;
+  if ((rc = download_states(h, st))) return rc;
+  for (int b = 0; b < h->dims.B; ++b) {
+    if (dV) dV[b] = st[b].dV;
+    if (status) status[b] = st[b].fwd_fail;
+  }
+  return FDDP_OK;
+}
+
+int fddp_expected_improvement(fddp_handle* h, double* d) {
+  if (!h) return fail(FDDP_ERR_INVALID_ARG, "null handle");
+  DeviceGuard g(h->device);
+  const Dev& D = h->D;
+  hipLaunchKernelGGL(ei_kernel, dim3((D.B + 255) / 256), dim3(256), 0, h->stream, D, h->d_out);
+  LAUNCH_CHECK();
+  if (d) HIP_TRY(hipMemcpyAsync(d, h->d_out, sizeof(double) * 2 * D.B, hipMemcpyDeviceToHost, h->stream));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  return FDDP_OK;
+}
+
+int fddp_stopping_criteria(fddp_handle* h, double* stop) {
+  if (!h) return fail(FDDP_ERR_INVALID_ARG, "null handle");
+  DeviceGuard g(h->device);
+  std::vector<ElemState> st;
+  int rc;
+  if ((rc = download_states(h, st))) return rc;
+  if (stop)
+    for (int b = 0; b < h->dims.B; ++b) stop[b] = st[b].stop;
+  return FDDP_OK;
+}
+
+// Solver state for the step API (reference: a fresh solver has iter_ = 0 and
+// xreg_ = ureg_ = NaN; tests also set them explicitly).
+int fddp_set_solver_state(fddp_handle* h, int iter, double xreg, double ureg, int was_feasible) {
+  if (!h) return fail(FDDP_ERR_INVALID_ARG, "null handle");
+  DeviceGuard g(h->device);
+  const Dev& D = h->D;
+  hipLaunchKernelGGL(step_state_kernel, dim3((D.B + 255) / 256), dim3(256), 0, h->stream, D, iter, xreg, ureg,
+                     was_feasible);
+  LAUNCH_CHECK();
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  return FDDP_OK;
+}
+
+int fddp_set_debug(fddp_handle* h, int on) {
+  if (!h) return fail(FDDP_ERR_INVALID_ARG, "null handle");
+  DeviceGuard g(h->device);
+  Dev& D = h->D;
+  if (on && !h->dbg[0]) {
+    const int64_t B = D.B, K1 = D.T + 1, K0 = D.T;
+    const int64_t sizes[7] = {B * K1 * D.sNN, B * K1 * D.sN, B * K0 * D.sNN, B * K0 * D.sNM,
+                              B * K0 * D.sMM, B * K0 * D.sN, B * K0 * D.sM};
+    int rc;
+    for (int i = 0; i < 7; ++i)
+      if ((rc = dalloc(h, &h->dbg[i], sizes[i]))) return rc;
+  }
+  double* const* p = h->dbg;
+  const bool a = on != 0;
+  D.dVxx = a ? p[0] : nullptr;
+  D.dVx = a ? p[1] : nullptr;
+  D.dQxx = a ? p[2] : nullptr;
+  D.dQxu = a ? p[3] : nullptr;
+  D.dQuu = a ? p[4] : nullptr;
+  D.dQx = a ? p[5] : nullptr;
+  D.dQu = a ? p[6] : nullptr;
+  h->debug = a;
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  return FDDP_OK;
+}
+
+int fddp_get_quantity(fddp_handle* h, int which, double* out) {
+  if (!h || !out) return fail(FDDP_ERR_INVALID_ARG, "fddp_get_quantity: null");
+  DeviceGuard g(h->device);
+  const Dev& D = h->D;
+  const int64_t n = D.n, m = D.m;
+  const double* src = nullptr;
+  int64_t per = 0, stride = 0, nk = 0;
+  int cur = -1;
+  switch (which) {
+    case FDDP_Q_FX: src = D.Fx; per = n * n; stride = D.sNN; nk = D.T + 1; break;
+    case FDDP_Q_FU: src = D.Fu; per = n * m; stride = D.sNM; nk = D.T + 1; break;
+    case FDDP_Q_LXX: src = D.Lxx; per = n * n; stride = D.sNN; nk = D.T + 1; break;
+    case FDDP_Q_LXU: src = D.Lxu; per = n * m; stride = D.sNM; nk = D.T + 1; break;
+    case FDDP_Q_LUU: src = D.Luu; per = m * m; stride = D.sMM; nk = D.T + 1; break;
+    case FDDP_Q_LX: src = D.Lx; per = n; stride = D.sN; nk = D.T + 1; break;
+    case FDDP_Q_LU: src = D.Lu; per = m; stride = D.sM; nk = D.T + 1; break;
+    case FDDP_Q_XNEXT: cur = 1; per = D.nx; stride = D.sX; nk = D.T; break;
+    case FDDP_Q_FS: src = D.fs; per = n; stride = D.sN; nk = D.T + 1; break;
+    case FDDP_Q_K: src = D.K; per = m * n; stride = D.sNM; nk = D.T; break;
+    case FDDP_Q_KV: src = D.k; per = m; stride = D.sM; nk = D.T; break;
+    case FDDP_Q_VXX: src = D.dVxx; per = n * n; stride = D.sNN; nk = D.T + 1; break;
+    case FDDP_Q_VX: src = D.dVx; per = n; stride = D.sN; nk = D.T + 1; break;
+    case FDDP_Q_QXX: src = D.dQxx; per = n * n; stride = D.sNN; nk = D.T; break;
+    case FDDP_Q_QXU: src = D.dQxu; per = n * m; stride = D.sNM; nk = D.T; break;
+    case FDDP_Q_QUU: src = D.dQuu; per = m * m; stride = D.sMM; nk = D.T; break;
+    case FDDP_Q_QX: src = D.dQx; per = n; stride = D.sN; nk = D.T; break;
+    case FDDP_Q_QU: src = D.dQu; per = m; stride = D.sM; nk = D.T; break;
+    default: return fail(FDDP_ERR_INVALID_ARG, "fddp_get_quantity: unknown quantity");
+  }
+  if (per == 0) return FDDP_OK;
+  if (cur >= 0) {
+    // xnext lives in the current trajectory buffer of each element
+    std::vector<ElemState> st;
+    int rc;
+    if ((rc = download_states(h, st))) return rc;
+    for (int b = 0; b < D.B; ++b) {
+      const double* s = D.xnext[st[b].cur] + (int64_t)b * nk * stride;
+      HIP_TRY(hipMemcpy2DAsync(out + (int64_t)b * nk * per, sizeof(double) * per, s, sizeof(double) * stride,
+                               sizeof(double) * per, nk, hipMemcpyDeviceToHost, h->stream));
+    }
+  } else {
+    if (!src) return fail(FDDP_ERR_INVALID_ARG, "fddp_get_quantity: enable fddp_set_debug first");
+    HIP_TRY(hipMemcpy2DAsync(out, sizeof(double) * per, src, sizeof(double) * stride, sizeof(double) * per,
+                             (size_t)D.B * nk, hipMemcpyDeviceToHost, h->stream));
+  }
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  return FDDP_OK;
+}
+
+int fddp_mpc_shift(fddp_handle* h) {
+  if (!h) return fail(FDDP_ERR_INVALID_ARG, "null handle");
+  DeviceGuard g(h->device);
+  const Dev& D = h->D;
+  hipLaunchKernelGGL(mpc_shift_kernel<kNT>, dim3(D.B), dim3(kNT), 0, h->stream, D);
+  LAUNCH_CHECK();
+  return FDDP_OK;
+}
+
+int fddp_synchronize(fddp_handle* h) {
+  if (!h) return fail(FDDP_ERR_INVALID_ARG, "null handle");
+  DeviceGuard g(h->device);
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  return FDDP_OK;
+}
+
+int fddp_get_stream(fddp_handle* h, void** stream) {
+  if (!h || !stream) return fail(FDDP_ERR_INVALID_ARG, "null");
+  *stream = (void*)h->stream;
+  return FDDP_OK;
+}
+
+int fddp_set_timing(fddp_handle* h, int on) {
+  if (!h) return fail(FDDP_ERR_INVALID_ARG, "null handle");
+  h->timing = on != 0;
+  return FDDP_OK;
+}
+
+int fddp_get_timing(fddp_handle* h, double* ms_out, int64_t* counts_out) {
+  if (!h) return fail(FDDP_ERR_INVALID_ARG, "null handle");
+  DeviceGuard g(h->device);
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  for (auto& r : h->ev_rec) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, r.second.first, r.second.second) == hipSuccess) {
+      h->t_ms[r.first] += ms;
+      h->t_cnt[r.first] += 1;
+    }
+    h->ev_pool.push_back(r.second.first);
+    h->ev_pool.push_back(r.second.second);
+  }
+  h->ev_rec.clear();
+  for (int i = 0; i < 4; ++i) {
+    if (ms_out) ms_out[i] = h->t_ms[i];
+    if (counts_out) counts_out[i] = h->t_cnt[i];
+    h->t_ms[i] = 0.;
+    h->t_cnt[i] = 0;
+  }
+  return FDDP_OK;
+}
+
+int64_t fddp_device_bytes(fddp_handle* h) { return h ? h->bytes : 0; }
+
+}  // extern "C"

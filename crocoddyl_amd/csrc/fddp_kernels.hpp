@@ -1,0 +1,689 @@
+// libfddp_hip kernels (generic sizes). One workgroup per knot for the
+// ShootingProblem fan-out, one workgroup per batch element for the serial
+// Riccati sweep and the line-searched rollout.
+#pragma once
+
+#include "fddp_device.hpp"
+#include "knots.hpp"
+
+namespace fddp {
+
+enum Sel { SEL_ACTIVE = 0, SEL_ALL = 1, SEL_ITER0 = 2, SEL_RECALC = 3 };
+
+__device__ inline bool selected(const ElemState& s, int sel) {
+  switch (sel) {
+    case SEL_ACTIVE: return s.active != 0;
+    case SEL_ALL: return true;
+    case SEL_ITER0: return s.iter == 0;
+    default: return s.active != 0 && s.recalc != 0;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Workgroup GEMM: C = C0 + sgn * op(A) op(B), column-major, 2x2 register tiles.
+// TA: A is stored K x M (use A^T).  TB: B is stored N x K (use B^T).
+// C0 may alias C (each output reads its own C0 entry before writing it).
+// C0 == nullptr means zero.
+// ---------------------------------------------------------------------------
+template <int NT, bool TA, bool TB>
+__device__ void wg_gemm(int M, int N, int K, const double* __restrict__ A, int lda, const double* __restrict__ Bm,
+                        int ldb, const double* C0, int ldc0, double* C, int ldc, double sgn) {
+  const int mt = (M + 1) >> 1, ntl = (N + 1) >> 1;
+  for (int tile = threadIdx.x; tile < mt * ntl; tile += NT) {
+    const int i0 = (tile % mt) * 2, j0 = (tile / mt) * 2;
+    const bool ok1 = i0 + 1 < M, okj = j0 + 1 < N;
+    const int i1 = ok1 ? i0 + 1 : i0, j1 = okj ? j0 + 1 : j0;
+    double c00 = 0., c01 = 0., c10 = 0., c11 = 0.;
+    for (int k = 0; k < K; ++k) {
+      const double a0 = TA ? A[(int64_t)i0 * lda + k] : A[(int64_t)k * lda + i0];
+      const double a1 = TA ? A[(int64_t)i1 * lda + k] : A[(int64_t)k * lda + i1];
+      const double b0 = TB ? Bm[(int64_t)k * ldb + j0] : Bm[(int64_t)j0 * ldb + k];
+      const double b1 = TB ? Bm[(int64_t)k * ldb + j1] : Bm[(int64_t)j1 * ldb + k];
+      c00 += a0 * b0;
+      c01 += a0 * b1;
+      c10 += a1 * b0;
+      c11 += a1 * b1;
+    }
+    auto put = [&](int i, int j, double c) {
+      const double base = C0 ? C0[(int64_t)j * ldc0 + i] : 0.;
+      C[(int64_t)j * ldc + i] = base + sgn * c;
+    };
+    put(i0, j0, c00);
+    if (okj) put(i0, j1, c01);
+    if (ok1) put(i1, j0, c10);
+    if (ok1 && okj) put(i1, j1, c11);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// ShootingProblem::calc fan-out (shooting.hxx:133-161): one workgroup per
+// (knot t, element b). Writes data[t].xnext and data[t].cost of trajectory cur.
+// ---------------------------------------------------------------------------
+template <int NT>
+__global__ __launch_bounds__(NT) void calc_kernel(Dev D, int sel) {
+  const int t = blockIdx.x, b = blockIdx.y;
+  const ElemState& s = D.st[b];
+  if (!selected(s, sel)) return;
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  double* x = sm;                // sX
+  double* u = x + D.sX;          // sM
+  double* xn = u + D.sM;         // sX
+  double* red = xn + D.sX;       // 5*NT/64
+  const int c = s.cur;
+  const double* xg = D.xs[c] + D.knot(b, t) * D.sX;
+  for (int i = threadIdx.x; i < D.nx; i += NT) x[i] = xg[i];
+  const bool running = t < D.T;
+  if (running) {
+    const double* ug = D.us[c] + D.run(b, t) * D.sM;
+    for (int i = threadIdx.x; i < D.m; i += NT) u[i] = ug[i];
+  }
+  __syncthreads();
+  const fddp_knot_desc kd = D.knots[t];
+  const double cost = knot_calc<NT>(kd, D.pblock(b, t), D.nx, x, u, running, xn, red);
+  if (running) {
+    double* xo = D.xnext[c] + D.run(b, t) * D.sX;
+    for (int i = threadIdx.x; i < D.nx; i += NT) xo[i] = xn[i];
+  }
+  if (threadIdx.x == 0) D.kcost[c][D.knot(b, t)] = cost;
+}
+
+// cost_ = sum of data[t].cost in knot order, terminal last (shooting.hxx:155-160).
+__global__ void cost_sum_kernel(Dev D, int sel, double* out) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= D.B) return;
+  ElemState& s = D.st[b];
+  if (!selected(s, sel)) return;
+  const double* kc = D.kcost[s.cur] + D.knot(b, 0);
+  double c = 0.;
+  for (int t = 0; t < D.T; ++t) c += kc[t];
+  c += kc[D.T];
+  s.cost = c;
+  if (out) out[b] = c;
+}
+
+// ---------------------------------------------------------------------------
+// ShootingProblem::calcDiff fan-out (shooting.hxx:164-195) fused with the gap
+// computation of SolverDDP::calcDiff (ddp.cpp:160-176). One workgroup per
+// (knot, element); blocks written with coalesced stores.
+// ---------------------------------------------------------------------------
+template <int NT>
+__global__ __launch_bounds__(NT) void calc_diff_kernel(Dev D, int sel, int gaps) {
+  const int t = blockIdx.x, b = blockIdx.y;
+  const ElemState& s = D.st[b];
+  if (!selected(s, sel)) return;
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  double* x = sm;
+  double* u = x + D.sX;
+  const int c = s.cur;
+  const int64_t kk = D.knot(b, t);
+  const double* xg = D.xs[c] + kk * D.sX;
+  for (int i = threadIdx.x; i < D.nx; i += NT) x[i] = xg[i];
+  const bool running = t < D.T;
+  if (running) {
+    const double* ug = D.us[c] + D.run(b, t) * D.sM;
+    for (int i = threadIdx.x; i < D.m; i += NT) u[i] = ug[i];
+  }
+  __syncthreads();
+  KnotDiffOut o;
+  o.Fx = D.Fx + kk * D.sNN;
+  o.Fu = D.Fu + kk * D.sNM;
+  o.Lxx = D.Lxx + kk * D.sNN;
+  o.Lxu = D.Lxu + kk * D.sNM;
+  o.Luu = D.Luu + kk * D.sMM;
+  o.Lx = D.Lx + kk * D.sN;
+  o.Lu = D.Lu + kk * D.sM;
+  const fddp_knot_desc kd = D.knots[t];
+  knot_calc_diff<NT>(kd, D.pblock(b, t), D.nx, D.m, x, u, running, o);
+  if (!gaps) return;
+  if (!s.is_feasible) {
+    // fs[0] = diff(xs[0], x0) = x0 - xs[0]; fs[t+1] = diff(xs[t+1], data[t].xnext)
+    if (t == 0) {
+      double* f = D.fs + D.knot(b, 0) * D.sN;
+      const double* x0 = D.x0 + (int64_t)b * D.sX;
+      for (int i = threadIdx.x; i < D.n; i += NT) f[i] = x0[i] - x[i];
+    }
+    if (running) {
+      double* f = D.fs + D.knot(b, t + 1) * D.sN;
+      const double* xn = D.xnext[c] + D.run(b, t) * D.sX;
+      const double* x1 = D.xs[c] + D.knot(b, t + 1) * D.sX;
+      for (int i = threadIdx.x; i < D.n; i += NT) f[i] = xn[i] - x1[i];
+    }
+  } else if (!s.was_feasible) {  // closing the gaps
+    double* f = D.fs + kk * D.sN;
+    for (int i = threadIdx.x; i < D.n; i += NT) f[i] = 0.;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Backward Riccati sweep — SolverDDP::backwardPass + computeGains
+// (ddp.cpp:180-253, 298-310), one workgroup per element, V_xx carried in LDS.
+// mode 0 (solve): on backward_error raise the regularisation and redo the
+// sweep without calcDiff, as SolverFDDP::solve does (fddp.cpp:35-48).
+// mode 1 (step API): one sweep with the element's current xreg/ureg.
+// Outputs K, k, Vxx*fs per knot and the per-element reductions of
+// updateExpectedImprovement (fddp.cpp:126-147) and stoppingCriteria
+// (ddp.cpp:132-142), summed in the reference's order.
+// ---------------------------------------------------------------------------
+struct BwdSmem {
+  double *V, *A, *BU, *Qxu, *Quu, *L, *vx, *qx, *qu, *kv, *quuk, *fsv, *vf, *red;
+  int* flag;
+  __device__ BwdSmem(double* sm, int n, int m) {
+    V = sm;
+    A = V + n * n;
+    BU = A + n * n;
+    Qxu = BU + pad2(m * n);
+    Quu = Qxu + pad2(n * m);
+    L = Quu + pad2(m * m);
+    vx = L + pad2(m * m);
+    qx = vx + pad2(n);
+    qu = qx + pad2(n);
+    kv = qu + pad2(m);
+    quuk = kv + pad2(m);
+    fsv = quuk + pad2(m);
+    vf = fsv + pad2(n);
+    red = vf + pad2(n);
+    flag = (int*)(red + 64);
+  }
+  __host__ static size_t bytes(int n, int m) {
+    return sizeof(double) * (2 * n * n + pad2(m * n) + pad2(n * m) + 2 * pad2(m * m) + 4 * pad2(n) + 3 * pad2(m) +
+                             64 + 2);
+  }
+};
+
+template <int NT>
+__device__ bool bwd_sweep(const Dev& D, int b, bool feas, double xreg, double ureg, BwdSmem& S) {
+  const int n = D.n, m = D.m, T = D.T, tid = threadIdx.x;
+  const bool xr = !isnan(xreg), ur = !isnan(ureg);
+  // terminal: Vxx = Lxx_T (+ xreg I), Vx = Lx_T (+ Vxx fs_T)
+  {
+    const int64_t kk = D.knot(b, T);
+    const double* Lxx = D.Lxx + kk * D.sNN;
+    const double* Lx = D.Lx + kk * D.sN;
+    for (int e = tid; e < n * n; e += NT) {
+      const int i = e % n, j = e / n;
+      S.V[e] = (xr && i == j) ? Lxx[e] + xreg : Lxx[e];
+    }
+    const double* fs = D.fs + kk * D.sN;
+    for (int i = tid; i < n; i += NT) S.fsv[i] = fs[i];
+    __syncthreads();
+    double pv[2] = {0., 0.};
+    for (int i = tid; i < n; i += NT) {
+      double v = Lx[i];
+      if (!feas) {
+        double a = 0.;
+        for (int j = 0; j < n; ++j) a += S.V[j * n + i] * S.fsv[j];
+        S.vf[i] = a;
+        D.Vxxfs[kk * D.sN + i] = a;
+        v += a;
+        pv[0] += v * S.fsv[i];   // Vx_T . fs_T
+        pv[1] += S.fsv[i] * a;   // fs_T . Vxx_T fs_T
+      }
+      S.vx[i] = v;
+    }
+    wg_sums<NT, 2>(pv, S.red);
+    if (tid == 0) {
+      double* p = D.part + kk * 8;
+      p[0] = 0.; p[1] = 0.; p[2] = pv[0]; p[3] = pv[1]; p[4] = 0.;
+    }
+    if (D.dVxx) {
+      for (int e = tid; e < n * n; e += NT) D.dVxx[kk * D.sNN + e] = S.V[e];
+      for (int i = tid; i < n; i += NT) D.dVx[kk * D.sN + i] = S.vx[i];
+    }
+  }
+  for (int t = T - 1; t >= 0; --t) {
+    const int64_t kk = D.knot(b, t);
+    const int nu = D.knots[t].nu;
+    const double* Fx = D.Fx + kk * D.sNN;
+    const double* Fu = D.Fu + kk * D.sNM;
+    __syncthreads();
+    // FxTVxx = Fx^T Vxx' ; FuTVxx = Fu^T Vxx'
+    wg_gemm<NT, true, false>(n, n, n, Fx, n, S.V, n, nullptr, 0, S.A, n, 1.);
+    if (nu) wg_gemm<NT, true, false>(nu, n, n, Fu, n, S.V, n, nullptr, 0, S.BU, m, 1.);
+    // Qx = Lx + Fx^T Vx' ; Qu = Lu + Fu^T Vx'
+    {
+      const double* Lx = D.Lx + kk * D.sN;
+      const double* Lu = D.Lu + kk * D.sM;
+      for (int i = tid; i < n; i += NT) {
+        double a = 0.;
+        for (int k2 = 0; k2 < n; ++k2) a += Fx[(int64_t)i * n + k2] * S.vx[k2];
+        S.qx[i] = Lx[i] + a;
+      }
+      for (int i = tid; i < nu; i += NT) {
+        double a = 0.;
+        for (int k2 = 0; k2 < n; ++k2) a += Fu[(int64_t)i * n + k2] * S.vx[k2];
+        S.qu[i] = Lu[i] + a;
+      }
+      const double* fs = D.fs + kk * D.sN;
+      for (int i = tid; i < n; i += NT) S.fsv[i] = fs[i];
+    }
+    __syncthreads();
+    // Qxx = Lxx + FxTVxx Fx (into V) ; Qxu = Lxu + FxTVxx Fu ; Quu = Luu + FuTVxx Fu (+ ureg I)
+    wg_gemm<NT, false, false>(n, n, n, S.A, n, Fx, n, D.Lxx + kk * D.sNN, n, S.V, n, 1.);
+    if (nu) {
+      wg_gemm<NT, false, false>(n, nu, n, S.A, n, Fu, n, D.Lxu + kk * D.sNM, n, S.Qxu, n, 1.);
+      wg_gemm<NT, false, false>(nu, nu, n, S.BU, m, Fu, n, D.Luu + kk * D.sMM, m, S.Quu, m, 1.);
+    }
+    __syncthreads();
+    if (nu && ur)
+      for (int i = tid; i < nu; i += NT) S.Quu[i * m + i] += ureg;
+    if (D.dQxx) {
+      const int64_t r = D.run(b, t);
+      for (int e = tid; e < n * n; e += NT) D.dQxx[r * D.sNN + e] = S.V[e];
+      for (int i = tid; i < n; i += NT) D.dQx[r * D.sN + i] = S.qx[i];
+      for (int e = tid; e < n * m; e += NT) D.dQxu[r * D.sNM + e] = (e / n < nu) ? S.Qxu[e] : 0.;
+      for (int e = tid; e < m * m; e += NT) D.dQuu[r * D.sMM + e] = (e % m < nu && e / m < nu) ? S.Quu[e] : 0.;
+      for (int i = tid; i < m; i += NT) D.dQu[r * D.sM + i] = i < nu ? S.qu[i] : 0.;
+    }
+    __syncthreads();
+    if (nu) {
+      // Cholesky (lower) of Quu — Eigen LLT fails on a pivot <= 0
+      for (int j = 0; j < nu; ++j) {
+        if (tid == 0) {
+          double sd = S.Quu[j * m + j];
+          for (int k2 = 0; k2 < j; ++k2) sd -= S.L[k2 * m + j] * S.L[k2 * m + j];
+          if (!(sd > 0.)) *S.flag = 1;
+          S.L[j * m + j] = sqrt(sd);
+        }
+        __syncthreads();
+        const double ljj = S.L[j * m + j];
+        for (int i = j + 1 + tid; i < nu; i += NT) {
+          double v = S.Quu[j * m + i];
+          for (int k2 = 0; k2 < j; ++k2) v -= S.L[k2 * m + i] * S.L[k2 * m + j];
+          S.L[j * m + i] = v / ljj;
+        }
+        __syncthreads();
+      }
+      if (*S.flag) return false;
+      // K = Quu^-1 Qxu^T (K in S.A, nu x n, ld m) ; k = Quu^-1 Qu
+      for (int j = tid; j <= n; j += NT) {
+        double* y = (j < n) ? S.A + j * m : S.kv;
+        for (int i = 0; i < nu; ++i) {
+          double v = (j < n) ? S.Qxu[i * n + j] : S.qu[i];
+          for (int k2 = 0; k2 < i; ++k2) v -= S.L[k2 * m + i] * y[k2];
+          y[i] = v / S.L[i * m + i];
+        }
+        for (int i = nu - 1; i >= 0; --i) {
+          double v = y[i];
+          for (int k2 = i + 1; k2 < nu; ++k2) v -= S.L[i * m + k2] * y[k2];
+          y[i] = v / S.L[i * m + i];
+        }
+      }
+      __syncthreads();
+      // store K, k ; Quuk = Quu k
+      {
+        const int64_t r = D.run(b, t);
+        double* Kg = D.K + r * D.sNM;
+        for (int e = tid; e < m * n; e += NT) Kg[e] = (e % m < nu) ? S.A[e] : 0.;
+        double* kg = D.k + r * D.sM;
+        for (int i = tid; i < m; i += NT) kg[i] = i < nu ? S.kv[i] : 0.;
+        for (int i = tid; i < nu; i += NT) {
+          double a = 0.;
+          for (int k2 = 0; k2 < nu; ++k2) a += S.Quu[k2 * m + i] * S.kv[k2];
+          S.quuk[i] = a;
+        }
+      }
+      __syncthreads();
+      // Vx = Qx + K^T Quuk - 2 K^T Qu   (or Qx - K^T Qu without ureg)
+      for (int i = tid; i < n; i += NT) {
+        const double* Kc = S.A + i * m;
+        if (ur) {
+          double a = 0., c = 0.;
+          for (int k2 = 0; k2 < nu; ++k2) a += Kc[k2] * S.quuk[k2];
+          for (int k2 = 0; k2 < nu; ++k2) c += Kc[k2] * S.qu[k2];
+          S.vx[i] = (S.qx[i] + a) - 2 * c;
+        } else {
+          double c = 0.;
+          for (int k2 = 0; k2 < nu; ++k2) c += Kc[k2] * S.qu[k2];
+          S.vx[i] = S.qx[i] - c;
+        }
+      }
+      // Vxx = Qxx - Qxu K
+      wg_gemm<NT, false, false>(n, n, nu, S.Qxu, n, S.A, m, S.V, n, S.V, n, -1.);
+    } else {
+      for (int i = tid; i < n; i += NT) S.vx[i] = S.qx[i];
+    }
+    __syncthreads();
+    // Vxx = 0.5 (Vxx + Vxx^T) (+ xreg I)
+    for (int e = tid; e < n * n; e += NT) {
+      const int i = e % n, j = e / n;
+      if (i < j) {
+        const double s2 = 0.5 * (S.V[j * n + i] + S.V[i * n + j]);
+        S.V[j * n + i] = s2;
+        S.V[i * n + j] = s2;
+      } else if (i == j && xr) {
+        S.V[e] += xreg;
+      }
+    }
+    __syncthreads();
+    // Vx += Vxx fs (infeasible), NaN checks, reduction terms
+    bool bad = false;
+    double pv[5] = {0., 0., 0., 0., 0.};
+    for (int i = tid; i < n; i += NT) {
+      double v = S.vx[i];
+      if (!feas) {
+        double a = 0.;
+        for (int j = 0; j < n; ++j) a += S.V[j * n + i] * S.fsv[j];
+        D.Vxxfs[kk * D.sN + i] = a;
+        v += a;
+        S.vx[i] = v;
+        pv[2] += v * S.fsv[i];
+        pv[3] += S.fsv[i] * a;
+      }
+      bad |= bad_entry(v);
+    }
+    for (int e = tid; e < n * n; e += NT) bad |= bad_entry(S.V[e]);
+    for (int i = tid; i < nu; i += NT) {
+      pv[0] += S.qu[i] * S.kv[i];    // Qu . k
+      pv[1] += S.kv[i] * S.quuk[i];  // k . Quuk
+      pv[4] += S.qu[i] * S.qu[i];    // |Qu|^2
+    }
+    if (bad) *S.flag = 1;
+    wg_sums<NT, 5>(pv, S.red);
+    if (tid == 0) {
+      double* p = D.part + kk * 8;
+      for (int j = 0; j < 5; ++j) p[j] = pv[j];
+    }
+    if (D.dVxx) {
+      for (int e = tid; e < n * n; e += NT) D.dVxx[kk * D.sNN + e] = S.V[e];
+      for (int i = tid; i < n; i += NT) D.dVx[kk * D.sN + i] = S.vx[i];
+    }
+    if (*S.flag) return false;
+  }
+  return true;
+}
+
+template <int NT>
+__global__ __launch_bounds__(NT) void backward_kernel(Dev D, Prm prm, int mode) {
+  const int b = blockIdx.x;
+  ElemState* st = D.st + b;
+  if (mode == 0 && !st->active) return;
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  BwdSmem S(sm, D.n, D.m);
+  const bool feas = st->is_feasible != 0;
+  double xreg = st->xreg, ureg = st->ureg;
+  bool ok;
+  for (;;) {
+    if (threadIdx.x == 0) *S.flag = 0;
+    __syncthreads();
+    ok = bwd_sweep<NT>(D, b, feas, xreg, ureg, S);
+    __syncthreads();
+    if (ok || mode == 1) break;
+    // increaseRegularization (ddp.cpp:312-318); abort at regmax (fddp.cpp:41-43)
+    xreg *= prm.regfactor;
+    if (xreg > prm.regmax) xreg = prm.regmax;
+    ureg = xreg;
+    if (xreg == prm.regmax) break;
+  }
+  if (threadIdx.x == 0) {
+    st->xreg = xreg;
+    st->ureg = ureg;
+    st->bwd_fail = ok ? 0 : 1;
+    if (!ok && mode == 0) {
+      st->status = FDDP_STATUS_REGMAX;
+      st->active = 0;
+    }
+    if (ok) {
+      // updateExpectedImprovement (fddp.cpp:126-147) and stoppingCriteria, in knot order
+      const double* p = D.part + D.knot(b, 0) * 8;
+      const int T = D.T;
+      double dg = 0., dq = 0., stop = 0.;
+      if (!feas) {
+        dg -= p[T * 8 + 2];
+        dq += p[T * 8 + 3];
+      }
+      for (int t = 0; t < T; ++t) {
+        if (D.knots[t].nu != 0) {
+          dg += p[t * 8 + 0];
+          dq -= p[t * 8 + 1];
+          stop += p[t * 8 + 4];
+        }
+        if (!feas) {
+          dg -= p[t * 8 + 2];
+          dq += p[t * 8 + 3];
+        }
+      }
+      st->dg = dg;
+      st->dq = dq;
+      st->stop = stop;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Forward pass — SolverFDDP::forwardPass (fddp.cpp:149-225) + the line search
+// and bookkeeping of SolverFDDP::solve (fddp.cpp:49-103). One workgroup per
+// element rolls the horizon out serially; trials are written into the other
+// trajectory buffer and accepted by flipping `cur` (no copy).
+// mode 0: full line search + regularisation/convergence update (solve).
+// mode 1: a single trial at `alpha` (tryStep), storing cost_try, dV and dv.
+// ---------------------------------------------------------------------------
+template <int NT>
+__device__ bool fwd_trial(const Dev& D, int b, const ElemState& s, double alpha, double* xv, double* uv, double* xn,
+                          double* red, int* flag, double& cost_try, double& dv) {
+  const int n = D.n, nx = D.nx, m = D.m, T = D.T, tid = threadIdx.x;
+  const int c = s.cur, o = 1 - c;
+  const bool feas = s.is_feasible != 0;
+  const bool full = feas || alpha == 1.;
+  const double* x0 = D.x0 + (int64_t)b * D.sX;
+  for (int i = tid; i < nx; i += NT) xn[i] = x0[i];
+  cost_try = 0.;
+  double* dvp = D.dvp + D.knot(b, 0);
+  __syncthreads();
+  for (int t = 0; t <= T; ++t) {
+    const int64_t kk = D.knot(b, t);
+    const double* fs = D.fs + kk * D.sN;
+    const double* xs = D.xs[c] + kk * D.sX;
+    double* xt = D.xs[o] + kk * D.sX;
+    // xs_try[t] = xnext  or  integrate(xnext, fs[t] * (alpha - 1))
+    double pd = 0.;
+    for (int i = tid; i < nx; i += NT) {
+      const double v = full ? xn[i] : xn[i] + fs[i] * (alpha - 1);
+      xv[i] = v;
+      xt[i] = v;
+      if (!feas) pd += (v - xs[i]) * D.Vxxfs[kk * D.sN + i];  // -fs^T Vxx diff(xs_try, xs)
+    }
+    __syncthreads();
+    const bool running = t < T;
+    const fddp_knot_desc kd = D.knots[t];
+    if (running) {
+      const int nu = kd.nu;
+      const double* us = D.us[c] + D.run(b, t) * D.sM;
+      const double* K = D.K + D.run(b, t) * D.sNM;
+      const double* kv = D.k + D.run(b, t) * D.sM;
+      double* ut = D.us[o] + D.run(b, t) * D.sM;
+      // us_try = us - k * alpha - K * dx ,  dx = diff(xs, xs_try)
+      for (int i = tid; i < m; i += NT) {
+        double v = 0.;
+        if (i < nu) {
+          double kd2 = 0.;
+          for (int j = 0; j < n; ++j) kd2 += K[(int64_t)j * m + i] * (xv[j] - xs[j]);
+          v = (us[i] - kv[i] * alpha) - kd2;
+        }
+        uv[i] = v;
+        ut[i] = v;
+      }
+      __syncthreads();
+    }
+    const double ct = knot_calc<NT>(kd, D.pblock(b, t), nx, xv, uv, running, xn, red);
+    bool bad = false;
+    if (running) {
+      double* xo = D.xnext[o] + D.run(b, t) * D.sX;
+      for (int i = tid; i < nx; i += NT) {
+        xo[i] = xn[i];
+        bad |= bad_entry(xn[i]);
+      }
+    }
+    if (!feas) pd = wg_sum<NT>(pd, red);
+    if (tid == 0) {
+      D.kcost[o][kk] = ct;
+      dvp[t] = pd;
+    }
+    cost_try += ct;
+    bad |= raise_if_nan(cost_try);
+    if (wg_any(bad, flag)) return false;
+  }
+  // dv: terminal first, then t = 0..T-1 (fddp.cpp:110-119). Summed by the
+  // thread that stored the terms (program order), broadcast through LDS.
+  if (tid == 0) {
+    double acc = 0.;
+    if (!feas) {
+      acc += dvp[T];
+      for (int t = 0; t < T; ++t) acc += dvp[t];
+    }
+    red[0] = acc;
+  }
+  __syncthreads();
+  dv = red[0];
+  __syncthreads();
+  return true;
+}
+
+template <int NT>
+__global__ __launch_bounds__(NT) void forward_kernel(Dev D, Prm prm, int mode, double alpha1, int* active_count) {
+  const int b = blockIdx.x;
+  ElemState* st = D.st + b;
+  if (mode == 0 && !st->active) return;
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  double* xv = sm;
+  double* uv = xv + D.sX;
+  double* xn = uv + D.sM;
+  double* red = xn + D.sX;
+  int* flag = (int*)(red + 5 * (NT / kWave) + 8);
+  ElemState s = *st;
+  if (mode == 1) {
+    double ct, dv;
+    const bool ok = fwd_trial<NT>(D, b, s, alpha1, xv, uv, xn, red, flag, ct, dv);
+    if (threadIdx.x == 0) {
+      st->fwd_fail = ok ? 0 : 1;
+      st->cost_try = ct;
+      st->dV = s.cost - ct;
+      st->dv = ok ? dv : 0.;
+    }
+    return;
+  }
+  // line search (fddp.cpp:53-81)
+  bool accepted = false;
+  for (int a = 0; a < prm.n_alphas; ++a) {
+    const double alpha = prm.alphas[a];
+    s.steplength = alpha;
+    double ct, dv;
+    if (!fwd_trial<NT>(D, b, s, alpha, xv, uv, xn, red, flag, ct, dv)) continue;
+    s.cost_try = ct;
+    s.dV = s.cost - ct;
+    s.dv = dv;
+    s.d0 = s.dg + dv;
+    s.d1 = s.dq - 2 * dv;
+    s.dVexp = alpha * (s.d0 + 0.5 * alpha * s.d1);
+    bool acc;
+    if (s.dVexp >= 0)
+      acc = s.d0 < prm.th_grad || s.dV > prm.th_acceptstep * s.dVexp;
+    else
+      acc = s.dV > prm.th_acceptnegstep * s.dVexp;
+    if (acc) {
+      s.was_feasible = s.is_feasible;
+      s.is_feasible = (s.was_feasible || alpha == 1.) ? 1 : 0;
+      s.cur = 1 - s.cur;
+      s.cost = ct;
+      accepted = true;
+      break;
+    }
+  }
+  s.recalc = accepted ? 1 : 0;
+  // regularisation schedule (fddp.cpp:83-91)
+  bool abort = false;
+  if (s.steplength > prm.th_stepdec) {
+    s.xreg /= prm.regfactor;
+    if (s.xreg < prm.regmin) s.xreg = prm.regmin;
+    s.ureg = s.xreg;
+  }
+  if (s.steplength <= prm.th_stepinc) {
+    s.xreg *= prm.regfactor;
+    if (s.xreg > prm.regmax) s.xreg = prm.regmax;
+    s.ureg = s.xreg;
+    if (s.xreg == prm.regmax) abort = true;
+  }
+  s.n_iter_run += 1;
+  if (abort) {
+    s.status = FDDP_STATUS_REGMAX;
+    s.active = 0;
+  } else if (s.was_feasible && s.stop < prm.th_stop) {  // fddp.cpp:100-102
+    s.status = FDDP_STATUS_CONVERGED;
+    s.active = 0;
+  } else {
+    s.iter += 1;
+  }
+  if (threadIdx.x == 0) {
+    *st = s;
+    if (s.active && active_count) atomicAdd(active_count, 1);
+  }
+}
+
+// x0 <- xs[1]; xs[t] <- xs[t+1]; us[t] <- us[t+1] (last kept), into the other buffer.
+template <int NT>
+__global__ __launch_bounds__(NT) void mpc_shift_kernel(Dev D) {
+  const int b = blockIdx.x;
+  ElemState* st = D.st + b;
+  const int c = st->cur, o = 1 - c, T = D.T;
+  const double* xs = D.xs[c] + D.knot(b, 0) * D.sX;
+  double* xo = D.xs[o] + D.knot(b, 0) * D.sX;
+  const double* us = D.us[c] + D.run(b, 0) * D.sM;
+  double* uo = D.us[o] + D.run(b, 0) * D.sM;
+  for (int64_t e = threadIdx.x; e < (int64_t)(T + 1) * D.sX; e += NT) {
+    const int64_t t = e / D.sX, i = e % D.sX;
+    const int64_t ts = t < T ? t + 1 : T;
+    xo[e] = xs[ts * D.sX + i];
+  }
+  for (int64_t e = threadIdx.x; e < (int64_t)T * D.sM; e += NT) {
+    const int64_t t = e / D.sM, i = e % D.sM;
+    const int64_t ts = t + 1 < T ? t + 1 : T - 1;
+    uo[e] = us[ts * D.sM + i];
+  }
+  for (int i = threadIdx.x; i < D.nx; i += NT) D.x0[(int64_t)b * D.sX + i] = xs[D.sX + i];
+  __syncthreads();
+  if (threadIdx.x == 0) st->cur = o;
+}
+
+// Solve prologue: per-element state (fddp.cpp:21-31, solver-base.cpp:66).
+__global__ void init_state_kernel(Dev D, int is_feasible, double xreg) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= D.B) return;
+  ElemState& s = D.st[b];
+  s.is_feasible = is_feasible;
+  s.xreg = xreg;
+  s.ureg = xreg;
+  s.was_feasible = 0;
+  s.recalc = 1;
+  s.iter = 0;
+  s.status = FDDP_STATUS_RUNNING;
+  s.active = 1;
+  s.n_iter_run = 0;
+  s.bwd_fail = 0;
+  s.fwd_fail = 0;
+}
+
+// Copy xs/us of the current buffer of every element into a dense output.
+__global__ void gather_traj_kernel(Dev D, int which, double* out) {
+  const int b = blockIdx.y;
+  const int c = D.st[b].cur;
+  const int64_t rows = which == 0 ? D.T + 1 : D.T;
+  const int w = which == 0 ? D.nx : D.m;
+  const int64_t sw = which == 0 ? D.sX : D.sM;
+  const double* src = (which == 0 ? D.xs[c] : D.us[c]) + (int64_t)b * rows * sw;
+  double* dst = out + (int64_t)b * rows * w;
+  for (int64_t e = blockIdx.x * blockDim.x + threadIdx.x; e < rows * w; e += (int64_t)gridDim.x * blockDim.x)
+    dst[e] = src[(e / w) * sw + e % w];
+}
+
+__global__ void scatter_traj_kernel(Dev D, int which, const double* in, int use_zero) {
+  const int b = blockIdx.y;
+  const int c = D.st[b].cur;
+  const int64_t rows = which == 0 ? D.T + 1 : D.T;
+  const int w = which == 0 ? D.nx : D.m;
+  const int64_t sw = which == 0 ? D.sX : D.sM;
+  double* dst = (which == 0 ? D.xs[c] : D.us[c]) + (int64_t)b * rows * sw;
+  const double* src = in + (int64_t)b * rows * w;
+  for (int64_t e = blockIdx.x * blockDim.x + threadIdx.x; e < rows * w; e += (int64_t)gridDim.x * blockDim.x)
+    dst[(e / w) * sw + e % w] = use_zero ? 0. : src[e];
+}
+
+}  // namespace fddp

@@ -1,0 +1,282 @@
+"""Knot (action) models with the reference's Python API, as parameter carriers.
+
+The models run on the device (crocoddyl_amd/csrc/knots.hpp); these classes
+only hold the parameters, validate them like the reference setters, and pack
+them into the C-ABI parameter blocks of include/fddp_hip.h (Eigen column-major).
+
+Every matrix/vector parameter may carry a leading batch axis (B, ...): then
+each batch element gets its own block (fddp_knot_desc.param_stride > 0).
+Without it the block is shared by all elements, as a reference model object
+shared by several knots is (benchmark/lqr-optctrl.cpp:28-31).
+
+Reference API mirrored (bindings/python/crocoddyl/core/...):
+  ActionModelLQR(nx, nu, driftFree=True)          core/actions/lqr.cpp:23-74
+  ActionModelUnicycle()  .costWeights               core/actions/unicycle.cpp:26-57
+  DifferentialActionModelLQR(nq, nu, driftFree=True) core/actions/diff-lqr.cpp
+  IntegratedActionModelEuler(diffModel, stepTime=1e-3, withCostResidual=True)
+                                                   core/integrator/euler.cpp
+"""
+import numpy as np
+
+from . import _abi
+
+_EPS = np.finfo(float).eps
+
+
+class StateVector:
+    """StateVector (core/states/euclidean.hxx): diff = x1 - x0, integrate = x + dx."""
+
+    def __init__(self, nx):
+        self.nx = int(nx)
+        self.ndx = int(nx)
+        self.nq = self.nx // 2 if self.nx % 2 == 0 else self.nx  # state-base.hxx:12-20
+        self.nv = self.ndx - self.nq if self.nx % 2 == 0 else 0
+
+    def zero(self):
+        return np.zeros(self.nx)
+
+    def rand(self):
+        return np.random.uniform(-1.0, 1.0, self.nx)  # Eigen VectorXs::Random
+
+    def diff(self, x0, x1):
+        return np.asarray(x1, float) - np.asarray(x0, float)
+
+    def integrate(self, x, dx):
+        return np.asarray(x, float) + np.asarray(dx, float)
+
+
+def _colmajor(a, r, c, name):
+    """(r,c) or (B,r,c) -> (Bm, r*c) column-major rows."""
+    a = np.asarray(a, dtype=np.float64)
+    if a.ndim == 2:
+        if a.shape != (r, c):
+            raise ValueError(f"Invalid argument: {name} has wrong dimension (it should be {r},{c})")
+        return a.T.reshape(1, -1)
+    if a.ndim == 3 and a.shape[1:] == (r, c):
+        return np.ascontiguousarray(a.transpose(0, 2, 1)).reshape(a.shape[0], -1)
+    raise ValueError(f"Invalid argument: {name} has wrong dimension (it should be {r},{c} or B,{r},{c})")
+
+
+def _vec(a, n, name):
+    a = np.asarray(a, dtype=np.float64)
+    if a.ndim == 1:
+        if a.shape != (n,):
+            raise ValueError(f"Invalid argument: {name} has wrong dimension (it should be {n})")
+        return a.reshape(1, -1)
+    if a.ndim == 2 and a.shape[1] == n:
+        return a
+    raise ValueError(f"Invalid argument: {name} has wrong dimension (it should be {n} or B,{n})")
+
+
+def _stack(parts, header):
+    """Concatenate (Bm_i, size_i) parts into (B, size) rows with a header."""
+    bs = {p.shape[0] for p in parts if p.shape[0] != 1}
+    if len(bs) > 1:
+        raise ValueError("Invalid argument: batched parameters have inconsistent batch sizes")
+    B = bs.pop() if bs else 1
+    hdr = np.broadcast_to(np.asarray(header, float).reshape(1, -1), (B, _abi.PARAM_HEADER))
+    cols = [hdr] + [np.broadcast_to(p, (B, p.shape[1])) for p in parts]
+    return np.ascontiguousarray(np.concatenate(cols, axis=1))
+
+
+class ActionModelAbstract:
+    """Base of the device-backed knot models (core/action-base.hpp:23-99)."""
+
+    kind = None
+
+    def __init__(self, state, nu, nr=0):
+        self.state = state
+        self.nu = int(nu)
+        self.nr = int(nr)
+        self._version = 0
+
+    def _touch(self):
+        self._version += 1
+
+    def pack(self):
+        """(kind, nu, blocks (Bm, size)) for the parameter pool."""
+        raise NotImplementedError
+
+    def createData(self):
+        return ActionData(self)
+
+
+class ActionData:
+    """Host view of one knot's ActionData (core/action-base.hpp:101-142),
+    filled from the device after ShootingProblem.calc/calcDiff."""
+
+    def __init__(self, model):
+        n, m = model.state.ndx, model.nu
+        self.cost = 0.0
+        self.xnext = np.zeros(model.state.nx)
+        self.Fx = np.zeros((n, n))
+        self.Fu = np.zeros((n, m))
+        self.Lx = np.zeros(n)
+        self.Lu = np.zeros(m)
+        self.Lxx = np.zeros((n, n))
+        self.Lxu = np.zeros((n, m))
+        self.Luu = np.zeros((m, m))
+
+
+class ActionModelLQR(ActionModelAbstract):
+    """ActionModelLQR (include/crocoddyl/core/actions/lqr.hxx:13-25 defaults)."""
+
+    kind = _abi.KNOT_LQR
+
+    def __init__(self, nx, nu, driftFree=True):
+        super().__init__(StateVector(nx), nu, 0)
+        nx, nu = int(nx), int(nu)
+        self.driftFree = bool(driftFree)
+        self._Fx = np.eye(nx)
+        self._Fu = np.eye(nx, nu)
+        self._f0 = np.ones(nx)
+        self._Lxx = np.eye(nx)
+        self._Lxu = np.eye(nx, nu)
+        self._Luu = np.eye(nu)
+        self._lx = np.ones(nx)
+        self._lu = np.ones(nu)
+
+    def _set(self, name, v, shape):
+        v = np.array(v, dtype=np.float64)
+        if v.shape[-len(shape):] != shape or v.ndim not in (len(shape), len(shape) + 1):
+            raise ValueError(f"Invalid argument: {name} has wrong dimension (it should be {shape})")
+        setattr(self, "_" + name, v)
+        self._touch()
+
+    nx_ = property(lambda s: s.state.nx)
+    Fx = property(lambda s: s._Fx, lambda s, v: s._set("Fx", v, (s.state.nx, s.state.nx)))
+    Fu = property(lambda s: s._Fu, lambda s, v: s._set("Fu", v, (s.state.nx, s.nu)))
+    f0 = property(lambda s: s._f0, lambda s, v: s._set("f0", v, (s.state.nx,)))
+    Lxx = property(lambda s: s._Lxx, lambda s, v: s._set("Lxx", v, (s.state.nx, s.state.nx)))
+    Lxu = property(lambda s: s._Lxu, lambda s, v: s._set("Lxu", v, (s.state.nx, s.nu)))
+    Luu = property(lambda s: s._Luu, lambda s, v: s._set("Luu", v, (s.nu, s.nu)))
+    lx = property(lambda s: s._lx, lambda s, v: s._set("lx", v, (s.state.nx,)))
+    lu = property(lambda s: s._lu, lambda s, v: s._set("lu", v, (s.nu,)))
+
+    def pack(self):
+        nx, nu = self.state.nx, self.nu
+        parts = [_colmajor(self._Fx, nx, nx, "Fx"), _colmajor(self._Fu, nx, nu, "Fu"), _vec(self._f0, nx, "f0"),
+                 _colmajor(self._Lxx, nx, nx, "Lxx"), _colmajor(self._Lxu, nx, nu, "Lxu"),
+                 _colmajor(self._Luu, nu, nu, "Luu"), _vec(self._lx, nx, "lx"), _vec(self._lu, nu, "lu")]
+        return self.kind, nu, _stack(parts, [1.0 if self.driftFree else 0.0, 0, 0, 0])
+
+
+class ActionModelUnicycle(ActionModelAbstract):
+    """ActionModelUnicycle (core/actions/unicycle.hxx:13-16): nx=3, nu=2, nr=5, dt=0.1."""
+
+    kind = _abi.KNOT_UNICYCLE
+
+    def __init__(self):
+        super().__init__(StateVector(3), 2, 5)
+        self._w = np.array([10.0, 1.0])
+        self._dt = 0.1
+
+    @property
+    def costWeights(self):
+        return self._w.copy()
+
+    @costWeights.setter
+    def costWeights(self, w):
+        w = np.asarray(w, float)
+        if w.shape != (2,):
+            raise ValueError("Invalid argument: costWeights has wrong dimension (it should be 2)")
+        self._w = w.copy()
+        self._touch()
+
+    @property
+    def dt(self):
+        return self._dt
+
+    @dt.setter
+    def dt(self, v):
+        self._dt = float(v)
+        self._touch()
+
+    def pack(self):
+        return self.kind, 2, np.array([[self._dt, self._w[0], self._w[1], 0.0]])
+
+
+class DifferentialActionModelLQR:
+    """DifferentialActionModelLQR (core/actions/diff-lqr.hxx:14-28 defaults).
+    Only usable inside IntegratedActionModelEuler on the device."""
+
+    def __init__(self, nq, nu, driftFree=True):
+        nq, nu = int(nq), int(nu)
+        self.state = StateVector(2 * nq)
+        self.nu = nu
+        self.nr = 0
+        self.driftFree = bool(driftFree)
+        nx = 2 * nq
+        self._Fq = np.eye(nq)
+        self._Fv = np.eye(nq)
+        self._Fu = np.eye(nq, nu)
+        self._f0 = np.ones(nq)
+        self._Lxx = np.eye(nx)
+        self._Lxu = np.eye(nx, nu)
+        self._Luu = np.eye(nu)
+        self._lx = np.ones(nx)
+        self._lu = np.ones(nu)
+        self._version = 0
+        self._owners = []
+
+    def _set(self, name, v, shape):
+        v = np.array(v, dtype=np.float64)
+        if v.shape[-len(shape):] != shape or v.ndim not in (len(shape), len(shape) + 1):
+            raise ValueError(f"Invalid argument: {name} has wrong dimension (it should be {shape})")
+        setattr(self, "_" + name, v)
+        self._version += 1
+        for o in self._owners:
+            o._touch()
+
+    @property
+    def nq(self):
+        return self.state.nx // 2
+
+    Fq = property(lambda s: s._Fq, lambda s, v: s._set("Fq", v, (s.nq, s.nq)))
+    Fv = property(lambda s: s._Fv, lambda s, v: s._set("Fv", v, (s.nq, s.nq)))
+    Fu = property(lambda s: s._Fu, lambda s, v: s._set("Fu", v, (s.nq, s.nu)))
+    f0 = property(lambda s: s._f0, lambda s, v: s._set("f0", v, (s.nq,)))
+    Lxx = property(lambda s: s._Lxx, lambda s, v: s._set("Lxx", v, (s.state.nx, s.state.nx)))
+    Lxu = property(lambda s: s._Lxu, lambda s, v: s._set("Lxu", v, (s.state.nx, s.nu)))
+    Luu = property(lambda s: s._Luu, lambda s, v: s._set("Luu", v, (s.nu, s.nu)))
+    lx = property(lambda s: s._lx, lambda s, v: s._set("lx", v, (s.state.nx,)))
+    lu = property(lambda s: s._lu, lambda s, v: s._set("lu", v, (s.nu,)))
+
+
+class IntegratedActionModelEuler(ActionModelAbstract):
+    """IntegratedActionModelEuler (core/integrator/euler.hxx:16-35) around a
+    DifferentialActionModelLQR (the device-covered differential model)."""
+
+    kind = _abi.KNOT_EULER_DIFFLQR
+
+    def __init__(self, diffModel, stepTime=1e-3, withCostResidual=True):
+        if not isinstance(diffModel, DifferentialActionModelLQR):
+            raise NotImplementedError("crocoddyl_amd: the device path covers Euler(DifferentialActionModelLQR) "
+                                      f"knots only; got {type(diffModel).__name__}")
+        super().__init__(diffModel.state, diffModel.nu, diffModel.nr)
+        self.differential = diffModel
+        diffModel._owners.append(self)
+        self.withCostResidual = bool(withCostResidual)
+        dt = float(stepTime)
+        if dt < 0.0:  # euler.hxx:27-31
+            dt = 1e-3
+        self._dt = dt
+
+    @property
+    def dt(self):
+        return self._dt
+
+    @dt.setter
+    def dt(self, v):
+        if v < 0.0:
+            raise ValueError("Invalid argument: dt has positive value")  # euler.hxx:160-167
+        self._dt = float(v)
+        self._touch()
+
+    def pack(self):
+        d = self.differential
+        nq, nu, nx = d.nq, d.nu, d.state.nx
+        parts = [_colmajor(d._Fq, nq, nq, "Fq"), _colmajor(d._Fv, nq, nq, "Fv"), _colmajor(d._Fu, nq, nu, "Fu"),
+                 _vec(d._f0, nq, "f0"), _colmajor(d._Lxx, nx, nx, "Lxx"), _colmajor(d._Lxu, nx, nu, "Lxu"),
+                 _colmajor(d._Luu, nu, nu, "Luu"), _vec(d._lx, nx, "lx"), _vec(d._lu, nu, "lu")]
+        return self.kind, nu, _stack(parts, [self._dt, 1.0 if d.driftFree else 0.0, 0, 0])

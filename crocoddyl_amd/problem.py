@@ -1,0 +1,576 @@
+"""ShootingProblem and SolverFDDP with the reference's Python API, batched.
+
+Reference API mirrored:
+  ShootingProblem(x0, runningModels, terminalModel)
+      bindings/python/crocoddyl/core/optctrl/shooting.cpp:18-120,
+      include/crocoddyl/core/optctrl/shooting.hxx:17-223
+  SolverFDDP(problem).solve(init_xs=[], init_us=[], maxiter=100, isFeasible=False, regInit=1e-9)
+      bindings/python/crocoddyl/core/solvers/fddp.cpp:18-70, core/solver-base.cpp:100-126,
+      core/solvers/ddp.cpp:84-125
+
+Batching: x0 of shape (B, nx) (or models with batched parameters) makes the
+problem a batch of B independent problems sharing the knot sequence. Then
+xs/us are arrays (B, T+1, nx) / (B, T, nu_max) and scalars become (B,)
+arrays; with a 1-D x0 everything has the reference's single-problem shapes.
+
+All computation runs in libfddp_hip on the GPU; nothing here computes.
+"""
+import ctypes as C
+import math
+import warnings
+
+import numpy as np
+
+from . import _abi
+from ._lib import FDDPError, check, default_params, lib
+from .models import ActionData, ActionModelAbstract
+
+
+def pack_problem(running, terminal, B):
+    """Knot descriptors + parameter pool for T running knots and the terminal.
+
+    Models shared by several knots get one block (or one block per batch
+    element if their parameters are batched)."""
+    models = list(running) + [terminal]
+    for m in models:
+        if not isinstance(m, ActionModelAbstract) or m.kind is None:
+            raise NotImplementedError(f"crocoddyl_amd: knot model {type(m).__name__} has no device implementation")
+    offsets = {}
+    pool = []
+    pos = 0
+    knots = []
+    for m in models:
+        key = id(m)
+        if key not in offsets:
+            kind, nu, blocks = m.pack()
+            if blocks.shape[0] not in (1, B):
+                raise ValueError(f"Invalid argument: model parameters are batched over {blocks.shape[0]} "
+                                 f"elements but the problem has B={B}")
+            stride = blocks.shape[1] if blocks.shape[0] == B and B > 1 else 0
+            offsets[key] = (kind, nu, pos, stride)
+            pool.append(blocks[0:1] if stride == 0 else blocks)
+            pos += blocks.size if stride else blocks.shape[1]
+        kind, nu, off, stride = offsets[key]
+        knots.append((kind, nu, off, stride))
+    flat = np.concatenate([p.reshape(-1) for p in pool]) if pool else np.zeros(1)
+    return knots, np.ascontiguousarray(flat, dtype=np.float64)
+
+
+def batch_size_of(x0, models):
+    x0 = np.asarray(x0, float)
+    B = x0.shape[0] if x0.ndim == 2 else 1
+    for m in models:
+        _, _, blocks = m.pack()
+        if blocks.shape[0] > 1:
+            if B == 1 and x0.ndim == 1:
+                B = blocks.shape[0]
+            elif blocks.shape[0] != B:
+                raise ValueError("Invalid argument: batched model parameters and x0 disagree on B")
+    return B
+
+
+class _Handle:
+    """Owns one fddp_handle (device memory for one batched problem+solver)."""
+
+    def __init__(self, problem, device):
+        self.problem = problem
+        self.device = device
+        self.ptr = C.c_void_p()
+        knots, pool = problem._packed()
+        self.n_params = pool.size
+        self._sig = problem._signature()
+        dims = problem._dims()
+        kd = (_abi.KnotDesc * len(knots))(*[_abi.KnotDesc(*k) for k in knots])
+        check(lib().fddp_create(C.byref(dims), kd, _abi.dptr(pool), pool.size, device, C.byref(self.ptr)))
+        self.set_x0(problem._x0b)
+
+    def refresh(self):
+        sig = self.problem._signature()
+        if sig != self._sig:
+            knots, pool = self.problem._packed()
+            if pool.size != self.n_params:
+                raise FDDPError("model parameter layout changed; rebuild the ShootingProblem")
+            check(lib().fddp_set_model_params(self.ptr, _abi.dptr(pool), pool.size))
+            self._sig = sig
+        return self.ptr
+
+    def set_x0(self, x0b):
+        check(lib().fddp_set_x0(self.ptr, _abi.dptr(np.ascontiguousarray(x0b, dtype=np.float64))))
+
+    def __del__(self):
+        try:
+            if self.ptr:
+                lib().fddp_destroy(self.ptr)
+                self.ptr = C.c_void_p()
+        except Exception:
+            pass
+
+
+class ShootingProblem:
+    """ShootingProblem (shooting.hxx:17-59): x0, T running models, terminal model."""
+
+    def __init__(self, x0, runningModels, terminalModel, device=0):
+        runningModels = list(runningModels)
+        if len(runningModels) < 1:
+            raise ValueError("Invalid argument: at least one running model is needed")
+        x0 = np.array(x0, dtype=np.float64)
+        self._models = runningModels
+        self._terminal = terminalModel
+        self.nx = runningModels[0].state.nx
+        self.ndx = runningModels[0].state.ndx
+        self.nu_max = max(m.nu for m in runningModels)
+        for i, m in enumerate(runningModels):  # shooting.hxx:39-49
+            if m.state.nx != self.nx:
+                raise ValueError(f"Invalid argument: nx in {i} node is not consistent with the other nodes")
+            if m.state.ndx != self.ndx:
+                raise ValueError(f"Invalid argument: ndx in {i} node is not consistent with the other nodes")
+        if terminalModel.state.nx != self.nx:
+            raise ValueError("Invalid argument: nx in terminal node is not consistent with the other nodes")
+        if x0.shape[-1] != self.nx or x0.ndim not in (1, 2):
+            raise ValueError(f"Invalid argument: x0 has wrong dimension (it should be {self.nx})")
+        self.batched = x0.ndim == 2 or any(m.pack()[2].shape[0] > 1 for m in set(runningModels + [terminalModel]))
+        self.B = batch_size_of(x0, set(runningModels + [terminalModel]))
+        self._x0b = np.broadcast_to(x0, (self.B, self.nx)).copy() if x0.ndim == 1 else x0.copy()
+        self.device = device
+        self._calc_h = None
+        self._solver_handles = []
+        self.runningDatas = [m.createData() for m in runningModels]
+        self.terminalData = terminalModel.createData()
+        self.cost = 0.0
+
+    # -- reference accessors -------------------------------------------------
+    @property
+    def T(self):
+        return len(self._models)
+
+    @property
+    def runningModels(self):
+        return list(self._models)
+
+    @property
+    def terminalModel(self):
+        return self._terminal
+
+    @property
+    def x0(self):
+        return self._x0b.copy() if self.batched else self._x0b[0].copy()
+
+    @x0.setter
+    def x0(self, x0):
+        """ShootingProblem::set_x0 (shooting.hxx:391-397)."""
+        x0 = np.asarray(x0, dtype=np.float64)
+        if x0.shape[-1] != self.nx:
+            raise ValueError(f"Invalid argument: x0 has wrong dimension (it should be {self.nx})")
+        self._x0b = np.broadcast_to(x0, (self.B, self.nx)).copy()
+        for h in self._handles():
+            h.set_x0(self._x0b)
+
+    # -- packing ---------------------------------------------------------------
+    def _dims(self):
+        return _abi.Dims(self.nx, self.ndx, self.nu_max, self.T, self.B)
+
+    def _packed(self):
+        return pack_problem(self._models, self._terminal, self.B)
+
+    def _signature(self):
+        return tuple((id(m), m._version) for m in self._models + [self._terminal])
+
+    def _handles(self):
+        hs = []
+        if self._calc_h is not None:
+            hs.append(self._calc_h)
+        hs.extend(self._solver_handles)
+        return hs
+
+    def _new_handle(self):
+        return _Handle(self, self.device)
+
+    def _calc_handle(self):
+        if self._calc_h is None:
+            self._calc_h = _Handle(self, self.device)
+        return self._calc_h.refresh()
+
+    # -- trajectories in/out ---------------------------------------------------
+    def _xs_array(self, xs):
+        T, nx, B = self.T, self.nx, self.B
+        if xs is None or (isinstance(xs, (list, tuple)) and len(xs) == 0):
+            return None
+        a = np.asarray(xs, dtype=np.float64) if not isinstance(xs, (list, tuple)) else np.stack(
+            [np.asarray(x, float) for x in xs], axis=-2)
+        if a.shape[-2:] != (T + 1, nx):
+            raise ValueError(f"Invalid argument: xs has wrong dimension (it should be {T + 1})")
+        return np.ascontiguousarray(np.broadcast_to(a, (B, T + 1, nx)))
+
+    def _us_array(self, us):
+        T, m, B = self.T, self.nu_max, self.B
+        if us is None or (isinstance(us, (list, tuple)) and len(us) == 0):
+            return None
+        if isinstance(us, (list, tuple)):
+            rows = []
+            for u in us:
+                u = np.asarray(u, float)
+                if u.shape[-1] != m:
+                    pad = np.zeros(u.shape[:-1] + (m,))
+                    pad[..., :u.shape[-1]] = u
+                    u = pad
+                rows.append(u)
+            a = np.stack(rows, axis=-2)
+        else:
+            a = np.asarray(us, dtype=np.float64)
+        if a.shape[-2:] != (T, m):
+            raise ValueError(f"Invalid argument: us has wrong dimension (it should be {T})")
+        return np.ascontiguousarray(np.broadcast_to(a, (B, T, m)))
+
+    def _out_x(self, a):
+        return a if self.batched else [a[0, t].copy() for t in range(a.shape[1])]
+
+    def _out_u(self, a):
+        if self.batched:
+            return a
+        return [a[0, t, :self._models[t].nu].copy() for t in range(a.shape[1])]
+
+    def _fill_datas(self, h, diff):
+        L = lib()
+        B, T, n, m = self.B, self.T, self.ndx, self.nu_max
+
+        def q(which, nk, per):
+            out = np.zeros((B, nk, per))
+            check(L.fddp_get_quantity(h, which, _abi.dptr(out)))
+            return out
+
+        xn = q(_abi.Q_XNEXT, T, self.nx)
+        if diff:
+            Fx = q(_abi.Q_FX, T + 1, n * n)
+            Fu = q(_abi.Q_FU, T + 1, n * m)
+            Lxx = q(_abi.Q_LXX, T + 1, n * n)
+            Lxu = q(_abi.Q_LXU, T + 1, n * m)
+            Luu = q(_abi.Q_LUU, T + 1, m * m)
+            Lx = q(_abi.Q_LX, T + 1, n)
+            Lu = q(_abi.Q_LU, T + 1, max(m, 0))
+        datas = self.runningDatas + [self.terminalData]
+        models = self._models + [self._terminal]
+        sel = (slice(None),) if self.batched else (0,)
+        for t, (d, mdl) in enumerate(zip(datas, models)):
+            if t < T:
+                d.xnext = xn[sel + (t,)].copy()
+            if diff:
+                d.Fx = _cm(Fx[:, t], n, n)[sel]
+                d.Fu = _cm(Fu[:, t], n, m)[sel][..., :mdl.nu]
+                d.Lxx = _cm(Lxx[:, t], n, n)[sel]
+                d.Lxu = _cm(Lxu[:, t], n, m)[sel][..., :mdl.nu]
+                d.Luu = _cm(Luu[:, t], m, m)[sel][..., :mdl.nu, :mdl.nu]
+                d.Lx = Lx[:, t][sel].copy()
+                d.Lu = Lu[:, t][sel][..., :mdl.nu].copy()
+
+    # -- ShootingProblem::calc / calcDiff / rollout ----------------------------
+    def calc(self, xs, us):
+        """shooting.hxx:133-161; returns the total cost (per element if batched)."""
+        h = self._calc_handle()
+        xa, ua = self._xs_array(xs), self._us_array(us)
+        if xa is None or (ua is None and self.nu_max > 0):
+            raise ValueError("Invalid argument: xs/us have wrong dimension")
+        check(lib().fddp_set_candidate(h, _abi.dptr(xa), _abi.dptr(ua), 0))
+        cost = np.zeros(self.B)
+        check(lib().fddp_problem_calc(h, _abi.dptr(cost)))
+        self._fill_datas(h, diff=False)
+        self.cost = cost if self.batched else float(cost[0])
+        return self.cost
+
+    def calcDiff(self, xs, us):
+        """shooting.hxx:164-195 (calc first, as the reference's datas carry the costs)."""
+        self.calc(xs, us)
+        h = self._calc_handle()
+        cost = np.zeros(self.B)
+        check(lib().fddp_problem_calc_diff(h, _abi.dptr(cost)))
+        self._fill_datas(h, diff=True)
+        self.cost = cost if self.batched else float(cost[0])
+        return self.cost
+
+    def rollout(self, us):
+        """shooting.hxx:198-223: xs[0] = x0, xs[t+1] = f(xs[t], us[t]).
+
+        Runs as the device forward pass with zero feedback gains (this
+        handle never computes a backward pass, so K = k = 0), alpha = 1."""
+        h = self._calc_handle()
+        ua = self._us_array(us)
+        check(lib().fddp_set_candidate(h, None, _abi.dptr(ua), 1))
+        st = np.zeros(self.B, dtype=np.int32)
+        check(lib().fddp_try_step(h, 1.0, None, st.ctypes.data_as(_abi.I32)))
+        xs = np.zeros((self.B, self.T + 1, self.nx))
+        check(lib().fddp_get_xs_try(h, _abi.dptr(xs)))
+        return self._out_x(xs)
+
+    def rollout_us(self, us):
+        return self.rollout(us)
+
+
+def _cm(flat, r, c):
+    """(B, r*c) column-major rows -> (B, r, c)."""
+    return np.ascontiguousarray(flat.reshape(flat.shape[0], c, r).transpose(0, 2, 1))
+
+
+class SolverFDDP:
+    """SolverFDDP (src/core/solvers/fddp.cpp) on the device, batched."""
+
+    def __init__(self, problem):
+        self.problem = problem
+        self._h = problem._new_handle()
+        problem._solver_handles.append(self._h)
+        self._prm = default_params()
+        self._results = None
+        self.callbacks = []
+
+    # -- helpers -----------------------------------------------------------
+    @property
+    def _ptr(self):
+        return self._h.refresh()
+
+    def _push_params(self):
+        check(lib().fddp_set_params(self._ptr, C.byref(self._prm)))
+
+    def _scalar(self, arr):
+        return arr if self.problem.batched else arr[0]
+
+    def _res(self):
+        if self._results is None:
+            r = (_abi.Result * self.problem.B)()
+            check(lib().fddp_get_results(self._ptr, r))
+            self._results = r
+        return self._results
+
+    def _field(self, name, conv=float):
+        r = self._res()
+        arr = np.array([conv(getattr(x, name)) for x in r])
+        return arr if self.problem.batched else arr[0]
+
+    # -- SolverAbstract::setCandidate / solve --------------------------------
+    def setCandidate(self, xs=[], us=[], isFeasible=False):
+        p = self.problem
+        xa, ua = p._xs_array(xs), p._us_array(us)
+        check(lib().fddp_set_candidate(self._ptr, _abi.dptr(xa), _abi.dptr(ua), 1 if isFeasible else 0))
+        self._results = None
+
+    def solve(self, init_xs=[], init_us=[], maxiter=100, isFeasible=False, regInit=1e-9):
+        """fddp.cpp:19-105 for every batch element; returns solve()'s bool
+        (an array of bools when batched)."""
+        self._push_params()
+        self.setCandidate(init_xs, init_us, isFeasible)
+        return self.solve_from_candidate(maxiter, isFeasible, regInit)
+
+    def solve_from_candidate(self, maxiter=100, isFeasible=False, regInit=1e-9):
+        """solve() without re-uploading a warm start (device-resident MPC loops)."""
+        self._push_params()
+        reg = float("nan") if regInit is None else float(regInit)
+        r = (_abi.Result * self.problem.B)()
+        check(lib().fddp_solve(self._ptr, int(maxiter), 1 if isFeasible else 0, reg, r))
+        self._results = r
+        ok = np.array([x.status == _abi.STATUS_CONVERGED for x in r])
+        for cb in self.callbacks:
+            cb(self)
+        return ok if self.problem.batched else bool(ok[0])
+
+    def setCallbacks(self, callbacks):
+        self.callbacks = list(callbacks)
+
+    def getCallbacks(self):
+        return list(self.callbacks)
+
+    # -- step API (SolverDDP methods) ----------------------------------------
+    def computeDirection(self, recalc=True):
+        """ddp.cpp:120-125. Raises on backward_error (single problem); returns
+        the per-element failure flags when batched."""
+        self._push_params()
+        st = np.zeros(self.problem.B, dtype=np.int32)
+        check(lib().fddp_compute_direction(self._ptr, 1 if recalc else 0, st.ctypes.data_as(_abi.I32)))
+        self._results = None
+        if not self.problem.batched and st[0]:
+            raise FDDPError("backward_error")
+        return st.astype(bool) if self.problem.batched else None
+
+    def tryStep(self, stepLength=1.0):
+        """ddp.cpp:127-130; returns cost - cost_try."""
+        dV = np.zeros(self.problem.B)
+        st = np.zeros(self.problem.B, dtype=np.int32)
+        check(lib().fddp_try_step(self._ptr, float(stepLength), _abi.dptr(dV), st.ctypes.data_as(_abi.I32)))
+        self._results = None
+        if not self.problem.batched and st[0]:
+            raise FDDPError("forward_error")
+        return self._scalar(dV)
+
+    def stoppingCriteria(self):
+        s = np.zeros(self.problem.B)
+        check(lib().fddp_stopping_criteria(self._ptr, _abi.dptr(s)))
+        return self._scalar(s)
+
+    def expectedImprovement(self):
+        d = np.zeros((self.problem.B, 2))
+        check(lib().fddp_expected_improvement(self._ptr, _abi.dptr(d)))
+        self._results = None
+        return d if self.problem.batched else d[0]
+
+    def updateExpectedImprovement(self):
+        check(lib().fddp_update_expected_improvement(self._ptr))
+
+    def setSolverState(self, iter=0, xreg=float("nan"), ureg=float("nan"), wasFeasible=False):
+        check(lib().fddp_set_solver_state(self._ptr, int(iter), float(xreg), float(ureg), int(wasFeasible)))
+        self._results = None
+
+    # -- trajectories -----------------------------------------------------------
+    @property
+    def xs(self):
+        p = self.problem
+        a = np.zeros((p.B, p.T + 1, p.nx))
+        check(lib().fddp_get_xs(self._ptr, _abi.dptr(a), 0))
+        return p._out_x(a)
+
+    @xs.setter
+    def xs(self, v):
+        self.setCandidate(v, self.us, bool(np.all(self._field("is_feasible", int))))
+
+    @property
+    def us(self):
+        p = self.problem
+        a = np.zeros((p.B, p.T, p.nu_max))
+        check(lib().fddp_get_us(self._ptr, _abi.dptr(a), 0))
+        return p._out_u(a)
+
+    @us.setter
+    def us(self, v):
+        self.setCandidate(self.xs, v, bool(np.all(self._field("is_feasible", int))))
+
+    def xs_device(self, out_ptr):
+        """Copy xs (B, T+1, nx) into a device buffer on the solver's GPU."""
+        check(lib().fddp_get_xs(self._ptr, C.cast(out_ptr, _abi.D), 1))
+
+    def us_device(self, out_ptr):
+        check(lib().fddp_get_us(self._ptr, C.cast(out_ptr, _abi.D), 1))
+
+    def _quantity(self, which, nk, r, c=None, nu_slice=None):
+        p = self.problem
+        per = r * (c or 1)
+        a = np.zeros((p.B, nk, per))
+        check(lib().fddp_get_quantity(self._ptr, which, _abi.dptr(a)))
+        if c is not None:
+            a = a.reshape(p.B, nk, c, r).transpose(0, 1, 3, 2)
+        if p.batched:
+            return a
+        out = []
+        models = p._models + [p._terminal]
+        for t in range(nk):
+            v = a[0, t]
+            if nu_slice == "rows":
+                v = v[:models[t].nu]
+            elif nu_slice == "cols":
+                v = v[..., :models[t].nu]
+            elif nu_slice == "both":
+                v = v[:models[t].nu, :models[t].nu]
+            out.append(np.array(v))
+        return out
+
+    def _debug(self, on=True):
+        check(lib().fddp_set_debug(self._ptr, 1 if on else 0))
+
+    # SolverDDP getters (ddp.hpp:60-271)
+    K = property(lambda s: s._quantity(_abi.Q_K, s.problem.T, s.problem.nu_max, s.problem.ndx, "rows"))
+    k = property(lambda s: s._quantity(_abi.Q_KV, s.problem.T, s.problem.nu_max, None, "rows"))
+    fs = property(lambda s: s._quantity(_abi.Q_FS, s.problem.T + 1, s.problem.ndx))
+    Vxx = property(lambda s: s._quantity(_abi.Q_VXX, s.problem.T + 1, s.problem.ndx, s.problem.ndx))
+    Vx = property(lambda s: s._quantity(_abi.Q_VX, s.problem.T + 1, s.problem.ndx))
+    Qxx = property(lambda s: s._quantity(_abi.Q_QXX, s.problem.T, s.problem.ndx, s.problem.ndx))
+    Qxu = property(lambda s: s._quantity(_abi.Q_QXU, s.problem.T, s.problem.ndx, s.problem.nu_max, "cols"))
+    Quu = property(lambda s: s._quantity(_abi.Q_QUU, s.problem.T, s.problem.nu_max, s.problem.nu_max, "both"))
+    Qx = property(lambda s: s._quantity(_abi.Q_QX, s.problem.T, s.problem.ndx))
+    Qu = property(lambda s: s._quantity(_abi.Q_QU, s.problem.T, s.problem.nu_max, None, "rows"))
+
+    # SolverAbstract getters (solver-base.cpp:100-126)
+    cost = property(lambda s: s._field("cost"))
+    stop = property(lambda s: s._field("stop"))
+    iter = property(lambda s: s._field("iter", int))
+    x_reg = property(lambda s: s._field("xreg"))
+    u_reg = property(lambda s: s._field("ureg"))
+    stepLength = property(lambda s: s._field("steplength"))
+    isFeasible = property(lambda s: s._field("is_feasible", bool))
+    dV = property(lambda s: s._field("dV"))
+    dVexp = property(lambda s: s._field("dVexp"))
+    status = property(lambda s: s._field("status", int))
+    n_iter_run = property(lambda s: s._field("n_iter_run", int))
+
+    @property
+    def d(self):
+        r = self._res()
+        a = np.array([[x.d0, x.d1] for x in r])
+        return a if self.problem.batched else a[0]
+
+    # thresholds with the reference setter validation (via fddp_set_params)
+    def _prm_prop(name, alias=None):
+        def get(self):
+            return getattr(self._prm, name)
+
+        def set_(self, v):
+            old = getattr(self._prm, name)
+            setattr(self._prm, name, float(v))
+            try:
+                self._push_params()
+            except FDDPError:
+                setattr(self._prm, name, old)
+                raise
+
+        return property(get, set_)
+
+    th_acceptStep = _prm_prop("th_acceptstep")
+    th_stop = _prm_prop("th_stop")
+    th_grad = _prm_prop("th_grad")
+    th_stepDec = _prm_prop("th_stepdec")
+    th_stepInc = _prm_prop("th_stepinc")
+    th_acceptNegStep = _prm_prop("th_acceptnegstep")
+    regFactor = _prm_prop("regfactor")
+    regMin = _prm_prop("regmin")
+    regMax = _prm_prop("regmax")
+
+    @property
+    def alphas(self):
+        return [self._prm.alphas[i] for i in range(self._prm.n_alphas)]
+
+    @alphas.setter
+    def alphas(self, a):
+        a = [float(x) for x in a]
+        if not a or len(a) > 16:
+            raise ValueError("Invalid argument: between 1 and 16 alphas")
+        if a[0] != 1.0:
+            warnings.warn("alpha[0] should be 1")  # ddp.cpp:446-448
+        old = (self._prm.n_alphas, list(self._prm.alphas))
+        self._prm.n_alphas = len(a)
+        for i in range(16):
+            self._prm.alphas[i] = a[i] if i < len(a) else 0.0
+        try:
+            self._push_params()
+        except FDDPError:
+            self._prm.n_alphas = old[0]
+            for i in range(16):
+                self._prm.alphas[i] = old[1][i]
+            raise
+
+    # -- MPC plumbing ---------------------------------------------------------
+    def mpcShift(self):
+        """x0 <- xs[1]; shift xs/us one knot (on device)."""
+        check(lib().fddp_mpc_shift(self._ptr))
+        x0 = np.zeros((self.problem.B, self.problem.nx))
+        check(lib().fddp_get_x0(self._ptr, _abi.dptr(x0)))
+        self.problem._x0b = x0
+        for h in self.problem._handles():
+            if h is not self._h:
+                h.set_x0(x0)
+
+    # -- timing (HIP events on the handle's stream) ----------------------------
+    def set_timing(self, on=True):
+        check(lib().fddp_set_timing(self._ptr, 1 if on else 0))
+
+    def get_timing(self):
+        ms = np.zeros(4)
+        cnt = np.zeros(4, dtype=np.int64)
+        check(lib().fddp_get_timing(self._ptr, _abi.dptr(ms), cnt.ctypes.data_as(C.POINTER(C.c_int64))))
+        names = ["calc", "calcDiff", "backward", "forward"]
+        return {n: (float(ms[i]), int(cnt[i])) for i, n in enumerate(names)}
+
+    def synchronize(self):
+        check(lib().fddp_synchronize(self._ptr))

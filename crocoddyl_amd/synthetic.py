@@ -1,0 +1,89 @@
+"""Seeded synthetic problems for the BASELINE.json configs.
+
+There is no robot data here (no URDFs, no Pinocchio), so C3-C5 use
+Euler(dt) ∘ DifferentialActionModelLQR knots with the exact (n, m, T, B) of
+the named robots: the solver core sees the same shapes and arithmetic
+intensity; multibody model cost is not represented (SURVEY §8d caveat).
+
+Every batch element gets its own seeded perturbation of the model matrices
+(shared over t), so every (b, t) derivative block is distinct data.
+"""
+import numpy as np
+
+from .models import (ActionModelLQR, ActionModelUnicycle, DifferentialActionModelLQR,
+                     IntegratedActionModelEuler)
+
+# name -> (kind, nx or nq, nu, T, B, dt)
+CONFIGS = {
+    "C1_unicycle": ("unicycle", 3, 2, 30, 1, 0.1),
+    "C2_lqr": ("lqr", 24, 12, 100, 256, None),
+    "C3_talos_arm": ("euler", 7, 7, 250, 512, 1e-3),
+    "C4_solo12": ("euler", 18, 12, 60, 1024, 1e-2),
+    "C5_talos_full": ("euler", 38, 32, 100, 1024, 1e-3),
+}
+
+
+def seed_of(name):
+    """Seed = 0x5EED + cfg_id."""
+    return 0x5EED + int(name[1])
+
+
+def _spd(rng, B, n, scale):
+    A = rng.standard_normal((B, n, n))
+    return np.einsum("bki,bkj->bij", A, A) / (n * scale) + np.eye(n)
+
+
+def lqr_models(nx, nu, B, rng, drift_free=True):
+    """ActionModelLQR(nx, nu) with per-element matrices (§8d C2 recipe)."""
+    m = ActionModelLQR(nx, nu, drift_free)
+    Fx = np.eye(nx) + 0.01 * rng.standard_normal((B, nx, nx))
+    rho = np.max(np.abs(np.linalg.eigvals(Fx)), axis=1)
+    Fx = np.where((rho > 1.05)[:, None, None], Fx * (1.05 / rho)[:, None, None], Fx)
+    m.Fx = Fx
+    m.Fu = np.eye(nx, nu) + 0.01 * rng.standard_normal((B, nx, nu))
+    m.Lxx = _spd(rng, B, nx, 1.0)
+    m.Luu = _spd(rng, B, nu, 1.0)
+    m.Lxu = 0.01 * rng.standard_normal((B, nx, nu))
+    m.lx = rng.uniform(-1, 1, (B, nx))
+    m.lu = rng.uniform(-1, 1, (B, nu))
+    if not drift_free:
+        m.f0 = rng.uniform(-1, 1, (B, nx))
+    return m
+
+
+def difflqr_model(nq, nu, B, rng, drift_free=True):
+    d = DifferentialActionModelLQR(nq, nu, drift_free)
+    nx = 2 * nq
+    d.Fq = -np.eye(nq) + 0.1 * rng.standard_normal((B, nq, nq)) / np.sqrt(nq)
+    d.Fv = -0.1 * np.eye(nq) + 0.1 * rng.standard_normal((B, nq, nq)) / np.sqrt(nq)
+    d.Fu = np.eye(nq, nu) + 0.1 * rng.standard_normal((B, nq, nu))
+    d.Lxx = _spd(rng, B, nx, 1.0)
+    d.Luu = _spd(rng, B, nu, 1.0)
+    d.Lxu = 0.01 * rng.standard_normal((B, nx, nu))
+    d.lx = rng.uniform(-1, 1, (B, nx))
+    d.lu = rng.uniform(-1, 1, (B, nu))
+    if not drift_free:
+        d.f0 = rng.uniform(-1, 1, (B, nq))
+    return d
+
+
+def build(name, T=None, B=None, seed=None, drift_free=True):
+    """(x0s (B, nx), running models [T], terminal model) for a config.
+    T/B override the config's sizes (parity tests use small ones)."""
+    kind, d1, nu, T0, B0, dt = CONFIGS[name]
+    T = T0 if T is None else T
+    B = B0 if B is None else B
+    rng = np.random.default_rng(seed_of(name) if seed is None else seed)
+    if kind == "unicycle":
+        model = ActionModelUnicycle()
+        x0s = np.vstack([[-1.0, -1.0, 1.0], rng.uniform(-1, 1, (max(B - 1, 0), 3))])[:B]
+        return x0s, [model] * T, model
+    if kind == "lqr":
+        model = lqr_models(d1, nu, B, rng, drift_free)
+        x0s = rng.uniform(-1, 1, (B, d1))
+        return x0s, [model] * T, model
+    dm = difflqr_model(d1, nu, B, rng, drift_free)
+    running = IntegratedActionModelEuler(dm, dt)
+    terminal = IntegratedActionModelEuler(dm, 0.0)
+    x0s = rng.uniform(-1, 1, (B, 2 * d1))
+    return x0s, [running] * T, terminal

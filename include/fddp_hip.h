@@ -1,0 +1,237 @@
+/*
+ * fddp_hip.h — C ABI of libfddp_hip, the MI355X-native batched FDDP solver.
+ *
+ * This is the drop-in boundary for the reference's hot path
+ *   ShootingProblem::calc/calcDiff + SolverFDDP
+ * (reference: /root/reference, a Crocoddyl 1.4.0 fork). One handle owns B
+ * independent optimal-control problems that share one knot sequence
+ * (T running knots + 1 terminal knot) and solves them together on one GPU.
+ *
+ * Conventions
+ *  - Every floating-point value is IEEE fp64.
+ *  - Host arrays are contiguous, batch-major: vectors [b][t][i]; matrix blocks
+ *    column-major exactly as Eigen stores them (element (i,j) at j*rows+i).
+ *  - Every entry point returns an int status (FDDP_OK == 0, negative on an
+ *    argument/runtime error; fddp_last_error() gives the message). No C++
+ *    exception crosses the ABI. Numerical failures (the reference's
+ *    backward_error / forward_error, src/core/solvers/ddp.cpp:246-251,
+ *    fddp.cpp:175-180) are handled per batch element inside fddp_solve,
+ *    exactly as SolverFDDP::solve catches them (fddp.cpp:35-60).
+ *  - No torch types, no HIP types in signatures. A device stream can be
+ *    obtained as an opaque pointer for callers that want to order work.
+ *
+ * Which reference interface each entry point replaces is cited per function.
+ */
+#ifndef FDDP_HIP_H_
+#define FDDP_HIP_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes -------------------------------------------------------- */
+#define FDDP_OK 0
+#define FDDP_ERR_INVALID_ARG (-1)   /* reference: throw_pretty("Invalid argument") */
+#define FDDP_ERR_RUNTIME (-2)       /* HIP runtime failure */
+#define FDDP_ERR_UNSUPPORTED (-3)   /* knot kind / size the device path does not cover */
+#define FDDP_ERR_NO_DEVICE (-4)     /* no usable gfx950 device */
+
+/* ---- per-element solve status (fddp_result.status) ----------------------- */
+#define FDDP_STATUS_RUNNING 0       /* maxiter reached without convergence (solve returned false) */
+#define FDDP_STATUS_CONVERGED 1     /* was_feasible && stop < th_stop (fddp.cpp:100-102) */
+#define FDDP_STATUS_REGMAX 2        /* xreg reached regmax (fddp.cpp:41-43, 88-90) */
+
+/* ---- knot model kinds ---------------------------------------------------- */
+/* ActionModelLQR (include/crocoddyl/core/actions/lqr.hxx:13-70). nx == ndx.
+ * Parameter block (doubles): [hdr0 = drift_free (1/0), hdr1..3 = 0]
+ *   Fx(nx*nx) Fu(nx*nu) f0(nx) Lxx(nx*nx) Lxu(nx*nu) Luu(nu*nu) lx(nx) lu(nu) */
+#define FDDP_KNOT_LQR 1
+/* ActionModelUnicycle (core/actions/unicycle.hxx:13-73). nx=ndx=3, nu=2.
+ * Parameter block: [dt, w_x, w_u, 0]  (dt=0.1, cost weights (10, 1) by default) */
+#define FDDP_KNOT_UNICYCLE 2
+/* IntegratedActionModelEuler (core/integrator/euler.hxx:41-131) around
+ * DifferentialActionModelLQR (core/actions/diff-lqr.hxx:13-82), Euclidean
+ * state x=(q,v), nq = nv = nx/2.
+ * Parameter block: [dt, drift_free, 0, 0]
+ *   Fq(nq*nq) Fv(nq*nq) Fu(nq*nu) f0(nq) Lxx(nx*nx) Lxu(nx*nu) Luu(nu*nu) lx(nx) lu(nu) */
+#define FDDP_KNOT_EULER_DIFFLQR 3
+
+#define FDDP_PARAM_HEADER 4 /* doubles of scalar header in front of every block */
+
+typedef struct {
+  int32_t nx;      /* state dimension (ShootingProblem::get_nx, shooting.hxx:25) */
+  int32_t ndx;     /* tangent dimension (== nx for the Euclidean states covered) */
+  int32_t nu_max;  /* max controls over the running knots (shooting.hxx:27-34) */
+  int32_t T;       /* number of running knots */
+  int32_t B;       /* number of independent problems in the batch */
+} fddp_dims;
+
+typedef struct {
+  int32_t kind;          /* FDDP_KNOT_* */
+  int32_t nu;            /* controls of this knot's model (0 allowed for running knots) */
+  int64_t param_offset;  /* offset (doubles) of this knot's block in the parameter pool */
+  int64_t param_stride;  /* doubles between batch elements' blocks; 0 = block shared by all */
+} fddp_knot_desc;
+
+/* Solver thresholds; defaults = reference constructors
+ * (solver-base.cpp:24-25, ddp.cpp:17-31, fddp.cpp:15). */
+typedef struct {
+  double th_acceptstep;    /* 0.1  */
+  double th_stop;          /* 1e-9 */
+  double th_grad;          /* 1e-12 */
+  double th_stepdec;       /* 0.5  */
+  double th_stepinc;       /* 0.01 */
+  double th_acceptnegstep; /* 2    */
+  double regfactor;        /* 10   */
+  double regmin;           /* 1e-9 */
+  double regmax;           /* 1e9  */
+  int32_t n_alphas;        /* 10   */
+  int32_t pad_;
+  double alphas[16];       /* 2^-k, k = 0..9 */
+} fddp_params;
+
+/* Per-element outcome of fddp_solve: the reference solver's public state
+ * after SolverFDDP::solve returns (solver-base.hpp getters). */
+typedef struct {
+  int32_t status;      /* FDDP_STATUS_* ; solve()'s bool == (status == CONVERGED) */
+  int32_t iter;        /* SolverAbstract::get_iter() after return */
+  int32_t is_feasible; /* get_is_feasible() */
+  int32_t n_iter_run;  /* loop bodies executed (for iterations/s accounting) */
+  double cost;         /* get_cost() */
+  double stop;         /* get_stop() */
+  double xreg;         /* get_xreg() */
+  double ureg;         /* get_ureg() */
+  double steplength;   /* get_steplength() */
+  double dV;           /* get_dV() */
+  double dVexp;        /* get_dVexp() */
+  double d0, d1;       /* get_d() */
+} fddp_result;
+
+typedef struct fddp_handle_s fddp_handle;
+
+/* Fill the reference defaults. Replaces the SolverDDP/SolverFDDP constructors
+ * (ddp.cpp:15-37, fddp.cpp:14-15). */
+void fddp_default_params(fddp_params* p);
+
+/* Create a batched problem + solver on `device`. Replaces
+ * ShootingProblem(x0, runningModels, terminalModel) (shooting.hxx:17-59) and
+ * SolverFDDP(problem) (fddp.cpp:14, allocateData ddp.cpp:328-384).
+ * knots: T+1 descriptors (running 0..T-1, terminal T). params: the parameter
+ * pool (n_params doubles) referenced by the descriptors. All device memory is
+ * allocated here, once. */
+int fddp_create(const fddp_dims* dims, const fddp_knot_desc* knots, const double* params, int64_t n_params,
+                int device, fddp_handle** out);
+void fddp_destroy(fddp_handle* h);
+
+/* Message of the last error on this thread ("" if none). */
+const char* fddp_last_error(void);
+
+/* Re-upload the parameter pool (same size). Replaces the model setters
+ * (e.g. ActionModelLQR::set_Fx, lqr.hxx:128-136) for a live handle. */
+int fddp_set_model_params(fddp_handle* h, const double* params, int64_t n_params);
+
+/* x0 for every element: B*nx. Replaces ShootingProblem::set_x0 (shooting.hxx:391-397). */
+int fddp_set_x0(fddp_handle* h, const double* x0);
+int fddp_get_x0(fddp_handle* h, double* x0);
+
+/* SolverFDDP thresholds. Replaces the setters (ddp.cpp:420-486,
+ * solver-base.cpp:159-173, fddp.cpp:229-235) with the same validation. */
+int fddp_set_params(fddp_handle* h, const fddp_params* p);
+int fddp_get_params(fddp_handle* h, fddp_params* p);
+
+/* Warm start. xs: B*(T+1)*nx or NULL (= state.zero()), us: B*T*nu_max or NULL
+ * (= zeros). Replaces SolverAbstract::setCandidate (solver-base.cpp:42-67). */
+int fddp_set_candidate(fddp_handle* h, const double* xs, const double* us, int is_feasible);
+
+/* SolverFDDP::solve (fddp.cpp:19-105) from the current candidate, for every
+ * element at once, each element with its own state machine. reg_init may be
+ * NaN (→ regmin). out: B results (may be NULL). Runs on the handle's stream and
+ * returns after the results are on the host. */
+int fddp_solve(fddp_handle* h, int maxiter, int is_feasible, double reg_init, fddp_result* out);
+
+/* Results of the last solve / current solver state per element. */
+int fddp_get_results(fddp_handle* h, fddp_result* out);
+/* xs: B*(T+1)*nx, us: B*T*nu_max. on_device != 0: `out` is a device pointer
+ * on the handle's device (copy is enqueued on the handle's stream). */
+int fddp_get_xs(fddp_handle* h, double* out, int on_device);
+int fddp_get_us(fddp_handle* h, double* out, int on_device);
+
+/* ---- step API: the SolverDDP/SolverFDDP methods one at a time --------------
+ * Used for parity tests against the reference's own step-level tests
+ * (unittest/bindings/test_solvers.py:38-96). cost/dV/d/stop outputs are B (or
+ * B*2) doubles, may be NULL. */
+/* ShootingProblem::calc (shooting.hxx:133-161) at the current candidate. */
+int fddp_problem_calc(fddp_handle* h, double* cost);
+/* ShootingProblem::calcDiff (shooting.hxx:164-195) at the current candidate. */
+int fddp_problem_calc_diff(fddp_handle* h, double* cost);
+/* SolverDDP::computeDirection(recalc) (ddp.cpp:120-125): calcDiff (with the
+ * iter==0 calc and the gaps, ddp.cpp:157-178) + backwardPass (ddp.cpp:180-253).
+ * status: B ints, 0 ok / 1 backward_error (may be NULL). */
+int fddp_compute_direction(fddp_handle* h, int recalc, int32_t* status);
+/* SolverFDDP::updateExpectedImprovement (fddp.cpp:126-147). */
+int fddp_update_expected_improvement(fddp_handle* h);
+/* SolverDDP::tryStep / SolverFDDP::forwardPass (ddp.cpp:127-130, fddp.cpp:149-225).
+ * dV = cost - cost_try; status: 0 ok / 1 forward_error. */
+int fddp_try_step(fddp_handle* h, double alpha, double* dV, int32_t* status);
+/* SolverFDDP::expectedImprovement (fddp.cpp:107-124) after a tryStep. d: B*2. */
+int fddp_expected_improvement(fddp_handle* h, double* d);
+/* SolverDDP::stoppingCriteria (ddp.cpp:132-142). */
+int fddp_stopping_criteria(fddp_handle* h, double* stop);
+/* Solver members the step API depends on, for every element: iter_ (the
+ * iter_==0 calc in SolverDDP::calcDiff, ddp.cpp:158), xreg_/ureg_ (NaN on a
+ * fresh solver, solver-base.cpp:19-20) and was_feasible_. */
+int fddp_set_solver_state(fddp_handle* h, int iter, double xreg, double ureg, int was_feasible);
+/* xs_try/us_try of the last tryStep. */
+int fddp_get_xs_try(fddp_handle* h, double* out);
+int fddp_get_us_try(fddp_handle* h, double* out);
+
+/* ---- inspection of per-knot data (ActionData members, action-base.hpp:101-142,
+ * and SolverDDP getters ddp.hpp:60-271). Sizes per element per knot below.  */
+#define FDDP_Q_FX 0   /* (T+1) x ndx*ndx  */
+#define FDDP_Q_FU 1   /* (T+1) x ndx*nu_max */
+#define FDDP_Q_LXX 2  /* (T+1) x ndx*ndx  */
+#define FDDP_Q_LXU 3  /* (T+1) x ndx*nu_max */
+#define FDDP_Q_LUU 4  /* (T+1) x nu_max*nu_max */
+#define FDDP_Q_LX 5   /* (T+1) x ndx */
+#define FDDP_Q_LU 6   /* (T+1) x nu_max */
+#define FDDP_Q_XNEXT 7 /* T x nx (data[t].xnext of the current candidate) */
+#define FDDP_Q_FS 8   /* (T+1) x ndx (gaps) */
+#define FDDP_Q_K 9    /* T x nu_max*ndx (K_, nu x ndx col-major) */
+#define FDDP_Q_KV 10  /* T x nu_max (k_) */
+/* The following need fddp_set_debug(h, 1) before the backward pass. */
+#define FDDP_Q_VXX 11 /* (T+1) x ndx*ndx */
+#define FDDP_Q_VX 12  /* (T+1) x ndx */
+#define FDDP_Q_QXX 13 /* T x ndx*ndx */
+#define FDDP_Q_QXU 14 /* T x ndx*nu_max */
+#define FDDP_Q_QUU 15 /* T x nu_max*nu_max */
+#define FDDP_Q_QX 16  /* T x ndx */
+#define FDDP_Q_QU 17  /* T x nu_max */
+int fddp_get_quantity(fddp_handle* h, int which, double* out);
+/* Store Vxx/Vx/Q* per knot during backward passes (costs HBM traffic). */
+int fddp_set_debug(fddp_handle* h, int on);
+
+/* ---- MPC plumbing -------------------------------------------------------- */
+/* Receding-horizon shift on device: x0 <- xs[1]; xs[t] <- xs[t+1] (last kept);
+ * us[t] <- us[t+1] (last kept). The device analogue of a user's shift between
+ * warm-started solve(maxiter=1) calls (benchmark/quadrupedal-gaits-optctrl.cpp:63). */
+int fddp_mpc_shift(fddp_handle* h);
+
+/* ---- runtime ------------------------------------------------------------ */
+int fddp_synchronize(fddp_handle* h);
+/* Opaque hipStream_t of the handle. */
+int fddp_get_stream(fddp_handle* h, void** stream);
+/* Device time (ms) of the named kernel class accumulated since the last reset,
+ * measured with HIP events on the handle's stream. which: 0 calc, 1 calcDiff,
+ * 2 backward, 3 forward/line-search. counts: launches. */
+int fddp_get_timing(fddp_handle* h, double* ms_out /*4*/, int64_t* counts_out /*4*/);
+int fddp_set_timing(fddp_handle* h, int on);
+/* Number of bytes of device memory owned by the handle. */
+int64_t fddp_device_bytes(fddp_handle* h);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FDDP_HIP_H_ */

@@ -1,0 +1,176 @@
+"""ctypes binding of the CPU oracle (oracle/_build/liboracle.so) — tests only.
+
+The oracle is test infrastructure (see oracle/fddp_oracle.cpp header). This
+module builds it on demand with oracle/Makefile (g++ -fopenmp) and exposes
+the same call shapes as libfddp_hip so parity tests read symmetric.
+"""
+import ctypes as C
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from crocoddyl_amd import _abi  # noqa: E402
+
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+ORACLE_SO = os.path.join(ORACLE_DIR, "_build", "liboracle.so")
+
+_lib = None
+
+
+def build(out_dir=None, arch=None):
+    env = dict(os.environ)
+    args = ["make", "-s", "-C", ORACLE_DIR]
+    if out_dir:
+        args.append(f"OUT={out_dir}")
+    if arch:
+        args.append(f"ARCH={arch}")
+    subprocess.run(args, check=True, env=env)
+
+
+def lib(path=None):
+    global _lib
+    if path is not None:
+        L = C.CDLL(path)
+        _bind(L)
+        return L
+    if _lib is None:
+        if not os.path.exists(ORACLE_SO) or os.path.getmtime(ORACLE_SO) < os.path.getmtime(
+                os.path.join(ORACLE_DIR, "fddp_oracle.cpp")):
+            build()
+        _lib = C.CDLL(ORACLE_SO)
+        _bind(_lib)
+    return _lib
+
+
+def _bind(L):
+    _abi.bind(L, "oracle_", {k: v for k, v in _abi.PROTOS.items() if k not in ("default_params",)})
+    L.oracle_default_params.restype = None
+    L.oracle_default_params.argtypes = [C.POINTER(_abi.Params)]
+    L.oracle_create.restype = C.c_int
+    L.oracle_create.argtypes = [C.POINTER(_abi.Dims), C.POINTER(_abi.KnotDesc), _abi.D, C.c_int64,
+                                C.POINTER(C.c_void_p)]
+    L.oracle_set_threading.restype = C.c_int
+    L.oracle_set_threading.argtypes = [C.c_void_p, C.c_int, C.c_int]
+    for n in ("get_xs", "get_us", "get_xs_try", "get_us_try"):
+        f = getattr(L, "oracle_" + n)
+        f.restype = C.c_int
+        f.argtypes = [C.c_void_p, _abi.D]
+    L.oracle_get_trace.restype = C.c_int
+    L.oracle_get_trace.argtypes = [C.c_void_p, C.c_int, _abi.D, C.c_int]
+
+
+class Oracle:
+    """One oracle handle (B problems on the CPU)."""
+
+    def __init__(self, dims, knots, pool, x0s, threads=1, mode=2):
+        self.L = lib()
+        self.dims = dims
+        self.h = C.c_void_p()
+        kd = (_abi.KnotDesc * len(knots))(*[_abi.KnotDesc(*k) for k in knots])
+        self.pool = np.ascontiguousarray(pool, dtype=np.float64)
+        rc = self.L.oracle_create(C.byref(dims), kd, _abi.dptr(self.pool), self.pool.size, C.byref(self.h))
+        assert rc == 0, self.L.oracle_last_error()
+        self.L.oracle_set_threading(self.h, mode, threads)
+        self.set_x0(x0s)
+
+    def __del__(self):
+        try:
+            self.L.oracle_destroy(self.h)
+        except Exception:
+            pass
+
+    def set_x0(self, x0s):
+        a = np.ascontiguousarray(x0s, dtype=np.float64)
+        self.L.oracle_set_x0(self.h, _abi.dptr(a))
+
+    def set_params(self, prm):
+        self.L.oracle_set_params(self.h, C.byref(prm))
+
+    def set_candidate(self, xs=None, us=None, is_feasible=False):
+        xa = None if xs is None else np.ascontiguousarray(xs, dtype=np.float64)
+        ua = None if us is None else np.ascontiguousarray(us, dtype=np.float64)
+        self.L.oracle_set_candidate(self.h, _abi.dptr(xa), _abi.dptr(ua), int(is_feasible))
+
+    def solve(self, maxiter=100, is_feasible=False, reg_init=1e-9):
+        r = (_abi.Result * self.dims.B)()
+        self.L.oracle_solve(self.h, maxiter, int(is_feasible), reg_init, r)
+        return r
+
+    def results(self):
+        r = (_abi.Result * self.dims.B)()
+        self.L.oracle_get_results(self.h, r)
+        return r
+
+    def xs(self, trial=False):
+        d = self.dims
+        a = np.zeros((d.B, d.T + 1, d.nx))
+        (self.L.oracle_get_xs_try if trial else self.L.oracle_get_xs)(self.h, _abi.dptr(a))
+        return a
+
+    def us(self, trial=False):
+        d = self.dims
+        a = np.zeros((d.B, d.T, d.nu_max))
+        (self.L.oracle_get_us_try if trial else self.L.oracle_get_us)(self.h, _abi.dptr(a))
+        return a
+
+    def quantity(self, which, nk, per):
+        a = np.zeros((self.dims.B, nk, per))
+        self.L.oracle_get_quantity(self.h, which, _abi.dptr(a))
+        return a
+
+    def trace(self, b, maxn=1000):
+        a = np.zeros((maxn, 8))
+        n = self.L.oracle_get_trace(self.h, b, _abi.dptr(a), maxn)
+        return a[:n]
+
+    # step API
+    def calc(self):
+        c = np.zeros(self.dims.B)
+        self.L.oracle_problem_calc(self.h, _abi.dptr(c))
+        return c
+
+    def calc_diff(self):
+        c = np.zeros(self.dims.B)
+        self.L.oracle_problem_calc_diff(self.h, _abi.dptr(c))
+        return c
+
+    def set_solver_state(self, it=0, xreg=float("nan"), ureg=float("nan"), was_feasible=0):
+        self.L.oracle_set_solver_state(self.h, it, xreg, ureg, was_feasible)
+
+    def compute_direction(self, recalc=True):
+        st = np.zeros(self.dims.B, dtype=np.int32)
+        self.L.oracle_compute_direction(self.h, int(recalc), st.ctypes.data_as(_abi.I32))
+        return st
+
+    def update_expected_improvement(self):
+        self.L.oracle_update_expected_improvement(self.h)
+
+    def try_step(self, alpha):
+        dV = np.zeros(self.dims.B)
+        st = np.zeros(self.dims.B, dtype=np.int32)
+        self.L.oracle_try_step(self.h, alpha, _abi.dptr(dV), st.ctypes.data_as(_abi.I32))
+        return dV, st
+
+    def expected_improvement(self):
+        d = np.zeros((self.dims.B, 2))
+        self.L.oracle_expected_improvement(self.h, _abi.dptr(d))
+        return d
+
+    def stopping_criteria(self):
+        s = np.zeros(self.dims.B)
+        self.L.oracle_stopping_criteria(self.h, _abi.dptr(s))
+        return s
+
+    def mpc_shift(self):
+        self.L.oracle_mpc_shift(self.h)
+
+
+def default_params():
+    p = _abi.Params()
+    lib().oracle_default_params(C.byref(p))
+    return p
