@@ -19,9 +19,26 @@ class FDDPError(RuntimeError):
     """Raised for argument errors (the reference's throw_pretty) and runtime failures."""
 
 
+def _share_torch_hip_runtime():
+    """A process may hold only one HIP runtime. PyTorch-ROCm wheels bundle
+    their own libamdhip64 (same soname, different file); if torch is
+    installed, load that one first (RTLD_GLOBAL) so libfddp_hip binds to it
+    and torch and this library share one runtime in either import order."""
+    import importlib.util
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.submodule_search_locations:
+        return
+    for d in spec.submodule_search_locations:
+        p = os.path.join(d, "lib", "libamdhip64.so")
+        if os.path.exists(p):
+            C.CDLL(p, mode=C.RTLD_GLOBAL)
+            return
+
+
 def lib():
     global _lib
     if _lib is None:
+        _share_torch_hip_runtime()
         if not os.path.exists(LIB_PATH):
             raise ImportError(f"crocoddyl_amd: HIP library not built ({LIB_PATH} missing); "
                               "run __graft_entry__.build() — there is no CPU fallback")

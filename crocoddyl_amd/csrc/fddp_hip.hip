@@ -316,8 +316,13 @@ int fddp_create(const fddp_dims* dims, const fddp_knot_desc* knots, const double
     return fail(FDDP_ERR_INVALID_ARG, "fddp_create: terminal nu exceeds nu_max");
 
   int ndev = 0;
-  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
-    return fail(FDDP_ERR_NO_DEVICE, "fddp_create: no HIP device visible");
+  const hipError_t ce = hipGetDeviceCount(&ndev);
+  if (ce != hipSuccess || ndev == 0) {
+    int rtv = 0;
+    (void)hipRuntimeGetVersion(&rtv);
+    return fail(FDDP_ERR_NO_DEVICE, std::string("fddp_create: no HIP device visible (") + hipGetErrorString(ce) +
+                                        ", runtime " + std::to_string(rtv) + ")");
+  }
   if (device < 0 || device >= ndev) return fail(FDDP_ERR_INVALID_ARG, "fddp_create: bad device index");
   hipDeviceProp_t prop;
   HIP_TRY(hipGetDeviceProperties(&prop, device));

@@ -418,9 +418,10 @@ __global__ __launch_bounds__(NT) void backward_kernel(Dev D, Prm prm, int mode) 
     st->xreg = xreg;
     st->ureg = ureg;
     st->bwd_fail = ok ? 0 : 1;
-    if (!ok && mode == 0) {
+    if (!ok && mode == 0) {  // solve() returns false inside this loop body
       st->status = FDDP_STATUS_REGMAX;
       st->active = 0;
+      st->n_iter_run += 1;
     }
     if (ok) {
       // updateExpectedImprovement (fddp.cpp:126-147) and stoppingCriteria, in knot order
