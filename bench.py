@@ -77,7 +77,9 @@ def cpu_baseline(cfg, T, seed, target_s=12.0):
     Bs = threads
     it, dt = run(Bs, 1)
     rate = it / max(dt, 1e-9)
-    steps = max(1, min(20, int(target_s * rate / Bs)))
+    steps = 4
+    Bs = int(max(threads, min(1024, target_s * rate / steps)))
+    Bs = max(threads, (Bs // threads) * threads)
     it, dt = run(Bs, steps)
     return {"value": it / dt, "unit": "FDDP iterations/s", "cores": threads, "kind": "port",
             "sample": f"{cfg} T={T}, {Bs} elements x {steps} warm-started solve(maxiter=1) "

@@ -12,8 +12,10 @@
 // counter per iteration to stop early.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -21,6 +23,7 @@
 #include "../../include/fddp_hip.h"
 #include "fddp_device.hpp"
 #include "fddp_kernels.hpp"
+#include "bwd_mfma.hpp"
 
 using namespace fddp;
 
@@ -83,6 +86,9 @@ struct fddp_handle_s {
   double* dbg[7] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   int64_t bytes = 0;
   size_t bwd_smem = 0, fwd_smem = 0, calc_smem = 0, cdiff_smem = 0;
+  int64_t pcap = 0;  // doubles of LDS reserved for a resident parameter block
+  int bwd_variant = 0;  // 0 generic, else NTL*10+MTL of the MFMA sweep
+  BwdSched sched;
   // timing
   bool timing = false;
   std::vector<hipEvent_t> ev_pool;
@@ -166,7 +172,7 @@ Prm to_prm(const fddp_params& p) {
 int launch_calc(fddp_handle* h, int sel) {
   Timed tm(h, 0);
   const Dev& D = h->D;
-  hipLaunchKernelGGL(calc_kernel<kNT>, dim3(D.T + 1, D.B), dim3(kNT), h->calc_smem, h->stream, D, sel);
+  hipLaunchKernelGGL(calc_kernel<kNT>, dim3(D.B), dim3(kNT), h->calc_smem, h->stream, D, sel, h->pcap);
   LAUNCH_CHECK();
   return FDDP_OK;
 }
@@ -179,22 +185,68 @@ int launch_cost_sum(fddp_handle* h, int sel, double* out) {
 int launch_calc_diff(fddp_handle* h, int sel, int gaps) {
   Timed tm(h, 1);
   const Dev& D = h->D;
-  hipLaunchKernelGGL(calc_diff_kernel<kNT>, dim3(D.T + 1, D.B), dim3(kNT), h->cdiff_smem, h->stream, D, sel, gaps);
+  hipLaunchKernelGGL(calc_diff_kernel<kNT>, dim3(D.B), dim3(kNT), h->cdiff_smem, h->stream, D, sel, gaps, h->pcap);
   LAUNCH_CHECK();
   return FDDP_OK;
 }
+template <int NTL, int MTL>
+void launch_bwd_mfma(fddp_handle* h, int mode) {
+  const Dev& D = h->D;
+  backward_mfma_kernel<NTL, MTL><<<dim3(D.B), dim3(256), MfmaCfg<NTL, MTL>::bytes, h->stream>>>(D, to_prm(h->prm), mode,
+                                                                                             h->sched);
+}
+
 int launch_backward(fddp_handle* h, int mode) {
   Timed tm(h, 2);
   const Dev& D = h->D;
-  hipLaunchKernelGGL(backward_kernel<kNT>, dim3(D.B), dim3(kNT), h->bwd_smem, h->stream, D, to_prm(h->prm), mode);
+  switch (h->bwd_variant) {
+    case 52: launch_bwd_mfma<5, 2>(h, mode); break;
+    case 31: launch_bwd_mfma<3, 1>(h, mode); break;
+    case 21: launch_bwd_mfma<2, 1>(h, mode); break;
+    case 11: launch_bwd_mfma<1, 1>(h, mode); break;
+    default:
+      hipLaunchKernelGGL(backward_kernel<kNT>, dim3(D.B), dim3(kNT), h->bwd_smem, h->stream, D, to_prm(h->prm), mode);
+  }
   LAUNCH_CHECK();
   return FDDP_OK;
+}
+
+template <int NTL, int MTL>
+int setup_bwd_mfma(fddp_handle* h) {
+  using Cfg = MfmaCfg<NTL, MTL>;
+  if (hipFuncSetAttribute((const void*)backward_mfma_kernel<NTL, MTL>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)Cfg::bytes) != hipSuccess)
+    return -1;
+  // LPT: wave 0 owns the u column blocks (Quu + its factorisation), waves 1-3
+  // share the x column blocks by cost G (NTL x 4NTL MFMAs) + H tiles (x 4NTL).
+  BwdSched& s = h->sched;
+  std::memset(&s, 0, sizeof(s));
+  for (int u = 0; u < MTL; ++u) {
+    s.blk[0][s.nown[0]] = NTL + u;
+    s.jstart[0][s.nown[0]] = NTL;
+    s.nown[0]++;
+  }
+  std::vector<std::pair<int, int>> xs;
+  for (int i = 0; i < NTL; ++i) xs.push_back({NTL * 4 * NTL + (NTL - i + MTL) * 4 * NTL, i});
+  std::sort(xs.rbegin(), xs.rend());
+  int load[4] = {0, 0, 0, 0};
+  for (auto& p : xs) {
+    int best = -1;
+    for (int w = 1; w < 4; ++w)
+      if (s.nown[w] < Cfg::MAXOWN && (best < 0 || load[w] < load[best])) best = w;
+    if (best < 0) return -1;
+    s.blk[best][s.nown[best]] = p.second;
+    s.jstart[best][s.nown[best]] = p.second;
+    s.nown[best]++;
+    load[best] += p.first;
+  }
+  return NTL * 10 + MTL;
 }
 int launch_forward(fddp_handle* h, int mode, double alpha, int* count) {
   Timed tm(h, 3);
   const Dev& D = h->D;
   hipLaunchKernelGGL(forward_kernel<kNT>, dim3(D.B), dim3(kNT), h->fwd_smem, h->stream, D, to_prm(h->prm), mode,
-                     alpha, count);
+                     alpha, count, h->pcap);
   LAUNCH_CHECK();
   return FDDP_OK;
 }
@@ -363,9 +415,15 @@ int fddp_create(const fddp_dims* dims, const fddp_knot_desc* knots, const double
   h->bwd_smem = BwdSmem::bytes(D.n, D.m);
   if (h->bwd_smem > 160 * 1024)
     return bail(fail(FDDP_ERR_UNSUPPORTED, "fddp_create: (ndx, nu_max) too large for the LDS-resident Riccati sweep"));
-  h->fwd_smem = sizeof(double) * (2 * D.sX + D.sM + 5 * (kNT / kWave) + 16);
+  {
+    int64_t pmax = 0;
+    for (int t = 0; t <= d.T; ++t) pmax = std::max<int64_t>(pmax, block_doubles(knots[t].kind, d.nx, knots[t].nu));
+    const int64_t budget = (150 * 1024) / 8 - (2 * D.sX + D.sM + 5 * (kNT / kWave) + 16);
+    h->pcap = pmax <= budget ? pad2(pmax) : 0;
+  }
+  h->fwd_smem = sizeof(double) * (h->pcap + 2 * D.sX + D.sM + 5 * (kNT / kWave) + 16);
   h->calc_smem = h->fwd_smem;
-  h->cdiff_smem = sizeof(double) * (D.sX + D.sM);
+  h->cdiff_smem = sizeof(double) * (h->pcap + D.sX + D.sM);
 
   double* p = nullptr;
   if ((rc = dalloc(h, &p, n_params))) return bail(rc);
@@ -414,8 +472,29 @@ int fddp_create(const fddp_dims* dims, const fddp_knot_desc* knots, const double
   if (hipMemcpyAsync(D.st, st0.data(), sizeof(ElemState) * B, hipMemcpyHostToDevice, h->stream) != hipSuccess)
     return bail(fail(FDDP_ERR_RUNTIME, "upload state"));
   if (hipFuncSetAttribute((const void*)backward_kernel<kNT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)h->bwd_smem) != hipSuccess)
-    return bail(fail(FDDP_ERR_RUNTIME, "hipFuncSetAttribute(backward_kernel)"));
+                          (int)h->bwd_smem) != hipSuccess ||
+      hipFuncSetAttribute((const void*)forward_kernel<kNT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)h->fwd_smem) != hipSuccess ||
+      hipFuncSetAttribute((const void*)calc_kernel<kNT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)h->calc_smem) != hipSuccess ||
+      hipFuncSetAttribute((const void*)calc_diff_kernel<kNT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)h->cdiff_smem) != hipSuccess)
+    return bail(fail(FDDP_ERR_RUNTIME, "hipFuncSetAttribute(dynamic LDS)"));
+  {  // backward sweep variant: MFMA tiles when every running knot has nu == nu_max
+    bool uniform_nu = d.nu_max > 0;
+    for (int t = 0; t < d.T; ++t) uniform_nu = uniform_nu && knots[t].nu == d.nu_max;
+    const char* env = std::getenv("FDDP_BACKWARD");
+    const bool force_generic = env && std::strcmp(env, "generic") == 0;
+    const int ntl = (d.ndx + 15) / 16, mtl = (d.nu_max + 15) / 16;
+    int v = -1;
+    if (uniform_nu && !force_generic) {
+      if (ntl == 5 && mtl == 2) v = setup_bwd_mfma<5, 2>(h);
+      else if (ntl == 3 && mtl == 1) v = setup_bwd_mfma<3, 1>(h);
+      else if (ntl == 2 && mtl == 1) v = setup_bwd_mfma<2, 1>(h);
+      else if (ntl == 1 && mtl == 1) v = setup_bwd_mfma<1, 1>(h);
+    }
+    h->bwd_variant = v > 0 ? v : 0;
+  }
   if (hipStreamSynchronize(h->stream) != hipSuccess) return bail(fail(FDDP_ERR_RUNTIME, "sync after create"));
   *out = h;
   return FDDP_OK;

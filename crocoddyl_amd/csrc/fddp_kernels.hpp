@@ -19,6 +19,41 @@ __device__ inline bool selected(const ElemState& s, int sel) {
   }
 }
 
+// Doubles in a knot's parameter block (layouts in include/fddp_hip.h).
+__device__ inline int64_t block_doubles_dev(int kind, int nx, int nu) {
+  if (kind == FDDP_KNOT_LQR) return FDDP_PARAM_HEADER + 2LL * nx * nx + 2LL * nx * nu + (int64_t)nu * nu + 2LL * nx + nu;
+  if (kind == FDDP_KNOT_UNICYCLE) return FDDP_PARAM_HEADER;
+  const int64_t nq = nx / 2;
+  return FDDP_PARAM_HEADER + 2 * nq * nq + nq * nu + nq + (int64_t)nx * nx + (int64_t)nx * nu + (int64_t)nu * nu + nx +
+         nu;
+}
+
+// Keep one knot parameter block resident in LDS across consecutive knots that
+// share it (a reference model object shared by several knots, or one
+// element's perturbed model used at every t). Returns the pointer to read the
+// block from (LDS copy, or global when it does not fit `cap` doubles).
+// Contains barriers when it (re)stages: call uniformly.
+template <int NT>
+__device__ inline const double* stage_params(const double* g, int64_t size, double* lds, int64_t cap,
+                                             const double*& cached) {
+  if (g == cached) return lds;
+  if (size > cap) return g;
+  __syncthreads();
+  const int64_t n2 = size & ~int64_t(1);
+  const bool al = ((reinterpret_cast<uintptr_t>(g) & 15) == 0);
+  if (al) {
+    const double2* s2 = reinterpret_cast<const double2*>(g);
+    double2* d2 = reinterpret_cast<double2*>(lds);
+    for (int64_t e = threadIdx.x; e < n2 / 2; e += NT) d2[e] = s2[e];
+    for (int64_t e = n2 + threadIdx.x; e < size; e += NT) lds[e] = g[e];
+  } else {
+    for (int64_t e = threadIdx.x; e < size; e += NT) lds[e] = g[e];
+  }
+  __syncthreads();
+  cached = g;
+  return lds;
+}
+
 // ---------------------------------------------------------------------------
 // Workgroup GEMM: C = C0 + sgn * op(A) op(B), column-major, 2x2 register tiles.
 // TA: A is stored K x M (use A^T).  TB: B is stored N x K (use B^T).
@@ -56,35 +91,43 @@ __device__ void wg_gemm(int M, int N, int K, const double* __restrict__ A, int l
 }
 
 // ---------------------------------------------------------------------------
-// ShootingProblem::calc fan-out (shooting.hxx:133-161): one workgroup per
-// (knot t, element b). Writes data[t].xnext and data[t].cost of trajectory cur.
+// ShootingProblem::calc (shooting.hxx:133-161): one workgroup per element
+// walks its T+1 knots (independent knots; the loop only lets the element's
+// parameter block stay in LDS). Writes data[t].xnext and data[t].cost of
+// trajectory cur.
 // ---------------------------------------------------------------------------
 template <int NT>
-__global__ __launch_bounds__(NT) void calc_kernel(Dev D, int sel) {
-  const int t = blockIdx.x, b = blockIdx.y;
+__global__ __launch_bounds__(NT) void calc_kernel(Dev D, int sel, int64_t pcap) {
+  const int b = blockIdx.x;
   const ElemState& s = D.st[b];
   if (!selected(s, sel)) return;
   extern __shared__ __attribute__((aligned(16))) double sm[];
-  double* x = sm;                // sX
+  double* pl = sm;               // pcap
+  double* x = pl + pcap;         // sX
   double* u = x + D.sX;          // sM
   double* xn = u + D.sM;         // sX
   double* red = xn + D.sX;       // 5*NT/64
   const int c = s.cur;
-  const double* xg = D.xs[c] + D.knot(b, t) * D.sX;
-  for (int i = threadIdx.x; i < D.nx; i += NT) x[i] = xg[i];
-  const bool running = t < D.T;
-  if (running) {
-    const double* ug = D.us[c] + D.run(b, t) * D.sM;
-    for (int i = threadIdx.x; i < D.m; i += NT) u[i] = ug[i];
+  const double* cached = nullptr;
+  for (int t = 0; t <= D.T; ++t) {
+    const fddp_knot_desc kd = D.knots[t];
+    const double* P = stage_params<NT>(D.pblock(b, t), block_doubles_dev(kd.kind, D.nx, kd.nu), pl, pcap, cached);
+    const double* xg = D.xs[c] + D.knot(b, t) * D.sX;
+    for (int i = threadIdx.x; i < D.nx; i += NT) x[i] = xg[i];
+    const bool running = t < D.T;
+    if (running) {
+      const double* ug = D.us[c] + D.run(b, t) * D.sM;
+      for (int i = threadIdx.x; i < D.m; i += NT) u[i] = ug[i];
+    }
+    __syncthreads();
+    const double cost = knot_calc<NT>(kd, P, D.nx, x, u, running, xn, red);
+    if (running) {
+      double* xo = D.xnext[c] + D.run(b, t) * D.sX;
+      for (int i = threadIdx.x; i < D.nx; i += NT) xo[i] = xn[i];
+    }
+    if (threadIdx.x == 0) D.kcost[c][D.knot(b, t)] = cost;
+    __syncthreads();
   }
-  __syncthreads();
-  const fddp_knot_desc kd = D.knots[t];
-  const double cost = knot_calc<NT>(kd, D.pblock(b, t), D.nx, x, u, running, xn, red);
-  if (running) {
-    double* xo = D.xnext[c] + D.run(b, t) * D.sX;
-    for (int i = threadIdx.x; i < D.nx; i += NT) xo[i] = xn[i];
-  }
-  if (threadIdx.x == 0) D.kcost[c][D.knot(b, t)] = cost;
 }
 
 // cost_ = sum of data[t].cost in knot order, terminal last (shooting.hxx:155-160).
@@ -102,55 +145,63 @@ __global__ void cost_sum_kernel(Dev D, int sel, double* out) {
 }
 
 // ---------------------------------------------------------------------------
-// ShootingProblem::calcDiff fan-out (shooting.hxx:164-195) fused with the gap
+// ShootingProblem::calcDiff (shooting.hxx:164-195) fused with the gap
 // computation of SolverDDP::calcDiff (ddp.cpp:160-176). One workgroup per
-// (knot, element); blocks written with coalesced stores.
+// element walks its knots with the parameter block LDS-resident; the
+// derivative blocks stream out with coalesced stores (HBM-write bound).
 // ---------------------------------------------------------------------------
 template <int NT>
-__global__ __launch_bounds__(NT) void calc_diff_kernel(Dev D, int sel, int gaps) {
-  const int t = blockIdx.x, b = blockIdx.y;
+__global__ __launch_bounds__(NT) void calc_diff_kernel(Dev D, int sel, int gaps, int64_t pcap) {
+  const int b = blockIdx.x;
   const ElemState& s = D.st[b];
   if (!selected(s, sel)) return;
   extern __shared__ __attribute__((aligned(16))) double sm[];
-  double* x = sm;
+  double* pl = sm;
+  double* x = pl + pcap;
   double* u = x + D.sX;
   const int c = s.cur;
-  const int64_t kk = D.knot(b, t);
-  const double* xg = D.xs[c] + kk * D.sX;
-  for (int i = threadIdx.x; i < D.nx; i += NT) x[i] = xg[i];
-  const bool running = t < D.T;
-  if (running) {
-    const double* ug = D.us[c] + D.run(b, t) * D.sM;
-    for (int i = threadIdx.x; i < D.m; i += NT) u[i] = ug[i];
-  }
-  __syncthreads();
-  KnotDiffOut o;
-  o.Fx = D.Fx + kk * D.sNN;
-  o.Fu = D.Fu + kk * D.sNM;
-  o.Lxx = D.Lxx + kk * D.sNN;
-  o.Lxu = D.Lxu + kk * D.sNM;
-  o.Luu = D.Luu + kk * D.sMM;
-  o.Lx = D.Lx + kk * D.sN;
-  o.Lu = D.Lu + kk * D.sM;
-  const fddp_knot_desc kd = D.knots[t];
-  knot_calc_diff<NT>(kd, D.pblock(b, t), D.nx, D.m, x, u, running, o);
-  if (!gaps) return;
-  if (!s.is_feasible) {
-    // fs[0] = diff(xs[0], x0) = x0 - xs[0]; fs[t+1] = diff(xs[t+1], data[t].xnext)
-    if (t == 0) {
-      double* f = D.fs + D.knot(b, 0) * D.sN;
-      const double* x0 = D.x0 + (int64_t)b * D.sX;
-      for (int i = threadIdx.x; i < D.n; i += NT) f[i] = x0[i] - x[i];
-    }
+  const double* cached = nullptr;
+  for (int t = 0; t <= D.T; ++t) {
+    const fddp_knot_desc kd = D.knots[t];
+    const double* P = stage_params<NT>(D.pblock(b, t), block_doubles_dev(kd.kind, D.nx, kd.nu), pl, pcap, cached);
+    const int64_t kk = D.knot(b, t);
+    const double* xg = D.xs[c] + kk * D.sX;
+    for (int i = threadIdx.x; i < D.nx; i += NT) x[i] = xg[i];
+    const bool running = t < D.T;
     if (running) {
-      double* f = D.fs + D.knot(b, t + 1) * D.sN;
-      const double* xn = D.xnext[c] + D.run(b, t) * D.sX;
-      const double* x1 = D.xs[c] + D.knot(b, t + 1) * D.sX;
-      for (int i = threadIdx.x; i < D.n; i += NT) f[i] = xn[i] - x1[i];
+      const double* ug = D.us[c] + D.run(b, t) * D.sM;
+      for (int i = threadIdx.x; i < D.m; i += NT) u[i] = ug[i];
     }
-  } else if (!s.was_feasible) {  // closing the gaps
-    double* f = D.fs + kk * D.sN;
-    for (int i = threadIdx.x; i < D.n; i += NT) f[i] = 0.;
+    __syncthreads();
+    KnotDiffOut o;
+    o.Fx = D.Fx + kk * D.sNN;
+    o.Fu = D.Fu + kk * D.sNM;
+    o.Lxx = D.Lxx + kk * D.sNN;
+    o.Lxu = D.Lxu + kk * D.sNM;
+    o.Luu = D.Luu + kk * D.sMM;
+    o.Lx = D.Lx + kk * D.sN;
+    o.Lu = D.Lu + kk * D.sM;
+    knot_calc_diff<NT>(kd, P, D.nx, D.m, x, u, running, o);
+    if (gaps) {
+      if (!s.is_feasible) {
+        // fs[0] = diff(xs[0], x0) = x0 - xs[0]; fs[t+1] = diff(xs[t+1], data[t].xnext)
+        if (t == 0) {
+          double* f = D.fs + D.knot(b, 0) * D.sN;
+          const double* x0 = D.x0 + (int64_t)b * D.sX;
+          for (int i = threadIdx.x; i < D.n; i += NT) f[i] = x0[i] - x[i];
+        }
+        if (running) {
+          double* f = D.fs + D.knot(b, t + 1) * D.sN;
+          const double* xn = D.xnext[c] + D.run(b, t) * D.sX;
+          const double* x1 = D.xs[c] + D.knot(b, t + 1) * D.sX;
+          for (int i = threadIdx.x; i < D.n; i += NT) f[i] = xn[i] - x1[i];
+        }
+      } else if (!s.was_feasible) {  // closing the gaps
+        double* f = D.fs + kk * D.sN;
+        for (int i = threadIdx.x; i < D.n; i += NT) f[i] = 0.;
+      }
+    }
+    __syncthreads();
   }
 }
 
@@ -460,7 +511,8 @@ __global__ __launch_bounds__(NT) void backward_kernel(Dev D, Prm prm, int mode) 
 // ---------------------------------------------------------------------------
 template <int NT>
 __device__ bool fwd_trial(const Dev& D, int b, const ElemState& s, double alpha, double* xv, double* uv, double* xn,
-                          double* red, int* flag, double& cost_try, double& dv) {
+                          double* red, int* flag, double& cost_try, double& dv, double* pl, int64_t pcap,
+                          const double*& cached) {
   const int n = D.n, nx = D.nx, m = D.m, T = D.T, tid = threadIdx.x;
   const int c = s.cur, o = 1 - c;
   const bool feas = s.is_feasible != 0;
@@ -486,6 +538,7 @@ __device__ bool fwd_trial(const Dev& D, int b, const ElemState& s, double alpha,
     __syncthreads();
     const bool running = t < T;
     const fddp_knot_desc kd = D.knots[t];
+    const double* P = stage_params<NT>(D.pblock(b, t), block_doubles_dev(kd.kind, nx, kd.nu), pl, pcap, cached);
     if (running) {
       const int nu = kd.nu;
       const double* us = D.us[c] + D.run(b, t) * D.sM;
@@ -505,7 +558,7 @@ __device__ bool fwd_trial(const Dev& D, int b, const ElemState& s, double alpha,
       }
       __syncthreads();
     }
-    const double ct = knot_calc<NT>(kd, D.pblock(b, t), nx, xv, uv, running, xn, red);
+    const double ct = knot_calc<NT>(kd, P, nx, xv, uv, running, xn, red);
     bool bad = false;
     if (running) {
       double* xo = D.xnext[o] + D.run(b, t) * D.sX;
@@ -540,12 +593,15 @@ __device__ bool fwd_trial(const Dev& D, int b, const ElemState& s, double alpha,
 }
 
 template <int NT>
-__global__ __launch_bounds__(NT) void forward_kernel(Dev D, Prm prm, int mode, double alpha1, int* active_count) {
+__global__ __launch_bounds__(NT) void forward_kernel(Dev D, Prm prm, int mode, double alpha1, int* active_count,
+                                                     int64_t pcap) {
   const int b = blockIdx.x;
   ElemState* st = D.st + b;
   if (mode == 0 && !st->active) return;
   extern __shared__ __attribute__((aligned(16))) double sm[];
-  double* xv = sm;
+  double* pl = sm;
+  const double* cached = nullptr;
+  double* xv = pl + pcap;
   double* uv = xv + D.sX;
   double* xn = uv + D.sM;
   double* red = xn + D.sX;
@@ -553,7 +609,7 @@ __global__ __launch_bounds__(NT) void forward_kernel(Dev D, Prm prm, int mode, d
   ElemState s = *st;
   if (mode == 1) {
     double ct, dv;
-    const bool ok = fwd_trial<NT>(D, b, s, alpha1, xv, uv, xn, red, flag, ct, dv);
+    const bool ok = fwd_trial<NT>(D, b, s, alpha1, xv, uv, xn, red, flag, ct, dv, pl, pcap, cached);
     if (threadIdx.x == 0) {
       st->fwd_fail = ok ? 0 : 1;
       st->cost_try = ct;
@@ -568,7 +624,7 @@ __global__ __launch_bounds__(NT) void forward_kernel(Dev D, Prm prm, int mode, d
     const double alpha = prm.alphas[a];
     s.steplength = alpha;
     double ct, dv;
-    if (!fwd_trial<NT>(D, b, s, alpha, xv, uv, xn, red, flag, ct, dv)) continue;
+    if (!fwd_trial<NT>(D, b, s, alpha, xv, uv, xn, red, flag, ct, dv, pl, pcap, cached)) continue;
     s.cost_try = ct;
     s.dV = s.cost - ct;
     s.dv = dv;

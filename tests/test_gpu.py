@@ -16,6 +16,17 @@ pytestmark = pytest.mark.gpu
 
 RTOL = 1e-6  # north_star: xs/us/cost within 1e-6 relative
 
+
+@pytest.fixture(params=["mfma", "generic"], autouse=True)
+def backward_variant(request, monkeypatch):
+    """Run every parity test with the MFMA Riccati sweep (default where the
+    shape allows) and with the generic LDS sweep (FDDP_BACKWARD=generic)."""
+    if request.param == "generic":
+        monkeypatch.setenv("FDDP_BACKWARD", "generic")
+    else:
+        monkeypatch.delenv("FDDP_BACKWARD", raising=False)
+    return request.param
+
 CASES = [
     ("C1_unicycle", dict(T=30, B=16)),
     ("C2_lqr", dict(T=20, B=8)),
