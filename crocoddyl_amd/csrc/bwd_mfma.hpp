@@ -87,8 +87,22 @@ __device__ __forceinline__ double zfrag(const double* __restrict__ Fx, const dou
   return (row < n && col < m) ? Fu[(int64_t)col * n + row] : 0.;
 }
 
+// Diagnostic phase timer (FDDP_STAMPS=1): per wave, cycles spent per phase.
+struct Stamp {
+  unsigned long long* out;
+  unsigned long long t0;
+  __device__ Stamp(unsigned long long* o) : out(o), t0(o ? __builtin_amdgcn_s_memtime() : 0) {}
+  __device__ __forceinline__ void mark(int ph) {
+    if (out) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      if ((threadIdx.x & 63) == 0) out[ph] += t - t0;
+      t0 = t;
+    }
+  }
+};
+
 template <int NTL, int MTL>
-__device__ bool bwd_sweep_mfma(const Dev& D, int b, bool feas, double xreg, double ureg, double* sm,
+__device__ __forceinline__ bool bwd_sweep_mfma(const Dev& D, int b, bool feas, double xreg, double ureg, double* sm,
                                const BwdSched& sch) {
   using Cfg = MfmaCfg<NTL, MTL>;
   constexpr int NP = Cfg::NP, MP = Cfg::MP, JT = Cfg::JT, LDV = Cfg::LDV, LDQ = Cfg::LDQ, MAXOWN = Cfg::MAXOWN;
@@ -113,6 +127,7 @@ __device__ bool bwd_sweep_mfma(const Dev& D, int b, bool feas, double xreg, doub
   const int n = D.n, m = D.m, T = D.T, tid = threadIdx.x;
   const int wid = tid >> 6, lane = tid & 63, q = lane >> 4, c = lane & 15;
   const bool xr = !isnan(xreg), ur = !isnan(ureg);
+  Stamp stamp(D.stamps ? D.stamps + ((int64_t)b * 4 + wid) * 8 : nullptr);
 
   // ---- terminal: Vxx = Lxx_T (+ xreg I), Vx = Lx_T (+ Vxx fs_T) ------------
   {
@@ -166,6 +181,7 @@ __device__ bool bwd_sweep_mfma(const Dev& D, int b, bool feas, double xreg, doub
     const double* Lxu = D.Lxu + kk * D.sNM;
     const double* Luu = D.Luu + kk * D.sMM;
     __syncthreads();
+    stamp.mark(7);
     // ---- phase 0: fs, Qx = Lx + Fx^T Vx', Qu = Lu + Fu^T Vx' -----------------
     {
       const double* fs = D.fs + kk * D.sN;
@@ -194,7 +210,9 @@ __device__ bool bwd_sweep_mfma(const Dev& D, int b, bool feas, double xreg, doub
       }
       if (tid == 0) *flag = 0;
     }
+    stamp.mark(0);
     __syncthreads();
+    stamp.mark(1);
     // ---- phase 1: G = V Z_i, H(i, j) = G_i^T Z_j + L(i, j) per owned block ---
     {
       const int nown = sch.nown[wid];
@@ -203,6 +221,54 @@ __device__ bool bwd_sweep_mfma(const Dev& D, int b, bool feas, double xreg, doub
       for (int o = 0; o < MAXOWN; ++o) {
         ib[o] = o < nown ? sch.blk[wid][o] : 0;
         js[o] = o < nown ? sch.jstart[wid][o] : JT;
+      }
+      // Initial accumulator of H(i, j): the cost block (symmetric part of Lxx
+      // for Qxx, which the reference reaches through its Vxx symmetrisation;
+      // Lxu for Qxu; Luu + ureg I for Quu).
+      auto linit = [&](f64x4(&acc)[MAXOWN], int j) {
+#pragma unroll
+        for (int o = 0; o < MAXOWN; ++o) {
+          acc[o] = f64x4{0., 0., 0., 0.};
+          if (o < nown && j >= js[o]) {
+            const int i = ib[o];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int R = 16 * i + q + 4 * r, C = 16 * j + c;
+              double v = 0.;
+              if (j < NTL) {
+                if (R < n && C < n) v = 0.5 * (Lxx[(int64_t)C * n + R] + Lxx[(int64_t)R * n + C]);
+              } else if (i < NTL) {
+                const int Cu = C - NP;
+                if (R < n && Cu < m) v = Lxu[(int64_t)Cu * n + R];
+              } else {
+                const int Ru = R - NP, Cu = C - NP;
+                if (Ru < m && Cu < m) {
+                  v = Luu[(int64_t)Cu * m + Ru];
+                  if (ur && Ru == Cu) v += ureg;
+                }
+              }
+              acc[o][r] = v;
+            }
+          }
+        }
+      };
+      int jmin = JT;
+#pragma unroll
+      for (int o = 0; o < MAXOWN; ++o) jmin = js[o] < jmin ? js[o] : jmin;
+      // Issue every global load of the G phase and of the first H column at
+      // once: the fragments are independent, so one memory latency is exposed
+      // per batch instead of one per k-step.
+      double zg[MAXOWN][4 * NTL];
+#pragma unroll
+      for (int o = 0; o < MAXOWN; ++o)
+#pragma unroll
+        for (int s2 = 0; s2 < 4 * NTL; ++s2) zg[o][s2] = o < nown ? zfrag<NTL, MTL>(Fx, Fu, n, m, s2, ib[o], q, c) : 0.;
+      double zc[4 * NTL];
+      f64x4 ac[MAXOWN];
+      if (jmin < JT) {
+#pragma unroll
+        for (int s2 = 0; s2 < 4 * NTL; ++s2) zc[s2] = zfrag<NTL, MTL>(Fx, Fu, n, m, s2, jmin, q, c);
+        linit(ac, jmin);
       }
       f64x4 G[MAXOWN][NTL];
 #pragma unroll
@@ -218,49 +284,28 @@ __device__ bool bwd_sweep_mfma(const Dev& D, int b, bool feas, double xreg, doub
 #pragma unroll
           for (int o = 0; o < MAXOWN; ++o) {
             if (o < nown) {
-              const double z = zfrag<NTL, MTL>(Fx, Fu, n, m, s, ib[o], q, c);
 #pragma unroll
-              for (int a = 0; a < NTL; ++a) G[o][a] = mfma4(vf[a], z, G[o][a]);
+              for (int a = 0; a < NTL; ++a) G[o][a] = mfma4(vf[a], zg[o][s], G[o][a]);
             }
           }
         }
       }
-      int jmin = JT;
-#pragma unroll
-      for (int o = 0; o < MAXOWN; ++o) jmin = js[o] < jmin ? js[o] : jmin;
+      // H columns, double-buffered: column j+1's fragments and cost block are
+      // in flight while column j's MFMAs run.
       for (int j = jmin; j < JT; ++j) {
-        f64x4 acc[MAXOWN];
+        const bool more = j + 1 < JT;
+        double zn[4 * NTL];
+        f64x4 an[MAXOWN];
+        if (more) {
 #pragma unroll
-        for (int o = 0; o < MAXOWN; ++o) {
-          acc[o] = f64x4{0., 0., 0., 0.};
-          if (o < nown && j >= js[o]) {
-            const int i = ib[o];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int R = 16 * i + q + 4 * r, C = 16 * j + c;
-              double v = 0.;
-              if (j < NTL) {  // Qxx block: symmetric part of Lxx (the reference symmetrises Vxx)
-                if (R < n && C < n) v = 0.5 * (Lxx[(int64_t)C * n + R] + Lxx[(int64_t)R * n + C]);
-              } else if (i < NTL) {  // Qxu block
-                const int Cu = C - NP;
-                if (R < n && Cu < m) v = Lxu[(int64_t)Cu * n + R];
-              } else {  // Quu block (+ ureg I)
-                const int Ru = R - NP, Cu = C - NP;
-                if (Ru < m && Cu < m) {
-                  v = Luu[(int64_t)Cu * m + Ru];
-                  if (ur && Ru == Cu) v += ureg;
-                }
-              }
-              acc[o][r] = v;
-            }
-          }
+          for (int s2 = 0; s2 < 4 * NTL; ++s2) zn[s2] = zfrag<NTL, MTL>(Fx, Fu, n, m, s2, j + 1, q, c);
+          linit(an, j + 1);
         }
 #pragma unroll
         for (int s = 0; s < 4 * NTL; ++s) {
-          const double z = zfrag<NTL, MTL>(Fx, Fu, n, m, s, j, q, c);
 #pragma unroll
           for (int o = 0; o < MAXOWN; ++o)
-            if (o < nown && j >= js[o]) acc[o] = mfma4(G[o][s >> 2][s & 3], z, acc[o]);
+            if (o < nown && j >= js[o]) ac[o] = mfma4(G[o][s >> 2][s & 3], zc[s], ac[o]);
         }
 #pragma unroll
         for (int o = 0; o < MAXOWN; ++o) {
@@ -269,76 +314,86 @@ __device__ bool bwd_sweep_mfma(const Dev& D, int b, bool feas, double xreg, doub
             if (j < NTL) {
               const int tq = i * NTL - (i * (i - 1)) / 2 + (j - i);
 #pragma unroll
-              for (int r = 0; r < 4; ++r) Qxx[tq * 256 + r * 64 + lane] = acc[o][r];
+              for (int r = 0; r < 4; ++r) Qxx[tq * 256 + r * 64 + lane] = ac[o][r];
             } else if (i < NTL) {
 #pragma unroll
-              for (int r = 0; r < 4; ++r) Qxu[(16 * (j - NTL) + c) * LDV + 16 * i + q + 4 * r] = acc[o][r];
+              for (int r = 0; r < 4; ++r) Qxu[(16 * (j - NTL) + c) * LDV + 16 * i + q + 4 * r] = ac[o][r];
             } else {
 #pragma unroll
-              for (int r = 0; r < 4; ++r) Quu[(16 * (j - NTL) + c) * LDQ + 16 * (i - NTL) + q + 4 * r] = acc[o][r];
+              for (int r = 0; r < 4; ++r) Quu[(16 * (j - NTL) + c) * LDQ + 16 * (i - NTL) + q + 4 * r] = ac[o][r];
             }
           }
         }
+        if (more) {
+#pragma unroll
+          for (int s2 = 0; s2 < 4 * NTL; ++s2) zc[s2] = zn[s2];
+#pragma unroll
+          for (int o = 0; o < MAXOWN; ++o) ac[o] = an[o];
+        }
       }
-      // ---- wave 0: Cholesky of Quu and Quu^-1 (overlaps waves 1-3) -----------
+      // ---- wave 0: Quu^-1 by in-place Gauss-Jordan (overlaps waves 1-3) ------
+      // Without pivoting on an SPD matrix the k-th pivot equals L(k,k)^2 of its
+      // Cholesky factor, so `pivot <= 0` is exactly Eigen LLT's failure
+      // (ddp.cpp:300-304). Lane l owns column j = l % MP and RPL rows
+      // i = (l / MP) * RPL + r of the MP x MP matrix; row k / column k are
+      // broadcast through LDS at each step.
       if (wid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's Quu stores landed
-        double a[MP];
-#pragma unroll
-        for (int k2 = 0; k2 < MP; ++k2) a[k2] = (lane < m && k2 < m) ? Quu[k2 * LDQ + lane] : 0.;
-        bool bad = false;
-#pragma unroll
-        for (int j = 0; j < MP; ++j) {
-          if (j < m) {
-            const double d = __shfl(a[j], j, 64);
-            if (!(d > 0.)) bad = true;  // Eigen LLT: NumericalIssue on a pivot <= 0
-            const double ljj = sqrt(d);
-            const double inv = 1. / ljj;
-            if (lane > j) a[j] *= inv;
-            if (lane == j) a[j] = ljj;
-            colbuf[lane] = a[j];
-            __builtin_amdgcn_s_waitcnt(0xc07f);
-            __builtin_amdgcn_wave_barrier();
-#pragma unroll
-            for (int k2 = j + 1; k2 < MP; ++k2)
-              if (k2 < m) a[k2] -= a[j] * colbuf[k2];
-            __builtin_amdgcn_s_waitcnt(0xc07f);
-            __builtin_amdgcn_wave_barrier();
-          }
-        }
-        // L to LDS (column-major, ld LDQ) and 1/diag
-        if (lane < MP) {
-#pragma unroll
-          for (int k2 = 0; k2 < MP; ++k2) Lm[k2 * LDQ + lane] = (k2 <= lane) ? a[k2] : 0.;
-          dinv[lane] = lane < m ? 1. / a[lane] : 0.;
-        }
-        __builtin_amdgcn_s_waitcnt(0xc07f);
+        constexpr int RPL = MP * MP / 64;
+        static_assert(MP * MP % 64 == 0 && 64 % MP == 0, "Gauss-Jordan lane layout");
+        const int jc = lane % MP, h = lane / MP;
+        double* rowbuf = dinv;  // MP doubles
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // this wave's Quu stores have landed
         __builtin_amdgcn_wave_barrier();
-        // column `lane` of Quu^-1 = L^-T L^-1 e_lane
-        double x[MP];
+        double A[RPL];
 #pragma unroll
-        for (int i = 0; i < MP; ++i) {
-          double s2 = (i == lane) ? 1. : 0.;
+        for (int r = 0; r < RPL; ++r) A[r] = Quu[jc * LDQ + h * RPL + r];
+        bool bad = false;
+        for (int k = 0; k < m; ++k) {
+          const int hk = k / RPL, rk = k % RPL;
+          // column k (before elimination) and the pivot
 #pragma unroll
-          for (int k2 = 0; k2 < i; ++k2) s2 -= Lm[k2 * LDQ + i] * x[k2];
-          x[i] = s2 * dinv[i];
+          for (int r = 0; r < RPL; ++r)
+            if (jc == k) colbuf[h * RPL + r] = A[r];
+          __builtin_amdgcn_s_waitcnt(0xc07f);
+          __builtin_amdgcn_wave_barrier();
+          const double p = colbuf[k];
+          if (!(p > 0.)) bad = true;
+          const double pinv = 1. / p;
+          // row k scaled by 1/p (A(k,k) <- 1 first, so it becomes 1/p)
+#pragma unroll
+          for (int r = 0; r < RPL; ++r) {
+            if (h == hk && r == rk) {
+              const double v = (jc == k ? 1. : A[r]) * pinv;
+              A[r] = v;
+              rowbuf[jc] = v;
+            }
+          }
+          __builtin_amdgcn_s_waitcnt(0xc07f);
+          __builtin_amdgcn_wave_barrier();
+          const double rkj = rowbuf[jc];
+#pragma unroll
+          for (int r = 0; r < RPL; ++r) {
+            const int i = h * RPL + r;
+            if (i != k) {
+              const double f = colbuf[i];
+              A[r] = (jc == k ? 0. : A[r]) - f * rkj;
+            }
+          }
+          __builtin_amdgcn_s_waitcnt(0xc07f);
+          __builtin_amdgcn_wave_barrier();
         }
+        // Quu^-1 is symmetric: store (i, j) at (j, i) (conflict-free rows)
 #pragma unroll
-        for (int i = MP - 1; i >= 0; --i) {
-          double s2 = x[i];
-#pragma unroll
-          for (int k2 = i + 1; k2 < MP; ++k2) s2 -= Lm[i * LDQ + k2] * x[k2];
-          x[i] = s2 * dinv[i];
-        }
-        if (lane < MP) {
-#pragma unroll
-          for (int i = 0; i < MP; ++i) Qi[i * LDQ + lane] = (lane < m && i < m) ? x[i] : 0.;
+        for (int r = 0; r < RPL; ++r) {
+          const int i = h * RPL + r;
+          Qi[i * LDQ + jc] = (i < m && jc < m) ? A[r] : 0.;
         }
         if (bad && lane == 0) *flag = 1;
       }
     }
+    stamp.mark(2);
     __syncthreads();
+    stamp.mark(3);
     if (*flag) return false;
     // ---- phase 2: K = Quu^-1 Qxu^T (MFMA), k = Quu^-1 Qu ------------------------
     for (int jt = wid; jt < NTL; jt += 4) {
@@ -369,6 +424,7 @@ __device__ bool bwd_sweep_mfma(const Dev& D, int b, bool feas, double xreg, doub
       kv[i] = a;
       if (i < m) D.k[rr * D.sM + i] = a;
     }
+    stamp.mark(4);
     __syncthreads();
     // ---- phase 2b: Quuk = Quu k ; Vxx = Qxx - Qxu K (+ xreg I), symmetric ------
     for (int i = tid; i < MP; i += 256) {
@@ -406,6 +462,7 @@ __device__ bool bwd_sweep_mfma(const Dev& D, int b, bool feas, double xreg, doub
       }
       if (bad) *flag = 1;
     }
+    stamp.mark(5);
     __syncthreads();
     // ---- phase 3: Vx, Vxx fs, checks, reduction terms, stores ----------------
     {
@@ -471,6 +528,7 @@ __device__ bool bwd_sweep_mfma(const Dev& D, int b, bool feas, double xreg, doub
         for (int i = tid; i < m; i += 256) D.dQu[rr * D.sM + i] = qu[i];
       }
     }
+    stamp.mark(6);
     __syncthreads();
     if (*flag) return false;
   }

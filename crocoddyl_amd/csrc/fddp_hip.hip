@@ -495,6 +495,13 @@ int fddp_create(const fddp_dims* dims, const fddp_knot_desc* knots, const double
     }
     h->bwd_variant = v > 0 ? v : 0;
   }
+  if (const char* e = std::getenv("FDDP_STAMPS")) {
+    if (e[0] == '1') {
+      double* p2 = nullptr;
+      if ((rc = dalloc(h, &p2, (int64_t)d.B * 32))) return bail(rc);
+      D.stamps = (unsigned long long*)p2;
+    }
+  }
   if (hipStreamSynchronize(h->stream) != hipSuccess) return bail(fail(FDDP_ERR_RUNTIME, "sync after create"));
   *out = h;
   return FDDP_OK;
@@ -504,6 +511,22 @@ void fddp_destroy(fddp_handle* h) {
   if (!h) return;
   DeviceGuard g(h->device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
+  if (h->D.stamps) {  // diagnostic summary: mean cycles per element per wave and phase
+    std::vector<unsigned long long> v((size_t)h->dims.B * 32);
+    if (hipMemcpy(v.data(), h->D.stamps, v.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
+      const char* names[8] = {"p0_prep", "p0_barrier", "p1_GH_fact", "p1_barrier", "p2_K", "p2b_Vupd", "p3_vec", "loop"};
+      std::fprintf(stderr, "[fddp stamps] mean cycles per element (variant %d):\n", h->bwd_variant);
+      for (int w = 0; w < 4; ++w) {
+        std::fprintf(stderr, "  wave %d:", w);
+        for (int ph = 0; ph < 8; ++ph) {
+          double s2 = 0;
+          for (int b = 0; b < h->dims.B; ++b) s2 += (double)v[((size_t)b * 4 + w) * 8 + ph];
+          std::fprintf(stderr, " %s=%.0f", names[ph], s2 / h->dims.B);
+        }
+        std::fprintf(stderr, "\n");
+      }
+    }
+  }
   for (void* p : h->allocs) (void)hipFree(p);
   for (auto& r : h->ev_rec) {
     (void)hipEventDestroy(r.second.first);

@@ -61,7 +61,7 @@ __device__ inline const double* stage_params(const double* g, int64_t size, doub
 // C0 == nullptr means zero.
 // ---------------------------------------------------------------------------
 template <int NT, bool TA, bool TB>
-__device__ void wg_gemm(int M, int N, int K, const double* __restrict__ A, int lda, const double* __restrict__ Bm,
+__device__ __forceinline__ void wg_gemm(int M, int N, int K, const double* __restrict__ A, int lda, const double* __restrict__ Bm,
                         int ldb, const double* C0, int ldc0, double* C, int ldc, double sgn) {
   const int mt = (M + 1) >> 1, ntl = (N + 1) >> 1;
   for (int tile = threadIdx.x; tile < mt * ntl; tile += NT) {
@@ -242,7 +242,7 @@ struct BwdSmem {
 };
 
 template <int NT>
-__device__ bool bwd_sweep(const Dev& D, int b, bool feas, double xreg, double ureg, BwdSmem& S) {
+__device__ __forceinline__ bool bwd_sweep(const Dev& D, int b, bool feas, double xreg, double ureg, BwdSmem& S) {
   const int n = D.n, m = D.m, T = D.T, tid = threadIdx.x;
   const bool xr = !isnan(xreg), ur = !isnan(ureg);
   // terminal: Vxx = Lxx_T (+ xreg I), Vx = Lx_T (+ Vxx fs_T)
@@ -510,7 +510,7 @@ __global__ __launch_bounds__(NT) void backward_kernel(Dev D, Prm prm, int mode) 
 // mode 1: a single trial at `alpha` (tryStep), storing cost_try, dV and dv.
 // ---------------------------------------------------------------------------
 template <int NT>
-__device__ bool fwd_trial(const Dev& D, int b, const ElemState& s, double alpha, double* xv, double* uv, double* xn,
+__device__ __forceinline__ bool fwd_trial(const Dev& D, int b, const ElemState& s, double alpha, double* xv, double* uv, double* xn,
                           double* red, int* flag, double& cost_try, double& dv, double* pl, int64_t pcap,
                           const double*& cached) {
   const int n = D.n, nx = D.nx, m = D.m, T = D.T, tid = threadIdx.x;

@@ -91,7 +91,7 @@ __device__ inline double lq_cost_total(const double (&t)[5]) {
 // Writes xnext[0..nx) and returns the knot cost in every thread.
 // `red`: LDS scratch of >= 5*NT/64 doubles. Contains barriers: call uniformly.
 template <int NT>
-__device__ double knot_calc(const fddp_knot_desc& kd, const double* P, int nx, const double* x, const double* u,
+__device__ __forceinline__ double knot_calc(const fddp_knot_desc& kd, const double* P, int nx, const double* x, const double* u,
                             bool use_u, double* xnext, double* red) {
   const int nu = kd.nu;
   use_u = use_u && nu > 0;
@@ -159,7 +159,7 @@ struct KnotDiffOut {
 // model->calcDiff(data, x, u) / calcDiff(data, x). Writes full blocks (entries
 // beyond the knot's nu are zero); Luu has leading dimension m = nu_max.
 template <int NT>
-__device__ void knot_calc_diff(const fddp_knot_desc& kd, const double* P, int nx, int m, const double* x,
+__device__ __forceinline__ void knot_calc_diff(const fddp_knot_desc& kd, const double* P, int nx, int m, const double* x,
                                const double* u, bool use_u, const KnotDiffOut& o) {
   const int n = nx;
   const int nu = kd.nu;
