@@ -8,16 +8,15 @@ exactly one FDDP iteration per element (calc, calcDiff + gaps, backward
 Riccati sweep, line search), so FDDP iterations/s == MPC solves/s.
 
 Multi-GPU: one process per GPU (torchrun), the batch axis is sharded (each
-rank owns B independent problems: weak scaling, no collective in the solve),
-and the converged trajectories are collected with one RCCL all-gather at the
-end of the timed region.
+rank owns B independent problems: weak scaling, no collective inside the
+solve), and the solved trajectories are collected with one RCCL all-gather at
+the end of the timed region (crocoddyl_amd/dist.py).
 
 Prints one JSON line (rank 0).
 """
 import argparse
 import json
 import os
-import subprocess
 import sys
 import time
 
@@ -28,7 +27,6 @@ import numpy as np  # noqa: E402
 
 METRIC = "FDDP iterations/sec + MPC solves/sec, Talos contact T=100, batch=1024"
 FP64_PEAK_TFLOPS = 78.6  # MI355X dense FP64 (vector == matrix rate on gfx950), datasheet
-HBM_PEAK_GBS = 8000.0
 
 
 def backward_flops_per_knot(n, m):
@@ -42,19 +40,20 @@ def backward_bytes_per_knot(n, m):
 
 
 def cpu_baseline(cfg, T, seed, target_s=12.0):
-    """Time the CPU oracle (port of the reference solver, OpenMP over batch
+    """Time the CPU oracle (C++ port of the reference solver, OpenMP over batch
     elements) on this host, on a bounded sample of the same workload."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import oracle_lib
     import helpers
+    import oracle_lib
 
     out = os.path.join("/tmp", f"oracle_native_{os.getpid()}")
     try:
         oracle_lib.build(out_dir=out, arch="-march=native")
-        so = os.path.join(out, "liboracle.so")
-        oracle_lib._lib = oracle_lib.lib(so)
+        oracle_lib._lib = oracle_lib.lib(os.path.join(out, "liboracle.so"))
+        flags = "-O3 -march=native"
     except Exception:
-        oracle_lib._lib = None  # fall back to the in-tree x86-64-v3 build
+        oracle_lib._lib = None  # the in-tree x86-64-v3 build
+        flags = "-O3 -march=x86-64-v3"
     try:
         cores = len(os.sched_getaffinity(0))
     except Exception:
@@ -74,24 +73,20 @@ def cpu_baseline(cfg, T, seed, target_s=12.0):
             it += sum(x.n_iter_run for x in r)
         return it, time.perf_counter() - t0
 
-    Bs = threads
-    it, dt = run(Bs, 1)
-    rate = it / max(dt, 1e-9)
+    it, dt = run(threads, 1)
     steps = 4
-    Bs = int(max(threads, min(1024, target_s * rate / steps)))
+    Bs = int(max(threads, min(1024, target_s * (it / max(dt, 1e-9)) / steps)))
     Bs = max(threads, (Bs // threads) * threads)
     it, dt = run(Bs, steps)
     return {"value": it / dt, "unit": "FDDP iterations/s", "cores": threads, "kind": "port",
-            "sample": f"{cfg} T={T}, {Bs} elements x {steps} warm-started solve(maxiter=1) "
-                      f"({it} element-iterations, {dt:.1f} s), oracle/fddp_oracle.cpp -O3 -march=native, "
+            "sample": f"{cfg} T={T}: {Bs} elements x {steps} warm-started solve(maxiter=1) "
+                      f"({it} element-iterations in {dt:.1f} s); oracle/fddp_oracle.cpp {flags} -fopenmp, "
                       f"OpenMP over elements"}
 
 
 def load_pmc(cfg):
-    path = os.path.join(ROOT, "profiles", "pmc_backward.json")
     try:
-        d = json.load(open(path))
-        return d.get(cfg)
+        return json.load(open(os.path.join(ROOT, "profiles", "pmc_backward.json"))).get(cfg)
     except Exception:
         return None
 
@@ -102,22 +97,18 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="C5_talos_full")
-    ap.add_argument("--batch", type=int, default=None, help="elements per GPU (default: config's)")
+    ap.add_argument("--batch", type=int, default=None, help="elements per GPU (default: the config's)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
-    import torch.distributed as dist
-
-    if world > 1:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    dev = local_rank
 
     from crocoddyl_amd import ShootingProblem, SolverFDDP, synthetic
+    from crocoddyl_amd import dist as cdist
+
+    ws, rank, local_rank = cdist.world()
+    cdist.init("nccl", local_rank)
+    dev = local_rank
 
     kind, d1, nu, T, B0, dt = synthetic.CONFIGS[args.config]
     B = args.batch or B0
@@ -127,22 +118,19 @@ def main():
     solver = SolverFDDP(problem)
     n, m, nx = problem.ndx, problem.nu_max, problem.nx
 
-    # converge once from a cold start, then receding-horizon warm-started solves
-    solver.solve(maxiter=5)
+    solver.solve(maxiter=5)  # converge once from a cold start
 
-    def step():
+    def step():  # one receding-horizon MPC solve, all elements
         solver.mpcShift()
         solver.solve_from_candidate(maxiter=1, isFeasible=False, regInit=0.1)
 
     for _ in range(args.warmup):
         step()
-    xs_all = None
-    if world > 1:
-        xs_local = torch.empty((B, T + 1, nx), dtype=torch.float64, device=f"cuda:{dev}")
-        xs_all = torch.empty((world * B, T + 1, nx), dtype=torch.float64, device=f"cuda:{dev}")
-        dist.barrier()
-    torch.cuda.synchronize(dev)
+    xs_local = torch.empty((B, T + 1, nx), dtype=torch.float64, device=f"cuda:{dev}")
+    if ws > 1:
+        torch.distributed.barrier()
     solver.synchronize()
+    torch.cuda.synchronize(dev)
     solver.get_timing()
     solver.set_timing(True)
     t0 = time.perf_counter()
@@ -150,26 +138,17 @@ def main():
     for _ in range(args.steps):
         step()
         iters += int(np.sum(solver.n_iter_run))
-    if world > 1:  # the single collective: gather the solved trajectories
-        solver.xs_device(xs_local.data_ptr())
-        solver.synchronize()
-        dist.all_gather_into_tensor(xs_all, xs_local)
+    solver.xs_device(xs_local.data_ptr())  # the solved trajectories, on device
     solver.synchronize()
+    xs_all = cdist.gather_rows(xs_local)  # the single collective (RCCL all-gather)
     torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
+    if ws > 1:
+        torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
     solver.set_timing(False)
     timing = solver.get_timing()
-    if world > 1:
-        t = torch.tensor([elapsed, float(iters)], dtype=torch.float64, device=f"cuda:{dev}")
-        tmax = t.clone()
-        dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
-        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
-        elapsed = float(tmax[0])
-        total_iters = float(t[1])
-    else:
-        total_iters = float(iters)
+    elapsed, total_iters = cdist.job_time_and_work(elapsed, iters, f"cuda:{dev}")
+    assert xs_all.shape[0] == ws * B
 
     if rank == 0:
         value = total_iters / elapsed
@@ -179,27 +158,27 @@ def main():
         Y = backward_bytes_per_knot(n, m) * B * T
         achieved = F / avg_bwd_s / 1e12
         pmc = load_pmc(args.config)
-        roof = {"kernel": "backward_kernel (Riccati sweep)", "bound": "mfma", "achieved": round(achieved, 3),
+        roof = {"kernel": "backward Riccati sweep (bwd_mfma.hpp)", "bound": "mfma", "achieved": round(achieved, 3),
                 "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / FP64_PEAK_TFLOPS, 4),
                 "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
                 "algorithmic_flops_per_launch": F, "algorithmic_bytes_per_launch": Y,
                 "achieved_algorithmic_GBps": round(Y / avg_bwd_s / 1e9, 1),
-                "avg_launch_ms": round(avg_bwd_s * 1e3, 3)}
+                "avg_launch_ms": round(avg_bwd_s * 1e3, 3), "timer": "HIP events on the solver stream"}
         cpu = None
-        if world == 1 and not args.no_cpu_baseline:
+        if ws == 1 and not args.no_cpu_baseline:
             try:
                 cpu = cpu_baseline(args.config, T, synthetic.seed_of(args.config))
             except Exception as e:  # reported, never fatal for the GPU number
                 cpu = {"error": repr(e)}
         out = {
-            "metric": METRIC, "value": round(value, 2), "unit": "FDDP iterations/s", "n_gpus": world,
+            "metric": METRIC, "value": round(value, 2), "unit": "FDDP iterations/s", "n_gpus": ws,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic: seeded Euler(dt)∘DifferentialActionModelLQR knots at the config's (n, m, T); "
                     "per-element matrices (SURVEY §8d); no robot model (Pinocchio/URDF absent)",
             "config": {"workload": f"{args.config}: n={n}, m={m}, T={T}, B={B} per GPU, warm-started "
                                    "solve(maxiter=1, reg_init=0.1) after a device receding-horizon shift",
-                       "global_batch": B * world, "T": T, "parallelism": f"batch-sharded x{world}"},
+                       "global_batch": B * ws, "T": T, "parallelism": f"batch-sharded x{ws}"},
             "mpc_solves_per_s": round(value, 2),
             "kernel_ms_per_step": {k: round(v[0] / max(args.steps, 1), 3) for k, v in timing.items()},
             "roofline": roof,
@@ -208,8 +187,8 @@ def main():
         if cpu and "value" in cpu:
             out["speedup_vs_cpu"] = round(value / cpu["value"], 2)
         print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    if ws > 1:
+        torch.distributed.destroy_process_group()
 
 
 if __name__ == "__main__":

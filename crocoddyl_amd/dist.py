@@ -1,0 +1,61 @@
+"""Multi-GPU plumbing: one process per GPU, the batch axis sharded.
+
+The B problems of a batch are independent (the reference has no coupling
+between problems), so each rank solves its own shard with no
+communication during solve(). The only collective is one all-gather of the
+solved trajectories at the end (RCCL over xGMI on the GPU box: backend
+"nccl"; gloo in the CPU tests).
+"""
+import os
+
+import torch
+import torch.distributed as dist
+
+
+def world():
+    """(world_size, rank, local_rank) from the torchrun environment."""
+    return (int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def init(backend, local_rank=None):
+    """Initialise the default process group (MASTER_ADDR/PORT from the env)."""
+    ws, rank, lr = world()
+    if ws <= 1 or dist.is_initialized():
+        return ws, rank
+    if backend == "nccl":
+        lr = lr if local_rank is None else local_rank
+        torch.cuda.set_device(lr)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", lr))
+    else:
+        dist.init_process_group(backend)
+    return ws, rank
+
+
+def shard(b_global, ws, rank):
+    """Contiguous block of batch elements owned by `rank`: (start, count)."""
+    base, rem = divmod(b_global, ws)
+    start = rank * base + min(rank, rem)
+    return start, base + (1 if rank < rem else 0)
+
+
+def gather_rows(local):
+    """All-gather equally shaped per-rank tensors along dim 0 (the one
+    collective of the batched solve)."""
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return local
+    out = torch.empty((dist.get_world_size() * local.shape[0],) + tuple(local.shape[1:]), dtype=local.dtype,
+                      device=local.device)
+    dist.all_gather_into_tensor(out, local.contiguous())
+    return out
+
+
+def job_time_and_work(elapsed_s, work, device):
+    """Whole-job numbers: the slowest rank's time, the sum of the work."""
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return float(elapsed_s), float(work)
+    t = torch.tensor([float(elapsed_s)], dtype=torch.float64, device=device)
+    w = torch.tensor([float(work)], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dist.all_reduce(w, op=dist.ReduceOp.SUM)
+    return float(t.item()), float(w.item())

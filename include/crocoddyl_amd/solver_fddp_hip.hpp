@@ -1,0 +1,289 @@
+// crocoddyl_amd C++ facade over libfddp_hip (include/fddp_hip.h), header-only.
+//
+// Mirrors the reference's C++ API for the hot path so a C++ caller switches by
+// swapping the namespace:
+//   crocoddyl::ShootingProblem(x0, running_models, terminal_model)
+//       include/crocoddyl/core/optctrl/shooting.hpp:48-63
+//   crocoddyl::SolverFDDP(problem).solve(init_xs, init_us, maxiter, is_feasible, reginit)
+//       include/crocoddyl/core/solvers/fddp.hpp:50-101, src/core/solvers/fddp.cpp:19-105
+//   crocoddyl::ActionModelLQR(nx, nu, drift_free)          core/actions/lqr.hpp:21-60
+//   crocoddyl::ActionModelUnicycle()                        core/actions/unicycle.hpp
+//   crocoddyl::DifferentialActionModelLQR(nq, nu, drift_free), IntegratedActionModelEuler(model, dt)
+// Errors raise crocoddyl_amd::Exception (the reference's throw_pretty /
+// crocoddyl::Exception, core/utils/exception.hpp:23-50). Vectors are any type
+// with data()/size() (std::vector<double>, Eigen::VectorXd); matrices are
+// column-major (Eigen's default order).
+// Link: -lfddp_hip (crocoddyl_amd/lib). All numerical work runs on the GPU.
+#ifndef CROCODDYL_AMD_SOLVER_FDDP_HIP_HPP_
+#define CROCODDYL_AMD_SOLVER_FDDP_HIP_HPP_
+
+#include <cmath>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../fddp_hip.h"
+
+namespace crocoddyl_amd {
+
+struct Exception : std::runtime_error {
+  explicit Exception(const std::string& m) : std::runtime_error(m) {}
+};
+
+inline void check(int rc, const char* what) {
+  if (rc != FDDP_OK) throw Exception(std::string(what) + ": " + fddp_last_error());
+}
+
+typedef std::vector<double> VectorXd;  // column vectors / column-major matrices
+
+template <class V>
+inline VectorXd to_vec(const V& v) {
+  return VectorXd(v.data(), v.data() + v.size());
+}
+
+// Parameter carriers with the reference defaults. pack() appends this
+// model's block (layout: include/fddp_hip.h) to `pool`.
+struct ActionModelBase {
+  virtual ~ActionModelBase() {}
+  virtual int kind() const = 0;
+  virtual int nx() const = 0;
+  virtual int nu() const = 0;
+  virtual void pack(VectorXd& pool) const = 0;
+};
+
+inline VectorXd eye(int r, int c) {
+  VectorXd m((size_t)r * c, 0.);
+  for (int i = 0; i < r && i < c; ++i) m[(size_t)i * r + i] = 1.;
+  return m;
+}
+
+struct ActionModelLQR : ActionModelBase {  // lqr.hxx:13-25
+  int nx_, nu_;
+  bool drift_free;
+  VectorXd Fx, Fu, f0, Lxx, Lxu, Luu, lx, lu;
+  ActionModelLQR(int nx, int nu, bool drift_free_ = true)
+      : nx_(nx), nu_(nu), drift_free(drift_free_), Fx(eye(nx, nx)), Fu(eye(nx, nu)), f0(nx, 1.), Lxx(eye(nx, nx)),
+        Lxu(eye(nx, nu)), Luu(eye(nu, nu)), lx(nx, 1.), lu(nu, 1.) {}
+  int kind() const { return FDDP_KNOT_LQR; }
+  int nx() const { return nx_; }
+  int nu() const { return nu_; }
+  void pack(VectorXd& p) const {
+    const double hdr[FDDP_PARAM_HEADER] = {drift_free ? 1. : 0., 0., 0., 0.};
+    p.insert(p.end(), hdr, hdr + FDDP_PARAM_HEADER);
+    for (const VectorXd* v : {&Fx, &Fu, &f0, &Lxx, &Lxu, &Luu, &lx, &lu}) p.insert(p.end(), v->begin(), v->end());
+  }
+};
+
+struct ActionModelUnicycle : ActionModelBase {  // unicycle.hxx:13-16
+  double dt = 0.1, wx = 10., wu = 1.;
+  int kind() const { return FDDP_KNOT_UNICYCLE; }
+  int nx() const { return 3; }
+  int nu() const { return 2; }
+  void pack(VectorXd& p) const {
+    const double hdr[FDDP_PARAM_HEADER] = {dt, wx, wu, 0.};
+    p.insert(p.end(), hdr, hdr + FDDP_PARAM_HEADER);
+  }
+};
+
+struct DifferentialActionModelLQR {  // diff-lqr.hxx:14-28
+  int nq, nu;
+  bool drift_free;
+  VectorXd Fq, Fv, Fu, f0, Lxx, Lxu, Luu, lx, lu;
+  DifferentialActionModelLQR(int nq_, int nu_, bool drift_free_ = true)
+      : nq(nq_), nu(nu_), drift_free(drift_free_), Fq(eye(nq_, nq_)), Fv(eye(nq_, nq_)), Fu(eye(nq_, nu_)),
+        f0(nq_, 1.), Lxx(eye(2 * nq_, 2 * nq_)), Lxu(eye(2 * nq_, nu_)), Luu(eye(nu_, nu_)), lx(2 * nq_, 1.),
+        lu(nu_, 1.) {}
+};
+
+struct IntegratedActionModelEuler : ActionModelBase {  // euler.hxx:16-35
+  std::shared_ptr<DifferentialActionModelLQR> differential;
+  double dt;
+  IntegratedActionModelEuler(std::shared_ptr<DifferentialActionModelLQR> d, double time_step = 1e-3)
+      : differential(d), dt(time_step < 0. ? 1e-3 : time_step) {}
+  int kind() const { return FDDP_KNOT_EULER_DIFFLQR; }
+  int nx() const { return 2 * differential->nq; }
+  int nu() const { return differential->nu; }
+  void pack(VectorXd& p) const {
+    const DifferentialActionModelLQR& d = *differential;
+    const double hdr[FDDP_PARAM_HEADER] = {dt, d.drift_free ? 1. : 0., 0., 0.};
+    p.insert(p.end(), hdr, hdr + FDDP_PARAM_HEADER);
+    for (const VectorXd* v : {&d.Fq, &d.Fv, &d.Fu, &d.f0, &d.Lxx, &d.Lxu, &d.Luu, &d.lx, &d.lu})
+      p.insert(p.end(), v->begin(), v->end());
+  }
+};
+
+// ShootingProblem over one problem (B = 1) or B problems sharing the models
+// (x0s of size B*nx).
+class ShootingProblem {
+ public:
+  template <class V>
+  ShootingProblem(const V& x0, const std::vector<std::shared_ptr<ActionModelBase> >& running,
+                  std::shared_ptr<ActionModelBase> terminal, int batch = 1)
+      : x0_(to_vec(x0)), running_(running), terminal_(terminal), B_(batch) {
+    if (running.empty()) throw Exception("Invalid argument: no running models");
+    nx_ = running[0]->nx();
+    nu_max_ = 0;
+    for (size_t i = 0; i < running.size(); ++i) {  // shooting.hxx:28-49
+      if (running[i]->nx() != nx_) throw Exception("Invalid argument: nx in " + std::to_string(i) + " node is not consistent");
+      if (running[i]->nu() > nu_max_) nu_max_ = running[i]->nu();
+    }
+    if (terminal->nx() != nx_) throw Exception("Invalid argument: nx in terminal node is not consistent");
+    if ((int)x0_.size() != nx_ * B_) throw Exception("Invalid argument: x0 has wrong dimension");
+  }
+  int get_T() const { return (int)running_.size(); }
+  int get_nx() const { return nx_; }
+  int get_ndx() const { return nx_; }
+  int get_nu_max() const { return nu_max_; }
+  int get_B() const { return B_; }
+  const VectorXd& get_x0() const { return x0_; }
+  template <class V>
+  void set_x0(const V& x0) {  // shooting.hxx:391-397
+    VectorXd v = to_vec(x0);
+    if ((int)v.size() != nx_ * B_) throw Exception("Invalid argument: x0 has wrong dimension");
+    x0_ = v;
+  }
+  // knot descriptors + pool (shared models packed once)
+  void pack(std::vector<fddp_knot_desc>& knots, VectorXd& pool) const {
+    std::vector<const ActionModelBase*> seen;
+    std::vector<int64_t> offs;
+    knots.clear();
+    pool.clear();
+    for (int t = 0; t <= get_T(); ++t) {
+      const ActionModelBase* m = t < get_T() ? running_[t].get() : terminal_.get();
+      int64_t off = -1;
+      for (size_t i = 0; i < seen.size(); ++i)
+        if (seen[i] == m) off = offs[i];
+      if (off < 0) {
+        off = (int64_t)pool.size();
+        m->pack(pool);
+        seen.push_back(m);
+        offs.push_back(off);
+      }
+      fddp_knot_desc d;
+      d.kind = m->kind();
+      d.nu = m->nu();
+      d.param_offset = off;
+      d.param_stride = 0;
+      knots.push_back(d);
+    }
+  }
+
+ private:
+  VectorXd x0_;
+  std::vector<std::shared_ptr<ActionModelBase> > running_;
+  std::shared_ptr<ActionModelBase> terminal_;
+  int nx_, nu_max_, B_;
+};
+
+// SolverFDDP (fddp.hpp:50-101) on the GPU.
+class SolverFDDP {
+ public:
+  explicit SolverFDDP(std::shared_ptr<ShootingProblem> problem, int device = 0) : problem_(problem) {
+    std::vector<fddp_knot_desc> knots;
+    VectorXd pool;
+    problem->pack(knots, pool);
+    fddp_dims d;
+    d.nx = problem->get_nx();
+    d.ndx = problem->get_ndx();
+    d.nu_max = problem->get_nu_max();
+    d.T = problem->get_T();
+    d.B = problem->get_B();
+    dims_ = d;
+    fddp_handle* h = nullptr;
+    check(fddp_create(&d, knots.data(), pool.data(), (int64_t)pool.size(), device, &h), "fddp_create");
+    h_.reset(h, fddp_destroy);
+    fddp_default_params(&params_);
+    check(fddp_set_x0(h, problem->get_x0().data()), "fddp_set_x0");
+    res_.resize(d.B);
+  }
+
+  // fddp.cpp:19-105 ; init vectors empty => state.zero() / zeros (solver-base.cpp:46-65)
+  template <class V = VectorXd>
+  bool solve(const std::vector<V>& init_xs = std::vector<V>(), const std::vector<V>& init_us = std::vector<V>(),
+             std::size_t maxiter = 100, bool is_feasible = false, double reginit = 1e-9) {
+    setCandidate(init_xs, init_us, is_feasible);
+    check(fddp_set_x0(h_.get(), problem_->get_x0().data()), "fddp_set_x0");
+    check(fddp_set_params(h_.get(), &params_), "fddp_set_params");
+    check(fddp_solve(h_.get(), (int)maxiter, is_feasible ? 1 : 0, reginit, res_.data()), "fddp_solve");
+    return res_[0].status == FDDP_STATUS_CONVERGED;
+  }
+
+  template <class V>
+  void setCandidate(const std::vector<V>& xs_warm, const std::vector<V>& us_warm, bool is_feasible) {
+    const int T = dims_.T, nx = dims_.nx, nu = dims_.nu_max, B = dims_.B;
+    VectorXd xs, us;
+    if (!xs_warm.empty()) {
+      if ((int)xs_warm.size() != T + 1) throw Exception("Warm start state has wrong dimension");
+      for (int b = 0; b < B; ++b)
+        for (const V& x : xs_warm) xs.insert(xs.end(), x.data(), x.data() + nx);
+    }
+    if (!us_warm.empty()) {
+      if ((int)us_warm.size() != T) throw Exception("Warm start control has wrong dimension");
+      for (int b = 0; b < B; ++b)
+        for (const V& u : us_warm) {
+          VectorXd row(nu, 0.);
+          for (int i = 0; i < (int)u.size() && i < nu; ++i) row[i] = u.data()[i];
+          us.insert(us.end(), row.begin(), row.end());
+        }
+    }
+    check(fddp_set_candidate(h_.get(), xs.empty() ? nullptr : xs.data(), us.empty() ? nullptr : us.data(),
+                             is_feasible ? 1 : 0),
+          "fddp_set_candidate");
+  }
+
+  std::vector<VectorXd> get_xs() const {  // element 0 (B = 1: the problem)
+    VectorXd a((size_t)dims_.B * (dims_.T + 1) * dims_.nx);
+    check(fddp_get_xs(h_.get(), a.data(), 0), "fddp_get_xs");
+    std::vector<VectorXd> out;
+    for (int t = 0; t <= dims_.T; ++t) out.push_back(VectorXd(a.begin() + t * dims_.nx, a.begin() + (t + 1) * dims_.nx));
+    return out;
+  }
+  std::vector<VectorXd> get_us() const {
+    VectorXd a((size_t)dims_.B * dims_.T * dims_.nu_max);
+    check(fddp_get_us(h_.get(), a.data(), 0), "fddp_get_us");
+    std::vector<VectorXd> out;
+    for (int t = 0; t < dims_.T; ++t)
+      out.push_back(VectorXd(a.begin() + t * dims_.nu_max, a.begin() + (t + 1) * dims_.nu_max));
+    return out;
+  }
+  const std::vector<fddp_result>& get_results() const { return res_; }  // per batch element
+  double get_cost() const { return res_[0].cost; }
+  double get_stop() const { return res_[0].stop; }
+  std::size_t get_iter() const { return (std::size_t)res_[0].iter; }
+  double get_xreg() const { return res_[0].xreg; }
+  double get_ureg() const { return res_[0].ureg; }
+  double get_steplength() const { return res_[0].steplength; }
+  bool get_is_feasible() const { return res_[0].is_feasible != 0; }
+
+  // thresholds with the reference setter validation (enforced by fddp_set_params)
+  void set_th_stop(double v) { params_.th_stop = v; push(); }
+  void set_th_acceptstep(double v) { params_.th_acceptstep = v; push(); }
+  void set_th_acceptnegstep(double v) { params_.th_acceptnegstep = v; push(); }
+  void set_th_grad(double v) { params_.th_grad = v; push(); }
+  void set_th_stepdec(double v) { params_.th_stepdec = v; push(); }
+  void set_th_stepinc(double v) { params_.th_stepinc = v; push(); }
+  void set_regfactor(double v) { params_.regfactor = v; push(); }
+  void set_regmin(double v) { params_.regmin = v; push(); }
+  void set_regmax(double v) { params_.regmax = v; push(); }
+  double get_th_stop() const { return params_.th_stop; }
+  fddp_handle* handle() const { return h_.get(); }
+
+ private:
+  void push() {
+    const int rc = fddp_set_params(h_.get(), &params_);
+    if (rc != FDDP_OK) {
+      fddp_get_params(h_.get(), &params_);  // keep the last valid thresholds
+      throw Exception(std::string("Invalid argument: ") + fddp_last_error());
+    }
+  }
+  std::shared_ptr<ShootingProblem> problem_;
+  std::shared_ptr<fddp_handle> h_;
+  fddp_dims dims_;
+  fddp_params params_;
+  std::vector<fddp_result> res_;
+};
+
+}  // namespace crocoddyl_amd
+
+#endif  // CROCODDYL_AMD_SOLVER_FDDP_HIP_HPP_

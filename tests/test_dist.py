@@ -1,0 +1,87 @@
+"""World-size-2 gloo test of the batch-sharded path (CPU): each rank solves
+its shard (the CPU oracle stands in for the GPU solver here), the results are
+all-gathered with the same helper bench.py uses, and rank 0 checks them
+against solving every shard in one process. Also checks the job-time
+reduction (max over ranks) and work sum."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _shard_problem(rank):
+    import helpers
+    return helpers.setup("C2_lqr", T=6, B=3, seed=1234 + rank)
+
+
+def _worker(rank, ws, port, q):
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, HERE)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(ws), RANK=str(rank),
+                      LOCAL_RANK=str(rank))
+    import torch
+
+    import oracle_lib
+    from crocoddyl_amd import dist as cdist
+
+    cdist.init("gloo")
+    S = _shard_problem(rank)
+    o = oracle_lib.Oracle(S["dims"], S["knots"], S["pool"], S["x0s"])
+    o.set_candidate(None, None, False)
+    r = o.solve(maxiter=10)
+    xs = torch.from_numpy(o.xs())
+    allxs = cdist.gather_rows(xs)
+    t, w = cdist.job_time_and_work(0.5 + rank, sum(x.n_iter_run for x in r), "cpu")
+    if rank == 0:
+        q.put((allxs.numpy(), t, w))
+    torch.distributed.barrier()
+    torch.distributed.destroy_process_group()
+
+
+def test_shard_bounds():
+    from crocoddyl_amd.dist import shard
+    for bg in (1, 7, 8, 1024, 8192):
+        for ws in (1, 2, 4, 8):
+            spans = [shard(bg, ws, r) for r in range(ws)]
+            assert sum(c for _, c in spans) == bg
+            assert all(spans[i][0] + spans[i][1] == spans[i + 1][0] for i in range(ws - 1))
+            assert max(c for _, c in spans) - min(c for _, c in spans) <= 1
+
+
+def test_world2_gloo_gather_matches_single_process():
+    import oracle_lib
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    allxs, t, w = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ref = []
+    iters = 0
+    for rank in range(2):
+        S = _shard_problem(rank)
+        o = oracle_lib.Oracle(S["dims"], S["knots"], S["pool"], S["x0s"])
+        o.set_candidate(None, None, False)
+        iters += sum(x.n_iter_run for x in o.solve(maxiter=10))
+        ref.append(o.xs())
+    np.testing.assert_array_equal(allxs, np.concatenate(ref))
+    assert t == pytest.approx(1.5)
+    assert w == iters
