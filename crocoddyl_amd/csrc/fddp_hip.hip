@@ -412,9 +412,13 @@ int fddp_create(const fddp_dims* dims, const fddp_knot_desc* knots, const double
   D.sMM = pad2((int64_t)d.nu_max * d.nu_max > 0 ? (int64_t)d.nu_max * d.nu_max : 1);
   const int64_t B = d.B, K1 = (int64_t)d.T + 1, K0 = d.T;
 
-  h->bwd_smem = BwdSmem::bytes(D.n, D.m);
-  if (h->bwd_smem > 160 * 1024)
-    return bail(fail(FDDP_ERR_UNSUPPORTED, "fddp_create: (ndx, nu_max) too large for the LDS-resident Riccati sweep"));
+  h->bwd_smem = BwdSmem::bytes(D.n, D.m, false);
+  if (h->bwd_smem > 160 * 1024) {
+    h->bwd_smem = BwdSmem::bytes(D.n, D.m, true);
+    if (h->bwd_smem > 160 * 1024)
+      return bail(fail(FDDP_ERR_UNSUPPORTED, "fddp_create: (ndx, nu_max) too large for the Riccati sweep"));
+    if ((rc = dalloc(h, &D.bwork, (int64_t)d.B * BwdSmem::work_doubles(D.n, D.m)))) return bail(rc);
+  }
   {
     int64_t pmax = 0;
     for (int t = 0; t <= d.T; ++t) pmax = std::max<int64_t>(pmax, block_doubles(knots[t].kind, d.nx, knots[t].nu));

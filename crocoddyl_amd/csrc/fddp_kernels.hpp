@@ -218,11 +218,20 @@ __global__ __launch_bounds__(NT) void calc_diff_kernel(Dev D, int sel, int gaps,
 struct BwdSmem {
   double *V, *A, *BU, *Qxu, *Quu, *L, *vx, *qx, *qu, *kv, *quuk, *fsv, *vf, *red;
   int* flag;
-  __device__ BwdSmem(double* sm, int n, int m) {
+  // gwork != null: FxT Vxx' (A) and FuT Vxx' (BU) live in this element's
+  // global workspace instead of LDS (large n, m).
+  __device__ BwdSmem(double* sm, int n, int m, double* gwork) {
     V = sm;
-    A = V + n * n;
-    BU = A + n * n;
-    Qxu = BU + pad2(m * n);
+    double* next = V + n * n;
+    if (gwork) {
+      A = gwork;
+      BU = gwork + n * n;
+    } else {
+      A = next;
+      BU = A + n * n;
+      next = BU + pad2(m * n);
+    }
+    Qxu = next;
     Quu = Qxu + pad2(n * m);
     L = Quu + pad2(m * m);
     vx = L + pad2(m * m);
@@ -235,10 +244,11 @@ struct BwdSmem {
     red = vf + pad2(n);
     flag = (int*)(red + 64);
   }
-  __host__ static size_t bytes(int n, int m) {
-    return sizeof(double) * (2 * n * n + pad2(m * n) + pad2(n * m) + 2 * pad2(m * m) + 4 * pad2(n) + 3 * pad2(m) +
-                             64 + 2);
+  __host__ static size_t bytes(int n, int m, bool global_work) {
+    const size_t work = global_work ? 0 : (size_t)(n * n + pad2(m * n));
+    return sizeof(double) * (n * n + work + pad2(n * m) + 2 * pad2(m * m) + 4 * pad2(n) + 3 * pad2(m) + 64 + 2);
   }
+  __host__ __device__ static int64_t work_doubles(int n, int m) { return (int64_t)n * n + pad2(m * n); }
 };
 
 template <int NT>
@@ -449,7 +459,7 @@ __global__ __launch_bounds__(NT) void backward_kernel(Dev D, Prm prm, int mode) 
   ElemState* st = D.st + b;
   if (mode == 0 && !st->active) return;
   extern __shared__ __attribute__((aligned(16))) double sm[];
-  BwdSmem S(sm, D.n, D.m);
+  BwdSmem S(sm, D.n, D.m, D.bwork ? D.bwork + (int64_t)b * BwdSmem::work_doubles(D.n, D.m) : nullptr);
   const bool feas = st->is_feasible != 0;
   double xreg = st->xreg, ureg = st->ureg;
   bool ok;
