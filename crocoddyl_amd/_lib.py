@@ -10,7 +10,7 @@ import os
 from . import _abi
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libfddp_hip.so")
+LIB_PATH = os.environ.get("CROCODDYL_AMD_LIB") or os.path.join(_HERE, "lib", "libfddp_hip.so")
 
 _lib = None
 

@@ -3,18 +3,35 @@
 // Same computation as bwd_sweep (SolverDDP::backwardPass + computeGains,
 // src/core/solvers/ddp.cpp:180-253, 298-310), reorganised for gfx950:
 //
-//   Z  = [Fx | Fu]                 (n x (n+m), streamed from HBM per knot)
+//   Z  = [Fx | Fu]                 (n x (n+m), staged in LDS by LDS-DMA)
 //   G  = Vxx' Z                    (MFMA; Vxx' LDS-resident)
 //   H  = G^T Z + [Lxx Lxu; . Luu]  = [[Qxx, Qxu], [Qux, Quu]]   (MFMA; the G
 //        accumulators are the A operands of H with no data movement:
 //        accumulator register r holds rows 4r..4r+3 of a 16-row block, which
 //        is exactly the k-slice of one 16x16x4 step; Vxx' is symmetric so
 //        G^T = Z^T Vxx' = Fx^T Vxx' as the reference forms it)
-//   Quu^-1 from a Cholesky factorisation (wave 0, overlapped with the Qxx /
-//        Qxu tiles of waves 1-3); a pivot <= 0 is the reference's LLT failure
-//   K  = Quu^-1 Qxu^T, k = Quu^-1 Qu (MFMA / VALU)
-//   Vxx = Qxx - Qxu K (+ xreg I), written symmetric (upper tile mirrored)
+//   Qx = Lx + Fx^T Vx', Qu = Lu + Fu^T Vx'  (VALU, folded into the G loop: the
+//        lane already holds the Z fragment)
+//   Quu^-1 by a symmetric sweep (Gauss-Jordan) on wave 0, overlapped with the
+//        Qxx/Qxu tiles of waves 1-3; a pivot <= 0 is the reference's LLT failure
+//   K  = Quu^-1 Qxu^T (MFMA), k = Quu^-1 Qu (VALU)
+//   Vxx = Qxx - K^T Qxu^T (+ xreg I), written symmetric; the owner of x block
+//        i keeps its K(:, i) tiles in registers and finds its Qxx(i, :) tiles
+//        in the (dead) Vxx' buffer, updating them in place
 //   Vx  = Qx + K^T Quu k - 2 K^T Qu (+ Vxx fs)
+//
+// Pipeline per knot t:
+//   P1  the knot's cost blocks (Lxx, Lxu, Luu) are loaded into registers in
+//       accumulator layout; G (LDS only) covers their latency; B0; then H,
+//       Qx/Qu ; wave 0: Quu^-1
+//   B1  -> an LDS-DMA of Fx, Fu, Lx, Lu of knot t-1 is issued; it lands
+//       while P2/P3 run (raw s_barrier, no vmcnt wait until B3).
+//       fs of knot t-1 follows right after B3 (its buffer is read in P3).
+//   P2  K, V update (waves 1-3); k, Quu k (wave 0)
+//   B2
+//   P3  Vx, Vxx fs, reduction terms
+//   B3  vmcnt(0) + barrier: the knot t-1 operands are resident.
+// (4 barriers per knot in all.)
 //
 // One workgroup (4 waves, one per SIMD) per batch element; the element's
 // horizon is swept serially. n and m are padded to 16-multiples (NTL, MTL
@@ -28,113 +45,632 @@
 namespace fddp {
 
 typedef double f64x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void* lds_void_ptr;
+
+// 1/d from v_rcp_f64 and Newton steps (the IEEE division sequence is ~3x
+// longer on the sweep's critical path; dependent f64 FMA latency is 32 cycles)
+__device__ __forceinline__ double rcp_f64(double d) {
+  double x = __builtin_amdgcn_rcp(d);
+  x = fma(fma(-d, x, 1.), x, x);
+#ifndef FDDP_RCP_ONE_NEWTON
+  x = fma(fma(-d, x, 1.), x, x);
+#endif
+  return x;
+}
 
 __device__ __forceinline__ f64x4 mfma4(double a, double b, f64x4 c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
 
-// Column blocks of Z owned by each wave (computed on the host, LPT).
-struct BwdSched {
-  int32_t nown[4];
-  int32_t blk[4][4];
-  int32_t jstart[4][4];
-};
+// Barrier that waits only for this wave's LDS traffic: an LDS-DMA in flight
+// stays in flight across it (a __syncthreads() would add vmcnt(0)).
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+// Barrier after which every LDS-DMA issued by the workgroup has landed.
+__device__ __forceinline__ void dma_barrier() {
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// Asynchronous copy global -> LDS by LDS-DMA (global_load_lds: the LDS
+// destination of one wave instruction is a wave-uniform base + lane * size).
+// dma_vec: nd contiguous doubles (16-B aligned both sides) over the 4 waves;
+// an odd tail double moves as two 4-byte DMAs.
+__device__ __forceinline__ void dma_vec(double* lds, const double* g, int nd, int wid, int lane) {
+  const int nch = nd >> 1;
+  for (int base = wid * 64; base < nch; base += 256) {
+    const int ch = base + lane;
+    if (ch < nch) __builtin_amdgcn_global_load_lds(g + 2 * ch, (lds_void_ptr)(lds + 2 * base), 16, 0, 0);
+  }
+  if ((nd & 1) && wid == 3 && lane < 2)
+    __builtin_amdgcn_global_load_lds((const char*)(g + nd - 1) + 4 * lane, (lds_void_ptr)(lds + nd - 1), 4, 0, 0);
+}
+// dma_cols: ncols columns of nr doubles (global ld nr) into LDS columns of
+// stride ld (a multiple of 2); one column per wave instruction (16-B chunks
+// when nr is even, else 4-byte pieces). Rows [nr, ld) are left untouched.
+__device__ __forceinline__ void dma_cols(double* lds, int ld, const double* g, int nr, int ncols, int wid, int lane) {
+  if ((nr & 1) == 0) {
+    const int nch = nr >> 1;
+    for (int col = wid; col < ncols; col += 4)
+      for (int base = 0; base < nch; base += 64)
+        if (base + lane < nch)
+          __builtin_amdgcn_global_load_lds(g + (int64_t)col * nr + 2 * (base + lane),
+                                           (lds_void_ptr)(lds + col * ld + 2 * base), 16, 0, 0);
+  } else {
+    const int nw = 2 * nr;
+    for (int col = wid; col < ncols; col += 4)
+      for (int base = 0; base < nw; base += 64)
+        if (base + lane < nw)
+          __builtin_amdgcn_global_load_lds((const char*)(g + (int64_t)col * nr) + 4 * (base + lane),
+                                           (lds_void_ptr)((char*)(lds + col * ld) + 4 * base), 4, 0, 0);
+  }
+}
 
 template <int NTL, int MTL>
 struct MfmaCfg {
   static constexpr int NP = 16 * NTL;
   static constexpr int MP = 16 * MTL;
   static constexpr int JT = NTL + MTL;
-  // leading dimensions = 16 (mod 32) doubles: the two 16-lane halves of a
-  // ds_read_b64 fragment read land on disjoint bank halves
+  // V / Qxu leading dimension = 16 (mod 32) doubles: the two 16-lane halves
+  // of a ds_read_b64 fragment read land on disjoint bank halves
   static constexpr int LDV = (NP % 32 == 0) ? NP + 16 : NP;
-  static constexpr int LDQ = (MP % 32 == 0) ? MP + 16 : MP;
-  static constexpr int NQXX = NTL * (NTL + 1) / 2;
-  static constexpr int MAXOWN = (MTL > (NTL + 2) / 3) ? MTL : (NTL + 2) / 3;
+  static constexpr int LDQ = MP;
   static_assert(MP <= 64, "u block must fit one wave for the factorisation");
-  // LDS carve (doubles)
+  // LDS carve (doubles). Z = [Fx | Fu] is stored with the compile-time
+  // column stride NP (zero rows/cols beyond n, m) so that every fragment
+  // address is a per-lane base plus an immediate offset.
   static constexpr int oV = 0;
-  static constexpr int oQxx = oV + LDV * NP;
-  static constexpr int oQxu = oQxx + NQXX * 256;
+  static constexpr int oQxu = oV + LDV * NP;
   static constexpr int oQuu = oQxu + LDV * MP;
   static constexpr int oQi = oQuu + LDQ * MP;
-  static constexpr int oKT = oQi + LDQ * MP;  // also the Cholesky factor during phase 1
-  static constexpr int oVec = oKT + (LDV * MP > LDQ * MP ? LDV * MP : LDQ * MP);
-  static constexpr int oVx = oVec;
+  static constexpr int oVx = oQi + LDQ * MP;
   static constexpr int oQx = oVx + NP;
-  static constexpr int oFs = oQx + NP;
-  static constexpr int oVf = oFs + NP;
-  static constexpr int oQu = oVf + NP;
-  static constexpr int oKv = oQu + MP;
+  static constexpr int oLx = oQx + NP;
+  static constexpr int oFs = oLx + NP;
+  static constexpr int oQu = oFs + NP;
+  static constexpr int oLu = oQu + MP;
+  static constexpr int oKv = oLu + MP;  // kv + quuk: the sweep's 64-double row buffer (wave 0, P1)
   static constexpr int oQuuk = oKv + MP;
-  static constexpr int oCol = oQuuk + MP;
-  static constexpr int oDinv = oCol + MP;
-  static constexpr int oRed = oDinv + MP;
-  static constexpr int oFlag = oRed + 64;
-  static constexpr int total = oFlag + 2;
+  static constexpr int oRed = oKv + (2 * MP > 64 ? 2 * MP : 64);  // 5 sums x 4 waves
+  static constexpr int oFlag = oRed + 20;
+  static constexpr int oZx = (oFlag + 2 + 1) & ~1;
+  static constexpr int oZu = oZx + NP * NP;
+  static constexpr int total = oZu + NP * MP;
   static constexpr size_t bytes = sizeof(double) * total;
 };
 
-template <int NTL, int MTL>
-__device__ __forceinline__ double zfrag(const double* __restrict__ Fx, const double* __restrict__ Fu, int n, int m,
-                                        int s, int j, int q, int c) {
-  const int row = 4 * s + q;
-  if (j < NTL) {
-    const int col = 16 * j + c;
-    return (row < n && col < n) ? Fx[(int64_t)col * n + row] : 0.;
-  }
-  const int col = 16 * (j - NTL) + c;
-  return (row < n && col < m) ? Fu[(int64_t)col * n + row] : 0.;
-}
-
-// Diagnostic phase timer (FDDP_STAMPS=1): per wave, cycles spent per phase.
+// Diagnostic phase timer (built with -DFDDP_STAMPS_BUILD, enabled by
+// FDDP_STAMPS=1): per wave, core cycles spent per phase, accumulated in
+// registers (a global read-modify-write per mark would drain the LDS-DMA in
+// flight) and flushed at the end of the sweep. Compiled out otherwise.
 struct Stamp {
+#ifdef FDDP_STAMPS_BUILD
   unsigned long long* out;
   unsigned long long t0;
-  __device__ Stamp(unsigned long long* o) : out(o), t0(o ? __builtin_amdgcn_s_memtime() : 0) {}
+  unsigned long long acc[8];
+  __device__ Stamp(unsigned long long* o) : out(o), t0(__builtin_amdgcn_s_memtime()), acc{} {}
   __device__ __forceinline__ void mark(int ph) {
-    if (out) {
-      const unsigned long long t = __builtin_amdgcn_s_memtime();
-      if ((threadIdx.x & 63) == 0) out[ph] += t - t0;
-      t0 = t;
+    const unsigned long long t = __builtin_amdgcn_s_memtime();
+    acc[ph] += t - t0;
+    t0 = t;
+  }
+  __device__ __forceinline__ void flush() {
+    if (out && (threadIdx.x & 63) == 0)
+      for (int i = 0; i < 8; ++i) out[i] += acc[i];
+  }
+#else
+  __device__ Stamp(unsigned long long*) {}
+  __device__ __forceinline__ void mark(int) {}
+  __device__ __forceinline__ void flush() {}
+#endif
+};
+
+// Quu^-1 by the symmetric sweep operator on one wave (Gauss-Jordan without
+// pivoting, which SPD matrices do not need). Pivot k is the k-th Schur
+// complement = L(k,k)^2 of the Cholesky factor, so `pivot <= 0` is exactly
+// Eigen LLT's failure (ddp.cpp:300-304); after sweeping every pivot the
+// matrix holds -Quu^-1. Lane l owns column jc = l % MP and rows h*RPL + r
+// (h = l / MP). Returns true if a pivot was not positive.
+// Fully unrolled so that the pivot register A[k % RPL] is static. Every lane
+// publishes one register per step (rb[lane], unconditionally, so the step
+// stays one basic block): the lanes of row group k / RPL publish row k, which
+// by symmetry doubles as column k. The next step's row is updated and
+// published first, so its LDS round trip overlaps the rest of this step's
+// updates. No s_waitcnt is needed: one wave's LDS accesses execute in order;
+// the empty asm fences only stop the compiler from forwarding a lane's own
+// write to its reads. Quu / Qi: column-major, leading dimension LDQ; rb: 64
+// doubles of LDS.
+template <int MP, int LDQ>
+__device__ __forceinline__ bool sym_sweep_inverse(const double* Quu, double* Qi, double* rb, int m, int lane) {
+  constexpr int RPL = MP * MP / 64;
+  static_assert(MP * MP % 64 == 0 && 64 % MP == 0, "sweep lane layout");
+  const int jc = lane % MP, h = lane / MP;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  double A[RPL];
+#pragma unroll
+  for (int r = 0; r < RPL; ++r) A[r] = Quu[(h * RPL + r) * LDQ + jc];
+  bool bad = false;
+  rb[lane] = A[0];
+#pragma unroll
+  for (int k = 0; k < MP; ++k) {
+    if (k < m) {
+      const int hk = k / RPL, rk = k % RPL;
+      const int r1 = (k + 1) % RPL;
+      asm volatile("" ::: "memory");
+      // step k's broadcast operands: pivot d = A(k, k), A(k, jc), row k at
+      // rows h*RPL + r (= column k by symmetry)
+      const double d = rb[hk * MP + k];
+      const double akj = rb[hk * MP + jc];
+      double ak[RPL];
+#pragma unroll
+      for (int r = 0; r < RPL; ++r) ak[r] = rb[hk * MP + h * RPL + r];
+      bad |= !(d > 0.);
+      const bool colk = jc == k;
+      // next step's row first, with the dependent chain kept short
+      // (A - (a_ik a_kj) * (1/d): the product does not wait for 1/d), then
+      // published so its LDS round trip overlaps this step's other updates
+      const double p1 = ak[r1] * akj;
+      const double dinv = rcp_f64(d);
+      {
+        const double u = colk ? ak[r1] * dinv : fma(-p1, dinv, A[r1]);
+        A[r1] = (r1 == rk && h == hk) ? (colk ? -dinv : akj * dinv) : u;
+      }
+      asm volatile("" ::: "memory");
+      rb[lane] = A[r1];
+      __builtin_amdgcn_sched_barrier(0);
+      // the rest: one FMA per element on every lane, then the lane(s) owning
+      // column k (exec-masked) overwrite theirs with A(i, k) / d, and row k's
+      // register becomes A(k, jc) / d (-1/d at (k, k))
+      const double w = akj * dinv;
+#pragma unroll
+      for (int r = 0; r < RPL; ++r)
+        if (r != r1) A[r] = fma(-ak[r], w, A[r]);
+      if (colk) {
+#pragma unroll
+        for (int r = 0; r < RPL; ++r)
+          if (r != r1) A[r] = ak[r] * dinv;
+      }
+      if (rk != r1 && h == hk) A[rk] = colk ? -dinv : w;
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < RPL; ++r) {
+    const int i = h * RPL + r;
+    Qi[i * LDQ + jc] = (i < m && jc < m) ? -A[r] : 0.;
+  }
+  return bad;
+}
+
+// Compile-time ownership of Z's column blocks: wave 0 takes the u blocks
+// (Quu and its inverse), waves 1-3 share the x blocks by longest-processing-
+// time on their MFMA count (G: 4NTL x NTL, H tiles j >= i: 4NTL each). With
+// the plan static, every wave's code path has only its own tiles, statically
+// indexed registers and no per-tile predicates.
+template <int NTL, int MTL>
+struct BwdPlan {
+  int nown[4];
+  int blk[4][8];
+  constexpr BwdPlan() : nown{0, 0, 0, 0}, blk{} {
+    for (int u = 0; u < MTL; ++u) blk[0][nown[0]++] = NTL + u;
+    int load[4] = {0, 0, 0, 0};
+    for (int i = 0; i < NTL; ++i) {  // the cost decreases with i: LPT order
+      int best = 1;
+      for (int w = 2; w < 4; ++w)
+        if (load[w] < load[best]) best = w;
+      blk[best][nown[best]++] = i;
+      load[best] += NTL + (NTL - i + MTL);
     }
   }
 };
+template <int NTL>
+__host__ __device__ constexpr int bwd_jstart(int i) {
+  return i < NTL ? i : NTL;
+}
+
+// LDS carve of one workgroup (see MfmaCfg).
+struct BwdLds {
+  double *V, *Qxu, *Quu, *Qi, *vx, *qx, *lxv, *fsb, *qu, *luv, *kv, *quuk, *rowbuf, *red, *Zx, *Zu;
+  int* flag;
+};
+
+// One knot of the sweep, as executed by wave W (all four waves call this
+// with their own W; the barriers inside line up one to one).
+template <int NTL, int MTL, int W>
+__device__ __forceinline__ bool bwd_knot(const Dev& D, const BwdLds& L, int b, int t, bool feas, double xreg,
+                                         double ureg, Stamp& stamp) {
+  using Cfg = MfmaCfg<NTL, MTL>;
+  constexpr int NP = Cfg::NP, MP = Cfg::MP, JT = Cfg::JT, LDV = Cfg::LDV, LDQ = Cfg::LDQ;
+  constexpr BwdPlan<NTL, MTL> P{};
+  constexpr int NO = P.nown[W];
+  constexpr int NA = NO > 0 ? NO : 1;
+  static_assert(NO <= 8, "column blocks per wave");
+  // The lane id and the dimensions are laundered through empty asm on every
+  // knot: otherwise LICM hoists every per-lane address of the unrolled code
+  // out of the knot loop and keeps them all live (hundreds of registers).
+  int lane = threadIdx.x & 63, n = D.n, m = D.m;
+  asm volatile("" : "+v"(lane));
+  asm volatile("" : "+s"(n), "+s"(m));
+  const int q = lane >> 4, c = lane & 15;
+  const bool xr = !isnan(xreg), ur = !isnan(ureg);
+  const int64_t kk = D.knot(b, t), rr = D.run(b, t);
+  double* V = L.V;
+  double* Qxu = L.Qxu;
+  double* Quu = L.Quu;
+  double* Qi = L.Qi;
+
+  // ---- P1: cost blocks in accumulator layout (both triangles of Lxx: Qxx
+  // uses its symmetric part, which the reference reaches through its Vxx
+  // symmetrisation); their latency is covered by the G loop
+  double Lp[NA][NTL][4][2];
+  double Lq[NA][MTL][4];
+  {
+    const double* Lxx = D.Lxx + kk * D.sNN;
+    const double* Lxu = D.Lxu + kk * D.sNM;
+    const double* Luu = D.Luu + kk * D.sMM;
+#pragma unroll
+    for (int o = 0; o < NO; ++o) {
+      const int i = P.blk[W][o];
+#pragma unroll
+      for (int j = 0; j < NTL; ++j) {
+        if (j >= bwd_jstart<NTL>(i)) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int R = 16 * i + q + 4 * r, C = 16 * j + c;
+            const bool ok = R < n && C < n;
+            Lp[o][j][r][0] = ok ? Lxx[(int64_t)C * n + R] : 0.;
+            Lp[o][j][r][1] = ok ? Lxx[(int64_t)R * n + C] : 0.;
+          }
+        }
+      }
+#pragma unroll
+      for (int ju = 0; ju < MTL; ++ju)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int Cu = 16 * ju + c;
+          double v = 0.;
+          if (i < NTL) {
+            const int R = 16 * i + q + 4 * r;
+            if (R < n && Cu < m) v = Lxu[(int64_t)Cu * n + R];
+          } else {
+            const int Ru = 16 * (i - NTL) + q + 4 * r;
+            if (Ru < m && Cu < m) v = Luu[(int64_t)Cu * m + Ru];
+          }
+          Lq[o][ju][r] = v;
+        }
+    }
+  }
+  // G_o = V' Z_i (i = owned block o) and the q-partials of Z_i^T Vx'
+  f64x4 G[NA][NTL];
+  double qp[NA];
+#pragma unroll
+  for (int o = 0; o < NA; ++o) {
+    qp[o] = 0.;
+#pragma unroll
+    for (int a = 0; a < NTL; ++a) G[o][a] = f64x4{0., 0., 0., 0.};
+  }
+  // software-pipelined two k-steps ahead; sched_barriers stop the scheduler
+  // from hoisting every fragment read of the unrolled loop (register blowup)
+  double vf[3][NTL], zf[3][NA], vxf[3];
+  auto gload = [&](int s, int buf) {
+    const int row = 4 * s + q;
+#pragma unroll
+    for (int a = 0; a < NTL; ++a) vf[buf][a] = V[row * LDV + 16 * a + c];
+    vxf[buf] = L.vx[row];
+#pragma unroll
+    for (int o = 0; o < NO; ++o) {
+      const int i = P.blk[W][o];
+      zf[buf][o] = i < NTL ? L.Zx[(16 * i + c) * NP + row] : L.Zu[(16 * (i - NTL) + c) * NP + row];
+    }
+  };
+  // (rows >= n of V' are exactly zero, so the padded k-steps add nothing;
+  // running them keeps the unrolled loop branch-free)
+  if (NO > 0) {
+    gload(0, 0);
+    gload(1, 1);
+  }
+#pragma unroll
+  for (int s = 0; s < 4 * NTL; ++s) {
+    if (NO > 0) {
+      if (s + 2 < 4 * NTL) gload(s + 2, (s + 2) % 3);
+      const int cb = s % 3;
+#pragma unroll
+      for (int o = 0; o < NO; ++o) {
+        qp[o] += zf[cb][o] * vxf[cb];
+#pragma unroll
+        for (int a = 0; a < NTL; ++a) G[o][a] = mfma4(vf[cb][a], zf[cb][o], G[o][a]);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+#pragma unroll
+  for (int o = 0; o < NO; ++o) {
+    double v = qp[o];
+    v += __shfl_xor(v, 16, 64);
+    v += __shfl_xor(v, 32, 64);
+    const int i = P.blk[W][o];
+    if (q == 0) {
+      if (i < NTL) {
+        const int R = 16 * i + c;
+        L.qx[R] = R < n ? L.lxv[R] + v : 0.;
+      } else {
+        const int Ru = 16 * (i - NTL) + c;
+        L.qu[Ru] = Ru < m ? L.luv[Ru] + v : 0.;
+      }
+    }
+  }
+  stamp.mark(0);
+  lds_barrier();  // B0: every wave is done reading V'
+  // H(i, j) = G_i^T Z_j + cost block, j >= jstart(i). Qxx(i, j) goes to the
+  // dead V' buffer at the mirrored position (R, C) -> V[R * LDV + C]
+  // (conflict-free, and a lower tile that no other wave touches before this
+  // wave updates it in place in P2); Qxu / Quu tiles go to their buffers.
+  // Column j's Z fragments are read into registers while column j-1's MFMAs
+  // run (any(j) is monotone in j, so the next column always exists).
+  double zc[4 * NTL], zn[4 * NTL];
+  bool first = true;
+  auto zload = [&](double(&zz)[4 * NTL], int j) {
+#pragma unroll
+    for (int s = 0; s < 4 * NTL; ++s)
+      zz[s] = j < NTL ? L.Zx[(16 * j + c) * NP + 4 * s + q] : L.Zu[(16 * (j - NTL) + c) * NP + 4 * s + q];
+  };
+#pragma unroll
+  for (int j = 0; j < JT; ++j) {
+    bool any = false;
+#pragma unroll
+    for (int o = 0; o < NO; ++o) any = any || j >= bwd_jstart<NTL>(P.blk[W][o]);
+    if (!any) continue;
+    if (first) zload(zc, j);
+    first = false;
+    if (j + 1 < JT) zload(zn, j + 1);
+    __builtin_amdgcn_sched_barrier(0);
+    const bool isx = j < NTL;
+    const int ju = j - NTL;
+    f64x4 acc[NA];
+#pragma unroll
+    for (int o = 0; o < NO; ++o) {
+      const int i = P.blk[W][o];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        double v;
+        if (isx) {
+          v = 0.5 * (Lp[o][isx ? j : 0][r][0] + Lp[o][isx ? j : 0][r][1]);
+        } else {
+          v = Lq[o][isx ? 0 : ju][r];
+          if (ur && i >= NTL && 16 * (i - NTL) + q + 4 * r == 16 * ju + c && 16 * ju + c < m) v += ureg;
+        }
+        acc[o][r] = v;
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < 4 * NTL; ++s) {
+#pragma unroll
+      for (int o = 0; o < NO; ++o)
+        if (j >= bwd_jstart<NTL>(P.blk[W][o])) acc[o] = mfma4(G[o][s >> 2][s & 3], zc[s], acc[o]);
+    }
+#pragma unroll
+    for (int o = 0; o < NO; ++o) {
+      const int i = P.blk[W][o];
+      if (j >= bwd_jstart<NTL>(i)) {
+        if (isx) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) V[(16 * i + q + 4 * r) * LDV + 16 * j + c] = acc[o][r];
+        } else if (i < NTL) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) Qxu[(16 * ju + c) * LDV + 16 * i + q + 4 * r] = acc[o][r];
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) Quu[(16 * ju + c) * LDQ + 16 * (i - NTL) + q + 4 * r] = acc[o][r];
+        }
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < 4 * NTL; ++s) zc[s] = zn[s];
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  stamp.mark(1);
+  // ---- wave 0: Quu^-1 by the symmetric sweep (overlaps waves 1-3) ----------
+  if constexpr (W == 0) {
+    if (sym_sweep_inverse<MP, LDQ>(Quu, Qi, L.rowbuf, m, lane) && lane == 0) *L.flag = 1;
+  }
+  stamp.mark(2);
+  dma_barrier();  // B1 (also retires the fs DMA issued at the end of the last knot)
+  stamp.mark(3);
+  if (*L.flag) return false;
+  if (t > 0) {  // operands of knot t-1 land during P2/P3
+    const int64_t k1 = kk - 1;
+    dma_cols(L.Zx, NP, D.Fx + k1 * D.sNN, n, n, W, lane);
+    dma_cols(L.Zu, NP, D.Fu + k1 * D.sNM, n, m, W, lane);
+    dma_vec(L.lxv, D.Lx + k1 * D.sN, n, W, lane);
+    dma_vec(L.luv, D.Lu + k1 * D.sM, m, W, lane);
+  }
+  // ---- P2: K(:, i) = Quu^-1 Qxu(i, :)^T ; Vxx(i, j) = Qxx(i, j) - K(:, i)^T Qxu(j, :)^T
+  f64x4 Kt[NA][MTL];
+  {
+    bool bad = false;
+    double* Kg = D.K + rr * D.sNM;
+#pragma unroll
+    for (int o = 0; o < NO; ++o) {
+      const int i = P.blk[W][o];
+      if (i < NTL) {
+#pragma unroll
+        for (int it = 0; it < MTL; ++it) Kt[o][it] = f64x4{0., 0., 0., 0.};
+#pragma unroll
+        for (int s = 0; s < 4 * MTL; ++s) {
+          const double bq = Qxu[(4 * s + q) * LDV + 16 * i + c];
+#pragma unroll
+          for (int it = 0; it < MTL; ++it) Kt[o][it] = mfma4(Qi[(4 * s + q) * LDQ + 16 * it + c], bq, Kt[o][it]);
+        }
+        const int C = 16 * i + c;
+#pragma unroll
+        for (int it = 0; it < MTL; ++it)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int R = 16 * it + q + 4 * r;
+            if (R < m && C < n) Kg[(int64_t)C * m + R] = Kt[o][it][r];
+          }
+      }
+    }
+    stamp.mark(4);
+#pragma unroll
+    for (int o = 0; o < NO; ++o) {
+      const int i = P.blk[W][o];
+      if (i < NTL) {
+#pragma unroll
+        for (int j = 0; j < NTL; ++j) {
+          if (j >= i) {
+            f64x4 acc;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[r] = V[(16 * i + q + 4 * r) * LDV + 16 * j + c];  // Qxx(i, j)
+            const f64x4 qxx = acc;
+#pragma unroll
+            for (int s = 0; s < 4 * MTL; ++s)
+              acc = mfma4(-Kt[o][s >> 2][s & 3], Qxu[(4 * s + q) * LDV + 16 * j + c], acc);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int R = 16 * i + q + 4 * r, C2 = 16 * j + c;
+              double v = acc[r];
+              if (xr && R == C2 && R < n) v += xreg;
+              if (i < j || R <= C2) {
+                V[C2 * LDV + R] = v;
+                V[R * LDV + C2] = v;
+                if (R < n && C2 < n) bad |= bad_entry(v);
+              }
+            }
+            if (D.dQxx) {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const int R = 16 * i + q + 4 * r, C2 = 16 * j + c;
+                if (R < n && C2 < n) {
+                  D.dQxx[rr * D.sNN + (int64_t)C2 * n + R] = qxx[r];
+                  if (i < j) D.dQxx[rr * D.sNN + (int64_t)R * n + C2] = qxx[r];
+                }
+              }
+            }
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    }
+    if constexpr (W == 0) {  // k = Quu^-1 Qu ; Quuk = Quu k
+      if (lane < MP) {
+        double a = 0.;
+        if (lane < m)
+          for (int k2 = 0; k2 < m; ++k2) a += Qi[k2 * LDQ + lane] * L.qu[k2];
+        L.kv[lane] = a;
+        if (lane < m) D.k[rr * D.sM + lane] = a;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+      if (lane < MP) {
+        double a = 0.;
+        if (lane < m)
+          for (int k2 = 0; k2 < m; ++k2) a += Quu[k2 * LDQ + lane] * L.kv[k2];
+        L.quuk[lane] = a;
+      }
+    }
+    if (bad) *L.flag = 1;
+  }
+  stamp.mark(5);
+  lds_barrier();  // B2
+  // ---- P3: Vx = Qx + K^T Quuk - 2 K^T Qu (+ Vxx fs), reduction terms -------
+  {
+    const double* fsv = L.fsb;
+    bool bad = false;
+    double pv[5] = {0., 0., 0., 0., 0.};
+#pragma unroll
+    for (int o = 0; o < NO; ++o) {
+      const int i = P.blk[W][o];
+      if (i < NTL) {
+        const int R = 16 * i + c;
+        double a = 0., c2 = 0., f = 0.;
+#pragma unroll
+        for (int it = 0; it < MTL; ++it)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int k2 = 16 * it + 4 * r + q;
+            a += Kt[o][it][r] * L.quuk[k2];
+            c2 += Kt[o][it][r] * L.qu[k2];
+          }
+        if (!feas)
+          for (int j = q; j < n; j += 4) f += V[j * LDV + R] * fsv[j];
+        a += __shfl_xor(a, 16, 64);
+        a += __shfl_xor(a, 32, 64);
+        c2 += __shfl_xor(c2, 16, 64);
+        c2 += __shfl_xor(c2, 32, 64);
+        f += __shfl_xor(f, 16, 64);
+        f += __shfl_xor(f, 32, 64);
+        if (q == 0) {
+          double v = 0.;
+          if (R < n) {
+            v = ur ? (L.qx[R] + a) - 2 * c2 : L.qx[R] - c2;
+            if (!feas) {
+              D.Vxxfs[kk * D.sN + R] = f;
+              v += f;
+              pv[2] += v * fsv[R];
+              pv[3] += fsv[R] * f;
+            }
+            bad |= bad_entry(v);
+          }
+          L.vx[R] = v;
+        }
+      }
+    }
+    if constexpr (W == 0) {
+      if (lane < m) {
+        pv[0] = L.qu[lane] * L.kv[lane];
+        pv[1] = L.kv[lane] * L.quuk[lane];
+        pv[4] = L.qu[lane] * L.qu[lane];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+      const double s = wave_sum(pv[j]);
+      if (lane == 0) L.red[j * 4 + W] = s;
+    }
+    if (bad) *L.flag = 1;
+  }
+  stamp.mark(6);
+  dma_barrier();  // B3: knot t-1 operands resident
+  // fs of knot t-1 (read in its P3; landed by the vmcnt(0) of its B1)
+  if (t > 0) dma_vec(L.fsb, D.fs + (kk - 1) * D.sN, n, W, lane);
+  return true;
+}
 
 template <int NTL, int MTL>
-__device__ __forceinline__ bool bwd_sweep_mfma(const Dev& D, int b, bool feas, double xreg, double ureg, double* sm,
-                               const BwdSched& sch) {
+__device__ __forceinline__ bool bwd_sweep_mfma(const Dev& D, int b, bool feas, double xreg, double ureg,
+                                               double* sm) {
   using Cfg = MfmaCfg<NTL, MTL>;
-  constexpr int NP = Cfg::NP, MP = Cfg::MP, JT = Cfg::JT, LDV = Cfg::LDV, LDQ = Cfg::LDQ, MAXOWN = Cfg::MAXOWN;
-  double* V = sm + Cfg::oV;
-  double* Qxx = sm + Cfg::oQxx;
-  double* Qxu = sm + Cfg::oQxu;
-  double* Quu = sm + Cfg::oQuu;
-  double* Qi = sm + Cfg::oQi;
-  double* KT = sm + Cfg::oKT;
-  double* Lm = sm + Cfg::oKT;
-  double* vx = sm + Cfg::oVx;
-  double* qx = sm + Cfg::oQx;
-  double* fsv = sm + Cfg::oFs;
-  double* qu = sm + Cfg::oQu;
-  double* kv = sm + Cfg::oKv;
-  double* quuk = sm + Cfg::oQuuk;
-  double* colbuf = sm + Cfg::oCol;
-  double* dinv = sm + Cfg::oDinv;
-  double* red = sm + Cfg::oRed;
-  int* flag = (int*)(sm + Cfg::oFlag);
-
+  constexpr int NP = Cfg::NP, MP = Cfg::MP, LDV = Cfg::LDV, LDQ = Cfg::LDQ;
   const int n = D.n, m = D.m, T = D.T, tid = threadIdx.x;
-  const int wid = tid >> 6, lane = tid & 63, q = lane >> 4, c = lane & 15;
-  const bool xr = !isnan(xreg), ur = !isnan(ureg);
+  const int wid = tid >> 6, lane = tid & 63;
+  BwdLds L;
+  L.V = sm + Cfg::oV;
+  L.Qxu = sm + Cfg::oQxu;
+  L.Quu = sm + Cfg::oQuu;
+  L.Qi = sm + Cfg::oQi;
+  L.vx = sm + Cfg::oVx;
+  L.qx = sm + Cfg::oQx;
+  L.lxv = sm + Cfg::oLx;
+  L.fsb = sm + Cfg::oFs;
+  L.qu = sm + Cfg::oQu;
+  L.luv = sm + Cfg::oLu;
+  L.kv = sm + Cfg::oKv;
+  L.quuk = sm + Cfg::oQuuk;
+  L.rowbuf = sm + Cfg::oKv;
+  L.red = sm + Cfg::oRed;
+  L.flag = (int*)(sm + Cfg::oFlag);
+  L.Zx = sm + Cfg::oZx;
+  L.Zu = sm + Cfg::oZu;
+  double* V = L.V;
+  const bool xr = !isnan(xreg);
   Stamp stamp(D.stamps ? D.stamps + ((int64_t)b * 4 + wid) * 8 : nullptr);
 
+  if (tid == 0) *L.flag = 0;
   // ---- terminal: Vxx = Lxx_T (+ xreg I), Vx = Lx_T (+ Vxx fs_T) ------------
   {
     const int64_t kk = D.knot(b, T);
     const double* Lxx = D.Lxx + kk * D.sNN;
     const double* Lx = D.Lx + kk * D.sN;
     const double* fs = D.fs + kk * D.sN;
+    double* fsv = L.fsb;
     // stored transposed so that G = V Z uses Lxx_T itself (it may be asymmetric)
     for (int e = tid; e < NP * NP; e += 256) {
       const int i = e % NP, j = e / NP;
@@ -143,6 +679,11 @@ __device__ __forceinline__ bool bwd_sweep_mfma(const Dev& D, int b, bool feas, d
       V[j * LDV + i] = v;
     }
     for (int i = tid; i < NP; i += 256) fsv[i] = i < n ? fs[i] : 0.;
+    // zero the padding of the per-knot vector buffers once (DMA fills [0, n))
+    // (and of Z: rows >= n, columns >= n / m are never written by the DMA)
+    for (int i = tid; i < NP; i += 256) L.lxv[i] = 0.;
+    for (int i = tid; i < MP; i += 256) L.luv[i] = 0.;
+    for (int e = tid; e < NP * (NP + MP); e += 256) L.Zx[e] = 0.;
     __syncthreads();
     double pv[2] = {0., 0.};
     for (int i = tid; i < NP; i += 256) {
@@ -156,9 +697,9 @@ __device__ __forceinline__ bool bwd_sweep_mfma(const Dev& D, int b, bool feas, d
         pv[0] += v * fsv[i];
         pv[1] += fsv[i] * a;
       }
-      vx[i] = v;
+      L.vx[i] = v;
     }
-    wg_sums<256, 2>(pv, red);
+    wg_sums<256, 2>(pv, L.red);
     if (tid == 0) {
       double* p = D.part + kk * 8;
       p[0] = 0.; p[1] = 0.; p[2] = pv[0]; p[3] = pv[1]; p[4] = 0.;
@@ -168,386 +709,72 @@ __device__ __forceinline__ bool bwd_sweep_mfma(const Dev& D, int b, bool feas, d
         const int i = e % n, j = e / n;
         D.dVxx[kk * D.sNN + e] = Lxx[e] + ((xr && i == j) ? xreg : 0.);
       }
-      for (int i = tid; i < n; i += 256) D.dVx[kk * D.sN + i] = vx[i];
+      for (int i = tid; i < n; i += 256) D.dVx[kk * D.sN + i] = L.vx[i];
     }
+    __syncthreads();
+    if (T > 0) {  // operands of knot T-1
+      const int64_t k1 = kk - 1;
+      dma_cols(L.Zx, NP, D.Fx + k1 * D.sNN, n, n, wid, lane);
+      dma_cols(L.Zu, NP, D.Fu + k1 * D.sNM, n, m, wid, lane);
+      dma_vec(L.lxv, D.Lx + k1 * D.sN, n, wid, lane);
+      dma_vec(L.luv, D.Lu + k1 * D.sM, m, wid, lane);
+      dma_vec(L.fsb, D.fs + k1 * D.sN, n, wid, lane);
+    }
+    dma_barrier();
   }
 
   for (int t = T - 1; t >= 0; --t) {
     const int64_t kk = D.knot(b, t);
     const int64_t rr = D.run(b, t);
-    const double* Fx = D.Fx + kk * D.sNN;
-    const double* Fu = D.Fu + kk * D.sNM;
-    const double* Lxx = D.Lxx + kk * D.sNN;
-    const double* Lxu = D.Lxu + kk * D.sNM;
-    const double* Luu = D.Luu + kk * D.sMM;
-    __syncthreads();
     stamp.mark(7);
-    // ---- phase 0: fs, Qx = Lx + Fx^T Vx', Qu = Lu + Fu^T Vx' -----------------
-    {
-      const double* fs = D.fs + kk * D.sN;
-      const double* Lx = D.Lx + kk * D.sN;
-      const double* Lu = D.Lu + kk * D.sM;
-      for (int i = tid; i < NP; i += 256) fsv[i] = i < n ? fs[i] : 0.;
-      for (int o = tid; o < NP + MP; o += 256) {
-        if (o < NP) {
-          double a = 0.;
-          if (o < n) {
-            const double* col = Fx + (int64_t)o * n;
-            for (int k2 = 0; k2 < n; ++k2) a += col[k2] * vx[k2];
-            a = Lx[o] + a;
-          }
-          qx[o] = a;
-        } else {
-          const int u = o - NP;
-          double a = 0.;
-          if (u < m) {
-            const double* col = Fu + (int64_t)u * n;
-            for (int k2 = 0; k2 < n; ++k2) a += col[k2] * vx[k2];
-            a = Lu[u] + a;
-          }
-          qu[u] = a;
-        }
-      }
-      if (tid == 0) *flag = 0;
+    bool ok;
+    switch (wid) {
+      case 0: ok = bwd_knot<NTL, MTL, 0>(D, L, b, t, feas, xreg, ureg, stamp); break;
+      case 1: ok = bwd_knot<NTL, MTL, 1>(D, L, b, t, feas, xreg, ureg, stamp); break;
+      case 2: ok = bwd_knot<NTL, MTL, 2>(D, L, b, t, feas, xreg, ureg, stamp); break;
+      default: ok = bwd_knot<NTL, MTL, 3>(D, L, b, t, feas, xreg, ureg, stamp); break;
     }
-    stamp.mark(0);
-    __syncthreads();
-    stamp.mark(1);
-    // ---- phase 1: G = V Z_i, H(i, j) = G_i^T Z_j + L(i, j) per owned block ---
-    {
-      const int nown = sch.nown[wid];
-      int ib[MAXOWN], js[MAXOWN];
-#pragma unroll
-      for (int o = 0; o < MAXOWN; ++o) {
-        ib[o] = o < nown ? sch.blk[wid][o] : 0;
-        js[o] = o < nown ? sch.jstart[wid][o] : JT;
-      }
-      // Initial accumulator of H(i, j): the cost block (symmetric part of Lxx
-      // for Qxx, which the reference reaches through its Vxx symmetrisation;
-      // Lxu for Qxu; Luu + ureg I for Quu).
-      auto linit = [&](f64x4(&acc)[MAXOWN], int j) {
-#pragma unroll
-        for (int o = 0; o < MAXOWN; ++o) {
-          acc[o] = f64x4{0., 0., 0., 0.};
-          if (o < nown && j >= js[o]) {
-            const int i = ib[o];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int R = 16 * i + q + 4 * r, C = 16 * j + c;
-              double v = 0.;
-              if (j < NTL) {
-                if (R < n && C < n) v = 0.5 * (Lxx[(int64_t)C * n + R] + Lxx[(int64_t)R * n + C]);
-              } else if (i < NTL) {
-                const int Cu = C - NP;
-                if (R < n && Cu < m) v = Lxu[(int64_t)Cu * n + R];
-              } else {
-                const int Ru = R - NP, Cu = C - NP;
-                if (Ru < m && Cu < m) {
-                  v = Luu[(int64_t)Cu * m + Ru];
-                  if (ur && Ru == Cu) v += ureg;
-                }
-              }
-              acc[o][r] = v;
-            }
-          }
-        }
-      };
-      int jmin = JT;
-#pragma unroll
-      for (int o = 0; o < MAXOWN; ++o) jmin = js[o] < jmin ? js[o] : jmin;
-      // Issue every global load of the G phase and of the first H column at
-      // once: the fragments are independent, so one memory latency is exposed
-      // per batch instead of one per k-step.
-      double zg[MAXOWN][4 * NTL];
-#pragma unroll
-      for (int o = 0; o < MAXOWN; ++o)
-#pragma unroll
-        for (int s2 = 0; s2 < 4 * NTL; ++s2) zg[o][s2] = o < nown ? zfrag<NTL, MTL>(Fx, Fu, n, m, s2, ib[o], q, c) : 0.;
-      double zc[4 * NTL];
-      f64x4 ac[MAXOWN];
-      if (jmin < JT) {
-#pragma unroll
-        for (int s2 = 0; s2 < 4 * NTL; ++s2) zc[s2] = zfrag<NTL, MTL>(Fx, Fu, n, m, s2, jmin, q, c);
-        linit(ac, jmin);
-      }
-      f64x4 G[MAXOWN][NTL];
-#pragma unroll
-      for (int o = 0; o < MAXOWN; ++o)
-#pragma unroll
-        for (int a = 0; a < NTL; ++a) G[o][a] = f64x4{0., 0., 0., 0.};
-      if (nown > 0) {
-#pragma unroll
-        for (int s = 0; s < 4 * NTL; ++s) {
-          double vf[NTL];
-#pragma unroll
-          for (int a = 0; a < NTL; ++a) vf[a] = V[(4 * s + q) * LDV + 16 * a + c];
-#pragma unroll
-          for (int o = 0; o < MAXOWN; ++o) {
-            if (o < nown) {
-#pragma unroll
-              for (int a = 0; a < NTL; ++a) G[o][a] = mfma4(vf[a], zg[o][s], G[o][a]);
-            }
-          }
-        }
-      }
-      // H columns, double-buffered: column j+1's fragments and cost block are
-      // in flight while column j's MFMAs run.
-      for (int j = jmin; j < JT; ++j) {
-        const bool more = j + 1 < JT;
-        double zn[4 * NTL];
-        f64x4 an[MAXOWN];
-        if (more) {
-#pragma unroll
-          for (int s2 = 0; s2 < 4 * NTL; ++s2) zn[s2] = zfrag<NTL, MTL>(Fx, Fu, n, m, s2, j + 1, q, c);
-          linit(an, j + 1);
-        }
-#pragma unroll
-        for (int s = 0; s < 4 * NTL; ++s) {
-#pragma unroll
-          for (int o = 0; o < MAXOWN; ++o)
-            if (o < nown && j >= js[o]) ac[o] = mfma4(G[o][s >> 2][s & 3], zc[s], ac[o]);
-        }
-#pragma unroll
-        for (int o = 0; o < MAXOWN; ++o) {
-          if (o < nown && j >= js[o]) {
-            const int i = ib[o];
-            if (j < NTL) {
-              const int tq = i * NTL - (i * (i - 1)) / 2 + (j - i);
-#pragma unroll
-              for (int r = 0; r < 4; ++r) Qxx[tq * 256 + r * 64 + lane] = ac[o][r];
-            } else if (i < NTL) {
-#pragma unroll
-              for (int r = 0; r < 4; ++r) Qxu[(16 * (j - NTL) + c) * LDV + 16 * i + q + 4 * r] = ac[o][r];
-            } else {
-#pragma unroll
-              for (int r = 0; r < 4; ++r) Quu[(16 * (j - NTL) + c) * LDQ + 16 * (i - NTL) + q + 4 * r] = ac[o][r];
-            }
-          }
-        }
-        if (more) {
-#pragma unroll
-          for (int s2 = 0; s2 < 4 * NTL; ++s2) zc[s2] = zn[s2];
-#pragma unroll
-          for (int o = 0; o < MAXOWN; ++o) ac[o] = an[o];
-        }
-      }
-      // ---- wave 0: Quu^-1 by in-place Gauss-Jordan (overlaps waves 1-3) ------
-      // Without pivoting on an SPD matrix the k-th pivot equals L(k,k)^2 of its
-      // Cholesky factor, so `pivot <= 0` is exactly Eigen LLT's failure
-      // (ddp.cpp:300-304). Lane l owns column j = l % MP and RPL rows
-      // i = (l / MP) * RPL + r of the MP x MP matrix; row k / column k are
-      // broadcast through LDS at each step.
-      if (wid == 0) {
-        constexpr int RPL = MP * MP / 64;
-        static_assert(MP * MP % 64 == 0 && 64 % MP == 0, "Gauss-Jordan lane layout");
-        const int jc = lane % MP, h = lane / MP;
-        double* rowbuf = dinv;  // MP doubles
-        __builtin_amdgcn_s_waitcnt(0xc07f);  // this wave's Quu stores have landed
-        __builtin_amdgcn_wave_barrier();
-        double A[RPL];
-#pragma unroll
-        for (int r = 0; r < RPL; ++r) A[r] = Quu[jc * LDQ + h * RPL + r];
-        bool bad = false;
-        for (int k = 0; k < m; ++k) {
-          const int hk = k / RPL, rk = k % RPL;
-          // column k (before elimination) and the pivot
-#pragma unroll
-          for (int r = 0; r < RPL; ++r)
-            if (jc == k) colbuf[h * RPL + r] = A[r];
-          __builtin_amdgcn_s_waitcnt(0xc07f);
-          __builtin_amdgcn_wave_barrier();
-          const double p = colbuf[k];
-          if (!(p > 0.)) bad = true;
-          const double pinv = 1. / p;
-          // row k scaled by 1/p (A(k,k) <- 1 first, so it becomes 1/p)
-#pragma unroll
-          for (int r = 0; r < RPL; ++r) {
-            if (h == hk && r == rk) {
-              const double v = (jc == k ? 1. : A[r]) * pinv;
-              A[r] = v;
-              rowbuf[jc] = v;
-            }
-          }
-          __builtin_amdgcn_s_waitcnt(0xc07f);
-          __builtin_amdgcn_wave_barrier();
-          const double rkj = rowbuf[jc];
-#pragma unroll
-          for (int r = 0; r < RPL; ++r) {
-            const int i = h * RPL + r;
-            if (i != k) {
-              const double f = colbuf[i];
-              A[r] = (jc == k ? 0. : A[r]) - f * rkj;
-            }
-          }
-          __builtin_amdgcn_s_waitcnt(0xc07f);
-          __builtin_amdgcn_wave_barrier();
-        }
-        // Quu^-1 is symmetric: store (i, j) at (j, i) (conflict-free rows)
-#pragma unroll
-        for (int r = 0; r < RPL; ++r) {
-          const int i = h * RPL + r;
-          Qi[i * LDQ + jc] = (i < m && jc < m) ? A[r] : 0.;
-        }
-        if (bad && lane == 0) *flag = 1;
-      }
+    if (!ok) {  // the factorisation failed (every wave saw the flag)
+      stamp.flush();
+      return false;
     }
-    stamp.mark(2);
-    __syncthreads();
-    stamp.mark(3);
-    if (*flag) return false;
-    // ---- phase 2: K = Quu^-1 Qxu^T (MFMA), k = Quu^-1 Qu ------------------------
-    for (int jt = wid; jt < NTL; jt += 4) {
-      f64x4 acc[MTL];
+    if (tid == 0) {
+      double* p = D.part + kk * 8;
+      const double* red = L.red;
 #pragma unroll
-      for (int it = 0; it < MTL; ++it) acc[it] = f64x4{0., 0., 0., 0.};
-#pragma unroll
-      for (int s = 0; s < 4 * MTL; ++s) {
-        const double bq = Qxu[(4 * s + q) * LDV + 16 * jt + c];
-#pragma unroll
-        for (int it = 0; it < MTL; ++it) acc[it] = mfma4(Qi[(4 * s + q) * LDQ + 16 * it + c], bq, acc[it]);
-      }
-      double* Kg = D.K + rr * D.sNM;
-      const int C = 16 * jt + c;
-#pragma unroll
-      for (int it = 0; it < MTL; ++it)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int R = 16 * it + q + 4 * r;
-          KT[R * LDV + C] = acc[it][r];
-          if (R < m && C < n) Kg[(int64_t)C * m + R] = acc[it][r];
-        }
+      for (int j = 0; j < 5; ++j) p[j] = red[j * 4] + red[j * 4 + 1] + red[j * 4 + 2] + red[j * 4 + 3];
     }
-    for (int i = tid; i < MP; i += 256) {
-      double a = 0.;
-      if (i < m)
-        for (int k2 = 0; k2 < m; ++k2) a += Qi[k2 * LDQ + i] * qu[k2];
-      kv[i] = a;
-      if (i < m) D.k[rr * D.sM + i] = a;
+    if (D.dQxx) {
+      for (int e = tid; e < n * n; e += 256) D.dVxx[kk * D.sNN + e] = V[(e / n) * LDV + e % n];
+      for (int e = tid; e < n * m; e += 256) D.dQxu[rr * D.sNM + e] = L.Qxu[(e / n) * LDV + e % n];
+      for (int e = tid; e < m * m; e += 256) D.dQuu[rr * D.sMM + e] = L.Quu[(e / m) * LDQ + e % m];
+      for (int i = tid; i < n; i += 256) {
+        D.dQx[rr * D.sN + i] = L.qx[i];
+        D.dVx[kk * D.sN + i] = L.vx[i];
+      }
+      for (int i = tid; i < m; i += 256) D.dQu[rr * D.sM + i] = L.qu[i];
+      __syncthreads();
     }
-    stamp.mark(4);
-    __syncthreads();
-    // ---- phase 2b: Quuk = Quu k ; Vxx = Qxx - Qxu K (+ xreg I), symmetric ------
-    for (int i = tid; i < MP; i += 256) {
-      double a = 0.;
-      if (i < m)
-        for (int k2 = 0; k2 < m; ++k2) a += Quu[k2 * LDQ + i] * kv[k2];
-      quuk[i] = a;
+    if (*L.flag) {
+      stamp.flush();
+      return false;
     }
-    {
-      bool bad = false;
-      for (int u = wid; u < Cfg::NQXX; u += 4) {
-        int i = 0, rem = u;
-        while (rem >= NTL - i) {
-          rem -= NTL - i;
-          ++i;
-        }
-        const int j = i + rem;
-        f64x4 acc;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) acc[r] = Qxx[u * 256 + r * 64 + lane];
-#pragma unroll
-        for (int s = 0; s < 4 * MTL; ++s)
-          acc = mfma4(-Qxu[(4 * s + q) * LDV + 16 * i + c], KT[(4 * s + q) * LDV + 16 * j + c], acc);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int R = 16 * i + q + 4 * r, C = 16 * j + c;
-          double v = acc[r];
-          if (xr && R == C && R < n) v += xreg;
-          if (i < j || R <= C) {
-            V[C * LDV + R] = v;
-            V[R * LDV + C] = v;
-            if (R < n && C < n) bad |= bad_entry(v);
-          }
-        }
-      }
-      if (bad) *flag = 1;
-    }
-    stamp.mark(5);
-    __syncthreads();
-    // ---- phase 3: Vx, Vxx fs, checks, reduction terms, stores ----------------
-    {
-      bool bad = false;
-      double pv[5] = {0., 0., 0., 0., 0.};
-      for (int i = tid; i < NP; i += 256) {
-        double v = 0.;
-        if (i < n) {
-          double a = 0., c2 = 0.;
-          for (int k2 = 0; k2 < m; ++k2) {
-            const double kt = KT[k2 * LDV + i];
-            a += kt * quuk[k2];
-            c2 += kt * qu[k2];
-          }
-          v = ur ? (qx[i] + a) - 2 * c2 : qx[i] - c2;
-          if (!feas) {
-            double f = 0.;
-            for (int j = 0; j < n; ++j) f += V[j * LDV + i] * fsv[j];
-            D.Vxxfs[kk * D.sN + i] = f;
-            v += f;
-            pv[2] += v * fsv[i];
-            pv[3] += fsv[i] * f;
-          }
-          bad |= bad_entry(v);
-        }
-        vx[i] = v;
-      }
-      for (int i = tid; i < m; i += 256) {
-        pv[0] += qu[i] * kv[i];
-        pv[1] += kv[i] * quuk[i];
-        pv[4] += qu[i] * qu[i];
-      }
-      if (bad) *flag = 1;
-      wg_sums<256, 5>(pv, red);
-      if (tid == 0) {
-        double* p = D.part + kk * 8;
-        for (int j = 0; j < 5; ++j) p[j] = pv[j];
-      }
-      if (D.dQxx) {
-        for (int e = tid; e < n * n; e += 256) {
-          const int R = e % n, C = e / n;
-          const int lo = R < C ? R : C, hi = R < C ? C : R;
-          const int i = lo / 16, j = hi / 16;
-          // Qxx tile (i, j) element (lo, hi) in accumulator order
-          const int tq = i * NTL - (i * (i - 1)) / 2 + (j - i);
-          const int rl = lo - 16 * i, cl = hi - 16 * j;
-          double v;
-          if (i == j) {
-            const int rr2 = R - 16 * i, cc2 = C - 16 * j;
-            v = Qxx[tq * 256 + (rr2 >> 2) * 64 + (rr2 & 3) * 16 + cc2];
-          } else {
-            v = Qxx[tq * 256 + (rl >> 2) * 64 + (rl & 3) * 16 + cl];
-          }
-          D.dQxx[rr * D.sNN + e] = v;
-          D.dVxx[kk * D.sNN + e] = V[C * LDV + R];
-        }
-        for (int e = tid; e < n * m; e += 256) D.dQxu[rr * D.sNM + e] = Qxu[(e / n) * LDV + e % n];
-        for (int e = tid; e < m * m; e += 256) D.dQuu[rr * D.sMM + e] = Quu[(e / m) * LDQ + e % m];
-        for (int i = tid; i < n; i += 256) {
-          D.dQx[rr * D.sN + i] = qx[i];
-          D.dVx[kk * D.sN + i] = vx[i];
-        }
-        for (int i = tid; i < m; i += 256) D.dQu[rr * D.sM + i] = qu[i];
-      }
-    }
-    stamp.mark(6);
-    __syncthreads();
-    if (*flag) return false;
   }
+  stamp.flush();
   return true;
 }
 
 template <int NTL, int MTL>
-__global__ __launch_bounds__(256) void backward_mfma_kernel(Dev D, Prm prm, int mode, BwdSched sch) {
+__global__ __launch_bounds__(256) void backward_mfma_kernel(Dev D, Prm prm, int mode) {
   const int b = blockIdx.x;
   ElemState* st = D.st + b;
   if (mode == 0 && !st->active) return;
   extern __shared__ __attribute__((aligned(16))) double sm[];
-  using Cfg = MfmaCfg<NTL, MTL>;
-  int* flag = (int*)(sm + Cfg::oFlag);
   const bool feas = st->is_feasible != 0;
   double xreg = st->xreg, ureg = st->ureg;
   bool ok;
   for (;;) {
-    ok = bwd_sweep_mfma<NTL, MTL>(D, b, feas, xreg, ureg, sm, sch);
+    ok = bwd_sweep_mfma<NTL, MTL>(D, b, feas, xreg, ureg, sm);
     __syncthreads();
     if (ok || mode == 1) break;
     xreg *= prm.regfactor;  // increaseRegularization (ddp.cpp:312-318)
@@ -555,7 +782,6 @@ __global__ __launch_bounds__(256) void backward_mfma_kernel(Dev D, Prm prm, int 
     ureg = xreg;
     if (xreg == prm.regmax) break;
   }
-  (void)flag;
   if (threadIdx.x == 0) {
     st->xreg = xreg;
     st->ureg = ureg;

@@ -88,7 +88,6 @@ struct fddp_handle_s {
   size_t bwd_smem = 0, fwd_smem = 0, calc_smem = 0, cdiff_smem = 0;
   int64_t pcap = 0;  // doubles of LDS reserved for a resident parameter block
   int bwd_variant = 0;  // 0 generic, else NTL*10+MTL of the MFMA sweep
-  BwdSched sched;
   // timing
   bool timing = false;
   std::vector<hipEvent_t> ev_pool;
@@ -192,8 +191,7 @@ int launch_calc_diff(fddp_handle* h, int sel, int gaps) {
 template <int NTL, int MTL>
 void launch_bwd_mfma(fddp_handle* h, int mode) {
   const Dev& D = h->D;
-  backward_mfma_kernel<NTL, MTL><<<dim3(D.B), dim3(256), MfmaCfg<NTL, MTL>::bytes, h->stream>>>(D, to_prm(h->prm), mode,
-                                                                                             h->sched);
+  backward_mfma_kernel<NTL, MTL><<<dim3(D.B), dim3(256), MfmaCfg<NTL, MTL>::bytes, h->stream>>>(D, to_prm(h->prm), mode);
 }
 
 int launch_backward(fddp_handle* h, int mode) {
@@ -214,32 +212,12 @@ int launch_backward(fddp_handle* h, int mode) {
 template <int NTL, int MTL>
 int setup_bwd_mfma(fddp_handle* h) {
   using Cfg = MfmaCfg<NTL, MTL>;
+  const size_t lds = Cfg::bytes;
+  if (lds > 160 * 1024) return -1;
   if (hipFuncSetAttribute((const void*)backward_mfma_kernel<NTL, MTL>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)Cfg::bytes) != hipSuccess)
+                          (int)lds) != hipSuccess)
     return -1;
-  // LPT: wave 0 owns the u column blocks (Quu + its factorisation), waves 1-3
-  // share the x column blocks by cost G (NTL x 4NTL MFMAs) + H tiles (x 4NTL).
-  BwdSched& s = h->sched;
-  std::memset(&s, 0, sizeof(s));
-  for (int u = 0; u < MTL; ++u) {
-    s.blk[0][s.nown[0]] = NTL + u;
-    s.jstart[0][s.nown[0]] = NTL;
-    s.nown[0]++;
-  }
-  std::vector<std::pair<int, int>> xs;
-  for (int i = 0; i < NTL; ++i) xs.push_back({NTL * 4 * NTL + (NTL - i + MTL) * 4 * NTL, i});
-  std::sort(xs.rbegin(), xs.rend());
-  int load[4] = {0, 0, 0, 0};
-  for (auto& p : xs) {
-    int best = -1;
-    for (int w = 1; w < 4; ++w)
-      if (s.nown[w] < Cfg::MAXOWN && (best < 0 || load[w] < load[best])) best = w;
-    if (best < 0) return -1;
-    s.blk[best][s.nown[best]] = p.second;
-    s.jstart[best][s.nown[best]] = p.second;
-    s.nown[best]++;
-    load[best] += p.first;
-  }
+  // column-block ownership per wave is static (BwdPlan in bwd_mfma.hpp)
   return NTL * 10 + MTL;
 }
 int launch_forward(fddp_handle* h, int mode, double alpha, int* count) {
@@ -518,7 +496,7 @@ void fddp_destroy(fddp_handle* h) {
   if (h->D.stamps) {  // diagnostic summary: mean cycles per element per wave and phase
     std::vector<unsigned long long> v((size_t)h->dims.B * 32);
     if (hipMemcpy(v.data(), h->D.stamps, v.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
-      const char* names[8] = {"p0_prep", "p0_barrier", "p1_GH_fact", "p1_barrier", "p2_K", "p2b_Vupd", "p3_vec", "loop"};
+      const char* names[8] = {"p1_G", "p1_H", "p1_inv", "b1_dma", "p2_K", "p2_Vupd", "b2_p3", "b3_wait"};
       std::fprintf(stderr, "[fddp stamps] mean cycles per element (variant %d):\n", h->bwd_variant);
       for (int w = 0; w < 4; ++w) {
         std::fprintf(stderr, "  wave %d:", w);

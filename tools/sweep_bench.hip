@@ -1,0 +1,59 @@
+// Micro-benchmark (diagnostic): cycles of one sym_sweep_inverse<32> (the
+// backward sweep's Quu^-1 on wave 0) in isolation, one wave per workgroup.
+// Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -o tools/sweep_bench tools/sweep_bench.hip
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <cmath>
+#include "../crocoddyl_amd/csrc/bwd_mfma.hpp"
+
+__global__ void k_sweep(const double* Q, double* Qi_out, unsigned long long* cyc, int reps, int m) {
+  __shared__ double Quu[32 * 32], Qi[32 * 32], rb[64];
+  const int lane = threadIdx.x;
+  for (int e = lane; e < 1024; e += 64) Quu[e] = Q[e];
+  __syncthreads();
+  unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  bool bad = false;
+  for (int r = 0; r < reps; ++r) bad |= fddp::sym_sweep_inverse<32, 32>(Quu, Qi, rb, m, lane);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  unsigned long long t1 = __builtin_amdgcn_s_memtime();
+  for (int e = lane; e < 1024; e += 64) Qi_out[blockIdx.x * 1024 + e] = Qi[e];
+  if (lane == 0) cyc[blockIdx.x] = (t1 - t0) / reps + (bad ? 1000000000ull : 0);
+}
+
+int main() {
+  const int m = 32;
+  double Q[1024], X[1024];
+  srand(1);
+  for (int i = 0; i < 1024; ++i) X[i] = (rand() / (double)RAND_MAX) - 0.5;
+  for (int i = 0; i < m; ++i)
+    for (int j = 0; j < m; ++j) {
+      double s = 0;
+      for (int k = 0; k < m; ++k) s += X[i * 32 + k] * X[j * 32 + k];
+      Q[j * 32 + i] = s + (i == j ? 1.0 : 0.0);
+    }
+  double *dQ, *dQi;
+  unsigned long long* dc;
+  hipMalloc(&dQ, sizeof(Q));
+  hipMalloc(&dQi, sizeof(double) * 1024 * 256);
+  hipMalloc(&dc, 8 * 256);
+  hipMemcpy(dQ, Q, sizeof(Q), hipMemcpyHostToDevice);
+  for (int blocks : {1, 256}) {
+    k_sweep<<<blocks, 64>>>(dQ, dQi, dc, 20, m);
+    hipDeviceSynchronize();
+    unsigned long long c[256];
+    hipMemcpy(c, dc, 8 * blocks, hipMemcpyDeviceToHost);
+    double Qi[1024];
+    hipMemcpy(Qi, dQi, sizeof(Qi), hipMemcpyDeviceToHost);
+    double err = 0;
+    for (int i = 0; i < m; ++i)
+      for (int j = 0; j < m; ++j) {
+        double s = 0;
+        for (int k = 0; k < m; ++k) s += Q[k * 32 + i] * Qi[j * 32 + k];
+        err = fmax(err, fabs(s - (i == j)));
+      }
+    printf("blocks=%d: %llu cycles per 32x32 inverse (%.0f per pivot), |Q Qi - I| = %.2e\n", blocks, c[0],
+           c[0] / 32.0, err);
+  }
+  return 0;
+}
