@@ -1,0 +1,523 @@
+// Fast path of ShootingProblem::calc / calcDiff and of the FDDP forward
+// rollout for the dense knot kinds (ActionModelLQR, Euler∘DifferentialLQR),
+// used when every knot is one of them and ndx, nu_max <= NT.
+//
+// Same arithmetic as knot_calc / knot_calc_diff (knots.hpp) and fwd_trial
+// (fddp_kernels.hpp), reorganised for latency: on gfx950 a dependent f64 FMA
+// takes 32 cycles, so a row-per-thread dot product of length n is a 32n-cycle
+// chain. Every matrix-vector product here splits each row over G = NT / rows
+// column segments (thread -> row i, segment g; consecutive threads read
+// consecutive rows of a column, conflict-free in LDS and coalesced in HBM),
+// four independent accumulators per segment, and one LDS reduction. The knot
+// cost is reduced from per-thread partials (wave shuffles + one LDS slot per
+// wave), and the forward pass defers its NaN checks to the end of the trial
+// (a trial that raises at knot t fails exactly as if it had stopped there).
+//
+// The dynamics of both kinds are one product with a contiguous block of the
+// parameter pool: LQR [Fx | Fu] (ld nx) times [x; u], Euler∘DiffLQR
+// [Fq | Fv | Fu] (ld nq) times [q; v; u]; the cost rows are [Lxx | Lxu]
+// (ld nx) times [x; u] and the u rows Lxu^T x + Luu u.
+#pragma once
+
+#include "fddp_kernels.hpp"
+
+namespace fddp {
+
+struct DenseKnot {
+  bool dlqr, integ, drift_free;
+  double dt, sc;  // Euler step; cost / derivative scale (dt when integrating)
+  int nr;         // dynamics rows: nx (LQR) or nq (Euler∘DiffLQR)
+  const double *F, *f0, *Lxx, *Lxu, *Luu, *lx, *lu;
+  __device__ DenseKnot(int kind, const double* P, int nx, int nu) {
+    if (kind == FDDP_KNOT_LQR) {
+      LQRBlk Bk(P, nx, nu);
+      dlqr = false;
+      integ = false;
+      dt = 0.;
+      sc = 1.;
+      drift_free = Bk.drift_free;
+      nr = nx;
+      F = Bk.Fx;
+      f0 = Bk.f0;
+      Lxx = Bk.Lxx;
+      Lxu = Bk.Lxu;
+      Luu = Bk.Luu;
+      lx = Bk.lx;
+      lu = Bk.lu;
+    } else {
+      DLQRBlk Bk(P, nx, nu);
+      dlqr = true;
+      dt = Bk.dt;
+      integ = dt != 0.;
+      sc = integ ? dt : 1.;
+      drift_free = Bk.drift_free;
+      nr = nx / 2;
+      F = Bk.Fq;
+      f0 = Bk.f0;
+      Lxx = Bk.Lxx;
+      Lxu = Bk.Lxu;
+      Luu = Bk.Luu;
+      lx = Bk.lx;
+      lu = Bk.lu;
+    }
+  }
+};
+
+__device__ __forceinline__ bool dense_kind(int kind) { return kind == FDDP_KNOT_LQR || kind == FDDP_KNOT_EULER_DIFFLQR; }
+
+// Thread -> (row i, column segment g) of a rows-row product; G segments.
+struct RowSeg {
+  int i, g, G;
+  bool on;
+  __device__ RowSeg(int rows, int nt, int tid) {
+    G = rows > 0 ? nt / rows : 1;
+    if (G < 1) G = 1;
+    i = rows > 0 ? tid % rows : 0;
+    g = rows > 0 ? tid / rows : 0;
+    on = rows > 0 && g < G;
+  }
+};
+
+// sum_{j = j0, j0+G, ... < cols} A[j*lda + i] * v[j], four accumulators.
+__device__ __forceinline__ double seg_dot(const double* A, int lda, int i, int j0, int G, int cols, const double* v) {
+  double a0 = 0., a1 = 0., a2 = 0., a3 = 0.;
+  int j = j0;
+  for (; j + 3 * G < cols; j += 4 * G) {
+    a0 = fma(A[j * lda + i], v[j], a0);
+    a1 = fma(A[(j + G) * lda + i], v[j + G], a1);
+    a2 = fma(A[(j + 2 * G) * lda + i], v[j + 2 * G], a2);
+    a3 = fma(A[(j + 3 * G) * lda + i], v[j + 3 * G], a3);
+  }
+  for (; j < cols; j += G) a0 = fma(A[j * lda + i], v[j], a0);
+  return (a0 + a1) + (a2 + a3);
+}
+// Transposed: sum_j A[i*lda + j] * v[j] (row i of A^T = column i of A).
+__device__ __forceinline__ double seg_dot_t(const double* A, int lda, int i, int j0, int G, int cols, const double* v) {
+  const double* a = A + i * lda;
+  double a0 = 0., a1 = 0., a2 = 0., a3 = 0.;
+  int j = j0;
+  for (; j + 3 * G < cols; j += 4 * G) {
+    a0 = fma(a[j], v[j], a0);
+    a1 = fma(a[j + G], v[j + G], a1);
+    a2 = fma(a[j + 2 * G], v[j + 2 * G], a2);
+    a3 = fma(a[j + 3 * G], v[j + 3 * G], a3);
+  }
+  for (; j < cols; j += G) a0 = fma(a[j], v[j], a0);
+  return (a0 + a1) + (a2 + a3);
+}
+
+// Per-thread partials of one dense knot at (x, u) = xu[0..nx), xu[nx..nx+nu):
+//   dyn : dynamics row partial (-> pdyn[g*nr + i])
+//   lx  : (Lxx x + Lxu u) row partial (-> plx[g*nx + i]) when want_lx
+//   lu  : (Lxu^T x + Luu u) row partial (-> plu[g*nu + i]) when want_lu
+// Returns this thread's share of the unscaled knot cost
+//   0.5 x.Lxx x + 0.5 u.Luu u + x.Lxu u + lx.x + lu.u   (lqr.hxx:47-48).
+template <int NT>
+__device__ __forceinline__ double dense_partials(const DenseKnot& K, int nx, int nu, bool use_u, const double* xu,
+                                                 bool want_dyn, bool want_lx, bool want_lu, bool want_cost,
+                                                 double* pdyn, double* plx, double* plu) {
+  const int tid = threadIdx.x;
+  const double* x = xu;
+  const double* u = xu + nx;
+  const int nuu = use_u ? nu : 0;
+  double cost = 0.;
+  if (want_dyn) {
+    const RowSeg r(K.nr, NT, tid);
+    if (r.on) pdyn[r.g * K.nr + r.i] = seg_dot(K.F, K.nr, r.i, r.g, r.G, nx + nuu, xu);
+  }
+  if (want_lx || want_cost) {
+    const RowSeg r(nx, NT, tid);
+    if (r.on) {
+      const double sx = seg_dot(K.Lxx, nx, r.i, r.g, r.G, nx, x);
+      const double su = nuu > 0 ? seg_dot(K.Lxu, nx, r.i, r.g, r.G, nuu, u) : 0.;
+      if (want_lx) plx[r.g * nx + r.i] = sx + su;
+      if (want_cost) {
+        cost = x[r.i] * (0.5 * sx + su);
+        if (r.g == 0) cost = fma(K.lx[r.i], x[r.i], cost);
+      }
+    }
+  }
+  if ((want_lu || want_cost) && nu > 0) {
+    const RowSeg r(nu, NT, tid);
+    if (r.on) {
+      const double a = seg_dot_t(K.Lxu, nx, r.i, r.g, r.G, nx, x);
+      const double bb = nuu > 0 ? seg_dot(K.Luu, nu, r.i, r.g, r.G, nuu, u) : 0.;
+      if (want_lu) plu[r.g * nu + r.i] = a + bb;
+      if (want_cost && nuu > 0) {
+        cost = fma(0.5 * u[r.i], bb, cost);
+        if (r.g == 0) cost = fma(K.lu[r.i], u[r.i], cost);
+      }
+    }
+  }
+  return cost;
+}
+
+// Sum of the G partials of row i.
+__device__ __forceinline__ double seg_sum(const double* p, int rows, int i, int nt) {
+  int G = nt / rows;
+  if (G < 1) G = 1;
+  double s = 0.;
+  for (int g = 0; g < G; ++g) s += p[g * rows + i];
+  return s;
+}
+
+// xnext rows i < nr from the reduced dynamics sum (lqr.hxx:38-44,
+// euler.hxx:60-70 with diff-lqr.hxx:36-44). Writes xnext[i] (and [nq + i]).
+__device__ __forceinline__ void dense_xnext(const DenseKnot& K, int nx, int i, double a, const double* x, double* xn) {
+  if (!K.drift_free) a += K.f0[i];
+  if (!K.dlqr) {
+    xn[i] = a;
+    return;
+  }
+  const int nq = nx / 2;
+  if (K.integ) {
+    const double dt = K.dt, dt2 = dt * dt;
+    const double dq = x[nq + i] * dt + a * dt2;  // v*dt + a*dt^2 (euler.hxx:66)
+    const double dv = a * dt;                    // a*dt (euler.hxx:67)
+    xn[i] = x[i] + dq;
+    xn[nq + i] = x[nq + i] + dv;
+  } else {
+    xn[i] = x[i];
+    xn[nq + i] = x[nq + i];
+  }
+}
+
+// Element (i, j) of a dense knot's derivative blocks (knot_calc_diff).
+__device__ __forceinline__ double dense_fx(const DenseKnot& K, int n, int i, int j) {
+  if (!K.dlqr) return K.F[j * n + i];
+  if (!K.integ) return i == j ? 1. : 0.;
+  const int nq = n / 2, nv = nq;
+  const double dt = K.dt, dt2 = dt * dt;
+  const int r = i < nv ? i : i - nv;
+  const double da = K.F[j * nq + r];  // [Fq | Fv] column j
+  double f = i < nv ? da * dt2 : da * dt;
+  if (i < nv && j == nv + i) f += dt;  // topRightCorner(nv,nv).diagonal() += dt
+  if (i == j) f += 1.;                 // Jintegrate(first, addto)
+  return f;
+}
+__device__ __forceinline__ double dense_fu(const DenseKnot& K, int n, int nu, int i, int j) {
+  if (j >= nu) return 0.;
+  if (!K.dlqr) return K.F[(n + j) * n + i];
+  if (!K.integ) return 0.;
+  const int nq = n / 2, nv = nq;
+  const int r = i < nv ? i : i - nv;
+  const double da = K.F[(n + j) * nq + r];  // Fu column j, after [Fq | Fv]
+  return i < nv ? da * K.dt * K.dt : da * K.dt;
+}
+
+// Streams one knot's derivative blocks out (coalesced, every thread).
+template <int NT>
+__device__ __forceinline__ void dense_write_blocks(const DenseKnot& K, int n, int m, int nu, const KnotDiffOut& o) {
+  const int tid = threadIdx.x;
+  const double sc = K.sc;
+  const bool scale = K.dlqr && K.integ;
+  {
+    const int tot = n * n;
+    const float inv = 1.f / (float)n;
+    for (int e = tid; e < tot; e += NT) {
+      int j = (int)((float)e * inv);
+      int i = e - j * n;
+      if (i < 0) { --j; i += n; }
+      if (i >= n) { ++j; i -= n; }
+      o.Fx[e] = dense_fx(K, n, i, j);
+      const double l = K.Lxx[e];
+      o.Lxx[e] = scale ? sc * l : l;
+    }
+  }
+  {
+    const int tot = n * m;
+    const float inv = 1.f / (float)n;
+    for (int e = tid; e < tot; e += NT) {
+      int j = (int)((float)e * inv);
+      int i = e - j * n;
+      if (i < 0) { --j; i += n; }
+      if (i >= n) { ++j; i -= n; }
+      o.Fu[e] = dense_fu(K, n, nu, i, j);
+      const double l = j < nu ? K.Lxu[e] : 0.;
+      o.Lxu[e] = scale ? sc * l : l;
+    }
+  }
+  {
+    const int tot = m * m;
+    const float inv = 1.f / (float)m;
+    for (int e = tid; e < tot; e += NT) {
+      int j = (int)((float)e * inv);
+      int i = e - j * m;
+      if (i < 0) { --j; i += m; }
+      if (i >= m) { ++j; i -= m; }
+      const double l = (i < nu && j < nu) ? K.Luu[j * nu + i] : 0.;
+      o.Luu[e] = scale ? sc * l : l;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// ShootingProblem::calc (shooting.hxx:133-161) and/or calcDiff (164-195) with
+// the gaps of SolverDDP::calcDiff (ddp.cpp:160-176), fused: one workgroup per
+// element walks its knots with the parameter block LDS-resident. Elements
+// selected by sel_calc get xnext and the knot costs, those selected by
+// sel_diff the derivative blocks (+ gaps when `gaps`).
+// ---------------------------------------------------------------------------
+template <int NT>
+__global__ __launch_bounds__(NT) void calc_fused_kernel(Dev D, int sel_calc, int sel_diff, int gaps, int64_t pcap) {
+  const int b = blockIdx.x;
+  const ElemState& s = D.st[b];
+  const bool do_calc = sel_calc >= 0 && selected(s, sel_calc);
+  const bool do_diff = sel_diff >= 0 && selected(s, sel_diff);
+  if (!do_calc && !do_diff) return;
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  double* pl = sm;                 // pcap
+  double* xu = pl + pcap;          // sX + sM
+  double* xn = xu + D.sX + D.sM;   // sX
+  double* pdyn = xn + D.sX;        // NT
+  double* plx = pdyn + NT;         // NT
+  double* plu = plx + NT;          // NT
+  double* red = plu + NT;          // 16
+  const int c = s.cur, nx = D.nx, n = D.n, m = D.m, T = D.T, tid = threadIdx.x;
+  const int lane = tid & 63, wid = tid >> 6;
+  const double* cached = nullptr;
+  // x and u of knot t+1 are loaded into registers while knot t computes
+  // (thread i holds x_i, u_i; nx, m <= NT on this path)
+  double px = 0., pu = 0.;
+  auto prefetch = [&](int t) {
+    if (t > T) return;
+    if (tid < nx) px = D.xs[c][D.knot(b, t) * D.sX + tid];
+    if (t < T && tid < m) pu = D.us[c][D.run(b, t) * D.sM + tid];
+  };
+  prefetch(0);
+  for (int t = 0; t <= T; ++t) {
+    const fddp_knot_desc kd = D.knots[t];
+    const double* P = stage_params<NT>(D.pblock(b, t), block_doubles_dev(kd.kind, nx, kd.nu), pl, pcap, cached);
+    const int64_t kk = D.knot(b, t);
+    const bool running = t < T;
+    const int nu = kd.nu;
+    const bool use_u = running && nu > 0;
+    if (tid < nx) xu[tid] = px;
+    if (use_u && tid < nu) xu[nx + tid] = pu;
+    prefetch(t + 1);
+    __syncthreads();
+    const DenseKnot K(kd.kind, P, nx, nu);
+    const bool want_dyn = do_calc && running;
+    double cp = dense_partials<NT>(K, nx, nu, use_u, xu, want_dyn, do_diff, do_diff, do_calc, pdyn, plx, plu);
+    if (do_calc) {
+      cp = wave_sum(cp);
+      if (lane == 0) red[wid] = cp;
+    }
+    __syncthreads();
+    if (want_dyn) {
+      for (int i = tid; i < K.nr; i += NT) dense_xnext(K, nx, i, seg_sum(pdyn, K.nr, i, NT), xu, xn);
+    }
+    if (do_calc && tid == 0) {
+      double cst = 0.;
+      for (int w = 0; w < NT / 64; ++w) cst += red[w];
+      cst = K.dlqr && K.integ ? K.dt * cst : cst;
+      D.kcost[c][kk] = cst;
+    }
+    if (do_diff) {
+      KnotDiffOut o;
+      o.Fx = D.Fx + kk * D.sNN;
+      o.Fu = D.Fu + kk * D.sNM;
+      o.Lxx = D.Lxx + kk * D.sNN;
+      o.Lxu = D.Lxu + kk * D.sNM;
+      o.Luu = D.Luu + kk * D.sMM;
+      o.Lx = D.Lx + kk * D.sN;
+      o.Lu = D.Lu + kk * D.sM;
+      const bool scale = K.dlqr && K.integ;
+      for (int i = tid; i < n; i += NT) {
+        const double l = K.lx[i] + seg_sum(plx, nx, i, NT);
+        o.Lx[i] = scale ? K.sc * l : l;
+      }
+      for (int i = tid; i < m; i += NT) {
+        double v = 0.;
+        if (i < nu) {
+          const double l = K.lu[i] + seg_sum(plu, nu, i, NT);
+          v = scale ? K.sc * l : l;
+        }
+        o.Lu[i] = v;
+      }
+      dense_write_blocks<NT>(K, n, m, nu, o);
+    }
+    __syncthreads();  // xn complete
+    if (want_dyn) {
+      double* xo = D.xnext[c] + D.run(b, t) * D.sX;
+      for (int i = tid; i < nx; i += NT) xo[i] = xn[i];
+    }
+    if (do_diff && gaps) {
+      if (!s.is_feasible) {
+        // fs[0] = diff(xs[0], x0) = x0 - xs[0]; fs[t+1] = diff(xs[t+1], data[t].xnext)
+        if (t == 0) {
+          double* f = D.fs + D.knot(b, 0) * D.sN;
+          const double* x0 = D.x0 + (int64_t)b * D.sX;
+          for (int i = tid; i < n; i += NT) f[i] = x0[i] - xu[i];
+        }
+        if (running && tid < n) {  // px holds xs[t+1][tid] now
+          double* f = D.fs + D.knot(b, t + 1) * D.sN;
+          const double* xng = D.xnext[c] + D.run(b, t) * D.sX;
+          f[tid] = (want_dyn ? xn[tid] : xng[tid]) - px;
+        }
+      } else if (!s.was_feasible) {  // closing the gaps
+        double* f = D.fs + kk * D.sN;
+        for (int i = tid; i < n; i += NT) f[i] = 0.;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// One forward trial (fwd_trial) with the dense-knot arithmetic above. Per
+// knot: us_try = us - alpha k - K dx (segmented product with K read once from
+// HBM; next knot's K, k, us, xs, fs, Vxx fs are prefetched into registers),
+// then the dynamics and cost partials, then xnext. Knot costs go to kcost;
+// the in-order running sum and the NaN checks run once at the end.
+// ---------------------------------------------------------------------------
+template <int NT, bool FAST>
+__device__ __forceinline__ bool fwd_trial_fast(const Dev& D, int b, const ElemState& s, double alpha, double* xu,
+                                               double* dxv, double* xn, double* pa, double* pdyn, double* red,
+                                               int* flag, double& cost_try, double& dv, double* pl, int64_t pcap,
+                                               const double*& cached) {
+  const int n = D.n, nx = D.nx, m = D.m, T = D.T, tid = threadIdx.x;
+  const int lane = tid & 63, wid = tid >> 6;
+  constexpr int NW = NT / 64;
+  const int c = s.cur, o = 1 - c;
+  const bool feas = s.is_feasible != 0;
+  const bool full = feas || alpha == 1.;
+  const double* x0 = D.x0 + (int64_t)b * D.sX;
+  if (tid < nx) xn[tid] = x0[tid];
+  bool bad = false;
+  // this thread's share of K dx: row rk.i of K (m x n, ld m), columns
+  // rk.g + s * rk.G, held in registers one knot ahead when they fit
+  const RowSeg rk(m, NT, tid);
+  constexpr int KMAX = 16;
+  const int kcols = rk.on ? (n - rk.g + rk.G - 1) / rk.G : 0;
+  const bool kreg = (n + rk.G - 1) / rk.G <= KMAX;
+  double pK[KMAX];
+  double pxs = 0., pfs = 0., pvf = 0., pus = 0., pkv = 0.;
+  auto prefetch = [&](int t) {
+    if (t > T) return;
+    const int64_t kk = D.knot(b, t);
+    if (tid < nx) {
+      pxs = D.xs[c][kk * D.sX + tid];
+      pfs = D.fs[kk * D.sN + tid];
+      pvf = feas ? 0. : D.Vxxfs[kk * D.sN + tid];
+    }
+    if (t < T) {
+      const int64_t rr = D.run(b, t);
+      if (tid < m) {
+        pus = D.us[c][rr * D.sM + tid];
+        pkv = D.k[rr * D.sM + tid];
+      }
+      if (kreg) {
+        const double* Kt = D.K + rr * D.sNM;
+#pragma unroll
+        for (int q = 0; q < KMAX; ++q) pK[q] = q < kcols ? Kt[(rk.g + q * rk.G) * m + rk.i] : 0.;
+      }
+    }
+  };
+  prefetch(0);
+  __syncthreads();
+  for (int t = 0; t <= T; ++t) {
+    const int64_t kk = D.knot(b, t);
+    const bool running = t < T;
+    const fddp_knot_desc kd = D.knots[t];
+    const int nu = kd.nu;
+    const double cxs = pxs, cfs = pfs, cvf = pvf, cus = pus, ckv = pkv;
+    double cK[KMAX];
+#pragma unroll
+    for (int q = 0; q < KMAX; ++q) cK[q] = pK[q];
+    prefetch(t + 1);
+    // xs_try[t] = xnext  or  integrate(xnext, fs[t] * (alpha - 1)); dx = xs_try - xs
+    double pd = 0.;
+    if (tid < nx) {
+      const double v = full ? xn[tid] : xn[tid] + cfs * (alpha - 1);
+      xu[tid] = v;
+      D.xs[o][kk * D.sX + tid] = v;
+      const double dxi = v - cxs;
+      dxv[tid] = dxi;
+      if (!feas) pd = dxi * cvf;  // -fs^T Vxx diff(xs_try, xs)
+    }
+    if (!feas) {
+      pd = wave_sum(pd);
+      if (lane == 0) red[8 + wid] = pd;
+    }
+    const double* P = stage_params<NT>(D.pblock(b, t), block_doubles_dev(kd.kind, nx, nu), pl, pcap, cached);
+    __syncthreads();
+    if (running) {
+      // us_try = us - k * alpha - K * dx
+      if (rk.on) {
+        double a;
+        if (kreg) {
+          double a0 = 0., a1 = 0.;
+#pragma unroll
+          for (int q = 0; q < KMAX; q += 2) {
+            if (q < kcols) a0 = fma(cK[q], dxv[rk.g + q * rk.G], a0);
+            if (q + 1 < kcols) a1 = fma(cK[q + 1], dxv[rk.g + (q + 1) * rk.G], a1);
+          }
+          a = a0 + a1;
+        } else {
+          a = seg_dot(D.K + D.run(b, t) * D.sNM, m, rk.i, rk.g, rk.G, n, dxv);
+        }
+        pa[rk.g * m + rk.i] = a;
+      }
+      __syncthreads();
+      if (tid < m) {
+        double v = 0.;
+        if (tid < nu) v = (cus - ckv * alpha) - seg_sum(pa, m, tid, NT);
+        xu[nx + tid] = v;
+        D.us[o][D.run(b, t) * D.sM + tid] = v;
+      }
+      __syncthreads();
+    }
+    const DenseKnot K(kd.kind, P, nx, nu);
+    double cp = dense_partials<NT>(K, nx, nu, running && nu > 0, xu, running, false, false, true, pdyn, nullptr,
+                                   nullptr);
+    cp = wave_sum(cp);
+    if (lane == 0) red[wid] = cp;
+    __syncthreads();
+    if (running) {
+      for (int i = tid; i < K.nr; i += NT) dense_xnext(K, nx, i, seg_sum(pdyn, K.nr, i, NT), xu, xn);
+    }
+    if (tid == 0) {
+      double cst = 0., p2 = 0.;
+      for (int w = 0; w < NW; ++w) {
+        cst += red[w];
+        p2 += red[8 + w];
+      }
+      D.kcost[o][kk] = K.dlqr && K.integ ? K.dt * cst : cst;
+      D.dvp[kk] = feas ? 0. : p2;
+    }
+    __syncthreads();  // xn complete; red / pa / pdyn free
+    if (running && tid < nx) {
+      D.xnext[o][D.run(b, t) * D.sX + tid] = xn[tid];
+      bad |= bad_entry(xn[tid]);
+    }
+  }
+  // cost_try in knot order with raiseIfNaN on every partial sum (fddp.cpp:
+  // 189-196); dv: terminal first, then t = 0..T-1 (fddp.cpp:110-119)
+  __syncthreads();
+  if (tid == 0) {
+    const double* kc = D.kcost[o] + D.knot(b, 0);
+    double ct = 0.;
+    bool nan = false;
+    for (int t = 0; t <= T; ++t) {
+      ct += kc[t];
+      nan |= raise_if_nan(ct);
+    }
+    double acc = 0.;
+    if (!feas) {
+      const double* dvp = D.dvp + D.knot(b, 0);
+      acc += dvp[T];
+      for (int t = 0; t < T; ++t) acc += dvp[t];
+    }
+    red[0] = ct;
+    red[1] = acc;
+    bad |= nan;
+  }
+  const bool any_bad = wg_any(bad, flag);
+  cost_try = red[0];
+  dv = red[1];
+  __syncthreads();
+  return !any_bad;
+}
+
+}  // namespace fddp

@@ -23,6 +23,7 @@
 #include "../../include/fddp_hip.h"
 #include "fddp_device.hpp"
 #include "fddp_kernels.hpp"
+#include "fast_path.hpp"
 #include "bwd_mfma.hpp"
 
 using namespace fddp;
@@ -86,6 +87,8 @@ struct fddp_handle_s {
   double* dbg[7] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   int64_t bytes = 0;
   size_t bwd_smem = 0, fwd_smem = 0, calc_smem = 0, cdiff_smem = 0;
+  bool fast = false;  // dense-knot fast path (fast_path.hpp) for calc / calcDiff / forward
+  size_t fused_smem = 0, fwd_fast_smem = 0;
   int64_t pcap = 0;  // doubles of LDS reserved for a resident parameter block
   int bwd_variant = 0;  // 0 generic, else NTL*10+MTL of the MFMA sweep
   // timing
@@ -168,7 +171,16 @@ Prm to_prm(const fddp_params& p) {
 }
 
 // ---- kernel launchers ------------------------------------------------------
+int launch_fused(fddp_handle* h, int sel_calc, int sel_diff, int gaps) {
+  Timed tm(h, sel_diff >= 0 ? 1 : 0);
+  const Dev& D = h->D;
+  hipLaunchKernelGGL(calc_fused_kernel<kNT>, dim3(D.B), dim3(kNT), h->fused_smem, h->stream, D, sel_calc, sel_diff,
+                     gaps, h->pcap);
+  LAUNCH_CHECK();
+  return FDDP_OK;
+}
 int launch_calc(fddp_handle* h, int sel) {
+  if (h->fast) return launch_fused(h, sel, -1, 0);
   Timed tm(h, 0);
   const Dev& D = h->D;
   hipLaunchKernelGGL(calc_kernel<kNT>, dim3(D.B), dim3(kNT), h->calc_smem, h->stream, D, sel, h->pcap);
@@ -182,11 +194,24 @@ int launch_cost_sum(fddp_handle* h, int sel, double* out) {
   return FDDP_OK;
 }
 int launch_calc_diff(fddp_handle* h, int sel, int gaps) {
+  if (h->fast) return launch_fused(h, -1, sel, gaps);
   Timed tm(h, 1);
   const Dev& D = h->D;
   hipLaunchKernelGGL(calc_diff_kernel<kNT>, dim3(D.B), dim3(kNT), h->cdiff_smem, h->stream, D, sel, gaps, h->pcap);
   LAUNCH_CHECK();
   return FDDP_OK;
+}
+// problem.calc (sel_calc) + cost_ = sum of knot costs, then problem.calcDiff
+// (sel_diff, + gaps): one fused pass on the fast path.
+int launch_calc_then_diff(fddp_handle* h, int sel_calc, int sel_calc_sum, int sel_diff, int gaps) {
+  int rc;
+  if (h->fast) {
+    if ((rc = launch_fused(h, sel_calc, sel_diff, gaps))) return rc;
+    return launch_cost_sum(h, sel_calc_sum, nullptr);
+  }
+  if ((rc = launch_calc(h, sel_calc))) return rc;
+  if ((rc = launch_cost_sum(h, sel_calc_sum, nullptr))) return rc;
+  return launch_calc_diff(h, sel_diff, gaps);
 }
 template <int NTL, int MTL>
 void launch_bwd_mfma(fddp_handle* h, int mode) {
@@ -223,8 +248,12 @@ int setup_bwd_mfma(fddp_handle* h) {
 int launch_forward(fddp_handle* h, int mode, double alpha, int* count) {
   Timed tm(h, 3);
   const Dev& D = h->D;
-  hipLaunchKernelGGL(forward_kernel<kNT>, dim3(D.B), dim3(kNT), h->fwd_smem, h->stream, D, to_prm(h->prm), mode,
-                     alpha, count, h->pcap);
+  if (h->fast)
+    hipLaunchKernelGGL((forward_kernel<kNT, true>), dim3(D.B), dim3(kNT), h->fwd_fast_smem, h->stream, D,
+                       to_prm(h->prm), mode, alpha, count, h->pcap);
+  else
+    hipLaunchKernelGGL((forward_kernel<kNT, false>), dim3(D.B), dim3(kNT), h->fwd_smem, h->stream, D,
+                       to_prm(h->prm), mode, alpha, count, h->pcap);
   LAUNCH_CHECK();
   return FDDP_OK;
 }
@@ -403,9 +432,19 @@ int fddp_create(const fddp_dims* dims, const fddp_knot_desc* knots, const double
     const int64_t budget = (150 * 1024) / 8 - (2 * D.sX + D.sM + 5 * (kNT / kWave) + 16);
     h->pcap = pmax <= budget ? pad2(pmax) : 0;
   }
-  h->fwd_smem = sizeof(double) * (h->pcap + 2 * D.sX + D.sM + 5 * (kNT / kWave) + 16);
-  h->calc_smem = h->fwd_smem;
+  h->fwd_smem = sizeof(double) * (h->pcap + fwd_lds_doubles<kNT, false>(D.sX, D.sN, D.sM));
+  h->calc_smem = sizeof(double) * (h->pcap + 2 * D.sX + D.sM + 5 * (kNT / kWave) + 16);
   h->cdiff_smem = sizeof(double) * (h->pcap + D.sX + D.sM);
+  {  // dense-knot fast path: every knot LQR / Euler∘DiffLQR, block LDS-resident
+    bool dense = h->pcap > 0 && d.nx == d.ndx && d.nx <= kNT && d.nu_max <= kNT;
+    for (int t = 0; t <= d.T; ++t)
+      dense = dense && (knots[t].kind == FDDP_KNOT_LQR || knots[t].kind == FDDP_KNOT_EULER_DIFFLQR);
+    h->fused_smem = sizeof(double) * (h->pcap + 2 * D.sX + D.sM + 3 * kNT + 16);
+    h->fwd_fast_smem = sizeof(double) * (h->pcap + fwd_lds_doubles<kNT, true>(D.sX, D.sN, D.sM));
+    const char* env = std::getenv("FDDP_FAST");
+    const bool off = env && env[0] == '0';
+    h->fast = dense && !off && h->fused_smem <= 160 * 1024 && h->fwd_fast_smem <= 160 * 1024;
+  }
 
   double* p = nullptr;
   if ((rc = dalloc(h, &p, n_params))) return bail(rc);
@@ -455,8 +494,12 @@ int fddp_create(const fddp_dims* dims, const fddp_knot_desc* knots, const double
     return bail(fail(FDDP_ERR_RUNTIME, "upload state"));
   if (hipFuncSetAttribute((const void*)backward_kernel<kNT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)h->bwd_smem) != hipSuccess ||
-      hipFuncSetAttribute((const void*)forward_kernel<kNT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+      hipFuncSetAttribute((const void*)forward_kernel<kNT, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)h->fwd_smem) != hipSuccess ||
+      hipFuncSetAttribute((const void*)forward_kernel<kNT, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)h->fwd_fast_smem) != hipSuccess ||
+      hipFuncSetAttribute((const void*)calc_fused_kernel<kNT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)h->fused_smem) != hipSuccess ||
       hipFuncSetAttribute((const void*)calc_kernel<kNT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)h->calc_smem) != hipSuccess ||
       hipFuncSetAttribute((const void*)calc_diff_kernel<kNT>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -611,10 +654,10 @@ int fddp_solve(fddp_handle* h, int maxiter, int is_feasible, double reg_init, fd
   int rc;
   for (int it = 0; it < maxiter; ++it) {
     if (it == 0) {
-      if ((rc = launch_calc(h, SEL_ACTIVE))) return rc;
-      if ((rc = launch_cost_sum(h, SEL_ACTIVE, nullptr))) return rc;
+      if ((rc = launch_calc_then_diff(h, SEL_ACTIVE, SEL_ACTIVE, SEL_RECALC, 1))) return rc;
+    } else {
+      if ((rc = launch_calc_diff(h, SEL_RECALC, 1))) return rc;
     }
-    if ((rc = launch_calc_diff(h, SEL_RECALC, 1))) return rc;
     if ((rc = launch_backward(h, 0))) return rc;
     HIP_TRY(hipMemsetAsync(h->d_count, 0, sizeof(int), h->stream));
     if ((rc = launch_forward(h, 0, 1., h->d_count))) return rc;
@@ -695,9 +738,7 @@ int fddp_compute_direction(fddp_handle* h, int recalc, int32_t* status) {
   DeviceGuard g(h->device);
   int rc;
   if (recalc) {
-    if ((rc = launch_calc(h, SEL_ITER0))) return rc;
-    if ((rc = launch_cost_sum(h, SEL_ITER0, nullptr))) return rc;
-    if ((rc = launch_calc_diff(h, SEL_ALL, 1))) return rc;
+    if ((rc = launch_calc_then_diff(h, SEL_ITER0, SEL_ITER0, SEL_ALL, 1))) return rc;
     if ((rc = launch_cost_sum(h, SEL_ALL, nullptr))) return rc;
   }
   if ((rc = launch_backward(h, 1))) return rc;

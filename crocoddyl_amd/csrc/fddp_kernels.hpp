@@ -602,7 +602,21 @@ __device__ __forceinline__ bool fwd_trial(const Dev& D, int b, const ElemState& 
   return true;
 }
 
-template <int NT>
+template <int NT, bool FAST>
+__device__ __forceinline__ bool fwd_trial_fast(const Dev& D, int b, const ElemState& s, double alpha, double* xu,
+                                               double* dxv, double* xn, double* pa, double* pdyn, double* red,
+                                               int* flag, double& cost_try, double& dv, double* pl, int64_t pcap,
+                                               const double*& cached);
+
+// Forward-pass LDS beyond the parameter block (doubles): generic trial
+// [xv sX | uv sM | xn sX | red 5*NW+8 | flag], fast trial
+// [xu sX+sM | dxv sN | xn sX | pa NT | pdyn NT | red 24 | flag].
+template <int NT, bool FAST>
+__host__ __device__ inline int64_t fwd_lds_doubles(int64_t sX, int64_t sN, int64_t sM) {
+  return FAST ? (sX + sM) + sN + sX + 2 * NT + 24 + 2 : 2 * sX + sM + 5 * (NT / 64) + 8 + 2;
+}
+
+template <int NT, bool FAST>
 __global__ __launch_bounds__(NT) void forward_kernel(Dev D, Prm prm, int mode, double alpha1, int* active_count,
                                                      int64_t pcap) {
   const int b = blockIdx.x;
@@ -611,15 +625,34 @@ __global__ __launch_bounds__(NT) void forward_kernel(Dev D, Prm prm, int mode, d
   extern __shared__ __attribute__((aligned(16))) double sm[];
   double* pl = sm;
   const double* cached = nullptr;
-  double* xv = pl + pcap;
-  double* uv = xv + D.sX;
-  double* xn = uv + D.sM;
-  double* red = xn + D.sX;
-  int* flag = (int*)(red + 5 * (NT / kWave) + 8);
+  double *xv, *uv, *xn, *red, *dxv = nullptr, *pa = nullptr, *pdyn = nullptr;
+  int* flag;
+  if (FAST) {
+    xv = pl + pcap;             // xu: x then u
+    uv = xv + D.sX;
+    dxv = xv + D.sX + D.sM;
+    xn = dxv + D.sN;
+    pa = xn + D.sX;
+    pdyn = pa + NT;
+    red = pdyn + NT;
+    flag = (int*)(red + 24);
+  } else {
+    xv = pl + pcap;
+    uv = xv + D.sX;
+    xn = uv + D.sM;
+    red = xn + D.sX;
+    flag = (int*)(red + 5 * (NT / kWave) + 8);
+  }
   ElemState s = *st;
+  auto trial = [&](double alpha, double& ct, double& dv) {
+    if constexpr (FAST)
+      return fwd_trial_fast<NT, true>(D, b, s, alpha, xv, dxv, xn, pa, pdyn, red, flag, ct, dv, pl, pcap, cached);
+    else
+      return fwd_trial<NT>(D, b, s, alpha, xv, uv, xn, red, flag, ct, dv, pl, pcap, cached);
+  };
   if (mode == 1) {
     double ct, dv;
-    const bool ok = fwd_trial<NT>(D, b, s, alpha1, xv, uv, xn, red, flag, ct, dv, pl, pcap, cached);
+    const bool ok = trial(alpha1, ct, dv);
     if (threadIdx.x == 0) {
       st->fwd_fail = ok ? 0 : 1;
       st->cost_try = ct;
@@ -634,7 +667,7 @@ __global__ __launch_bounds__(NT) void forward_kernel(Dev D, Prm prm, int mode, d
     const double alpha = prm.alphas[a];
     s.steplength = alpha;
     double ct, dv;
-    if (!fwd_trial<NT>(D, b, s, alpha, xv, uv, xn, red, flag, ct, dv, pl, pcap, cached)) continue;
+    if (!trial(alpha, ct, dv)) continue;
     s.cost_try = ct;
     s.dV = s.cost - ct;
     s.dv = dv;
