@@ -182,71 +182,53 @@ __device__ __forceinline__ void dense_xnext(const DenseKnot& K, int nx, int i, d
   }
 }
 
-// Element (i, j) of a dense knot's derivative blocks (knot_calc_diff).
-__device__ __forceinline__ double dense_fx(const DenseKnot& K, int n, int i, int j) {
-  if (!K.dlqr) return K.F[j * n + i];
-  if (!K.integ) return i == j ? 1. : 0.;
-  const int nq = n / 2, nv = nq;
-  const double dt = K.dt, dt2 = dt * dt;
-  const int r = i < nv ? i : i - nv;
-  const double da = K.F[j * nq + r];  // [Fq | Fv] column j
-  double f = i < nv ? da * dt2 : da * dt;
-  if (i < nv && j == nv + i) f += dt;  // topRightCorner(nv,nv).diagonal() += dt
-  if (i == j) f += 1.;                 // Jintegrate(first, addto)
-  return f;
-}
-__device__ __forceinline__ double dense_fu(const DenseKnot& K, int n, int nu, int i, int j) {
-  if (j >= nu) return 0.;
-  if (!K.dlqr) return K.F[(n + j) * n + i];
-  if (!K.integ) return 0.;
-  const int nq = n / 2, nv = nq;
-  const int r = i < nv ? i : i - nv;
-  const double da = K.F[(n + j) * nq + r];  // Fu column j, after [Fq | Fv]
-  return i < nv ? da * K.dt * K.dt : da * K.dt;
-}
-
-// Streams one knot's derivative blocks out (coalesced, every thread).
+// Streams one knot's derivative blocks out. Thread -> (row i, column
+// segment): the per-row factors of the Euler integration are per-thread
+// constants, each column is a coalesced store across consecutive rows.
 template <int NT>
 __device__ __forceinline__ void dense_write_blocks(const DenseKnot& K, int n, int m, int nu, const KnotDiffOut& o) {
   const int tid = threadIdx.x;
-  const double sc = K.sc;
   const bool scale = K.dlqr && K.integ;
+  const double sc = scale ? K.sc : 1.;
   {
-    const int tot = n * n;
-    const float inv = 1.f / (float)n;
-    for (int e = tid; e < tot; e += NT) {
-      int j = (int)((float)e * inv);
-      int i = e - j * n;
-      if (i < 0) { --j; i += n; }
-      if (i >= n) { ++j; i -= n; }
-      o.Fx[e] = dense_fx(K, n, i, j);
-      const double l = K.Lxx[e];
-      o.Lxx[e] = scale ? sc * l : l;
+    const RowSeg r(n, NT, tid);
+    if (r.on) {
+      const int i = r.i;
+      // Fx(i, j) = a_i * F(ri, j) + [j == jd] dt + [j == i]   (Euler∘DiffLQR)
+      //          = F(i, j)                                   (LQR)
+      int ldf = n, ri = i, jd = -1;
+      double a = 1., dtd = 0.;
+      if (K.dlqr) {
+        const int nv = n / 2;
+        ldf = nv;
+        ri = i < nv ? i : i - nv;
+        a = K.integ ? (i < nv ? K.dt * K.dt : K.dt) : 0.;
+        jd = (K.integ && i < nv) ? nv + i : -1;
+        dtd = K.dt;
+      }
+      for (int j = r.g; j < n; j += r.G) {
+        double f = K.dlqr ? (K.integ ? a * K.F[j * ldf + ri] : 0.) : K.F[j * n + i];
+        if (j == jd) f += dtd;
+        if (K.dlqr && j == i) f += 1.;
+        o.Fx[j * n + i] = f;
+        o.Lxx[j * n + i] = sc * K.Lxx[j * n + i];
+      }
+      for (int j = r.g; j < m; j += r.G) {
+        double f = 0., l = 0.;
+        if (j < nu) {
+          f = K.dlqr ? (K.integ ? a * K.F[(n + j) * ldf + ri] : 0.) : K.F[(n + j) * n + i];
+          l = sc * K.Lxu[j * n + i];
+        }
+        o.Fu[j * n + i] = f;
+        o.Lxu[j * n + i] = l;
+      }
     }
   }
   {
-    const int tot = n * m;
-    const float inv = 1.f / (float)n;
-    for (int e = tid; e < tot; e += NT) {
-      int j = (int)((float)e * inv);
-      int i = e - j * n;
-      if (i < 0) { --j; i += n; }
-      if (i >= n) { ++j; i -= n; }
-      o.Fu[e] = dense_fu(K, n, nu, i, j);
-      const double l = j < nu ? K.Lxu[e] : 0.;
-      o.Lxu[e] = scale ? sc * l : l;
-    }
-  }
-  {
-    const int tot = m * m;
-    const float inv = 1.f / (float)m;
-    for (int e = tid; e < tot; e += NT) {
-      int j = (int)((float)e * inv);
-      int i = e - j * m;
-      if (i < 0) { --j; i += m; }
-      if (i >= m) { ++j; i -= m; }
-      const double l = (i < nu && j < nu) ? K.Luu[j * nu + i] : 0.;
-      o.Luu[e] = scale ? sc * l : l;
+    const RowSeg r(m, NT, tid);
+    if (r.on) {
+      const int i = r.i;
+      for (int j = r.g; j < m; j += r.G) o.Luu[j * m + i] = (i < nu && j < nu) ? sc * K.Luu[j * nu + i] : 0.;
     }
   }
 }
@@ -276,15 +258,16 @@ __global__ __launch_bounds__(NT) void calc_fused_kernel(Dev D, int sel_calc, int
   const int c = s.cur, nx = D.nx, n = D.n, m = D.m, T = D.T, tid = threadIdx.x;
   const int lane = tid & 63, wid = tid >> 6;
   const double* cached = nullptr;
-  // x and u of knot t+1 are loaded into registers while knot t computes
-  // (thread i holds x_i, u_i; nx, m <= NT on this path)
-  double px = 0., pu = 0.;
-  auto prefetch = [&](int t) {
-    if (t > T) return;
-    if (tid < nx) px = D.xs[c][D.knot(b, t) * D.sX + tid];
-    if (t < T && tid < m) pu = D.us[c][D.run(b, t) * D.sM + tid];
+  // x and u of knots t+1..t+PD are in flight in registers while knot t
+  // computes (a rotating window; thread i holds x_i, u_i; nx, m <= NT here)
+  constexpr int PD = 4;
+  double px[PD], pu[PD];
+  auto fetch = [&](int t, double& x_, double& u_) {
+    x_ = (t <= T && tid < nx) ? D.xs[c][D.knot(b, t) * D.sX + tid] : 0.;
+    u_ = (t < T && tid < m) ? D.us[c][D.run(b, t) * D.sM + tid] : 0.;
   };
-  prefetch(0);
+#pragma unroll
+  for (int q = 0; q < PD; ++q) fetch(q, px[q], pu[q]);
   for (int t = 0; t <= T; ++t) {
     const fddp_knot_desc kd = D.knots[t];
     const double* P = stage_params<NT>(D.pblock(b, t), block_doubles_dev(kd.kind, nx, kd.nu), pl, pcap, cached);
@@ -292,9 +275,14 @@ __global__ __launch_bounds__(NT) void calc_fused_kernel(Dev D, int sel_calc, int
     const bool running = t < T;
     const int nu = kd.nu;
     const bool use_u = running && nu > 0;
-    if (tid < nx) xu[tid] = px;
-    if (use_u && tid < nu) xu[nx + tid] = pu;
-    prefetch(t + 1);
+    if (tid < nx) xu[tid] = px[0];
+    if (use_u && tid < nu) xu[nx + tid] = pu[0];
+#pragma unroll
+    for (int q = 0; q + 1 < PD; ++q) {
+      px[q] = px[q + 1];
+      pu[q] = pu[q + 1];
+    }
+    fetch(t + PD, px[PD - 1], pu[PD - 1]);
     __syncthreads();
     const DenseKnot K(kd.kind, P, nx, nu);
     const bool want_dyn = do_calc && running;
@@ -350,10 +338,10 @@ __global__ __launch_bounds__(NT) void calc_fused_kernel(Dev D, int sel_calc, int
           const double* x0 = D.x0 + (int64_t)b * D.sX;
           for (int i = tid; i < n; i += NT) f[i] = x0[i] - xu[i];
         }
-        if (running && tid < n) {  // px holds xs[t+1][tid] now
+        if (running && tid < n) {  // px[0] holds xs[t+1][tid] now
           double* f = D.fs + D.knot(b, t + 1) * D.sN;
           const double* xng = D.xnext[c] + D.run(b, t) * D.sX;
-          f[tid] = (want_dyn ? xn[tid] : xng[tid]) - px;
+          f[tid] = (want_dyn ? xn[tid] : xng[tid]) - px[0];
         }
       } else if (!s.was_feasible) {  // closing the gaps
         double* f = D.fs + kk * D.sN;
@@ -391,41 +379,56 @@ __device__ __forceinline__ bool fwd_trial_fast(const Dev& D, int b, const ElemSt
   constexpr int KMAX = 16;
   const int kcols = rk.on ? (n - rk.g + rk.G - 1) / rk.G : 0;
   const bool kreg = (n + rk.G - 1) / rk.G <= KMAX;
-  double pK[KMAX];
-  double pxs = 0., pfs = 0., pvf = 0., pus = 0., pkv = 0.;
-  auto prefetch = [&](int t) {
+  // knots t+1..t+PD in flight in registers (rotating window; deeper windows
+  // measured slower: register pressure)
+  constexpr int PD = 1;
+  double pK[PD][KMAX];
+  double pxs[PD], pfs[PD], pvf[PD], pus[PD], pkv[PD];
+  auto fetch = [&](int t, int q) {
+    pxs[q] = pfs[q] = pvf[q] = pus[q] = pkv[q] = 0.;
     if (t > T) return;
     const int64_t kk = D.knot(b, t);
     if (tid < nx) {
-      pxs = D.xs[c][kk * D.sX + tid];
-      pfs = D.fs[kk * D.sN + tid];
-      pvf = feas ? 0. : D.Vxxfs[kk * D.sN + tid];
+      pxs[q] = D.xs[c][kk * D.sX + tid];
+      pfs[q] = D.fs[kk * D.sN + tid];
+      pvf[q] = feas ? 0. : D.Vxxfs[kk * D.sN + tid];
     }
     if (t < T) {
       const int64_t rr = D.run(b, t);
       if (tid < m) {
-        pus = D.us[c][rr * D.sM + tid];
-        pkv = D.k[rr * D.sM + tid];
+        pus[q] = D.us[c][rr * D.sM + tid];
+        pkv[q] = D.k[rr * D.sM + tid];
       }
       if (kreg) {
         const double* Kt = D.K + rr * D.sNM;
 #pragma unroll
-        for (int q = 0; q < KMAX; ++q) pK[q] = q < kcols ? Kt[(rk.g + q * rk.G) * m + rk.i] : 0.;
+        for (int j = 0; j < KMAX; ++j) pK[q][j] = j < kcols ? Kt[(rk.g + j * rk.G) * m + rk.i] : 0.;
       }
     }
   };
-  prefetch(0);
+#pragma unroll
+  for (int q = 0; q < PD; ++q) fetch(q, q);
   __syncthreads();
   for (int t = 0; t <= T; ++t) {
     const int64_t kk = D.knot(b, t);
     const bool running = t < T;
     const fddp_knot_desc kd = D.knots[t];
     const int nu = kd.nu;
-    const double cxs = pxs, cfs = pfs, cvf = pvf, cus = pus, ckv = pkv;
+    const double cxs = pxs[0], cfs = pfs[0], cvf = pvf[0], cus = pus[0], ckv = pkv[0];
     double cK[KMAX];
 #pragma unroll
-    for (int q = 0; q < KMAX; ++q) cK[q] = pK[q];
-    prefetch(t + 1);
+    for (int j = 0; j < KMAX; ++j) cK[j] = pK[0][j];
+#pragma unroll
+    for (int q = 0; q + 1 < PD; ++q) {
+      pxs[q] = pxs[q + 1];
+      pfs[q] = pfs[q + 1];
+      pvf[q] = pvf[q + 1];
+      pus[q] = pus[q + 1];
+      pkv[q] = pkv[q + 1];
+#pragma unroll
+      for (int j = 0; j < KMAX; ++j) pK[q][j] = pK[q + 1][j];
+    }
+    fetch(t + PD, PD - 1);
     // xs_try[t] = xnext  or  integrate(xnext, fs[t] * (alpha - 1)); dx = xs_try - xs
     double pd = 0.;
     if (tid < nx) {

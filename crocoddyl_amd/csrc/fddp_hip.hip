@@ -33,6 +33,7 @@ namespace {
 thread_local std::string g_err;
 
 constexpr int kNT = 256;
+constexpr int kNTF = 512;  // fused calc/calcDiff: 8 waves per CU keep the derivative stores streaming
 
 int fail(int code, const std::string& msg) {
   g_err = msg;
@@ -174,7 +175,7 @@ Prm to_prm(const fddp_params& p) {
 int launch_fused(fddp_handle* h, int sel_calc, int sel_diff, int gaps) {
   Timed tm(h, sel_diff >= 0 ? 1 : 0);
   const Dev& D = h->D;
-  hipLaunchKernelGGL(calc_fused_kernel<kNT>, dim3(D.B), dim3(kNT), h->fused_smem, h->stream, D, sel_calc, sel_diff,
+  hipLaunchKernelGGL(calc_fused_kernel<kNTF>, dim3(D.B), dim3(kNTF), h->fused_smem, h->stream, D, sel_calc, sel_diff,
                      gaps, h->pcap);
   LAUNCH_CHECK();
   return FDDP_OK;
@@ -436,10 +437,10 @@ int fddp_create(const fddp_dims* dims, const fddp_knot_desc* knots, const double
   h->calc_smem = sizeof(double) * (h->pcap + 2 * D.sX + D.sM + 5 * (kNT / kWave) + 16);
   h->cdiff_smem = sizeof(double) * (h->pcap + D.sX + D.sM);
   {  // dense-knot fast path: every knot LQR / Euler∘DiffLQR, block LDS-resident
-    bool dense = h->pcap > 0 && d.nx == d.ndx && d.nx <= kNT && d.nu_max <= kNT;
+    bool dense = h->pcap > 0 && d.nx == d.ndx && d.nx <= kNT && d.nu_max <= kNT && d.nx <= kNTF;
     for (int t = 0; t <= d.T; ++t)
       dense = dense && (knots[t].kind == FDDP_KNOT_LQR || knots[t].kind == FDDP_KNOT_EULER_DIFFLQR);
-    h->fused_smem = sizeof(double) * (h->pcap + 2 * D.sX + D.sM + 3 * kNT + 16);
+    h->fused_smem = sizeof(double) * (h->pcap + 2 * D.sX + D.sM + 3 * kNTF + 16);
     h->fwd_fast_smem = sizeof(double) * (h->pcap + fwd_lds_doubles<kNT, true>(D.sX, D.sN, D.sM));
     const char* env = std::getenv("FDDP_FAST");
     const bool off = env && env[0] == '0';
@@ -498,7 +499,7 @@ int fddp_create(const fddp_dims* dims, const fddp_knot_desc* knots, const double
                           (int)h->fwd_smem) != hipSuccess ||
       hipFuncSetAttribute((const void*)forward_kernel<kNT, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)h->fwd_fast_smem) != hipSuccess ||
-      hipFuncSetAttribute((const void*)calc_fused_kernel<kNT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+      hipFuncSetAttribute((const void*)calc_fused_kernel<kNTF>, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)h->fused_smem) != hipSuccess ||
       hipFuncSetAttribute((const void*)calc_kernel<kNT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)h->calc_smem) != hipSuccess ||
