@@ -51,9 +51,11 @@ typedef __attribute__((address_space(3))) void* lds_void_ptr;
 // longer on the sweep's critical path; dependent f64 FMA latency is 32 cycles)
 __device__ __forceinline__ double rcp_f64(double d) {
   double x = __builtin_amdgcn_rcp(d);
+#ifndef FDDP_RCP_NO_NEWTON
   x = fma(fma(-d, x, 1.), x, x);
 #ifndef FDDP_RCP_ONE_NEWTON
   x = fma(fma(-d, x, 1.), x, x);
+#endif
 #endif
   return x;
 }
@@ -74,33 +76,57 @@ __device__ __forceinline__ void dma_barrier() {
 // destination of one wave instruction is a wave-uniform base + lane * size).
 // dma_vec: nd contiguous doubles (16-B aligned both sides) over the 4 waves;
 // an odd tail double moves as two 4-byte DMAs.
+template <int NW>  // NW participating waves, wid = this wave's rank among them
 __device__ __forceinline__ void dma_vec(double* lds, const double* g, int nd, int wid, int lane) {
   const int nch = nd >> 1;
-  for (int base = wid * 64; base < nch; base += 256) {
+  for (int base = wid * 64; base < nch; base += NW * 64) {
     const int ch = base + lane;
     if (ch < nch) __builtin_amdgcn_global_load_lds(g + 2 * ch, (lds_void_ptr)(lds + 2 * base), 16, 0, 0);
   }
-  if ((nd & 1) && wid == 3 && lane < 2)
+  if ((nd & 1) && wid == NW - 1 && lane < 2)
     __builtin_amdgcn_global_load_lds((const char*)(g + nd - 1) + 4 * lane, (lds_void_ptr)(lds + nd - 1), 4, 0, 0);
 }
 // dma_cols: ncols columns of nr doubles (global ld nr) into LDS columns of
 // stride ld (a multiple of 2); one column per wave instruction (16-B chunks
 // when nr is even, else 4-byte pieces). Rows [nr, ld) are left untouched.
+template <int NW>
 __device__ __forceinline__ void dma_cols(double* lds, int ld, const double* g, int nr, int ncols, int wid, int lane) {
   if ((nr & 1) == 0) {
     const int nch = nr >> 1;
-    for (int col = wid; col < ncols; col += 4)
+    for (int col = wid; col < ncols; col += NW)
       for (int base = 0; base < nch; base += 64)
         if (base + lane < nch)
           __builtin_amdgcn_global_load_lds(g + (int64_t)col * nr + 2 * (base + lane),
                                            (lds_void_ptr)(lds + col * ld + 2 * base), 16, 0, 0);
   } else {
     const int nw = 2 * nr;
-    for (int col = wid; col < ncols; col += 4)
+    for (int col = wid; col < ncols; col += NW)
       for (int base = 0; base < nw; base += 64)
         if (base + lane < nw)
           __builtin_amdgcn_global_load_lds((const char*)(g + (int64_t)col * nr) + 4 * (base + lane),
                                            (lds_void_ptr)((char*)(lds + col * ld) + 4 * base), 4, 0, 0);
+  }
+}
+
+// The columns of an n x ncols column-major global block into LDS columns of
+// LDZ doubles (LDZ even, nr even): every wave instruction moves a full 1 KiB
+// (64 lanes x 16 B, a per-lane gather), the LDZ - nr padding rows of each
+// column are filled from a 16-byte zero source. 39% fewer instructions than
+// one per column at n = 76, and a DMA instruction costs ~60-185 cycles of
+// issue whatever its size.
+template <int NWD, int LDZ>
+__device__ __forceinline__ void dma_cols_full(double* lds, const double* g, int nr, int ncols, const double* zero16,
+                                              int rank, int lane) {
+  constexpr int CPC = LDZ / 2;  // 16-B chunks per LDS column
+  const int dpc = nr >> 1;      // of which data
+  const int tot = ncols * CPC;
+  for (int base = rank * 64; base < tot; base += NWD * 64) {
+    const int e = base + lane;
+    if (e < tot) {
+      const int col = e / CPC, p = e - col * CPC;
+      const double* src = p < dpc ? g + (int64_t)col * nr + 2 * p : zero16;
+      __builtin_amdgcn_global_load_lds(src, (lds_void_ptr)(lds + 2 * base), 16, 0, 0);
+    }
   }
 }
 
@@ -109,9 +135,11 @@ struct MfmaCfg {
   static constexpr int NP = 16 * NTL;
   static constexpr int MP = 16 * MTL;
   static constexpr int JT = NTL + MTL;
-  // V / Qxu leading dimension = 16 (mod 32) doubles: the two 16-lane halves
-  // of a ds_read_b64 fragment read land on disjoint bank halves
-  static constexpr int LDV = (NP % 32 == 0) ? NP + 16 : NP;
+  // V / Qxu leading dimension = 2 (mod 4) doubles: 16 lanes stepping along
+  // the leading dimension hit 16 distinct bank pairs (stores of tiles in the
+  // transposed direction, the transposed P2 tiles), and a fragment read along
+  // it (lanes c consecutive, q rows apart) is nearly conflict-free
+  static constexpr int LDV = NP + 2;
   static constexpr int LDQ = MP;
   static_assert(MP <= 64, "u block must fit one wave for the factorisation");
   // LDS carve (doubles). Z = [Fx | Fu] is stored with the compile-time
@@ -129,11 +157,17 @@ struct MfmaCfg {
   static constexpr int oLu = oQu + MP;
   static constexpr int oKv = oLu + MP;  // kv + quuk: the sweep's 64-double row buffer (wave 0, P1)
   static constexpr int oQuuk = oKv + MP;
-  static constexpr int oRed = oKv + (2 * MP > 64 ? 2 * MP : 64);  // 5 sums x 4 waves
-  static constexpr int oFlag = oRed + 20;
+  static constexpr int oRed = oKv + (2 * MP > 64 ? 2 * MP : 64);  // 5 sums x up to 8 waves
+  static constexpr int oFlag = oRed + 40;  // flag; Quu-ready, G-done, P2-done counters (4 ints)
+  // Z column stride ZLD = NP - 2 (= 2 mod 4): the 16 lanes of a B fragment
+  // read 16 columns at a stride of 2*ZLD = 4 (mod 8) banks, conflict-free
+  // (a stride of NP was an 8-way conflict). k-steps past ZLD read the next
+  // column's first rows (or the 2 zero doubles after the last column); they
+  // only ever multiply the zero rows of Vxx' / G, so nothing changes.
+  static constexpr int ZLD = NP - 2;
   static constexpr int oZx = (oFlag + 2 + 1) & ~1;
-  static constexpr int oZu = oZx + NP * NP;
-  static constexpr int total = oZu + NP * MP;
+  static constexpr int oZu = oZx + NP * ZLD;
+  static constexpr int total = oZu + MP * ZLD + 2;
   static constexpr size_t bytes = sizeof(double) * total;
 };
 
@@ -239,25 +273,220 @@ __device__ __forceinline__ bool sym_sweep_inverse(const double* Quu, double* Qi,
   return bad;
 }
 
-// Compile-time ownership of Z's column blocks: wave 0 takes the u blocks
-// (Quu and its inverse), waves 1-3 share the x blocks by longest-processing-
-// time on their MFMA count (G: 4NTL x NTL, H tiles j >= i: 4NTL each). With
-// the plan static, every wave's code path has only its own tiles, statically
-// indexed registers and no per-tile predicates.
-template <int NTL, int MTL>
-struct BwdPlan {
-  int nown[4];
-  int blk[4][8];
-  constexpr BwdPlan() : nown{0, 0, 0, 0}, blk{} {
-    for (int u = 0; u < MTL; ++u) blk[0][nown[0]++] = NTL + u;
-    int load[4] = {0, 0, 0, 0};
-    for (int i = 0; i < NTL; ++i) {  // the cost decreases with i: LPT order
-      int best = 1;
-      for (int w = 2; w < 4; ++w)
-        if (load[w] < load[best]) best = w;
-      blk[best][nown[best]++] = i;
-      load[best] += NTL + (NTL - i + MTL);
+// Same sweep with each lane owning a BS x BS block of the matrix (BS = MP/8,
+// an 8 x 8 grid of blocks over the 64 lanes): per step one FMA per element
+// as before, but the column-k / row-k fix-ups touch BS elements of 8 lanes
+// instead of MP elements of 2 lanes, and the broadcast reads are 2 x BS
+// contiguous doubles. VALU-issue bound (f64 ops issue at 8 cycles), so this
+// is ~1.8x fewer cycles per pivot than the column-per-lane layout.
+template <int MP, int LDQ>
+__device__ __forceinline__ bool sym_sweep_inverse_blk(const double* Quu, double* Qi, double* rb, int m, int lane) {
+  constexpr int BS = MP / 8;
+  static_assert(MP % 8 == 0 && BS >= 1, "8 x 8 lane grid");
+  const int bi = lane >> 3, bj = lane & 7;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  double A[BS][BS];
+#pragma unroll
+  for (int a = 0; a < BS; ++a)
+#pragma unroll
+    for (int b = 0; b < BS; ++b) A[a][b] = Quu[(BS * bj + b) * LDQ + BS * bi + a];
+  bool bad = false;
+  if (bi == 0) {
+#pragma unroll
+    for (int b = 0; b < BS; ++b) rb[BS * bj + b] = A[0][b];
+  }
+#pragma unroll
+  for (int k = 0; k < MP; ++k) {
+    if (k < m) {
+      const int kb = k / BS, kr = k % BS;
+      const int k1 = k + 1, kb1 = k1 / BS, kr1 = k1 % BS;
+      (void)k1;
+      asm volatile("" ::: "memory");
+      const double d = rb[k];
+      double rowv[BS], colv[BS];
+#pragma unroll
+      for (int b = 0; b < BS; ++b) rowv[b] = rb[BS * bj + b];  // A(k, my columns)
+#pragma unroll
+      for (int a = 0; a < BS; ++a) colv[a] = rb[BS * bi + a];  // A(my rows, k) by symmetry
+      bad |= !(d > 0.);
+      const double dinv = rcp_f64(d);
+      double w[BS];
+#pragma unroll
+      for (int b = 0; b < BS; ++b) w[b] = rowv[b] * dinv;
+      const bool colk = bj == kb, rowk = bi == kb;
+      auto fix = [&](int a, int b, double v) {  // column-k / row-k / (k, k) fix-ups
+        if (colk && b == kr) v = colv[a] * dinv;
+        if (rowk && a == kr) v = (colk && b == kr) ? -dinv : w[b];
+        return v;
+      };
+      // next step's row first (register row kr1 holds it in lanes bi == kb1;
+      // after the last pivot the publish is dead and harmless)
+#pragma unroll
+      for (int b = 0; b < BS; ++b) A[kr1][b] = fix(kr1, b, fma(-colv[kr1], w[b], A[kr1][b]));
+      asm volatile("" ::: "memory");
+      if (bi == kb1) {
+#pragma unroll
+        for (int b = 0; b < BS; ++b) rb[BS * bj + b] = A[kr1][b];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int a = 0; a < BS; ++a) {
+        if (a == kr1) continue;
+#pragma unroll
+        for (int b = 0; b < BS; ++b) A[a][b] = fix(a, b, fma(-colv[a], w[b], A[a][b]));
+      }
     }
+  }
+#pragma unroll
+  for (int a = 0; a < BS; ++a)
+#pragma unroll
+    for (int b = 0; b < BS; ++b) {
+      const int i = BS * bi + a, j = BS * bj + b;
+      Qi[j * LDQ + i] = (i < m && j < m) ? -A[a][b] : 0.;
+    }
+  return bad;
+}
+
+// Compile-time work plan of the sweep: which wave owns which column blocks
+// of Z (G = Vxx' Z_i and the H tiles (i, j >= jstart(i))), and which wave
+// updates which Vxx tile in P2. With the plan static, every wave's code path
+// has only its own tiles, statically indexed registers and no per-tile
+// predicates.
+//  NW = 4: wave 0 takes the u blocks (Quu and its inverse), waves 1-3 share
+//          the x blocks by longest-processing-time on their MFMA count.
+//  NW = 8: two waves per SIMD (wave w on SIMD w % 4). Wave 0 only inverts Quu
+//          (VALU), sharing its SIMD with the smallest block; the other blocks
+//          are paired largest-with-smallest so that the SIMDs get equal MFMA
+//          loads, and the u-block owners signal wave 0 through an LDS counter
+//          as soon as their Quu rows are stored.
+// V tile (i, j), i <= j, is updated by the owner of i or of j (whoever has
+// fewer), using the K(:, i) or K(:, j) tiles that owner holds in registers.
+template <int NTL, int MTL>
+__host__ __device__ constexpr int bwd_block_cost(int i) {
+  return 4 * NTL * NTL + (i < NTL ? (NTL - i + MTL) : MTL) * 4 * NTL;
+}
+
+template <int NTL, int MTL, int NW>
+struct BwdPlan {
+  static constexpr int JT = NTL + MTL;
+  static_assert(NW == 4 || NW == 8, "4 or 8 waves");
+  static_assert(NW == 4 || JT <= 7, "8-wave plan: at most 7 column blocks");
+  int nown[8];
+  int blk[8][8];
+  int ntile[8];
+  int tile[8][24][2];
+  int uwaves;  // waves other than 0 that own u blocks
+  int gwaves;  // waves owning any block (they read Vxx' in G)
+  int ndma;    // waves issuing the LDS-DMA of the next knot's operands
+  int dmarank[8];
+  int xwaves;  // waves owning x blocks (the P3 consumers)
+  constexpr BwdPlan() : nown{}, blk{}, ntile{}, tile{}, uwaves(0), gwaves(0), ndma(0), dmarank{}, xwaves(0) {
+    int owner[16] = {};
+    if (NW == 4) {
+      for (int u = 0; u < MTL; ++u) {
+        blk[0][nown[0]++] = NTL + u;
+        owner[NTL + u] = 0;
+      }
+      int load[4] = {0, 0, 0, 0};
+      for (int i = 0; i < NTL; ++i) {  // the cost decreases with i: LPT order
+        int best = 1;
+        for (int w = 2; w < 4; ++w)
+          if (load[w] < load[best]) best = w;
+        blk[best][nown[best]++] = i;
+        owner[i] = best;
+        load[best] += bwd_block_cost<NTL, MTL>(i);
+      }
+    } else {
+      // eight items: the blocks, the inversion (-1) and empty slots (-2)
+      int item[8] = {}, cost[8] = {};
+      for (int k = 0; k < 8; ++k) {
+        item[k] = k < JT ? k : (k == JT ? -1 : -2);
+        // the inversion counts as the largest item, so it shares its SIMD with
+        // the smallest block (a u block, done before the inversion starts):
+        // it is VALU-issue bound, and an MFMA partner steals its issue slots
+        cost[k] = k < JT ? bwd_block_cost<NTL, MTL>(k) : (k == JT ? 1 << 20 : 0);
+      }
+      for (int a = 0; a < 8; ++a)  // sort by cost, descending
+        for (int b2 = a + 1; b2 < 8; ++b2)
+          if (cost[b2] > cost[a]) {
+            const int ti = item[a], tc = cost[a];
+            item[a] = item[b2];
+            cost[a] = cost[b2];
+            item[b2] = ti;
+            cost[b2] = tc;
+          }
+      int gp = 0;  // the pair holding the inversion goes to SIMD 0
+      for (int p = 0; p < 4; ++p)
+        if (item[p] == -1 || item[7 - p] == -1) gp = p;
+      int simd = 1;
+      for (int p = 0; p < 4; ++p) {
+        const int s2 = p == gp ? 0 : simd++;
+        const int a2 = item[p], b3 = item[7 - p];
+        int wa = s2, wb = s2 + 4;
+        if (b3 == -1) {  // the inversion item always takes wave 0
+          wa = s2 + 4;
+          wb = s2;
+        }
+        if (a2 >= 0) {
+          blk[wa][nown[wa]++] = a2;
+          owner[a2] = wa;
+        }
+        if (b3 >= 0) {
+          blk[wb][nown[wb]++] = b3;
+          owner[b3] = wb;
+        }
+      }
+    }
+    for (int w = 1; w < NW; ++w)
+      for (int o = 0; o < nown[w]; ++o)
+        if (blk[w][o] >= NTL) {
+          ++uwaves;
+          break;
+        }
+    for (int w = 0; w < NW; ++w) gwaves += nown[w] > 0 ? 1 : 0;
+    // the next knot's LDS-DMA: each instruction blocks its wave for a few
+    // hundred cycles, so in the 8-wave plan it goes to the waves that have no
+    // x blocks (no P2 / P3 MFMA work); they skip B2 (see bwd_knot)
+    for (int w = 0; w < NW; ++w) dmarank[w] = -1;
+    if (NW == 4) {
+      for (int w = 0; w < NW; ++w) dmarank[w] = ndma++;
+    } else {  // the waves without x blocks: no MFMA work in P2 / P3
+      for (int w = 0; w < NW; ++w)
+        if (!owns_x(w)) dmarank[w] = ndma++;
+    }
+    for (int w = 0; w < NW; ++w) xwaves += owns_x(w) ? 1 : 0;
+    // V tiles: the diagonal with its owner, the rest greedily
+    int vload[8] = {};
+    for (int i = 0; i < NTL; ++i) {
+      const int w = owner[i];
+      tile[w][ntile[w]][0] = i;
+      tile[w][ntile[w]][1] = i;
+      ++ntile[w];
+      vload[w] += 3;  // K(:, i) + the diagonal tile
+    }
+    for (int i = 0; i < NTL; ++i)
+      for (int j = i + 1; j < NTL; ++j) {
+        const int w = vload[owner[j]] < vload[owner[i]] ? owner[j] : owner[i];
+        tile[w][ntile[w]][0] = i;
+        tile[w][ntile[w]][1] = j;
+        ++ntile[w];
+        vload[w] += 1;
+      }
+  }
+  constexpr bool owns_x(int w) const {
+    for (int o = 0; o < nown[w]; ++o)
+      if (blk[w][o] < NTL) return true;
+    return false;
+  }
+  constexpr bool owns_u(int w) const {
+    for (int o = 0; o < nown[w]; ++o)
+      if (blk[w][o] >= NTL) return true;
+    return false;
+  }
+  constexpr int slot(int w, int blockid) const {  // index o of blockid in blk[w], or -1
+    for (int o = 0; o < nown[w]; ++o)
+      if (blk[w][o] == blockid) return o;
+    return -1;
   }
 };
 template <int NTL>
@@ -273,12 +502,12 @@ struct BwdLds {
 
 // One knot of the sweep, as executed by wave W (all four waves call this
 // with their own W; the barriers inside line up one to one).
-template <int NTL, int MTL, int W>
+template <int NTL, int MTL, int NW, int W>
 __device__ __forceinline__ bool bwd_knot(const Dev& D, const BwdLds& L, int b, int t, bool feas, double xreg,
                                          double ureg, Stamp& stamp) {
   using Cfg = MfmaCfg<NTL, MTL>;
-  constexpr int NP = Cfg::NP, MP = Cfg::MP, JT = Cfg::JT, LDV = Cfg::LDV, LDQ = Cfg::LDQ;
-  constexpr BwdPlan<NTL, MTL> P{};
+  constexpr int NP = Cfg::NP, MP = Cfg::MP, JT = Cfg::JT, LDV = Cfg::LDV, LDQ = Cfg::LDQ, ZLD = Cfg::ZLD;
+  constexpr BwdPlan<NTL, MTL, NW> P{};
   constexpr int NO = P.nown[W];
   constexpr int NA = NO > 0 ? NO : 1;
   static_assert(NO <= 8, "column blocks per wave");
@@ -291,6 +520,25 @@ __device__ __forceinline__ bool bwd_knot(const Dev& D, const BwdLds& L, int b, i
   const int q = lane >> 4, c = lane & 15;
   const bool xr = !isnan(xreg), ur = !isnan(ureg);
   const int64_t kk = D.knot(b, t), rr = D.run(b, t);
+  if constexpr (W != 0 && P.owns_u(W)) __builtin_amdgcn_s_setprio(2);  // Quu first: the inversion waits on it
+  // the next knot's operands (LDS-DMA; lands during P2 / P3)
+  auto issue_dma = [&]() {
+  if constexpr (P.dmarank[W] >= 0) {
+    if (t > 0) {  // operands of knot t-1 land during P2/P3
+      constexpr int ND = P.ndma, RK = P.dmarank[W];
+      const int64_t k1 = kk - 1;
+      if ((n & 1) == 0 && ZLD - n <= 2 * 64) {
+        dma_cols_full<ND, ZLD>(L.Zx, D.Fx + k1 * D.sNN, n, n, D.zero16, RK, lane);
+        dma_cols_full<ND, ZLD>(L.Zu, D.Fu + k1 * D.sNM, n, m, D.zero16, RK, lane);
+      } else {
+        dma_cols<ND>(L.Zx, ZLD, D.Fx + k1 * D.sNN, n, n, RK, lane);
+        dma_cols<ND>(L.Zu, ZLD, D.Fu + k1 * D.sNM, n, m, RK, lane);
+      }
+      dma_vec<ND>(L.lxv, D.Lx + k1 * D.sN, n, RK, lane);
+      dma_vec<ND>(L.luv, D.Lu + k1 * D.sM, m, RK, lane);
+    }
+  }
+  };
   double* V = L.V;
   double* Qxu = L.Qxu;
   double* Quu = L.Quu;
@@ -299,27 +547,33 @@ __device__ __forceinline__ bool bwd_knot(const Dev& D, const BwdLds& L, int b, i
   // ---- P1: cost blocks in accumulator layout (both triangles of Lxx: Qxx
   // uses its symmetric part, which the reference reaches through its Vxx
   // symmetrisation); their latency is covered by the G loop
-  double Lp[NA][NTL][4][2];
+  // Lv: both triangles of Lxx at this wave's P2 V tiles (Qxx uses the
+  // symmetric part of Lxx, which the reference reaches through its Vxx
+  // symmetrisation; it is added to the G^T Z part in P2). Lq: the Lxu / Luu
+  // inits of this wave's Qxu / Quu tiles.
+  constexpr int NVT = P.ntile[W] > 0 ? P.ntile[W] : 1;
+  double Lv[NVT][4][2];
   double Lq[NA][MTL][4];
   {
     const double* Lxx = D.Lxx + kk * D.sNN;
     const double* Lxu = D.Lxu + kk * D.sNM;
     const double* Luu = D.Luu + kk * D.sMM;
 #pragma unroll
+    for (int k3 = 0; k3 < P.ntile[W]; ++k3) {
+      const int i = P.tile[W][k3][0], j = P.tile[W][k3][1];
+      const bool rowf = P.slot(W, i) >= 0;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        // the Qxx(i, j) element that acc[r] of this tile holds in P2
+        const int R = rowf ? 16 * i + q + 4 * r : 16 * i + c, C = rowf ? 16 * j + c : 16 * j + q + 4 * r;
+        const bool ok = R < n && C < n;
+        Lv[k3][r][0] = ok ? Lxx[(int64_t)C * n + R] : 0.;
+        Lv[k3][r][1] = ok ? Lxx[(int64_t)R * n + C] : 0.;
+      }
+    }
+#pragma unroll
     for (int o = 0; o < NO; ++o) {
       const int i = P.blk[W][o];
-#pragma unroll
-      for (int j = 0; j < NTL; ++j) {
-        if (j >= bwd_jstart<NTL>(i)) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int R = 16 * i + q + 4 * r, C = 16 * j + c;
-            const bool ok = R < n && C < n;
-            Lp[o][j][r][0] = ok ? Lxx[(int64_t)C * n + R] : 0.;
-            Lp[o][j][r][1] = ok ? Lxx[(int64_t)R * n + C] : 0.;
-          }
-        }
-      }
 #pragma unroll
       for (int ju = 0; ju < MTL; ++ju)
 #pragma unroll
@@ -357,7 +611,7 @@ __device__ __forceinline__ bool bwd_knot(const Dev& D, const BwdLds& L, int b, i
 #pragma unroll
     for (int o = 0; o < NO; ++o) {
       const int i = P.blk[W][o];
-      zf[buf][o] = i < NTL ? L.Zx[(16 * i + c) * NP + row] : L.Zu[(16 * (i - NTL) + c) * NP + row];
+      zf[buf][o] = i < NTL ? L.Zx[(16 * i + c) * ZLD + row] : L.Zu[(16 * (i - NTL) + c) * ZLD + row];
     }
   };
   // (rows >= n of V' are exactly zero, so the padded k-steps add nothing;
@@ -397,19 +651,35 @@ __device__ __forceinline__ bool bwd_knot(const Dev& D, const BwdLds& L, int b, i
     }
   }
   stamp.mark(0);
-  lds_barrier();  // B0: every wave is done reading V'
-  // H(i, j) = G_i^T Z_j + cost block, j >= jstart(i). Qxx(i, j) goes to the
+  // B0 (partial, LDS counter): the x-block owners write Qxx into the V'
+  // buffer, so they wait until every block owner is done reading V' in G.
+  // The u-block owners only write Quu and go on (their Quu rows are what the
+  // inversion waits for); the inversion wave does not read V' at all.
+  if constexpr (NO > 0) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (lane == 0) __hip_atomic_fetch_add(L.flag + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  if constexpr (P.owns_x(W)) {
+    const int target = P.gwaves * (D.T - t);
+    while (__hip_atomic_load(L.flag + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target)
+      __builtin_amdgcn_s_sleep(1);
+    asm volatile("" ::: "memory");
+  }
+  // H(i, j) = G_i^T Z_j (+ Lxu / Luu + ureg I), j >= jstart(i). Qxx(i, j) goes to the
   // dead V' buffer at the mirrored position (R, C) -> V[R * LDV + C]
   // (conflict-free, and a lower tile that no other wave touches before this
   // wave updates it in place in P2); Qxu / Quu tiles go to their buffers.
   // Column j's Z fragments are read into registers while column j-1's MFMAs
-  // run (any(j) is monotone in j, so the next column always exists).
-  double zc[4 * NTL], zn[4 * NTL];
+  // run (any(j) is monotone in j, so the next column always exists). With two
+  // waves per SIMD the partner wave covers that latency instead, and the
+  // second buffer's registers are better spent elsewhere.
+  constexpr bool ZDB = NW == 4;
+  double zc[4 * NTL], zn[ZDB ? 4 * NTL : 1];
   bool first = true;
   auto zload = [&](double(&zz)[4 * NTL], int j) {
 #pragma unroll
     for (int s = 0; s < 4 * NTL; ++s)
-      zz[s] = j < NTL ? L.Zx[(16 * j + c) * NP + 4 * s + q] : L.Zu[(16 * (j - NTL) + c) * NP + 4 * s + q];
+      zz[s] = j < NTL ? L.Zx[(16 * j + c) * ZLD + 4 * s + q] : L.Zu[(16 * (j - NTL) + c) * ZLD + 4 * s + q];
   };
 #pragma unroll
   for (int j = 0; j < JT; ++j) {
@@ -417,9 +687,13 @@ __device__ __forceinline__ bool bwd_knot(const Dev& D, const BwdLds& L, int b, i
 #pragma unroll
     for (int o = 0; o < NO; ++o) any = any || j >= bwd_jstart<NTL>(P.blk[W][o]);
     if (!any) continue;
-    if (first) zload(zc, j);
-    first = false;
-    if (j + 1 < JT) zload(zn, j + 1);
+    if constexpr (ZDB) {
+      if (first) zload(zc, j);
+      first = false;
+      if (j + 1 < JT) zload(zn, j + 1);
+    } else {
+      zload(zc, j);
+    }
     __builtin_amdgcn_sched_barrier(0);
     const bool isx = j < NTL;
     const int ju = j - NTL;
@@ -431,7 +705,7 @@ __device__ __forceinline__ bool bwd_knot(const Dev& D, const BwdLds& L, int b, i
       for (int r = 0; r < 4; ++r) {
         double v;
         if (isx) {
-          v = 0.5 * (Lp[o][isx ? j : 0][r][0] + Lp[o][isx ? j : 0][r][1]);
+          v = 0.;  // + sym(Lxx) in P2
         } else {
           v = Lq[o][isx ? 0 : ju][r];
           if (ur && i >= NTL && 16 * (i - NTL) + q + 4 * r == 16 * ju + c && 16 * ju + c < m) v += ureg;
@@ -461,26 +735,33 @@ __device__ __forceinline__ bool bwd_knot(const Dev& D, const BwdLds& L, int b, i
         }
       }
     }
+    if constexpr (ZDB) {
 #pragma unroll
-    for (int s = 0; s < 4 * NTL; ++s) zc[s] = zn[s];
+      for (int s = 0; s < 4 * NTL; ++s) zc[s] = zn[s < (ZDB ? 4 * NTL : 1) ? s : 0];
+    }
     __builtin_amdgcn_sched_barrier(0);
+  }
+  if constexpr (W != 0 && P.owns_u(W)) {  // this wave's Quu rows are stored: tell wave 0
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (lane == 0) __hip_atomic_fetch_add(L.flag + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __builtin_amdgcn_s_setprio(0);
   }
   stamp.mark(1);
   // ---- wave 0: Quu^-1 by the symmetric sweep (overlaps waves 1-3) ----------
   if constexpr (W == 0) {
+    if constexpr (P.uwaves > 0) {  // wait for the other u-block owners' Quu rows
+      const int target = P.uwaves * (D.T - t);
+      while (__hip_atomic_load(L.flag + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target)
+        __builtin_amdgcn_s_sleep(1);
+      asm volatile("" ::: "memory");
+    }
     if (sym_sweep_inverse<MP, LDQ>(Quu, Qi, L.rowbuf, m, lane) && lane == 0) *L.flag = 1;
   }
   stamp.mark(2);
   dma_barrier();  // B1 (also retires the fs DMA issued at the end of the last knot)
   stamp.mark(3);
   if (*L.flag) return false;
-  if (t > 0) {  // operands of knot t-1 land during P2/P3
-    const int64_t k1 = kk - 1;
-    dma_cols(L.Zx, NP, D.Fx + k1 * D.sNN, n, n, W, lane);
-    dma_cols(L.Zu, NP, D.Fu + k1 * D.sNM, n, m, W, lane);
-    dma_vec(L.lxv, D.Lx + k1 * D.sN, n, W, lane);
-    dma_vec(L.luv, D.Lu + k1 * D.sM, m, W, lane);
-  }
+  if constexpr (NW == 4) issue_dma();
   // ---- P2: K(:, i) = Quu^-1 Qxu(i, :)^T ; Vxx(i, j) = Qxx(i, j) - K(:, i)^T Qxu(j, :)^T
   f64x4 Kt[NA][MTL];
   {
@@ -509,67 +790,94 @@ __device__ __forceinline__ bool bwd_knot(const Dev& D, const BwdLds& L, int b, i
       }
     }
     stamp.mark(4);
+    // this wave's V tiles (i, j), i <= j: with K(:, i) when it owns block i
+    // ("row" form, V(i, j) = Qxx(i, j) - K(:, i)^T Qxu(j, :)^T), else with
+    // K(:, j) on the transposed tile V(j, i) = Qxx(i, j)^T - K(:, j)^T Qxu(i, :)^T
 #pragma unroll
-    for (int o = 0; o < NO; ++o) {
-      const int i = P.blk[W][o];
-      if (i < NTL) {
+    for (int k3 = 0; k3 < P.ntile[W]; ++k3) {
+      const int i = P.tile[W][k3][0], j = P.tile[W][k3][1];
+      const int oi = P.slot(W, i);
+      const bool rowf = oi >= 0;
+      const int oa = rowf ? oi : P.slot(W, j);
+      const int ra = rowf ? i : j, ca = rowf ? j : i;  // tile rows / cols of the result
+      f64x4 acc;
 #pragma unroll
-        for (int j = 0; j < NTL; ++j) {
-          if (j >= i) {
-            f64x4 acc;
+      for (int r = 0; r < 4; ++r) {  // Qxx(i, j) lives at V[R * LDV + C] (R in i, C in j)
+        const double fvf = rowf ? V[(16 * i + q + 4 * r) * LDV + 16 * j + c] : V[(16 * i + c) * LDV + 16 * j + q + 4 * r];
+        acc[r] = 0.5 * (Lv[k3][r][0] + Lv[k3][r][1]) + fvf;
+      }
+      const f64x4 qxx = acc;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) acc[r] = V[(16 * i + q + 4 * r) * LDV + 16 * j + c];  // Qxx(i, j)
-            const f64x4 qxx = acc;
+      for (int s = 0; s < 4 * MTL; ++s)
+        acc = mfma4(-Kt[oa < 0 ? 0 : oa][s >> 2][s & 3], Qxu[(4 * s + q) * LDV + 16 * ca + c], acc);
 #pragma unroll
-            for (int s = 0; s < 4 * MTL; ++s)
-              acc = mfma4(-Kt[o][s >> 2][s & 3], Qxu[(4 * s + q) * LDV + 16 * j + c], acc);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int R = 16 * i + q + 4 * r, C2 = 16 * j + c;
-              double v = acc[r];
-              if (xr && R == C2 && R < n) v += xreg;
-              if (i < j || R <= C2) {
-                V[C2 * LDV + R] = v;
-                V[R * LDV + C2] = v;
-                if (R < n && C2 < n) bad |= bad_entry(v);
-              }
-            }
-            if (D.dQxx) {
-#pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                const int R = 16 * i + q + 4 * r, C2 = 16 * j + c;
-                if (R < n && C2 < n) {
-                  D.dQxx[rr * D.sNN + (int64_t)C2 * n + R] = qxx[r];
-                  if (i < j) D.dQxx[rr * D.sNN + (int64_t)R * n + C2] = qxx[r];
-                }
-              }
-            }
-          }
-          __builtin_amdgcn_sched_barrier(0);
+      for (int r = 0; r < 4; ++r) {
+        const int R = 16 * ra + q + 4 * r, C2 = 16 * ca + c;
+        double v = acc[r];
+        if (xr && R == C2 && R < n) v += xreg;
+        if (ra != ca || R <= C2) {
+          V[C2 * LDV + R] = v;
+          V[R * LDV + C2] = v;
+          if (R < n && C2 < n) bad |= bad_entry(v);
         }
       }
+      if (D.dQxx) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int R = 16 * ra + q + 4 * r, C2 = 16 * ca + c;
+          if (R < n && C2 < n) {
+            D.dQxx[rr * D.sNN + (int64_t)C2 * n + R] = qxx[r];
+            if (ra != ca) D.dQxx[rr * D.sNN + (int64_t)R * n + C2] = qxx[r];
+          }
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
     }
-    if constexpr (W == 0) {  // k = Quu^-1 Qu ; Quuk = Quu k
-      if (lane < MP) {
-        double a = 0.;
-        if (lane < m)
-          for (int k2 = 0; k2 < m; ++k2) a += Qi[k2 * LDQ + lane] * L.qu[k2];
-        L.kv[lane] = a;
-        if (lane < m) D.k[rr * D.sM + lane] = a;
+    if constexpr (W == 0) {  // k = Quu^-1 Qu ; Quuk = Quu k (64 / MP lanes per row)
+      constexpr int LPR = 64 / MP;
+      const int row = lane % MP, part = lane / MP;
+      double a0 = 0., a1 = 0.;
+      for (int k2 = part; k2 < m; k2 += 2 * LPR) {
+        a0 = fma(Qi[k2 * LDQ + row], L.qu[k2], a0);
+        if (k2 + LPR < m) a1 = fma(Qi[(k2 + LPR) * LDQ + row], L.qu[k2 + LPR], a1);
       }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_wave_barrier();
-      if (lane < MP) {
-        double a = 0.;
-        if (lane < m)
-          for (int k2 = 0; k2 < m; ++k2) a += Quu[k2 * LDQ + lane] * L.kv[k2];
-        L.quuk[lane] = a;
+      double a = a0 + a1;
+#pragma unroll
+      for (int o2 = MP; o2 < 64; o2 <<= 1) a += __shfl_xor(a, o2, 64);
+      if (part == 0) {
+        if (row >= m) a = 0.;
+        L.kv[row] = a;
+        if (row < m) D.k[rr * D.sM + row] = a;
       }
+      asm volatile("" ::: "memory");
+      a0 = 0.;
+      a1 = 0.;
+      for (int k2 = part; k2 < m; k2 += 2 * LPR) {
+        a0 = fma(Quu[k2 * LDQ + row], L.kv[k2], a0);
+        if (k2 + LPR < m) a1 = fma(Quu[(k2 + LPR) * LDQ + row], L.kv[k2 + LPR], a1);
+      }
+      a = a0 + a1;
+#pragma unroll
+      for (int o2 = MP; o2 < 64; o2 <<= 1) a += __shfl_xor(a, o2, 64);
+      if (part == 0) L.quuk[row] = row < m ? a : 0.;
     }
     if (bad) *L.flag = 1;
   }
   stamp.mark(5);
-  lds_barrier();  // B2
+  // B2 (partial, LDS counter): P3 (the x-block owners) needs every V tile
+  // and wave 0's Quu k; the other waves only signal (when they produced
+  // something) and go on issuing the DMA.
+  if constexpr (W == 0 || P.owns_x(W)) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (lane == 0) __hip_atomic_fetch_add(L.flag + 3, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  if constexpr (P.owns_x(W)) {
+    const int target = (P.xwaves + (P.owns_x(0) ? 0 : 1)) * (D.T - t);
+    while (__hip_atomic_load(L.flag + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target)
+      __builtin_amdgcn_s_sleep(1);
+    asm volatile("" ::: "memory");
+  }
+  if constexpr (NW == 8) issue_dma();
   // ---- P3: Vx = Qx + K^T Quuk - 2 K^T Qu (+ Vxx fs), reduction terms -------
   {
     const double* fsv = L.fsb;
@@ -589,8 +897,18 @@ __device__ __forceinline__ bool bwd_knot(const Dev& D, const BwdLds& L, int b, i
             a += Kt[o][it][r] * L.quuk[k2];
             c2 += Kt[o][it][r] * L.qu[k2];
           }
-        if (!feas)
-          for (int j = q; j < n; j += 4) f += V[j * LDV + R] * fsv[j];
+        if (!feas) {
+          double f0 = 0., f1 = 0., f2 = 0., f3 = 0.;
+          int j = q;
+          for (; j + 12 < n; j += 16) {
+            f0 = fma(V[j * LDV + R], fsv[j], f0);
+            f1 = fma(V[(j + 4) * LDV + R], fsv[j + 4], f1);
+            f2 = fma(V[(j + 8) * LDV + R], fsv[j + 8], f2);
+            f3 = fma(V[(j + 12) * LDV + R], fsv[j + 12], f3);
+          }
+          for (; j < n; j += 4) f0 = fma(V[j * LDV + R], fsv[j], f0);
+          f = (f0 + f1) + (f2 + f3);
+        }
         a += __shfl_xor(a, 16, 64);
         a += __shfl_xor(a, 32, 64);
         c2 += __shfl_xor(c2, 16, 64);
@@ -623,22 +941,25 @@ __device__ __forceinline__ bool bwd_knot(const Dev& D, const BwdLds& L, int b, i
 #pragma unroll
     for (int j = 0; j < 5; ++j) {
       const double s = wave_sum(pv[j]);
-      if (lane == 0) L.red[j * 4 + W] = s;
+      if (lane == 0) L.red[j * NW + W] = s;
     }
     if (bad) *L.flag = 1;
   }
   stamp.mark(6);
   dma_barrier();  // B3: knot t-1 operands resident
   // fs of knot t-1 (read in its P3; landed by the vmcnt(0) of its B1)
-  if (t > 0) dma_vec(L.fsb, D.fs + (kk - 1) * D.sN, n, W, lane);
+  if constexpr (P.dmarank[W] >= 0) {
+    if (t > 0) dma_vec<P.ndma>(L.fsb, D.fs + (kk - 1) * D.sN, n, P.dmarank[W], lane);
+  }
   return true;
 }
 
-template <int NTL, int MTL>
+template <int NTL, int MTL, int NW>
 __device__ __forceinline__ bool bwd_sweep_mfma(const Dev& D, int b, bool feas, double xreg, double ureg,
                                                double* sm) {
   using Cfg = MfmaCfg<NTL, MTL>;
   constexpr int NP = Cfg::NP, MP = Cfg::MP, LDV = Cfg::LDV, LDQ = Cfg::LDQ;
+  constexpr int NT = NW * 64;
   const int n = D.n, m = D.m, T = D.T, tid = threadIdx.x;
   const int wid = tid >> 6, lane = tid & 63;
   BwdLds L;
@@ -661,9 +982,14 @@ __device__ __forceinline__ bool bwd_sweep_mfma(const Dev& D, int b, bool feas, d
   L.Zu = sm + Cfg::oZu;
   double* V = L.V;
   const bool xr = !isnan(xreg);
-  Stamp stamp(D.stamps ? D.stamps + ((int64_t)b * 4 + wid) * 8 : nullptr);
+  Stamp stamp(D.stamps ? D.stamps + ((int64_t)b * 8 + wid) * 8 : nullptr);
 
-  if (tid == 0) *L.flag = 0;
+  if (tid == 0) {
+    L.flag[0] = 0;
+    L.flag[1] = 0;  // Quu-ready counter (8-wave plan)
+    L.flag[2] = 0;  // G-done counter (partial B0)
+    L.flag[3] = 0;  // P2-done counter (partial B2)
+  }
   // ---- terminal: Vxx = Lxx_T (+ xreg I), Vx = Lx_T (+ Vxx fs_T) ------------
   {
     const int64_t kk = D.knot(b, T);
@@ -672,21 +998,21 @@ __device__ __forceinline__ bool bwd_sweep_mfma(const Dev& D, int b, bool feas, d
     const double* fs = D.fs + kk * D.sN;
     double* fsv = L.fsb;
     // stored transposed so that G = V Z uses Lxx_T itself (it may be asymmetric)
-    for (int e = tid; e < NP * NP; e += 256) {
+    for (int e = tid; e < NP * NP; e += NT) {
       const int i = e % NP, j = e / NP;
       double v = (i < n && j < n) ? Lxx[(int64_t)i * n + j] : 0.;
       if (xr && i == j && i < n) v += xreg;
       V[j * LDV + i] = v;
     }
-    for (int i = tid; i < NP; i += 256) fsv[i] = i < n ? fs[i] : 0.;
+    for (int i = tid; i < NP; i += NT) fsv[i] = i < n ? fs[i] : 0.;
     // zero the padding of the per-knot vector buffers once (DMA fills [0, n))
     // (and of Z: rows >= n, columns >= n / m are never written by the DMA)
-    for (int i = tid; i < NP; i += 256) L.lxv[i] = 0.;
-    for (int i = tid; i < MP; i += 256) L.luv[i] = 0.;
-    for (int e = tid; e < NP * (NP + MP); e += 256) L.Zx[e] = 0.;
+    for (int i = tid; i < NP; i += NT) L.lxv[i] = 0.;
+    for (int i = tid; i < MP; i += NT) L.luv[i] = 0.;
+    for (int e = tid; e < (NP + MP) * Cfg::ZLD + 2; e += NT) L.Zx[e] = 0.;
     __syncthreads();
     double pv[2] = {0., 0.};
-    for (int i = tid; i < NP; i += 256) {
+    for (int i = tid; i < NP; i += NT) {
       double v = i < n ? Lx[i] : 0.;
       if (!feas && i < n) {
         double a = 0.;
@@ -699,26 +1025,26 @@ __device__ __forceinline__ bool bwd_sweep_mfma(const Dev& D, int b, bool feas, d
       }
       L.vx[i] = v;
     }
-    wg_sums<256, 2>(pv, L.red);
+    wg_sums<NT, 2>(pv, L.red);
     if (tid == 0) {
       double* p = D.part + kk * 8;
       p[0] = 0.; p[1] = 0.; p[2] = pv[0]; p[3] = pv[1]; p[4] = 0.;
     }
     if (D.dVxx) {
-      for (int e = tid; e < n * n; e += 256) {
+      for (int e = tid; e < n * n; e += NT) {
         const int i = e % n, j = e / n;
         D.dVxx[kk * D.sNN + e] = Lxx[e] + ((xr && i == j) ? xreg : 0.);
       }
-      for (int i = tid; i < n; i += 256) D.dVx[kk * D.sN + i] = L.vx[i];
+      for (int i = tid; i < n; i += NT) D.dVx[kk * D.sN + i] = L.vx[i];
     }
     __syncthreads();
     if (T > 0) {  // operands of knot T-1
       const int64_t k1 = kk - 1;
-      dma_cols(L.Zx, NP, D.Fx + k1 * D.sNN, n, n, wid, lane);
-      dma_cols(L.Zu, NP, D.Fu + k1 * D.sNM, n, m, wid, lane);
-      dma_vec(L.lxv, D.Lx + k1 * D.sN, n, wid, lane);
-      dma_vec(L.luv, D.Lu + k1 * D.sM, m, wid, lane);
-      dma_vec(L.fsb, D.fs + k1 * D.sN, n, wid, lane);
+      dma_cols<NW>(L.Zx, Cfg::ZLD, D.Fx + k1 * D.sNN, n, n, wid, lane);
+      dma_cols<NW>(L.Zu, Cfg::ZLD, D.Fu + k1 * D.sNM, n, m, wid, lane);
+      dma_vec<NW>(L.lxv, D.Lx + k1 * D.sN, n, wid, lane);
+      dma_vec<NW>(L.luv, D.Lu + k1 * D.sM, m, wid, lane);
+      dma_vec<NW>(L.fsb, D.fs + k1 * D.sN, n, wid, lane);
     }
     dma_barrier();
   }
@@ -729,10 +1055,14 @@ __device__ __forceinline__ bool bwd_sweep_mfma(const Dev& D, int b, bool feas, d
     stamp.mark(7);
     bool ok;
     switch (wid) {
-      case 0: ok = bwd_knot<NTL, MTL, 0>(D, L, b, t, feas, xreg, ureg, stamp); break;
-      case 1: ok = bwd_knot<NTL, MTL, 1>(D, L, b, t, feas, xreg, ureg, stamp); break;
-      case 2: ok = bwd_knot<NTL, MTL, 2>(D, L, b, t, feas, xreg, ureg, stamp); break;
-      default: ok = bwd_knot<NTL, MTL, 3>(D, L, b, t, feas, xreg, ureg, stamp); break;
+      case 0: ok = bwd_knot<NTL, MTL, NW, 0>(D, L, b, t, feas, xreg, ureg, stamp); break;
+      case 1: ok = bwd_knot<NTL, MTL, NW, 1>(D, L, b, t, feas, xreg, ureg, stamp); break;
+      case 2: ok = bwd_knot<NTL, MTL, NW, 2>(D, L, b, t, feas, xreg, ureg, stamp); break;
+      case 3: ok = bwd_knot<NTL, MTL, NW, 3>(D, L, b, t, feas, xreg, ureg, stamp); break;
+      case 4: if constexpr (NW > 4) ok = bwd_knot<NTL, MTL, NW, 4>(D, L, b, t, feas, xreg, ureg, stamp); break;
+      case 5: if constexpr (NW > 4) ok = bwd_knot<NTL, MTL, NW, 5>(D, L, b, t, feas, xreg, ureg, stamp); break;
+      case 6: if constexpr (NW > 4) ok = bwd_knot<NTL, MTL, NW, 6>(D, L, b, t, feas, xreg, ureg, stamp); break;
+      default: if constexpr (NW > 4) ok = bwd_knot<NTL, MTL, NW, 7>(D, L, b, t, feas, xreg, ureg, stamp); break;
     }
     if (!ok) {  // the factorisation failed (every wave saw the flag)
       stamp.flush();
@@ -742,17 +1072,21 @@ __device__ __forceinline__ bool bwd_sweep_mfma(const Dev& D, int b, bool feas, d
       double* p = D.part + kk * 8;
       const double* red = L.red;
 #pragma unroll
-      for (int j = 0; j < 5; ++j) p[j] = red[j * 4] + red[j * 4 + 1] + red[j * 4 + 2] + red[j * 4 + 3];
+      for (int j = 0; j < 5; ++j) {
+        double a = 0.;
+        for (int w = 0; w < NW; ++w) a += red[j * NW + w];
+        p[j] = a;
+      }
     }
     if (D.dQxx) {
-      for (int e = tid; e < n * n; e += 256) D.dVxx[kk * D.sNN + e] = V[(e / n) * LDV + e % n];
-      for (int e = tid; e < n * m; e += 256) D.dQxu[rr * D.sNM + e] = L.Qxu[(e / n) * LDV + e % n];
-      for (int e = tid; e < m * m; e += 256) D.dQuu[rr * D.sMM + e] = L.Quu[(e / m) * LDQ + e % m];
-      for (int i = tid; i < n; i += 256) {
+      for (int e = tid; e < n * n; e += NT) D.dVxx[kk * D.sNN + e] = V[(e / n) * LDV + e % n];
+      for (int e = tid; e < n * m; e += NT) D.dQxu[rr * D.sNM + e] = L.Qxu[(e / n) * LDV + e % n];
+      for (int e = tid; e < m * m; e += NT) D.dQuu[rr * D.sMM + e] = L.Quu[(e / m) * LDQ + e % m];
+      for (int i = tid; i < n; i += NT) {
         D.dQx[rr * D.sN + i] = L.qx[i];
         D.dVx[kk * D.sN + i] = L.vx[i];
       }
-      for (int i = tid; i < m; i += 256) D.dQu[rr * D.sM + i] = L.qu[i];
+      for (int i = tid; i < m; i += NT) D.dQu[rr * D.sM + i] = L.qu[i];
       __syncthreads();
     }
     if (*L.flag) {
@@ -764,8 +1098,8 @@ __device__ __forceinline__ bool bwd_sweep_mfma(const Dev& D, int b, bool feas, d
   return true;
 }
 
-template <int NTL, int MTL>
-__global__ __launch_bounds__(256) void backward_mfma_kernel(Dev D, Prm prm, int mode) {
+template <int NTL, int MTL, int NW>
+__global__ __launch_bounds__(NW * 64) void backward_mfma_kernel(Dev D, Prm prm, int mode) {
   const int b = blockIdx.x;
   ElemState* st = D.st + b;
   if (mode == 0 && !st->active) return;
@@ -774,7 +1108,7 @@ __global__ __launch_bounds__(256) void backward_mfma_kernel(Dev D, Prm prm, int 
   double xreg = st->xreg, ureg = st->ureg;
   bool ok;
   for (;;) {
-    ok = bwd_sweep_mfma<NTL, MTL>(D, b, feas, xreg, ureg, sm);
+    ok = bwd_sweep_mfma<NTL, MTL, NW>(D, b, feas, xreg, ureg, sm);
     __syncthreads();
     if (ok || mode == 1) break;
     xreg *= prm.regfactor;  // increaseRegularization (ddp.cpp:312-318)

@@ -60,6 +60,7 @@ struct Dev {
   double *dVxx, *dVx, *dQxx, *dQxu, *dQuu, *dQx, *dQu;
   ElemState* st;             // [B]
   double* bwork;             // generic sweep's global workspace when LDS is too small (else null)
+  double* zero16;            // 16 zero bytes: source of the LDS-DMA gap fill
   unsigned long long* stamps;  // diagnostic: [B][4 waves][8 phases] cycles (null = off)
 
   __device__ __host__ int64_t knot(int b, int t) const { return (int64_t)b * (T + 1) + t; }

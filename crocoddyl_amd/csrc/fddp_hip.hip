@@ -91,7 +91,7 @@ struct fddp_handle_s {
   bool fast = false;  // dense-knot fast path (fast_path.hpp) for calc / calcDiff / forward
   size_t fused_smem = 0, fwd_fast_smem = 0;
   int64_t pcap = 0;  // doubles of LDS reserved for a resident parameter block
-  int bwd_variant = 0;  // 0 generic, else NTL*10+MTL of the MFMA sweep
+  int bwd_variant = 0;  // 0 generic, else (NTL*10+MTL)*10+waves of the MFMA sweep
   // timing
   bool timing = false;
   std::vector<hipEvent_t> ev_pool;
@@ -214,20 +214,25 @@ int launch_calc_then_diff(fddp_handle* h, int sel_calc, int sel_calc_sum, int se
   if ((rc = launch_cost_sum(h, sel_calc_sum, nullptr))) return rc;
   return launch_calc_diff(h, sel_diff, gaps);
 }
-template <int NTL, int MTL>
+template <int NTL, int MTL, int NW>
 void launch_bwd_mfma(fddp_handle* h, int mode) {
   const Dev& D = h->D;
-  backward_mfma_kernel<NTL, MTL><<<dim3(D.B), dim3(256), MfmaCfg<NTL, MTL>::bytes, h->stream>>>(D, to_prm(h->prm), mode);
+  backward_mfma_kernel<NTL, MTL, NW><<<dim3(D.B), dim3(NW * 64), MfmaCfg<NTL, MTL>::bytes, h->stream>>>(
+      D, to_prm(h->prm), mode);
 }
 
 int launch_backward(fddp_handle* h, int mode) {
   Timed tm(h, 2);
   const Dev& D = h->D;
   switch (h->bwd_variant) {
-    case 52: launch_bwd_mfma<5, 2>(h, mode); break;
-    case 31: launch_bwd_mfma<3, 1>(h, mode); break;
-    case 21: launch_bwd_mfma<2, 1>(h, mode); break;
-    case 11: launch_bwd_mfma<1, 1>(h, mode); break;
+    case 528: launch_bwd_mfma<5, 2, 8>(h, mode); break;
+    case 524: launch_bwd_mfma<5, 2, 4>(h, mode); break;
+    case 318: launch_bwd_mfma<3, 1, 8>(h, mode); break;
+    case 314: launch_bwd_mfma<3, 1, 4>(h, mode); break;
+    case 218: launch_bwd_mfma<2, 1, 8>(h, mode); break;
+    case 214: launch_bwd_mfma<2, 1, 4>(h, mode); break;
+    case 118: launch_bwd_mfma<1, 1, 8>(h, mode); break;
+    case 114: launch_bwd_mfma<1, 1, 4>(h, mode); break;
     default:
       hipLaunchKernelGGL(backward_kernel<kNT>, dim3(D.B), dim3(kNT), h->bwd_smem, h->stream, D, to_prm(h->prm), mode);
   }
@@ -235,16 +240,20 @@ int launch_backward(fddp_handle* h, int mode) {
   return FDDP_OK;
 }
 
-template <int NTL, int MTL>
+template <int NTL, int MTL, int NW>
 int setup_bwd_mfma(fddp_handle* h) {
   using Cfg = MfmaCfg<NTL, MTL>;
   const size_t lds = Cfg::bytes;
-  if (lds > 160 * 1024) return -1;
-  if (hipFuncSetAttribute((const void*)backward_mfma_kernel<NTL, MTL>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)lds) != hipSuccess)
+  if (lds > 160 * 1024 || h->D.n > Cfg::ZLD) return -1;
+  if (hipFuncSetAttribute((const void*)backward_mfma_kernel<NTL, MTL, NW>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return -1;
   // column-block ownership per wave is static (BwdPlan in bwd_mfma.hpp)
-  return NTL * 10 + MTL;
+  return (NTL * 10 + MTL) * 10 + NW;
+}
+template <int NTL, int MTL>
+int setup_bwd_mfma_nw(fddp_handle* h, int nw) {
+  return nw == 4 ? setup_bwd_mfma<NTL, MTL, 4>(h) : setup_bwd_mfma<NTL, MTL, 8>(h);
 }
 int launch_forward(fddp_handle* h, int mode, double alpha, int* count) {
   Timed tm(h, 3);
@@ -468,6 +477,7 @@ int fddp_create(const fddp_dims* dims, const fddp_knot_desc* knots, const double
       {&D.Lxx, B * K1 * D.sNN},   {&D.Lxu, B * K1 * D.sNM},  {&D.Luu, B * K1 * D.sMM},  {&D.Lx, B * K1 * D.sN},
       {&D.Lu, B * K1 * D.sM},     {&D.fs, B * K1 * D.sN},    {&D.K, B * K0 * D.sNM},    {&D.k, B * K0 * D.sM},
       {&D.Vxxfs, B * K1 * D.sN},  {&D.part, B * K1 * 8},     {&D.dvp, B * K1},
+      {&D.zero16, 2},
   };
   for (auto& a : plan)
     if ((rc = dalloc(h, a.p, a.n))) return bail(rc);
@@ -514,17 +524,19 @@ int fddp_create(const fddp_dims* dims, const fddp_knot_desc* knots, const double
     const int ntl = (d.ndx + 15) / 16, mtl = (d.nu_max + 15) / 16;
     int v = -1;
     if (uniform_nu && !force_generic) {
-      if (ntl == 5 && mtl == 2) v = setup_bwd_mfma<5, 2>(h);
-      else if (ntl == 3 && mtl == 1) v = setup_bwd_mfma<3, 1>(h);
-      else if (ntl == 2 && mtl == 1) v = setup_bwd_mfma<2, 1>(h);
-      else if (ntl == 1 && mtl == 1) v = setup_bwd_mfma<1, 1>(h);
+      const char* ew = std::getenv("FDDP_BWD_WAVES");
+      const int nw = (ew && ew[0] == '4') ? 4 : 8;
+      if (ntl == 5 && mtl == 2) v = setup_bwd_mfma_nw<5, 2>(h, nw);
+      else if (ntl == 3 && mtl == 1) v = setup_bwd_mfma_nw<3, 1>(h, nw);
+      else if (ntl == 2 && mtl == 1) v = setup_bwd_mfma_nw<2, 1>(h, nw);
+      else if (ntl == 1 && mtl == 1) v = setup_bwd_mfma_nw<1, 1>(h, nw);
     }
     h->bwd_variant = v > 0 ? v : 0;
   }
   if (const char* e = std::getenv("FDDP_STAMPS")) {
     if (e[0] == '1') {
       double* p2 = nullptr;
-      if ((rc = dalloc(h, &p2, (int64_t)d.B * 32))) return bail(rc);
+      if ((rc = dalloc(h, &p2, (int64_t)d.B * 64))) return bail(rc);
       D.stamps = (unsigned long long*)p2;
     }
   }
@@ -538,15 +550,15 @@ void fddp_destroy(fddp_handle* h) {
   DeviceGuard g(h->device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   if (h->D.stamps) {  // diagnostic summary: mean cycles per element per wave and phase
-    std::vector<unsigned long long> v((size_t)h->dims.B * 32);
+    std::vector<unsigned long long> v((size_t)h->dims.B * 64);
     if (hipMemcpy(v.data(), h->D.stamps, v.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
       const char* names[8] = {"p1_G", "p1_H", "p1_inv", "b1_dma", "p2_K", "p2_Vupd", "b2_p3", "b3_wait"};
       std::fprintf(stderr, "[fddp stamps] mean cycles per element (variant %d):\n", h->bwd_variant);
-      for (int w = 0; w < 4; ++w) {
+      for (int w = 0; w < h->bwd_variant % 10; ++w) {
         std::fprintf(stderr, "  wave %d:", w);
         for (int ph = 0; ph < 8; ++ph) {
           double s2 = 0;
-          for (int b = 0; b < h->dims.B; ++b) s2 += (double)v[((size_t)b * 4 + w) * 8 + ph];
+          for (int b = 0; b < h->dims.B; ++b) s2 += (double)v[((size_t)b * 8 + w) * 8 + ph];
           std::fprintf(stderr, " %s=%.0f", names[ph], s2 / h->dims.B);
         }
         std::fprintf(stderr, "\n");

@@ -1,0 +1,10 @@
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1
+rc=$?
+tail -3 gpurun_out/pytest_gpu.log
+[ $rc -ne 0 ] && exit $rc
+for nw in 8 4; do
+FDDP_BWD_WAVES=$nw timeout -k 10 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/bench_$nw.log 2>&1 && tail -1 gpurun_out/bench_$nw.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('waves', $nw, d['value'], d['ms_per_step'], d['kernel_ms_per_step'], d['roofline']['frac'])"
+done
+CROCODDYL_AMD_LIB=$PWD/crocoddyl_amd/lib/libfddp_hip_stamps.so FDDP_STAMPS=1 timeout -k 10 300 python bench.py --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/bench_stamps.log 2>&1 && grep -A9 "fddp stamps" gpurun_out/bench_stamps.log

@@ -14,14 +14,40 @@ __global__ void k_sweep(const double* Q, double* Qi_out, unsigned long long* cyc
   __syncthreads();
   unsigned long long t0 = __builtin_amdgcn_s_memtime();
   bool bad = false;
-  for (int r = 0; r < reps; ++r) bad |= fddp::sym_sweep_inverse<32, 32>(Quu, Qi, rb, m, lane);
+  for (int r = 0; r < reps; ++r) {
+#ifdef SWEEP_BLK
+    bad |= fddp::sym_sweep_inverse_blk<32, 32>(Quu, Qi, rb, m, lane);
+#else
+    bad |= fddp::sym_sweep_inverse<32, 32>(Quu, Qi, rb, m, lane);
+#endif
+  }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   unsigned long long t1 = __builtin_amdgcn_s_memtime();
   for (int e = lane; e < 1024; e += 64) Qi_out[blockIdx.x * 1024 + e] = Qi[e];
   if (lane == 0) cyc[blockIdx.x] = (t1 - t0) / reps + (bad ? 1000000000ull : 0);
 }
 
+// relative accuracy of rcp_f64 over a wide range of pivots
+__global__ void k_rcp(const double* d, double* err, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) err[i] = fabs(fddp::rcp_f64(d[i]) * d[i] - 1.0);
+}
+
 int main() {
+  {
+    const int N = 1 << 16;
+    double* h = (double*)malloc(N * 8);
+    for (int i = 0; i < N; ++i) h[i] = exp(-30.0 + 60.0 * (rand() / (double)RAND_MAX)) * (1 + 1e-3 * i);
+    double *dd, *de;
+    hipMalloc(&dd, N * 8);
+    hipMalloc(&de, N * 8);
+    hipMemcpy(dd, h, N * 8, hipMemcpyHostToDevice);
+    k_rcp<<<N / 256, 256>>>(dd, de, N);
+    hipMemcpy(h, de, N * 8, hipMemcpyDeviceToHost);
+    double mx = 0;
+    for (int i = 0; i < N; ++i) mx = fmax(mx, h[i]);
+    printf("rcp_f64: max |rcp(d) d - 1| = %.3e\n", mx);
+  }
   const int m = 32;
   double Q[1024], X[1024];
   srand(1);
