@@ -1,0 +1,65 @@
+"""Summarise a rocprofv3 profiling run (tools/prof.sh) into profiles/.
+
+Inputs (gpurun_out/prof/...):
+  kt/run_kernel_stats.csv            rocprofv3 --kernel-trace --stats
+  pmc_fetch/run_counter_collection.csv   rocprofv3 --pmc FETCH_SIZE
+  pmc_write/run_counter_collection.csv   rocprofv3 --pmc WRITE_SIZE
+Outputs:
+  profiles/<tag>_kernel_stats.csv    (copy)
+  profiles/pmc_backward.json         HBM bytes per backward launch, as bench.py's roofline "traffic"
+
+FETCH_SIZE / WRITE_SIZE are in KiB per dispatch. On gfx950 FETCH_SIZE reports
+half the bytes of a wide coalesced streaming read (MI355X_MICROARCH.md, HBM
+section): it is doubled here; WRITE_SIZE is taken as is.
+"""
+import csv
+import json
+import os
+import shutil
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def counter(path, name_sub, counter_name):
+    vals = []
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            if name_sub in row["Kernel_Name"] and row["Counter_Name"] == counter_name:
+                vals.append(float(row["Counter_Value"]))
+    return vals
+
+
+def main():
+    tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
+    cfg = sys.argv[2] if len(sys.argv) > 2 else "C5_talos_full"
+    src = os.path.join(ROOT, "gpurun_out", "prof")
+    prof = os.path.join(ROOT, "profiles")
+    os.makedirs(prof, exist_ok=True)
+    shutil.copy(os.path.join(src, "kt", "run_kernel_stats.csv"), os.path.join(prof, f"{tag}_kernel_stats.csv"))
+    out = {}
+    for kname, key in (("backward_mfma_kernel", "backward"), ("calc_fused_kernel", "calc_fused"),
+                       ("forward_kernel", "forward")):
+        f = counter(os.path.join(src, "pmc_fetch", "run_counter_collection.csv"), kname, "FETCH_SIZE")
+        w = counter(os.path.join(src, "pmc_write", "run_counter_collection.csv"), kname, "WRITE_SIZE")
+        if not f or not w:
+            continue
+        # steady state: drop the first (cold) dispatch when there are several
+        f = f[1:] if len(f) > 2 else f
+        w = w[1:] if len(w) > 2 else w
+        fetch = 2.0 * statistics.mean(f) * 1024.0
+        write = statistics.mean(w) * 1024.0
+        out[key] = {"hbm_bytes_per_launch": fetch + write, "fetch_bytes": fetch, "write_bytes": write,
+                    "dispatches": [len(f), len(w)]}
+    path = os.path.join(prof, "pmc_backward.json")
+    data = json.load(open(path)) if os.path.exists(path) else {}
+    data[cfg] = dict(out.get("backward", {}), kernels=out, tag=tag,
+                     note="FETCH_SIZE x2 (gfx950 streaming-read correction) + WRITE_SIZE, KiB -> bytes, "
+                          "mean over steady-state dispatches")
+    json.dump(data, open(path, "w"), indent=1)
+    print(json.dumps(data[cfg], indent=1))
+
+
+if __name__ == "__main__":
+    main()
