@@ -20,6 +20,7 @@
 #pragma once
 
 #include "fddp_kernels.hpp"
+#include "bwd_mfma.hpp"  // Stamp
 
 namespace fddp {
 
@@ -115,8 +116,7 @@ __device__ __forceinline__ double seg_dot_t(const double* A, int lda, int i, int
 template <int NT>
 __device__ __forceinline__ double dense_partials(const DenseKnot& K, int nx, int nu, bool use_u, const double* xu,
                                                  bool want_dyn, bool want_lx, bool want_lu, bool want_cost,
-                                                 double* pdyn, double* plx, double* plu) {
-  const int tid = threadIdx.x;
+                                                 double* pdyn, double* plx, double* plu, int tid) {
   const double* x = xu;
   const double* u = xu + nx;
   const int nuu = use_u ? nu : 0;
@@ -182,53 +182,97 @@ __device__ __forceinline__ void dense_xnext(const DenseKnot& K, int nx, int i, d
   }
 }
 
-// Streams one knot's derivative blocks out. Thread -> (row i, column
-// segment): the per-row factors of the Euler integration are per-thread
-// constants, each column is a coalesced store across consecutive rows.
+// Streams one knot's derivative blocks out: thread -> (row pair, column
+// segment), 16-byte stores (n even; odd n falls back to 8-byte stores). The
+// per-row factors of the Euler integration are per-thread constants; each
+// column is a coalesced store across consecutive row pairs.
+__device__ __forceinline__ void dense_fx_rows(const DenseKnot& K, int n, int i, int& ldf, int& ri, int& jd, double& a) {
+  ldf = n;
+  ri = i;
+  jd = -1;
+  a = 1.;
+  if (K.dlqr) {
+    const int nv = n / 2;
+    ldf = nv;
+    ri = i < nv ? i : i - nv;
+    a = K.integ ? (i < nv ? K.dt * K.dt : K.dt) : 0.;
+    jd = (K.integ && i < nv) ? nv + i : -1;
+  }
+}
+__device__ __forceinline__ double dense_fx_at(const DenseKnot& K, int n, int i, int j, int ldf, int ri, int jd, double a) {
+  double f = K.dlqr ? (K.integ ? a * K.F[j * ldf + ri] : 0.) : K.F[j * n + i];
+  if (j == jd) f += K.dt;
+  if (K.dlqr && j == i) f += 1.;
+  return f;
+}
+__device__ __forceinline__ double dense_fu_at(const DenseKnot& K, int n, int nu, int i, int j, int ldf, int ri, double a) {
+  if (j >= nu) return 0.;
+  return K.dlqr ? (K.integ ? a * K.F[(n + j) * ldf + ri] : 0.) : K.F[(n + j) * n + i];
+}
+
 template <int NT>
-__device__ __forceinline__ void dense_write_blocks(const DenseKnot& K, int n, int m, int nu, const KnotDiffOut& o) {
-  const int tid = threadIdx.x;
+__device__ __forceinline__ void dense_write_blocks(const DenseKnot& K, int n, int m, int nu, const KnotDiffOut& o,
+                                                   int part, int tid) {
   const bool scale = K.dlqr && K.integ;
   const double sc = scale ? K.sc : 1.;
-  {
-    const RowSeg r(n, NT, tid);
-    if (r.on) {
-      const int i = r.i;
-      // Fx(i, j) = a_i * F(ri, j) + [j == jd] dt + [j == i]   (Euler∘DiffLQR)
-      //          = F(i, j)                                   (LQR)
-      int ldf = n, ri = i, jd = -1;
-      double a = 1., dtd = 0.;
-      if (K.dlqr) {
-        const int nv = n / 2;
-        ldf = nv;
-        ri = i < nv ? i : i - nv;
-        a = K.integ ? (i < nv ? K.dt * K.dt : K.dt) : 0.;
-        jd = (K.integ && i < nv) ? nv + i : -1;
-        dtd = K.dt;
-      }
-      for (int j = r.g; j < n; j += r.G) {
-        double f = K.dlqr ? (K.integ ? a * K.F[j * ldf + ri] : 0.) : K.F[j * n + i];
-        if (j == jd) f += dtd;
-        if (K.dlqr && j == i) f += 1.;
-        o.Fx[j * n + i] = f;
-        o.Lxx[j * n + i] = sc * K.Lxx[j * n + i];
-      }
-      for (int j = r.g; j < m; j += r.G) {
-        double f = 0., l = 0.;
-        if (j < nu) {
-          f = K.dlqr ? (K.integ ? a * K.F[(n + j) * ldf + ri] : 0.) : K.F[(n + j) * n + i];
-          l = sc * K.Lxu[j * n + i];
-        }
-        o.Fu[j * n + i] = f;
-        o.Lxu[j * n + i] = l;
+  const bool wide = (n & 1) == 0;
+  const int rows = wide ? n / 2 : n;  // row pairs (or rows)
+  const RowSeg r(rows, NT, tid);
+  const int i0 = wide ? 2 * r.i : r.i;
+  int ldf0, ri0, jd0, ldf1, ri1, jd1;
+  double a0, a1;
+  dense_fx_rows(K, n, i0, ldf0, ri0, jd0, a0);
+  dense_fx_rows(K, n, i0 + 1, ldf1, ri1, jd1, a1);
+  if ((part & 1) && r.on) {  // Fx, Lxx
+    for (int j = r.g; j < n; j += r.G) {
+      const int e = j * n + i0;
+      if (wide) {
+        double2 f, l;
+        f.x = dense_fx_at(K, n, i0, j, ldf0, ri0, jd0, a0);
+        f.y = dense_fx_at(K, n, i0 + 1, j, ldf1, ri1, jd1, a1);
+        l.x = sc * K.Lxx[e];
+        l.y = sc * K.Lxx[e + 1];
+        *reinterpret_cast<double2*>(o.Fx + e) = f;
+        *reinterpret_cast<double2*>(o.Lxx + e) = l;
+      } else {
+        o.Fx[e] = dense_fx_at(K, n, i0, j, ldf0, ri0, jd0, a0);
+        o.Lxx[e] = sc * K.Lxx[e];
       }
     }
   }
-  {
-    const RowSeg r(m, NT, tid);
-    if (r.on) {
-      const int i = r.i;
-      for (int j = r.g; j < m; j += r.G) o.Luu[j * m + i] = (i < nu && j < nu) ? sc * K.Luu[j * nu + i] : 0.;
+  if (part & 2) {  // Fu, Lxu, Luu
+    for (int j = r.g; r.on && j < m; j += r.G) {
+      const int e = j * n + i0;
+      const bool in = j < nu;
+      if (wide) {
+        double2 f, l;
+        f.x = dense_fu_at(K, n, nu, i0, j, ldf0, ri0, a0);
+        f.y = dense_fu_at(K, n, nu, i0 + 1, j, ldf1, ri1, a1);
+        l.x = in ? sc * K.Lxu[e] : 0.;
+        l.y = in ? sc * K.Lxu[e + 1] : 0.;
+        *reinterpret_cast<double2*>(o.Fu + e) = f;
+        *reinterpret_cast<double2*>(o.Lxu + e) = l;
+      } else {
+        o.Fu[e] = dense_fu_at(K, n, nu, i0, j, ldf0, ri0, a0);
+        o.Lxu[e] = in ? sc * K.Lxu[e] : 0.;
+      }
+    }
+    // Luu (m x m): row pairs of m when m is even
+    const bool wu = (m & 1) == 0;
+    const RowSeg r2(wu ? m / 2 : m, NT, tid);
+    if (r2.on) {
+      const int u0 = wu ? 2 * r2.i : r2.i;
+      for (int j = r2.g; j < m; j += r2.G) {
+        const double v0 = (u0 < nu && j < nu) ? sc * K.Luu[j * nu + u0] : 0.;
+        if (wu) {
+          double2 v;
+          v.x = v0;
+          v.y = (u0 + 1 < nu && j < nu) ? sc * K.Luu[j * nu + u0 + 1] : 0.;
+          *reinterpret_cast<double2*>(o.Luu + j * m + u0) = v;
+        } else {
+          o.Luu[j * m + u0] = v0;
+        }
+      }
     }
   }
 }
@@ -239,11 +283,16 @@ __device__ __forceinline__ void dense_write_blocks(const DenseKnot& K, int n, in
 // element walks its knots with the parameter block LDS-resident. Elements
 // selected by sel_calc get xnext and the knot costs, those selected by
 // sel_diff the derivative blocks (+ gaps when `gaps`).
+// The derivative blocks (140 KB per knot at C5) dominate: they are written
+// by every wave with 16-byte stores (a wave's store throughput is bounded by
+// its outstanding stores, so bytes per store and waves per CU both count),
+// half of them before the LDS-bound partial sums so that they drain while
+// those run.
 // ---------------------------------------------------------------------------
 template <int NT>
 __global__ __launch_bounds__(NT) void calc_fused_kernel(Dev D, int sel_calc, int sel_diff, int gaps, int64_t pcap) {
   const int b = blockIdx.x;
-  const ElemState& s = D.st[b];
+  const ElemState s = D.st[b];  // by value: a reference would re-load it from HBM after every store
   const bool do_calc = sel_calc >= 0 && selected(s, sel_calc);
   const bool do_diff = sel_diff >= 0 && selected(s, sel_diff);
   if (!do_calc && !do_diff) return;
@@ -258,6 +307,7 @@ __global__ __launch_bounds__(NT) void calc_fused_kernel(Dev D, int sel_calc, int
   const int c = s.cur, nx = D.nx, n = D.n, m = D.m, T = D.T, tid = threadIdx.x;
   const int lane = tid & 63, wid = tid >> 6;
   const double* cached = nullptr;
+  Stamp stamp(D.stamps ? D.stamps + (int64_t)D.B * 64 + ((int64_t)b * 8 + wid) * 8 : nullptr);
   // x and u of knots t+1..t+PD are in flight in registers while knot t
   // computes (a rotating window; thread i holds x_i, u_i; nx, m <= NT here)
   constexpr int PD = 4;
@@ -283,73 +333,85 @@ __global__ __launch_bounds__(NT) void calc_fused_kernel(Dev D, int sel_calc, int
       pu[q] = pu[q + 1];
     }
     fetch(t + PD, px[PD - 1], pu[PD - 1]);
+    stamp.mark(0);
     __syncthreads();
+    stamp.mark(1);
     const DenseKnot K(kd.kind, P, nx, nu);
     const bool want_dyn = do_calc && running;
-    double cp = dense_partials<NT>(K, nx, nu, use_u, xu, want_dyn, do_diff, do_diff, do_calc, pdyn, plx, plu);
+    KnotDiffOut o;
+    o.Fx = D.Fx + kk * D.sNN;
+    o.Fu = D.Fu + kk * D.sNM;
+    o.Lxx = D.Lxx + kk * D.sNN;
+    o.Lxu = D.Lxu + kk * D.sNM;
+    o.Luu = D.Luu + kk * D.sMM;
+    if (do_diff) dense_write_blocks<NT>(K, n, m, nu, o, 1, tid);
+    double cp = dense_partials<NT>(K, nx, nu, use_u, xu, want_dyn, do_diff, do_diff, do_calc, pdyn, plx, plu, tid);
     if (do_calc) {
       cp = wave_sum(cp);
       if (lane == 0) red[wid] = cp;
     }
+    stamp.mark(2);
     __syncthreads();
+    stamp.mark(3);
+    // reductions spread over the waves: xnext rows from thread 0, Lu rows
+    // from 64, Lx rows from 128 (NT = 512 here), the cost on thread NT - 1
+    constexpr int TLU = NT >= 256 ? 64 : 0, TLX = NT >= 256 ? 128 : 0, TC = NT - 1;
     if (want_dyn) {
       for (int i = tid; i < K.nr; i += NT) dense_xnext(K, nx, i, seg_sum(pdyn, K.nr, i, NT), xu, xn);
     }
-    if (do_calc && tid == 0) {
+    if (do_calc && tid == TC) {
       double cst = 0.;
       for (int w = 0; w < NT / 64; ++w) cst += red[w];
       cst = K.dlqr && K.integ ? K.dt * cst : cst;
       D.kcost[c][kk] = cst;
     }
     if (do_diff) {
-      KnotDiffOut o;
-      o.Fx = D.Fx + kk * D.sNN;
-      o.Fu = D.Fu + kk * D.sNM;
-      o.Lxx = D.Lxx + kk * D.sNN;
-      o.Lxu = D.Lxu + kk * D.sNM;
-      o.Luu = D.Luu + kk * D.sMM;
-      o.Lx = D.Lx + kk * D.sN;
-      o.Lu = D.Lu + kk * D.sM;
       const bool scale = K.dlqr && K.integ;
-      for (int i = tid; i < n; i += NT) {
+      double* Lx = D.Lx + kk * D.sN;
+      double* Lu = D.Lu + kk * D.sM;
+      for (int i = tid - TLX; i >= 0 && i < n; i += NT) {
         const double l = K.lx[i] + seg_sum(plx, nx, i, NT);
-        o.Lx[i] = scale ? K.sc * l : l;
+        Lx[i] = scale ? K.sc * l : l;
       }
-      for (int i = tid; i < m; i += NT) {
+      for (int i = tid - TLU; i >= 0 && i < m; i += NT) {
         double v = 0.;
         if (i < nu) {
           const double l = K.lu[i] + seg_sum(plu, nu, i, NT);
           v = scale ? K.sc * l : l;
         }
-        o.Lu[i] = v;
+        Lu[i] = v;
       }
-      dense_write_blocks<NT>(K, n, m, nu, o);
+      stamp.mark(4);
+      dense_write_blocks<NT>(K, n, m, nu, o, 2, tid);
     }
+    stamp.mark(5);
     __syncthreads();  // xn complete
+    stamp.mark(6);
     if (want_dyn) {
       double* xo = D.xnext[c] + D.run(b, t) * D.sX;
-      for (int i = tid; i < nx; i += NT) xo[i] = xn[i];
+      if (tid < nx) xo[tid] = xn[tid];
     }
     if (do_diff && gaps) {
       if (!s.is_feasible) {
         // fs[0] = diff(xs[0], x0) = x0 - xs[0]; fs[t+1] = diff(xs[t+1], data[t].xnext)
-        if (t == 0) {
+        if (t == 0 && tid < n) {
           double* f = D.fs + D.knot(b, 0) * D.sN;
           const double* x0 = D.x0 + (int64_t)b * D.sX;
-          for (int i = tid; i < n; i += NT) f[i] = x0[i] - xu[i];
+          f[tid] = x0[tid] - xu[tid];
         }
         if (running && tid < n) {  // px[0] holds xs[t+1][tid] now
           double* f = D.fs + D.knot(b, t + 1) * D.sN;
           const double* xng = D.xnext[c] + D.run(b, t) * D.sX;
           f[tid] = (want_dyn ? xn[tid] : xng[tid]) - px[0];
         }
-      } else if (!s.was_feasible) {  // closing the gaps
-        double* f = D.fs + kk * D.sN;
-        for (int i = tid; i < n; i += NT) f[i] = 0.;
+      } else if (!s.was_feasible && tid < n) {  // closing the gaps
+        D.fs[kk * D.sN + tid] = 0.;
       }
     }
     __syncthreads();
+    stamp.mark(7);
   }
+  stamp.flush();
 }
 
 // ---------------------------------------------------------------------------
@@ -473,7 +535,7 @@ __device__ __forceinline__ bool fwd_trial_fast(const Dev& D, int b, const ElemSt
     }
     const DenseKnot K(kd.kind, P, nx, nu);
     double cp = dense_partials<NT>(K, nx, nu, running && nu > 0, xu, running, false, false, true, pdyn, nullptr,
-                                   nullptr);
+                                   nullptr, tid);
     cp = wave_sum(cp);
     if (lane == 0) red[wid] = cp;
     __syncthreads();

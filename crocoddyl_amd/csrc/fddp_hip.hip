@@ -446,7 +446,7 @@ int fddp_create(const fddp_dims* dims, const fddp_knot_desc* knots, const double
   h->calc_smem = sizeof(double) * (h->pcap + 2 * D.sX + D.sM + 5 * (kNT / kWave) + 16);
   h->cdiff_smem = sizeof(double) * (h->pcap + D.sX + D.sM);
   {  // dense-knot fast path: every knot LQR / Euler∘DiffLQR, block LDS-resident
-    bool dense = h->pcap > 0 && d.nx == d.ndx && d.nx <= kNT && d.nu_max <= kNT && d.nx <= kNTF;
+    bool dense = h->pcap > 0 && d.nx == d.ndx && d.nx <= kNT && d.nu_max <= kNT;
     for (int t = 0; t <= d.T; ++t)
       dense = dense && (knots[t].kind == FDDP_KNOT_LQR || knots[t].kind == FDDP_KNOT_EULER_DIFFLQR);
     h->fused_smem = sizeof(double) * (h->pcap + 2 * D.sX + D.sM + 3 * kNTF + 16);
@@ -536,7 +536,7 @@ int fddp_create(const fddp_dims* dims, const fddp_knot_desc* knots, const double
   if (const char* e = std::getenv("FDDP_STAMPS")) {
     if (e[0] == '1') {
       double* p2 = nullptr;
-      if ((rc = dalloc(h, &p2, (int64_t)d.B * 64))) return bail(rc);
+      if ((rc = dalloc(h, &p2, (int64_t)d.B * 128))) return bail(rc);
       D.stamps = (unsigned long long*)p2;
     }
   }
@@ -550,7 +550,7 @@ void fddp_destroy(fddp_handle* h) {
   DeviceGuard g(h->device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   if (h->D.stamps) {  // diagnostic summary: mean cycles per element per wave and phase
-    std::vector<unsigned long long> v((size_t)h->dims.B * 64);
+    std::vector<unsigned long long> v((size_t)h->dims.B * 128);
     if (hipMemcpy(v.data(), h->D.stamps, v.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
       const char* names[8] = {"p1_G", "p1_H", "p1_inv", "b1_dma", "p2_K", "p2_Vupd", "b2_p3", "b3_wait"};
       std::fprintf(stderr, "[fddp stamps] mean cycles per element (variant %d):\n", h->bwd_variant);
@@ -562,6 +562,19 @@ void fddp_destroy(fddp_handle* h) {
           std::fprintf(stderr, " %s=%.0f", names[ph], s2 / h->dims.B);
         }
         std::fprintf(stderr, "\n");
+      }
+      if (h->fast) {
+        const char* fn[8] = {"stage", "bar1", "blocks1+partials", "bar2", "finalize", "blocks2", "bar3", "tail"};
+        std::fprintf(stderr, "[fddp stamps] fused calc/calcDiff, mean cycles per element:\n");
+        for (int w = 0; w < 8; ++w) {
+          std::fprintf(stderr, "  wave %d:", w);
+          for (int ph = 0; ph < 8; ++ph) {
+            double s2 = 0;
+            for (int b = 0; b < h->dims.B; ++b) s2 += (double)v[(size_t)h->dims.B * 64 + ((size_t)b * 8 + w) * 8 + ph];
+            std::fprintf(stderr, " %s=%.0f", fn[ph], s2 / h->dims.B);
+          }
+          std::fprintf(stderr, "\n");
+        }
       }
     }
   }

@@ -99,7 +99,7 @@ __device__ __forceinline__ void wg_gemm(int M, int N, int K, const double* __res
 template <int NT>
 __global__ __launch_bounds__(NT) void calc_kernel(Dev D, int sel, int64_t pcap) {
   const int b = blockIdx.x;
-  const ElemState& s = D.st[b];
+  const ElemState s = D.st[b];  // by value: a reference would re-load it from HBM after every store
   if (!selected(s, sel)) return;
   extern __shared__ __attribute__((aligned(16))) double sm[];
   double* pl = sm;               // pcap
@@ -153,7 +153,7 @@ __global__ void cost_sum_kernel(Dev D, int sel, double* out) {
 template <int NT>
 __global__ __launch_bounds__(NT) void calc_diff_kernel(Dev D, int sel, int gaps, int64_t pcap) {
   const int b = blockIdx.x;
-  const ElemState& s = D.st[b];
+  const ElemState s = D.st[b];  // by value: a reference would re-load it from HBM after every store
   if (!selected(s, sel)) return;
   extern __shared__ __attribute__((aligned(16))) double sm[];
   double* pl = sm;
