@@ -17,14 +17,21 @@ pytestmark = pytest.mark.gpu
 RTOL = 1e-6  # north_star: xs/us/cost within 1e-6 relative
 
 
-@pytest.fixture(params=["mfma", "generic"], autouse=True)
+@pytest.fixture(params=["default", "mfma4_slowpath", "generic"], autouse=True)
 def backward_variant(request, monkeypatch):
-    """Run every parity test with the MFMA Riccati sweep (default where the
-    shape allows) and with the generic LDS sweep (FDDP_BACKWARD=generic)."""
+    """Run every parity test on each device code path:
+    default         8-wave MFMA Riccati sweep (where the shape allows) and the
+                    dense-knot fast path for calc / calcDiff / forward;
+    mfma4_slowpath  4-wave MFMA sweep (FDDP_BWD_WAVES=4) and the generic
+                    calc / calcDiff / forward kernels (FDDP_FAST=0);
+    generic         the generic LDS Riccati sweep (FDDP_BACKWARD=generic)."""
+    for var in ("FDDP_BACKWARD", "FDDP_BWD_WAVES", "FDDP_FAST"):
+        monkeypatch.delenv(var, raising=False)
     if request.param == "generic":
         monkeypatch.setenv("FDDP_BACKWARD", "generic")
-    else:
-        monkeypatch.delenv("FDDP_BACKWARD", raising=False)
+    elif request.param == "mfma4_slowpath":
+        monkeypatch.setenv("FDDP_BWD_WAVES", "4")
+        monkeypatch.setenv("FDDP_FAST", "0")
     return request.param
 
 CASES = [
