@@ -20,92 +20,10 @@
 #pragma once
 
 #include "fddp_kernels.hpp"
+#include "dense_knot.hpp"
 #include "bwd_mfma.hpp"  // Stamp
 
 namespace fddp {
-
-struct DenseKnot {
-  bool dlqr, integ, drift_free;
-  double dt, sc;  // Euler step; cost / derivative scale (dt when integrating)
-  int nr;         // dynamics rows: nx (LQR) or nq (Euler∘DiffLQR)
-  const double *F, *f0, *Lxx, *Lxu, *Luu, *lx, *lu;
-  __device__ DenseKnot(int kind, const double* P, int nx, int nu) {
-    if (kind == FDDP_KNOT_LQR) {
-      LQRBlk Bk(P, nx, nu);
-      dlqr = false;
-      integ = false;
-      dt = 0.;
-      sc = 1.;
-      drift_free = Bk.drift_free;
-      nr = nx;
-      F = Bk.Fx;
-      f0 = Bk.f0;
-      Lxx = Bk.Lxx;
-      Lxu = Bk.Lxu;
-      Luu = Bk.Luu;
-      lx = Bk.lx;
-      lu = Bk.lu;
-    } else {
-      DLQRBlk Bk(P, nx, nu);
-      dlqr = true;
-      dt = Bk.dt;
-      integ = dt != 0.;
-      sc = integ ? dt : 1.;
-      drift_free = Bk.drift_free;
-      nr = nx / 2;
-      F = Bk.Fq;
-      f0 = Bk.f0;
-      Lxx = Bk.Lxx;
-      Lxu = Bk.Lxu;
-      Luu = Bk.Luu;
-      lx = Bk.lx;
-      lu = Bk.lu;
-    }
-  }
-};
-
-__device__ __forceinline__ bool dense_kind(int kind) { return kind == FDDP_KNOT_LQR || kind == FDDP_KNOT_EULER_DIFFLQR; }
-
-// Thread -> (row i, column segment g) of a rows-row product; G segments.
-struct RowSeg {
-  int i, g, G;
-  bool on;
-  __device__ RowSeg(int rows, int nt, int tid) {
-    G = rows > 0 ? nt / rows : 1;
-    if (G < 1) G = 1;
-    i = rows > 0 ? tid % rows : 0;
-    g = rows > 0 ? tid / rows : 0;
-    on = rows > 0 && g < G;
-  }
-};
-
-// sum_{j = j0, j0+G, ... < cols} A[j*lda + i] * v[j], four accumulators.
-__device__ __forceinline__ double seg_dot(const double* A, int lda, int i, int j0, int G, int cols, const double* v) {
-  double a0 = 0., a1 = 0., a2 = 0., a3 = 0.;
-  int j = j0;
-  for (; j + 3 * G < cols; j += 4 * G) {
-    a0 = fma(A[j * lda + i], v[j], a0);
-    a1 = fma(A[(j + G) * lda + i], v[j + G], a1);
-    a2 = fma(A[(j + 2 * G) * lda + i], v[j + 2 * G], a2);
-    a3 = fma(A[(j + 3 * G) * lda + i], v[j + 3 * G], a3);
-  }
-  for (; j < cols; j += G) a0 = fma(A[j * lda + i], v[j], a0);
-  return (a0 + a1) + (a2 + a3);
-}
-// Transposed: sum_j A[i*lda + j] * v[j] (row i of A^T = column i of A).
-__device__ __forceinline__ double seg_dot_t(const double* A, int lda, int i, int j0, int G, int cols, const double* v) {
-  const double* a = A + i * lda;
-  double a0 = 0., a1 = 0., a2 = 0., a3 = 0.;
-  int j = j0;
-  for (; j + 3 * G < cols; j += 4 * G) {
-    a0 = fma(a[j], v[j], a0);
-    a1 = fma(a[j + G], v[j + G], a1);
-    a2 = fma(a[j + 2 * G], v[j + 2 * G], a2);
-    a3 = fma(a[j + 3 * G], v[j + 3 * G], a3);
-  }
-  for (; j < cols; j += G) a0 = fma(a[j], v[j], a0);
-  return (a0 + a1) + (a2 + a3);
-}
 
 // Per-thread partials of one dense knot at (x, u) = xu[0..nx), xu[nx..nx+nu):
 //   dyn : dynamics row partial (-> pdyn[g*nr + i])
@@ -182,34 +100,6 @@ __device__ __forceinline__ void dense_xnext(const DenseKnot& K, int nx, int i, d
   }
 }
 
-// Streams one knot's derivative blocks out: thread -> (row pair, column
-// segment), 16-byte stores (n even; odd n falls back to 8-byte stores). The
-// per-row factors of the Euler integration are per-thread constants; each
-// column is a coalesced store across consecutive row pairs.
-__device__ __forceinline__ void dense_fx_rows(const DenseKnot& K, int n, int i, int& ldf, int& ri, int& jd, double& a) {
-  ldf = n;
-  ri = i;
-  jd = -1;
-  a = 1.;
-  if (K.dlqr) {
-    const int nv = n / 2;
-    ldf = nv;
-    ri = i < nv ? i : i - nv;
-    a = K.integ ? (i < nv ? K.dt * K.dt : K.dt) : 0.;
-    jd = (K.integ && i < nv) ? nv + i : -1;
-  }
-}
-__device__ __forceinline__ double dense_fx_at(const DenseKnot& K, int n, int i, int j, int ldf, int ri, int jd, double a) {
-  double f = K.dlqr ? (K.integ ? a * K.F[j * ldf + ri] : 0.) : K.F[j * n + i];
-  if (j == jd) f += K.dt;
-  if (K.dlqr && j == i) f += 1.;
-  return f;
-}
-__device__ __forceinline__ double dense_fu_at(const DenseKnot& K, int n, int nu, int i, int j, int ldf, int ri, double a) {
-  if (j >= nu) return 0.;
-  return K.dlqr ? (K.integ ? a * K.F[(n + j) * ldf + ri] : 0.) : K.F[(n + j) * n + i];
-}
-
 template <int NT>
 __device__ __forceinline__ void dense_write_blocks(const DenseKnot& K, int n, int m, int nu, const KnotDiffOut& o,
                                                    int part, int tid) {
@@ -280,136 +170,379 @@ __device__ __forceinline__ void dense_write_blocks(const DenseKnot& K, int n, in
 // ---------------------------------------------------------------------------
 // ShootingProblem::calc (shooting.hxx:133-161) and/or calcDiff (164-195) with
 // the gaps of SolverDDP::calcDiff (ddp.cpp:160-176), fused: one workgroup per
-// element walks its knots with the parameter block LDS-resident. Elements
-// selected by sel_calc get xnext and the knot costs, those selected by
-// sel_diff the derivative blocks (+ gaps when `gaps`).
-// The derivative blocks (140 KB per knot at C5) dominate: they are written
-// by every wave with 16-byte stores (a wave's store throughput is bounded by
-// its outstanding stores, so bytes per store and waves per CU both count),
-// half of them before the LDS-bound partial sums so that they drain while
-// those run.
+// element, the parameter block LDS-resident. Elements selected by sel_calc
+// get xnext and the knot costs, those selected by sel_diff the derivative
+// blocks, Lx, Lu (+ gaps when `gaps`).
+// Knots that share one parameter block (the reference's std::vector(T, model)
+// shares one model over the running knots; host-computed segments) go in
+// tiles of 8: the per-knot matrix-vector products of a tile become one small
+// matrix product, [Lxx | Lxu] [x; u], [Lxu^T | Luu] [x; u] and F [x; u]
+// (F = [Fx | Fu] or [Fq | Fv | Fu]) with one output row per lane and 8 knot
+// columns in flight (8 independent FMA chains, operands broadcast from LDS);
+// Lx, Lu, xnext, gaps and knot costs are written straight from registers.
+// The 140 KB of derivative blocks per knot (C5) are the bulk: dedicated
+// waves stream them with 16-byte stores and never load from global memory.
 // ---------------------------------------------------------------------------
+__device__ __forceinline__ void dense_xnext2(const DenseKnot& K, int nx, int i, double a, double xi, double vi,
+                                             double& o0, double& o1) {  // dense_xnext for one row pair
+  if (!K.drift_free) a += K.f0[i];
+  if (!K.dlqr) {
+    o0 = a;
+    return;
+  }
+  if (K.integ) {
+    const double dt = K.dt, dt2 = dt * dt;
+    const double dq = vi * dt + a * dt2;  // v*dt + a*dt^2 (euler.hxx:66)
+    const double dv = a * dt;             // a*dt (euler.hxx:67)
+    o0 = xi + dq;
+    o1 = vi + dv;
+  } else {
+    o0 = xi;
+    o1 = vi;
+  }
+}
+
+constexpr int kCalcKT = 16;  // knots per compute tile (the MFMA N dimension)
+constexpr int kCalcKP = 18;  // xu columns: the tile's knots + x of the next knot, padded even
+
+// LDS doubles of calc_tiled_kernel besides the parameter block
+__host__ __device__ inline int64_t calc_tiled_lds(int64_t sX, int64_t sM) {
+  return (sX + sM) * kCalcKP + 8 * 16 + 16;
+}
+
+// Knot descriptors and segment ends through the constant address space:
+// scalar loads (lgkmcnt), which do not queue behind the global stores in
+// flight the way vector loads do (loads and stores share vmcnt, in order).
+__device__ __forceinline__ fddp_knot_desc knot_desc_s(const Dev& D, int t) {
+  typedef __attribute__((address_space(4))) const fddp_knot_desc* cptr;
+  const cptr p = (cptr)D.knots + t;
+  fddp_knot_desc k;
+  k.kind = p->kind;
+  k.nu = p->nu;
+  k.param_offset = p->param_offset;
+  k.param_stride = p->param_stride;
+  return k;
+}
+__device__ __forceinline__ int segend_s(const Dev& D, int t) {
+  typedef __attribute__((address_space(4))) const int* cptr;
+  return ((cptr)D.segend)[t];
+}
+
+// Parameter block -> LDS by LDS-DMA (no register round trip: every chunk of
+// the block is in flight at once). The fast path guarantees size <= the LDS
+// reserve (fddp_create); callers then read the block through the LDS pointer
+// itself, so that the compiler emits LDS reads: a flat read (pointer of
+// unknown address space) also waits on vmcnt, i.e. for every global store
+// still in flight.
 template <int NT>
-__global__ __launch_bounds__(NT) void calc_fused_kernel(Dev D, int sel_calc, int sel_diff, int gaps, int64_t pcap) {
+__device__ __forceinline__ void stage_params_batched(const double* g, int64_t size, double* lds, const double*& cached) {
+  if (g == cached) return;
+  __syncthreads();
+  if ((reinterpret_cast<uintptr_t>(g) & 15) == 0) {
+    dma_vec<NT / 64>(lds, g, (int)size, threadIdx.x >> 6, threadIdx.x & 63);
+    dma_barrier();
+  } else {
+    for (int64_t e = threadIdx.x; e < size; e += NT) lds[e] = g[e];
+    __syncthreads();
+  }
+  cached = g;
+}
+
+// One compute tile (knots t0..t0+nt-1, nt <= 16, one parameter block) on the
+// workgroup's fp64 matrix cores: the stacked products
+//   R1 = [Lxx x | Lxu u]   (Lx, cost)      rows i < nx
+//   R2 = [Lxu^T x | Luu u] (Lu, cost)      rows j < nu
+//   R3 = F [x; u]          (xnext, gaps)   rows i < nr   (calc only)
+// for the tile's 16 knot columns, in 16-row blocks spread over the waves
+// (v_mfma_f64_16x16x4: A = parameter rows from LDS, B = xu[k][knot] from
+// LDS; accumulator register r of lane (q, c) = row q + 4r of knot column c).
+// The x and u parts of R1 / R2 accumulate separately (the cost uses
+// 0.5 x.Lxx x + x.Lxu u). Outputs are written from the accumulators; knot
+// costs are reduced through `red` ([8 waves][16]).
+template <int NT>
+__device__ __forceinline__ void calc_tile_mfma(const Dev& D, const DenseKnot& K, const ElemState& s, int b, int t0,
+                                               int nt, int nu, bool do_calc, bool do_diff, int gaps, double* xu,
+                                               double* red, int tid) {
+  constexpr int KP = kCalcKP, NW = NT / 64;
+  const int c_ = s.cur, nx = D.nx, n = D.n, m = D.m, T = D.T;
+  const int lane = tid & 63, wid = tid >> 6, q = lane >> 4, cc = lane & 15;
+  const bool running = t0 < T;
+  const int nuu = running ? nu : 0, nk = nx + nuu;
+  // xu: x of knots t0..t0+nt (the last for the gaps; none after the terminal
+  // knot), u of t0..t0+nt-1; entry e -> (column tt, row k), rows fastest
+  {
+    const int cnt = nk * nt + (t0 + nt <= T ? nx : 0);
+    constexpr int U = 4;
+    for (int base = 0; base < cnt; base += NT * U) {
+      double r[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int e0 = base + NT * u + tid, e = e0 < cnt ? e0 : cnt - 1;
+        const int tt = e / nk, k = e - tt * nk;
+        r[u] = k < nx ? D.xs[c_][D.knot(b, t0 + tt) * D.sX + k] : D.us[c_][D.run(b, t0 + tt) * D.sM + k - nx];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int e = base + NT * u + tid;
+        if (e < cnt) {
+          const int tt = e / nk, k = e - tt * nk;
+          xu[k * KP + tt] = r[u];
+        }
+      }
+    }
+  }
+  __syncthreads();
+  const bool scale = K.dlqr && K.integ;
+  const bool want_dyn = do_calc && running;
+  const bool infeas_gaps = do_diff && gaps && !s.is_feasible;
+  const int nb1 = (nx + 15) >> 4, nb2 = nu > 0 ? (nu + 15) >> 4 : 0, nb3 = want_dyn ? (K.nr + 15) >> 4 : 0;
+  const int nq = nx / 2;
+  const bool col_ok = cc < nt;
+  const int t = t0 + cc;
+  double cp = 0.;  // this lane's share of knot cc's cost
+  for (int rb = wid; rb < nb1 + nb2 + nb3; rb += NW) {
+    f64x4 a1 = {0., 0., 0., 0.}, a2 = {0., 0., 0., 0.};
+    if (rb < nb1) {  // R1 rows r0 + c: Lxx (x part) and Lxu (u part)
+      const int r0 = 16 * rb, ra = r0 + cc;
+      for (int k0 = 0; k0 < nx; k0 += 4) {
+        const int k = k0 + q;
+        const double av = (ra < nx && k < nx) ? K.Lxx[k * nx + ra] : 0.;
+        const double bv = k < nx ? xu[k * KP + cc] : 0.;
+        a1 = mfma4(av, bv, a1);
+      }
+      for (int k0 = 0; k0 < nuu; k0 += 4) {
+        const int k = k0 + q;
+        const double av = (ra < nx && k < nuu) ? K.Lxu[k * nx + ra] : 0.;
+        const double bv = k < nuu ? xu[(nx + k) * KP + cc] : 0.;
+        a2 = mfma4(av, bv, a2);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = r0 + q + 4 * r;
+        if (col_ok && i < nx) {
+          const double xi = xu[i * KP + cc];
+          if (do_diff) {
+            const double l = K.lx[i] + (a1[r] + a2[r]);
+            D.Lx[D.knot(b, t) * D.sN + i] = scale ? K.sc * l : l;
+          }
+          cp += fma(K.lx[i], xi, xi * (0.5 * a1[r] + a2[r]));
+        }
+      }
+    } else if (rb < nb1 + nb2) {  // R2 rows: Lxu^T (x part) and Luu (u part)
+      const int r0 = 16 * (rb - nb1), ra = r0 + cc;
+      for (int k0 = 0; k0 < nx; k0 += 4) {
+        const int k = k0 + q;
+        const double av = (ra < nu && k < nx) ? K.Lxu[ra * nx + k] : 0.;
+        const double bv = k < nx ? xu[k * KP + cc] : 0.;
+        a1 = mfma4(av, bv, a1);
+      }
+      for (int k0 = 0; k0 < nuu; k0 += 4) {
+        const int k = k0 + q;
+        const double av = (ra < nu && k < nuu) ? K.Luu[k * nu + ra] : 0.;
+        const double bv = k < nuu ? xu[(nx + k) * KP + cc] : 0.;
+        a2 = mfma4(av, bv, a2);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int j = r0 + q + 4 * r;
+        if (col_ok && j < nu) {
+          if (do_diff) {
+            const double l = K.lu[j] + (a1[r] + a2[r]);
+            D.Lu[D.knot(b, t) * D.sM + j] = scale ? K.sc * l : l;
+          }
+          if (nuu > 0) {
+            const double uj = xu[(nx + j) * KP + cc];
+            cp += fma(K.lu[j], uj, 0.5 * uj * a2[r]);
+          }
+        }
+      }
+    } else {  // R3 rows of F [x; u]: xnext (+ the gaps fs[t+1] = xnext - xs[t+1])
+      const int r0 = 16 * (rb - nb1 - nb2), ra = r0 + cc;
+      for (int k0 = 0; k0 < nk; k0 += 4) {
+        const int k = k0 + q;
+        const double av = (ra < K.nr && k < nk) ? K.F[k * K.nr + ra] : 0.;
+        const double bv = k < nk ? xu[k * KP + cc] : 0.;
+        a1 = mfma4(av, bv, a1);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = r0 + q + 4 * r;
+        if (col_ok && i < K.nr) {
+          double* xo = D.xnext[c_] + D.run(b, t) * D.sX;
+          double* f = D.fs + D.knot(b, t + 1) * D.sN;
+          double o0, o1 = 0.;
+          dense_xnext2(K, nx, i, a1[r], xu[i * KP + cc], K.dlqr ? xu[(nq + i) * KP + cc] : 0., o0, o1);
+          xo[i] = o0;
+          if (infeas_gaps) f[i] = o0 - xu[i * KP + cc + 1];
+          if (K.dlqr) {
+            xo[nq + i] = o1;
+            if (infeas_gaps) f[nq + i] = o1 - xu[(nq + i) * KP + cc + 1];
+          }
+        }
+      }
+    }
+  }
+  if (do_calc) {
+    cp += __shfl_xor(cp, 16, 64);
+    cp += __shfl_xor(cp, 32, 64);
+    if (q == 0) red[wid * 16 + cc] = cp;
+  }
+  __syncthreads();
+  if (do_calc && tid < nt) {
+    double cst = 0.;
+    for (int w = 0; w < NW; ++w) cst += red[w * 16 + tid];
+    D.kcost[c_][D.knot(b, t0 + tid)] = scale ? K.dt * cst : cst;
+  }
+  if (do_diff && m > nu) {  // Lu rows nu..m-1 of the padded block
+    for (int e = tid; e < nt * (m - nu); e += NT) {
+      const int tt = e / (m - nu), j = nu + e - tt * (m - nu);
+      D.Lu[D.knot(b, t0 + tt) * D.sM + j] = 0.;
+    }
+  }
+  if (do_diff && gaps) {
+    if (!s.is_feasible) {
+      // fs[0] = diff(xs[0], x0) = x0 - xs[0]; fs[t+1] = diff(xs[t+1], data[t].xnext)
+      if (t0 == 0)
+        for (int i = tid; i < n; i += NT) D.fs[D.knot(b, 0) * D.sN + i] = D.x0[(int64_t)b * D.sX + i] - xu[i * KP];
+      if (running && !want_dyn)  // xnext of the current candidate (computed by an earlier calc)
+        for (int e = tid; e < nt * n; e += NT) {
+          const int tt = e / n, i = e - tt * n;
+          D.fs[D.knot(b, t0 + tt + 1) * D.sN + i] = D.xnext[c_][D.run(b, t0 + tt) * D.sX + i] - xu[i * KP + tt + 1];
+        }
+    } else if (!s.was_feasible) {  // closing the gaps
+      for (int e = tid; e < nt * n; e += NT) {
+        const int tt = e / n, i = e - tt * n;
+        D.fs[D.knot(b, t0 + tt) * D.sN + i] = 0.;
+      }
+    }
+  }
+  __syncthreads();  // xu / red free for the next tile
+}
+
+// The derivative blocks of knots [ts, te) (one parameter block, so the same
+// values at every knot): each thread computes its 16-byte units of a block
+// once (unit u = doubles 2u, 2u+1 of the column-major block: rows 2p, 2p+1 of
+// column j) and then only stores them, knot after knot. Same values as
+// dense_write_blocks. Needs n and m even (callers check).
+// A: 0 Lxx, 1 Fx, 2 Fu, 3 Lxu, 4 Luu.
+template <int A>
+__device__ __forceinline__ double2 block_unit(const DenseKnot& K, int n, int nu, double sc, int i0, int j) {
+  double2 w;
+  if constexpr (A == 0) {
+    w.x = sc * K.Lxx[j * n + i0];
+    w.y = sc * K.Lxx[j * n + i0 + 1];
+  } else if constexpr (A == 1 || A == 2) {
+    int ldf0, ri0, jd0, ldf1, ri1, jd1;
+    double a0, a1;
+    dense_fx_rows(K, n, i0, ldf0, ri0, jd0, a0);
+    dense_fx_rows(K, n, i0 + 1, ldf1, ri1, jd1, a1);
+    if constexpr (A == 1) {
+      w.x = dense_fx_at(K, n, i0, j, ldf0, ri0, jd0, a0);
+      w.y = dense_fx_at(K, n, i0 + 1, j, ldf1, ri1, jd1, a1);
+    } else {
+      w.x = dense_fu_at(K, n, nu, i0, j, ldf0, ri0, a0);
+      w.y = dense_fu_at(K, n, nu, i0 + 1, j, ldf1, ri1, a1);
+    }
+  } else if constexpr (A == 3) {
+    const bool in = j < nu;
+    w.x = in ? sc * K.Lxu[j * n + i0] : 0.;
+    w.y = in ? sc * K.Lxu[j * n + i0 + 1] : 0.;
+  } else {
+    w.x = (i0 < nu && j < nu) ? sc * K.Luu[j * nu + i0] : 0.;
+    w.y = (i0 + 1 < nu && j < nu) ? sc * K.Luu[j * nu + i0 + 1] : 0.;
+  }
+  return w;
+}
+
+template <int A, int NB>
+__device__ __forceinline__ void write_block_segment(const Dev& D, const DenseKnot& K, int b, int ts, int te, int nu,
+                                                    double sc, int ptid) {
+  constexpr int UK = 8;  // units per thread in flight
+  const int n = D.n, m = D.m;
+  double* const base = A == 0 ? D.Lxx : A == 1 ? D.Fx : A == 2 ? D.Fu : A == 3 ? D.Lxu : D.Luu;
+  const int64_t stride = A <= 1 ? D.sNN : A <= 3 ? D.sNM : D.sMM;
+  const int nrow = A <= 3 ? n : m, ncol = A <= 1 ? n : m;
+  const int np = nrow / 2, units = np * ncol;
+  for (int u0 = 0; u0 < units; u0 += UK * NB) {
+    double2 v[UK];
+#pragma unroll
+    for (int k = 0; k < UK; ++k) {
+      const int u = u0 + k * NB + ptid, uc = u < units ? u : units - 1;
+      const int j = uc / np, i0 = 2 * (uc - j * np);
+      v[k] = block_unit<A>(K, n, nu, sc, i0, j);
+    }
+    for (int t = ts; t < te; ++t) {
+      double2* dst = reinterpret_cast<double2*>(base + D.knot(b, t) * stride);
+#pragma unroll
+      for (int k = 0; k < UK; ++k) {
+        const int u = u0 + k * NB + ptid;
+        if (u < units) dst[u] = v[k];
+      }
+    }
+  }
+}
+
+template <int NB>
+__device__ __forceinline__ void write_blocks_segment(const Dev& D, const DenseKnot& K, int b, int ts, int te, int nu,
+                                                     int ptid) {
+  const double sc = (K.dlqr && K.integ) ? K.sc : 1.;
+  write_block_segment<0, NB>(D, K, b, ts, te, nu, sc, ptid);
+  write_block_segment<1, NB>(D, K, b, ts, te, nu, sc, ptid);
+  write_block_segment<2, NB>(D, K, b, ts, te, nu, sc, ptid);
+  write_block_segment<3, NB>(D, K, b, ts, te, nu, sc, ptid);
+  write_block_segment<4, NB>(D, K, b, ts, te, nu, sc, ptid);
+}
+
+// Per segment: the compute tiles (calc_tile_mfma, the whole workgroup), then
+// every wave streams its share of the derivative blocks (params in LDS ->
+// registers -> global; the block writer loads nothing from global memory, so
+// its stores never wait, and no compute load queues behind them).
+template <int NT>
+__global__ __launch_bounds__(NT) void calc_tiled_kernel(Dev D, int sel_calc, int sel_diff, int gaps, int64_t pcap) {
+  constexpr int KT = kCalcKT, KP = kCalcKP;
   const int b = blockIdx.x;
   const ElemState s = D.st[b];  // by value: a reference would re-load it from HBM after every store
   const bool do_calc = sel_calc >= 0 && selected(s, sel_calc);
   const bool do_diff = sel_diff >= 0 && selected(s, sel_diff);
   if (!do_calc && !do_diff) return;
   extern __shared__ __attribute__((aligned(16))) double sm[];
-  double* pl = sm;                 // pcap
-  double* xu = pl + pcap;          // sX + sM
-  double* xn = xu + D.sX + D.sM;   // sX
-  double* pdyn = xn + D.sX;        // NT
-  double* plx = pdyn + NT;         // NT
-  double* plu = plx + NT;          // NT
-  double* red = plu + NT;          // 16
-  const int c = s.cur, nx = D.nx, n = D.n, m = D.m, T = D.T, tid = threadIdx.x;
-  const int lane = tid & 63, wid = tid >> 6;
+  const int nx = D.nx, n = D.n, m = D.m, T = D.T, tid = threadIdx.x;
+  const int wid = tid >> 6;
+  double* pl = sm;
+  double* xu = pl + pcap;                   // [nx + m][KP]
+  double* red = xu + (D.sX + D.sM) * KP;    // [8][16]
   const double* cached = nullptr;
   Stamp stamp(D.stamps ? D.stamps + (int64_t)D.B * 64 + ((int64_t)b * 8 + wid) * 8 : nullptr);
-  // x and u of knots t+1..t+PD are in flight in registers while knot t
-  // computes (a rotating window; thread i holds x_i, u_i; nx, m <= NT here)
-  constexpr int PD = 4;
-  double px[PD], pu[PD];
-  auto fetch = [&](int t, double& x_, double& u_) {
-    x_ = (t <= T && tid < nx) ? D.xs[c][D.knot(b, t) * D.sX + tid] : 0.;
-    u_ = (t < T && tid < m) ? D.us[c][D.run(b, t) * D.sM + tid] : 0.;
-  };
-#pragma unroll
-  for (int q = 0; q < PD; ++q) fetch(q, px[q], pu[q]);
-  for (int t = 0; t <= T; ++t) {
-    const fddp_knot_desc kd = D.knots[t];
-    const double* P = stage_params<NT>(D.pblock(b, t), block_doubles_dev(kd.kind, nx, kd.nu), pl, pcap, cached);
-    const int64_t kk = D.knot(b, t);
-    const bool running = t < T;
+  for (int ts = 0; ts <= T;) {
+    const int te = segend_s(D, ts);  // knots [ts, te) share knot desc and parameter block
+    const fddp_knot_desc kd = knot_desc_s(D, ts);
     const int nu = kd.nu;
-    const bool use_u = running && nu > 0;
-    if (tid < nx) xu[tid] = px[0];
-    if (use_u && tid < nu) xu[nx + tid] = pu[0];
-#pragma unroll
-    for (int q = 0; q + 1 < PD; ++q) {
-      px[q] = px[q + 1];
-      pu[q] = pu[q + 1];
-    }
-    fetch(t + PD, px[PD - 1], pu[PD - 1]);
+    stage_params_batched<NT>(D.params + kd.param_offset + (int64_t)b * kd.param_stride,
+                             block_doubles_dev(kd.kind, nx, nu), pl, cached);
     stamp.mark(0);
-    __syncthreads();
+    const DenseKnot K(kd.kind, pl, nx, nu);
+    for (int t0 = ts; t0 < te; t0 += KT) {
+      const int nt = te - t0 < KT ? te - t0 : KT;
+      calc_tile_mfma<NT>(D, K, s, b, t0, nt, nu, do_calc, do_diff, gaps, xu, red, tid);
+    }
     stamp.mark(1);
-    const DenseKnot K(kd.kind, P, nx, nu);
-    const bool want_dyn = do_calc && running;
-    KnotDiffOut o;
-    o.Fx = D.Fx + kk * D.sNN;
-    o.Fu = D.Fu + kk * D.sNM;
-    o.Lxx = D.Lxx + kk * D.sNN;
-    o.Lxu = D.Lxu + kk * D.sNM;
-    o.Luu = D.Luu + kk * D.sMM;
-    if (do_diff) dense_write_blocks<NT>(K, n, m, nu, o, 1, tid);
-    double cp = dense_partials<NT>(K, nx, nu, use_u, xu, want_dyn, do_diff, do_diff, do_calc, pdyn, plx, plu, tid);
-    if (do_calc) {
-      cp = wave_sum(cp);
-      if (lane == 0) red[wid] = cp;
-    }
-    stamp.mark(2);
-    __syncthreads();
-    stamp.mark(3);
-    // reductions spread over the waves: xnext rows from thread 0, Lu rows
-    // from 64, Lx rows from 128 (NT = 512 here), the cost on thread NT - 1
-    constexpr int TLU = NT >= 256 ? 64 : 0, TLX = NT >= 256 ? 128 : 0, TC = NT - 1;
-    if (want_dyn) {
-      for (int i = tid; i < K.nr; i += NT) dense_xnext(K, nx, i, seg_sum(pdyn, K.nr, i, NT), xu, xn);
-    }
-    if (do_calc && tid == TC) {
-      double cst = 0.;
-      for (int w = 0; w < NT / 64; ++w) cst += red[w];
-      cst = K.dlqr && K.integ ? K.dt * cst : cst;
-      D.kcost[c][kk] = cst;
-    }
-    if (do_diff) {
-      const bool scale = K.dlqr && K.integ;
-      double* Lx = D.Lx + kk * D.sN;
-      double* Lu = D.Lu + kk * D.sM;
-      for (int i = tid - TLX; i >= 0 && i < n; i += NT) {
-        const double l = K.lx[i] + seg_sum(plx, nx, i, NT);
-        Lx[i] = scale ? K.sc * l : l;
+    if (do_diff && (n & 1) == 0 && (m & 1) == 0) {
+      write_blocks_segment<NT>(D, K, b, ts, te, nu, tid);
+    } else if (do_diff) {
+      for (int t = ts; t < te; ++t) {
+        const int64_t kk = D.knot(b, t);
+        KnotDiffOut o;
+        o.Fx = D.Fx + kk * D.sNN;
+        o.Fu = D.Fu + kk * D.sNM;
+        o.Lxx = D.Lxx + kk * D.sNN;
+        o.Lxu = D.Lxu + kk * D.sNM;
+        o.Luu = D.Luu + kk * D.sMM;
+        dense_write_blocks<NT>(K, n, m, nu, o, 3, tid);
       }
-      for (int i = tid - TLU; i >= 0 && i < m; i += NT) {
-        double v = 0.;
-        if (i < nu) {
-          const double l = K.lu[i] + seg_sum(plu, nu, i, NT);
-          v = scale ? K.sc * l : l;
-        }
-        Lu[i] = v;
-      }
-      stamp.mark(4);
-      dense_write_blocks<NT>(K, n, m, nu, o, 2, tid);
     }
     stamp.mark(5);
-    __syncthreads();  // xn complete
-    stamp.mark(6);
-    if (want_dyn) {
-      double* xo = D.xnext[c] + D.run(b, t) * D.sX;
-      if (tid < nx) xo[tid] = xn[tid];
-    }
-    if (do_diff && gaps) {
-      if (!s.is_feasible) {
-        // fs[0] = diff(xs[0], x0) = x0 - xs[0]; fs[t+1] = diff(xs[t+1], data[t].xnext)
-        if (t == 0 && tid < n) {
-          double* f = D.fs + D.knot(b, 0) * D.sN;
-          const double* x0 = D.x0 + (int64_t)b * D.sX;
-          f[tid] = x0[tid] - xu[tid];
-        }
-        if (running && tid < n) {  // px[0] holds xs[t+1][tid] now
-          double* f = D.fs + D.knot(b, t + 1) * D.sN;
-          const double* xng = D.xnext[c] + D.run(b, t) * D.sX;
-          f[tid] = (want_dyn ? xn[tid] : xng[tid]) - px[0];
-        }
-      } else if (!s.was_feasible && tid < n) {  // closing the gaps
-        D.fs[kk * D.sN + tid] = 0.;
-      }
-    }
-    __syncthreads();
-    stamp.mark(7);
+    ts = te;
   }
   stamp.flush();
 }
@@ -505,7 +638,8 @@ __device__ __forceinline__ bool fwd_trial_fast(const Dev& D, int b, const ElemSt
       pd = wave_sum(pd);
       if (lane == 0) red[8 + wid] = pd;
     }
-    const double* P = stage_params<NT>(D.pblock(b, t), block_doubles_dev(kd.kind, nx, nu), pl, pcap, cached);
+    stage_params_batched<NT>(D.pblock(b, t), block_doubles_dev(kd.kind, nx, nu), pl, cached);
+    const double* P = pl;
     __syncthreads();
     if (running) {
       // us_try = us - k * alpha - K * dx

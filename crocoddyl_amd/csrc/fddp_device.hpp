@@ -61,6 +61,7 @@ struct Dev {
   ElemState* st;             // [B]
   double* bwork;             // generic sweep's global workspace when LDS is too small (else null)
   double* zero16;            // 16 zero bytes: source of the LDS-DMA gap fill
+  const int* segend;         // [T+1] end of the run of knots from t sharing desc + parameter block
   unsigned long long* stamps;  // diagnostic: [B][4 waves][8 phases] cycles (null = off)
 
   __device__ __host__ int64_t knot(int b, int t) const { return (int64_t)b * (T + 1) + t; }
@@ -77,6 +78,18 @@ struct Prm {
   int n_alphas;
   double alphas[16];
 };
+
+// Which batch elements a launch works on (host-side selectors).
+enum Sel { SEL_ACTIVE = 0, SEL_ALL = 1, SEL_ITER0 = 2, SEL_RECALC = 3 };
+
+__device__ inline bool selected(const ElemState& s, int sel) {
+  switch (sel) {
+    case SEL_ACTIVE: return s.active != 0;
+    case SEL_ALL: return true;
+    case SEL_ITER0: return s.iter == 0;
+    default: return s.active != 0 && s.recalc != 0;
+  }
+}
 
 // raiseIfNaN — src/core/solver-base.cpp:175-181
 __device__ inline bool raise_if_nan(double v) { return isnan(v) || isinf(v) || v >= 1e30; }

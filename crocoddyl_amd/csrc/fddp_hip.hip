@@ -175,7 +175,7 @@ Prm to_prm(const fddp_params& p) {
 int launch_fused(fddp_handle* h, int sel_calc, int sel_diff, int gaps) {
   Timed tm(h, sel_diff >= 0 ? 1 : 0);
   const Dev& D = h->D;
-  hipLaunchKernelGGL(calc_fused_kernel<kNTF>, dim3(D.B), dim3(kNTF), h->fused_smem, h->stream, D, sel_calc, sel_diff,
+  hipLaunchKernelGGL(calc_tiled_kernel<kNTF>, dim3(D.B), dim3(kNTF), h->fused_smem, h->stream, D, sel_calc, sel_diff,
                      gaps, h->pcap);
   LAUNCH_CHECK();
   return FDDP_OK;
@@ -449,7 +449,7 @@ int fddp_create(const fddp_dims* dims, const fddp_knot_desc* knots, const double
     bool dense = h->pcap > 0 && d.nx == d.ndx && d.nx <= kNT && d.nu_max <= kNT;
     for (int t = 0; t <= d.T; ++t)
       dense = dense && (knots[t].kind == FDDP_KNOT_LQR || knots[t].kind == FDDP_KNOT_EULER_DIFFLQR);
-    h->fused_smem = sizeof(double) * (h->pcap + 2 * D.sX + D.sM + 3 * kNTF + 16);
+    h->fused_smem = sizeof(double) * (h->pcap + calc_tiled_lds(D.sX, D.sM));
     h->fwd_fast_smem = sizeof(double) * (h->pcap + fwd_lds_doubles<kNT, true>(D.sX, D.sN, D.sM));
     const char* env = std::getenv("FDDP_FAST");
     const bool off = env && env[0] == '0';
@@ -481,6 +481,21 @@ int fddp_create(const fddp_dims* dims, const fddp_knot_desc* knots, const double
   };
   for (auto& a : plan)
     if ((rc = dalloc(h, a.p, a.n))) return bail(rc);
+  {  // knot segments: runs of knots with the same desc and parameter block
+     // (running runs stop before the terminal knot), for the tiled calc
+    std::vector<int> se(d.T + 1);
+    for (int t = d.T; t >= 0; --t) {
+      const bool same = t + 1 < d.T && knots[t + 1].kind == knots[t].kind && knots[t + 1].nu == knots[t].nu &&
+                        knots[t + 1].param_offset == knots[t].param_offset &&
+                        knots[t + 1].param_stride == knots[t].param_stride;
+      se[t] = same ? se[t + 1] : t + 1;
+    }
+    double* sp = nullptr;
+    if ((rc = dalloc(h, &sp, (d.T + 2) / 2 + 1))) return bail(rc);
+    if (hipMemcpyAsync(sp, se.data(), sizeof(int) * se.size(), hipMemcpyHostToDevice, h->stream) != hipSuccess)
+      return bail(fail(FDDP_ERR_RUNTIME, "upload segments"));
+    D.segend = (const int*)sp;
+  }
   double* stp = nullptr;
   if ((rc = dalloc(h, &stp, (int64_t)(sizeof(ElemState) / 8) * B))) return bail(rc);
   D.st = (ElemState*)stp;
@@ -509,7 +524,7 @@ int fddp_create(const fddp_dims* dims, const fddp_knot_desc* knots, const double
                           (int)h->fwd_smem) != hipSuccess ||
       hipFuncSetAttribute((const void*)forward_kernel<kNT, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)h->fwd_fast_smem) != hipSuccess ||
-      hipFuncSetAttribute((const void*)calc_fused_kernel<kNTF>, hipFuncAttributeMaxDynamicSharedMemorySize,
+      hipFuncSetAttribute((const void*)calc_tiled_kernel<kNTF>, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)h->fused_smem) != hipSuccess ||
       hipFuncSetAttribute((const void*)calc_kernel<kNT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)h->calc_smem) != hipSuccess ||
@@ -564,7 +579,7 @@ void fddp_destroy(fddp_handle* h) {
         std::fprintf(stderr, "\n");
       }
       if (h->fast) {
-        const char* fn[8] = {"stage", "bar1", "blocks1+partials", "bar2", "finalize", "blocks2", "bar3", "tail"};
+        const char* fn[8] = {"stage", "compute", "-", "-", "-", "blocks", "-", "-"};
         std::fprintf(stderr, "[fddp stamps] fused calc/calcDiff, mean cycles per element:\n");
         for (int w = 0; w < 8; ++w) {
           std::fprintf(stderr, "  wave %d:", w);

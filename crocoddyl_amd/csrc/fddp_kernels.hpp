@@ -8,17 +8,6 @@
 
 namespace fddp {
 
-enum Sel { SEL_ACTIVE = 0, SEL_ALL = 1, SEL_ITER0 = 2, SEL_RECALC = 3 };
-
-__device__ inline bool selected(const ElemState& s, int sel) {
-  switch (sel) {
-    case SEL_ACTIVE: return s.active != 0;
-    case SEL_ALL: return true;
-    case SEL_ITER0: return s.iter == 0;
-    default: return s.active != 0 && s.recalc != 0;
-  }
-}
-
 // Doubles in a knot's parameter block (layouts in include/fddp_hip.h).
 __device__ inline int64_t block_doubles_dev(int kind, int nx, int nu) {
   if (kind == FDDP_KNOT_LQR) return FDDP_PARAM_HEADER + 2LL * nx * nx + 2LL * nx * nu + (int64_t)nu * nu + 2LL * nx + nu;

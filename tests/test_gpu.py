@@ -151,6 +151,59 @@ def test_step_api_parity(name, kw):
         np.testing.assert_allclose(g.expected_improvement(), o.expected_improvement(), rtol=1e-8, atol=1e-9)
 
 
+DATA_Q = [(_abi.Q_FX, "nn"), (_abi.Q_FU, "nm"), (_abi.Q_LXX, "nn"), (_abi.Q_LXU, "nm"), (_abi.Q_LUU, "mm"),
+          (_abi.Q_LX, "n"), (_abi.Q_LU, "m")]
+
+
+def _assert_datas(g, o, d, tol):
+    """Knot datas (Fx, Fu, Lxx, Lxu, Luu, Lx, Lu of every knot) vs the oracle."""
+    n, m, T = d.ndx, d.nu_max, d.T
+    per = dict(nn=n * n, nm=n * m, mm=m * m, n=n, m=m)
+    for q, shape in DATA_Q:
+        a, b = g.quantity(q, T + 1, per[shape]), o.quantity(q, T + 1, per[shape])
+        if q == _abi.Q_LU:
+            a, b = a[:, :T], b[:, :T]
+        np.testing.assert_allclose(a, b, **tol, err_msg=f"quantity {q}")
+
+
+@pytest.mark.parametrize("name,kw", [("C2_lqr", dict(T=10, B=4)), ("C4_solo12", dict(T=12, B=4)),
+                                     ("C5_talos_full", dict(T=6, B=3))])
+def test_datas_after_solve(name, kw):
+    """The derivative blocks a solve leaves in the knot datas (on the fast
+    path the 8-wave sweep writes calcDiff's blocks itself, two knots ahead of
+    its own position) equal the oracle's after the same SolverFDDP::solve."""
+    S = helpers.setup(name, **kw)
+    d = S["dims"]
+    rng = np.random.default_rng(5)
+    xs = rng.uniform(-1, 1, (d.B, d.T + 1, d.nx))
+    us = rng.uniform(-1, 1, (d.B, d.T, d.nu_max))
+    g, o = _pair(S)
+    for h in (g, o):
+        h.set_candidate(xs, us, False)
+    _assert_results(g.solve(maxiter=2, reg_init=0.1), o.solve(maxiter=2, reg_init=0.1))
+    _assert_datas(g, o, d, dict(rtol=1e-9, atol=1e-9))
+
+
+def test_datas_after_regmax_abort():
+    """A sweep that fails on every retry still leaves calcDiff's blocks of
+    every knot (the reference computes them all before the backward pass)."""
+    from crocoddyl_amd.models import ActionModelLQR
+    from crocoddyl_amd.problem import pack_problem
+    model = ActionModelLQR(4, 2, True)
+    model.Luu = -2e10 * np.eye(2)
+    T = 7
+    knots, pool = pack_problem([model] * T, model, 1)
+    dims = _abi.Dims(4, 4, 2, T, 2)
+    S = dict(dims=dims, knots=knots, pool=pool, x0s=np.ones((2, 4)))
+    g, o = _pair(S)
+    for h in (g, o):
+        h.set_candidate(None, None, False)
+    rg, ro = g.solve(maxiter=10), o.solve(maxiter=10)
+    assert ro[0].status == _abi.STATUS_REGMAX
+    _assert_results(rg, ro)
+    _assert_datas(g, o, dims, dict(rtol=1e-12, atol=1e-12))
+
+
 def test_unregularised_fresh_solver_direction():
     """A fresh solver has xreg = ureg = NaN: no regularisation and
     Vx = Qx - K^T Qu (ddp.cpp:216-238)."""
