@@ -19,6 +19,9 @@ PARAM_HEADER = 4
 
 Q_FX, Q_FU, Q_LXX, Q_LXU, Q_LUU, Q_LX, Q_LU, Q_XNEXT, Q_FS, Q_K, Q_KV = range(11)
 Q_VXX, Q_VX, Q_QXX, Q_QXU, Q_QUU, Q_QX, Q_QU = range(11, 18)
+Q_QUU_INV = 18
+
+SOLVER_FDDP, SOLVER_BOXFDDP = 0, 1
 
 
 class Dims(C.Structure):
@@ -36,6 +39,11 @@ class Params(C.Structure):
                 ("n_alphas", C.c_int32), ("pad_", C.c_int32), ("alphas", C.c_double * 16)]
 
 
+class BoxQPParams(C.Structure):
+    _fields_ = [("maxiter", C.c_int32), ("n_alphas", C.c_int32), ("th_acceptstep", C.c_double),
+                ("th_grad", C.c_double), ("reg", C.c_double), ("alphas", C.c_double * 16)]
+
+
 class Result(C.Structure):
     _fields_ = [("status", C.c_int32), ("iter", C.c_int32), ("is_feasible", C.c_int32), ("n_iter_run", C.c_int32),
                 ("cost", C.c_double), ("stop", C.c_double), ("xreg", C.c_double), ("ureg", C.c_double),
@@ -46,6 +54,7 @@ class Result(C.Structure):
 P = C.c_void_p
 D = C.POINTER(C.c_double)
 I32 = C.POINTER(C.c_int32)
+U64 = C.POINTER(C.c_uint64)
 
 # name -> (restype, argtypes); `h` is an opaque handle pointer
 PROTOS = {
@@ -67,6 +76,8 @@ PROTOS = {
     "set_solver_state": (C.c_int, [P, C.c_int, C.c_double, C.c_double, C.c_int]),
     "get_quantity": (C.c_int, [P, C.c_int, D]),
     "mpc_shift": (C.c_int, [P]),
+    "set_solver_kind": (C.c_int, [P, C.c_int]),
+    "set_control_limits": (C.c_int, [P, D, D]),
 }
 
 # product-only entry points (libfddp_hip)
@@ -85,6 +96,9 @@ PROTOS_GPU = {
     "get_timing": (C.c_int, [P, D, C.POINTER(C.c_int64)]),
     "set_timing": (C.c_int, [P, C.c_int]),
     "device_bytes": (C.c_int64, [P]),
+    "get_solver_kind": (C.c_int, [P, I32]),
+    "boxqp_default_params": (None, [C.POINTER(BoxQPParams)]),
+    "boxqp_solve": (C.c_int, [C.c_int, C.c_int, C.c_int, D, D, D, D, D, C.POINTER(BoxQPParams), D, U64, U64, D, I32]),
 }
 
 

@@ -40,6 +40,7 @@
 // B[k=lane>>4][j=lane&15], C/D col=lane&15, row=(lane>>4)+4*reg.
 #pragma once
 
+#include "box_qp.hpp"
 #include "fddp_device.hpp"
 
 namespace fddp {
@@ -273,6 +274,27 @@ __device__ __forceinline__ bool sym_sweep_inverse(const double* Quu, double* Qi,
   return bad;
 }
 
+// The masked / relabelled inverse an InvMap describes (the box QP's free
+// Hessian, box_qp.hpp) with the register sweep: the masked matrix is staged
+// into Qi, swept in place (the sweep reads all of it before writing), and
+// the result is cut to the `out` set.
+template <int MP, int LDQ>
+__device__ __forceinline__ bool sym_sweep_inverse_masked(const double* H, double* Qi, double* rb, int m, int lane,
+                                                         const InvMap& mp) {
+  for (int e = lane; e < m * m; e += 64) {
+    const int i = e % m, j = e / m;
+    Qi[j * LDQ + i] = mp.load(H, LDQ, i, j);
+  }
+  const bool bad = sym_sweep_inverse<MP, LDQ>(Qi, Qi, rb, m, lane);
+  asm volatile("" ::: "memory");
+  for (int e = lane; e < m * m; e += 64) {
+    const int i = e % m, j = e / m;
+    if (!(mp.out(i) && mp.out(j))) Qi[j * LDQ + i] = 0.;
+  }
+  asm volatile("" ::: "memory");
+  return bad;
+}
+
 // Same sweep with each lane owning a BS x BS block of the matrix (BS = MP/8,
 // an 8 x 8 grid of blocks over the 64 lanes): per step one FMA per element
 // as before, but the column-k / row-k fix-ups touch BS elements of 8 lanes
@@ -500,11 +522,47 @@ struct BwdLds {
   int* flag;
 };
 
+// SolverBoxFDDP::computeGains on wave 0 (box-fddp.cpp:48-79): the box QP
+// (box_qp.hpp) on Quu, Qu with bounds u_lb - us, u_ub - us, warm-started at
+// the previous k; leaves Quu_inv in Qi, k = -x in kv (and in D.k), and Qu
+// zeroed on the clamped set. Returns false where the reference raises
+// backward_error (including its qp_ size check: the QP has
+// runningModels[0]->nu variables, box-fddp.cpp:16, box-qp.cpp:53-72).
+template <int MP, int LDQ>
+__device__ __forceinline__ bool box_gains_wave(const Dev& D, const BwdLds& L, int b, int t, int cur, int lane) {
+  const int nu = D.knots[t].nu;
+  if (nu != D.knots[0].nu) return false;
+  const int64_t rr = D.run(b, t);
+  const bool valid = lane < nu;
+  double q = 0., lb = 0., ub = 0., x = 0.;
+  if (valid) {
+    const double u = D.us[cur][rr * D.sM + lane];
+    q = L.qu[lane];
+    lb = D.ulb[rr * D.sM + lane] - u;
+    ub = D.uub[rr * D.sM + lane] - u;
+    x = D.k[rr * D.sM + lane];
+  }
+  uint64_t fsol, finv;
+  int iters;
+  auto inv = [&](const InvMap& mp) { return sym_sweep_inverse_masked<MP, LDQ>(L.Quu, L.Qi, L.rowbuf, nu, lane, mp); };
+  if (!box_qp_wave(L.Quu, LDQ, L.Qi, LDQ, L.rowbuf, nu, lane, q, lb, ub, x, D.boxcfg, inv, true, fsol, finv, iters))
+    return false;
+  asm volatile("" ::: "memory");
+  if (lane < MP) L.kv[lane] = valid ? -x : 0.;
+  if (valid) {
+    D.k[rr * D.sM + lane] = -x;
+    if (!((fsol >> lane) & 1)) L.qu[lane] = 0.;
+  }
+  if (D.dQuuInv)
+    for (int e = lane; e < nu * nu; e += 64) D.dQuuInv[rr * D.sMM + (e / nu) * D.m + e % nu] = L.Qi[(e / nu) * LDQ + e % nu];
+  return true;
+}
+
 // One knot of the sweep, as executed by wave W (all four waves call this
 // with their own W; the barriers inside line up one to one).
 template <int NTL, int MTL, int NW, int W>
 __device__ __forceinline__ bool bwd_knot(const Dev& D, const BwdLds& L, int b, int t, bool feas, double xreg,
-                                         double ureg, Stamp& stamp) {
+                                         double ureg, int cur, Stamp& stamp) {
   using Cfg = MfmaCfg<NTL, MTL>;
   constexpr int NP = Cfg::NP, MP = Cfg::MP, JT = Cfg::JT, LDV = Cfg::LDV, LDQ = Cfg::LDQ, ZLD = Cfg::ZLD;
   constexpr BwdPlan<NTL, MTL, NW> P{};
@@ -520,6 +578,7 @@ __device__ __forceinline__ bool bwd_knot(const Dev& D, const BwdLds& L, int b, i
   const int q = lane >> 4, c = lane & 15;
   const bool xr = !isnan(xreg), ur = !isnan(ureg);
   const int64_t kk = D.knot(b, t), rr = D.run(b, t);
+  const bool boxk = feas && D.box_knot(b, t);  // SolverBoxFDDP gains on this knot
   if constexpr (W != 0 && P.owns_u(W)) __builtin_amdgcn_s_setprio(2);  // Quu first: the inversion waits on it
   // the next knot's operands (LDS-DMA; lands during P2 / P3)
   auto issue_dma = [&]() {
@@ -755,7 +814,11 @@ __device__ __forceinline__ bool bwd_knot(const Dev& D, const BwdLds& L, int b, i
         __builtin_amdgcn_s_sleep(1);
       asm volatile("" ::: "memory");
     }
-    if (sym_sweep_inverse<MP, LDQ>(Quu, Qi, L.rowbuf, m, lane) && lane == 0) *L.flag = 1;
+    if (boxk) {
+      if (!box_gains_wave<MP, LDQ>(D, L, b, t, cur, lane) && lane == 0) *L.flag = 1;
+    } else if (sym_sweep_inverse<MP, LDQ>(Quu, Qi, L.rowbuf, m, lane) && lane == 0) {
+      *L.flag = 1;
+    }
   }
   stamp.mark(2);
   dma_barrier();  // B1 (also retires the fs DMA issued at the end of the last knot)
@@ -833,23 +896,26 @@ __device__ __forceinline__ bool bwd_knot(const Dev& D, const BwdLds& L, int b, i
       }
       __builtin_amdgcn_sched_barrier(0);
     }
-    if constexpr (W == 0) {  // k = Quu^-1 Qu ; Quuk = Quu k (64 / MP lanes per row)
+    if constexpr (W == 0) {  // k = Quu^-1 Qu (box knots: k = -x, set) ; Quuk = Quu k (64 / MP lanes per row)
       constexpr int LPR = 64 / MP;
       const int row = lane % MP, part = lane / MP;
       double a0 = 0., a1 = 0.;
-      for (int k2 = part; k2 < m; k2 += 2 * LPR) {
-        a0 = fma(Qi[k2 * LDQ + row], L.qu[k2], a0);
-        if (k2 + LPR < m) a1 = fma(Qi[(k2 + LPR) * LDQ + row], L.qu[k2 + LPR], a1);
-      }
-      double a = a0 + a1;
+      if (!boxk) {
+        for (int k2 = part; k2 < m; k2 += 2 * LPR) {
+          a0 = fma(Qi[k2 * LDQ + row], L.qu[k2], a0);
+          if (k2 + LPR < m) a1 = fma(Qi[(k2 + LPR) * LDQ + row], L.qu[k2 + LPR], a1);
+        }
+        double a = a0 + a1;
 #pragma unroll
-      for (int o2 = MP; o2 < 64; o2 <<= 1) a += __shfl_xor(a, o2, 64);
-      if (part == 0) {
-        if (row >= m) a = 0.;
-        L.kv[row] = a;
-        if (row < m) D.k[rr * D.sM + row] = a;
+        for (int o2 = MP; o2 < 64; o2 <<= 1) a += __shfl_xor(a, o2, 64);
+        if (part == 0) {
+          if (row >= m) a = 0.;
+          L.kv[row] = a;
+          if (row < m) D.k[rr * D.sM + row] = a;
+        }
       }
       asm volatile("" ::: "memory");
+      double a;
       a0 = 0.;
       a1 = 0.;
       for (int k2 = part; k2 < m; k2 += 2 * LPR) {
@@ -955,7 +1021,7 @@ __device__ __forceinline__ bool bwd_knot(const Dev& D, const BwdLds& L, int b, i
 }
 
 template <int NTL, int MTL, int NW>
-__device__ __forceinline__ bool bwd_sweep_mfma(const Dev& D, int b, bool feas, double xreg, double ureg,
+__device__ __forceinline__ bool bwd_sweep_mfma(const Dev& D, int b, bool feas, double xreg, double ureg, int cur,
                                                double* sm) {
   using Cfg = MfmaCfg<NTL, MTL>;
   constexpr int NP = Cfg::NP, MP = Cfg::MP, LDV = Cfg::LDV, LDQ = Cfg::LDQ;
@@ -1053,16 +1119,16 @@ __device__ __forceinline__ bool bwd_sweep_mfma(const Dev& D, int b, bool feas, d
     const int64_t kk = D.knot(b, t);
     const int64_t rr = D.run(b, t);
     stamp.mark(7);
-    bool ok;
+    bool ok = false;
     switch (wid) {
-      case 0: ok = bwd_knot<NTL, MTL, NW, 0>(D, L, b, t, feas, xreg, ureg, stamp); break;
-      case 1: ok = bwd_knot<NTL, MTL, NW, 1>(D, L, b, t, feas, xreg, ureg, stamp); break;
-      case 2: ok = bwd_knot<NTL, MTL, NW, 2>(D, L, b, t, feas, xreg, ureg, stamp); break;
-      case 3: ok = bwd_knot<NTL, MTL, NW, 3>(D, L, b, t, feas, xreg, ureg, stamp); break;
-      case 4: if constexpr (NW > 4) ok = bwd_knot<NTL, MTL, NW, 4>(D, L, b, t, feas, xreg, ureg, stamp); break;
-      case 5: if constexpr (NW > 4) ok = bwd_knot<NTL, MTL, NW, 5>(D, L, b, t, feas, xreg, ureg, stamp); break;
-      case 6: if constexpr (NW > 4) ok = bwd_knot<NTL, MTL, NW, 6>(D, L, b, t, feas, xreg, ureg, stamp); break;
-      default: if constexpr (NW > 4) ok = bwd_knot<NTL, MTL, NW, 7>(D, L, b, t, feas, xreg, ureg, stamp); break;
+      case 0: ok = bwd_knot<NTL, MTL, NW, 0>(D, L, b, t, feas, xreg, ureg, cur, stamp); break;
+      case 1: ok = bwd_knot<NTL, MTL, NW, 1>(D, L, b, t, feas, xreg, ureg, cur, stamp); break;
+      case 2: ok = bwd_knot<NTL, MTL, NW, 2>(D, L, b, t, feas, xreg, ureg, cur, stamp); break;
+      case 3: ok = bwd_knot<NTL, MTL, NW, 3>(D, L, b, t, feas, xreg, ureg, cur, stamp); break;
+      case 4: if constexpr (NW > 4) ok = bwd_knot<NTL, MTL, NW, 4>(D, L, b, t, feas, xreg, ureg, cur, stamp); break;
+      case 5: if constexpr (NW > 4) ok = bwd_knot<NTL, MTL, NW, 5>(D, L, b, t, feas, xreg, ureg, cur, stamp); break;
+      case 6: if constexpr (NW > 4) ok = bwd_knot<NTL, MTL, NW, 6>(D, L, b, t, feas, xreg, ureg, cur, stamp); break;
+      default: if constexpr (NW > 4) ok = bwd_knot<NTL, MTL, NW, 7>(D, L, b, t, feas, xreg, ureg, cur, stamp); break;
     }
     if (!ok) {  // the factorisation failed (every wave saw the flag)
       stamp.flush();
@@ -1108,7 +1174,7 @@ __global__ __launch_bounds__(NW * 64) void backward_mfma_kernel(Dev D, Prm prm, 
   double xreg = st->xreg, ureg = st->ureg;
   bool ok;
   for (;;) {
-    ok = bwd_sweep_mfma<NTL, MTL, NW>(D, b, feas, xreg, ureg, sm);
+    ok = bwd_sweep_mfma<NTL, MTL, NW>(D, b, feas, xreg, ureg, st->cur, sm);
     __syncthreads();
     if (ok || mode == 1) break;
     xreg *= prm.regfactor;  // increaseRegularization (ddp.cpp:312-318)

@@ -578,9 +578,11 @@ __device__ __forceinline__ bool fwd_trial_fast(const Dev& D, int b, const ElemSt
   // measured slower: register pressure)
   constexpr int PD = 1;
   double pK[PD][KMAX];
-  double pxs[PD], pfs[PD], pvf[PD], pus[PD], pkv[PD];
+  double pxs[PD], pfs[PD], pvf[PD], pus[PD], pkv[PD], plb[PD], pub[PD];
   auto fetch = [&](int t, int q) {
     pxs[q] = pfs[q] = pvf[q] = pus[q] = pkv[q] = 0.;
+    plb[q] = -INFINITY;  // no limits: the clamp below is an exact no-op
+    pub[q] = INFINITY;
     if (t > T) return;
     const int64_t kk = D.knot(b, t);
     if (tid < nx) {
@@ -593,6 +595,10 @@ __device__ __forceinline__ bool fwd_trial_fast(const Dev& D, int b, const ElemSt
       if (tid < m) {
         pus[q] = D.us[c][rr * D.sM + tid];
         pkv[q] = D.k[rr * D.sM + tid];
+        if (D.box_knot(b, t)) {
+          plb[q] = D.ulb[rr * D.sM + tid];
+          pub[q] = D.uub[rr * D.sM + tid];
+        }
       }
       if (kreg) {
         const double* Kt = D.K + rr * D.sNM;
@@ -609,7 +615,7 @@ __device__ __forceinline__ bool fwd_trial_fast(const Dev& D, int b, const ElemSt
     const bool running = t < T;
     const fddp_knot_desc kd = D.knots[t];
     const int nu = kd.nu;
-    const double cxs = pxs[0], cfs = pfs[0], cvf = pvf[0], cus = pus[0], ckv = pkv[0];
+    const double cxs = pxs[0], cfs = pfs[0], cvf = pvf[0], cus = pus[0], ckv = pkv[0], clb = plb[0], cub = pub[0];
     double cK[KMAX];
 #pragma unroll
     for (int j = 0; j < KMAX; ++j) cK[j] = pK[0][j];
@@ -620,6 +626,8 @@ __device__ __forceinline__ bool fwd_trial_fast(const Dev& D, int b, const ElemSt
       pvf[q] = pvf[q + 1];
       pus[q] = pus[q + 1];
       pkv[q] = pkv[q + 1];
+      plb[q] = plb[q + 1];
+      pub[q] = pub[q + 1];
 #pragma unroll
       for (int j = 0; j < KMAX; ++j) pK[q][j] = pK[q + 1][j];
     }
@@ -662,6 +670,8 @@ __device__ __forceinline__ bool fwd_trial_fast(const Dev& D, int b, const ElemSt
       if (tid < m) {
         double v = 0.;
         if (tid < nu) v = (cus - ckv * alpha) - seg_sum(pa, m, tid, NT);
+        // SolverBoxFDDP::forwardPass clamp (box-fddp.cpp:100-102); +-inf when unlimited
+        if (D.box && tid < nu) v = std_min(std_max(v, clb), cub);
         xu[nx + tid] = v;
         D.us[o][D.run(b, t) * D.sM + tid] = v;
       }

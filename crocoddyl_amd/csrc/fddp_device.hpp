@@ -37,6 +37,13 @@ static_assert(sizeof(ElemState) % 8 == 0, "ElemState alignment");
 
 __host__ __device__ inline int64_t pad2(int64_t v) { return (v + 1) & ~int64_t(1); }
 
+// fddp_boxqp_params on the device (BoxQP, box-qp.hpp:92-93)
+struct BoxQPCfg {
+  int maxiter, n_alphas;
+  double th_acceptstep, th_grad, reg;
+  double alphas[16];
+};
+
 // All device buffers of one handle. Every per-knot array is [b][t][...] with
 // the per-knot stride padded to an even number of doubles (16-B aligned rows).
 struct Dev {
@@ -63,6 +70,14 @@ struct Dev {
   double* zero16;            // 16 zero bytes: source of the LDS-DMA gap fill
   const int* segend;         // [T+1] end of the run of knots from t sharing desc + parameter block
   unsigned long long* stamps;  // diagnostic: [B][4 waves][8 phases] cycles (null = off)
+  // SolverBoxFDDP (box-fddp.cpp:15-160): box QP gains on limited knots once
+  // feasible, clamped controls in the forward pass
+  int box;                         // solver kind == FDDP_SOLVER_BOXFDDP
+  const double *ulb, *uub;         // [B][T][sM] control limits (null = none set)
+  const unsigned char* haslim;     // [B][T] has_control_limits (null = none)
+  double* dQuuInv;                 // debug [B][T][sMM] Quu_inv_ (null unless debug + box)
+  BoxQPCfg boxcfg;                 // qp_(nu, 100, 0.1, 1e-5, 0.) (box-fddp.cpp:16)
+  __device__ bool box_knot(int b, int t) const { return box && haslim && haslim[(int64_t)b * T + t]; }
 
   __device__ __host__ int64_t knot(int b, int t) const { return (int64_t)b * (T + 1) + t; }
   __device__ __host__ int64_t run(int b, int t) const { return (int64_t)b * T + t; }

@@ -86,6 +86,11 @@ struct fddp_handle_s {
   int* h_count = nullptr;   // pinned
   bool debug = false;
   double* dbg[7] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  double* dqi = nullptr;  // SolverBoxFDDP::Quu_inv_ debug store (allocated with debug on)
+  int solver_kind = FDDP_SOLVER_FDDP;
+  double* d_ulb = nullptr;  // control limits, allocated on first fddp_set_control_limits
+  double* d_uub = nullptr;
+  unsigned char* d_haslim = nullptr;
   int64_t bytes = 0;
   size_t bwd_smem = 0, fwd_smem = 0, calc_smem = 0, cdiff_smem = 0;
   bool fast = false;  // dense-knot fast path (fast_path.hpp) for calc / calcDiff / forward
@@ -169,6 +174,17 @@ Prm to_prm(const fddp_params& p) {
   q.n_alphas = p.n_alphas;
   for (int i = 0; i < 16; ++i) q.alphas[i] = p.alphas[i];
   return q;
+}
+
+BoxQPCfg to_boxcfg(const fddp_boxqp_params& p) {
+  BoxQPCfg c;
+  c.maxiter = p.maxiter;
+  c.n_alphas = p.n_alphas;
+  c.th_acceptstep = p.th_acceptstep;
+  c.th_grad = p.th_grad;
+  c.reg = p.reg;
+  for (int i = 0; i < 16; ++i) c.alphas[i] = p.alphas[i];
+  return c;
 }
 
 // ---- kernel launchers ------------------------------------------------------
@@ -428,6 +444,13 @@ int fddp_create(const fddp_dims* dims, const fddp_knot_desc* knots, const double
   D.sNM = pad2((int64_t)d.ndx * (d.nu_max > 0 ? d.nu_max : 1));
   D.sMM = pad2((int64_t)d.nu_max * d.nu_max > 0 ? (int64_t)d.nu_max * d.nu_max : 1);
   const int64_t B = d.B, K1 = (int64_t)d.T + 1, K0 = d.T;
+  {  // SolverBoxFDDP's qp_(nu, 100, 0.1, 1e-5, 0.) (box-fddp.cpp:16); unused until BOXFDDP
+    fddp_boxqp_params bp;
+    fddp_boxqp_default_params(&bp);
+    bp.th_grad = 1e-5;
+    bp.reg = 0.;
+    D.boxcfg = to_boxcfg(bp);
+  }
 
   h->bwd_smem = BwdSmem::bytes(D.n, D.m, false);
   if (h->bwd_smem > 160 * 1024) {
@@ -871,6 +894,11 @@ int fddp_set_debug(fddp_handle* h, int on) {
   D.dQuu = a ? p[4] : nullptr;
   D.dQx = a ? p[5] : nullptr;
   D.dQu = a ? p[6] : nullptr;
+  if (on && !h->dqi) {
+    int rc;
+    if ((rc = dalloc(h, &h->dqi, (int64_t)D.B * D.T * D.sMM))) return rc;
+  }
+  D.dQuuInv = a ? h->dqi : nullptr;
   h->debug = a;
   HIP_TRY(hipStreamSynchronize(h->stream));
   return FDDP_OK;
@@ -903,6 +931,7 @@ int fddp_get_quantity(fddp_handle* h, int which, double* out) {
     case FDDP_Q_QUU: src = D.dQuu; per = m * m; stride = D.sMM; nk = D.T; break;
     case FDDP_Q_QX: src = D.dQx; per = n; stride = D.sN; nk = D.T; break;
     case FDDP_Q_QU: src = D.dQu; per = m; stride = D.sM; nk = D.T; break;
+    case FDDP_Q_QUU_INV: src = D.dQuuInv; per = m * m; stride = D.sMM; nk = D.T; break;
     default: return fail(FDDP_ERR_INVALID_ARG, "fddp_get_quantity: unknown quantity");
   }
   if (per == 0) return FDDP_OK;
@@ -923,6 +952,135 @@ int fddp_get_quantity(fddp_handle* h, int which, double* out) {
   }
   HIP_TRY(hipStreamSynchronize(h->stream));
   return FDDP_OK;
+}
+
+int fddp_set_solver_kind(fddp_handle* h, int kind) {
+  if (!h) return fail(FDDP_ERR_INVALID_ARG, "fddp_set_solver_kind: null handle");
+  if (kind != FDDP_SOLVER_FDDP && kind != FDDP_SOLVER_BOXFDDP)
+    return fail(FDDP_ERR_INVALID_ARG, "fddp_set_solver_kind: unknown solver kind");
+  if (kind == FDDP_SOLVER_BOXFDDP && h->dims.nu_max > 64)
+    return fail(FDDP_ERR_UNSUPPORTED, "fddp_set_solver_kind: the box QP holds at most 64 controls (one wave)");
+  h->solver_kind = kind;
+  h->D.box = kind == FDDP_SOLVER_BOXFDDP ? 1 : 0;
+  return FDDP_OK;
+}
+
+int fddp_get_solver_kind(fddp_handle* h, int* kind) {
+  if (!h || !kind) return fail(FDDP_ERR_INVALID_ARG, "fddp_get_solver_kind: null");
+  *kind = h->solver_kind;
+  return FDDP_OK;
+}
+
+int fddp_set_control_limits(fddp_handle* h, const double* u_lb, const double* u_ub) {
+  if (!h) return fail(FDDP_ERR_INVALID_ARG, "fddp_set_control_limits: null handle");
+  if ((u_lb == nullptr) != (u_ub == nullptr))
+    return fail(FDDP_ERR_INVALID_ARG, "fddp_set_control_limits: give both u_lb and u_ub, or neither");
+  DeviceGuard g(h->device);
+  Dev& D = h->D;
+  if (!u_lb) {
+    D.ulb = D.uub = nullptr;
+    D.haslim = nullptr;
+    return FDDP_OK;
+  }
+  const int64_t B = D.B, T = D.T, m = D.m;
+  int rc;
+  if (!h->d_ulb) {
+    if ((rc = dalloc(h, &h->d_ulb, B * T * D.sM))) return rc;
+    if ((rc = dalloc(h, &h->d_uub, B * T * D.sM))) return rc;
+    double* hl = nullptr;
+    if ((rc = dalloc(h, &hl, (B * T + 7) / 8))) return rc;
+    h->d_haslim = (unsigned char*)hl;
+  }
+  // update_has_control_limits (action-base.hxx:142-144) per knot and element
+  std::vector<unsigned char> lim((size_t)(B * T));
+  std::vector<double> lb((size_t)(B * T * D.sM), -INFINITY), ub((size_t)(B * T * D.sM), INFINITY);
+  for (int64_t b = 0; b < B; ++b)
+    for (int64_t t = 0; t < T; ++t) {
+      const int nu = h->knots[t].nu;
+      bool al = false, au = false;
+      for (int64_t i = 0; i < m; ++i) {
+        const double l = u_lb[(b * T + t) * m + i], u = u_ub[(b * T + t) * m + i];
+        lb[(b * T + t) * D.sM + i] = l;
+        ub[(b * T + t) * D.sM + i] = u;
+        if (i < nu) {
+          al = al || std::isfinite(l);
+          au = au || std::isfinite(u);
+        }
+      }
+      lim[b * T + t] = (al && au) ? 1 : 0;
+    }
+  HIP_TRY(hipMemcpyAsync(h->d_ulb, lb.data(), sizeof(double) * lb.size(), hipMemcpyHostToDevice, h->stream));
+  HIP_TRY(hipMemcpyAsync(h->d_uub, ub.data(), sizeof(double) * ub.size(), hipMemcpyHostToDevice, h->stream));
+  HIP_TRY(hipMemcpyAsync(h->d_haslim, lim.data(), lim.size(), hipMemcpyHostToDevice, h->stream));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  D.ulb = h->d_ulb;
+  D.uub = h->d_uub;
+  D.haslim = h->d_haslim;
+  return FDDP_OK;
+}
+
+void fddp_boxqp_default_params(fddp_boxqp_params* p) {
+  if (!p) return;
+  std::memset(p, 0, sizeof(*p));
+  p->maxiter = 100;
+  p->n_alphas = 10;
+  p->th_acceptstep = 0.1;
+  p->th_grad = 1e-9;
+  p->reg = 1e-9;
+  for (int i = 0; i < 10; ++i) p->alphas[i] = 1. / std::pow(2., (double)i);
+}
+
+int fddp_boxqp_solve(int device, int B, int nx, const double* H, const double* q, const double* lb,
+                     const double* ub, const double* xinit, const fddp_boxqp_params* p, double* x,
+                     uint64_t* free_mask, uint64_t* inv_mask, double* Hff_inv, int32_t* status) {
+  g_err.clear();
+  if (B < 0 || nx < 1 || !H || !q || !lb || !ub || !xinit || !p)
+    return fail(FDDP_ERR_INVALID_ARG, "fddp_boxqp_solve: invalid argument");
+  if (nx > 64) return fail(FDDP_ERR_UNSUPPORTED, "fddp_boxqp_solve: nx > 64 (one wave per QP)");
+  // BoxQP setters' validation (box-qp.cpp:203-249)
+  if (p->th_grad < 0.) return fail(FDDP_ERR_INVALID_ARG, "th_grad value has to be positive.");
+  if (p->reg < 0.) return fail(FDDP_ERR_INVALID_ARG, "reg value has to be positive.");
+  if (p->n_alphas < 1 || p->n_alphas > 16) return fail(FDDP_ERR_INVALID_ARG, "n_alphas must be in [1, 16]");
+  for (int i = 1; i < p->n_alphas; ++i) {
+    if (0. >= p->alphas[i]) return fail(FDDP_ERR_INVALID_ARG, "alpha values has to be positive.");
+    if (p->alphas[i] >= p->alphas[i - 1]) return fail(FDDP_ERR_INVALID_ARG, "alpha values are monotonously decreasing.");
+  }
+  if (B == 0) return FDDP_OK;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(FDDP_ERR_NO_DEVICE, "fddp_boxqp_solve: no HIP device");
+  if (device < 0 || device >= ndev) return fail(FDDP_ERR_INVALID_ARG, "fddp_boxqp_solve: bad device index");
+  DeviceGuard g(device);
+  const size_t nn = (size_t)B * nx * nx, nv = (size_t)B * nx;
+  // one allocation: H | q lb ub xinit | x | Hinv | masks (2B) | status (B)
+  const size_t nd = 2 * nn + 5 * nv + 2 * (size_t)B + ((size_t)B + 1) / 2;
+  double* buf = nullptr;
+  HIP_TRY(hipMalloc(&buf, sizeof(double) * nd));
+  double *dH = buf, *dq = dH + nn, *dl = dq + nv, *du = dl + nv, *dx0 = du + nv, *dx = dx0 + nv, *dHi = dx + nv;
+  uint64_t* dm = (uint64_t*)(dHi + nn);
+  int32_t* ds = (int32_t*)(dm + 2 * (size_t)B);
+  int rc = FDDP_OK;
+  auto run = [&]() -> int {
+    HIP_TRY(hipMemcpy(dH, H, sizeof(double) * nn, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(dq, q, sizeof(double) * nv, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(dl, lb, sizeof(double) * nv, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(du, ub, sizeof(double) * nv, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(dx0, xinit, sizeof(double) * nv, hipMemcpyHostToDevice));
+    const size_t smem = sizeof(double) * (2 * (size_t)nx * nx + 64);
+    HIP_TRY(hipFuncSetAttribute((const void*)boxqp_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
+    hipLaunchKernelGGL(boxqp_kernel, dim3(B), dim3(64), smem, 0, nx, dH, dq, dl, du, dx0, to_boxcfg(*p), dx, dm,
+                       dm + B, dHi, ds);
+    LAUNCH_CHECK();
+    HIP_TRY(hipDeviceSynchronize());
+    if (x) HIP_TRY(hipMemcpy(x, dx, sizeof(double) * nv, hipMemcpyDeviceToHost));
+    if (free_mask) HIP_TRY(hipMemcpy(free_mask, dm, sizeof(uint64_t) * B, hipMemcpyDeviceToHost));
+    if (inv_mask) HIP_TRY(hipMemcpy(inv_mask, dm + B, sizeof(uint64_t) * B, hipMemcpyDeviceToHost));
+    if (Hff_inv) HIP_TRY(hipMemcpy(Hff_inv, dHi, sizeof(double) * nn, hipMemcpyDeviceToHost));
+    if (status) HIP_TRY(hipMemcpy(status, ds, sizeof(int32_t) * B, hipMemcpyDeviceToHost));
+    return FDDP_OK;
+  };
+  rc = run();
+  (void)hipFree(buf);
+  return rc;
 }
 
 int fddp_mpc_shift(fddp_handle* h) {

@@ -4,6 +4,7 @@
 #pragma once
 
 #include "fddp_device.hpp"
+#include "box_qp.hpp"
 #include "knots.hpp"
 
 namespace fddp {
@@ -240,8 +241,40 @@ struct BwdSmem {
   __host__ __device__ static int64_t work_doubles(int n, int m) { return (int64_t)n * n + pad2(m * n); }
 };
 
+// SolverBoxFDDP::computeGains (box-fddp.cpp:48-79) on wave 0 of the generic
+// sweep: the box QP (box_qp.hpp) with the LDS sweep inverse; Quu_inv into
+// Qi (ld m), k = -x into kv and D.k, Qu zeroed on the clamped set. False
+// where the reference raises backward_error.
+__device__ inline bool box_gains_generic(const Dev& D, BwdSmem& S, double* Qi, int b, int t, int cur, int lane) {
+  const int nu = D.knots[t].nu, m = D.m;
+  if (nu != D.knots[0].nu) return false;  // qp_ has runningModels[0]->nu variables (box-fddp.cpp:16)
+  const int64_t rr = D.run(b, t);
+  const bool valid = lane < nu;
+  double q = 0., lb = 0., ub = 0., x = 0.;
+  if (valid) {
+    const double u = D.us[cur][rr * D.sM + lane];
+    q = S.qu[lane];
+    lb = D.ulb[rr * D.sM + lane] - u;
+    ub = D.uub[rr * D.sM + lane] - u;
+    x = D.k[rr * D.sM + lane];
+  }
+  uint64_t fsol, finv;
+  int iters;
+  auto inv = [&](const InvMap& mp) { return wave_sweep_inverse_lds(S.Quu, m, Qi, m, S.red, nu, mp, lane); };
+  if (!box_qp_wave(S.Quu, m, Qi, m, S.red, nu, lane, q, lb, ub, x, D.boxcfg, inv, true, fsol, finv, iters))
+    return false;
+  if (valid) {
+    S.kv[lane] = -x;
+    if (!((fsol >> lane) & 1)) S.qu[lane] = 0.;
+  }
+  if (D.dQuuInv)
+    for (int e = lane; e < nu * nu; e += 64) D.dQuuInv[rr * D.sMM + (e / nu) * m + e % nu] = Qi[(e / nu) * m + e % nu];
+  return true;
+}
+
 template <int NT>
-__device__ __forceinline__ bool bwd_sweep(const Dev& D, int b, bool feas, double xreg, double ureg, BwdSmem& S) {
+__device__ __forceinline__ bool bwd_sweep(const Dev& D, int b, bool feas, double xreg, double ureg, int cur,
+                                          BwdSmem& S) {
   const int n = D.n, m = D.m, T = D.T, tid = threadIdx.x;
   const bool xr = !isnan(xreg), ur = !isnan(ureg);
   // terminal: Vxx = Lxx_T (+ xreg I), Vx = Lx_T (+ Vxx fs_T)
@@ -325,7 +358,19 @@ __device__ __forceinline__ bool bwd_sweep(const Dev& D, int b, bool feas, double
       for (int i = tid; i < m; i += NT) D.dQu[r * D.sM + i] = i < nu ? S.qu[i] : 0.;
     }
     __syncthreads();
-    if (nu) {
+    if (nu && feas && D.box_knot(b, t)) {
+      // box QP gains; K = Quu_inv Qxu^T (S.A, nu x n, ld m)
+      if (tid < 64 && !box_gains_generic(D, S, S.L, b, t, cur, tid) && tid == 0) *S.flag = 1;
+      __syncthreads();
+      if (*S.flag) return false;
+      for (int e = tid; e < nu * n; e += NT) {
+        const int i = e % nu, j = e / nu;
+        double a = 0.;
+        for (int l = 0; l < nu; ++l) a += S.L[l * m + i] * S.Qxu[l * n + j];
+        S.A[j * m + i] = a;
+      }
+      __syncthreads();
+    } else if (nu) {
       // Cholesky (lower) of Quu — Eigen LLT fails on a pivot <= 0
       for (int j = 0; j < nu; ++j) {
         if (tid == 0) {
@@ -359,6 +404,8 @@ __device__ __forceinline__ bool bwd_sweep(const Dev& D, int b, bool feas, double
         }
       }
       __syncthreads();
+    }
+    if (nu) {
       // store K, k ; Quuk = Quu k
       {
         const int64_t r = D.run(b, t);
@@ -455,7 +502,7 @@ __global__ __launch_bounds__(NT) void backward_kernel(Dev D, Prm prm, int mode) 
   for (;;) {
     if (threadIdx.x == 0) *S.flag = 0;
     __syncthreads();
-    ok = bwd_sweep<NT>(D, b, feas, xreg, ureg, S);
+    ok = bwd_sweep<NT>(D, b, feas, xreg, ureg, st->cur, S);
     __syncthreads();
     if (ok || mode == 1) break;
     // increaseRegularization (ddp.cpp:312-318); abort at regmax (fddp.cpp:41-43)
@@ -551,6 +598,8 @@ __device__ __forceinline__ bool fwd_trial(const Dev& D, int b, const ElemState& 
           double kd2 = 0.;
           for (int j = 0; j < n; ++j) kd2 += K[(int64_t)j * m + i] * (xv[j] - xs[j]);
           v = (us[i] - kv[i] * alpha) - kd2;
+          // SolverBoxFDDP::forwardPass: cwiseMax(u_lb).cwiseMin(u_ub) (box-fddp.cpp:100-102)
+          if (D.box_knot(b, t)) v = std_min(std_max(v, D.ulb[D.run(b, t) * D.sM + i]), D.uub[D.run(b, t) * D.sM + i]);
         }
         uv[i] = v;
         ut[i] = v;
@@ -773,6 +822,41 @@ __global__ void scatter_traj_kernel(Dev D, int which, const double* in, int use_
   const double* src = in + (int64_t)b * rows * w;
   for (int64_t e = blockIdx.x * blockDim.x + threadIdx.x; e < rows * w; e += (int64_t)gridDim.x * blockDim.x)
     dst[(e / w) * sw + e % w] = use_zero ? 0. : src[e];
+}
+
+
+// ---------------------------------------------------------------------------
+// Standalone batched box QP (fddp_boxqp_solve): BoxQP::solve (box-qp.cpp:
+// 51-182), one wave per problem, H and the free-Hessian inverse in LDS.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void boxqp_kernel(int nx, const double* H, const double* q, const double* lb,
+                                                   const double* ub, const double* xinit, BoxQPCfg c, double* x,
+                                                   uint64_t* free_mask, uint64_t* inv_mask, double* Hinv,
+                                                   int32_t* status) {
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  const int b = blockIdx.x, lane = threadIdx.x;
+  const int64_t nn = (int64_t)nx * nx;
+  double* Hs = sm;
+  double* Qi = sm + nn;
+  double* vb = Qi + nn;
+  for (int64_t e = lane; e < nn; e += 64) Hs[e] = H[b * nn + e];
+  __syncthreads();
+  const bool valid = lane < nx;
+  const int64_t o = (int64_t)b * nx + lane;
+  double xv = valid ? xinit[o] : 0.;
+  uint64_t fs = 0, fi = 0;
+  int iters = 0;
+  auto inv = [&](const InvMap& mp) { return wave_sweep_inverse_lds(Hs, nx, Qi, nx, vb, nx, mp, lane); };
+  const bool ok = box_qp_wave(Hs, nx, Qi, nx, vb, nx, lane, valid ? q[o] : 0., valid ? lb[o] : 0.,
+                              valid ? ub[o] : 0., xv, c, inv, false, fs, fi, iters);
+  __syncthreads();
+  if (valid) x[o] = xv;
+  for (int64_t e = lane; e < nn; e += 64) Hinv[b * nn + e] = ok ? Qi[e] : 0.;
+  if (lane == 0) {
+    free_mask[b] = fs;
+    inv_mask[b] = fi;
+    status[b] = ok ? 0 : 1;
+  }
 }
 
 }  // namespace fddp

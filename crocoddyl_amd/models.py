@@ -79,7 +79,40 @@ def _stack(parts, header):
     return np.ascontiguousarray(np.concatenate(cols, axis=1))
 
 
-class ActionModelAbstract:
+class _ControlLimits:
+    """u_lb / u_ub / has_control_limits of ActionModelAbstract and
+    DifferentialActionModelAbstract (core/action-base.hxx:20-22,107-144,
+    core/diff-action-base.hxx:21-23,99-136): -inf / +inf by default, setters
+    check the size, and has_control_limits = any(isfinite(u_lb)) and
+    any(isfinite(u_ub)). A leading batch axis (B, nu) gives every batch
+    element its own limits."""
+
+    def _init_limits(self):
+        self._u_lb = np.full(self.nu, -np.inf)
+        self._u_ub = np.full(self.nu, np.inf)
+        self._lim_version = 0
+
+    def _set_limit(self, name, v):
+        v = np.array(v, dtype=np.float64)
+        if v.shape[-1:] != (self.nu,) or v.ndim not in (1, 2):
+            raise ValueError(f"Invalid argument: {'lower' if name == 'u_lb' else 'upper'} bound has wrong "
+                             f"dimension (it should be {self.nu})")
+        setattr(self, "_" + name, v)
+        self._lim_version += 1
+
+    u_lb = property(lambda s: s._u_lb, lambda s, v: s._set_limit("u_lb", v))
+    u_ub = property(lambda s: s._u_ub, lambda s, v: s._set_limit("u_ub", v))
+
+    @property
+    def has_control_limits(self):
+        """update_has_control_limits (action-base.hxx:142-144); per element when batched."""
+        lb = np.isfinite(np.atleast_2d(self._u_lb)).any(axis=-1)
+        ub = np.isfinite(np.atleast_2d(self._u_ub)).any(axis=-1)
+        r = lb & ub
+        return r if (np.ndim(self._u_lb) == 2 or np.ndim(self._u_ub) == 2) else bool(r[0])
+
+
+class ActionModelAbstract(_ControlLimits):
     """Base of the device-backed knot models (core/action-base.hpp:23-99)."""
 
     kind = None
@@ -89,6 +122,7 @@ class ActionModelAbstract:
         self.nu = int(nu)
         self.nr = int(nr)
         self._version = 0
+        self._init_limits()
 
     def _touch(self):
         self._version += 1
@@ -196,7 +230,7 @@ class ActionModelUnicycle(ActionModelAbstract):
         return self.kind, 2, np.array([[self._dt, self._w[0], self._w[1], 0.0]])
 
 
-class DifferentialActionModelLQR:
+class DifferentialActionModelLQR(_ControlLimits):
     """DifferentialActionModelLQR (core/actions/diff-lqr.hxx:14-28 defaults).
     Only usable inside IntegratedActionModelEuler on the device."""
 
@@ -205,6 +239,7 @@ class DifferentialActionModelLQR:
         self.state = StateVector(2 * nq)
         self.nu = nu
         self.nr = 0
+        self._init_limits()
         self.driftFree = bool(driftFree)
         nx = 2 * nq
         self._Fq = np.eye(nq)
@@ -254,6 +289,9 @@ class IntegratedActionModelEuler(ActionModelAbstract):
             raise NotImplementedError("crocoddyl_amd: the device path covers Euler(DifferentialActionModelLQR) "
                                       f"knots only; got {type(diffModel).__name__}")
         super().__init__(diffModel.state, diffModel.nu, diffModel.nr)
+        # the integrated model copies the differential model's limits (euler.hxx:25-26)
+        self.u_lb = diffModel.u_lb
+        self.u_ub = diffModel.u_ub
         self.differential = diffModel
         diffModel._owners.append(self)
         self.withCostResidual = bool(withCostResidual)

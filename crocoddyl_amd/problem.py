@@ -83,6 +83,15 @@ class _Handle:
         kd = (_abi.KnotDesc * len(knots))(*[_abi.KnotDesc(*k) for k in knots])
         check(lib().fddp_create(C.byref(dims), kd, _abi.dptr(pool), pool.size, device, C.byref(self.ptr)))
         self.set_x0(problem._x0b)
+        self._lsig = None
+        self._push_limits()
+
+    def _push_limits(self):
+        lsig = self.problem._limits_signature()
+        if lsig != self._lsig:
+            lb, ub = self.problem._limits()
+            check(lib().fddp_set_control_limits(self.ptr, _abi.dptr(lb), _abi.dptr(ub)))
+            self._lsig = lsig
 
     def refresh(self):
         sig = self.problem._signature()
@@ -92,6 +101,7 @@ class _Handle:
                 raise FDDPError("model parameter layout changed; rebuild the ShootingProblem")
             check(lib().fddp_set_model_params(self.ptr, _abi.dptr(pool), pool.size))
             self._sig = sig
+        self._push_limits()
         return self.ptr
 
     def set_x0(self, x0b):
@@ -174,6 +184,22 @@ class ShootingProblem:
 
     def _signature(self):
         return tuple((id(m), m._version) for m in self._models + [self._terminal])
+
+    def _limits_signature(self):
+        return tuple((id(m), m._lim_version) for m in self._models)
+
+    def _limits(self):
+        """Control limits of the running models as (B, T, nu_max) arrays
+        (fddp_set_control_limits), or (None, None) when no model has any."""
+        B, T, m = self.B, self.T, self.nu_max
+        if not any(np.isfinite(md._u_lb).any() or np.isfinite(md._u_ub).any() for md in self._models):
+            return None, None
+        lb = np.full((B, T, max(m, 1)), -np.inf)
+        ub = np.full((B, T, max(m, 1)), np.inf)
+        for t, md in enumerate(self._models):
+            lb[:, t, :md.nu] = np.broadcast_to(md._u_lb, (B, md.nu))
+            ub[:, t, :md.nu] = np.broadcast_to(md._u_ub, (B, md.nu))
+        return np.ascontiguousarray(lb[..., :m]), np.ascontiguousarray(ub[..., :m])
 
     def _handles(self):
         hs = []
@@ -574,3 +600,24 @@ class SolverFDDP:
 
     def synchronize(self):
         check(lib().fddp_synchronize(self._ptr))
+
+
+class SolverBoxFDDP(SolverFDDP):
+    """SolverBoxFDDP (src/core/solvers/box-fddp.cpp:15-164) on the device:
+    control-limited FDDP. Once an element is feasible, knots whose model has
+    control limits get their gains from a box QP on (Quu, Qu) with bounds
+    u_lb - us, u_ub - us; the forward pass clamps the controls. th_stop
+    defaults to 5e-5 (box-fddp.cpp:28)."""
+
+    def __init__(self, problem):
+        super().__init__(problem)
+        check(lib().fddp_set_solver_kind(self._h.ptr, _abi.SOLVER_BOXFDDP))
+        self._prm.th_stop = 5e-5
+        self._push_params()
+
+    @property
+    def Quu_inv(self):
+        """SolverBoxFDDP::get_Quu_inv (box-fddp.cpp:162); needs _debug(True)
+        before the backward pass (device-side store)."""
+        p = self.problem
+        return self._quantity(_abi.Q_QUU_INV, p.T, p.nu_max, p.nu_max, "both")

@@ -208,9 +208,60 @@ int fddp_get_us_try(fddp_handle* h, double* out);
 #define FDDP_Q_QUU 15 /* T x nu_max*nu_max */
 #define FDDP_Q_QX 16  /* T x ndx */
 #define FDDP_Q_QU 17  /* T x nu_max */
+#define FDDP_Q_QUU_INV 18 /* T x nu_max*nu_max: SolverBoxFDDP::get_Quu_inv (box-fddp.cpp:162);
+                             like the reference, a knot keeps its last value
+                             (zero initially) while the box QP does not run on it */
 int fddp_get_quantity(fddp_handle* h, int which, double* out);
 /* Store Vxx/Vx/Q* per knot during backward passes (costs HBM traffic). */
 int fddp_set_debug(fddp_handle* h, int on);
+
+/* ---- control limits and the box-constrained solver ------------------------ */
+/* Solver variants of a handle. FDDP: SolverFDDP (fddp.cpp:14-225); control
+ * limits are ignored, as SolverFDDP ignores them. BOXFDDP: SolverBoxFDDP
+ * (box-fddp.cpp:15-160): on knots whose model has control limits, and once the
+ * element is feasible, computeGains solves a box QP (BoxQP, box-qp.cpp:51-182)
+ * warm-started at the previous k; the forward pass clamps us_try to the
+ * limits. The reference's SolverBoxFDDP ctor also sets th_stop = 5e-5; this
+ * ABI leaves th_stop to fddp_set_params (the facades apply the default). */
+#define FDDP_SOLVER_FDDP 0
+#define FDDP_SOLVER_BOXFDDP 1
+/* Replaces constructing SolverBoxFDDP(problem) instead of SolverFDDP(problem)
+ * (box-fddp.cpp:15-29). FDDP_ERR_UNSUPPORTED if BOXFDDP is asked with
+ * nu_max > 64 (one wave holds one box QP). */
+int fddp_set_solver_kind(fddp_handle* h, int kind);
+int fddp_get_solver_kind(fddp_handle* h, int* kind);
+/* Control limits of every running knot and element: u_lb, u_ub are
+ * B*T*nu_max doubles ([b][t][i], entries i >= nu(t) ignored); -inf / +inf =
+ * no limit. Replaces ActionModelAbstract::set_u_lb / set_u_ub
+ * (action-base.hxx:122-144): a knot "has control limits" iff any of its
+ * u_lb is finite and any of its u_ub is finite (update_has_control_limits,
+ * action-base.hxx:142-144). NULL, NULL removes all limits. */
+int fddp_set_control_limits(fddp_handle* h, const double* u_lb, const double* u_ub);
+
+/* Projected-Newton box QP  x = argmin 0.5 x'Hx + q'x  s.t. lb <= x <= ub
+ * (BoxQP, box-qp.hpp:29-206, box-qp.cpp:14-182). */
+typedef struct {
+  int32_t maxiter;       /* 100 */
+  int32_t n_alphas;      /* 10 */
+  double th_acceptstep;  /* 0.1 */
+  double th_grad;        /* 1e-9 (SolverBoxFDDP's own QP uses 1e-5) */
+  double reg;            /* 1e-9 (SolverBoxFDDP's own QP uses 0) */
+  double alphas[16];     /* 2^-k, k = 0..9 */
+} fddp_boxqp_params;
+/* BoxQP(nx) constructor defaults (box-qp.hpp:92-93, box-qp.cpp:14-46). */
+void fddp_boxqp_default_params(fddp_boxqp_params* p);
+/* B independent box QPs of dimension nx (1 <= nx <= 64) solved on `device`,
+ * one wave each. Host arrays: H B*nx*nx (column-major), q, lb, ub, xinit B*nx.
+ * Outputs (host; any may be NULL): x B*nx (BoxQPSolution::x); free_mask B
+ * (bit i set = i in BoxQPSolution::free_idx, the rest is clamped_idx);
+ * inv_mask B (the free set Hff_inv was factorised on) and Hff_inv B*nx*nx,
+ * the inverse embedded at inv_mask's indices (zero elsewhere): the
+ * reference's compact nf x nf Hff_inv is its inv_mask rows/cols in order;
+ * status B: 0 ok, 1 the LLT of a free Hessian failed (the reference throws
+ * "backward_error"). Replaces BoxQP::solve (box-qp.cpp:51-182). */
+int fddp_boxqp_solve(int device, int B, int nx, const double* H, const double* q, const double* lb,
+                     const double* ub, const double* xinit, const fddp_boxqp_params* p, double* x,
+                     uint64_t* free_mask, uint64_t* inv_mask, double* Hff_inv, int32_t* status);
 
 /* ---- MPC plumbing -------------------------------------------------------- */
 /* Receding-horizon shift on device: x0 <- xs[1]; xs[t] <- xs[t+1] (last kept);

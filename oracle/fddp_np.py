@@ -17,6 +17,8 @@ SURVEY.md §8a "Restatement traps"):
   * ActionModelUnicycle                core/actions/unicycle.hxx:22-73
   * IntegratedActionModelEuler∘DifferentialActionModelLQR
                                        core/integrator/euler.hxx:41-131, core/actions/diff-lqr.hxx:34-79
+  * BoxQP::solve                       src/core/solvers/box-qp.cpp:51-182
+  * SolverBoxFDDP computeGains / forwardPass  src/core/solvers/box-fddp.cpp:48-160
 It also restates SolverKKT (src/core/solvers/kkt.cpp:34-227), the dense
 Newton/KKT solver the reference uses as the oracle of its DDP/FDDP tests
 (unittest/test_solvers.cpp:65-110).
@@ -174,12 +176,79 @@ def block_size(kind, nx, nu):
     return HDR + 2 * nq * nq + nq * nu + nq + nx * nx + nx * nu + nu * nu + nx + nu
 
 
+def box_qp(H, q, lb, ub, xinit, maxiter=100, th_acceptstep=0.1, th_grad=1e-9, reg=1e-9, alphas=None):
+    """BoxQP::solve (box-qp.cpp:51-182), numpy linear algebra.
+
+    Returns dict(x, free_idx, clamped_idx, Hff_inv (compact), inv_idx (the
+    free set Hff_inv was factorised on), iters) or None where the reference
+    throws "backward_error" (LLT failure)."""
+    alphas = alphas if alphas is not None else [2.0 ** (-k) for k in range(10)]
+    H = np.asarray(H, float)
+    q = np.asarray(q, float)
+    n = q.size
+    x = np.maximum(np.minimum(np.asarray(xinit, float), ub), lb)
+    Hff_inv, inv_idx = np.zeros((0, 0)), []
+    free, clamped = [], []
+    iters = 0
+
+    def chol_inv(idx):
+        Hff = H[np.ix_(idx, idx)] + (reg * np.eye(len(idx)) if reg != 0.0 else 0.0)
+        try:
+            L = np.linalg.cholesky(Hff)
+        except np.linalg.LinAlgError:
+            return None, None
+        if len(idx) and not np.all(np.diag(L) > 0):
+            return None, None
+        I = np.eye(len(idx))
+        return L, np.linalg.solve(L.T, np.linalg.solve(L, I))
+
+    for k in range(maxiter):
+        g = q + H @ x
+        clamped = [j for j in range(n) if (x[j] == lb[j] and g[j] > 0.0) or (x[j] == ub[j] and g[j] < 0.0)]
+        free = [j for j in range(n) if j not in clamped]
+        if np.max(np.abs(g)) <= th_grad or len(free) == 0:
+            if k == 0:
+                L, Hi = chol_inv(free)
+                if Hi is None:
+                    return None
+                Hff_inv, inv_idx = Hi, list(free)
+            return dict(x=x, free_idx=free, clamped_idx=clamped, Hff_inv=Hff_inv, inv_idx=inv_idx, iters=iters)
+        iters += 1
+        L, Hi = chol_inv(free)
+        if Hi is None:
+            return None
+        Hff_inv, inv_idx = Hi, list(free)
+        rhs = -q[free]
+        if clamped:
+            rhs = rhs - H[np.ix_(free, clamped)] @ x[clamped]
+        dxf = np.linalg.solve(L.T, np.linalg.solve(L, rhs)) - x[free]
+        dx = np.zeros(n)
+        dx[free] = dxf
+        fold = 0.5 * x @ (H @ x) + q @ x
+        for a in alphas:
+            xnew = np.maximum(np.minimum(x + a * dx, ub), lb)
+            fnew = 0.5 * xnew @ (H @ xnew) + q @ xnew
+            if fold - fnew > th_acceptstep * (g @ (x - xnew)):
+                x = xnew
+                break
+    return dict(x=x, free_idx=free, clamped_idx=clamped, Hff_inv=Hff_inv, inv_idx=inv_idx, iters=iters)
+
+
 class FDDP:
     """SolverFDDP over one problem (x0, models[0..T-1], models[T])."""
 
-    def __init__(self, x0, models, params=None):
+    def __init__(self, x0, models, params=None, box=False, u_lb=None, u_ub=None):
+        """box=True: SolverBoxFDDP (box-fddp.cpp) with per-knot limits u_lb/u_ub
+        (lists of T arrays of the knot's nu; None = no limits)."""
         self.x0 = np.array(x0, dtype=np.float64)
         self.models = models
+        self.box = box
+        T0 = len(models) - 1
+        self.u_lb = u_lb if u_lb is not None else [np.full(m.nu, -np.inf) for m in models[:-1]]
+        self.u_ub = u_ub if u_ub is not None else [np.full(m.nu, np.inf) for m in models[:-1]]
+        self.haslim = [bool(np.isfinite(self.u_lb[t]).any() and np.isfinite(self.u_ub[t]).any()) for t in range(T0)]
+        self.kprev = [np.zeros(m.nu) for m in models[:-1]]  # k_ persists across sweeps (warm start)
+        self.Quu_inv = [np.zeros((m.nu, m.nu)) for m in models[:-1]]
         self.T = len(models) - 1
         self.nx = models[0].nx
         self.nu_max = max(m.nu for m in models[:-1])
@@ -271,14 +340,35 @@ class FDDP:
                 Qu = d["Lu"] + d["Fu"].T @ Vx_p
                 if not math.isnan(self.ureg):
                     Quu = Quu + self.ureg * np.eye(nu)
-                try:
-                    L = np.linalg.cholesky(Quu)
-                except np.linalg.LinAlgError:
-                    return False
-                if not np.all(np.diag(L) > 0):
-                    return False
-                K = np.linalg.solve(L.T, np.linalg.solve(L, Qxu.T))
-                k = np.linalg.solve(L.T, np.linalg.solve(L, Qu))
+                if self.box and self.haslim[t] and self.is_feasible:
+                    # SolverBoxFDDP::computeGains (box-fddp.cpp:48-79)
+                    if nu != self.models[0].nu:
+                        return False  # qp_ has runningModels[0]->nu variables
+                    u = self.us[t][:nu]
+                    sol = box_qp(Quu, Qu, self.u_lb[t] - u, self.u_ub[t] - u, self.kprev[t], 100, 0.1, 1e-5, 0.0)
+                    if sol is None:
+                        return False
+                    Qi = np.zeros((nu, nu))
+                    Hi, f = sol["Hff_inv"], sol["free_idx"]
+                    ni = Hi.shape[0]
+                    for i, fi in enumerate(f):
+                        for j, fj in enumerate(f):
+                            Qi[fi, fj] = Hi[i, j] if (i < ni and j < ni) else 0.0
+                    self.Quu_inv[t] = Qi
+                    K = Qi @ Qxu.T
+                    k = -sol["x"]
+                    Qu = Qu.copy()
+                    Qu[sol["clamped_idx"]] = 0.0
+                else:
+                    try:
+                        L = np.linalg.cholesky(Quu)
+                    except np.linalg.LinAlgError:
+                        return False
+                    if not np.all(np.diag(L) > 0):
+                        return False
+                    K = np.linalg.solve(L.T, np.linalg.solve(L, Qxu.T))
+                    k = np.linalg.solve(L.T, np.linalg.solve(L, Qu))
+                self.kprev[t] = k
                 self.Qxu[t], self.Quu[t], self.Qu[t], self.K[t], self.k[t] = Qxu, Quu, Qu, K, k
                 if math.isnan(self.ureg):
                     Vx = Vx - K.T @ Qu
@@ -326,6 +416,8 @@ class FDDP:
             dx = xt - self.xs[t]
             if m.nu != 0:
                 u = (self.us[t][:m.nu] - self.k[t] * alpha) - self.K[t] @ dx
+                if self.box and self.haslim[t]:  # box-fddp.cpp:100-102
+                    u = np.minimum(np.maximum(u, self.u_lb[t]), self.u_ub[t])
                 self.us_try[t][:m.nu] = u
                 xnext, c = m.calc(xt, u)
             else:

@@ -385,6 +385,167 @@ struct TraceRec {
   double cost, stop, d0, d1, xreg, ureg, steplength, is_feasible;
 };
 
+
+// ---------------------------------------------------------------------------
+// Eigen LLT (lower) of a dense SPD matrix; false = NumericalIssue (a pivot
+// <= 0 or NaN), as Eigen::LLT::info() reports it.
+// ---------------------------------------------------------------------------
+static bool llt(const Mat& A, Mat& L) {
+  const int n = A.r;
+  L.resize(n, n);
+  for (int j = 0; j < n; ++j) {
+    double s = A(j, j);
+    for (int kk = 0; kk < j; ++kk) s -= L(j, kk) * L(j, kk);
+    if (!(s > 0.)) return false;
+    const double ljj = std::sqrt(s);
+    L(j, j) = ljj;
+    for (int i = j + 1; i < n; ++i) {
+      double v = A(i, j);
+      for (int kk = 0; kk < j; ++kk) v -= L(i, kk) * L(j, kk);
+      L(i, j) = v / ljj;
+    }
+  }
+  return true;
+}
+// L L^T y = b in place (LLT::solveInPlace)
+static void llt_solve(const Mat& L, double* b) {
+  const int n = L.r;
+  for (int i = 0; i < n; ++i) {
+    double v = b[i];
+    for (int kk = 0; kk < i; ++kk) v -= L(i, kk) * b[kk];
+    b[i] = v / L(i, i);
+  }
+  for (int i = n - 1; i >= 0; --i) {
+    double v = b[i];
+    for (int kk = i + 1; kk < n; ++kk) v -= L(kk, i) * b[kk];
+    b[i] = v / L(i, i);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// BoxQP — projected Newton for  min 0.5 x'Hx + q'x  s.t. lb <= x <= ub
+// (src/core/solvers/box-qp.cpp:14-182, include/.../box-qp.hpp:29-206).
+// ---------------------------------------------------------------------------
+struct BoxQPSolution {  // box-qp.hpp:29-53
+  Mat Hff_inv;
+  Vec x;
+  std::vector<int> free_idx, clamped_idx;
+};
+
+struct BoxQP {
+  int nx = 0, maxiter = 100;
+  double th_acceptstep = 0.1, th_grad = 1e-9, reg = 1e-9;
+  std::vector<double> alphas;
+  BoxQPSolution sol;
+  std::vector<int> inv_idx;  // the free set sol.Hff_inv was factorised on (harness)
+  int iters = 0;  // Newton iterations run by the last solve (diagnostic)
+
+  // box-qp.cpp:14-46 (alphas 2^-k, k = 0..9)
+  void init(int n, int mi, double ta, double tg, double rg) {
+    nx = n;
+    maxiter = mi;
+    th_acceptstep = ta;
+    th_grad = tg;
+    reg = rg;
+    alphas.resize(10);
+    for (int k = 0; k < 10; ++k) alphas[k] = 1. / std::pow(2., (double)k);
+  }
+
+  // box-qp.cpp:51-182. Returns false where the reference throws
+  // "backward_error" (the LLT of the free Hessian failed).
+  bool solve(const Mat& H, const double* q, const double* lb, const double* ub, const double* xinit) {
+    const int n = nx;
+    Vec x(n), g(n), Hx(n), dx(n), xnew(n), Hxn(n);
+    inv_idx.clear();
+    for (int i = 0; i < n; ++i) x[i] = std::max(std::min(xinit[i], ub[i]), lb[i]);  // :89-91
+    iters = 0;
+    for (int k = 0; k < maxiter; ++k) {
+      sol.clamped_idx.clear();
+      sol.free_idx.clear();
+      gemv(H.a.data(), n, n, x.data(), Hx.data());  // g = q + H x (:97-99)
+      for (int i = 0; i < n; ++i) g[i] = q[i] + Hx[i];
+      for (int j = 0; j < n; ++j) {  // :100-110
+        if ((x[j] == lb[j] && g[j] > 0.) || (x[j] == ub[j] && g[j] < 0.))
+          sol.clamped_idx.push_back(j);
+        else
+          sol.free_idx.push_back(j);
+      }
+      const int nf = (int)sol.free_idx.size(), nc = (int)sol.clamped_idx.size();
+      if (normInf(g) <= th_grad || nf == 0) {  // :113-135
+        if (k == 0) {
+          Mat Hff, L;
+          Hff.resize(nf, nf);
+          for (int i = 0; i < nf; ++i)
+            for (int j = 0; j < nf; ++j) Hff(i, j) = H(sol.free_idx[i], sol.free_idx[j]);
+          if (reg != 0.)
+            for (int i = 0; i < nf; ++i) Hff(i, i) += reg;
+          if (!llt(Hff, L)) return false;
+          sol.Hff_inv.resize(nf, nf);
+          for (int j = 0; j < nf; ++j) {
+            sol.Hff_inv(j, j) = 1.;
+            llt_solve(L, &sol.Hff_inv.a[(size_t)j * nf]);
+          }
+          inv_idx = sol.free_idx;
+        }
+        sol.x = x;
+        return true;
+      }
+      ++iters;
+      // Newton step on the free subspace (:138-175)
+      Mat Hff, Hfc, L;
+      Hff.resize(nf, nf);
+      Hfc.resize(nf, nc);
+      Vec qf(nf), xf(nf), xc(nc), dxf(nf);
+      for (int i = 0; i < nf; ++i) {
+        const int fi = sol.free_idx[i];
+        qf[i] = q[fi];
+        xf[i] = x[fi];
+        for (int j = 0; j < nf; ++j) Hff(i, j) = H(fi, sol.free_idx[j]);
+        for (int j = 0; j < nc; ++j) {
+          const int cj = sol.clamped_idx[j];
+          xc[j] = x[cj];
+          Hfc(i, j) = H(fi, cj);
+        }
+      }
+      if (reg != 0.)
+        for (int i = 0; i < nf; ++i) Hff(i, i) += reg;
+      if (!llt(Hff, L)) return false;
+      sol.Hff_inv.resize(nf, nf);
+      for (int j = 0; j < nf; ++j) {
+        sol.Hff_inv(j, j) = 1.;
+        llt_solve(L, &sol.Hff_inv.a[(size_t)j * nf]);
+      }
+      inv_idx = sol.free_idx;
+      for (int i = 0; i < nf; ++i) dxf[i] = -qf[i];
+      if (nc != 0)
+        for (int i = 0; i < nf; ++i) {
+          double s = 0.;
+          for (int j = 0; j < nc; ++j) s += Hfc(i, j) * xc[j];
+          dxf[i] -= s;
+        }
+      llt_solve(L, dxf.data());
+      for (int i = 0; i < nf; ++i) dxf[i] -= xf[i];
+      std::fill(dx.begin(), dx.end(), 0.);
+      for (int i = 0; i < nf; ++i) dx[sol.free_idx[i]] = dxf[i];
+      // line search (:178-189)
+      const double fold = 0.5 * dot(x.data(), Hx.data(), n) + dot(q, x.data(), n);
+      for (double a : alphas) {
+        for (int i = 0; i < n; ++i) xnew[i] = std::max(std::min(x[i] + a * dx[i], ub[i]), lb[i]);
+        gemv(H.a.data(), n, n, xnew.data(), Hxn.data());
+        const double fnew = 0.5 * dot(xnew.data(), Hxn.data(), n) + dot(q, xnew.data(), n);
+        double gd = 0.;
+        for (int i = 0; i < n; ++i) gd += g[i] * (x[i] - xnew[i]);
+        if (fold - fnew > th_acceptstep * gd) {
+          x = xnew;
+          break;
+        }
+      }
+    }
+    sol.x = x;
+    return true;
+  }
+};
+
 // ---------------------------------------------------------------------------
 // SolverDDP / SolverFDDP (src/core/solvers/ddp.cpp, fddp.cpp) for one element.
 // ---------------------------------------------------------------------------
@@ -406,6 +567,12 @@ struct Solver {
   bool was_feasible = false;
   // SolverFDDP
   double dg = 0., dq = 0., dv = 0.;
+  // SolverBoxFDDP (box-fddp.cpp:15-47): limits per knot, qp_, Quu_inv_
+  bool box = false;
+  std::vector<Vec> ulb, uub;      // [T][nu_max] (-inf / +inf = none)
+  std::vector<char> haslim;       // has_control_limits per running knot
+  std::vector<Mat> Quu_inv;
+  BoxQP qp;
   // bookkeeping for the harness
   int status = FDDP_STATUS_RUNNING;
   int n_iter_run = 0;
@@ -458,6 +625,13 @@ struct Solver {
     FxTVxx.resize(ndx, ndx);
     fTVxx.assign(ndx, 0.);
     xnext.assign(nx, 0.);
+    // SolverBoxFDDP: qp_(runningModels[0]->nu, 100, 0.1, 1e-5, 0.) (box-fddp.cpp:16)
+    qp.init(P->models[0].nu, 100, 0.1, 1e-5, 0.);
+    Quu_inv.resize(T);
+    for (int t = 0; t < T; ++t) Quu_inv[t].resize(nu, nu);
+    ulb.assign(T, Vec(nu, -INFINITY));
+    uub.assign(T, Vec(nu, INFINITY));
+    haslim.assign(T, 0);
   }
 
   // solver-base.cpp:42-67 (xs_warm / us_warm may be null => zeros)
@@ -490,8 +664,46 @@ struct Solver {
     return cost;
   }
 
+  // SolverBoxFDDP::computeGains (box-fddp.cpp:48-79)
+  bool computeGainsBox(int t) {
+    const int nu = P->models[t].nu;
+    if (nu <= 0) return true;
+    if (!haslim[t] || !is_feasible) return computeGainsDDP(t);  // vanilla DDP gains
+    // qp_ has runningModels[0]->nu variables; BoxQP::solve throws on any other
+    // size (box-qp.cpp:53-72) and solve() catches every exception as a
+    // backward_error (fddp.cpp:37-38)
+    if (nu != qp.nx) return false;
+    const int n = P->ndx;
+    Vec dlb(nu), dub(nu);
+    for (int i = 0; i < nu; ++i) {
+      dlb[i] = ulb[t][i] - us[t][i];
+      dub[i] = uub[t][i] - us[t][i];
+    }
+    if (!qp.solve(Quu[t], Qu[t].data(), dlb.data(), dub.data(), k[t].data())) return false;
+    const BoxQPSolution& sol = qp.sol;
+    // Quu_inv(free_i, free_j) = Hff_inv(i, j). Hff_inv is the one of the last
+    // Newton iteration; when the QP converges at k > 0 the free set may have
+    // changed since, and the reference then indexes Hff_inv by position
+    // (beyond its size is out of bounds in Eigen: taken as 0 here).
+    Mat& Qi = Quu_inv[t];
+    std::fill(Qi.a.begin(), Qi.a.end(), 0.);
+    const int nf = (int)sol.free_idx.size(), ni = sol.Hff_inv.r;
+    for (int i = 0; i < nf; ++i)
+      for (int j = 0; j < nf; ++j) Qi(sol.free_idx[i], sol.free_idx[j]) = (i < ni && j < ni) ? sol.Hff_inv(i, j) : 0.;
+    for (int j = 0; j < n; ++j)  // K = Quu_inv Qxu^T
+      for (int i = 0; i < nu; ++i) {
+        double s = 0.;
+        for (int l = 0; l < nu; ++l) s += Qi(i, l) * Qxu[t](j, l);
+        K[t](i, j) = s;
+      }
+    for (int i = 0; i < nu; ++i) k[t][i] = -sol.x[i];
+    for (int c : sol.clamped_idx) Qu[t][c] = 0.;
+    return true;
+  }
+  bool computeGains(int t) { return box ? computeGainsBox(t) : computeGainsDDP(t); }
+
   // ddp.cpp:298-310 — Eigen LLT (lower) + solveInPlace
-  bool computeGains(int t) {
+  bool computeGainsDDP(int t) {
     const int nu = P->models[t].nu;
     if (nu <= 0) return true;
     const int n = P->ndx;
@@ -657,6 +869,9 @@ struct Solver {
           double kd = 0.;
           for (int j = 0; j < n; ++j) kd += K[t](i, j) * dx[t][j];
           us_try[t][i] = v - kd;
+          // SolverBoxFDDP::forwardPass clamps (box-fddp.cpp:100-102):
+          // cwiseMax(u_lb).cwiseMin(u_ub)
+          if (box && haslim[t]) us_try[t][i] = std::min(std::max(us_try[t][i], ulb[t][i]), uub[t][i]);
         }
         oracle::calc(m, d, xs_try[t].data(), us_try[t].data());
       } else {
@@ -1140,6 +1355,81 @@ int oracle_mpc_shift(oracle_handle* h) {
     h->problems[b].x0 = s.xs[1];
     for (int t = 0; t < D.T; ++t) s.xs[t] = s.xs[t + 1];
     for (int t = 0; t + 1 < D.T; ++t) s.us[t] = s.us[t + 1];
+  }
+  return FDDP_OK;
+}
+
+
+// SolverBoxFDDP / SolverFDDP selection (fddp_set_solver_kind).
+int oracle_set_solver_kind(oracle_handle* h, int kind) {
+  for (auto& s : h->solvers) s.box = kind == FDDP_SOLVER_BOXFDDP;
+  return FDDP_OK;
+}
+// Control limits (fddp_set_control_limits): B*T*nu_max each, or both NULL.
+int oracle_set_control_limits(oracle_handle* h, const double* lb, const double* ub) {
+  const fddp_dims& D = h->dims;
+  for (int b = 0; b < D.B; ++b) {
+    Solver& s = h->solvers[b];
+    for (int t = 0; t < D.T; ++t) {
+      const int nu = h->problems[b].models[t].nu;
+      bool anylb = false, anyub = false;
+      for (int i = 0; i < D.nu_max; ++i) {
+        const size_t e = ((size_t)b * D.T + t) * D.nu_max + i;
+        s.ulb[t][i] = lb ? lb[e] : -INFINITY;
+        s.uub[t][i] = ub ? ub[e] : INFINITY;
+        if (i < nu) {  // update_has_control_limits (action-base.hxx:142-144)
+          anylb = anylb || std::isfinite(s.ulb[t][i]);
+          anyub = anyub || std::isfinite(s.uub[t][i]);
+        }
+      }
+      s.haslim[t] = (anylb && anyub) ? 1 : 0;
+    }
+  }
+  return FDDP_OK;
+}
+// SolverBoxFDDP::get_Quu_inv, same layout as FDDP_Q_QUU_INV.
+int oracle_get_quu_inv(oracle_handle* h, double* out) {
+  const fddp_dims& D = h->dims;
+  const int m = D.nu_max;
+  for (int b = 0; b < D.B; ++b)
+    for (int t = 0; t < D.T; ++t)
+      std::memcpy(out + ((size_t)b * D.T + t) * m * m, h->solvers[b].Quu_inv[t].a.data(), sizeof(double) * m * m);
+  return FDDP_OK;
+}
+// Batched BoxQP, same contract as fddp_boxqp_solve.
+int oracle_boxqp_solve(int B, int nx, const double* H, const double* q, const double* lb, const double* ub,
+                       const double* xinit, const fddp_boxqp_params* p, double* x, uint64_t* free_mask,
+                       uint64_t* inv_mask, double* Hff_inv, int32_t* status, int32_t* iters) {
+  if (B < 0 || nx < 1 || nx > 64 || !H || !q || !lb || !ub || !xinit || !p) {
+    g_err = "oracle_boxqp_solve: invalid argument";
+    return FDDP_ERR_INVALID_ARG;
+  }
+  for (int b = 0; b < B; ++b) {
+    BoxQP qp;
+    qp.init(nx, p->maxiter, p->th_acceptstep, p->th_grad, p->reg);
+    qp.alphas.assign(p->alphas, p->alphas + p->n_alphas);
+    Mat Hm;
+    Hm.resize(nx, nx);
+    std::memcpy(Hm.a.data(), H + (size_t)b * nx * nx, sizeof(double) * nx * nx);
+    const size_t o = (size_t)b * nx;
+    const bool ok = qp.solve(Hm, q + o, lb + o, ub + o, xinit + o);
+    if (status) status[b] = ok ? 0 : 1;
+    if (iters) iters[b] = qp.iters;
+    if (x) std::memcpy(x + o, qp.sol.x.data(), sizeof(double) * std::min<size_t>(nx, qp.sol.x.size()));
+    uint64_t fm = 0;
+    for (int i : qp.sol.free_idx) fm |= 1ull << i;
+    if (free_mask) free_mask[b] = fm;
+    // Hff_inv embedded at the indices of the free set it was factorised on
+    const int ni = qp.sol.Hff_inv.r;
+    uint64_t im = 0;
+    for (int i : qp.inv_idx) im |= 1ull << i;
+    if (inv_mask) inv_mask[b] = im;
+    if (Hff_inv) {
+      double* Ho = Hff_inv + (size_t)b * nx * nx;
+      std::memset(Ho, 0, sizeof(double) * nx * nx);
+      for (int j = 0; j < ni; ++j)
+        for (int i = 0; i < ni; ++i) Ho[(size_t)qp.inv_idx[j] * nx + qp.inv_idx[i]] = qp.sol.Hff_inv(i, j);
+    }
   }
   return FDDP_OK;
 }

@@ -128,6 +128,17 @@ class Gpu:
     def mpc_shift(self):
         self._ok(self.L.fddp_mpc_shift(self.h))
 
+    def set_solver_kind(self, kind):
+        self._ok(self.L.fddp_set_solver_kind(self.h, int(kind)))
+
+    def set_control_limits(self, lb, ub):
+        la = None if lb is None else np.ascontiguousarray(lb, dtype=np.float64)
+        ua = None if ub is None else np.ascontiguousarray(ub, dtype=np.float64)
+        self._ok(self.L.fddp_set_control_limits(self.h, _abi.dptr(la), _abi.dptr(ua)))
+
+    def quu_inv(self):
+        return self.quantity(_abi.Q_QUU_INV, self.dims.T, self.dims.nu_max * self.dims.nu_max)
+
 
 def rel_err(a, b):
     a = np.asarray(a, float)

@@ -62,6 +62,32 @@ def _bind(L):
         f.argtypes = [C.c_void_p, _abi.D]
     L.oracle_get_trace.restype = C.c_int
     L.oracle_get_trace.argtypes = [C.c_void_p, C.c_int, _abi.D, C.c_int]
+    L.oracle_get_quu_inv.restype = C.c_int
+    L.oracle_get_quu_inv.argtypes = [C.c_void_p, _abi.D]
+    L.oracle_boxqp_solve.restype = C.c_int
+    L.oracle_boxqp_solve.argtypes = [C.c_int, C.c_int, _abi.D, _abi.D, _abi.D, _abi.D, _abi.D,
+                                     C.POINTER(_abi.BoxQPParams), _abi.D, _abi.U64, _abi.U64, _abi.D, _abi.I32,
+                                     _abi.I32]
+
+
+def boxqp_solve(H, q, lb, ub, xinit, prm):
+    """Batched BoxQP on the oracle (same contract as fddp_boxqp_solve).
+    H: (B, n, n) row-major numpy; returns dict of x, free_mask, inv_mask,
+    Hinv (B, n, n) embedded, status, iters."""
+    L = lib()
+    H = np.asarray(H, float)
+    B, n = H.shape[0], H.shape[1]
+    Hc = np.ascontiguousarray(H.transpose(0, 2, 1))
+    vs = [np.ascontiguousarray(np.broadcast_to(np.asarray(v, float), (B, n))) for v in (q, lb, ub, xinit)]
+    out = dict(x=np.zeros((B, n)), free_mask=np.zeros(B, np.uint64), inv_mask=np.zeros(B, np.uint64),
+               Hinv=np.zeros((B, n, n)), status=np.zeros(B, np.int32), iters=np.zeros(B, np.int32))
+    rc = L.oracle_boxqp_solve(B, n, _abi.dptr(Hc), *[_abi.dptr(v) for v in vs], C.byref(prm),
+                              _abi.dptr(out["x"]), out["free_mask"].ctypes.data_as(_abi.U64),
+                              out["inv_mask"].ctypes.data_as(_abi.U64), _abi.dptr(out["Hinv"]),
+                              out["status"].ctypes.data_as(_abi.I32), out["iters"].ctypes.data_as(_abi.I32))
+    assert rc == 0
+    out["Hinv"] = np.ascontiguousarray(out["Hinv"].transpose(0, 2, 1))
+    return out
 
 
 class Oracle:
@@ -168,6 +194,21 @@ class Oracle:
 
     def mpc_shift(self):
         self.L.oracle_mpc_shift(self.h)
+
+    # SolverBoxFDDP
+    def set_solver_kind(self, kind):
+        self.L.oracle_set_solver_kind(self.h, int(kind))
+
+    def set_control_limits(self, lb, ub):
+        la = None if lb is None else np.ascontiguousarray(lb, dtype=np.float64)
+        ua = None if ub is None else np.ascontiguousarray(ub, dtype=np.float64)
+        self.L.oracle_set_control_limits(self.h, _abi.dptr(la), _abi.dptr(ua))
+
+    def quu_inv(self):
+        d = self.dims
+        a = np.zeros((d.B, d.T, d.nu_max * d.nu_max))
+        self.L.oracle_get_quu_inv(self.h, _abi.dptr(a))
+        return a
 
 
 def default_params():
