@@ -39,7 +39,10 @@ def backward_bytes_per_knot(n, m):
     return 8 * ((2 * n * n + 2 * n * m + m * m + 2 * n + m) + (m * n + 2 * m + 2 * n + m))
 
 
-def cpu_baseline(cfg, T, seed, target_s=12.0):
+BOX_LIMIT = 1.0  # --solver boxfddp: |u_i| <= 1 on every running knot (~30% of the C5 controls saturate)
+
+
+def cpu_baseline(cfg, T, seed, target_s=12.0, box=False):
     """Time the CPU oracle (C++ port of the reference solver, OpenMP over batch
     elements) on this host, on a bounded sample of the same workload."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -60,16 +63,25 @@ def cpu_baseline(cfg, T, seed, target_s=12.0):
         cores = os.cpu_count() or 1
     threads = max(1, min(16, cores))
 
+    from crocoddyl_amd import _abi
+
     def run(Bs, steps):
         S = helpers.setup(cfg, T=T, B=Bs, seed=seed)
+        d = S["dims"]
         o = oracle_lib.Oracle(S["dims"], S["knots"], S["pool"], S["x0s"], threads=threads, mode=2)
+        if box:
+            o.set_solver_kind(_abi.SOLVER_BOXFDDP)
+            o.set_control_limits(np.full((d.B, d.T, d.nu_max), -BOX_LIMIT), np.full((d.B, d.T, d.nu_max), BOX_LIMIT))
+            p = oracle_lib.default_params()
+            p.th_stop = 5e-5
+            o.set_params(p)
         o.set_candidate(None, None, False)
         o.solve(maxiter=2)
         t0 = time.perf_counter()
         it = 0
         for _ in range(steps):
             o.mpc_shift()
-            r = o.solve(maxiter=1, reg_init=0.1)
+            r = o.solve(maxiter=2 if box else 1, reg_init=0.1)
             it += sum(x.n_iter_run for x in r)
         return it, time.perf_counter() - t0
 
@@ -79,9 +91,9 @@ def cpu_baseline(cfg, T, seed, target_s=12.0):
     Bs = max(threads, (Bs // threads) * threads)
     it, dt = run(Bs, steps)
     return {"value": it / dt, "unit": "FDDP iterations/s", "cores": threads, "kind": "port",
-            "sample": f"{cfg} T={T}: {Bs} elements x {steps} warm-started solve(maxiter=1) "
+            "sample": f"{cfg} T={T}: {Bs} elements x {steps} warm-started solve(maxiter={2 if box else 1}) "
                       f"({it} element-iterations in {dt:.1f} s); oracle/fddp_oracle.cpp {flags} -fopenmp, "
-                      f"OpenMP over elements"}
+                      f"OpenMP over elements{', SolverBoxFDDP |u| <= 1' if box else ''}"}
 
 
 def load_pmc(cfg):
@@ -99,11 +111,15 @@ def main():
     ap.add_argument("--config", default="C5_talos_full")
     ap.add_argument("--batch", type=int, default=None, help="elements per GPU (default: the config's)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--solver", choices=["fddp", "boxfddp"], default="fddp",
+                    help="boxfddp: SolverBoxFDDP with |u| <= 1 limits, solve(maxiter=2) per MPC step so the "
+                         "box QP runs (iteration 1 is feasible)")
     args = ap.parse_args()
+    box = args.solver == "boxfddp"
 
     import torch
 
-    from crocoddyl_amd import ShootingProblem, SolverFDDP, synthetic
+    from crocoddyl_amd import ShootingProblem, SolverBoxFDDP, SolverFDDP, synthetic
     from crocoddyl_amd import dist as cdist
 
     ws, rank, local_rank = cdist.world()
@@ -114,15 +130,20 @@ def main():
     B = args.batch or B0
     seed = synthetic.seed_of(args.config) + 1000 * rank  # each rank owns distinct problems
     x0s, running, terminal = synthetic.build(args.config, B=B, seed=seed)
+    if box:
+        for md in set(running):
+            md.u_lb = np.full(md.nu, -BOX_LIMIT)
+            md.u_ub = np.full(md.nu, BOX_LIMIT)
     problem = ShootingProblem(x0s, running, terminal, device=dev)
-    solver = SolverFDDP(problem)
+    solver = SolverBoxFDDP(problem) if box else SolverFDDP(problem)
     n, m, nx = problem.ndx, problem.nu_max, problem.nx
+    mpc_iters = 2 if box else 1
 
     solver.solve(maxiter=5)  # converge once from a cold start
 
     def step():  # one receding-horizon MPC solve, all elements
         solver.mpcShift()
-        solver.solve_from_candidate(maxiter=1, isFeasible=False, regInit=0.1)
+        solver.solve_from_candidate(maxiter=mpc_iters, isFeasible=False, regInit=0.1)
 
     for _ in range(args.warmup):
         step()
@@ -167,7 +188,7 @@ def main():
         cpu = None
         if ws == 1 and not args.no_cpu_baseline:
             try:
-                cpu = cpu_baseline(args.config, T, synthetic.seed_of(args.config))
+                cpu = cpu_baseline(args.config, T, synthetic.seed_of(args.config), box=box)
             except Exception as e:  # reported, never fatal for the GPU number
                 cpu = {"error": repr(e)}
         out = {
@@ -177,9 +198,11 @@ def main():
             "data": "synthetic: seeded Euler(dt)∘DifferentialActionModelLQR knots at the config's (n, m, T); "
                     "per-element matrices (SURVEY §8d); no robot model (Pinocchio/URDF absent)",
             "config": {"workload": f"{args.config}: n={n}, m={m}, T={T}, B={B} per GPU, warm-started "
-                                   "solve(maxiter=1, reg_init=0.1) after a device receding-horizon shift",
-                       "global_batch": B * ws, "T": T, "parallelism": f"batch-sharded x{ws}"},
-            "mpc_solves_per_s": round(value, 2),
+                                   f"solve(maxiter={mpc_iters}, reg_init=0.1) after a device receding-horizon shift"
+                                   + (", SolverBoxFDDP with |u| <= 1" if box else ""),
+                       "global_batch": B * ws, "T": T, "parallelism": f"batch-sharded x{ws}",
+                       "solver": "SolverBoxFDDP" if box else "SolverFDDP"},
+            "mpc_solves_per_s": round(B * ws * args.steps / elapsed, 2),
             "kernel_ms_per_step": {k: round(v[0] / max(args.steps, 1), 3) for k, v in timing.items()},
             "roofline": roof,
             "cpu_baseline": cpu,

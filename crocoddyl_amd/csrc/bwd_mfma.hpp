@@ -816,8 +816,13 @@ __device__ __forceinline__ bool bwd_knot(const Dev& D, const BwdLds& L, int b, i
     }
     if (boxk) {
       if (!box_gains_wave<MP, LDQ>(D, L, b, t, cur, lane) && lane == 0) *L.flag = 1;
-    } else if (sym_sweep_inverse<MP, LDQ>(Quu, Qi, L.rowbuf, m, lane) && lane == 0) {
-      *L.flag = 1;
+    } else {
+#ifdef FDDP_INV_BLK
+      const bool bad = sym_sweep_inverse_blk<MP, LDQ>(Quu, Qi, L.rowbuf, m, lane);
+#else
+      const bool bad = sym_sweep_inverse<MP, LDQ>(Quu, Qi, L.rowbuf, m, lane);
+#endif
+      if (bad && lane == 0) *L.flag = 1;
     }
   }
   stamp.mark(2);

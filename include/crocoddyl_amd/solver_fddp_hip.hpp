@@ -6,6 +6,8 @@
 //       include/crocoddyl/core/optctrl/shooting.hpp:48-63
 //   crocoddyl::SolverFDDP(problem).solve(init_xs, init_us, maxiter, is_feasible, reginit)
 //       include/crocoddyl/core/solvers/fddp.hpp:50-101, src/core/solvers/fddp.cpp:19-105
+//   crocoddyl::SolverBoxFDDP(problem)  include/crocoddyl/core/solvers/box-fddp.hpp, src/core/solvers/box-fddp.cpp
+//   ActionModelAbstract::set_u_lb / set_u_ub / get_has_control_limits  core/action-base.hxx:107-144
 //   crocoddyl::ActionModelLQR(nx, nu, drift_free)          core/actions/lqr.hpp:21-60
 //   crocoddyl::ActionModelUnicycle()                        core/actions/unicycle.hpp
 //   crocoddyl::DifferentialActionModelLQR(nq, nu, drift_free), IntegratedActionModelEuler(model, dt)
@@ -44,12 +46,40 @@ inline VectorXd to_vec(const V& v) {
 
 // Parameter carriers with the reference defaults. pack() appends this
 // model's block (layout: include/fddp_hip.h) to `pool`.
-struct ActionModelBase {
+// Control limits (action-base.hxx:20-22, 107-144): -inf / +inf by default.
+struct ControlLimits {
+  template <class V>
+  void set_u_lb(const V& v) {
+    if ((int)v.size() != limits_nu()) throw Exception("Invalid argument: lower bound has wrong dimension");
+    u_lb_ = to_vec(v);
+  }
+  template <class V>
+  void set_u_ub(const V& v) {
+    if ((int)v.size() != limits_nu()) throw Exception("Invalid argument: upper bound has wrong dimension");
+    u_ub_ = to_vec(v);
+  }
+  VectorXd get_u_lb() const { return u_lb_.empty() ? VectorXd(limits_nu(), -INFINITY) : u_lb_; }
+  VectorXd get_u_ub() const { return u_ub_.empty() ? VectorXd(limits_nu(), INFINITY) : u_ub_; }
+  bool get_has_control_limits() const {  // update_has_control_limits (action-base.hxx:142-144)
+    bool l = false, u = false;
+    for (double v : get_u_lb()) l = l || std::isfinite(v);
+    for (double v : get_u_ub()) u = u || std::isfinite(v);
+    return l && u;
+  }
+  virtual ~ControlLimits() {}
+  virtual int limits_nu() const = 0;
+
+ protected:
+  VectorXd u_lb_, u_ub_;
+};
+
+struct ActionModelBase : ControlLimits {
   virtual ~ActionModelBase() {}
   virtual int kind() const = 0;
   virtual int nx() const = 0;
   virtual int nu() const = 0;
   virtual void pack(VectorXd& pool) const = 0;
+  int limits_nu() const { return nu(); }
 };
 
 inline VectorXd eye(int r, int c) {
@@ -86,8 +116,9 @@ struct ActionModelUnicycle : ActionModelBase {  // unicycle.hxx:13-16
   }
 };
 
-struct DifferentialActionModelLQR {  // diff-lqr.hxx:14-28
+struct DifferentialActionModelLQR : ControlLimits {  // diff-lqr.hxx:14-28
   int nq, nu;
+  int limits_nu() const { return nu; }
   bool drift_free;
   VectorXd Fq, Fv, Fu, f0, Lxx, Lxu, Luu, lx, lu;
   DifferentialActionModelLQR(int nq_, int nu_, bool drift_free_ = true)
@@ -100,7 +131,10 @@ struct IntegratedActionModelEuler : ActionModelBase {  // euler.hxx:16-35
   std::shared_ptr<DifferentialActionModelLQR> differential;
   double dt;
   IntegratedActionModelEuler(std::shared_ptr<DifferentialActionModelLQR> d, double time_step = 1e-3)
-      : differential(d), dt(time_step < 0. ? 1e-3 : time_step) {}
+      : differential(d), dt(time_step < 0. ? 1e-3 : time_step) {
+    set_u_lb(d->get_u_lb());  // euler.hxx:25-26
+    set_u_ub(d->get_u_ub());
+  }
   int kind() const { return FDDP_KNOT_EULER_DIFFLQR; }
   int nx() const { return 2 * differential->nq; }
   int nu() const { return differential->nu; }
@@ -168,6 +202,25 @@ class ShootingProblem {
       knots.push_back(d);
     }
   }
+  // control limits of the running knots, B*T*nu_max each (fddp_set_control_limits);
+  // false when no model has any limit
+  bool pack_limits(VectorXd& lb, VectorXd& ub) const {
+    const int T = get_T(), m = nu_max_;
+    lb.assign((size_t)B_ * T * m, -INFINITY);
+    ub.assign((size_t)B_ * T * m, INFINITY);
+    bool any = false;
+    for (int t = 0; t < T; ++t) {
+      const VectorXd l = running_[t]->get_u_lb(), u = running_[t]->get_u_ub();
+      for (int i = 0; i < running_[t]->nu(); ++i) {
+        any = any || std::isfinite(l[i]) || std::isfinite(u[i]);
+        for (int b = 0; b < B_; ++b) {
+          lb[((size_t)b * T + t) * m + i] = l[i];
+          ub[((size_t)b * T + t) * m + i] = u[i];
+        }
+      }
+    }
+    return any;
+  }
 
  private:
   VectorXd x0_;
@@ -204,6 +257,10 @@ class SolverFDDP {
              std::size_t maxiter = 100, bool is_feasible = false, double reginit = 1e-9) {
     setCandidate(init_xs, init_us, is_feasible);
     check(fddp_set_x0(h_.get(), problem_->get_x0().data()), "fddp_set_x0");
+    VectorXd lb, ub;  // the models' current limits (SolverFDDP ignores them)
+    const bool lim = problem_->pack_limits(lb, ub);
+    check(fddp_set_control_limits(h_.get(), lim ? lb.data() : nullptr, lim ? ub.data() : nullptr),
+          "fddp_set_control_limits");
     check(fddp_set_params(h_.get(), &params_), "fddp_set_params");
     check(fddp_solve(h_.get(), (int)maxiter, is_feasible ? 1 : 0, reginit, res_.data()), "fddp_solve");
     return res_[0].status == FDDP_STATUS_CONVERGED;
@@ -269,7 +326,7 @@ class SolverFDDP {
   double get_th_stop() const { return params_.th_stop; }
   fddp_handle* handle() const { return h_.get(); }
 
- private:
+ protected:
   void push() {
     const int rc = fddp_set_params(h_.get(), &params_);
     if (rc != FDDP_OK) {
@@ -282,6 +339,17 @@ class SolverFDDP {
   fddp_dims dims_;
   fddp_params params_;
   std::vector<fddp_result> res_;
+};
+
+// SolverBoxFDDP (box-fddp.cpp:15-164): box-QP gains on limited knots once
+// feasible, clamped controls in the forward pass; th_stop = 5e-5 (:28).
+class SolverBoxFDDP : public SolverFDDP {
+ public:
+  explicit SolverBoxFDDP(std::shared_ptr<ShootingProblem> problem, int device = 0) : SolverFDDP(problem, device) {
+    check(fddp_set_solver_kind(h_.get(), FDDP_SOLVER_BOXFDDP), "fddp_set_solver_kind");
+    params_.th_stop = 5e-5;
+    push();
+  }
 };
 
 }  // namespace crocoddyl_amd

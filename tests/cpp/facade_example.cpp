@@ -1,5 +1,7 @@
 // The reference's benchmark/lqr-optctrl.cpp usage pattern written against the
 // crocoddyl_amd C++ facade: only the namespace changes.
+#include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <memory>
 #include <vector>
@@ -30,6 +32,19 @@ int main(int argc, char** argv) {
     const auto xs = usolver.get_xs();
     std::printf("unicycle converged=%d iter=%zu cost=%.12e xT=(%.3e %.3e %.3e)\n", uok, usolver.get_iter(),
                 usolver.get_cost(), xs.back()[0], xs.back()[1], xs.back()[2]);
+    // control-limited LQR with SolverBoxFDDP (box-fddp.cpp)
+    auto bmodel = std::make_shared<croc::ActionModelLQR>(24, 12, false);
+    bmodel->set_u_lb(croc::VectorXd(12, -0.05));
+    bmodel->set_u_ub(croc::VectorXd(12, 0.05));
+    std::vector<std::shared_ptr<croc::ActionModelBase> > brun(T, bmodel);
+    auto bprob = std::make_shared<croc::ShootingProblem>(x0, brun, bmodel);
+    croc::SolverBoxFDDP bsolver(bprob);
+    const bool bok = bsolver.solve();
+    double umax = 0.;
+    for (const auto& u : bsolver.get_us())
+      for (double v : u) umax = std::max(umax, std::fabs(v));
+    std::printf("box converged=%d iter=%zu cost=%.12e umax=%.6f th_stop=%.1e\n", bok, bsolver.get_iter(),
+                bsolver.get_cost(), umax, bsolver.get_th_stop());
     try {
       usolver.set_th_stepdec(2.0);  // ddp.cpp:464-470 rejects this
       std::printf("setter validation MISSING\n");
@@ -37,7 +52,7 @@ int main(int argc, char** argv) {
     } catch (const croc::Exception&) {
       std::printf("setter validation ok\n");
     }
-    return (ok && uok) ? 0 : 2;
+    return (ok && uok && bok && umax <= 0.05) ? 0 : 2;
   } catch (const croc::Exception& e) {
     std::printf("exception: %s\n", e.what());
     return 1;

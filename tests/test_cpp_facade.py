@@ -48,3 +48,17 @@ def test_facade_solves_on_gpu(tmp_path):
         cost = float(lines[key].split("cost=")[1].split()[0])
         assert abs(cost - r0.cost) <= 1e-6 * max(1, abs(r0.cost))
         assert f"iter={r0.iter}" in lines[key]
+    # SolverBoxFDDP on the limited LQR
+    assert "converged=1" in lines["box"] and "th_stop=5.0e-05" in lines["box"]
+    model = ActionModelLQR(24, 12, False)
+    knots, pool = pack_problem([model] * 100, model, 1)
+    o = oracle_lib.Oracle(_abi.Dims(24, 24, 12, 100, 1), knots, pool, np.zeros((1, 24)))
+    o.set_solver_kind(_abi.SOLVER_BOXFDDP)
+    o.set_control_limits(np.full((1, 100, 12), -0.05), np.full((1, 100, 12), 0.05))
+    p = oracle_lib.default_params()
+    p.th_stop = 5e-5
+    o.set_params(p)
+    o.set_candidate(None, None, False)
+    r0 = o.solve(100)[0]
+    cost = float(lines["box"].split("cost=")[1].split()[0])
+    assert abs(cost - r0.cost) <= 1e-6 * max(1, abs(r0.cost)) and f"iter={r0.iter}" in lines["box"]
