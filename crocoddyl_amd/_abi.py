@@ -78,6 +78,7 @@ PROTOS = {
     "mpc_shift": (C.c_int, [P]),
     "set_solver_kind": (C.c_int, [P, C.c_int]),
     "set_control_limits": (C.c_int, [P, D, D]),
+    "set_knots": (C.c_int, [P, C.POINTER(KnotDesc), D, C.c_int64]),
 }
 
 # product-only entry points (libfddp_hip)

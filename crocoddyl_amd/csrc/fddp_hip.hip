@@ -68,6 +68,36 @@ int64_t block_doubles(int kind, int nx, int nu) {
   return -1;
 }
 
+
+// Validation of a knot sequence against the handle's dims (fddp_create,
+// fddp_set_knots). exact_nu_max: the running knots' max nu must equal
+// nu_max (creation); otherwise it may be smaller (the reference's
+// circularAppend / updateNode checks, shooting.hxx:249-252).
+int check_knots(const fddp_dims& d, const fddp_knot_desc* knots, int64_t n_params, const char* who,
+                bool exact_nu_max) {
+  const std::string w(who);
+  int nu_max = 0;
+  for (int t = 0; t <= d.T; ++t) {
+    const fddp_knot_desc& k = knots[t];
+    if (k.nu < 0) return fail(FDDP_ERR_INVALID_ARG, w + ": negative nu");
+    if (t < d.T && k.nu > nu_max) nu_max = k.nu;
+    if (k.kind == FDDP_KNOT_UNICYCLE && (d.nx != 3 || k.nu != 2))
+      return fail(FDDP_ERR_INVALID_ARG, w + ": unicycle knots need nx=3, nu=2");
+    if (k.kind == FDDP_KNOT_EULER_DIFFLQR && (d.nx % 2))
+      return fail(FDDP_ERR_INVALID_ARG, w + ": Euler(DiffLQR) knots need an even nx");
+    const int64_t sz = block_doubles(k.kind, d.nx, k.nu);
+    if (sz < 0) return fail(FDDP_ERR_UNSUPPORTED, w + ": unknown knot kind " + std::to_string(k.kind));
+    if (k.param_offset < 0 || k.param_stride < 0 ||
+        k.param_offset + (int64_t)(d.B - 1) * k.param_stride + sz > n_params)
+      return fail(FDDP_ERR_INVALID_ARG, w + ": knot " + std::to_string(t) + " parameter block out of range");
+  }
+  if (exact_nu_max ? nu_max != d.nu_max : nu_max > d.nu_max)
+    return fail(FDDP_ERR_INVALID_ARG, exact_nu_max ? w + ": nu_max must equal the max nu over the running knots"
+                                                   : w + ": nu node is bigger than the maximum nu");
+  if (knots[d.T].nu > d.nu_max) return fail(FDDP_ERR_INVALID_ARG, w + ": terminal nu exceeds nu_max");
+  return FDDP_OK;
+}
+
 }  // namespace
 
 struct fddp_handle_s {
@@ -76,6 +106,7 @@ struct fddp_handle_s {
   hipStream_t stream = nullptr;
   std::vector<fddp_knot_desc> knots;
   int64_t n_params = 0;
+  int64_t params_cap = 0;  // doubles allocated for the parameter pool
   fddp_params prm;
   Dev D;
   std::vector<void*> allocs;
@@ -370,6 +401,102 @@ void fddp_default_params(fddp_params* p) {
   for (int i = 0; i < 16; ++i) p->alphas[i] = i < 10 ? 1. / std::pow(2., (double)i) : 0.;
 }
 
+namespace {
+
+// Knot-dependent device state of a handle: LDS plans and the fast-path
+// choice, the parameter pool, the knot descriptors, the knot segments of the
+// tiled calc, and the Riccati sweep variant (fddp_create, fddp_set_knots).
+int apply_knots(fddp_handle* h, const fddp_knot_desc* knots, const double* params, int64_t n_params) {
+  Dev& D = h->D;
+  const fddp_dims& d = h->dims;
+  const int64_t K1 = (int64_t)d.T + 1;
+  int rc;
+  h->knots.assign(knots, knots + K1);
+  {
+    int64_t pmax = 0;
+    for (int t = 0; t <= d.T; ++t) pmax = std::max<int64_t>(pmax, block_doubles(knots[t].kind, d.nx, knots[t].nu));
+    const int64_t budget = (150 * 1024) / 8 - (2 * D.sX + D.sM + 5 * (kNT / kWave) + 16);
+    h->pcap = pmax <= budget ? pad2(pmax) : 0;
+  }
+  h->fwd_smem = sizeof(double) * (h->pcap + fwd_lds_doubles<kNT, false>(D.sX, D.sN, D.sM));
+  h->calc_smem = sizeof(double) * (h->pcap + 2 * D.sX + D.sM + 5 * (kNT / kWave) + 16);
+  h->cdiff_smem = sizeof(double) * (h->pcap + D.sX + D.sM);
+  {  // dense-knot fast path: every knot LQR / Euler∘DiffLQR, block LDS-resident
+    bool dense = h->pcap > 0 && d.nx == d.ndx && d.nx <= kNT && d.nu_max <= kNT;
+    for (int t = 0; t <= d.T; ++t)
+      dense = dense && (knots[t].kind == FDDP_KNOT_LQR || knots[t].kind == FDDP_KNOT_EULER_DIFFLQR);
+    h->fused_smem = sizeof(double) * (h->pcap + calc_tiled_lds(D.sX, D.sM));
+    h->fwd_fast_smem = sizeof(double) * (h->pcap + fwd_lds_doubles<kNT, true>(D.sX, D.sN, D.sM));
+    const char* env = std::getenv("FDDP_FAST");
+    const bool off = env && env[0] == '0';
+    h->fast = dense && !off && h->fused_smem <= 160 * 1024 && h->fwd_fast_smem <= 160 * 1024;
+  }
+  if (n_params > h->params_cap) {  // the old pool stays owned by the handle until fddp_destroy
+    double* p = nullptr;
+    if ((rc = dalloc(h, &p, n_params))) return rc;
+    D.params = p;
+    h->params_cap = n_params;
+  }
+  h->n_params = n_params;
+  HIP_TRY(hipMemcpyAsync((void*)D.params, params, sizeof(double) * n_params, hipMemcpyHostToDevice, h->stream));
+  if (!D.knots) {
+    fddp_knot_desc* kd = nullptr;
+    if ((rc = dalloc(h, (double**)&kd, (sizeof(fddp_knot_desc) * K1 + 7) / 8))) return rc;
+    D.knots = kd;
+  }
+  HIP_TRY(hipMemcpyAsync((void*)D.knots, knots, sizeof(fddp_knot_desc) * K1, hipMemcpyHostToDevice, h->stream));
+  {  // knot segments: runs of knots with the same desc and parameter block
+     // (running runs stop before the terminal knot), for the tiled calc
+    std::vector<int> se(d.T + 1);
+    for (int t = d.T; t >= 0; --t) {
+      const bool same = t + 1 < d.T && knots[t + 1].kind == knots[t].kind && knots[t + 1].nu == knots[t].nu &&
+                        knots[t + 1].param_offset == knots[t].param_offset &&
+                        knots[t + 1].param_stride == knots[t].param_stride;
+      se[t] = same ? se[t + 1] : t + 1;
+    }
+    if (!D.segend) {
+      double* sp = nullptr;
+      if ((rc = dalloc(h, &sp, (d.T + 2) / 2 + 1))) return rc;
+      D.segend = (const int*)sp;
+    }
+    HIP_TRY(hipMemcpyAsync((void*)D.segend, se.data(), sizeof(int) * se.size(), hipMemcpyHostToDevice, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));  // the host staging vectors go out of scope
+  }
+  if (hipFuncSetAttribute((const void*)backward_kernel<kNT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)h->bwd_smem) != hipSuccess ||
+      hipFuncSetAttribute((const void*)forward_kernel<kNT, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)h->fwd_smem) != hipSuccess ||
+      hipFuncSetAttribute((const void*)forward_kernel<kNT, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)h->fwd_fast_smem) != hipSuccess ||
+      hipFuncSetAttribute((const void*)calc_tiled_kernel<kNTF>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)h->fused_smem) != hipSuccess ||
+      hipFuncSetAttribute((const void*)calc_kernel<kNT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)h->calc_smem) != hipSuccess ||
+      hipFuncSetAttribute((const void*)calc_diff_kernel<kNT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)h->cdiff_smem) != hipSuccess)
+    return fail(FDDP_ERR_RUNTIME, "hipFuncSetAttribute(dynamic LDS)");
+  {  // backward sweep variant: MFMA tiles when every running knot has nu == nu_max
+    bool uniform_nu = d.nu_max > 0;
+    for (int t = 0; t < d.T; ++t) uniform_nu = uniform_nu && knots[t].nu == d.nu_max;
+    const char* env = std::getenv("FDDP_BACKWARD");
+    const bool force_generic = env && std::strcmp(env, "generic") == 0;
+    const int ntl = (d.ndx + 15) / 16, mtl = (d.nu_max + 15) / 16;
+    int v = -1;
+    if (uniform_nu && !force_generic) {
+      const char* ew = std::getenv("FDDP_BWD_WAVES");
+      const int nw = (ew && ew[0] == '4') ? 4 : 8;
+      if (ntl == 5 && mtl == 2) v = setup_bwd_mfma_nw<5, 2>(h, nw);
+      else if (ntl == 3 && mtl == 1) v = setup_bwd_mfma_nw<3, 1>(h, nw);
+      else if (ntl == 2 && mtl == 1) v = setup_bwd_mfma_nw<2, 1>(h, nw);
+      else if (ntl == 1 && mtl == 1) v = setup_bwd_mfma_nw<1, 1>(h, nw);
+    }
+    h->bwd_variant = v > 0 ? v : 0;
+  }
+  return FDDP_OK;
+}
+
+}  // namespace
+
 int fddp_create(const fddp_dims* dims, const fddp_knot_desc* knots, const double* params, int64_t n_params,
                 int device, fddp_handle** out) {
   g_err.clear();
@@ -380,25 +507,10 @@ int fddp_create(const fddp_dims* dims, const fddp_knot_desc* knots, const double
     return fail(FDDP_ERR_INVALID_ARG, "fddp_create: T, B, nx must be positive");
   if (d.nx != d.ndx) return fail(FDDP_ERR_UNSUPPORTED, "fddp_create: only Euclidean states (nx == ndx) are supported");
   if (d.B > 65535) return fail(FDDP_ERR_INVALID_ARG, "fddp_create: B > 65535 per handle");
-  int nu_max = 0;
-  for (int t = 0; t <= d.T; ++t) {
-    const fddp_knot_desc& k = knots[t];
-    if (k.nu < 0) return fail(FDDP_ERR_INVALID_ARG, "fddp_create: negative nu");
-    if (t < d.T && k.nu > nu_max) nu_max = k.nu;
-    if (k.kind == FDDP_KNOT_UNICYCLE && (d.nx != 3 || k.nu != 2))
-      return fail(FDDP_ERR_INVALID_ARG, "fddp_create: unicycle knots need nx=3, nu=2");
-    if (k.kind == FDDP_KNOT_EULER_DIFFLQR && (d.nx % 2))
-      return fail(FDDP_ERR_INVALID_ARG, "fddp_create: Euler(DiffLQR) knots need an even nx");
-    const int64_t sz = block_doubles(k.kind, d.nx, k.nu);
-    if (sz < 0) return fail(FDDP_ERR_UNSUPPORTED, "fddp_create: unknown knot kind " + std::to_string(k.kind));
-    if (k.param_offset < 0 || k.param_stride < 0 ||
-        k.param_offset + (int64_t)(d.B - 1) * k.param_stride + sz > n_params)
-      return fail(FDDP_ERR_INVALID_ARG, "fddp_create: knot " + std::to_string(t) + " parameter block out of range");
+  {
+    const int rc0 = check_knots(d, knots, n_params, "fddp_create", true);
+    if (rc0) return rc0;
   }
-  if (nu_max != d.nu_max)
-    return fail(FDDP_ERR_INVALID_ARG, "fddp_create: nu_max must equal the max nu over the running knots");
-  if (knots[d.T].nu > d.nu_max)
-    return fail(FDDP_ERR_INVALID_ARG, "fddp_create: terminal nu exceeds nu_max");
 
   int ndev = 0;
   const hipError_t ce = hipGetDeviceCount(&ndev);
@@ -419,8 +531,6 @@ int fddp_create(const fddp_dims* dims, const fddp_knot_desc* knots, const double
   auto* h = new fddp_handle_s();
   h->dims = d;
   h->device = device;
-  h->knots.assign(knots, knots + d.T + 1);
-  h->n_params = n_params;
   fddp_default_params(&h->prm);
   int rc;
   auto bail = [&](int code) {
@@ -459,37 +569,6 @@ int fddp_create(const fddp_dims* dims, const fddp_knot_desc* knots, const double
       return bail(fail(FDDP_ERR_UNSUPPORTED, "fddp_create: (ndx, nu_max) too large for the Riccati sweep"));
     if ((rc = dalloc(h, &D.bwork, (int64_t)d.B * BwdSmem::work_doubles(D.n, D.m)))) return bail(rc);
   }
-  {
-    int64_t pmax = 0;
-    for (int t = 0; t <= d.T; ++t) pmax = std::max<int64_t>(pmax, block_doubles(knots[t].kind, d.nx, knots[t].nu));
-    const int64_t budget = (150 * 1024) / 8 - (2 * D.sX + D.sM + 5 * (kNT / kWave) + 16);
-    h->pcap = pmax <= budget ? pad2(pmax) : 0;
-  }
-  h->fwd_smem = sizeof(double) * (h->pcap + fwd_lds_doubles<kNT, false>(D.sX, D.sN, D.sM));
-  h->calc_smem = sizeof(double) * (h->pcap + 2 * D.sX + D.sM + 5 * (kNT / kWave) + 16);
-  h->cdiff_smem = sizeof(double) * (h->pcap + D.sX + D.sM);
-  {  // dense-knot fast path: every knot LQR / Euler∘DiffLQR, block LDS-resident
-    bool dense = h->pcap > 0 && d.nx == d.ndx && d.nx <= kNT && d.nu_max <= kNT;
-    for (int t = 0; t <= d.T; ++t)
-      dense = dense && (knots[t].kind == FDDP_KNOT_LQR || knots[t].kind == FDDP_KNOT_EULER_DIFFLQR);
-    h->fused_smem = sizeof(double) * (h->pcap + calc_tiled_lds(D.sX, D.sM));
-    h->fwd_fast_smem = sizeof(double) * (h->pcap + fwd_lds_doubles<kNT, true>(D.sX, D.sN, D.sM));
-    const char* env = std::getenv("FDDP_FAST");
-    const bool off = env && env[0] == '0';
-    h->fast = dense && !off && h->fused_smem <= 160 * 1024 && h->fwd_fast_smem <= 160 * 1024;
-  }
-
-  double* p = nullptr;
-  if ((rc = dalloc(h, &p, n_params))) return bail(rc);
-  D.params = p;
-  if (hipMemcpyAsync(p, params, sizeof(double) * n_params, hipMemcpyHostToDevice, h->stream) != hipSuccess)
-    return bail(fail(FDDP_ERR_RUNTIME, "upload params"));
-  fddp_knot_desc* kd = nullptr;
-  if ((rc = dalloc(h, (double**)&kd, (sizeof(fddp_knot_desc) * K1 + 7) / 8))) return bail(rc);
-  D.knots = kd;
-  if (hipMemcpyAsync(kd, knots, sizeof(fddp_knot_desc) * K1, hipMemcpyHostToDevice, h->stream) != hipSuccess)
-    return bail(fail(FDDP_ERR_RUNTIME, "upload knots"));
-
   struct A {
     double** p;
     int64_t n;
@@ -504,21 +583,6 @@ int fddp_create(const fddp_dims* dims, const fddp_knot_desc* knots, const double
   };
   for (auto& a : plan)
     if ((rc = dalloc(h, a.p, a.n))) return bail(rc);
-  {  // knot segments: runs of knots with the same desc and parameter block
-     // (running runs stop before the terminal knot), for the tiled calc
-    std::vector<int> se(d.T + 1);
-    for (int t = d.T; t >= 0; --t) {
-      const bool same = t + 1 < d.T && knots[t + 1].kind == knots[t].kind && knots[t + 1].nu == knots[t].nu &&
-                        knots[t + 1].param_offset == knots[t].param_offset &&
-                        knots[t + 1].param_stride == knots[t].param_stride;
-      se[t] = same ? se[t + 1] : t + 1;
-    }
-    double* sp = nullptr;
-    if ((rc = dalloc(h, &sp, (d.T + 2) / 2 + 1))) return bail(rc);
-    if (hipMemcpyAsync(sp, se.data(), sizeof(int) * se.size(), hipMemcpyHostToDevice, h->stream) != hipSuccess)
-      return bail(fail(FDDP_ERR_RUNTIME, "upload segments"));
-    D.segend = (const int*)sp;
-  }
   double* stp = nullptr;
   if ((rc = dalloc(h, &stp, (int64_t)(sizeof(ElemState) / 8) * B))) return bail(rc);
   D.st = (ElemState*)stp;
@@ -541,36 +605,7 @@ int fddp_create(const fddp_dims* dims, const fddp_knot_desc* knots, const double
   }
   if (hipMemcpyAsync(D.st, st0.data(), sizeof(ElemState) * B, hipMemcpyHostToDevice, h->stream) != hipSuccess)
     return bail(fail(FDDP_ERR_RUNTIME, "upload state"));
-  if (hipFuncSetAttribute((const void*)backward_kernel<kNT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)h->bwd_smem) != hipSuccess ||
-      hipFuncSetAttribute((const void*)forward_kernel<kNT, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)h->fwd_smem) != hipSuccess ||
-      hipFuncSetAttribute((const void*)forward_kernel<kNT, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)h->fwd_fast_smem) != hipSuccess ||
-      hipFuncSetAttribute((const void*)calc_tiled_kernel<kNTF>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)h->fused_smem) != hipSuccess ||
-      hipFuncSetAttribute((const void*)calc_kernel<kNT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)h->calc_smem) != hipSuccess ||
-      hipFuncSetAttribute((const void*)calc_diff_kernel<kNT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)h->cdiff_smem) != hipSuccess)
-    return bail(fail(FDDP_ERR_RUNTIME, "hipFuncSetAttribute(dynamic LDS)"));
-  {  // backward sweep variant: MFMA tiles when every running knot has nu == nu_max
-    bool uniform_nu = d.nu_max > 0;
-    for (int t = 0; t < d.T; ++t) uniform_nu = uniform_nu && knots[t].nu == d.nu_max;
-    const char* env = std::getenv("FDDP_BACKWARD");
-    const bool force_generic = env && std::strcmp(env, "generic") == 0;
-    const int ntl = (d.ndx + 15) / 16, mtl = (d.nu_max + 15) / 16;
-    int v = -1;
-    if (uniform_nu && !force_generic) {
-      const char* ew = std::getenv("FDDP_BWD_WAVES");
-      const int nw = (ew && ew[0] == '4') ? 4 : 8;
-      if (ntl == 5 && mtl == 2) v = setup_bwd_mfma_nw<5, 2>(h, nw);
-      else if (ntl == 3 && mtl == 1) v = setup_bwd_mfma_nw<3, 1>(h, nw);
-      else if (ntl == 2 && mtl == 1) v = setup_bwd_mfma_nw<2, 1>(h, nw);
-      else if (ntl == 1 && mtl == 1) v = setup_bwd_mfma_nw<1, 1>(h, nw);
-    }
-    h->bwd_variant = v > 0 ? v : 0;
-  }
+  if ((rc = apply_knots(h, knots, params, n_params))) return bail(rc);
   if (const char* e = std::getenv("FDDP_STAMPS")) {
     if (e[0] == '1') {
       double* p2 = nullptr;
@@ -952,6 +987,15 @@ int fddp_get_quantity(fddp_handle* h, int which, double* out) {
   }
   HIP_TRY(hipStreamSynchronize(h->stream));
   return FDDP_OK;
+}
+
+int fddp_set_knots(fddp_handle* h, const fddp_knot_desc* knots, const double* params, int64_t n_params) {
+  if (!h || !knots || !params) return fail(FDDP_ERR_INVALID_ARG, "fddp_set_knots: null argument");
+  int rc;
+  if ((rc = check_knots(h->dims, knots, n_params, "fddp_set_knots", false))) return rc;
+  DeviceGuard g(h->device);
+  HIP_TRY(hipStreamSynchronize(h->stream));  // no launch may still read the old knots
+  return apply_knots(h, knots, params, n_params);
 }
 
 int fddp_set_solver_kind(fddp_handle* h, int kind) {

@@ -78,6 +78,7 @@ class _Handle:
         self.ptr = C.c_void_p()
         knots, pool = problem._packed()
         self.n_params = pool.size
+        self._knots = knots
         self._sig = problem._signature()
         dims = problem._dims()
         kd = (_abi.KnotDesc * len(knots))(*[_abi.KnotDesc(*k) for k in knots])
@@ -94,12 +95,17 @@ class _Handle:
             self._lsig = lsig
 
     def refresh(self):
+        """Push model changes: parameter setters (same layout) or a new knot
+        sequence (circularAppend / updateNode / updateModel -> fddp_set_knots)."""
         sig = self.problem._signature()
         if sig != self._sig:
             knots, pool = self.problem._packed()
-            if pool.size != self.n_params:
-                raise FDDPError("model parameter layout changed; rebuild the ShootingProblem")
-            check(lib().fddp_set_model_params(self.ptr, _abi.dptr(pool), pool.size))
+            if pool.size == self.n_params and knots == self._knots:
+                check(lib().fddp_set_model_params(self.ptr, _abi.dptr(pool), pool.size))
+            else:
+                kd = (_abi.KnotDesc * len(knots))(*[_abi.KnotDesc(*k) for k in knots])
+                check(lib().fddp_set_knots(self.ptr, kd, _abi.dptr(pool), pool.size))
+                self._knots, self.n_params = knots, pool.size
             self._sig = sig
         self._push_limits()
         return self.ptr
@@ -184,6 +190,56 @@ class ShootingProblem:
 
     def _signature(self):
         return tuple((id(m), m._version) for m in self._models + [self._terminal])
+
+    # -- MPC plumbing (shooting.hxx:235-346) -------------------------------------
+    def _check_node(self, model, data=None):
+        if model.state.nx != self.nx:
+            raise ValueError("Invalid argument: nx is not consistent with the other nodes")
+        if model.state.ndx != self.ndx:
+            raise ValueError("Invalid argument: ndx node is not consistent with the other nodes")
+        if model.nu > self.nu_max:
+            raise ValueError("Invalid argument: nu node is not bigger than the maximun nu")
+        if data is not None and (not isinstance(data, ActionData) or data.Fu.shape[1] != model.nu):
+            raise ValueError("Invalid argument: action data is not consistent with the action model")
+        if model.pack()[2].shape[0] not in (1, self.B):
+            raise ValueError(f"Invalid argument: model parameters are batched over {model.pack()[2].shape[0]} "
+                             f"elements but the problem has B={self.B}")
+
+    def circularAppend(self, model, data=None):
+        """ShootingProblem::circularAppend (shooting.hxx:235-281): drop the
+        first running node, append (model, data) at the end. The device handles
+        get the rotated knot sequence on their next use (fddp_set_knots)."""
+        self._check_node(model, data)
+        self._models = self._models[1:] + [model]
+        self.runningDatas = self.runningDatas[1:] + [data if data is not None else model.createData()]
+
+    def updateNode(self, i, model, data):
+        """ShootingProblem::updateNode (shooting.hxx:283-315): node i < T is a
+        running node, i == T the terminal one. (The reference accepts i == T+1
+        and then writes past its running models; that is an error here.)"""
+        if not 0 <= i <= self.T:
+            raise ValueError(f"Invalid argument: i is bigger than the allocated horizon (it should be less than "
+                             f"or equal to {self.T})")
+        self._check_node(model, data)
+        if i == self.T:
+            self._terminal, self.terminalData = model, data
+        else:
+            self._models[i] = model
+            self.runningDatas[i] = data
+
+    def updateModel(self, i, model):
+        """ShootingProblem::updateModel (shooting.hxx:317-346): i < T running,
+        i == T+1 terminal, with a fresh data. (The reference's i == T indexes
+        past its running models; that is an error here.)"""
+        if not (0 <= i < self.T or i == self.T + 1):
+            raise ValueError(f"Invalid argument: i is bigger than the allocated horizon (it should be lower than "
+                             f"{self.T} or equal to {self.T + 1})")
+        self._check_node(model)
+        if i == self.T + 1:
+            self._terminal, self.terminalData = model, model.createData()
+        else:
+            self._models[i] = model
+            self.runningDatas[i] = model.createData()
 
     def _limits_signature(self):
         return tuple((id(m), m._lim_version) for m in self._models)

@@ -87,3 +87,36 @@ def build(name, T=None, B=None, seed=None, drift_free=True):
     terminal = IntegratedActionModelEuler(dm, 0.0)
     x0s = rng.uniform(-1, 1, (B, 2 * d1))
     return x0s, [running] * T, terminal
+
+
+def build_hetero(name, T=None, B=None, seed=None, phase=10, impulse_every=7):
+    """Heterogeneous knot sequence at a config's dims (optional
+    variant; §8f #4): two parameter sets alternating every `phase` knots
+    (contact phases) and a control-free knot (nu = 0, impulse-like) at every
+    `impulse_every`-th running knot. Returns (x0s, running, terminal)."""
+    kind, d1, nu, T0, B0, dt = CONFIGS[name]
+    T = T0 if T is None else T
+    B = B0 if B is None else B
+    rng = np.random.default_rng(seed_of(name) + 77 if seed is None else seed)
+    if kind == "lqr":
+        A = lqr_models(d1, nu, B, rng)
+        Bm = lqr_models(d1, nu, B, rng)
+        Z = lqr_models(d1, 0, B, rng)
+        terminal = A
+        nx = d1
+    elif kind == "euler":
+        A = IntegratedActionModelEuler(difflqr_model(d1, nu, B, rng), dt)
+        Bm = IntegratedActionModelEuler(difflqr_model(d1, nu, B, rng), dt)
+        Z = IntegratedActionModelEuler(difflqr_model(d1, 0, B, rng), dt)
+        terminal = IntegratedActionModelEuler(A.differential, 0.0)
+        nx = 2 * d1
+    else:
+        raise ValueError("heterogeneous sequences are built for the LQR / Euler configs")
+    running = []
+    for t in range(T):
+        if impulse_every and t % impulse_every == impulse_every - 1:
+            running.append(Z)
+        else:
+            running.append(A if (t // phase) % 2 == 0 else Bm)
+    x0s = rng.uniform(-1, 1, (B, nx))
+    return x0s, running, terminal

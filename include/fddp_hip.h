@@ -132,6 +132,13 @@ const char* fddp_last_error(void);
  * (e.g. ActionModelLQR::set_Fx, lqr.hxx:128-136) for a live handle. */
 int fddp_set_model_params(fddp_handle* h, const double* params, int64_t n_params);
 
+/* Replace the knot sequence and the parameter pool of a live handle (same T,
+ * nx, B; every nu <= nu_max), keeping trajectories, gains and solver state.
+ * Replaces ShootingProblem::circularAppend / updateNode / updateModel
+ * (shooting.hxx:235-346): the caller rotates or swaps models on its side and
+ * uploads the new sequence; shared models are still one block. */
+int fddp_set_knots(fddp_handle* h, const fddp_knot_desc* knots, const double* params, int64_t n_params);
+
 /* x0 for every element: B*nx. Replaces ShootingProblem::set_x0 (shooting.hxx:391-397). */
 int fddp_set_x0(fddp_handle* h, const double* x0);
 int fddp_get_x0(fddp_handle* h, double* x0);

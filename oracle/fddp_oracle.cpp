@@ -634,6 +634,21 @@ struct Solver {
     haslim.assign(T, 0);
   }
 
+  // per-knot buffers after the model at knot t changed (fddp_set_knots):
+  // sized by the new nu as Eigen's resizing assignments leave them; k keeps
+  // its first entries (the box QP's warm start reads them)
+  void resize_knot(int t, int nut) {
+    const int ndx = P->ndx;
+    if (Quu[t].r == nut) return;
+    Qxu[t].resize(ndx, nut);
+    Quu[t].resize(nut, nut);
+    K[t].resize(nut, ndx);
+    FuTVxx[t].resize(nut, ndx);
+    Qu[t].assign(nut, 0.);
+    Quuk[t].assign(nut, 0.);
+    k[t].resize(nut, 0.);
+  }
+
   // solver-base.cpp:42-67 (xs_warm / us_warm may be null => zeros)
   void setCandidate(const double* xs_warm, const double* us_warm, bool feasible) {
     const int T = P->T, nx = P->nx, nu = P->nu_max;
@@ -1359,6 +1374,30 @@ int oracle_mpc_shift(oracle_handle* h) {
   return FDDP_OK;
 }
 
+
+// New knot sequence + parameter pool, same contract as fddp_set_knots:
+// models are rebound and their datas recreated (createData); solver state,
+// trajectories and gains are kept.
+int oracle_set_knots(oracle_handle* h, const fddp_knot_desc* knots, const double* params, int64_t n_params) {
+  const fddp_dims& D = h->dims;
+  h->knots.assign(knots, knots + D.T + 1);
+  h->params.assign(params, params + n_params);
+  for (int b = 0; b < D.B; ++b) {
+    Problem& P = h->problems[b];
+    for (int t = 0; t <= D.T; ++t) {
+      Model& m = P.models[t];
+      m.kind = knots[t].kind;
+      m.nu = knots[t].nu;
+    }
+  }
+  bind_models(h);
+  for (int b = 0; b < D.B; ++b) {
+    Problem& P = h->problems[b];
+    for (int t = 0; t <= D.T; ++t) createData(P.models[t], P.datas[t]);
+    for (int t = 0; t < D.T; ++t) h->solvers[b].resize_knot(t, knots[t].nu);
+  }
+  return FDDP_OK;
+}
 
 // SolverBoxFDDP / SolverFDDP selection (fddp_set_solver_kind).
 int oracle_set_solver_kind(oracle_handle* h, int kind) {
