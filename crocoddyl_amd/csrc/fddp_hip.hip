@@ -69,12 +69,68 @@ int64_t block_doubles(int kind, int nx, int nu) {
 }
 
 
+// Checks one FDDP_KNOT_EULER_FREEFWD block (layout in include/fddp_hip.h)
+// against nx / nu and the space left in the pool. Returns its size in doubles,
+// or -1 with `why` set. nj / nframe: joints and frame costs (LDS sizing).
+int64_t mb_block_check(const double* P, int64_t avail, int nx, int nu, std::string& why, int* nj_out,
+                       int* nframe_out) {
+  using namespace fddp::mb;
+  if (avail < FDDP_PARAM_HEADER) return why = "block out of range", -1;
+  const double dt = P[0];
+  const int nj = (int)P[1], ncost = (int)P[2];
+  const int64_t size = (int64_t)P[3];
+  if (!(dt >= 0.) || !std::isfinite(dt)) return why = "dt has positive value", -1;
+  if ((double)nj != P[1] || nj < 1 || nj > kMaxJ) return why = "number of joints out of [1, 32]", -1;
+  if (nx != 2 * nj) return why = "free-fwddyn knots need nx = 2 nv", -1;
+  if (nu != nj) return why = "ActuationModelFull needs nu = nv", -1;
+  if ((double)ncost != P[2] || ncost < 0) return why = "bad number of costs", -1;
+  if (size > avail || (double)size != P[3]) return why = "block out of range", -1;
+  int64_t o = FDDP_PARAM_HEADER + 3 + nj;
+  if (o + (int64_t)kJRec * nj > size) return why = "block too small for its joints", -1;
+  for (int i = 0; i < nj; ++i) {
+    const double* J = P + o + (int64_t)kJRec * i;
+    const int par = (int)J[0];
+    if ((double)par != J[0] || par < -1 || par >= i) return why = "joint parents must precede their children", -1;
+    const double an = std::sqrt(J[1] * J[1] + J[2] * J[2] + J[3] * J[3]);
+    if (!(std::fabs(an - 1.) < 1e-9)) return why = "joint axes must be unit vectors", -1;
+    if (!(J[16] >= 0.)) return why = "negative body mass", -1;
+  }
+  o += (int64_t)kJRec * nj;
+  int nframe = 0;
+  for (int k = 0; k < ncost; ++k) {
+    if (o + kCHdr > size) return why = "cost records out of range", -1;
+    const double* C = P + o;
+    const int type = (int)C[0];
+    const int64_t rs = (int64_t)C[3];
+    int64_t want = -1;
+    if (type == C_STATE) want = kCHdr + 2 * nx;
+    if (type == C_CONTROL) want = kCHdr + 2 * nu;
+    if (type == C_FRAME_PLACEMENT) want = kCHdr + 31;
+    if (type == C_FRAME_TRANSLATION) want = kCHdr + 19;
+    if (want < 0) return why = "unknown cost type " + std::to_string(type), -1;
+    if (rs != want || o + rs > size) return why = "cost record of the wrong size", -1;
+    if (type == C_FRAME_PLACEMENT || type == C_FRAME_TRANSLATION) {
+      const int fj = (int)C[kCHdr];
+      if ((double)fj != C[kCHdr] || fj < 0 || fj >= nj) return why = "frame attached to an unknown joint", -1;
+      ++nframe;
+    }
+    o += rs;
+  }
+  if (o != size) return why = "block size does not match its records", -1;
+  if (nframe > kMaxFrameCosts) return why = "more than 8 frame costs in one knot", -1;
+  if (diff_layout(nj, nframe).total * 8 > 160 * 1024) return why = "too many joints for the calcDiff LDS plan", -1;
+  if (nj_out) *nj_out = std::max(*nj_out, nj);
+  if (nframe_out) *nframe_out = std::max(*nframe_out, nframe);
+  return size;
+}
+
 // Validation of a knot sequence against the handle's dims (fddp_create,
-// fddp_set_knots). exact_nu_max: the running knots' max nu must equal
-// nu_max (creation); otherwise it may be smaller (the reference's
-// circularAppend / updateNode checks, shooting.hxx:249-252).
-int check_knots(const fddp_dims& d, const fddp_knot_desc* knots, int64_t n_params, const char* who,
-                bool exact_nu_max) {
+// fddp_set_knots, fddp_set_model_params). exact_nu_max: the running knots' max
+// nu must equal nu_max (creation); otherwise it may be smaller (the
+// reference's circularAppend / updateNode checks, shooting.hxx:249-252).
+// Multibody blocks are checked for every batch element they cover.
+int check_knots(const fddp_dims& d, const fddp_knot_desc* knots, const double* params, int64_t n_params,
+                const char* who, bool exact_nu_max) {
   const std::string w(who);
   int nu_max = 0;
   for (int t = 0; t <= d.T; ++t) {
@@ -85,10 +141,27 @@ int check_knots(const fddp_dims& d, const fddp_knot_desc* knots, int64_t n_param
       return fail(FDDP_ERR_INVALID_ARG, w + ": unicycle knots need nx=3, nu=2");
     if (k.kind == FDDP_KNOT_EULER_DIFFLQR && (d.nx % 2))
       return fail(FDDP_ERR_INVALID_ARG, w + ": Euler(DiffLQR) knots need an even nx");
-    const int64_t sz = block_doubles(k.kind, d.nx, k.nu);
+    if (k.param_offset < 0 || k.param_stride < 0 || k.param_offset + (int64_t)(d.B - 1) * k.param_stride >= n_params)
+      return fail(FDDP_ERR_INVALID_ARG, w + ": knot " + std::to_string(t) + " parameter block out of range");
+    int64_t sz;
+    if (k.kind == FDDP_KNOT_EULER_FREEFWD) {
+      if (!params) return fail(FDDP_ERR_INVALID_ARG, w + ": null parameter pool");
+      sz = 0;
+      const int nb = k.param_stride > 0 ? d.B : 1;
+      for (int b = 0; b < nb; ++b) {
+        const int64_t off = k.param_offset + (int64_t)b * k.param_stride;
+        std::string why;
+        const int64_t s1 = mb_block_check(params + off, n_params - off, d.nx, k.nu, why, nullptr, nullptr);
+        if (s1 < 0) return fail(FDDP_ERR_INVALID_ARG, w + ": knot " + std::to_string(t) + ": " + why);
+        if (k.param_stride > 0 && s1 > k.param_stride)
+          return fail(FDDP_ERR_INVALID_ARG, w + ": knot " + std::to_string(t) + " blocks overlap (stride too small)");
+        sz = std::max(sz, s1);
+      }
+    } else {
+      sz = block_doubles(k.kind, d.nx, k.nu);
+    }
     if (sz < 0) return fail(FDDP_ERR_UNSUPPORTED, w + ": unknown knot kind " + std::to_string(k.kind));
-    if (k.param_offset < 0 || k.param_stride < 0 ||
-        k.param_offset + (int64_t)(d.B - 1) * k.param_stride + sz > n_params)
+    if (k.param_offset + (int64_t)(d.B - 1) * k.param_stride + sz > n_params)
       return fail(FDDP_ERR_INVALID_ARG, w + ": knot " + std::to_string(t) + " parameter block out of range");
   }
   if (exact_nu_max ? nu_max != d.nu_max : nu_max > d.nu_max)
@@ -127,6 +200,8 @@ struct fddp_handle_s {
   bool fast = false;  // dense-knot fast path (fast_path.hpp) for calc / calcDiff / forward
   size_t fused_smem = 0, fwd_fast_smem = 0;
   int64_t pcap = 0;  // doubles of LDS reserved for a resident parameter block
+  bool has_mb = false;     // multibody knots present (mb_calc_diff_kernel)
+  size_t mb_diff_smem = 0; // its dynamic LDS
   int bwd_variant = 0;  // 0 generic, else (NTL*10+MTL)*10+waves of the MFMA sweep
   // timing
   bool timing = false;
@@ -245,6 +320,10 @@ int launch_calc_diff(fddp_handle* h, int sel, int gaps) {
   if (h->fast) return launch_fused(h, -1, sel, gaps);
   Timed tm(h, 1);
   const Dev& D = h->D;
+  if (h->has_mb) {  // multibody knots: one workgroup per knot, before the gaps pass
+    hipLaunchKernelGGL(mb_calc_diff_kernel, dim3(D.T + 1, D.B), dim3(64), h->mb_diff_smem, h->stream, D, sel);
+    LAUNCH_CHECK();
+  }
   hipLaunchKernelGGL(calc_diff_kernel<kNT>, dim3(D.B), dim3(kNT), h->cdiff_smem, h->stream, D, sel, gaps, h->pcap);
   LAUNCH_CHECK();
   return FDDP_OK;
@@ -414,12 +493,31 @@ int apply_knots(fddp_handle* h, const fddp_knot_desc* knots, const double* param
   h->knots.assign(knots, knots + K1);
   {
     int64_t pmax = 0;
-    for (int t = 0; t <= d.T; ++t) pmax = std::max<int64_t>(pmax, block_doubles(knots[t].kind, d.nx, knots[t].nu));
-    const int64_t budget = (150 * 1024) / 8 - (2 * D.sX + D.sM + 5 * (kNT / kWave) + 16);
+    int mb_nj = 0, mb_nframe = 0;
+    h->has_mb = false;
+    for (int t = 0; t <= d.T; ++t) {
+      int64_t sz;
+      if (knots[t].kind == FDDP_KNOT_EULER_FREEFWD) {
+        h->has_mb = true;
+        sz = 0;
+        const int nb = knots[t].param_stride > 0 ? d.B : 1;
+        for (int b = 0; b < nb; ++b) {  // validated by check_knots
+          const int64_t off = knots[t].param_offset + (int64_t)b * knots[t].param_stride;
+          std::string why;
+          sz = std::max(sz, mb_block_check(params + off, n_params - off, d.nx, knots[t].nu, why, &mb_nj, &mb_nframe));
+        }
+      } else {
+        sz = block_doubles(knots[t].kind, d.nx, knots[t].nu);
+      }
+      pmax = std::max<int64_t>(pmax, sz);
+    }
+    D.mbw = h->has_mb ? pad2(fddp::mb::calc_work_doubles(mb_nj)) : 0;
+    h->mb_diff_smem = h->has_mb ? sizeof(double) * fddp::mb::diff_layout(mb_nj, mb_nframe).total : 0;
+    const int64_t budget = (150 * 1024) / 8 - (2 * D.sX + D.sM + 5 * (kNT / kWave) + 16) - D.mbw;
     h->pcap = pmax <= budget ? pad2(pmax) : 0;
   }
-  h->fwd_smem = sizeof(double) * (h->pcap + fwd_lds_doubles<kNT, false>(D.sX, D.sN, D.sM));
-  h->calc_smem = sizeof(double) * (h->pcap + 2 * D.sX + D.sM + 5 * (kNT / kWave) + 16);
+  h->fwd_smem = sizeof(double) * (h->pcap + fwd_lds_doubles<kNT, false>(D.sX, D.sN, D.sM) + D.mbw);
+  h->calc_smem = sizeof(double) * (h->pcap + 2 * D.sX + D.sM + 5 * (kNT / kWave) + 16 + D.mbw);
   h->cdiff_smem = sizeof(double) * (h->pcap + D.sX + D.sM);
   {  // dense-knot fast path: every knot LQR / Euler∘DiffLQR, block LDS-resident
     bool dense = h->pcap > 0 && d.nx == d.ndx && d.nx <= kNT && d.nu_max <= kNT;
@@ -473,7 +571,9 @@ int apply_knots(fddp_handle* h, const fddp_knot_desc* knots, const double* param
       hipFuncSetAttribute((const void*)calc_kernel<kNT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)h->calc_smem) != hipSuccess ||
       hipFuncSetAttribute((const void*)calc_diff_kernel<kNT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)h->cdiff_smem) != hipSuccess)
+                          (int)h->cdiff_smem) != hipSuccess ||
+      (h->has_mb && hipFuncSetAttribute((const void*)mb_calc_diff_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        (int)h->mb_diff_smem) != hipSuccess))
     return fail(FDDP_ERR_RUNTIME, "hipFuncSetAttribute(dynamic LDS)");
   {  // backward sweep variant: MFMA tiles when every running knot has nu == nu_max
     bool uniform_nu = d.nu_max > 0;
@@ -508,7 +608,7 @@ int fddp_create(const fddp_dims* dims, const fddp_knot_desc* knots, const double
   if (d.nx != d.ndx) return fail(FDDP_ERR_UNSUPPORTED, "fddp_create: only Euclidean states (nx == ndx) are supported");
   if (d.B > 65535) return fail(FDDP_ERR_INVALID_ARG, "fddp_create: B > 65535 per handle");
   {
-    const int rc0 = check_knots(d, knots, n_params, "fddp_create", true);
+    const int rc0 = check_knots(d, knots, params, n_params, "fddp_create", true);
     if (rc0) return rc0;
   }
 
@@ -665,6 +765,13 @@ void fddp_destroy(fddp_handle* h) {
 int fddp_set_model_params(fddp_handle* h, const double* params, int64_t n_params) {
   if (!h || !params || n_params != h->n_params) return fail(FDDP_ERR_INVALID_ARG, "fddp_set_model_params: size");
   DeviceGuard g(h->device);
+  if (h->has_mb) {  // variable-size multibody blocks: re-validate and re-plan the LDS
+    int rc;
+    if ((rc = check_knots(h->dims, h->knots.data(), params, n_params, "fddp_set_model_params", false))) return rc;
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    const std::vector<fddp_knot_desc> kn = h->knots;
+    return apply_knots(h, kn.data(), params, n_params);
+  }
   HIP_TRY(hipMemcpyAsync((void*)h->D.params, params, sizeof(double) * n_params, hipMemcpyHostToDevice, h->stream));
   HIP_TRY(hipStreamSynchronize(h->stream));
   return FDDP_OK;
@@ -992,7 +1099,7 @@ int fddp_get_quantity(fddp_handle* h, int which, double* out) {
 int fddp_set_knots(fddp_handle* h, const fddp_knot_desc* knots, const double* params, int64_t n_params) {
   if (!h || !knots || !params) return fail(FDDP_ERR_INVALID_ARG, "fddp_set_knots: null argument");
   int rc;
-  if ((rc = check_knots(h->dims, knots, n_params, "fddp_set_knots", false))) return rc;
+  if ((rc = check_knots(h->dims, knots, params, n_params, "fddp_set_knots", false))) return rc;
   DeviceGuard g(h->device);
   HIP_TRY(hipStreamSynchronize(h->stream));  // no launch may still read the old knots
   return apply_knots(h, knots, params, n_params);

@@ -9,8 +9,10 @@
 
 namespace fddp {
 
-// Doubles in a knot's parameter block (layouts in include/fddp_hip.h).
-__device__ inline int64_t block_doubles_dev(int kind, int nx, int nu) {
+// Doubles in a knot's parameter block (layouts in include/fddp_hip.h); the
+// multibody block carries its size in its header (g: the block).
+__device__ inline int64_t block_doubles_dev(int kind, int nx, int nu, const double* g = nullptr) {
+  if (kind == FDDP_KNOT_EULER_FREEFWD) return (int64_t)g[3];
   if (kind == FDDP_KNOT_LQR) return FDDP_PARAM_HEADER + 2LL * nx * nx + 2LL * nx * nu + (int64_t)nu * nu + 2LL * nx + nu;
   if (kind == FDDP_KNOT_UNICYCLE) return FDDP_PARAM_HEADER;
   const int64_t nq = nx / 2;
@@ -97,11 +99,12 @@ __global__ __launch_bounds__(NT) void calc_kernel(Dev D, int sel, int64_t pcap) 
   double* u = x + D.sX;          // sM
   double* xn = u + D.sM;         // sX
   double* red = xn + D.sX;       // 5*NT/64
+  double* mbw = red + 5 * (NT / kWave) + 16;  // multibody calc scratch (D.mbw)
   const int c = s.cur;
   const double* cached = nullptr;
   for (int t = 0; t <= D.T; ++t) {
     const fddp_knot_desc kd = D.knots[t];
-    const double* P = stage_params<NT>(D.pblock(b, t), block_doubles_dev(kd.kind, D.nx, kd.nu), pl, pcap, cached);
+    const double* P = stage_params<NT>(D.pblock(b, t), block_doubles_dev(kd.kind, D.nx, kd.nu, D.pblock(b, t)), pl, pcap, cached);
     const double* xg = D.xs[c] + D.knot(b, t) * D.sX;
     for (int i = threadIdx.x; i < D.nx; i += NT) x[i] = xg[i];
     const bool running = t < D.T;
@@ -110,7 +113,7 @@ __global__ __launch_bounds__(NT) void calc_kernel(Dev D, int sel, int64_t pcap) 
       for (int i = threadIdx.x; i < D.m; i += NT) u[i] = ug[i];
     }
     __syncthreads();
-    const double cost = knot_calc<NT>(kd, P, D.nx, x, u, running, xn, red);
+    const double cost = knot_calc<NT>(kd, P, D.nx, x, u, running, xn, red, mbw);
     if (running) {
       double* xo = D.xnext[c] + D.run(b, t) * D.sX;
       for (int i = threadIdx.x; i < D.nx; i += NT) xo[i] = xn[i];
@@ -153,7 +156,7 @@ __global__ __launch_bounds__(NT) void calc_diff_kernel(Dev D, int sel, int gaps,
   const double* cached = nullptr;
   for (int t = 0; t <= D.T; ++t) {
     const fddp_knot_desc kd = D.knots[t];
-    const double* P = stage_params<NT>(D.pblock(b, t), block_doubles_dev(kd.kind, D.nx, kd.nu), pl, pcap, cached);
+    const double* P = stage_params<NT>(D.pblock(b, t), block_doubles_dev(kd.kind, D.nx, kd.nu, D.pblock(b, t)), pl, pcap, cached);
     const int64_t kk = D.knot(b, t);
     const double* xg = D.xs[c] + kk * D.sX;
     for (int i = threadIdx.x; i < D.nx; i += NT) x[i] = xg[i];
@@ -193,6 +196,26 @@ __global__ __launch_bounds__(NT) void calc_diff_kernel(Dev D, int sel, int gaps,
     }
     __syncthreads();
   }
+}
+
+// Multibody knots' calcDiff (multibody.hpp): one 64-thread workgroup per
+// (knot t = blockIdx.x, element b = blockIdx.y); knots of other kinds return.
+// The gaps of these knots are written by calc_diff_kernel as for any knot.
+__global__ __launch_bounds__(64) void mb_calc_diff_kernel(Dev D, int sel) {
+  const int t = blockIdx.x, b = blockIdx.y;
+  const fddp_knot_desc kd = D.knots[t];
+  if (kd.kind != FDDP_KNOT_EULER_FREEFWD) return;
+  const ElemState s = D.st[b];
+  if (!selected(s, sel)) return;
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  const int c = s.cur;
+  const int64_t kk = D.knot(b, t);
+  const bool running = t < D.T;
+  const double* xg = D.xs[c] + kk * D.sX;
+  const double* ug = running ? D.us[c] + D.run(b, t) * D.sM : nullptr;
+  mb::knot_calc_diff(D.pblock(b, t), D.nx, D.m, xg, ug, running && kd.nu > 0, sm, D.Fx + kk * D.sNN,
+                     D.Fu + kk * D.sNM, D.Lxx + kk * D.sNN, D.Lxu + kk * D.sNM, D.Luu + kk * D.sMM, D.Lx + kk * D.sN,
+                     D.Lu + kk * D.sM);
 }
 
 // ---------------------------------------------------------------------------
@@ -558,7 +581,7 @@ __global__ __launch_bounds__(NT) void backward_kernel(Dev D, Prm prm, int mode) 
 template <int NT>
 __device__ __forceinline__ bool fwd_trial(const Dev& D, int b, const ElemState& s, double alpha, double* xv, double* uv, double* xn,
                           double* red, int* flag, double& cost_try, double& dv, double* pl, int64_t pcap,
-                          const double*& cached) {
+                          const double*& cached, double* mbw) {
   const int n = D.n, nx = D.nx, m = D.m, T = D.T, tid = threadIdx.x;
   const int c = s.cur, o = 1 - c;
   const bool feas = s.is_feasible != 0;
@@ -584,7 +607,7 @@ __device__ __forceinline__ bool fwd_trial(const Dev& D, int b, const ElemState& 
     __syncthreads();
     const bool running = t < T;
     const fddp_knot_desc kd = D.knots[t];
-    const double* P = stage_params<NT>(D.pblock(b, t), block_doubles_dev(kd.kind, nx, kd.nu), pl, pcap, cached);
+    const double* P = stage_params<NT>(D.pblock(b, t), block_doubles_dev(kd.kind, nx, kd.nu, D.pblock(b, t)), pl, pcap, cached);
     if (running) {
       const int nu = kd.nu;
       const double* us = D.us[c] + D.run(b, t) * D.sM;
@@ -606,7 +629,7 @@ __device__ __forceinline__ bool fwd_trial(const Dev& D, int b, const ElemState& 
       }
       __syncthreads();
     }
-    const double ct = knot_calc<NT>(kd, P, nx, xv, uv, running, xn, red);
+    const double ct = knot_calc<NT>(kd, P, nx, xv, uv, running, xn, red, mbw);
     bool bad = false;
     if (running) {
       double* xo = D.xnext[o] + D.run(b, t) * D.sX;
@@ -647,7 +670,7 @@ __device__ __forceinline__ bool fwd_trial_fast(const Dev& D, int b, const ElemSt
                                                const double*& cached);
 
 // Forward-pass LDS beyond the parameter block (doubles): generic trial
-// [xv sX | uv sM | xn sX | red 5*NW+8 | flag], fast trial
+// [xv sX | uv sM | xn sX | red 5*NW+8 | flag | multibody scratch D.mbw], fast trial
 // [xu sX+sM | dxv sN | xn sX | pa NT | pdyn NT | red 24 | flag].
 template <int NT, bool FAST>
 __host__ __device__ inline int64_t fwd_lds_doubles(int64_t sX, int64_t sN, int64_t sM) {
@@ -686,7 +709,7 @@ __global__ __launch_bounds__(NT) void forward_kernel(Dev D, Prm prm, int mode, d
     if constexpr (FAST)
       return fwd_trial_fast<NT, true>(D, b, s, alpha, xv, dxv, xn, pa, pdyn, red, flag, ct, dv, pl, pcap, cached);
     else
-      return fwd_trial<NT>(D, b, s, alpha, xv, uv, xn, red, flag, ct, dv, pl, pcap, cached);
+      return fwd_trial<NT>(D, b, s, alpha, xv, uv, xn, red, flag, ct, dv, pl, pcap, cached, (double*)flag + 2);
   };
   if (mode == 1) {
     double ct, dv;

@@ -7,6 +7,7 @@
 //              include/crocoddyl/core/actions/diff-lqr.hxx:34-79 (Euclidean state,
 //              so JintegrateTransport is a no-op and Jintegrate adds I,
 //              core/states/euclidean.hxx:74-147).
+//   Euler∘FreeFwdDynamics  multibody.hpp (multibody/actions/free-fwddyn.hxx)
 // Parameter-block layouts are declared in include/fddp_hip.h.
 //
 // Threads split the rows of every matrix-vector product (column-major blocks:
@@ -15,6 +16,7 @@
 #pragma once
 
 #include "fddp_device.hpp"
+#include "multibody.hpp"
 
 namespace fddp {
 
@@ -89,12 +91,14 @@ __device__ inline double lq_cost_total(const double (&t)[5]) {
 // model->calc(data, x, u) (use_u) or model->calc(data, x) with unone_ = 0
 // (action-base.hxx:28-31). x, u: readable by every thread (LDS or global).
 // Writes xnext[0..nx) and returns the knot cost in every thread.
-// `red`: LDS scratch of >= 5*NT/64 doubles. Contains barriers: call uniformly.
+// `red`: LDS scratch of >= 5*NT/64 doubles; `mbw`: LDS scratch of
+// mb::calc_work_doubles(nj) for multibody knots. Contains barriers: call uniformly.
 template <int NT>
 __device__ __forceinline__ double knot_calc(const fddp_knot_desc& kd, const double* P, int nx, const double* x, const double* u,
-                            bool use_u, double* xnext, double* red) {
+                            bool use_u, double* xnext, double* red, double* mbw) {
   const int nu = kd.nu;
   use_u = use_u && nu > 0;
+  if (kd.kind == FDDP_KNOT_EULER_FREEFWD) return mb::knot_calc<NT>(P, nx, x, u, use_u, xnext, mbw);
   double t[5] = {0., 0., 0., 0., 0.};
   if (kd.kind == FDDP_KNOT_LQR) {
     LQRBlk Pm(P, nx, nu);
@@ -158,6 +162,8 @@ struct KnotDiffOut {
 
 // model->calcDiff(data, x, u) / calcDiff(data, x). Writes full blocks (entries
 // beyond the knot's nu are zero); Luu has leading dimension m = nu_max.
+// Multibody knots are differentiated by mb_calc_diff_kernel (one workgroup
+// per knot) instead.
 template <int NT>
 __device__ __forceinline__ void knot_calc_diff(const fddp_knot_desc& kd, const double* P, int nx, int m, const double* x,
                                const double* u, bool use_u, const KnotDiffOut& o) {
@@ -165,6 +171,7 @@ __device__ __forceinline__ void knot_calc_diff(const fddp_knot_desc& kd, const d
   const int nu = kd.nu;
   use_u = use_u && nu > 0;
   const int tid = threadIdx.x;
+  if (kd.kind == FDDP_KNOT_EULER_FREEFWD) return;
   if (kd.kind == FDDP_KNOT_LQR) {  // lqr.hxx:51-70
     LQRBlk Pm(P, nx, nu);
     for (int i = tid; i < n; i += NT) {

@@ -280,25 +280,46 @@ class DifferentialActionModelLQR(_ControlLimits):
 
 class IntegratedActionModelEuler(ActionModelAbstract):
     """IntegratedActionModelEuler (core/integrator/euler.hxx:16-35) around a
-    DifferentialActionModelLQR (the device-covered differential model)."""
+    device-covered differential model: DifferentialActionModelLQR, or
+    DifferentialActionModelFreeFwdDynamics (crocoddyl_amd.multibody)."""
 
     kind = _abi.KNOT_EULER_DIFFLQR
 
     def __init__(self, diffModel, stepTime=1e-3, withCostResidual=True):
-        if not isinstance(diffModel, DifferentialActionModelLQR):
+        from .multibody import DifferentialActionModelFreeFwdDynamics
+        self._mb = isinstance(diffModel, DifferentialActionModelFreeFwdDynamics)
+        if not (self._mb or isinstance(diffModel, DifferentialActionModelLQR)):
             raise NotImplementedError("crocoddyl_amd: the device path covers Euler(DifferentialActionModelLQR) "
-                                      f"knots only; got {type(diffModel).__name__}")
+                                      "and Euler(DifferentialActionModelFreeFwdDynamics) knots only; got "
+                                      f"{type(diffModel).__name__}")
+        if self._mb:
+            self.kind = _abi.KNOT_EULER_FREEFWD
         super().__init__(diffModel.state, diffModel.nu, diffModel.nr)
         # the integrated model copies the differential model's limits (euler.hxx:25-26)
         self.u_lb = diffModel.u_lb
         self.u_ub = diffModel.u_ub
         self.differential = diffModel
-        diffModel._owners.append(self)
+        if not self._mb:
+            diffModel._owners.append(self)
         self.withCostResidual = bool(withCostResidual)
         dt = float(stepTime)
         if dt < 0.0:  # euler.hxx:27-31
             dt = 1e-3
         self._dt = dt
+
+    # the multibody DAM's parameters (robot, costs, armature) are part of the
+    # version the problem compares before re-uploading parameter blocks
+    @property
+    def _version(self):
+        own = self.__dict__.get("_own_version", 0)
+        return (own, self.differential.version()) if self.__dict__.get("_mb") else own
+
+    @_version.setter
+    def _version(self, v):
+        self.__dict__["_own_version"] = v if not isinstance(v, tuple) else v[0]
+
+    def _touch(self):
+        self.__dict__["_own_version"] = self.__dict__.get("_own_version", 0) + 1
 
     @property
     def dt(self):
@@ -313,6 +334,8 @@ class IntegratedActionModelEuler(ActionModelAbstract):
 
     def pack(self):
         d = self.differential
+        if self._mb:
+            return self.kind, d.nu, d.pack_body(self._dt)
         nq, nu, nx = d.nq, d.nu, d.state.nx
         parts = [_colmajor(d._Fq, nq, nq, "Fq"), _colmajor(d._Fv, nq, nq, "Fv"), _colmajor(d._Fu, nq, nu, "Fu"),
                  _vec(d._f0, nq, "f0"), _colmajor(d._Lxx, nx, nx, "Lxx"), _colmajor(d._Lxu, nx, nu, "Lxu"),

@@ -1,0 +1,504 @@
+"""Multibody knot models with the reference's Python API, as parameter carriers.
+
+The device computes these knots (crocoddyl_amd/csrc/multibody.hpp); the
+classes here hold the parameters, validate them like the reference, and pack
+the FDDP_KNOT_EULER_FREEFWD parameter block declared in include/fddp_hip.h.
+
+Reference API mirrored:
+  StateMultibody(model)                         multibody/states/multibody.hxx
+  ActuationModelFull(state)                     multibody/actuations/full.hpp
+  ActivationModelQuad(nr), ActivationModelWeightedQuad(weights)
+                                                core/activations/{quadratic,weighted-quadratic}.hpp
+  CostModelSum(state, nu).addCost(name, cost, weight)   multibody/costs/cost-sum.hxx:18-85
+  CostModelState / CostModelControl / CostModelFramePlacement / CostModelFrameTranslation
+                                                multibody/costs/{state,control,frame-placement,frame-translation}.hxx
+  FramePlacement(id, SE3), FrameTranslation(id, p)      multibody/frames.hpp
+  DifferentialActionModelFreeFwdDynamics(state, actuation, costs)  .armature
+                                                multibody/actions/free-fwddyn.hxx:24-160
+Pinocchio is not available offline, so ``RobotModel`` stands in for
+``pinocchio.Model`` over the subset the device covers: a fixed-base
+kinematic tree of revolute joints (any unit axis), with joint placements,
+body inertias, operational frames and gravity. Joint and frame indices
+follow Pinocchio's (joint 0 / frame 0 = universe).
+"""
+import numpy as np
+
+from . import _abi
+
+JOINT_REC = 26
+COST_HDR = 4
+COST_STATE, COST_CONTROL, COST_FRAME_PLACEMENT, COST_FRAME_TRANSLATION = 1, 2, 3, 4
+MAX_JOINTS = 32
+
+
+class SE3:
+    """pinocchio.SE3 subset: rotation (3x3), translation (3)."""
+
+    def __init__(self, rotation=None, translation=None):
+        self.rotation = np.eye(3) if rotation is None else np.array(rotation, dtype=np.float64).reshape(3, 3)
+        self.translation = np.zeros(3) if translation is None else np.array(translation, np.float64).reshape(3)
+
+    @staticmethod
+    def Identity():
+        return SE3()
+
+    def inverse(self):
+        Rt = self.rotation.T
+        return SE3(Rt, -Rt @ self.translation)
+
+    def __mul__(self, o):
+        return SE3(self.rotation @ o.rotation, self.translation + self.rotation @ o.translation)
+
+    def __repr__(self):
+        return f"SE3(R={self.rotation.tolist()}, p={self.translation.tolist()})"
+
+
+class Inertia:
+    """pinocchio.Inertia: mass, lever (CoM in the joint frame), rotational
+    inertia about the CoM (3x3 symmetric)."""
+
+    def __init__(self, mass, lever, inertia):
+        self.mass = float(mass)
+        self.lever = np.array(lever, np.float64).reshape(3)
+        I = np.array(inertia, np.float64).reshape(3, 3)
+        if not np.allclose(I, I.T):
+            raise ValueError("Invalid argument: the rotational inertia must be symmetric")
+        self.inertia = I
+
+    @staticmethod
+    def Zero():
+        return Inertia(0.0, np.zeros(3), np.zeros((3, 3)))
+
+    def se3Action(self, M):
+        """Inertia expressed in the frame M maps to (pinocchio Inertia::se3Action)."""
+        return Inertia(self.mass, M.rotation @ self.lever + M.translation,
+                       M.rotation @ self.inertia @ M.rotation.T)
+
+    def __add__(self, o):
+        """Sum of two inertias in the same frame (pinocchio Inertia::operator+)."""
+        m = self.mass + o.mass
+        if m == 0:
+            return Inertia.Zero()
+        c = (self.mass * self.lever + o.mass * o.lever) / m
+        def shift(I, mi, ci):
+            d = ci - c
+            return I + mi * (np.dot(d, d) * np.eye(3) - np.outer(d, d))
+        return Inertia(m, c, shift(self.inertia, self.mass, self.lever) + shift(o.inertia, o.mass, o.lever))
+
+
+class RobotModel:
+    """Stand-in for pinocchio.Model over fixed-base revolute trees."""
+
+    def __init__(self):
+        self.names = ["universe"]
+        self.parents = [0]
+        self.axes = [np.zeros(3)]
+        self.jointPlacements = [SE3()]
+        self.inertias = [Inertia.Zero()]
+        self.frames = [("universe", 0, SE3())]
+        self.gravity = np.array([0.0, 0.0, -9.81])  # pinocchio Model::gravity981
+        self._version = 0
+
+    @property
+    def njoints(self):
+        return len(self.names)
+
+    @property
+    def nq(self):
+        return self.njoints - 1
+
+    nv = nq
+
+    def addJoint(self, parent_id, axis, placement, name):
+        """Revolute joint about the unit ``axis`` (joint frame), placed at
+        ``placement`` in the parent joint's frame. Returns its index."""
+        parent_id = int(parent_id)
+        if not 0 <= parent_id < self.njoints:
+            raise ValueError("Invalid argument: unknown parent joint")
+        if self.nq >= MAX_JOINTS:
+            raise ValueError(f"Invalid argument: the device path holds at most {MAX_JOINTS} joints")
+        ax = np.array(axis, np.float64).reshape(3)
+        nrm = np.linalg.norm(ax)
+        if nrm == 0:
+            raise ValueError("Invalid argument: zero joint axis")
+        self.names.append(str(name))
+        self.parents.append(parent_id)
+        self.axes.append(ax / nrm)
+        self.jointPlacements.append(placement if placement is not None else SE3())
+        self.inertias.append(Inertia.Zero())
+        self._version += 1
+        return self.njoints - 1
+
+    def appendBodyToJoint(self, joint_id, inertia, placement=None):
+        """pinocchio Model::appendBodyToJoint: add a body (inertia given in
+        the body frame ``placement`` relative to the joint)."""
+        M = placement if placement is not None else SE3()
+        self.inertias[joint_id] = self.inertias[joint_id] + inertia.se3Action(M)
+        self._version += 1
+
+    def addFrame(self, name, parent_joint, placement=None):
+        self.frames.append((str(name), int(parent_joint), placement if placement is not None else SE3()))
+        self._version += 1
+        return len(self.frames) - 1
+
+    def getFrameId(self, name):
+        for i, f in enumerate(self.frames):
+            if f[0] == name:
+                return i
+        raise ValueError(f"Invalid argument: unknown frame {name}")
+
+    def existFrame(self, name):
+        return any(f[0] == name for f in self.frames)
+
+    def pack_robot(self, armature):
+        """gravity(3) armature(nv) then one 26-double record per joint."""
+        nv = self.nv
+        rows = [self.gravity, np.asarray(armature, float).reshape(nv)]
+        for j in range(1, self.njoints):
+            P = self.jointPlacements[j]
+            I = self.inertias[j]
+            Ic = I.inertia
+            rows.append(np.concatenate([[self.parents[j] - 1], self.axes[j], P.rotation.T.reshape(-1),
+                                        P.translation, [I.mass], I.lever,
+                                        [Ic[0, 0], Ic[1, 1], Ic[2, 2], Ic[0, 1], Ic[0, 2], Ic[1, 2]]]))
+        return np.concatenate(rows)
+
+
+def sample_talos_arm():
+    """A 7-DoF arm with the kinematic layout and mass distribution of a
+    humanoid (Talos-class) left arm: shoulder yaw/roll/pitch, elbow, forearm
+    twist, wrist pitch/roll, and a ``gripper_left_joint`` frame 0.1 m past
+    the wrist. Synthetic stand-in: example-robot-data's URDF is absent
+    offline (benchmark/factory/arm.hpp:47-56 loads talos_left_arm.urdf)."""
+    m = RobotModel()
+    specs = [  # (axis, placement translation, mass, lever, diag inertia)
+        ((0, 0, 1), (0.0, 0.157, 0.232), 2.71, (-0.002, 0.04, 0.0), (0.012, 0.004, 0.011)),
+        ((1, 0, 0), (0.0, 0.0, 0.0), 1.51, (0.01, 0.0, -0.06), (0.008, 0.008, 0.002)),
+        ((0, 0, 1), (0.0, 0.0, -0.0), 1.43, (0.0, 0.0, -0.15), (0.012, 0.012, 0.002)),
+        ((0, 1, 0), (0.02, 0.0, -0.273), 1.02, (-0.01, 0.0, -0.05), (0.004, 0.004, 0.001)),
+        ((0, 0, 1), (-0.02, 0.0, -0.1), 1.12, (0.0, 0.0, -0.08), (0.006, 0.006, 0.001)),
+        ((1, 0, 0), (0.0, 0.0, -0.164), 0.52, (0.0, 0.0, -0.01), (0.0005, 0.0005, 0.0003)),
+        ((0, 1, 0), (0.0, 0.0, 0.0), 0.40, (0.0, 0.0, -0.05), (0.0004, 0.0004, 0.0002)),
+    ]
+    parent = 0
+    for k, (ax, p, mass, c, d) in enumerate(specs):
+        j = m.addJoint(parent, ax, SE3(np.eye(3), p), f"arm_left_{k + 1}_joint")
+        m.appendBodyToJoint(j, Inertia(mass, c, np.diag(d)))
+        parent = j
+    m.addFrame("gripper_left_joint", parent, SE3(np.eye(3), (0.0, 0.0, -0.1)))
+    return m
+
+
+def sample_tree(nj, seed=0, branching=True):
+    """Random kinematic tree (tests): random axes, placements and inertias."""
+    rng = np.random.default_rng(seed)
+    m = RobotModel()
+    for j in range(1, nj + 1):
+        parent = int(rng.integers(0, j)) if branching else j - 1
+        ax = rng.normal(size=3)
+        ang = rng.normal(size=3) * 0.5
+        t = np.linalg.norm(ang)
+        K = np.array([[0, -ang[2], ang[1]], [ang[2], 0, -ang[0]], [-ang[1], ang[0], 0]])
+        R = np.eye(3) + np.sin(t) / t * K + (1 - np.cos(t)) / t ** 2 * K @ K
+        jid = m.addJoint(parent, ax, SE3(R, rng.uniform(-0.3, 0.3, 3)), f"j{j}")
+        A = rng.normal(size=(3, 3)) * 0.05
+        m.appendBodyToJoint(jid, Inertia(rng.uniform(0.3, 3.0), rng.uniform(-0.1, 0.1, 3),
+                                         A @ A.T + 0.01 * np.eye(3)))
+    m.addFrame("tip", nj, SE3(np.eye(3), (0.0, 0.0, -0.1)))
+    return m
+
+
+class StateMultibody:
+    """StateMultibody over a revolute-only model: q and v spaces coincide,
+    so diff / integrate are Euclidean (multibody.hxx:54-91 with Pinocchio's
+    revolute difference / integrate)."""
+
+    def __init__(self, model):
+        if not isinstance(model, RobotModel):
+            raise TypeError("StateMultibody needs a crocoddyl_amd.multibody.RobotModel")
+        self.pinocchio = model
+        self.nq = model.nq
+        self.nv = model.nv
+        self.nx = self.nq + self.nv
+        self.ndx = 2 * self.nv
+
+    def zero(self):
+        return np.zeros(self.nx)
+
+    def rand(self):
+        return np.concatenate([np.random.uniform(-np.pi, np.pi, self.nq), np.random.uniform(-1, 1, self.nv)])
+
+    def diff(self, x0, x1):
+        return np.asarray(x1, float) - np.asarray(x0, float)
+
+    def integrate(self, x, dx):
+        return np.asarray(x, float) + np.asarray(dx, float)
+
+
+class ActuationModelFull:
+    """ActuationModelFull: tau = u, nu = nv."""
+
+    def __init__(self, state):
+        self.state = state
+        self.nu = state.nv
+
+
+class ActivationModelQuad:
+    """a = 0.5 ||r||^2, Ar = r, Arr = I (core/activations/quadratic.hpp)."""
+
+    def __init__(self, nr):
+        self.nr = int(nr)
+        self.weights = None
+
+
+class ActivationModelWeightedQuad:
+    """a = 0.5 r^T diag(w) r, Ar = w r, Arr = diag(w) (weighted-quadratic.hpp:42-71)."""
+
+    def __init__(self, weights):
+        self.weights = np.array(weights, np.float64).reshape(-1)
+        self.nr = self.weights.size
+
+
+class FramePlacement:
+    def __init__(self, id, placement):
+        self.id = int(id)
+        self.placement = placement
+
+
+class FrameTranslation:
+    def __init__(self, id, translation):
+        self.id = int(id)
+        self.translation = np.array(translation, np.float64)
+
+
+class _Cost:
+    """CostModelAbstract (multibody/cost-base.hxx): state, activation, nu."""
+
+    type = 0
+
+    def __init__(self, state, activation, nr, nu):
+        self.state = state
+        self.nu = state.nv if nu is None else int(nu)
+        self.activation = activation if activation is not None else ActivationModelQuad(nr)
+        if self.activation.nr != nr:
+            raise ValueError(f"Invalid argument: nr is equals to {nr}")
+
+    def _payload(self):
+        raise NotImplementedError
+
+    def pack(self):
+        """(Bm, size) record: [type, weight=0 (set by the sum), weighted, size] + payload."""
+        parts = self._payload()
+        w = self.activation.weights
+        parts.append(np.ones((1, self.activation.nr)) if w is None else w.reshape(1, -1))
+        Bm = max(p.shape[0] for p in parts)
+        size = COST_HDR + sum(p.shape[1] for p in parts)
+        hdr = np.array([[self.type, 0.0, 0.0 if w is None else 1.0, size]])
+        return np.concatenate([np.broadcast_to(p, (Bm, p.shape[1])) for p in [hdr] + parts], axis=1)
+
+
+def _rows(a, n):
+    a = np.asarray(a, np.float64)
+    return a.reshape(1, n) if a.ndim == 1 else a.reshape(a.shape[0], n)
+
+
+def _cost_args(args, kw):
+    """Sort the reference's overloads: (activation?, reference?, nu?)."""
+    act = ref = nu = None
+    for a in args:
+        if isinstance(a, (ActivationModelQuad, ActivationModelWeightedQuad)):
+            act = a
+        elif isinstance(a, (int, np.integer)) and not isinstance(a, bool):
+            nu = int(a)
+        else:
+            ref = a
+    act = kw.get("activation", act)
+    nu = kw.get("nu", nu)
+    return act, ref, nu
+
+
+class CostModelState(_Cost):
+    """r = diff(xref, x) = x - xref (state.hxx:130-169); xref defaults to state.zero()."""
+
+    type = COST_STATE
+
+    def __init__(self, state, *args, **kw):
+        act, ref, nu = _cost_args(args, kw)
+        ref = kw.get("xref", ref)
+        super().__init__(state, act, state.ndx, nu)
+        self.xref = state.zero() if ref is None else np.array(ref, np.float64)
+        if self.xref.shape[-1] != state.nx:
+            raise ValueError(f"Invalid argument: xref has wrong dimension (it should be {state.nx})")
+
+    def _payload(self):
+        return [_rows(self.xref, self.state.nx)]
+
+
+class CostModelControl(_Cost):
+    """r = u - uref (control.hxx:56-87); uref defaults to zeros(nu)."""
+
+    type = COST_CONTROL
+
+    def __init__(self, state, *args, **kw):
+        act, ref, nu = _cost_args(args, kw)
+        ref = kw.get("uref", ref)
+        if ref is not None:
+            nu = np.asarray(ref).shape[-1]
+        elif act is not None and nu is None:
+            nu = act.nr
+        nu = state.nv if nu is None else nu
+        super().__init__(state, act, nu, nu)
+        self.uref = np.zeros(nu) if ref is None else np.array(ref, np.float64)
+
+    def _payload(self):
+        return [_rows(self.uref, self.nu)]
+
+
+class CostModelFramePlacement(_Cost):
+    """r = log6(Mref^-1 oMf) (frame-placement.hxx:45-80)."""
+
+    type = COST_FRAME_PLACEMENT
+
+    def __init__(self, state, *args, **kw):
+        act, ref, nu = _cost_args(args, kw)
+        ref = kw.get("Mref", ref)
+        if not isinstance(ref, FramePlacement):
+            raise TypeError("CostModelFramePlacement needs a FramePlacement reference")
+        super().__init__(state, act, 6, nu)
+        self.Mref = ref
+
+    def _payload(self):
+        model = self.state.pinocchio
+        name, pj, pl = model.frames[self.Mref.id]
+        if pj == 0:
+            raise ValueError("Invalid argument: frames attached to the universe are not supported")
+        Pinv = self.Mref.placement.inverse()
+        frame = np.concatenate([[pj - 1], pl.rotation.T.reshape(-1), pl.translation]).reshape(1, -1)
+        return [frame, np.concatenate([Pinv.rotation.T.reshape(-1), Pinv.translation]).reshape(1, -1)]
+
+
+class CostModelFrameTranslation(_Cost):
+    """r = oMf.translation - pref (frame-translation.hxx:50-81). ``xref.translation``
+    may carry a leading batch axis (B, 3): one target per batch element."""
+
+    type = COST_FRAME_TRANSLATION
+
+    def __init__(self, state, *args, **kw):
+        act, ref, nu = _cost_args(args, kw)
+        ref = kw.get("xref", ref)
+        if not isinstance(ref, FrameTranslation):
+            raise TypeError("CostModelFrameTranslation needs a FrameTranslation reference")
+        super().__init__(state, act, 3, nu)
+        self.xref = ref
+
+    def _payload(self):
+        model = self.state.pinocchio
+        name, pj, pl = model.frames[self.xref.id]
+        if pj == 0:
+            raise ValueError("Invalid argument: frames attached to the universe are not supported")
+        frame = np.concatenate([[pj - 1], pl.rotation.T.reshape(-1), pl.translation]).reshape(1, -1)
+        return [frame, _rows(self.xref.translation, 3)]
+
+
+class CostItem:
+    def __init__(self, name, cost, weight, active=True):
+        self.name, self.cost, self.weight, self.active = name, cost, float(weight), bool(active)
+
+
+class CostModelSum:
+    """CostModelSum (cost-sum.hxx:18-85): named costs in a std::map, so they
+    are evaluated and summed in name order."""
+
+    def __init__(self, state, nu=None):
+        self.state = state
+        self.nu = state.nv if nu is None else int(nu)
+        self.costs = {}
+        self._version = 0
+
+    def addCost(self, name, cost, weight, active=True):
+        if cost.nu != self.nu:
+            raise ValueError(f"Invalid argument: {name} cost item doesn't have the same control dimension "
+                             f"(it should be {self.nu})")
+        if name in self.costs:
+            raise ValueError(f"Invalid argument: {name} cost item already existed")
+        self.costs[name] = CostItem(name, cost, weight, active)
+        self._version += 1
+
+    def removeCost(self, name):
+        if name not in self.costs:
+            raise ValueError(f"Invalid argument: {name} cost item doesn't exist")
+        del self.costs[name]
+        self._version += 1
+
+    def changeCostStatus(self, name, active):
+        if name not in self.costs:
+            raise ValueError(f"Invalid argument: {name} cost item doesn't exist")
+        self.costs[name].active = bool(active)
+        self._version += 1
+
+    @property
+    def nr(self):
+        return sum(c.cost.activation.nr for c in self.costs.values() if c.active)
+
+    def pack(self):
+        recs = []
+        for name in sorted(self.costs):  # std::map<std::string, ...> order
+            it = self.costs[name]
+            if not it.active:
+                continue
+            r = np.array(it.cost.pack())
+            r[:, 1] = it.weight
+            recs.append(r)
+        return recs
+
+
+class DifferentialActionModelFreeFwdDynamics:
+    """free-fwddyn.hxx:24-160: a = ABA(q, v, tau(u)) (or (M + diag(armature))^-1
+    (tau - nle) once an armature is set), cost = costs.calc(x, u)."""
+
+    def __init__(self, state, actuation, costs):
+        if not isinstance(actuation, ActuationModelFull):
+            raise NotImplementedError("crocoddyl_amd: the device path covers ActuationModelFull only")
+        if costs.nu != actuation.nu:
+            raise ValueError(f"Invalid argument: Costs doesn't have the same control dimension "
+                             f"(it should be {actuation.nu})")
+        self.state = state
+        self.actuation = actuation
+        self.costs = costs
+        self.nu = actuation.nu
+        self.nr = costs.nr
+        self._armature = np.zeros(state.nv)
+        self._arm_version = 0
+        self._u_lb = np.full(self.nu, -np.inf)
+        self._u_ub = np.full(self.nu, np.inf)
+
+    u_lb = property(lambda s: s._u_lb)
+    u_ub = property(lambda s: s._u_ub)
+
+    @property
+    def armature(self):
+        return self._armature.copy()
+
+    @armature.setter
+    def armature(self, a):
+        a = np.array(a, np.float64).reshape(-1)
+        if a.size != self.state.nv:
+            raise ValueError(f"Invalid argument: The armature dimension is wrong (it should be {self.state.nv})")
+        self._armature = a
+        self._arm_version += 1
+
+    def version(self):
+        return (self.state.pinocchio._version, self.costs._version, self._arm_version,
+                tuple(getattr(c.cost, "_version", 0) for c in self.costs.costs.values()))
+
+    def pack_body(self, dt):
+        """(Bm, size) rows of the FDDP_KNOT_EULER_FREEFWD block for step dt."""
+        model = self.state.pinocchio
+        robot = model.pack_robot(self._armature).reshape(1, -1)
+        recs = self.costs.pack()
+        parts = [robot] + recs
+        Bm = max(p.shape[0] for p in parts)
+        size = _abi.PARAM_HEADER + sum(p.shape[1] for p in parts)
+        hdr = np.array([[dt, model.nv, len(recs), size]])
+        return np.ascontiguousarray(
+            np.concatenate([np.broadcast_to(p, (Bm, p.shape[1])) for p in [hdr] + parts], axis=1))

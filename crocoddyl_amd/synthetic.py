@@ -120,3 +120,43 @@ def build_hetero(name, T=None, B=None, seed=None, phase=10, impulse_every=7):
             running.append(A if (t // phase) % 2 == 0 else Bm)
     x0s = rng.uniform(-1, 1, (B, nx))
     return x0s, running, terminal
+
+
+def build_arm(T=None, B=None, seed=None, robot=None, dt=1e-3, weighted=False, armature=None, w_x=1e-4, w_u=1e-4):
+    """The reference's arm-manipulation problem (benchmark/factory/arm.hpp:31-96,
+    benchmark/arm-manipulation-optctrl.cpp:20-40) on real multibody knots:
+    Euler(dt) ∘ DifferentialActionModelFreeFwdDynamics with costs
+    gripperPose (FramePlacement to (I, (0, 0, 0.4)), weight 1), xReg (1e-4),
+    uReg (1e-4); the terminal model is Euler(runningDAM, 0) as in the factory.
+    x0_b = (q0 ~ U[-1,1]^nq, v0 ~ U[-1,1]^nv) per element. ``robot``: a
+    multibody.RobotModel (default: the 7-DoF Talos-class arm, C3's robot).
+    ``weighted`` adds a weighted xReg activation and a FrameTranslation cost
+    (parity coverage of the remaining cost / activation kinds). w_x / w_u: the
+    xReg / uReg weights (the factory's 1e-4 by default)."""
+    from . import multibody as mb
+    _, _, _, T0, B0, _ = CONFIGS["C3_talos_arm"]
+    T = T0 if T is None else T
+    B = B0 if B is None else B
+    rng = np.random.default_rng(seed_of("C3_talos_arm") + 1 if seed is None else seed)
+    model = mb.sample_talos_arm() if robot is None else robot
+    state = mb.StateMultibody(model)
+    act = mb.ActuationModelFull(state)
+    fid = model.getFrameId("gripper_left_joint") if model.existFrame("gripper_left_joint") else len(model.frames) - 1
+    Mref = mb.FramePlacement(fid, mb.SE3(np.eye(3), (0.0, 0.0, 0.4)))
+    costs = mb.CostModelSum(state)
+    costs.addCost("gripperPose", mb.CostModelFramePlacement(state, Mref), 1.0)
+    if weighted:
+        w = np.linspace(0.5, 2.0, state.ndx)
+        costs.addCost("xReg", mb.CostModelState(state, mb.ActivationModelWeightedQuad(w)), w_x)
+        costs.addCost("gripperTrans", mb.CostModelFrameTranslation(
+            state, mb.FrameTranslation(fid, (0.1, 0.2, 0.3))), 0.3)
+    else:
+        costs.addCost("xReg", mb.CostModelState(state), w_x)
+    costs.addCost("uReg", mb.CostModelControl(state), w_u)
+    dam = mb.DifferentialActionModelFreeFwdDynamics(state, act, costs)
+    if armature is not None:
+        dam.armature = armature
+    running = IntegratedActionModelEuler(dam, dt)
+    terminal = IntegratedActionModelEuler(dam, 0.0)
+    x0s = np.hstack([rng.uniform(-1, 1, (B, state.nq)), rng.uniform(-1, 1, (B, state.nv))])
+    return x0s, [running] * T, terminal

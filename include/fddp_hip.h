@@ -57,6 +57,29 @@ extern "C" {
  * Parameter block: [dt, drift_free, 0, 0]
  *   Fq(nq*nq) Fv(nq*nq) Fu(nq*nu) f0(nq) Lxx(nx*nx) Lxu(nx*nu) Luu(nu*nu) lx(nx) lu(nu) */
 #define FDDP_KNOT_EULER_DIFFLQR 3
+/* IntegratedActionModelEuler (euler.hxx:41-131) around
+ * DifferentialActionModelFreeFwdDynamics (multibody/actions/free-fwddyn.hxx:44-118)
+ * with ActuationModelFull (tau = u) and a CostModelSum (cost-sum.hxx:89-160),
+ * over a fixed-base kinematic tree of nv revolute joints (StateMultibody with
+ * nq = nv: nx = ndx = 2 nv, nu = nv). Variable-size block:
+ *   header [dt, nv, ncost, size (doubles, header included)]
+ *   gravity(3)  armature(nv)
+ *   nv joint records of 26 doubles, parents before children (Pinocchio order):
+ *     parent (-1 = universe), axis(3, unit, joint frame), placement in the
+ *     parent joint frame R(9, column-major) p(3), body mass, CoM(3, joint
+ *     frame), rotational inertia about the CoM (Ixx Iyy Izz Ixy Ixz Iyz)
+ *   ncost cost records in name order (CostModelSum's std::map), each
+ *     [type, weight, weighted (0: ActivationModelQuad, 1: WeightedQuad), size]
+ *     then the payload and the activation weights (ones when unweighted):
+ *     1 CostModelState (state.hxx:130-169):       xref(nx) w(nx)
+ *     2 CostModelControl (control.hxx:56-87):     uref(nu) w(nu)
+ *     3 CostModelFramePlacement (frame-placement.hxx:45-80): frame joint,
+ *       frame placement in that joint R(9) p(3), Mref^-1 R(9) p(3), w(6)
+ *     4 CostModelFrameTranslation (frame-translation.hxx:50-81): frame joint,
+ *       frame placement R(9) p(3), reference translation(3), w(3)
+ * At most 32 joints (fewer when the calcDiff LDS plan does not fit) and 8
+ * frame costs per knot. */
+#define FDDP_KNOT_EULER_FREEFWD 4
 
 #define FDDP_PARAM_HEADER 4 /* doubles of scalar header in front of every block */
 

@@ -17,6 +17,8 @@ SURVEY.md §8a "Restatement traps"):
   * ActionModelUnicycle                core/actions/unicycle.hxx:22-73
   * IntegratedActionModelEuler∘DifferentialActionModelLQR
                                        core/integrator/euler.hxx:41-131, core/actions/diff-lqr.hxx:34-79
+  * Euler∘DifferentialActionModelFreeFwdDynamics (multibody knots)
+                                       oracle/multibody_np.py
   * BoxQP::solve                       src/core/solvers/box-qp.cpp:51-182
   * SolverBoxFDDP computeGains / forwardPass  src/core/solvers/box-fddp.cpp:48-160
 It also restates SolverKKT (src/core/solvers/kkt.cpp:34-227), the dense
@@ -27,7 +29,7 @@ import math
 
 import numpy as np
 
-LQR, UNICYCLE, EULER_DIFFLQR = 1, 2, 3
+LQR, UNICYCLE, EULER_DIFFLQR, EULER_FREEFWD = 1, 2, 3, 4
 HDR = 4
 
 
@@ -162,6 +164,10 @@ def bind_problem(knot_descs, pool, b, nx):
     out = []
     for kind, nu, off, stride in knot_descs:
         o = off + b * stride
+        if kind == EULER_FREEFWD:  # variable-size multibody block (oracle/multibody_np.py)
+            from oracle.multibody_np import FreeFwdKnot
+            out.append(FreeFwdKnot(pool[o:o + int(pool[o + 3])], nx, nu))
+            continue
         size = block_size(kind, nx, nu)
         out.append(Knot(kind, nx, nu, pool[o:o + size]))
     return out

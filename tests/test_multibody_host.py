@@ -1,0 +1,74 @@
+"""The device multibody knot code (crocoddyl_amd/csrc/multibody.hpp), compiled
+for the host with the sequential-lane executor (tests/cpp/mb_host.cpp), vs the
+numpy oracle (oracle/multibody_np.py: ABA + complex-step derivatives). CPU
+only: the same arithmetic the GPU runs, checked without a GPU (the GPU run of
+it is tests/test_multibody_gpu.py)."""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from crocoddyl_amd import multibody as mb, synthetic
+from oracle import multibody_np as onp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(ROOT, "tests", "cpp", "mb_host.cpp")
+OUT = os.path.join(ROOT, "tests", "_build", "libmb_host.so")
+D = C.POINTER(C.c_double)
+
+
+@pytest.fixture(scope="module")
+def lib():
+    hdr = os.path.join(ROOT, "crocoddyl_amd", "csrc", "multibody.hpp")
+    if not os.path.exists(OUT) or os.path.getmtime(OUT) < max(os.path.getmtime(SRC), os.path.getmtime(hdr)):
+        os.makedirs(os.path.dirname(OUT), exist_ok=True)
+        subprocess.check_call(["/opt/rocm/bin/hipcc", "-x", "hip", "--offload-arch=gfx950", "-O2", "-std=c++17",
+                               "-shared", "-fPIC", "-o", OUT, SRC])
+    L = C.CDLL(OUT)
+    L.mb_host_calc.restype = C.c_double
+    L.mb_host_calc.argtypes = [D, C.c_int, D, D, C.c_int, D]
+    L.mb_host_calc_diff.argtypes = [D, C.c_int, C.c_int, D, D, C.c_int] + [D] * 7
+    return L
+
+
+def _p(a):
+    return a.ctypes.data_as(D)
+
+
+CASES = [dict(), dict(weighted=True), dict(robot=mb.sample_tree(6, seed=4), weighted=True),
+         dict(robot=mb.sample_tree(9, seed=8, branching=False), armature=np.full(9, 0.05)),
+         dict(robot=mb.sample_tree(12, seed=2), weighted=True, armature=np.linspace(0.0, 0.2, 12))]
+
+
+@pytest.mark.parametrize("case", range(len(CASES)))
+@pytest.mark.parametrize("terminal", [False, True])
+def test_device_code_vs_oracle(lib, case, terminal):
+    x0s, running, term = synthetic.build_arm(T=2, B=1, **CASES[case])
+    em = term if terminal else running[0]
+    _, nu, blk = em.pack()
+    blk = np.ascontiguousarray(blk[0])
+    nx = em.state.nx
+    k = onp.FreeFwdKnot(blk, nx, nu)
+    rng = np.random.default_rng(case)
+    for _ in range(3):
+        x, u = rng.uniform(-2, 2, nx), rng.uniform(-3, 3, nu)
+        use_u = 0 if terminal else 1
+        uo = None if terminal else u
+        xn = np.zeros(nx)
+        c = lib.mb_host_calc(_p(blk), nx, _p(x), _p(u), use_u, _p(xn))
+        xo, co = k.calc(x, uo)
+        np.testing.assert_allclose(xn, xo, rtol=1e-12, atol=1e-12)
+        assert c == pytest.approx(co, rel=1e-12, abs=1e-14)
+        n, m = nx, nu
+        out = {q: np.zeros(s) for q, s in [("Fx", n * n), ("Fu", n * m), ("Lxx", n * n), ("Lxu", n * m),
+                                           ("Luu", m * m), ("Lx", n), ("Lu", m)]}
+        lib.mb_host_calc_diff(_p(blk), nx, m, _p(x), _p(u), use_u,
+                              *[_p(out[q]) for q in ["Fx", "Fu", "Lxx", "Lxu", "Luu", "Lx", "Lu"]])
+        ref = k.calc_diff(x, uo)
+        for q, a in out.items():
+            rows = m if q == "Luu" else n
+            got = a.reshape(-1, rows).T if q in ("Fx", "Fu", "Lxx", "Lxu", "Luu") else a
+            scale = max(1.0, float(np.max(np.abs(ref[q]))))
+            assert float(np.max(np.abs(got - ref[q]))) / scale < 1e-10, (q, case, terminal)

@@ -1,0 +1,162 @@
+"""Pins the numpy multibody oracle (oracle/multibody_np.py) — CPU only.
+
+Pinocchio is absent offline, so the rigid-body arithmetic is pinned by
+  * closed-form pendulum / double-pendulum equations of motion (textbook
+    Lagrangian dynamics: M(q), Coriolis and gravity terms),
+  * algorithm identities: ABA == CRBA^-1 (tau - RNEA(q, v, 0)) and
+    RNEA(q, v, ABA(q, v, tau)) == tau, incl. armature and branching trees,
+  * SE(3): exp6(log6(M)) == M over all angle ranges,
+  * the reference's own derivative test design: analytic (here complex-step)
+    vs finite differences at tol 3e4 * sqrt(2 eps) (unittest/test_actions.cpp:70-110),
+and the packing of crocoddyl_amd.multibody is checked against the oracle's
+parser (same block, same numbers).
+"""
+import numpy as np
+import pytest
+
+import crocoddyl_amd as croc
+from crocoddyl_amd import multibody as mb
+from oracle import multibody_np as onp
+
+G = 9.81
+
+
+def _robot(model, armature=None):
+    nv = model.nv
+    body = model.pack_robot(np.zeros(nv) if armature is None else armature)
+    r, _ = onp.parse_robot(body, nv)
+    return r
+
+
+def _pendulum(m=1.3, l=0.7):
+    model = mb.RobotModel()
+    j = model.addJoint(0, (0, 1, 0), mb.SE3(), "j1")
+    model.appendBodyToJoint(j, mb.Inertia(m, (0, 0, -l), np.zeros((3, 3))))
+    return model
+
+
+def _double_pendulum(m1=1.1, m2=0.7, l1=0.9, l2=0.6):
+    model = mb.RobotModel()
+    j1 = model.addJoint(0, (0, 1, 0), mb.SE3(), "j1")
+    model.appendBodyToJoint(j1, mb.Inertia(m1, (0, 0, -l1), np.zeros((3, 3))))
+    j2 = model.addJoint(j1, (0, 1, 0), mb.SE3(np.eye(3), (0, 0, -l1)), "j2")
+    model.appendBodyToJoint(j2, mb.Inertia(m2, (0, 0, -l2), np.zeros((3, 3))))
+    return model
+
+
+def test_pendulum_closed_form():
+    m, l = 1.3, 0.7
+    r = _robot(_pendulum(m, l))
+    for q, v, tau in [(0.3, -0.4, 0.5), (-2.0, 1.5, 0.0), (3.0, 0.0, -1.0)]:
+        qdd = r.aba(np.array([q]), np.array([v]), np.array([tau]))[0]
+        assert qdd == pytest.approx((tau - m * G * l * np.sin(q)) / (m * l * l), rel=1e-13, abs=1e-13)
+        t = r.rnea(np.array([q]), np.array([v]), np.array([qdd]))[0]
+        assert t == pytest.approx(tau, abs=1e-12)
+
+
+def test_double_pendulum_closed_form():
+    m1, m2, l1, l2 = 1.1, 0.7, 0.9, 0.6
+    r = _robot(_double_pendulum(m1, m2, l1, l2))
+    rng = np.random.default_rng(3)
+    for _ in range(5):
+        q, v, a = rng.uniform(-3, 3, 2), rng.uniform(-2, 2, 2), rng.uniform(-2, 2, 2)
+        c2 = np.cos(q[1])
+        M = np.array([[m1 * l1 ** 2 + m2 * (l1 ** 2 + l2 ** 2 + 2 * l1 * l2 * c2), m2 * (l2 ** 2 + l1 * l2 * c2)],
+                      [m2 * (l2 ** 2 + l1 * l2 * c2), m2 * l2 ** 2]])
+        h = m2 * l1 * l2 * np.sin(q[1])
+        cor = np.array([-h * (2 * v[0] * v[1] + v[1] ** 2), h * v[0] ** 2])
+        g = np.array([(m1 + m2) * G * l1 * np.sin(q[0]) + m2 * G * l2 * np.sin(q[0] + q[1]),
+                      m2 * G * l2 * np.sin(q[0] + q[1])])
+        np.testing.assert_allclose(r.crba(q), M, rtol=1e-13, atol=1e-13)
+        np.testing.assert_allclose(r.rnea(q, v, a), M @ a + cor + g, rtol=1e-12, atol=1e-12)
+
+
+@pytest.mark.parametrize("branching", [False, True])
+@pytest.mark.parametrize("with_armature", [False, True])
+def test_aba_crba_rnea_identities(branching, with_armature):
+    model = mb.sample_tree(9, seed=11, branching=branching)
+    rng = np.random.default_rng(5)
+    arm = rng.uniform(0.01, 0.2, model.nv) if with_armature else np.zeros(model.nv)
+    r = _robot(model, arm)
+    for _ in range(3):
+        q, v, tau = rng.uniform(-3, 3, model.nv), rng.uniform(-2, 2, model.nv), rng.uniform(-5, 5, model.nv)
+        a = r.aba(q, v, tau)
+        M = r.crba(q) + np.diag(arm)
+        nle = r.rnea(q, v, np.zeros(model.nv))
+        np.testing.assert_allclose(a, np.linalg.solve(M, tau - nle), rtol=1e-10, atol=1e-10)
+        np.testing.assert_allclose(r.rnea(q, v, a) + arm * a, tau, rtol=1e-10, atol=1e-10)
+        np.testing.assert_allclose(M, M.T, atol=1e-14)
+        assert np.all(np.linalg.eigvalsh(M) > 0)
+
+
+@pytest.mark.parametrize("angle", [0.0, 1e-9, 1e-5, 0.3, 1.2, 2.0, 2.9, np.pi - 1e-3, np.pi - 1e-7])
+def test_log6_exp6_roundtrip(angle):
+    rng = np.random.default_rng(int(angle * 1e3) + 1)
+    ax = rng.normal(size=3)
+    ax /= np.linalg.norm(ax)
+    nu = np.concatenate([rng.normal(size=3), angle * ax])
+    R, p = onp.exp6(nu)
+    R2, p2 = onp.exp6(onp.log6(R, p))
+    np.testing.assert_allclose(R2, R, atol=1e-9 if angle > 3 else 1e-12)
+    np.testing.assert_allclose(p2, p, atol=1e-7 if angle > 3 else 1e-11)
+
+
+def _arm_knot(dt=1e-3, weighted=False):
+    model = mb.sample_talos_arm()
+    state = mb.StateMultibody(model)
+    act = mb.ActuationModelFull(state)
+    fid = model.getFrameId("gripper_left_joint")
+    Mref = mb.FramePlacement(fid, mb.SE3(np.eye(3), (0.0, 0.0, 0.4)))
+    costs = mb.CostModelSum(state)
+    costs.addCost("gripperPose", mb.CostModelFramePlacement(state, Mref), 1.0)
+    if weighted:
+        costs.addCost("xReg", mb.CostModelState(state, mb.ActivationModelWeightedQuad(np.linspace(0.5, 2, 14))), 1e-4)
+        costs.addCost("tip", mb.CostModelFrameTranslation(state, mb.FrameTranslation(fid, (0.1, 0.2, 0.3))), 0.5)
+    else:
+        costs.addCost("xReg", mb.CostModelState(state), 1e-4)
+    costs.addCost("uReg", mb.CostModelControl(state), 1e-4)
+    dam = mb.DifferentialActionModelFreeFwdDynamics(state, act, costs)
+    return croc.IntegratedActionModelEuler(dam, dt)
+
+
+def test_pack_matches_oracle_parser():
+    em = _arm_knot(weighted=True)
+    kind, nu, blk = em.pack()
+    assert kind == 4 and nu == 7 and blk.shape[0] == 1
+    k = onp.FreeFwdKnot(blk[0], 14, 7)
+    assert k.size == blk.shape[1]
+    assert [c.type for c in k.costs] == [onp.FRAME_PLACEMENT, onp.FRAME_TRANSLATION, onp.CONTROL, onp.STATE]
+    assert k.costs[0].weight == 1.0 and k.costs[1].weight == 0.5
+    np.testing.assert_allclose(k.costs[3].w, np.linspace(0.5, 2, 14))
+
+
+@pytest.mark.parametrize("weighted", [False, True])
+@pytest.mark.parametrize("dt", [1e-2, 0.0])
+def test_knot_derivatives_vs_numdiff(weighted, dt):
+    """Complex-step derivatives vs central differences (test_actions.cpp:70-110 design)."""
+    em = _arm_knot(dt=dt, weighted=weighted)
+    _, _, blk = em.pack()
+    k = onp.FreeFwdKnot(blk[0], 14, 7)
+    rng = np.random.default_rng(9)
+    x, u = rng.uniform(-1, 1, 14), rng.uniform(-3, 3, 7)
+    d = k.calc_diff(x, u)
+    h = np.sqrt(2 * np.finfo(float).eps)
+    tol = 3e4 * h
+    z = np.concatenate([x, u])
+    F = np.zeros((14, 21))
+    L = np.zeros(21)
+    for j in range(21):
+        e = np.zeros(21)
+        e[j] = h
+        xp, cp = k.calc(z[:14] + e[:14], z[14:] + e[14:])
+        xm, cm = k.calc(z[:14] - e[:14], z[14:] - e[14:])
+        F[:, j] = (xp - xm) / (2 * h)
+        L[j] = (cp - cm) / (2 * h)
+    np.testing.assert_allclose(d["Fx"], F[:, :14], atol=tol)
+    np.testing.assert_allclose(d["Fu"], F[:, 14:], atol=tol)
+    np.testing.assert_allclose(d["Lx"], L[:14], atol=tol)
+    np.testing.assert_allclose(d["Lu"], L[14:], atol=tol)
+    # Gauss-Newton Hessians are symmetric positive semi-definite
+    Lzz = np.block([[d["Lxx"], d["Lxu"]], [d["Lxu"].T, d["Luu"]]])
+    np.testing.assert_allclose(Lzz, Lzz.T, atol=1e-12)
+    assert np.linalg.eigvalsh(Lzz).min() > -1e-10
