@@ -195,8 +195,11 @@ def main():
             "metric": METRIC, "value": round(value, 2), "unit": "FDDP iterations/s", "n_gpus": ws,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
-            "data": "synthetic: seeded Euler(dt)∘DifferentialActionModelLQR knots at the config's (n, m, T); "
-                    "per-element matrices (SURVEY §8d); no robot model (Pinocchio/URDF absent)",
+            "data": ("synthetic: arm-manipulation problem of benchmark/factory/arm.hpp on real multibody knots "
+                     "(Euler ∘ FreeFwdDynamics, 7-DoF Talos-class arm model built in code: the URDF is absent), "
+                     "per-element x0" if kind == "multibody" else
+                     "synthetic: seeded Euler(dt)∘DifferentialActionModelLQR knots at the config's (n, m, T); "
+                     "per-element matrices (SURVEY §8d); no robot model (Pinocchio/URDF absent)"),
             "config": {"workload": f"{args.config}: n={n}, m={m}, T={T}, B={B} per GPU, warm-started "
                                    f"solve(maxiter={mpc_iters}, reg_init=0.1) after a device receding-horizon shift"
                                    + (", SolverBoxFDDP with |u| <= 1" if box else ""),

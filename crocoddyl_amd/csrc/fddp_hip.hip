@@ -83,7 +83,7 @@ int64_t mb_block_check(const double* P, int64_t avail, int nx, int nu, std::stri
   if ((double)nj != P[1] || nj < 1 || nj > kMaxJ) return why = "number of joints out of [1, 32]", -1;
   if (nx != 2 * nj) return why = "free-fwddyn knots need nx = 2 nv", -1;
   if (nu != nj) return why = "ActuationModelFull needs nu = nv", -1;
-  if ((double)ncost != P[2] || ncost < 0) return why = "bad number of costs", -1;
+  if ((double)ncost != P[2] || ncost < 0 || ncost > kMaxCosts) return why = "number of costs out of [0, 64]", -1;
   if (size > avail || (double)size != P[3]) return why = "block out of range", -1;
   int64_t o = FDDP_PARAM_HEADER + 3 + nj;
   if (o + (int64_t)kJRec * nj > size) return why = "block too small for its joints", -1;
@@ -200,7 +200,8 @@ struct fddp_handle_s {
   bool fast = false;  // dense-knot fast path (fast_path.hpp) for calc / calcDiff / forward
   size_t fused_smem = 0, fwd_fast_smem = 0;
   int64_t pcap = 0;  // doubles of LDS reserved for a resident parameter block
-  bool has_mb = false;     // multibody knots present (mb_calc_diff_kernel)
+  bool has_mb = false;     // multibody knots present (mb_knot_kernel)
+  bool all_mb = false;     // every knot is a multibody knot
   size_t mb_diff_smem = 0; // its dynamic LDS
   int bwd_variant = 0;  // 0 generic, else (NTL*10+MTL)*10+waves of the MFMA sweep
   // timing
@@ -302,11 +303,25 @@ int launch_fused(fddp_handle* h, int sel_calc, int sel_diff, int gaps) {
   LAUNCH_CHECK();
   return FDDP_OK;
 }
+// Multibody knots (knot-parallel): calc for sel_calc, calcDiff for sel_diff (-1: none).
+int launch_mb(fddp_handle* h, int sel_calc, int sel_diff) {
+  const Dev& D = h->D;
+  hipLaunchKernelGGL(mb_knot_kernel, dim3(D.T + 1, D.B), dim3(64), h->mb_diff_smem, h->stream, D, sel_calc, sel_diff);
+  LAUNCH_CHECK();
+  return FDDP_OK;
+}
 int launch_calc(fddp_handle* h, int sel) {
   if (h->fast) return launch_fused(h, sel, -1, 0);
   Timed tm(h, 0);
   const Dev& D = h->D;
-  hipLaunchKernelGGL(calc_kernel<kNT>, dim3(D.B), dim3(kNT), h->calc_smem, h->stream, D, sel, h->pcap);
+  if (h->has_mb) {
+    int rc;
+    if ((rc = launch_mb(h, sel, -1))) return rc;
+    if (!h->all_mb)
+      hipLaunchKernelGGL(calc_kernel<kNT>, dim3(D.B), dim3(kNT), h->calc_smem, h->stream, D, sel, h->pcap, 1);
+  } else {
+    hipLaunchKernelGGL(calc_kernel<kNT>, dim3(D.B), dim3(kNT), h->calc_smem, h->stream, D, sel, h->pcap, 0);
+  }
   LAUNCH_CHECK();
   return FDDP_OK;
 }
@@ -321,8 +336,8 @@ int launch_calc_diff(fddp_handle* h, int sel, int gaps) {
   Timed tm(h, 1);
   const Dev& D = h->D;
   if (h->has_mb) {  // multibody knots: one workgroup per knot, before the gaps pass
-    hipLaunchKernelGGL(mb_calc_diff_kernel, dim3(D.T + 1, D.B), dim3(64), h->mb_diff_smem, h->stream, D, sel);
-    LAUNCH_CHECK();
+    int rc;
+    if ((rc = launch_mb(h, -1, sel))) return rc;
   }
   hipLaunchKernelGGL(calc_diff_kernel<kNT>, dim3(D.B), dim3(kNT), h->cdiff_smem, h->stream, D, sel, gaps, h->pcap);
   LAUNCH_CHECK();
@@ -335,6 +350,25 @@ int launch_calc_then_diff(fddp_handle* h, int sel_calc, int sel_calc_sum, int se
   if (h->fast) {
     if ((rc = launch_fused(h, sel_calc, sel_diff, gaps))) return rc;
     return launch_cost_sum(h, sel_calc_sum, nullptr);
+  }
+  if (h->has_mb) {  // multibody knots: their calc fused into the knot-parallel calcDiff
+    {
+      Timed tm(h, 1);
+      if ((rc = launch_mb(h, sel_calc, sel_diff))) return rc;
+    }
+    if (!h->all_mb) {
+      Timed tm(h, 0);
+      const Dev& D = h->D;
+      hipLaunchKernelGGL(calc_kernel<kNT>, dim3(D.B), dim3(kNT), h->calc_smem, h->stream, D, sel_calc, h->pcap, 1);
+      LAUNCH_CHECK();
+    }
+    if ((rc = launch_cost_sum(h, sel_calc_sum, nullptr))) return rc;
+    Timed tm(h, 1);
+    const Dev& D = h->D;
+    hipLaunchKernelGGL(calc_diff_kernel<kNT>, dim3(D.B), dim3(kNT), h->cdiff_smem, h->stream, D, sel_diff, gaps,
+                       h->pcap);
+    LAUNCH_CHECK();
+    return FDDP_OK;
   }
   if ((rc = launch_calc(h, sel_calc))) return rc;
   if ((rc = launch_cost_sum(h, sel_calc_sum, nullptr))) return rc;
@@ -511,6 +545,8 @@ int apply_knots(fddp_handle* h, const fddp_knot_desc* knots, const double* param
       }
       pmax = std::max<int64_t>(pmax, sz);
     }
+    h->all_mb = true;
+    for (int t = 0; t <= d.T; ++t) h->all_mb = h->all_mb && knots[t].kind == FDDP_KNOT_EULER_FREEFWD;
     D.mbw = h->has_mb ? pad2(fddp::mb::calc_work_doubles(mb_nj)) : 0;
     h->mb_diff_smem = h->has_mb ? sizeof(double) * fddp::mb::diff_layout(mb_nj, mb_nframe).total : 0;
     const int64_t budget = (150 * 1024) / 8 - (2 * D.sX + D.sM + 5 * (kNT / kWave) + 16) - D.mbw;
@@ -572,7 +608,7 @@ int apply_knots(fddp_handle* h, const fddp_knot_desc* knots, const double* param
                           (int)h->calc_smem) != hipSuccess ||
       hipFuncSetAttribute((const void*)calc_diff_kernel<kNT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)h->cdiff_smem) != hipSuccess ||
-      (h->has_mb && hipFuncSetAttribute((const void*)mb_calc_diff_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+      (h->has_mb && hipFuncSetAttribute((const void*)mb_knot_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                         (int)h->mb_diff_smem) != hipSuccess))
     return fail(FDDP_ERR_RUNTIME, "hipFuncSetAttribute(dynamic LDS)");
   {  // backward sweep variant: MFMA tiles when every running knot has nu == nu_max

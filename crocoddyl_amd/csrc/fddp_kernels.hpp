@@ -89,7 +89,7 @@ __device__ __forceinline__ void wg_gemm(int M, int N, int K, const double* __res
 // trajectory cur.
 // ---------------------------------------------------------------------------
 template <int NT>
-__global__ __launch_bounds__(NT) void calc_kernel(Dev D, int sel, int64_t pcap) {
+__global__ __launch_bounds__(NT) void calc_kernel(Dev D, int sel, int64_t pcap, int skip_mb) {
   const int b = blockIdx.x;
   const ElemState s = D.st[b];  // by value: a reference would re-load it from HBM after every store
   if (!selected(s, sel)) return;
@@ -104,6 +104,7 @@ __global__ __launch_bounds__(NT) void calc_kernel(Dev D, int sel, int64_t pcap) 
   const double* cached = nullptr;
   for (int t = 0; t <= D.T; ++t) {
     const fddp_knot_desc kd = D.knots[t];
+    if (skip_mb && kd.kind == FDDP_KNOT_EULER_FREEFWD) continue;  // computed by mb_knot_kernel
     const double* P = stage_params<NT>(D.pblock(b, t), block_doubles_dev(kd.kind, D.nx, kd.nu, D.pblock(b, t)), pl, pcap, cached);
     const double* xg = D.xs[c] + D.knot(b, t) * D.sX;
     for (int i = threadIdx.x; i < D.nx; i += NT) x[i] = xg[i];
@@ -198,24 +199,35 @@ __global__ __launch_bounds__(NT) void calc_diff_kernel(Dev D, int sel, int gaps,
   }
 }
 
-// Multibody knots' calcDiff (multibody.hpp): one 64-thread workgroup per
+// Multibody knots (multibody.hpp), knot-parallel: one 64-thread workgroup per
 // (knot t = blockIdx.x, element b = blockIdx.y); knots of other kinds return.
-// The gaps of these knots are written by calc_diff_kernel as for any knot.
-__global__ __launch_bounds__(64) void mb_calc_diff_kernel(Dev D, int sel) {
+// calc (xnext, knot cost) for elements selected by sel_calc and calcDiff
+// (derivative blocks) for those selected by sel_diff (-1: none), fused: the
+// calcDiff evaluates the dynamics the calc needs anyway. The gaps of these
+// knots are written by calc_diff_kernel as for any knot.
+__global__ __launch_bounds__(64) void mb_knot_kernel(Dev D, int sel_calc, int sel_diff) {
   const int t = blockIdx.x, b = blockIdx.y;
   const fddp_knot_desc kd = D.knots[t];
   if (kd.kind != FDDP_KNOT_EULER_FREEFWD) return;
   const ElemState s = D.st[b];
-  if (!selected(s, sel)) return;
+  const bool do_calc = sel_calc >= 0 && selected(s, sel_calc);
+  const bool do_diff = sel_diff >= 0 && selected(s, sel_diff);
+  if (!do_calc && !do_diff) return;
   extern __shared__ __attribute__((aligned(16))) double sm[];
   const int c = s.cur;
   const int64_t kk = D.knot(b, t);
   const bool running = t < D.T;
   const double* xg = D.xs[c] + kk * D.sX;
   const double* ug = running ? D.us[c] + D.run(b, t) * D.sM : nullptr;
-  mb::knot_calc_diff(D.pblock(b, t), D.nx, D.m, xg, ug, running && kd.nu > 0, sm, D.Fx + kk * D.sNN,
-                     D.Fu + kk * D.sNM, D.Lxx + kk * D.sNN, D.Lxu + kk * D.sNM, D.Luu + kk * D.sMM, D.Lx + kk * D.sN,
-                     D.Lu + kk * D.sM);
+  double* xn = (do_calc && running) ? D.xnext[c] + D.run(b, t) * D.sX : nullptr;
+  double* cost = do_calc ? D.kcost[c] + kk : nullptr;
+  if (do_diff)
+    mb::knot_calc_diff(D.pblock(b, t), D.nx, D.m, xg, ug, running && kd.nu > 0, sm, D.Fx + kk * D.sNN,
+                       D.Fu + kk * D.sNM, D.Lxx + kk * D.sNN, D.Lxu + kk * D.sNM, D.Luu + kk * D.sMM,
+                       D.Lx + kk * D.sN, D.Lu + kk * D.sM, xn, cost);
+  else
+    mb::knot_calc_diff(D.pblock(b, t), D.nx, D.m, xg, ug, running && kd.nu > 0, sm, nullptr, nullptr, nullptr,
+                       nullptr, nullptr, nullptr, nullptr, xn, cost);
 }
 
 // ---------------------------------------------------------------------------

@@ -8,10 +8,11 @@
 //   multibody/costs/{state,control,frame-placement,frame-translation}.hxx; the rigid-body
 //   arithmetic the reference takes from Pinocchio (aba, computeABADerivatives,
 //   updateFramePlacement, getFrameJacobian, log6, Jlog6) is computed here as:
-//   * forward dynamics: a = (M + diag(armature))^-1 (tau - nle), M by the composite-
-//     rigid-body algorithm (one column per lane, walking the ancestors), nle by a
-//     recursive Newton-Euler value pass, the solve by Gauss-Jordan with one column
-//     per lane. (The reference's default path is ABA, the same function.)
+//   * forward dynamics: a = (M + diag(armature))^-1 (tau - nle), with RNEA and the
+//     composite-rigid-body algorithm in world coordinates, where every recursion is
+//     an ancestor / subtree sum evaluated one joint per lane, and the solve by
+//     Gauss-Jordan with one column per lane. (The reference's default path is ABA,
+//     the same function.)
 //   * derivatives: the RNEA linearised along each state direction (one lane per
 //     q_j / v_j direction, tangents kept in LDS), da/dx = -(M + A)^-1 dtau/dx — the
 //     identity computeABADerivatives implements;
@@ -207,141 +208,6 @@ MB_HD inline void joint_rotation(const double* Rpl, const double* ax, double q, 
   matmul3(Rpl, Rj, R);
 }
 
-// Recursive Newton-Euler value pass (one thread). Placements (liMi, oMi),
-// velocities, accelerations (qdd == nullptr: zero) and the accumulated joint
-// forces; tau = S^T F. With `composite`, also the composite inertia of every
-// subtree (CRBA). rnea (Featherstone Table 5.1), crba (Table 6.2).
-MB_HD inline void value_pass(const Blk& b, const double* q, const double* qd, const double* qdd, const Vals& V,
-                                  double* tau, bool kin, bool composite) {
-  const int nj = b.nj;
-  for (int e = 0; e < 6; ++e) {
-    V.root_v()[e] = 0.;
-    V.root_a()[e] = e < 3 ? -b.g[e] : 0.;
-  }
-  for (int i = 0; i < nj; ++i) {
-    const JRec J(b, i);
-    const int lam = J.parent();
-    const double* ax = J.axis();
-    double* R = V.R(i);
-    double* p = V.p(i);
-    if (kin) {
-      joint_rotation(J.Rpl(), ax, q[i], R);
-      p[0] = J.ppl()[0];
-      p[1] = J.ppl()[1];
-      p[2] = J.ppl()[2];
-      if (lam >= 0) {
-        matmul3(V.oR(lam), R, V.oR(i));
-        double t[3];
-        matvec3(V.oR(lam), p, t);
-        V.op(i)[0] = V.op(lam)[0] + t[0];
-        V.op(i)[1] = V.op(lam)[1] + t[1];
-        V.op(i)[2] = V.op(lam)[2] + t[2];
-      } else {
-        for (int e = 0; e < 9; ++e) V.oR(i)[e] = R[e];
-        for (int e = 0; e < 3; ++e) V.op(i)[e] = p[e];
-      }
-    }
-    const double* vp = lam >= 0 ? V.v(lam) : V.root_v();
-    const double* ap = lam >= 0 ? V.a(lam) : V.root_a();
-    double* v = V.v(i);
-    double* a = V.a(i);
-    const double w = qd[i];
-    motion_act_inv(R, p, vp, v);
-    v[3] += ax[0] * w;
-    v[4] += ax[1] * w;
-    v[5] += ax[2] * w;
-    motion_act_inv(R, p, ap, a);
-    const double qa = qdd ? qdd[i] : 0.;
-    a[3] += ax[0] * qa;
-    a[4] += ax[1] * qa;
-    a[5] += ax[2] * qa;
-    // + v x (S qd)
-    const double sv[6] = {0., 0., 0., ax[0] * w, ax[1] * w, ax[2] * w};
-    double t6[6];
-    cross_m(v, sv, t6);
-    for (int e = 0; e < 6; ++e) a[e] += t6[e];
-    // f = I a + v x* (I v)
-    double Iv[6], f[6];
-    inertia_mul(J.mass(), J.com(), J.I6(), a, f);
-    inertia_mul(J.mass(), J.com(), J.I6(), v, Iv);
-    cross_f(v, Iv, t6);
-    for (int e = 0; e < 6; ++e) V.F(i)[e] = f[e] + t6[e];
-    if (composite) {
-      *V.cm(i) = J.mass();
-      for (int e = 0; e < 3; ++e) V.cc(i)[e] = J.com()[e];
-      for (int e = 0; e < 6; ++e) V.cI(i)[e] = J.I6()[e];
-    }
-  }
-  for (int i = nj - 1; i >= 0; --i) {
-    const JRec J(b, i);
-    const double* F = V.F(i);
-    tau[i] = dot3(J.axis(), F + 3);
-    const int lam = J.parent();
-    if (lam < 0) continue;
-    double t6[6];
-    force_act(V.R(i), V.p(i), F, t6);
-    for (int e = 0; e < 6; ++e) V.F(lam)[e] += t6[e];
-    if (composite) {  // composite inertia of the subtree, carried to the parent and summed
-      const double m1 = *V.cm(i), m0 = *V.cm(lam);
-      const double* R = V.R(i);
-      double c1[3], I1[9], tmp[9];
-      matvec3(R, V.cc(i), c1);
-      c1[0] += V.p(i)[0];
-      c1[1] += V.p(i)[1];
-      c1[2] += V.p(i)[2];
-      const double* s = V.cI(i);
-      const double Is[9] = {s[0], s[3], s[4], s[3], s[1], s[5], s[4], s[5], s[2]};
-      matmul3(R, Is, tmp);
-      // I1 = tmp R^T
-      for (int r = 0; r < 3; ++r)
-        for (int c = 0; c < 3; ++c) I1[c * 3 + r] = tmp[r] * R[c] + tmp[3 + r] * R[3 + c] + tmp[6 + r] * R[6 + c];
-      const double m = m0 + m1;
-      if (m > 0.) {
-        const double* c0 = V.cc(lam);
-        const double cn[3] = {(m0 * c0[0] + m1 * c1[0]) / m, (m0 * c0[1] + m1 * c1[1]) / m,
-                              (m0 * c0[2] + m1 * c1[2]) / m};
-        const double d0[3] = {c0[0] - cn[0], c0[1] - cn[1], c0[2] - cn[2]};
-        const double d1[3] = {c1[0] - cn[0], c1[1] - cn[1], c1[2] - cn[2]};
-        const double q0 = dot3(d0, d0), q1 = dot3(d1, d1);
-        double* o = V.cI(lam);
-        // parallel-axis shift of both to the new CoM: I + m (|d|^2 I - d d^T)
-        o[0] = o[0] + m0 * (q0 - d0[0] * d0[0]) + I1[0] + m1 * (q1 - d1[0] * d1[0]);
-        o[1] = o[1] + m0 * (q0 - d0[1] * d0[1]) + I1[4] + m1 * (q1 - d1[1] * d1[1]);
-        o[2] = o[2] + m0 * (q0 - d0[2] * d0[2]) + I1[8] + m1 * (q1 - d1[2] * d1[2]);
-        o[3] = o[3] - m0 * d0[0] * d0[1] + I1[3] - m1 * d1[0] * d1[1];
-        o[4] = o[4] - m0 * d0[0] * d0[2] + I1[6] - m1 * d1[0] * d1[2];
-        o[5] = o[5] - m0 * d0[1] * d0[2] + I1[7] - m1 * d1[1] * d1[2];
-        *V.cm(lam) = m;
-        V.cc(lam)[0] = cn[0];
-        V.cc(lam)[1] = cn[1];
-        V.cc(lam)[2] = cn[2];
-      }
-    }
-  }
-}
-
-// CRBA column j (thread j < nj): F = Ic_j S_j, M_jj = S_j^T F, then carried up
-// the ancestors i: M_ij = M_ji = S_i^T F. A: column-major, ld = lda; the
-// caller zeroes A first (entries of unrelated joints stay 0).
-MB_HD inline void crba_column(const Blk& b, const Vals& V, int j, double* A, int lda) {
-  const JRec Jj(b, j);
-  const double S[6] = {0., 0., 0., Jj.axis()[0], Jj.axis()[1], Jj.axis()[2]};
-  double F[6], t6[6];
-  inertia_mul(*V.cm(j), V.cc(j), V.cI(j), S, F);
-  A[(int64_t)j * lda + j] = dot3(Jj.axis(), F + 3) + b.arm[j];
-  int i = j;
-  while (true) {
-    const int lam = JRec(b, i).parent();
-    if (lam < 0) break;
-    force_act(V.R(i), V.p(i), F, t6);
-    for (int e = 0; e < 6; ++e) F[e] = t6[e];
-    i = lam;
-    const double Mij = dot3(JRec(b, i).axis(), F + 3);
-    A[(int64_t)j * lda + i] = Mij;
-    A[(int64_t)i * lda + j] = Mij;
-  }
-}
-
 // Phase executor: run(f) calls f(lane) for every thread of the workgroup and
 // then synchronises (device), or for lanes 0..nt-1 in order (host emulation,
 // tests/test_multibody_host.py). Within one phase no lane reads what another
@@ -377,12 +243,23 @@ MB_HD inline bool gauss_jordan(const X& ex, double* A, int nr, int nc, int* flag
       if (!(piv > 0.)) {
         if (lane == 0) *flag = 1;
       } else if (lane < nc && lane > k) {
+        // pivot column and own column in chunks of 8 rows through registers
+        // (independent loads, then the updates): no LDS round trip per row
         double* col = A + (int64_t)lane * nr;
         const double* pc = A + (int64_t)k * nr;
         const double akc = col[k] / piv;
-        for (int r = 0; r < nr; ++r)
-          if (r != k) col[r] -= pc[r] * akc;
-        col[k] = akc;
+        for (int r0 = 0; r0 < nr; r0 += 8) {
+          double pv[8], cv[8];
+#pragma unroll
+          for (int r = 0; r < 8; ++r)
+            if (r0 + r < nr) {
+              pv[r] = pc[r0 + r];
+              cv[r] = col[r0 + r];
+            }
+#pragma unroll
+          for (int r = 0; r < 8; ++r)
+            if (r0 + r < nr) col[r0 + r] = (r0 + r == k) ? akc : cv[r] - pv[r] * akc;
+        }
       }
     });
   }
@@ -392,79 +269,98 @@ MB_HD inline bool gauss_jordan(const X& ex, double* A, int nr, int nc, int* flag
 // ---- dual numbers for the log6 Jacobian -----------------------------------
 struct Dual {
   double v, d;
+  Dual() = default;
+  MB_HD constexpr Dual(double v_, double d_ = 0.) : v(v_), d(d_) {}
 };
 MB_HD __forceinline__ Dual operator+(Dual a, Dual b) { return {a.v + b.v, a.d + b.d}; }
 MB_HD __forceinline__ Dual operator-(Dual a, Dual b) { return {a.v - b.v, a.d - b.d}; }
 MB_HD __forceinline__ Dual operator*(Dual a, Dual b) { return {a.v * b.v, a.d * b.v + a.v * b.d}; }
 MB_HD __forceinline__ Dual operator*(double s, Dual a) { return {s * a.v, s * a.d}; }
 MB_HD __forceinline__ Dual operator/(Dual a, Dual b) { return {a.v / b.v, (a.d * b.v - a.v * b.d) / (b.v * b.v)}; }
-MB_HD __forceinline__ Dual dsqrt(Dual a) {
+MB_HD __forceinline__ Dual msqrt(Dual a) {
   const double s = sqrt(a.v);
   return {s, a.d / (2. * s)};
 }
-MB_HD __forceinline__ Dual dasin(Dual a) { return {asin(a.v), a.d / sqrt(1. - a.v * a.v)}; }
-MB_HD __forceinline__ Dual dacos(Dual a) { return {acos(a.v), -a.d / sqrt(1. - a.v * a.v)}; }
-MB_HD __forceinline__ Dual dsin(Dual a) { return {sin(a.v), a.d * cos(a.v)}; }
-MB_HD __forceinline__ Dual dcos(Dual a) { return {cos(a.v), -a.d * sin(a.v)}; }
+MB_HD __forceinline__ Dual masin(Dual a) { return {asin(a.v), a.d / sqrt(1. - a.v * a.v)}; }
+MB_HD __forceinline__ Dual macos(Dual a) { return {acos(a.v), -a.d / sqrt(1. - a.v * a.v)}; }
+MB_HD __forceinline__ Dual msin(Dual a) { return {sin(a.v), a.d * cos(a.v)}; }
+MB_HD __forceinline__ Dual mcos(Dual a) { return {cos(a.v), -a.d * sin(a.v)}; }
+MB_HD __forceinline__ double mval(Dual a) { return a.v; }
+MB_HD __forceinline__ double msqrt(double a) { return sqrt(a); }
+MB_HD __forceinline__ double masin(double a) { return asin(a); }
+MB_HD __forceinline__ double macos(double a) { return acos(a); }
+MB_HD __forceinline__ double msin(double a) { return sin(a); }
+MB_HD __forceinline__ double mcos(double a) { return cos(a); }
+MB_HD __forceinline__ double mval(double a) { return a; }
 
-// log6(R, p) -> (lin, ang) (pinocchio::log6), R column-major; in dual numbers
-// so that the tangent along (dR, dp) is Jlog6 * xi. Same branches as
+// log6(R, p) -> (lin, ang) (pinocchio::log6), R column-major. T = double, or
+// Dual so that the tangent along (dR, dp) is Jlog6 * xi. Same branches as
 // oracle/multibody_np.py:log3/log6.
-MB_HD inline void log6_dual(const Dual* R, const Dual* p, Dual* out) {
+template <class T>
+MB_HD inline void log6_t(const T* R, const T* p, T* out) {
   auto at = [&](int r, int c) { return R[c * 3 + r]; };
-  const Dual tr = at(0, 0) + at(1, 1) + at(2, 2);
-  const Dual c = 0.5 * (tr - Dual{1., 0.});
-  Dual w[3] = {at(2, 1) - at(1, 2), at(0, 2) - at(2, 0), at(1, 0) - at(0, 1)};
-  const Dual s2 = 0.25 * (w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
-  Dual om[3];
-  if (s2.v < 1e-8 && c.v > 0.) {
-    const Dual k = 0.5 * (Dual{1., 0.} + (1. / 6.) * s2 + (3. / 40.) * (s2 * s2) + (5. / 112.) * (s2 * s2 * s2));
+  const T one(1.);
+  const T tr = at(0, 0) + at(1, 1) + at(2, 2);
+  const T c = 0.5 * (tr - one);
+  const T w[3] = {at(2, 1) - at(1, 2), at(0, 2) - at(2, 0), at(1, 0) - at(0, 1)};
+  const T s2 = 0.25 * (w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+  T om[3];
+  T sth = T(0.), thg = T(0.);  // sin(theta), theta of the generic branch (beta reuses them)
+  bool generic = false;
+  if (mval(s2) < 1e-8 && mval(c) > 0.) {
+    const T k = 0.5 * (one + (1. / 6.) * s2 + (3. / 40.) * (s2 * s2) + (5. / 112.) * (s2 * s2 * s2));
     for (int e = 0; e < 3; ++e) om[e] = k * w[e];
-  } else if (s2.v < 1e-8) {  // theta near pi: axis from the symmetric part (value only)
+  } else if (mval(s2) < 1e-8) {  // theta near pi: axis from the symmetric part (value only)
     // (explicit selects: no runtime-indexed arrays, which would live in scratch)
-    const double cv = c.v < -1. ? -1. : c.v;
+    const double cv = mval(c) < -1. ? -1. : mval(c);
     const double th = acos(cv);
     auto axc = [&](double d) {
       const double t = (d - cv) / (1. - cv);
       return t > 0. ? sqrt(t) : 0.;
     };
-    const double a0 = axc(at(0, 0).v), a1 = axc(at(1, 1).v), a2 = axc(at(2, 2).v);
+    const double a0 = axc(mval(at(0, 0))), a1 = axc(mval(at(1, 1))), a2 = axc(mval(at(2, 2)));
     const int i0 = (a1 > a0) ? ((a2 > a1) ? 2 : 1) : ((a2 > a0) ? 2 : 0);
-    const double s01 = at(0, 1).v + at(1, 0).v, s02 = at(0, 2).v + at(2, 0).v, s12 = at(1, 2).v + at(2, 1).v;
+    const double s01 = mval(at(0, 1)) + mval(at(1, 0)), s02 = mval(at(0, 2)) + mval(at(2, 0)),
+                 s12 = mval(at(1, 2)) + mval(at(2, 1));
     auto sgn = [](double v) { return v >= 0. ? 1. : -1.; };
     const double g0 = i0 == 0 ? 1. : (i0 == 1 ? sgn(s01) : sgn(s02));
     const double g1 = i0 == 1 ? 1. : (i0 == 0 ? sgn(s01) : sgn(s12));
     const double g2 = i0 == 2 ? 1. : (i0 == 0 ? sgn(s02) : sgn(s12));
-    const double wi = i0 == 0 ? w[0].v : (i0 == 1 ? w[1].v : w[2].v);
+    const double wi = i0 == 0 ? mval(w[0]) : (i0 == 1 ? mval(w[1]) : mval(w[2]));
     const double flip = wi < 0. ? -th : th;
-    om[0] = Dual{flip * g0 * a0, 0.};
-    om[1] = Dual{flip * g1 * a1, 0.};
-    om[2] = Dual{flip * g2 * a2, 0.};
+    om[0] = T(flip * g0 * a0);
+    om[1] = T(flip * g1 * a1);
+    om[2] = T(flip * g2 * a2);
   } else {
-    const Dual s = dsqrt(s2);
-    Dual th;
-    if (c.v > 0.5)
-      th = dasin(s);
-    else if (c.v < -0.5)
-      th = Dual{M_PI, 0.} - dasin(s);
+    const T s = msqrt(s2);
+    T th;
+    if (mval(c) > 0.5)
+      th = masin(s);
+    else if (mval(c) < -0.5)
+      th = T(M_PI) - masin(s);
     else
-      th = dacos(c);
-    const Dual k = th / (2. * s);
+      th = macos(c);
+    const T k = th / (2. * s);
     for (int e = 0; e < 3; ++e) om[e] = k * w[e];
+    sth = s;
+    thg = th;
+    generic = true;
   }
-  const Dual t2 = om[0] * om[0] + om[1] * om[1] + om[2] * om[2];
-  Dual beta;
-  if (t2.v < 1e-2) {
-    beta = Dual{1. / 12., 0.} + (1. / 720.) * t2 + (1. / 30240.) * (t2 * t2) + (1. / 1209600.) * (t2 * t2 * t2);
+  const T t2 = om[0] * om[0] + om[1] * om[1] + om[2] * om[2];
+  T beta;
+  if (mval(t2) < 1e-2) {
+    beta = T(1. / 12.) + (1. / 720.) * t2 + (1. / 30240.) * (t2 * t2) + (1. / 1209600.) * (t2 * t2 * t2);
+  } else if (generic) {  // 1/t^2 - sin t / (2 t (1 - cos t)) with sin, cos of theta read off R
+    beta = one / (thg * thg) - sth / (2. * thg * (one - c));
   } else {
-    const Dual t = dsqrt(t2);
-    beta = Dual{1., 0.} / t2 - dsin(t) / (2. * t * (Dual{1., 0.} - dcos(t)));
+    const T t = msqrt(t2);
+    beta = one / t2 - msin(t) / (2. * t * (one - mcos(t)));
   }
   // v = (I - 0.5 [w]x + beta [w]x^2) p ; [w]x^2 p = w (w.p) - |w|^2 p
-  const Dual wp = om[0] * p[0] + om[1] * p[1] + om[2] * p[2];
-  const Dual wxp[3] = {om[1] * p[2] - om[2] * p[1], om[2] * p[0] - om[0] * p[2], om[0] * p[1] - om[1] * p[0]};
+  const T wp = om[0] * p[0] + om[1] * p[1] + om[2] * p[2];
+  const T wxp[3] = {om[1] * p[2] - om[2] * p[1], om[2] * p[0] - om[0] * p[2], om[0] * p[1] - om[1] * p[0]};
   for (int e = 0; e < 3; ++e) {
-    const Dual w2p = om[e] * wp - t2 * p[e];
+    const T w2p = om[e] * wp - t2 * p[e];
     out[e] = p[e] - 0.5 * wxp[e] + beta * w2p;
     out[3 + e] = om[e];
   }
@@ -479,8 +375,9 @@ struct CRec {
   MB_HD const double* d() const { return r + kCHdr; }
 };
 
-// oMf of a frame record d = [joint, R 9, p 3, ...]
-MB_HD inline void frame_placement(const Vals& V, const double* d, double* R, double* p) {
+// oMf of a frame record d = [joint, R 9, p 3, ...]; VT: any values type with oR(i), op(i)
+template <class VT>
+MB_HD inline void frame_placement(const VT& V, const double* d, double* R, double* p) {
   const int j = (int)d[0];
   matmul3(V.oR(j), d + 1, R);
   matvec3(V.oR(j), d + 10, p);
@@ -530,6 +427,10 @@ MB_HD inline int frame_residual(const Blk& b, const Vals& V, const CRec& C, int 
       r[e] = pf[e] - pref[e];
       if (Jc) Jc[e] = dp[e];
     }
+    for (int e = 3; e < 6; ++e) {
+      r[e] = 0.;
+      if (Jc) Jc[e] = 0.;
+    }
     return 3;
   }
   // rMf = Mref^-1 oMf
@@ -546,7 +447,7 @@ MB_HD inline int frame_residual(const Blk& b, const Vals& V, const CRec& C, int 
   Dual RD[9], PD[3], o[6];
   for (int e = 0; e < 9; ++e) RD[e] = Dual{Rr[e], dRr[e]};
   for (int e = 0; e < 3; ++e) PD[e] = Dual{pr[e], dpr[e]};
-  log6_dual(RD, PD, o);
+  log6_t<Dual>(RD, PD, o);
   for (int e = 0; e < 6; ++e) {
     r[e] = o[e].v;
     if (Jc) Jc[e] = sup ? o[e].d : 0.;
@@ -562,67 +463,407 @@ MB_HD inline int cost_nr(const CRec& C, int nx, int nu) {
 }
 MB_HD inline const double* cost_weights(const CRec& C, int nx, int nu) { return C.r + C.size() - cost_nr(C, nx, nu); }
 
+// Residual of a frame cost, value only (calc). Returns the residual size.
+template <class VT>
+MB_HD __forceinline__ int frame_residual_value(const VT& V, const CRec& C, double* r) {
+  const double* d = C.d();
+  double Rf[9], pf[3];
+  frame_placement(V, d, Rf, pf);
+  if (C.type() == C_FRAME_TRANSLATION) {
+    for (int e = 0; e < 3; ++e) r[e] = pf[e] - d[13 + e];
+    return 3;
+  }
+  double Rr[9], pr[3];
+  matmul3(d + 13, Rf, Rr);
+  matvec3(d + 13, pf, pr);
+  for (int e = 0; e < 3; ++e) pr[e] += d[22 + e];
+  log6_t<double>(Rr, pr, r);
+  return 6;
+}
+
+// 0.5 r^T W r of one cost record (kinematics in V).
+template <class VT>
+MB_HD __forceinline__ double cost_activation(const VT& V, const CRec& C, const double* x, const double* u, int nx, int nu) {
+  const double* w = cost_weights(C, nx, nu);
+  double a = 0.;
+  if (C.type() == C_STATE) {
+    for (int i = 0; i < nx; ++i) {
+      const double r = x[i] - C.d()[i];
+      a += w[i] * r * r;
+    }
+  } else if (C.type() == C_CONTROL) {
+    for (int i = 0; i < nu; ++i) {
+      const double r = u[i] - C.d()[i];
+      a += w[i] * r * r;
+    }
+  } else {
+    double r[6] = {0., 0., 0., 0., 0., 0.};
+    const int nr = frame_residual_value(V, C, r);
+#pragma unroll
+    for (int i = 0; i < 6; ++i)  // fixed trip count: r stays in registers
+      if (i < nr) a += w[i] * r[i] * r[i];
+  }
+  return 0.5 * a;
+}
+
 // Cost value of the DAM (one thread; kinematics in V): sum of weight * 0.5 r^T W r
 // in record (name) order (cost-sum.hxx:89-117).
-MB_HD inline double cost_value(const Blk& b, const Vals& V, const double* x, const double* u, int nx, int nu) {
+template <class VT>
+MB_HD inline double cost_value(const Blk& b, const VT& V, const double* x, const double* u, int nx, int nu) {
   double total = 0.;
   const double* cr = b.C;
   for (int k = 0; k < b.ncost; ++k) {
     const CRec C{cr};
-    const double* w = cost_weights(C, nx, nu);
-    double a = 0.;
-    if (C.type() == C_STATE) {
-      const double* xr = C.d();
-      for (int i = 0; i < nx; ++i) {
-        const double r = x[i] - xr[i];
-        a += w[i] * r * r;
-      }
-    } else if (C.type() == C_CONTROL) {
-      const double* ur = C.d();
-      for (int i = 0; i < nu; ++i) {
-        const double r = u[i] - ur[i];
-        a += w[i] * r * r;
-      }
-    } else {
-      double r[6];
-      const int nr = frame_residual(b, V, C, -1, r, nullptr);
-      for (int i = 0; i < nr; ++i) a += w[i] * r[i] * r[i];
-    }
-    total += C.weight() * (0.5 * a);
+    total += C.weight() * cost_activation(V, C, x, u, nx, nu);
     cr += C.size();
   }
   return total;
 }
 
-// LDS (doubles) of the calc scratch for nj joints: values + [M | b] + small.
-__host__ __device__ inline int64_t calc_work_doubles(int nj) {
-  return (int64_t)kValsPerJoint * nj + 12 + (int64_t)nj * (nj + 1) + 4 * nj + 8;
+// ---------------------------------------------------------------------------
+// World-frame dynamics (the calc path). Spatial quantities are expressed at
+// the world origin in world axes, so every recursion of RNEA/CRBA becomes a
+// sum over the ancestors or the subtree of a joint
+//   v_i = sum_{k <= i} S_k qd_k,  a_i = -g + sum_{k <= i} (S_k qdd_k + v_k x S_k qd_k),
+//   tau_i = S_i . sum_{k in subtree(i)} f_k,  Ic_i = sum_{k in subtree(i)} I_k,
+//   M_ij = S_i . (Ic_j S_j)  (i ancestor of j),
+// which each lane evaluates for its own joint: no serial chain through LDS.
+// The placements oMi = oMparent * liMi are composed by pointer jumping
+// (ceil(log2 nj) rounds). Same functions as the local-frame value_pass,
+// rounded differently (tests/test_multibody_host.py checks both vs the oracle).
+// ---------------------------------------------------------------------------
+constexpr int kWPerJoint = 96;
+constexpr int kMaxCosts = 64;
+struct WVals {
+  double* base;
+  int nj;
+  MB_HD double* R(int i) const { return base + kWPerJoint * i; }  // liMi rotation
+  MB_HD double* p(int i) const { return R(i) + 9; }
+  MB_HD double* oR(int i) const { return R(i) + 12; }  // oMi (also pointer-jumping buffer A)
+  MB_HD double* op(int i) const { return R(i) + 21; }
+  MB_HD double* S(int i) const { return R(i) + 24; }   // joint motion subspace (world)
+  MB_HD double* m(int i) const { return R(i) + 30; }   // body mass
+  MB_HD double* c(int i) const { return R(i) + 31; }   // body CoM (world)
+  MB_HD double* Ic(int i) const { return R(i) + 34; }  // body inertia about its CoM, world axes (6)
+  MB_HD double* v(int i) const { return R(i) + 40; }
+  MB_HD double* a(int i) const { return R(i) + 46; }
+  MB_HD double* F(int i) const { return R(i) + 52; }   // body force, then accumulated joint force
+  MB_HD double* cm(int i) const { return R(i) + 58; }  // composite inertia, origin form: m, h = m c, I_O (6)
+  MB_HD double* ch(int i) const { return R(i) + 59; }
+  MB_HD double* cI(int i) const { return R(i) + 62; }
+  MB_HD double* cq(int i) const { return R(i) + 68; }  // S_i qdd_i + v_i x S_i qd_i
+  MB_HD double* Rb(int i) const { return R(i) + 74; }  // pointer-jumping buffer B
+  MB_HD double* pb(int i) const { return R(i) + 83; }
+  MB_HD double* jA(int i) const { return R(i) + 86; }  // jump targets of buffers A / B
+  MB_HD double* jB(int i) const { return R(i) + 87; }
+  MB_HD double* fb(int i) const { return R(i) + 90; }  // body force I a + v x* I v
+  MB_HD unsigned* anc(int i) const { return (unsigned*)(base + kWPerJoint * nj) + i; }  // ancestors-or-self bits
+  MB_HD double* root_a() const { return base + kWPerJoint * nj + (nj + 1) / 2 + 1; }
+  MB_HD static int64_t doubles(int nj) { return (int64_t)kWPerJoint * nj + (nj + 1) / 2 + 1 + 6; }
+};
+
+MB_HD inline int jump_rounds(int nj) {
+  int r = 0;
+  while ((1 << r) < nj) ++r;
+  return r;
+}
+
+MB_HD __forceinline__ double dot6(const double* a, const double* b) {
+  return a[0] * b[0] + a[1] * b[1] + a[2] * b[2] + a[3] * b[3] + a[4] * b[4] + a[5] * b[5];
+}
+
+// lane i < nj: local placement (buffer A starts as liMi), ancestor bits.
+MB_HD inline void w_joint_local(const Blk& b, const WVals& W, const double* q, int i) {
+  const JRec J(b, i);
+  double ax[3], Rpl[9], R[9];
+  for (int e = 0; e < 3; ++e) ax[e] = J.axis()[e];
+  for (int e = 0; e < 9; ++e) Rpl[e] = J.Rpl()[e];
+  joint_rotation(Rpl, ax, q[i], R);
+  for (int e = 0; e < 9; ++e) {
+    W.R(i)[e] = R[e];
+    W.oR(i)[e] = R[e];
+  }
+  for (int e = 0; e < 3; ++e) {
+    W.p(i)[e] = J.ppl()[e];
+    W.op(i)[e] = J.ppl()[e];
+  }
+  *W.jA(i) = (double)J.parent();
+  if (i == 0) {
+    for (int e = 0; e < 6; ++e) W.root_a()[e] = e < 3 ? -b.g[e] : 0.;
+  }
+  unsigned m = 1u << i;
+  for (int k = J.parent(); k >= 0; k = JRec(b, k).parent()) m |= 1u << k;
+  *W.anc(i) = m;
+}
+
+// lane i < nj, round r: T_i <- T_j(i) o T_i, j(i) <- j(j(i)) (A -> B on even
+// rounds, B -> A on odd ones).
+MB_HD inline void w_jump(const WVals& W, int i, int r) {
+  const bool ab = (r & 1) == 0;
+  double* sR = ab ? W.oR(i) : W.Rb(i);
+  double* sp = ab ? W.op(i) : W.pb(i);
+  double* dR = ab ? W.Rb(i) : W.oR(i);
+  double* dp = ab ? W.pb(i) : W.op(i);
+  const int j = (int)*(ab ? W.jA(i) : W.jB(i));
+  double R[9], p[3];
+  for (int e = 0; e < 9; ++e) R[e] = sR[e];
+  for (int e = 0; e < 3; ++e) p[e] = sp[e];
+  if (j >= 0) {
+    double Rj[9], pj[3], Ro[9], t[3];
+    const double* jR = ab ? W.oR(j) : W.Rb(j);
+    const double* jp = ab ? W.op(j) : W.pb(j);
+    for (int e = 0; e < 9; ++e) Rj[e] = jR[e];
+    for (int e = 0; e < 3; ++e) pj[e] = jp[e];
+    matmul3(Rj, R, Ro);
+    matvec3(Rj, p, t);
+    for (int e = 0; e < 9; ++e) dR[e] = Ro[e];
+    for (int e = 0; e < 3; ++e) dp[e] = pj[e] + t[e];
+    *(ab ? W.jB(i) : W.jA(i)) = *(ab ? W.jA(j) : W.jB(j));
+  } else {
+    for (int e = 0; e < 9; ++e) dR[e] = R[e];
+    for (int e = 0; e < 3; ++e) dp[e] = p[e];
+    *(ab ? W.jB(i) : W.jA(i)) = -1.;
+  }
+}
+
+// lane i < nj: oMi into oR/op (from buffer B after an odd number of rounds),
+// world motion subspace and body inertia.
+MB_HD inline void w_joint_world(const Blk& b, const WVals& W, int i, bool from_b) {
+  const JRec J(b, i);
+  double oR[9], op[3], w[3], vl[3], c[3], t[3];
+  for (int e = 0; e < 9; ++e) oR[e] = from_b ? W.Rb(i)[e] : W.oR(i)[e];
+  for (int e = 0; e < 3; ++e) op[e] = from_b ? W.pb(i)[e] : W.op(i)[e];
+  if (from_b) {
+    for (int e = 0; e < 9; ++e) W.oR(i)[e] = oR[e];
+    for (int e = 0; e < 3; ++e) W.op(i)[e] = op[e];
+  }
+  matvec3(oR, J.axis(), w);
+  cross3(op, w, vl);  // velocity of the world origin: w x (0 - op) = op x w
+  matvec3(oR, J.com(), t);
+  for (int e = 0; e < 3; ++e) c[e] = op[e] + t[e];
+  // Ic_w = oR Ic oR^T
+  const double* s = J.I6();
+  const double Is[9] = {s[0], s[3], s[4], s[3], s[1], s[5], s[4], s[5], s[2]};
+  double tmp[9], Iw[9];
+  matmul3(oR, Is, tmp);
+  for (int r = 0; r < 3; ++r)
+    for (int cc = 0; cc < 3; ++cc) Iw[cc * 3 + r] = tmp[r] * oR[cc] + tmp[3 + r] * oR[3 + cc] + tmp[6 + r] * oR[6 + cc];
+  for (int e = 0; e < 3; ++e) {
+    W.S(i)[e] = vl[e];
+    W.S(i)[3 + e] = w[e];
+    W.c(i)[e] = c[e];
+  }
+  *W.m(i) = J.mass();
+  double* o = W.Ic(i);
+  o[0] = Iw[0];
+  o[1] = Iw[4];
+  o[2] = Iw[8];
+  o[3] = Iw[3];
+  o[4] = Iw[6];
+  o[5] = Iw[7];
+}
+
+// lane i < nj: composite inertia of the subtree of i in origin form
+// (m, h = m c, I_O = Ic + m (|c|^2 I - c c^T)): additive over the subtree.
+MB_HD inline void w_composite(const Blk& b, const WVals& W, int i) {
+  double m = 0., h[3] = {0., 0., 0.}, I[6] = {0., 0., 0., 0., 0., 0.};
+  for (int k = i; k < b.nj; ++k) {
+    if (!((*W.anc(k) >> i) & 1u)) continue;
+    const double mk = *W.m(k);
+    double c[3], Ic[6];
+    for (int e = 0; e < 3; ++e) c[e] = W.c(k)[e];
+    for (int e = 0; e < 6; ++e) Ic[e] = W.Ic(k)[e];
+    const double cc = c[0] * c[0] + c[1] * c[1] + c[2] * c[2];
+    m += mk;
+    for (int e = 0; e < 3; ++e) h[e] += mk * c[e];
+    I[0] += Ic[0] + mk * (cc - c[0] * c[0]);
+    I[1] += Ic[1] + mk * (cc - c[1] * c[1]);
+    I[2] += Ic[2] + mk * (cc - c[2] * c[2]);
+    I[3] += Ic[3] - mk * c[0] * c[1];
+    I[4] += Ic[4] - mk * c[0] * c[2];
+    I[5] += Ic[5] - mk * c[1] * c[2];
+  }
+  *W.cm(i) = m;
+  for (int e = 0; e < 3; ++e) W.ch(i)[e] = h[e];
+  for (int e = 0; e < 6; ++e) W.cI(i)[e] = I[e];
+}
+
+// lane i < nj: v_i = sum over ancestors-or-self of S_k qd_k
+MB_HD inline void w_velocity(const WVals& W, const double* qd, int i) {
+  double v[6] = {0., 0., 0., 0., 0., 0.};
+  const unsigned am = *W.anc(i);
+  for (int k = 0; k <= i; ++k) {
+    if (!((am >> k) & 1u)) continue;
+    const double w = qd[k];
+    for (int e = 0; e < 6; ++e) v[e] += W.S(k)[e] * w;
+  }
+  for (int e = 0; e < 6; ++e) W.v(i)[e] = v[e];
+}
+
+// lane i < nj: cq_i = S_i qdd_i + v_i x (S_i qd_i)
+MB_HD inline void w_accel_term(const WVals& W, const double* qd, const double* qdd, int i) {
+  double S[6], v[6], Sw[6], t6[6];
+  const double w = qd[i], qa = qdd ? qdd[i] : 0.;
+  for (int e = 0; e < 6; ++e) {
+    S[e] = W.S(i)[e];
+    v[e] = W.v(i)[e];
+    Sw[e] = S[e] * w;
+  }
+  cross_m(v, Sw, t6);
+  for (int e = 0; e < 6; ++e) W.cq(i)[e] = S[e] * qa + t6[e];
+}
+
+// lane i < nj: a_i = -g + sum over ancestors-or-self of cq_k, then the body
+// force f_i = I_i a_i + v_i x* (I_i v_i)
+MB_HD inline void w_accel_force(const WVals& W, int i) {
+  double a[6];
+  for (int e = 0; e < 6; ++e) a[e] = W.root_a()[e];
+  const unsigned am = *W.anc(i);
+  for (int k = 0; k <= i; ++k) {
+    if (!((am >> k) & 1u)) continue;
+    for (int e = 0; e < 6; ++e) a[e] += W.cq(k)[e];
+  }
+  double v[6], f[6], Iv[6], t6[6], c[3], I6[6];
+  for (int e = 0; e < 6; ++e) {
+    W.a(i)[e] = a[e];
+    v[e] = W.v(i)[e];
+    I6[e] = W.Ic(i)[e];
+  }
+  for (int e = 0; e < 3; ++e) c[e] = W.c(i)[e];
+  const double m = *W.m(i);
+  inertia_mul(m, c, I6, a, f);
+  inertia_mul(m, c, I6, v, Iv);
+  cross_f(v, Iv, t6);
+  for (int e = 0; e < 6; ++e) W.fb(i)[e] = f[e] + t6[e];
+}
+
+// lane i < nj: F_i = sum over the subtree of the body forces, tau_i = S_i . F_i
+MB_HD inline void w_joint_force(const Blk& b, const WVals& W, double* tau, int i) {
+  double F[6] = {0., 0., 0., 0., 0., 0.};
+  for (int k = i; k < b.nj; ++k) {
+    if (!((*W.anc(k) >> i) & 1u)) continue;
+    for (int e = 0; e < 6; ++e) F[e] += W.fb(k)[e];
+  }
+  for (int e = 0; e < 6; ++e) W.F(i)[e] = F[e];
+  tau[i] = dot6(W.S(i), F);
+}
+
+// lane j < nj: CRBA column j in world frame: F = Ic_j S_j, M_ij = S_i . F for
+// the ancestors-or-self i of j (+ armature on the diagonal). A: ld lda, zeroed.
+MB_HD inline void w_crba_column(const Blk& b, const WVals& W, int j, double* A, int lda) {
+  double S[6], F[6], t[3];
+  for (int e = 0; e < 6; ++e) S[e] = W.S(j)[e];
+  const double m = *W.cm(j);
+  const double* h = W.ch(j);
+  const double* I = W.cI(j);
+  // (m v - h x w, I_O w + h x v)
+  cross3(h, S + 3, t);
+  for (int e = 0; e < 3; ++e) F[e] = m * S[e] - t[e];
+  cross3(h, S, t);
+  F[3] = I[0] * S[3] + I[3] * S[4] + I[4] * S[5] + t[0];
+  F[4] = I[3] * S[3] + I[1] * S[4] + I[5] * S[5] + t[1];
+  F[5] = I[4] * S[3] + I[5] * S[4] + I[2] * S[5] + t[2];
+  A[(int64_t)j * lda + j] = dot6(S, F) + b.arm[j];
+  const unsigned am = *W.anc(j);
+  for (int i = 0; i < j; ++i) {
+    if (!((am >> i) & 1u)) continue;
+    const double Mij = dot6(W.S(i), F);
+    A[(int64_t)j * lda + i] = Mij;
+    A[(int64_t)i * lda + j] = Mij;
+  }
+}
+
+// Placements, world quantities, composite inertias and M (into A, zeroed by
+// the caller) for configuration q; `costs(wave, l)` runs on waves >= 2 in
+// the phase after the kinematics (nullptr-like no-op allowed).
+template <class X, class CostF>
+MB_HD inline void world_kinematics(const X& ex, const Blk& b, const WVals& W, const double* q, double* A,
+                                   CostF costs) {
+  const int nj = b.nj, R = jump_rounds(nj);
+  ex.run([&](int lane) {
+    if (lane < nj) w_joint_local(b, W, q, lane);
+  });
+  for (int r = 0; r < R; ++r)
+    ex.run([&](int lane) {
+      if (lane < nj) w_jump(W, lane, r);
+    });
+  ex.run([&](int lane) {
+    if (lane < nj) w_joint_world(b, W, lane, (R & 1) != 0);
+  });
+  ex.run([&](int lane) {
+    const int wave = lane >> 6, l = lane & 63;
+    if (wave == 0 && l < nj) w_composite(b, W, l);
+    if (wave >= 2) costs(wave, l);
+  });
+  ex.run([&](int lane) {
+    if (lane < nj) w_crba_column(b, W, lane, A, nj);
+  });
+}
+
+// Joint torques of RNEA(q, qd, qdd) (qdd == nullptr: 0) with the kinematics in W.
+template <class X>
+MB_HD inline void world_rnea(const X& ex, const Blk& b, const WVals& W, const double* qd, const double* qdd,
+                             double* tau) {
+  const int nj = b.nj;
+  ex.run([&](int lane) {
+    if (lane < nj) w_velocity(W, qd, lane);
+  });
+  ex.run([&](int lane) {
+    if (lane < nj) w_accel_term(W, qd, qdd, lane);
+  });
+  ex.run([&](int lane) {
+    if (lane < nj) w_accel_force(W, lane);
+  });
+  ex.run([&](int lane) {
+    if (lane < nj) w_joint_force(b, W, tau, lane);
+  });
+}
+
+// LDS (doubles) of the calc scratch for nj joints.
+MB_HD inline int64_t calc_work_doubles(int nj) {
+  return WVals::doubles(nj) + (int64_t)nj * (nj + 1) + 2 * nj + kMaxCosts + 8;
 }
 
 // model->calc(data, x, u) for the Euler∘FreeFwdDynamics knot (euler.hxx:41-80,
-// free-fwddyn.hxx:44-79). Lanes < 64 do the work; every thread of the
-// workgroup must call (phases end in barriers). x, u readable by all lanes;
+// free-fwddyn.hxx:44-79): a = (M + diag(armature))^-1 (u - nle) in world frame.
+// Needs >= 256 threads (4 waves): independent work of one phase runs on
+// different waves (divergent lanes of one wave would serialise) — wave 0 the
+// recursions, wave 1 composite inertias and CRBA, waves 2-3 the cost records.
+// Every thread must call (phases end in barriers). x, u readable by all lanes;
 // writes xnext[0..nx) and returns the knot cost. `w`: calc_work_doubles(nj).
 template <class X>
 MB_HD inline double knot_calc_x(const X& ex, const double* P, int nx, const double* x, const double* u, bool use_u,
                                 double* xnext, double* w) {
   const Blk b = parse(P);
   const int nj = b.nj;
-  const Vals V{w, nj};
-  double* A = w + (int64_t)kValsPerJoint * nj + 12;  // nj x (nj + 1), ld nj
-  double* tau = A + (int64_t)nj * (nj + 1);          // nle
-  double* ub = tau + nj;                              // u (zero if !use_u)
-  double* red = ub + nj;
-  int* flag = (int*)(red + 2 * nj + 4);
+  const WVals W{w, nj};
+  double* A = w + WVals::doubles(nj);  // nj x (nj + 1), ld nj
+  double* tau = A + (int64_t)nj * (nj + 1);
+  double* ub = tau + nj;  // u (zero if !use_u)
+  double* cv = ub + nj;   // per-cost activations
+  double* red = cv + kMaxCosts;
+  int* flag = (int*)(red + 2);
   ex.run([&](int lane) {
     if (lane < nj) ub[lane] = use_u ? u[lane] : 0.;
     for (int e = lane; e < nj * (nj + 1); e += ex.nt) A[e] = 0.;
-    if (lane == 0) value_pass(b, x, x + nj, nullptr, V, tau, true, true);
   });
+  // cost records k on wave 2 + (k & 1), lane k >> 1, once the placements exist
+  world_kinematics(ex, b, W, x, A, [&](int wave, int l) {
+    const double* cr = b.C;
+    for (int k = 0; k < b.ncost; ++k) {
+      const CRec C{cr};
+      if (wave == 2 + (k & 1) && l == (k >> 1)) cv[k] = C.weight() * cost_activation(W, C, x, ub, nx, nj);
+      cr += C.size();
+    }
+  });
+  world_rnea(ex, b, W, x + nj, nullptr, tau);
   ex.run([&](int lane) {
-    if (lane < nj) crba_column(b, V, lane, A, nj);
-    if (lane == 0) red[0] = cost_value(b, V, x, ub, nx, nj);
     if (lane < nj) A[(int64_t)nj * nj + lane] = ub[lane] - tau[lane];
+    if (lane == 64) {
+      double total = 0.;
+      for (int k = 0; k < b.ncost; ++k) total += cv[k];
+      red[0] = total;
+    }
   });
   const bool ok = gauss_jordan(ex, A, nj, nj + 1, flag);
   const double cc = red[0];
@@ -646,6 +887,7 @@ MB_HD inline double knot_calc_x(const X& ex, const double* P, int nx, const doub
 template <int NT>
 __device__ inline double knot_calc(const double* P, int nx, const double* x, const double* u, bool use_u, double* xnext,
                                    double* w) {
+  static_assert(NT >= 256, "the multibody calc splits its phases over 4 waves");
   return knot_calc_x(DevExec{NT}, P, nx, x, u, use_u, xnext, w);
 }
 
@@ -653,12 +895,13 @@ __device__ inline double knot_calc(const double* P, int nx, const double* x, con
 // calcDiff: one 64-thread workgroup per (element, knot).
 // ---------------------------------------------------------------------------
 struct DiffLayout {
-  int64_t vals, A, tang, dtau, J, xu, red, total;
+  int64_t wv, vals, A, tang, dtau, J, xu, red, total;
 };
 __host__ __device__ inline DiffLayout diff_layout(int nj, int nframe) {
   const int L = 2 * nj;
   DiffLayout l;
-  l.vals = 0;
+  l.wv = 0;
+  l.vals = l.wv + pad2(WVals::doubles(nj));
   l.A = l.vals + (int64_t)kValsPerJoint * nj + 12;
   l.tang = l.A + (int64_t)nj * 2 * nj;          // [M | I] -> [. | Minv]
   l.dtau = l.tang + (int64_t)18 * nj * L;       // per lane: dv, da, df per joint, [i][c][L]
@@ -754,10 +997,13 @@ MB_HD inline void rnea_tangent(const Blk& b, const Vals& V, const double* qd, in
 // beyond nu zero); Lxu is zero (no cost couples x and u). A mass matrix that is
 // not positive definite leaves NaN in Fx/Fu, which the backward pass reports
 // as backward_error. `w`: diff_layout(nj, nframe).total doubles of LDS.
+// xnext_out / cost_out (may be null): the knot's calc (xnext, cost) as well;
+// Fx == nullptr: calc only (no derivative block is written).
 template <class X>
 MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, const double* xg, const double* ug,
                                    bool use_u, double* w, double* Fx, double* Fu, double* Lxx, double* Lxu,
-                                   double* Luu, double* Lx, double* Lu) {
+                                   double* Luu, double* Lx, double* Lu, double* xnext_out = nullptr,
+                                   double* cost_out = nullptr) {
   const Blk b = parse(P);
   const int nj = b.nj, n = nx, L = 2 * nj;
   int nframe = 0;
@@ -770,6 +1016,7 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
     }
   }
   const DiffLayout l = diff_layout(nj, nframe);
+  const WVals W{w + l.wv, nj};
   const Vals V{w + l.vals, nj};
   double* A = w + l.A;
   double* T = w + l.tang;
@@ -788,13 +1035,9 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
       A[e] = (c == nj + r) ? 1. : 0.;
     }
   });
-  // nle -> dtau[0..nj), composite inertias and placements
-  ex.run([&](int lane) {
-    if (lane == 0) value_pass(b, x, x + nj, nullptr, V, dtau, true, true);
-  });
-  ex.run([&](int lane) {
-    if (lane < nj) crba_column(b, V, lane, A, nj);
-  });
+  // world-frame kinematics, M into the left half of [M | I], nle -> dtau[0..nj)
+  world_kinematics(ex, b, W, x, A, [](int, int) {});
+  world_rnea(ex, b, W, x + nj, nullptr, dtau);
   const bool ok = gauss_jordan(ex, A, nj, 2 * nj, flag);
   const double* Minv = A + (int64_t)nj * nj;  // column-major nj x nj
   // a = (M + A)^-1 (tau - nle) -> dtau[nj..2nj)
@@ -805,10 +1048,67 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
     dtau[nj + lane] = ok ? s : NAN;
   });
   // accelerations and forces at the solved a (the linearisation point of
-  // computeABADerivatives); tau lands in red-free scratch dtau[2nj..3nj)
-  ex.run([&](int lane) {
-    if (lane == 0) value_pass(b, x, x + nj, dtau + nj, V, dtau + 2 * nj, false, false);
+  // computeABADerivatives); tau lands in dtau[2nj..3nj) and is not used
+  world_rnea(ex, b, W, x + nj, dtau + nj, dtau + 2 * nj);
+  // joint-frame values for the tangent recursion: liMi, oMi, and v, a, F moved
+  // from world to joint coordinates (SE3::actInv of oMi)
+  ex.run([&](int i) {
+    if (i == 0)
+      for (int e = 0; e < 6; ++e) {
+        V.root_v()[e] = 0.;
+        V.root_a()[e] = e < 3 ? -b.g[e] : 0.;
+      }
+    if (i >= nj) return;
+    double oR[9], op[3], t6[6], m6[6];
+    for (int e = 0; e < 9; ++e) {
+      oR[e] = W.oR(i)[e];
+      V.R(i)[e] = W.R(i)[e];
+      V.oR(i)[e] = oR[e];
+    }
+    for (int e = 0; e < 3; ++e) {
+      op[e] = W.op(i)[e];
+      V.p(i)[e] = W.p(i)[e];
+      V.op(i)[e] = op[e];
+    }
+    for (int e = 0; e < 6; ++e) m6[e] = W.v(i)[e];
+    motion_act_inv(oR, op, m6, t6);
+    for (int e = 0; e < 6; ++e) V.v(i)[e] = t6[e];
+    for (int e = 0; e < 6; ++e) m6[e] = W.a(i)[e];
+    motion_act_inv(oR, op, m6, t6);
+    for (int e = 0; e < 6; ++e) V.a(i)[e] = t6[e];
+    // force actInv: f' = R^T f, n' = R^T (n - p x f)
+    double f[3], nn[3], c[3];
+    for (int e = 0; e < 3; ++e) {
+      f[e] = W.F(i)[e];
+      nn[e] = W.F(i)[3 + e];
+    }
+    cross3(op, f, c);
+    for (int e = 0; e < 3; ++e) nn[e] -= c[e];
+    matTvec3(oR, f, t6);
+    matTvec3(oR, nn, t6 + 3);
+    for (int e = 0; e < 6; ++e) V.F(i)[e] = t6[e];
   });
+  if (xnext_out || cost_out) {  // the knot's calc, fused (iteration 0 of a solve, or calc only)
+    ex.run([&](int lane) {
+      const double dt = b.dt;
+      if (xnext_out && lane < nj) {
+        const double ai = dtau[nj + lane];
+        if (dt != 0.) {
+          const double v = x[nj + lane];
+          xnext_out[lane] = x[lane] + (v * dt + ai * dt * dt);
+          xnext_out[nj + lane] = v + ai * dt;
+        } else {
+          xnext_out[lane] = x[lane];
+          xnext_out[nj + lane] = x[nj + lane];
+        }
+      }
+      if (cost_out && lane == 0) {
+        const double cc = cost_value(b, W, x, u, nx, nj);
+        *cost_out = dt != 0. ? dt * cc : cc;
+      }
+    });
+  }
+  if (!Fx) return;  // calc only
   // tangents (lanes < 2 nj) and frame-cost residuals / Jacobian columns (lanes < nj)
   ex.run([&](int lane) {
     if (lane < L) rnea_tangent(b, V, x + nj, lane < nj ? 0 : 1, lane % nj, T, L, lane, dtau);
@@ -820,9 +1120,12 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
       if (C.type() == C_FRAME_PLACEMENT || C.type() == C_FRAME_TRANSLATION) {
         double r[6], Jc[6];
         const int nr = frame_residual(b, V, C, lane, r, Jc);
-        for (int e = 0; e < nr; ++e) Jf[((int64_t)f * 6 + e) * nj + lane] = Jc[e];
-        if (lane == 0)
-          for (int e = 0; e < nr; ++e) rf[6 * f + e] = r[e];
+#pragma unroll
+        for (int e = 0; e < 6; ++e)
+          if (e < nr) {
+            Jf[((int64_t)f * 6 + e) * nj + lane] = Jc[e];
+            if (lane == 0) rf[6 * f + e] = r[e];
+          }
         ++f;
       }
       cr += C.size();
@@ -924,8 +1227,8 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
 
 __device__ inline void knot_calc_diff(const double* P, int nx, int m, const double* xg, const double* ug, bool use_u,
                                       double* w, double* Fx, double* Fu, double* Lxx, double* Lxu, double* Luu,
-                                      double* Lx, double* Lu) {
-  knot_calc_diff_x(DevExec{64}, P, nx, m, xg, ug, use_u, w, Fx, Fu, Lxx, Lxu, Luu, Lx, Lu);
+                                      double* Lx, double* Lu, double* xnext_out, double* cost_out) {
+  knot_calc_diff_x(DevExec{64}, P, nx, m, xg, ug, use_u, w, Fx, Fu, Lxx, Lxu, Luu, Lx, Lu, xnext_out, cost_out);
 }
 
 }  // namespace mb

@@ -20,6 +20,8 @@ CONFIGS = {
     "C3_talos_arm": ("euler", 7, 7, 250, 512, 1e-3),
     "C4_solo12": ("euler", 18, 12, 60, 1024, 1e-2),
     "C5_talos_full": ("euler", 38, 32, 100, 1024, 1e-3),
+    # C3 on real multibody knots: Euler ∘ FreeFwdDynamics of the 7-DoF arm (build_arm)
+    "C3_arm_multibody": ("multibody", 7, 7, 250, 512, 1e-3),
 }
 
 
@@ -73,6 +75,8 @@ def build(name, T=None, B=None, seed=None, drift_free=True):
     kind, d1, nu, T0, B0, dt = CONFIGS[name]
     T = T0 if T is None else T
     B = B0 if B is None else B
+    if kind == "multibody":
+        return build_arm(T=T, B=B, seed=seed)
     rng = np.random.default_rng(seed_of(name) if seed is None else seed)
     if kind == "unicycle":
         model = ActionModelUnicycle()

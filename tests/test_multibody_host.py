@@ -29,7 +29,7 @@ def lib():
     L = C.CDLL(OUT)
     L.mb_host_calc.restype = C.c_double
     L.mb_host_calc.argtypes = [D, C.c_int, D, D, C.c_int, D]
-    L.mb_host_calc_diff.argtypes = [D, C.c_int, C.c_int, D, D, C.c_int] + [D] * 7
+    L.mb_host_calc_diff.argtypes = [D, C.c_int, C.c_int, D, D, C.c_int] + [D] * 9
     return L
 
 
@@ -64,8 +64,12 @@ def test_device_code_vs_oracle(lib, case, terminal):
         n, m = nx, nu
         out = {q: np.zeros(s) for q, s in [("Fx", n * n), ("Fu", n * m), ("Lxx", n * n), ("Lxu", n * m),
                                            ("Luu", m * m), ("Lx", n), ("Lu", m)]}
+        xn2, c2 = np.zeros(nx), np.zeros(1)
         lib.mb_host_calc_diff(_p(blk), nx, m, _p(x), _p(u), use_u,
-                              *[_p(out[q]) for q in ["Fx", "Fu", "Lxx", "Lxu", "Luu", "Lx", "Lu"]])
+                              *[_p(out[q]) for q in ["Fx", "Fu", "Lxx", "Lxu", "Luu", "Lx", "Lu"]], _p(xn2), _p(c2))
+        # the calc fused into calcDiff (iteration 0 of a solve)
+        np.testing.assert_allclose(xn2, xo, rtol=1e-12, atol=1e-12)
+        assert c2[0] == pytest.approx(co, rel=1e-12, abs=1e-14)
         ref = k.calc_diff(x, uo)
         for q, a in out.items():
             rows = m if q == "Luu" else n
