@@ -34,6 +34,7 @@
 #endif
 
 #include "../include/fddp_hip.h"
+#include "multibody_oracle.hpp"
 
 namespace oracle {
 
@@ -258,6 +259,12 @@ static void calc(const Model& m, Data& d, const double* x, const double* u_in) {
       }
       break;
     }
+    case FDDP_KNOT_EULER_FREEFWD: {  // euler.hxx:41-80 around free-fwddyn.hxx:44-79 (multibody_oracle.hpp)
+      mbo::Knot k;
+      k.parse(m.p);
+      k.calc(x, u, d.xnext.data(), &d.cost);
+      break;
+    }
   }
 }
 
@@ -333,6 +340,13 @@ static void calcDiff(const Model& m, Data& d, const double* x, const double* u_i
         d.Lxu.a = d.dLxu.a;
         d.Luu.a = d.dLuu.a;
       }
+      break;
+    }
+    case FDDP_KNOT_EULER_FREEFWD: {  // euler.hxx:83-131 around free-fwddyn.hxx:82-118 (multibody_oracle.hpp)
+      mbo::Knot k;
+      k.parse(m.p);
+      k.calc_diff(x, u, m.nu, d.Fx.a.data(), d.Fu.a.data(), d.Lxx.a.data(), d.Lxu.a.data(), d.Luu.a.data(),
+                  d.Lx.data(), d.Lu.data());
       break;
     }
   }

@@ -39,8 +39,8 @@ def lib(path=None):
         _bind(L)
         return L
     if _lib is None:
-        if not os.path.exists(ORACLE_SO) or os.path.getmtime(ORACLE_SO) < os.path.getmtime(
-                os.path.join(ORACLE_DIR, "fddp_oracle.cpp")):
+        srcs = [os.path.join(ORACLE_DIR, f) for f in ("fddp_oracle.cpp", "multibody_oracle.hpp")]
+        if not os.path.exists(ORACLE_SO) or os.path.getmtime(ORACLE_SO) < max(os.path.getmtime(f) for f in srcs):
             build()
         _lib = C.CDLL(ORACLE_SO)
         _bind(_lib)

@@ -160,3 +160,75 @@ def test_knot_derivatives_vs_numdiff(weighted, dt):
     Lzz = np.block([[d["Lxx"], d["Lxu"]], [d["Lxu"].T, d["Luu"]]])
     np.testing.assert_allclose(Lzz, Lzz.T, atol=1e-12)
     assert np.linalg.eigvalsh(Lzz).min() > -1e-10
+
+
+# ---- C++ oracle restatement (oracle/multibody_oracle.hpp) vs the numpy one ----
+def _cpp_setup(T, B, **kw):
+    import oracle_lib
+    from crocoddyl_amd import _abi
+    from crocoddyl_amd.problem import pack_problem
+    from oracle import fddp_np
+    from crocoddyl_amd import synthetic
+    x0s, running, terminal = synthetic.build_arm(T=T, B=B, **kw)
+    knots, pool = pack_problem(running, terminal, B)
+    nx, nu = running[0].state.nx, running[0].nu
+    dims = _abi.Dims(nx, nx, nu, T, B)
+    o = oracle_lib.Oracle(dims, knots, pool, x0s, threads=2)
+    models = [fddp_np.bind_problem(knots, pool, b, nx) for b in range(B)]
+    return o, models, x0s, dims
+
+
+CPP_CASES = [dict(), dict(weighted=True), dict(robot=mb.sample_tree(6, seed=4), weighted=True),
+             dict(robot=mb.sample_tree(9, seed=8, branching=False), armature=np.full(9, 0.05))]
+
+
+@pytest.mark.parametrize("case", range(len(CPP_CASES)))
+def test_cpp_oracle_knots_vs_numpy(case):
+    """ABA + analytic RNEA derivatives (C++) vs ABA + complex step (numpy)."""
+    from crocoddyl_amd import _abi
+    o, models, x0s, d = _cpp_setup(5, 2, dt=1e-2, **CPP_CASES[case])
+    rng = np.random.default_rng(case)
+    xs = np.repeat(x0s[:, None, :], d.T + 1, axis=1) + 0.1 * rng.standard_normal((d.B, d.T + 1, d.nx))
+    us = rng.uniform(-2, 2, (d.B, d.T, d.nu_max))
+    o.set_candidate(xs, us)
+    cost = o.calc()
+    xn = o.quantity(_abi.Q_XNEXT, d.T, d.nx)
+    o.calc_diff()
+    n, m = d.nx, d.nu_max
+    Q = {k: o.quantity(q, d.T + 1, s) for k, q, s in [("Fx", _abi.Q_FX, n * n), ("Fu", _abi.Q_FU, n * m),
+                                                      ("Lxx", _abi.Q_LXX, n * n), ("Lx", _abi.Q_LX, n),
+                                                      ("Luu", _abi.Q_LUU, m * m), ("Lu", _abi.Q_LU, m)]}
+    for b in range(d.B):
+        tot = 0.0
+        for t in range(d.T + 1):
+            k = models[b][t]
+            u = us[b, t] if t < d.T else None
+            xo, co = k.calc(xs[b, t], u)
+            tot += co
+            if t < d.T:
+                np.testing.assert_allclose(xn[b, t], xo, rtol=1e-12, atol=1e-13)
+            ref = k.calc_diff(xs[b, t], u)
+            for name, shape in [("Fx", (n, n)), ("Fu", (n, m)), ("Lxx", (n, n)), ("Luu", (m, m)), ("Lx", (n,)),
+                                ("Lu", (m,))]:
+                got = Q[name][b, t].reshape(shape[::-1]).T if len(shape) == 2 else Q[name][b, t]
+                scale = max(1.0, float(np.max(np.abs(ref[name]))))
+                assert float(np.max(np.abs(got - ref[name]))) / scale < 1e-10, (case, b, t, name)
+        assert cost[b] == pytest.approx(tot, rel=1e-12)
+
+
+@pytest.mark.parametrize("case", [0, 3])
+def test_cpp_oracle_solve_vs_numpy(case):
+    from crocoddyl_amd import _abi
+    from oracle import fddp_np
+    T, B = 15, 2
+    o, models, x0s, d = _cpp_setup(T, B, dt=1e-2, w_x=1e-2, w_u=1e-2, **CPP_CASES[case])
+    o.set_candidate(np.repeat(x0s[:, None, :], T + 1, axis=1), None)
+    r = o.solve(maxiter=25, is_feasible=False, reg_init=1e-9)
+    xs = o.xs()
+    for b in range(B):
+        n = fddp_np.FDDP(x0s[b], models[b])
+        conv = n.solve([x0s[b]] * (T + 1), None, maxiter=25, is_feasible=False, reg_init=1e-9)
+        assert conv and r[b].status == _abi.STATUS_CONVERGED
+        assert r[b].iter == n.iter
+        assert r[b].cost == pytest.approx(n.cost, rel=1e-9)
+        np.testing.assert_allclose(xs[b], np.array(n.xs), rtol=1e-8, atol=1e-9)
