@@ -44,17 +44,41 @@ BOX_LIMIT = 1.0  # --solver boxfddp: |u_i| <= 1 on every running knot (~30% of t
 
 def cpu_baseline(cfg, T, seed, target_s=12.0, box=False):
     """Time the CPU oracle (C++ port of the reference solver, OpenMP over batch
-    elements) on this host, on a bounded sample of the same workload."""
+    elements) on this host, on a bounded sample of the same workload. Runs in a
+    child process: first the -march=native build, and if that fails (the
+    native build of the multibody oracle crashes on some host CPUs under gcc
+    11) the in-tree -march=x86-64-v3 build; the sample string says which."""
+    import subprocess
+    errs = []
+    for arch in ("native", "x86-64-v3"):
+        cmd = [sys.executable, os.path.abspath(__file__), "--cpu-baseline-child", cfg, str(T), str(seed),
+               str(target_s), "1" if box else "0", arch]
+        try:
+            p = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+        except subprocess.TimeoutExpired:
+            errs.append(f"{arch}: timeout")
+            continue
+        lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+        if p.returncode == 0 and lines:
+            out = json.loads(lines[-1])
+            if errs:
+                out["sample"] += f" (native build failed: {'; '.join(errs)})"
+            return out
+        errs.append(f"{arch}: exit {p.returncode}")
+    return {"error": "; ".join(errs)}
+
+
+def _cpu_baseline_child(cfg, T, seed, target_s, box, arch):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import helpers
     import oracle_lib
 
-    out = os.path.join("/tmp", f"oracle_native_{os.getpid()}")
-    try:
+    if arch == "native":
+        out = os.path.join("/tmp", f"oracle_native_{os.getpid()}")
         oracle_lib.build(out_dir=out, arch="-march=native")
         oracle_lib._lib = oracle_lib.lib(os.path.join(out, "liboracle.so"))
         flags = "-O3 -march=native"
-    except Exception:
+    else:
         oracle_lib._lib = None  # the in-tree x86-64-v3 build
         flags = "-O3 -march=x86-64-v3"
     try:
@@ -90,10 +114,10 @@ def cpu_baseline(cfg, T, seed, target_s=12.0, box=False):
     Bs = int(max(threads, min(1024, target_s * (it / max(dt, 1e-9)) / steps)))
     Bs = max(threads, (Bs // threads) * threads)
     it, dt = run(Bs, steps)
-    return {"value": it / dt, "unit": "FDDP iterations/s", "cores": threads, "kind": "port",
-            "sample": f"{cfg} T={T}: {Bs} elements x {steps} warm-started solve(maxiter={2 if box else 1}) "
-                      f"({it} element-iterations in {dt:.1f} s); oracle/fddp_oracle.cpp {flags} -fopenmp, "
-                      f"OpenMP over elements{', SolverBoxFDDP |u| <= 1' if box else ''}"}
+    print(json.dumps({"value": it / dt, "unit": "FDDP iterations/s", "cores": threads, "kind": "port",
+                      "sample": f"{cfg} T={T}: {Bs} elements x {steps} warm-started solve(maxiter={2 if box else 1}) "
+                                f"({it} element-iterations in {dt:.1f} s); oracle/fddp_oracle.cpp {flags} -fopenmp, "
+                                f"OpenMP over elements{', SolverBoxFDDP |u| <= 1' if box else ''}"}), flush=True)
 
 
 def load_pmc(cfg):
@@ -104,6 +128,10 @@ def load_pmc(cfg):
 
 
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "--cpu-baseline-child":
+        a = sys.argv[2:]
+        _cpu_baseline_child(a[0], int(a[1]), int(a[2]), float(a[3]), a[4] == "1", a[5])
+        return
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)

@@ -148,3 +148,33 @@ def test_steps_vs_oracle(case):
             assert helpers.rel_err(xt[b], np.array(o.xs_try)) < 1e-8, (alpha, b)
             assert helpers.rel_err(ut[b], np.array(o.us_try)) < 1e-8, (alpha, b)
             assert abs(dV[b] - dVo) <= 1e-8 * max(1.0, abs(dVo)), (alpha, b, dV[b], dVo)
+
+
+def test_full_size_c3_vs_cpp_oracle():
+    """C3 at full size (7-DoF arm, T = 250, B = 512, the factory's weights):
+    a warm-started MPC step (solve(maxiter=1, regInit=0.1)) of every element;
+    all finite, and spot elements identical to the C++ oracle (identical
+    branch decisions, xs / us / cost within 1e-6)."""
+    import oracle_lib
+    x0s, running, terminal = synthetic.build("C3_arm_multibody")
+    B, T = x0s.shape[0], len(running)
+    knots, pool = pack_problem(running, terminal, B)
+    d = _abi.Dims(14, 14, 7, T, B)
+    g = helpers.Gpu(d, knots, pool, x0s)
+    g.set_candidate(None, None)
+    r = helpers.results_dict(g.solve(maxiter=1, is_feasible=False, reg_init=0.1))
+    xs, us = g.xs(), g.us()
+    assert np.all(np.isfinite(r["cost"])) and np.all(np.isfinite(xs)) and np.all(np.isfinite(us))
+    spots = [0, 1, 257, B - 1]
+    sub = np.array(spots)
+    ds = _abi.Dims(14, 14, 7, T, len(spots))
+    ks, ps = pack_problem(running, terminal, len(spots))
+    o = oracle_lib.Oracle(ds, ks, ps, x0s[sub], threads=4)
+    o.set_candidate(None, None, False)
+    ro = o.solve(maxiter=1, is_feasible=False, reg_init=0.1)
+    xo, uo = o.xs(), o.us()
+    for i, b in enumerate(spots):
+        assert r["steplength"][b] == ro[i].steplength and r["status"][b] == ro[i].status
+        assert abs(r["cost"][b] - ro[i].cost) <= 1e-6 * abs(ro[i].cost)
+        assert helpers.rel_err(xs[b], xo[i]) < 1e-6
+        assert helpers.rel_err(us[b], uo[i]) < 1e-6
