@@ -78,6 +78,7 @@ struct Dev {
   double* dQuuInv;                 // debug [B][T][sMM] Quu_inv_ (null unless debug + box)
   BoxQPCfg boxcfg;                 // qp_(nu, 100, 0.1, 1e-5, 0.) (box-fddp.cpp:16)
   int64_t mbw;                     // LDS doubles of the multibody calc scratch (0: no multibody knots)
+  int64_t mbd;                     // LDS doubles of the multibody calcDiff work area (its parameter block follows)
   __device__ bool box_knot(int b, int t) const { return box && haslim && haslim[(int64_t)b * T + t]; }
 
   __device__ __host__ int64_t knot(int b, int t) const { return (int64_t)b * (T + 1) + t; }

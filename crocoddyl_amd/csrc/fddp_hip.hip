@@ -118,7 +118,8 @@ int64_t mb_block_check(const double* P, int64_t avail, int nx, int nu, std::stri
   }
   if (o != size) return why = "block size does not match its records", -1;
   if (nframe > kMaxFrameCosts) return why = "more than 8 frame costs in one knot", -1;
-  if (diff_layout(nj, nframe).total * 8 > 160 * 1024) return why = "too many joints for the calcDiff LDS plan", -1;
+  if ((pad2(diff_layout(nj, nframe).total) + pad2(size)) * 8 > 160 * 1024)
+    return why = "too many joints for the calcDiff LDS plan", -1;
   if (nj_out) *nj_out = std::max(*nj_out, nj);
   if (nframe_out) *nframe_out = std::max(*nframe_out, nframe);
   return size;
@@ -548,7 +549,15 @@ int apply_knots(fddp_handle* h, const fddp_knot_desc* knots, const double* param
     h->all_mb = true;
     for (int t = 0; t <= d.T; ++t) h->all_mb = h->all_mb && knots[t].kind == FDDP_KNOT_EULER_FREEFWD;
     D.mbw = h->has_mb ? pad2(fddp::mb::calc_work_doubles(mb_nj)) : 0;
-    h->mb_diff_smem = h->has_mb ? sizeof(double) * fddp::mb::diff_layout(mb_nj, mb_nframe).total : 0;
+    int64_t mb_pmax = 0;  // largest multibody parameter block (staged in LDS by mb_knot_kernel)
+    for (int t = 0; t <= d.T; ++t)
+      if (knots[t].kind == FDDP_KNOT_EULER_FREEFWD) {
+        const int nb = knots[t].param_stride > 0 ? d.B : 1;
+        for (int b = 0; b < nb; ++b)
+          mb_pmax = std::max<int64_t>(mb_pmax, (int64_t)params[knots[t].param_offset + (int64_t)b * knots[t].param_stride + 3]);
+      }
+    D.mbd = h->has_mb ? pad2(fddp::mb::diff_layout(mb_nj, mb_nframe).total) : 0;
+    h->mb_diff_smem = h->has_mb ? sizeof(double) * (D.mbd + pad2(mb_pmax)) : 0;
     const int64_t budget = (150 * 1024) / 8 - (2 * D.sX + D.sM + 5 * (kNT / kWave) + 16) - D.mbw;
     h->pcap = pmax <= budget ? pad2(pmax) : 0;
   }

@@ -221,13 +221,19 @@ __global__ __launch_bounds__(64) void mb_knot_kernel(Dev D, int sel_calc, int se
   const double* ug = running ? D.us[c] + D.run(b, t) * D.sM : nullptr;
   double* xn = (do_calc && running) ? D.xnext[c] + D.run(b, t) * D.sX : nullptr;
   double* cost = do_calc ? D.kcost[c] + kk : nullptr;
+  // the parameter block is read in every phase: stage it in LDS (D.mbp doubles, after the work area)
+  const double* Pg = D.pblock(b, t);
+  double* P = sm + D.mbd;
+  const int psz = (int)Pg[3];
+  for (int e = threadIdx.x; e < psz; e += 64) P[e] = Pg[e];
+  __syncthreads();
   if (do_diff)
-    mb::knot_calc_diff(D.pblock(b, t), D.nx, D.m, xg, ug, running && kd.nu > 0, sm, D.Fx + kk * D.sNN,
-                       D.Fu + kk * D.sNM, D.Lxx + kk * D.sNN, D.Lxu + kk * D.sNM, D.Luu + kk * D.sMM,
-                       D.Lx + kk * D.sN, D.Lu + kk * D.sM, xn, cost);
+    mb::knot_calc_diff(P, D.nx, D.m, xg, ug, running && kd.nu > 0, sm, D.Fx + kk * D.sNN, D.Fu + kk * D.sNM,
+                       D.Lxx + kk * D.sNN, D.Lxu + kk * D.sNM, D.Luu + kk * D.sMM, D.Lx + kk * D.sN,
+                       D.Lu + kk * D.sM, xn, cost);
   else
-    mb::knot_calc_diff(D.pblock(b, t), D.nx, D.m, xg, ug, running && kd.nu > 0, sm, nullptr, nullptr, nullptr,
-                       nullptr, nullptr, nullptr, nullptr, xn, cost);
+    mb::knot_calc_diff(P, D.nx, D.m, xg, ug, running && kd.nu > 0, sm, nullptr, nullptr, nullptr, nullptr, nullptr,
+                       nullptr, nullptr, xn, cost);
 }
 
 // ---------------------------------------------------------------------------

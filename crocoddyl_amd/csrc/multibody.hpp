@@ -1102,7 +1102,7 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
           xnext_out[nj + lane] = x[nj + lane];
         }
       }
-      if (cost_out && lane == 0) {
+      if (cost_out && !Fx && lane == 0) {  // calc only (with derivatives: from the residuals below)
         const double cc = cost_value(b, W, x, u, nx, nj);
         *cost_out = dt != 0. ? dt * cc : cc;
       }
@@ -1134,44 +1134,38 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
   const double dt = b.dt, dt2 = dt * dt;
   const bool integ = dt != 0.;
   const double sc = integ ? dt : 1.;
+  // Output blocks, entry by entry over all lanes (consecutive lanes write
+  // consecutive addresses of the column-major blocks).
   ex.run([&](int lane) {
-    // Fx column `lane` (< n): da/dx = -Minv dtau(:, lane)
-    if (lane < n) {
-      double* col = Fx + (int64_t)lane * n;
-      for (int i = 0; i < nj; ++i) {
+    // Fx(i, c): da/dx = -Minv dtau(:, c), Euler assembly (euler.hxx:100-112)
+    for (int e = lane; e < n * n; e += ex.nt) {
+      const int c = e / n, i = e % n, r = i < nj ? i : i - nj;
+      double f;
+      if (integ) {
         double s = 0.;
-        for (int k = 0; k < nj; ++k) s += Minv[(int64_t)k * nj + i] * dtau[(int64_t)k * L + lane];
+        for (int k = 0; k < nj; ++k) s += Minv[(int64_t)k * nj + r] * dtau[(int64_t)k * L + c];
         const double da = ok ? -s : NAN;
-        double top, bot;
-        if (integ) {
-          top = da * dt2 + (lane == nj + i ? dt : 0.) + (lane == i ? 1. : 0.);
-          bot = da * dt + (lane == nj + i ? 1. : 0.);
-        } else {
-          top = lane == i ? 1. : 0.;
-          bot = lane == nj + i ? 1. : 0.;
-        }
-        col[i] = top;
-        col[nj + i] = bot;
+        f = i < nj ? da * dt2 + (c == nj + i ? dt : 0.) + (c == i ? 1. : 0.) : da * dt + (c == i ? 1. : 0.);
+      } else {
+        f = c == i ? 1. : 0.;
       }
+      Fx[e] = f;
     }
-    // Fu column `lane` (< m): Minv(:, lane) (ActuationModelFull: dtau/du = I)
-    if (lane < m) {
-      double* col = Fu + (int64_t)lane * n;
-      for (int i = 0; i < n; ++i) {
-        double f = 0.;
-        if (integ && lane < nj) {
-          const double mi = ok ? Minv[(int64_t)lane * nj + (i < nj ? i : i - nj)] : NAN;
-          f = i < nj ? mi * dt2 : mi * dt;
-        }
-        col[i] = f;
+    // Fu(i, c) = Minv(i mod nj, c) dt^2 | dt (ActuationModelFull: dtau/du = I); Lxu = 0
+    for (int e = lane; e < n * m; e += ex.nt) {
+      const int c = e / n, i = e % n;
+      double f = 0.;
+      if (integ && c < nj) {
+        const double mi = ok ? Minv[(int64_t)c * nj + (i < nj ? i : i - nj)] : NAN;
+        f = i < nj ? mi * dt2 : mi * dt;
       }
+      Fu[e] = f;
+      Lxu[e] = 0.;
     }
-    // cost derivatives (Gauss-Newton): Lx[lane], Lxx column `lane`
-    if (lane < n) {
-      const int j = lane;
-      double lx = 0.;
-      double* col = Lxx + (int64_t)j * n;
-      for (int i = 0; i < n; ++i) col[i] = 0.;
+    // Lxx(i, j): Gauss-Newton, cost-sum.hxx:122-160
+    for (int e = lane; e < n * n; e += ex.nt) {
+      const int j = e / n, i = e % n;
+      double l = 0.;
       const double* cr = b.C;
       int f = 0;
       for (int k = 0; k < b.ncost; ++k) {
@@ -1179,48 +1173,95 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
         const double wt = C.weight();
         const double* wv = cost_weights(C, nx, nj);
         if (C.type() == C_STATE) {
-          lx += wt * wv[j] * (x[j] - C.d()[j]);
-          col[j] += wt * wv[j];
+          if (i == j) l += wt * wv[j];
         } else if (C.type() == C_FRAME_PLACEMENT || C.type() == C_FRAME_TRANSLATION) {
-          const int nr = C.type() == C_FRAME_PLACEMENT ? 6 : 3;
-          if (j < nj) {
+          if (i < nj && j < nj) {
+            const int nr = C.type() == C_FRAME_PLACEMENT ? 6 : 3;
             const double* Jk = Jf + (int64_t)f * 6 * nj;
-            for (int r = 0; r < nr; ++r) lx += wt * Jk[(int64_t)r * nj + j] * wv[r] * rf[6 * f + r];
-            for (int i = 0; i < nj; ++i) {
-              double s = 0.;
-              for (int r = 0; r < nr; ++r) s += Jk[(int64_t)r * nj + i] * wv[r] * Jk[(int64_t)r * nj + j];
-              col[i] += wt * s;
-            }
+            double s2 = 0.;
+            for (int r = 0; r < nr; ++r) s2 += Jk[(int64_t)r * nj + i] * wv[r] * Jk[(int64_t)r * nj + j];
+            l += wt * s2;
           }
           ++f;
         }
         cr += C.size();
       }
-      Lx[j] = integ ? sc * lx : lx;
-      if (integ)
-        for (int i = 0; i < n; ++i) col[i] *= sc;
+      Lxx[e] = integ ? sc * l : l;
     }
-    // Lu[lane], Luu / Lxu columns `lane` (< m)
+    // Luu (diagonal), Lu, Lx
+    for (int e = lane; e < m * m; e += ex.nt) {
+      const int j = e / m, i = e % m;
+      double l = 0.;
+      if (i == j && j < nj) {
+        const double* cr = b.C;
+        for (int k = 0; k < b.ncost; ++k) {
+          const CRec C{cr};
+          if (C.type() == C_CONTROL) l += C.weight() * cost_weights(C, nx, nj)[j];
+          cr += C.size();
+        }
+      }
+      Luu[e] = integ ? sc * l : l;
+    }
     if (lane < m) {
       const int j = lane;
-      double lu = 0., luu = 0.;
+      double lu = 0.;
       if (j < nj) {
         const double* cr = b.C;
         for (int k = 0; k < b.ncost; ++k) {
           const CRec C{cr};
-          if (C.type() == C_CONTROL) {
-            const double* wv = cost_weights(C, nx, nj);
-            lu += C.weight() * wv[j] * (u[j] - C.d()[j]);
-            luu += C.weight() * wv[j];
-          }
+          if (C.type() == C_CONTROL) lu += C.weight() * cost_weights(C, nx, nj)[j] * (u[j] - C.d()[j]);
           cr += C.size();
         }
       }
       Lu[j] = integ ? sc * lu : lu;
-      double* col = Luu + (int64_t)j * m;
-      for (int i = 0; i < m; ++i) col[i] = (i == j) ? (integ ? sc * luu : luu) : 0.;
-      double* cx = Lxu + (int64_t)j * n;
-      for (int i = 0; i < n; ++i) cx[i] = 0.;
+    }
+    {
+      const int j = lane;
+      if (j < n) {
+        double lx = 0.;
+        const double* cr = b.C;
+        int f = 0;
+        for (int k = 0; k < b.ncost; ++k) {
+          const CRec C{cr};
+          const double wt = C.weight();
+          const double* wv = cost_weights(C, nx, nj);
+          if (C.type() == C_STATE) {
+            lx += wt * wv[j] * (x[j] - C.d()[j]);
+          } else if (C.type() == C_FRAME_PLACEMENT || C.type() == C_FRAME_TRANSLATION) {
+            const int nr = C.type() == C_FRAME_PLACEMENT ? 6 : 3;
+            if (j < nj) {
+              const double* Jk = Jf + (int64_t)f * 6 * nj;
+              for (int r = 0; r < nr; ++r) lx += wt * Jk[(int64_t)r * nj + j] * wv[r] * rf[6 * f + r];
+            }
+            ++f;
+          }
+          cr += C.size();
+        }
+        Lx[j] = integ ? sc * lx : lx;
+      }
+    }
+    // the fused calc's cost: frame residuals from the Jacobian phase (cost-sum.hxx:89-117)
+    if (cost_out && lane == 0) {
+      double total = 0.;
+      const double* cr = b.C;
+      int f = 0;
+      for (int k = 0; k < b.ncost; ++k) {
+        const CRec C{cr};
+        const double* wv = cost_weights(C, nx, nj);
+        double a = 0.;
+        if (C.type() == C_STATE) {
+          for (int i = 0; i < nx; ++i) a += wv[i] * (x[i] - C.d()[i]) * (x[i] - C.d()[i]);
+        } else if (C.type() == C_CONTROL) {
+          for (int i = 0; i < nj; ++i) a += wv[i] * (u[i] - C.d()[i]) * (u[i] - C.d()[i]);
+        } else {
+          const int nr = C.type() == C_FRAME_PLACEMENT ? 6 : 3;
+          for (int i = 0; i < nr; ++i) a += wv[i] * rf[6 * f + i] * rf[6 * f + i];
+          ++f;
+        }
+        total += C.weight() * (0.5 * a);
+        cr += C.size();
+      }
+      *cost_out = integ ? dt * total : total;
     }
   });
 }
