@@ -9,6 +9,11 @@
 
 namespace fddp {
 
+// Multibody knots (variable-size blocks, multibody.hpp): free and contact dynamics.
+__host__ __device__ inline bool is_mb_kind(int kind) {
+  return kind == FDDP_KNOT_EULER_FREEFWD || kind == FDDP_KNOT_EULER_CONTACTFWD;
+}
+
 constexpr int kWave = 64;
 
 // Per-element FDDP state machine (SolverAbstract/SolverDDP/SolverFDDP members,

@@ -69,11 +69,12 @@ int64_t block_doubles(int kind, int nx, int nu) {
 }
 
 
-// Checks one FDDP_KNOT_EULER_FREEFWD block (layout in include/fddp_hip.h)
-// against nx / nu and the space left in the pool. Returns its size in doubles,
-// or -1 with `why` set. nj / nframe: joints and frame costs (LDS sizing).
-int64_t mb_block_check(const double* P, int64_t avail, int nx, int nu, std::string& why, int* nj_out,
-                       int* nframe_out) {
+// Checks one FDDP_KNOT_EULER_FREEFWD / _CONTACTFWD block (layouts in
+// include/fddp_hip.h) against nx / nu and the space left in the pool. Returns
+// its size in doubles, or -1 with `why` set. nj / nframe / nc: joints, frame
+// costs and contact rows (LDS sizing).
+int64_t mb_block_check(const double* P, int64_t avail, int kind, int nx, int nu, std::string& why, int* nj_out,
+                       int* nframe_out, int* nc_out) {
   using namespace fddp::mb;
   if (avail < FDDP_PARAM_HEADER) return why = "block out of range", -1;
   const double dt = P[0];
@@ -81,8 +82,9 @@ int64_t mb_block_check(const double* P, int64_t avail, int nx, int nu, std::stri
   const int64_t size = (int64_t)P[3];
   if (!(dt >= 0.) || !std::isfinite(dt)) return why = "dt has positive value", -1;
   if ((double)nj != P[1] || nj < 1 || nj > kMaxJ) return why = "number of joints out of [1, 32]", -1;
-  if (nx != 2 * nj) return why = "free-fwddyn knots need nx = 2 nv", -1;
-  if (nu != nj) return why = "ActuationModelFull needs nu = nv", -1;
+  if (nx != 2 * nj) return why = "multibody knots need nx = 2 nv", -1;
+  const bool contact = kind == FDDP_KNOT_EULER_CONTACTFWD;
+  if (!contact && nu != nj) return why = "ActuationModelFull needs nu = nv", -1;
   if ((double)ncost != P[2] || ncost < 0 || ncost > kMaxCosts) return why = "number of costs out of [0, 64]", -1;
   if (size > avail || (double)size != P[3]) return why = "block out of range", -1;
   int64_t o = FDDP_PARAM_HEADER + 3 + nj;
@@ -104,7 +106,7 @@ int64_t mb_block_check(const double* P, int64_t avail, int nx, int nu, std::stri
     const int64_t rs = (int64_t)C[3];
     int64_t want = -1;
     if (type == C_STATE) want = kCHdr + 2 * nx;
-    if (type == C_CONTROL) want = kCHdr + 2 * nu;
+    if (type == C_CONTROL) want = kCHdr + 2 * (int64_t)nu;
     if (type == C_FRAME_PLACEMENT) want = kCHdr + 31;
     if (type == C_FRAME_TRANSLATION) want = kCHdr + 19;
     if (want < 0) return why = "unknown cost type " + std::to_string(type), -1;
@@ -116,12 +118,41 @@ int64_t mb_block_check(const double* P, int64_t avail, int nx, int nu, std::stri
     }
     o += rs;
   }
+  int nc = 0;
+  if (contact) {  // [nun, damping, ncontact, 0] + contact records
+    if (o + 4 > size) return why = "contact section out of range", -1;
+    const int nun = (int)P[o], ncon = (int)P[o + 2];
+    const double damping = P[o + 1];
+    if ((double)nun != P[o] || nun < 0 || nun >= nj) return why = "unactuated dofs out of [0, nv)", -1;
+    if (nu != nj - nun) return why = "ActuationModelFloatingBase needs nu = nv - nun", -1;
+    if (!(damping >= 0.) || !std::isfinite(damping)) return why = "The damping factor has to be positive", -1;
+    if ((double)ncon != P[o + 2] || ncon < 0) return why = "negative number of contacts", -1;
+    o += 4;
+    for (int k = 0; k < ncon; ++k) {
+      if (o + kCHdr + 1 > size) return why = "contact records out of range", -1;
+      const double* C = P + o;
+      const int type = (int)C[0];
+      const int64_t rs = (int64_t)C[3];
+      int64_t want = -1;
+      if (type == C_CONTACT_3D) want = kCHdr + 16;
+      if (type == C_CONTACT_6D) want = kCHdr + 25;
+      if (want < 0) return why = "unknown contact type " + std::to_string(type), -1;
+      if (rs != want || o + rs > size) return why = "contact record of the wrong size", -1;
+      const int fj = (int)C[kCHdr];
+      if ((double)fj != C[kCHdr] || fj < 0 || fj >= nj) return why = "contact frame attached to an unknown joint", -1;
+      if (!std::isfinite(C[1]) || !std::isfinite(C[2])) return why = "non-finite contact gains", -1;
+      nc += type == C_CONTACT_3D ? 3 : 6;
+      o += rs;
+    }
+    if (nc > kMaxNc) return why = "more than 24 contact rows in one knot", -1;
+  }
   if (o != size) return why = "block size does not match its records", -1;
   if (nframe > kMaxFrameCosts) return why = "more than 8 frame costs in one knot", -1;
-  if ((pad2(diff_layout(nj, nframe).total) + pad2(size)) * 8 > 160 * 1024)
+  if ((pad2(diff_layout(nj, nframe, nc).total) + pad2(size)) * 8 > 160 * 1024)
     return why = "too many joints for the calcDiff LDS plan", -1;
   if (nj_out) *nj_out = std::max(*nj_out, nj);
   if (nframe_out) *nframe_out = std::max(*nframe_out, nframe);
+  if (nc_out) *nc_out = std::max(*nc_out, nc);
   return size;
 }
 
@@ -145,14 +176,14 @@ int check_knots(const fddp_dims& d, const fddp_knot_desc* knots, const double* p
     if (k.param_offset < 0 || k.param_stride < 0 || k.param_offset + (int64_t)(d.B - 1) * k.param_stride >= n_params)
       return fail(FDDP_ERR_INVALID_ARG, w + ": knot " + std::to_string(t) + " parameter block out of range");
     int64_t sz;
-    if (k.kind == FDDP_KNOT_EULER_FREEFWD) {
+    if (is_mb_kind(k.kind)) {
       if (!params) return fail(FDDP_ERR_INVALID_ARG, w + ": null parameter pool");
       sz = 0;
       const int nb = k.param_stride > 0 ? d.B : 1;
       for (int b = 0; b < nb; ++b) {
         const int64_t off = k.param_offset + (int64_t)b * k.param_stride;
         std::string why;
-        const int64_t s1 = mb_block_check(params + off, n_params - off, d.nx, k.nu, why, nullptr, nullptr);
+        const int64_t s1 = mb_block_check(params + off, n_params - off, k.kind, d.nx, k.nu, why, nullptr, nullptr, nullptr);
         if (s1 < 0) return fail(FDDP_ERR_INVALID_ARG, w + ": knot " + std::to_string(t) + ": " + why);
         if (k.param_stride > 0 && s1 > k.param_stride)
           return fail(FDDP_ERR_INVALID_ARG, w + ": knot " + std::to_string(t) + " blocks overlap (stride too small)");
@@ -528,18 +559,19 @@ int apply_knots(fddp_handle* h, const fddp_knot_desc* knots, const double* param
   h->knots.assign(knots, knots + K1);
   {
     int64_t pmax = 0;
-    int mb_nj = 0, mb_nframe = 0;
+    int mb_nj = 0, mb_nframe = 0, mb_nc = 0;
     h->has_mb = false;
     for (int t = 0; t <= d.T; ++t) {
       int64_t sz;
-      if (knots[t].kind == FDDP_KNOT_EULER_FREEFWD) {
+      if (is_mb_kind(knots[t].kind)) {
         h->has_mb = true;
         sz = 0;
         const int nb = knots[t].param_stride > 0 ? d.B : 1;
         for (int b = 0; b < nb; ++b) {  // validated by check_knots
           const int64_t off = knots[t].param_offset + (int64_t)b * knots[t].param_stride;
           std::string why;
-          sz = std::max(sz, mb_block_check(params + off, n_params - off, d.nx, knots[t].nu, why, &mb_nj, &mb_nframe));
+          sz = std::max(sz, mb_block_check(params + off, n_params - off, knots[t].kind, d.nx, knots[t].nu, why, &mb_nj,
+                                           &mb_nframe, &mb_nc));
         }
       } else {
         sz = block_doubles(knots[t].kind, d.nx, knots[t].nu);
@@ -547,16 +579,16 @@ int apply_knots(fddp_handle* h, const fddp_knot_desc* knots, const double* param
       pmax = std::max<int64_t>(pmax, sz);
     }
     h->all_mb = true;
-    for (int t = 0; t <= d.T; ++t) h->all_mb = h->all_mb && knots[t].kind == FDDP_KNOT_EULER_FREEFWD;
-    D.mbw = h->has_mb ? pad2(fddp::mb::calc_work_doubles(mb_nj)) : 0;
+    for (int t = 0; t <= d.T; ++t) h->all_mb = h->all_mb && is_mb_kind(knots[t].kind);
+    D.mbw = h->has_mb ? pad2(fddp::mb::calc_work_doubles(mb_nj, mb_nc)) : 0;
     int64_t mb_pmax = 0;  // largest multibody parameter block (staged in LDS by mb_knot_kernel)
     for (int t = 0; t <= d.T; ++t)
-      if (knots[t].kind == FDDP_KNOT_EULER_FREEFWD) {
+      if (is_mb_kind(knots[t].kind)) {
         const int nb = knots[t].param_stride > 0 ? d.B : 1;
         for (int b = 0; b < nb; ++b)
           mb_pmax = std::max<int64_t>(mb_pmax, (int64_t)params[knots[t].param_offset + (int64_t)b * knots[t].param_stride + 3]);
       }
-    D.mbd = h->has_mb ? pad2(fddp::mb::diff_layout(mb_nj, mb_nframe).total) : 0;
+    D.mbd = h->has_mb ? pad2(fddp::mb::diff_layout(mb_nj, mb_nframe, mb_nc).total) : 0;
     h->mb_diff_smem = h->has_mb ? sizeof(double) * (D.mbd + pad2(mb_pmax)) : 0;
     const int64_t budget = (150 * 1024) / 8 - (2 * D.sX + D.sM + 5 * (kNT / kWave) + 16) - D.mbw;
     h->pcap = pmax <= budget ? pad2(pmax) : 0;

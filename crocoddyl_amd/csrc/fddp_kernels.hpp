@@ -12,7 +12,7 @@ namespace fddp {
 // Doubles in a knot's parameter block (layouts in include/fddp_hip.h); the
 // multibody block carries its size in its header (g: the block).
 __device__ inline int64_t block_doubles_dev(int kind, int nx, int nu, const double* g = nullptr) {
-  if (kind == FDDP_KNOT_EULER_FREEFWD) return (int64_t)g[3];
+  if (is_mb_kind(kind)) return (int64_t)g[3];
   if (kind == FDDP_KNOT_LQR) return FDDP_PARAM_HEADER + 2LL * nx * nx + 2LL * nx * nu + (int64_t)nu * nu + 2LL * nx + nu;
   if (kind == FDDP_KNOT_UNICYCLE) return FDDP_PARAM_HEADER;
   const int64_t nq = nx / 2;
@@ -104,7 +104,7 @@ __global__ __launch_bounds__(NT) void calc_kernel(Dev D, int sel, int64_t pcap, 
   const double* cached = nullptr;
   for (int t = 0; t <= D.T; ++t) {
     const fddp_knot_desc kd = D.knots[t];
-    if (skip_mb && kd.kind == FDDP_KNOT_EULER_FREEFWD) continue;  // computed by mb_knot_kernel
+    if (skip_mb && is_mb_kind(kd.kind)) continue;  // computed by mb_knot_kernel
     const double* P = stage_params<NT>(D.pblock(b, t), block_doubles_dev(kd.kind, D.nx, kd.nu, D.pblock(b, t)), pl, pcap, cached);
     const double* xg = D.xs[c] + D.knot(b, t) * D.sX;
     for (int i = threadIdx.x; i < D.nx; i += NT) x[i] = xg[i];
@@ -208,7 +208,7 @@ __global__ __launch_bounds__(NT) void calc_diff_kernel(Dev D, int sel, int gaps,
 __global__ __launch_bounds__(64) void mb_knot_kernel(Dev D, int sel_calc, int sel_diff) {
   const int t = blockIdx.x, b = blockIdx.y;
   const fddp_knot_desc kd = D.knots[t];
-  if (kd.kind != FDDP_KNOT_EULER_FREEFWD) return;
+  if (!is_mb_kind(kd.kind)) return;
   const ElemState s = D.st[b];
   const bool do_calc = sel_calc >= 0 && selected(s, sel_calc);
   const bool do_diff = sel_diff >= 0 && selected(s, sel_diff);

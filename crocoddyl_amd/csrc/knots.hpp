@@ -98,7 +98,7 @@ __device__ __forceinline__ double knot_calc(const fddp_knot_desc& kd, const doub
                             bool use_u, double* xnext, double* red, double* mbw) {
   const int nu = kd.nu;
   use_u = use_u && nu > 0;
-  if (kd.kind == FDDP_KNOT_EULER_FREEFWD) return mb::knot_calc<NT>(P, nx, x, u, use_u, xnext, mbw);
+  if (is_mb_kind(kd.kind)) return mb::knot_calc<NT>(P, nx, x, u, use_u, xnext, mbw);
   double t[5] = {0., 0., 0., 0., 0.};
   if (kd.kind == FDDP_KNOT_LQR) {
     LQRBlk Pm(P, nx, nu);
@@ -171,7 +171,7 @@ __device__ __forceinline__ void knot_calc_diff(const fddp_knot_desc& kd, const d
   const int nu = kd.nu;
   use_u = use_u && nu > 0;
   const int tid = threadIdx.x;
-  if (kd.kind == FDDP_KNOT_EULER_FREEFWD) return;
+  if (is_mb_kind(kd.kind)) return;
   if (kd.kind == FDDP_KNOT_LQR) {  // lqr.hxx:51-70
     LQRBlk Pm(P, nx, nu);
     for (int i = tid; i < n; i += NT) {

@@ -36,7 +36,10 @@ constexpr int kJRec = 26;       // doubles per joint record
 constexpr int kCHdr = 4;        // doubles of a cost record's header
 constexpr int kMaxFrameCosts = 8;
 constexpr int kValsPerJoint = 52;  // R 9, p 3, oR 9, op 3, v 6, a 6, F 6, composite m 1, c 3, I 6
-enum { C_STATE = 1, C_CONTROL = 2, C_FRAME_PLACEMENT = 3, C_FRAME_TRANSLATION = 4 };
+constexpr int kMaxNc = 24;         // stacked contact rows (FDDP_KNOT_EULER_CONTACTFWD)
+// Cost record types; contact records (after the costs) use 5 / 6 and the same
+// frame payload as the frame costs, so frame_residual serves both.
+enum { C_STATE = 1, C_CONTROL = 2, C_FRAME_PLACEMENT = 3, C_FRAME_TRANSLATION = 4, C_CONTACT_3D = 5, C_CONTACT_6D = 6 };
 
 struct Blk {
   double dt;
@@ -45,6 +48,11 @@ struct Blk {
   const double* arm;  // armature (nj)
   const double* J;    // joint records
   const double* C;    // cost records
+  // contact section (DifferentialActionModelContactFwdDynamics); ncon == 0 without
+  int nun;            // leading unactuated dofs: tau = [0_nun; u], nu = nj - nun
+  int ncon, nc;       // active contact records, stacked rows
+  double damping;     // JMinvJt_damping
+  const double* K;    // contact records
 };
 
 MB_HD inline Blk parse(const double* P) {
@@ -56,6 +64,23 @@ MB_HD inline Blk parse(const double* P) {
   b.arm = b.g + 3;
   b.J = b.arm + b.nj;
   b.C = b.J + (int64_t)kJRec * b.nj;
+  const double* e = b.C;
+  for (int k = 0; k < b.ncost; ++k) e += (int)e[3];
+  b.nun = 0;
+  b.ncon = b.nc = 0;
+  b.damping = 0.;
+  b.K = e;
+  if (e - P < (int64_t)P[3]) {  // [nun, damping, ncontact, 0] + records
+    b.nun = (int)e[0];
+    b.damping = e[1];
+    b.ncon = (int)e[2];
+    b.K = e + 4;
+    const double* r = b.K;
+    for (int k = 0; k < b.ncon; ++k) {
+      b.nc += (int)r[0] == C_CONTACT_3D ? 3 : 6;
+      r += (int)r[3];
+    }
+  }
   return b;
 }
 
@@ -421,7 +446,7 @@ MB_HD inline int frame_residual(const Blk& b, const Vals& V, const CRec& C, int 
       }
     }
   }
-  if (C.type() == C_FRAME_TRANSLATION) {
+  if (C.type() == C_FRAME_TRANSLATION || C.type() == C_CONTACT_3D) {
     const double* pref = d + 13;
     for (int e = 0; e < 3; ++e) {
       r[e] = pf[e] - pref[e];
@@ -469,7 +494,7 @@ MB_HD __forceinline__ int frame_residual_value(const VT& V, const CRec& C, doubl
   const double* d = C.d();
   double Rf[9], pf[3];
   frame_placement(V, d, Rf, pf);
-  if (C.type() == C_FRAME_TRANSLATION) {
+  if (C.type() == C_FRAME_TRANSLATION || C.type() == C_CONTACT_3D) {
     for (int e = 0; e < 3; ++e) r[e] = pf[e] - d[13 + e];
     return 3;
   }
@@ -715,7 +740,7 @@ MB_HD inline void w_accel_term(const WVals& W, const double* qd, const double* q
 
 // lane i < nj: a_i = -g + sum over ancestors-or-self of cq_k, then the body
 // force f_i = I_i a_i + v_i x* (I_i v_i)
-MB_HD inline void w_accel_force(const WVals& W, int i) {
+MB_HD inline void w_accel_force(const WVals& W, int i, const double* fx = nullptr) {
   double a[6];
   for (int e = 0; e < 6; ++e) a[e] = W.root_a()[e];
   const unsigned am = *W.anc(i);
@@ -734,7 +759,7 @@ MB_HD inline void w_accel_force(const WVals& W, int i) {
   inertia_mul(m, c, I6, a, f);
   inertia_mul(m, c, I6, v, Iv);
   cross_f(v, Iv, t6);
-  for (int e = 0; e < 6; ++e) W.fb(i)[e] = f[e] + t6[e];
+  for (int e = 0; e < 6; ++e) W.fb(i)[e] = f[e] + t6[e] - (fx ? fx[6 * i + e] : 0.);
 }
 
 // lane i < nj: F_i = sum over the subtree of the body forces, tau_i = S_i . F_i
@@ -773,6 +798,108 @@ MB_HD inline void w_crba_column(const Blk& b, const WVals& W, int j, double* A, 
   }
 }
 
+// ---- contacts (ContactModel3D / 6D in the LOCAL frame) ----------------------
+// Row offset of contact record k and its record pointer.
+MB_HD inline const double* contact_rec(const Blk& b, int k, int* row0) {
+  const double* r = b.K;
+  int row = 0;
+  for (int i = 0; i < k; ++i) {
+    row += (int)r[0] == C_CONTACT_3D ? 3 : 6;
+    r += (int)r[3];
+  }
+  *row0 = row;
+  return r;
+}
+
+// Column c of the contact's LOCAL frame Jacobian (pinocchio getFrameJacobian
+// LOCAL, contact-3d.hxx:29 / contact-6d.hxx:29): the world motion S_c moved to
+// the frame (SE3::actInv of oMf), zero unless c supports the frame's joint.
+template <class VT>
+MB_HD inline void contact_jac_col(const VT& V, const unsigned* anc_j, const double* d, int c, const double* Sc,
+                                  double* o) {
+  if (!((*anc_j >> c) & 1u)) {
+    for (int e = 0; e < 6; ++e) o[e] = 0.;
+    return;
+  }
+  double Rf[9], pf[3];
+  frame_placement(V, d, Rf, pf);
+  motion_act_inv(Rf, pf, Sc, o);
+}
+
+// a0 of a contact (contact-3d.hxx:35-43, contact-6d.hxx:31-44) from the world
+// velocity / drift acceleration (gravity included, as RNEA) of its joint.
+MB_HD inline int contact_a0(const Blk& b, const WVals& W, const CRec& C, double* a0) {
+  const double* d = C.d();
+  const int j = (int)d[0];
+  double Rf[9], pf[3], m6[6], vf[6], af[6];
+  frame_placement(W, d, Rf, pf);
+  for (int e = 0; e < 6; ++e) m6[e] = W.v(j)[e];
+  motion_act_inv(Rf, pf, m6, vf);
+  for (int e = 0; e < 6; ++e) m6[e] = W.a(j)[e] - W.root_a()[e];  // data.a has no gravity
+  motion_act_inv(Rf, pf, m6, af);
+  const double kp = C.r[1], kd = C.r[2];
+  double r[6] = {0., 0., 0., 0., 0., 0.};
+  if (kp != 0.) frame_residual_value(W, C, r);
+  if (C.type() == C_CONTACT_3D) {
+    double wxv[3];
+    cross3(vf + 3, vf, wxv);
+    for (int e = 0; e < 3; ++e) a0[e] = af[e] + wxv[e] + kp * r[e] + kd * vf[e];
+    return 3;
+  }
+  for (int e = 0; e < 6; ++e) a0[e] = af[e] + kp * r[e] + kd * vf[e];
+  return 6;
+}
+
+// World force (at the origin) of contact record C for the multipliers lam
+// (updateForce: jMf.act(Force(lambda[, 0])), contact-3d.hxx:59-67).
+MB_HD inline void contact_world_force(const WVals& W, const CRec& C, const double* lam, double* o) {
+  double Rf[9], pf[3], f[6];
+  frame_placement(W, C.d(), Rf, pf);
+  const bool c3 = C.type() == C_CONTACT_3D;
+  for (int e = 0; e < 6; ++e) f[e] = (c3 && e >= 3) ? 0. : lam[e];
+  force_act(Rf, pf, f, o);
+}
+
+// lane j < nj: sum of the contact forces acting on joint j (world) into fx[6j..]
+MB_HD inline void contact_joint_forces(const Blk& b, const WVals& W, const double* lam, double* fx, int j) {
+  double F[6] = {0., 0., 0., 0., 0., 0.};
+  const double* r = b.K;
+  int row = 0;
+  for (int k = 0; k < b.ncon; ++k) {
+    const CRec C{r};
+    if ((int)C.d()[0] == j) {
+      double o[6];
+      contact_world_force(W, C, lam + row, o);
+      for (int e = 0; e < 6; ++e) F[e] += o[e];
+    }
+    row += C.type() == C_CONTACT_3D ? 3 : 6;
+    r += C.size();
+  }
+  for (int e = 0; e < 6; ++e) fx[6 * j + e] = F[e];
+}
+
+// lane c < nj: column c of the stacked contact Jacobian Jc (nc x nj,
+// Jc[row * nj + c]); with At != null also into the columns [nj + row] of A (ld nj).
+MB_HD inline void contact_jac_lane(const Blk& b, const WVals& W, int c, double* Jc, double* At) {
+  double Sc[6];
+  for (int e = 0; e < 6; ++e) Sc[e] = W.S(c)[e];
+  const double* r = b.K;
+  int row = 0;
+  for (int k = 0; k < b.ncon; ++k) {
+    const CRec C{r};
+    const int j = (int)C.d()[0];
+    double o[6];
+    contact_jac_col(W, W.anc(j), C.d(), c, Sc, o);
+    const int n = C.type() == C_CONTACT_3D ? 3 : 6;
+    for (int e = 0; e < n; ++e) {
+      Jc[(int64_t)(row + e) * b.nj + c] = o[e];
+      if (At) At[(int64_t)(b.nj + row + e) * b.nj + c] = o[e];
+    }
+    row += n;
+    r += C.size();
+  }
+}
+
 // Placements, world quantities, composite inertias and M (into A, zeroed by
 // the caller) for configuration q; `costs(wave, l)` runs on waves >= 2 in
 // the phase after the kinematics (nullptr-like no-op allowed).
@@ -800,10 +927,12 @@ MB_HD inline void world_kinematics(const X& ex, const Blk& b, const WVals& W, co
   });
 }
 
-// Joint torques of RNEA(q, qd, qdd) (qdd == nullptr: 0) with the kinematics in W.
+// Joint torques of RNEA(q, qd, qdd) (qdd == nullptr: 0) with the kinematics in W;
+// fx (6 per joint, world frame at the origin, may be null): external forces,
+// as pinocchio::rnea(model, data, q, v, a, fext).
 template <class X>
 MB_HD inline void world_rnea(const X& ex, const Blk& b, const WVals& W, const double* qd, const double* qdd,
-                             double* tau) {
+                             double* tau, const double* fx = nullptr) {
   const int nj = b.nj;
   ex.run([&](int lane) {
     if (lane < nj) w_velocity(W, qd, lane);
@@ -812,63 +941,98 @@ MB_HD inline void world_rnea(const X& ex, const Blk& b, const WVals& W, const do
     if (lane < nj) w_accel_term(W, qd, qdd, lane);
   });
   ex.run([&](int lane) {
-    if (lane < nj) w_accel_force(W, lane);
+    if (lane < nj) w_accel_force(W, lane, fx);
   });
   ex.run([&](int lane) {
     if (lane < nj) w_joint_force(b, W, tau, lane);
   });
 }
 
-// LDS (doubles) of the calc scratch for nj joints.
-MB_HD inline int64_t calc_work_doubles(int nj) {
-  return WVals::doubles(nj) + (int64_t)nj * (nj + 1) + 2 * nj + kMaxCosts + 8;
+// LDS (doubles) of the calc scratch for nj joints and nc contact rows.
+MB_HD inline int64_t calc_work_doubles(int nj, int nc = 0) {
+  return WVals::doubles(nj) + (int64_t)nj * (nj + nc + 1) + 2 * nj + kMaxCosts + 8 + (int64_t)nc * nj + nc +
+         (int64_t)nc * (nc + 1);
 }
 
 // model->calc(data, x, u) for the Euler∘FreeFwdDynamics knot (euler.hxx:41-80,
-// free-fwddyn.hxx:44-79): a = (M + diag(armature))^-1 (u - nle) in world frame.
+// free-fwddyn.hxx:44-79): a = (M + diag(armature))^-1 (u - nle) in world frame;
+// with contacts, Euler∘ContactFwdDynamics (contact-fwddyn.hxx:59-104):
+// pinocchio::forwardDynamics by the Schur complement,
+//   [Y | z] = M^-1 [Jc^T | tau - nle],  S = Jc Y + damping I,
+//   lambda = -S^-1 (Jc z + a0),  a = z + Y lambda.
 // Needs >= 256 threads (4 waves): independent work of one phase runs on
 // different waves (divergent lanes of one wave would serialise) — wave 0 the
 // recursions, wave 1 composite inertias and CRBA, waves 2-3 the cost records.
 // Every thread must call (phases end in barriers). x, u readable by all lanes;
-// writes xnext[0..nx) and returns the knot cost. `w`: calc_work_doubles(nj).
+// writes xnext[0..nx) and returns the knot cost. `w`: calc_work_doubles(nj, nc).
 template <class X>
 MB_HD inline double knot_calc_x(const X& ex, const double* P, int nx, const double* x, const double* u, bool use_u,
                                 double* xnext, double* w) {
   const Blk b = parse(P);
-  const int nj = b.nj;
+  const int nj = b.nj, nc = b.nc, nu = nj - b.nun, ncol = nj + nc + 1;
   const WVals W{w, nj};
-  double* A = w + WVals::doubles(nj);  // nj x (nj + 1), ld nj
-  double* tau = A + (int64_t)nj * (nj + 1);
+  double* A = w + WVals::doubles(nj);  // nj x (nj + nc + 1), ld nj: [M | Jc^T | tau - nle]
+  double* tau = A + (int64_t)nj * ncol;
   double* ub = tau + nj;  // u (zero if !use_u)
   double* cv = ub + nj;   // per-cost activations
   double* red = cv + kMaxCosts;
   int* flag = (int*)(red + 2);
+  double* Jc = red + 8;                  // nc x nj
+  double* a0 = Jc + (int64_t)nc * nj;    // nc
+  double* S = a0 + nc;                   // nc x (nc + 1), ld nc: [S | Jc z + a0]
   ex.run([&](int lane) {
-    if (lane < nj) ub[lane] = use_u ? u[lane] : 0.;
-    for (int e = lane; e < nj * (nj + 1); e += ex.nt) A[e] = 0.;
+    if (lane < nu) ub[lane] = use_u ? u[lane] : 0.;
+    for (int e = lane; e < nj * ncol; e += ex.nt) A[e] = 0.;
   });
   // cost records k on wave 2 + (k & 1), lane k >> 1, once the placements exist
   world_kinematics(ex, b, W, x, A, [&](int wave, int l) {
     const double* cr = b.C;
     for (int k = 0; k < b.ncost; ++k) {
       const CRec C{cr};
-      if (wave == 2 + (k & 1) && l == (k >> 1)) cv[k] = C.weight() * cost_activation(W, C, x, ub, nx, nj);
+      if (wave == 2 + (k & 1) && l == (k >> 1)) cv[k] = C.weight() * cost_activation(W, C, x, ub, nx, nu);
       cr += C.size();
     }
   });
   world_rnea(ex, b, W, x + nj, nullptr, tau);
   ex.run([&](int lane) {
-    if (lane < nj) A[(int64_t)nj * nj + lane] = ub[lane] - tau[lane];
-    if (lane == 64) {
+    if (lane < nj) {
+      const double ti = lane < b.nun ? 0. : ub[lane - b.nun];  // ActuationModelFloatingBase: tau = [0; u]
+      A[(int64_t)nj * (nj + nc) + lane] = ti - tau[lane];
+      if (nc) contact_jac_lane(b, W, lane, Jc, A);
+    }
+    if (lane >= 64 && lane < 64 + b.ncon) {
+      int row0;
+      const CRec C{contact_rec(b, lane - 64, &row0)};
+      contact_a0(b, W, C, a0 + row0);
+    }
+    if (lane == 128) {
       double total = 0.;
       for (int k = 0; k < b.ncost; ++k) total += cv[k];
       red[0] = total;
     }
   });
-  const bool ok = gauss_jordan(ex, A, nj, nj + 1, flag);
+  bool ok = gauss_jordan(ex, A, nj, ncol, flag);
+  double* a = A + (int64_t)nj * (nj + nc);  // z, then a
+  if (nc > 0) {
+    ex.run([&](int lane) {
+      for (int e = lane; e < nc * (nc + 1); e += ex.nt) {
+        const int col = e / nc, row = e % nc;
+        const double* yc = A + (int64_t)nj * (nj + col);  // column col of Y, or z
+        double s = 0.;
+        for (int i = 0; i < nj; ++i) s += Jc[(int64_t)row * nj + i] * yc[i];
+        S[e] = col < nc ? s + (row == col ? b.damping : 0.) : s + a0[row];
+      }
+    });
+    ok = gauss_jordan(ex, S, nc, nc + 1, flag) && ok;
+    ex.run([&](int lane) {
+      if (lane >= nj) return;
+      double s = a[lane];
+      for (int k = 0; k < nc; ++k) s -= A[(int64_t)nj * (nj + k) + lane] * S[(int64_t)nc * nc + k];
+      a[lane] = s;
+    });
+  }
   const double cc = red[0];
   const double dt = b.dt;
-  const double* a = A + (int64_t)nj * nj;
   ex.run([&](int i) {
     if (i >= nj) return;
     const double ai = ok ? a[i] : NAN;  // a singular mass matrix surfaces as forward_error
@@ -895,9 +1059,12 @@ __device__ inline double knot_calc(const double* P, int nx, const double* x, con
 // calcDiff: one 64-thread workgroup per (element, knot).
 // ---------------------------------------------------------------------------
 struct DiffLayout {
-  int64_t wv, vals, A, tang, dtau, J, xu, red, total;
+  int64_t wv, vals, A, tang, dtau, J, xu, red, ct, total;
+  // contact area (nc > 0): Jc nc x nj, a0 nc, lambda nc, Y = Minv Jc^T and
+  // H = Y S^-1 (nj x nc each), [S | I | r] nc x (2nc + 1), da0/dx nc x L, fx 6 nj
+  int64_t Jc, a0, lam, Y, H, Sx, da0, fx;
 };
-__host__ __device__ inline DiffLayout diff_layout(int nj, int nframe) {
+__host__ __device__ inline DiffLayout diff_layout(int nj, int nframe, int nc = 0) {
   const int L = 2 * nj;
   DiffLayout l;
   l.wv = 0;
@@ -908,7 +1075,16 @@ __host__ __device__ inline DiffLayout diff_layout(int nj, int nframe) {
   l.J = l.dtau + ((int64_t)nj * L > 3 * nj ? (int64_t)nj * L : 3 * nj);  // dtau [i][L] (nle, a first)
   l.xu = l.J + (int64_t)6 * nj * (nframe > 0 ? nframe : 1);  // frame-cost Jacobians [cost][6][nj] + residuals
   l.red = l.xu + 3 * nj + 6 * kMaxFrameCosts + 8;  // x (2nj), u (nj), frame residuals
-  l.total = l.red + 8;  // red: flag
+  l.ct = l.red + 8;  // red: flag
+  l.Jc = l.ct;
+  l.a0 = l.Jc + (int64_t)nc * nj;
+  l.lam = l.a0 + nc;
+  l.Y = l.lam + nc;
+  l.H = l.Y + (int64_t)nj * nc;
+  l.Sx = l.H + (int64_t)nj * nc;
+  l.da0 = l.Sx + (int64_t)nc * (2 * nc + 1);
+  l.fx = l.da0 + (int64_t)nc * L;
+  l.total = nc > 0 ? l.fx + 6 * nj : l.ct;
   return l;
 }
 
@@ -992,6 +1168,56 @@ MB_HD inline void rnea_tangent(const Blk& b, const Vals& V, const double* qd, in
   }
 }
 
+// da0/dx along the tangent direction of this lane (q_c if dir == 0, v_c if
+// dir == 1), from the joint tangents of rnea_tangent (at ddq = a fixed, as
+// getJointAccelerationDerivatives after computeRNEADerivatives): the frame
+// motion tangents (jMf.actInv), the classical-acceleration term of a 3D
+// contact, the gravity that RNEA's tangents carry removed, and the Baumgarte
+// terms (contact-3d.hxx:46-71, contact-6d.hxx:48-66). da0[row * L + lane].
+MB_HD inline void contact_tangent(const Blk& b, const Vals& V, const WVals& W, int dir, int c, const double* T,
+                                  int L, int lane, double* da0) {
+  const double* r = b.K;
+  int row = 0;
+  for (int k = 0; k < b.ncon; ++k) {
+    const CRec C{r};
+    const double* d = C.d();
+    const int j = (int)d[0];
+    double dv[6], da[6];
+    for (int e = 0; e < 6; ++e) {
+      dv[e] = T[((int64_t)j * 18 + e) * L + lane];
+      da[e] = T[((int64_t)j * 18 + 6 + e) * L + lane];
+    }
+    const bool sup = (*W.anc(j) >> c) & 1u;
+    if (dir == 0 && sup) {  // d(-R_j^T g)/dq_c = R_j^T (w_c x g)
+      double wc[3], wg[3], t[3];
+      matvec3(V.oR(c), JRec(b, c).axis(), wc);
+      cross3(wc, b.g, wg);
+      matTvec3(V.oR(j), wg, t);
+      for (int e = 0; e < 3; ++e) da[e] -= t[e];
+    }
+    double dvf[6], daf[6], vf[6], vj[6];
+    for (int e = 0; e < 6; ++e) vj[e] = V.v(j)[e];
+    motion_act_inv(d + 1, d + 10, dv, dvf);
+    motion_act_inv(d + 1, d + 10, da, daf);
+    motion_act_inv(d + 1, d + 10, vj, vf);
+    const double kp = C.r[1], kd = C.r[2];
+    double rr[6], Jk[6] = {0., 0., 0., 0., 0., 0.};
+    if (kp != 0. && dir == 0 && sup) frame_residual(b, V, C, c, rr, Jk);
+    if (C.type() == C_CONTACT_3D) {
+      double t1[3], t2[3];
+      cross3(dvf + 3, vf, t1);
+      cross3(vf + 3, dvf, t2);
+      for (int e = 0; e < 3; ++e)
+        da0[(int64_t)(row + e) * L + lane] = daf[e] + t1[e] + t2[e] + kd * dvf[e] + kp * Jk[e];
+      row += 3;
+    } else {
+      for (int e = 0; e < 6; ++e) da0[(int64_t)(row + e) * L + lane] = daf[e] + kd * dvf[e] + kp * Jk[e];
+      row += 6;
+    }
+    r += C.size();
+  }
+}
+
 // model->calcDiff for one knot by one 64-thread workgroup (euler.hxx:83-131,
 // free-fwddyn.hxx:82-118, cost-sum.hxx:122-160). Writes full blocks (entries
 // beyond nu zero); Lxu is zero (no cost couples x and u). A mass matrix that is
@@ -1005,7 +1231,7 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
                                    double* Luu, double* Lx, double* Lu, double* xnext_out = nullptr,
                                    double* cost_out = nullptr) {
   const Blk b = parse(P);
-  const int nj = b.nj, n = nx, L = 2 * nj;
+  const int nj = b.nj, n = nx, L = 2 * nj, nc = b.nc, nu = nj - b.nun;
   int nframe = 0;
   {
     const double* cr = b.C;
@@ -1015,7 +1241,7 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
       cr += C.size();
     }
   }
-  const DiffLayout l = diff_layout(nj, nframe);
+  const DiffLayout l = diff_layout(nj, nframe, nc);
   const WVals W{w + l.wv, nj};
   const Vals V{w + l.vals, nj};
   double* A = w + l.A;
@@ -1027,9 +1253,17 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
   double* rf = u + nj;  // frame residuals, 6 per frame cost
   double* red = w + l.red;
   int* flag = (int*)(red + 4);
+  double* Jc = w + l.Jc;
+  double* a0 = w + l.a0;
+  double* lam = w + l.lam;
+  double* Y = w + l.Y;
+  double* H = w + l.H;
+  double* Sx = w + l.Sx;
+  double* da0 = w + l.da0;
+  double* fx = w + l.fx;
   ex.run([&](int lane) {
     if (lane < nx) x[lane] = xg[lane];
-    if (lane < nj) u[lane] = use_u ? ug[lane] : 0.;
+    if (lane < nu) u[lane] = use_u ? ug[lane] : 0.;
     for (int e = lane; e < 2 * nj * nj; e += ex.nt) {
       const int c = e / nj, r = e % nj;
       A[e] = (c == nj + r) ? 1. : 0.;
@@ -1038,18 +1272,85 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
   // world-frame kinematics, M into the left half of [M | I], nle -> dtau[0..nj)
   world_kinematics(ex, b, W, x, A, [](int, int) {});
   world_rnea(ex, b, W, x + nj, nullptr, dtau);
-  const bool ok = gauss_jordan(ex, A, nj, 2 * nj, flag);
-  const double* Minv = A + (int64_t)nj * nj;  // column-major nj x nj
-  // a = (M + A)^-1 (tau - nle) -> dtau[nj..2nj)
+  if (nc > 0)  // contact rows at the drift (ddq = 0; ContactModelMultiple::calc)
+    ex.run([&](int lane) {
+      if (lane < nj) contact_jac_lane(b, W, lane, Jc, nullptr);
+      for (int k = lane; k < b.ncon; k += ex.nt) {
+        int row0;
+        const CRec C{contact_rec(b, k, &row0)};
+        contact_a0(b, W, C, a0 + row0);
+      }
+    });
+  bool ok = gauss_jordan(ex, A, nj, 2 * nj, flag);
+  double* Minv = A + (int64_t)nj * nj;  // column-major nj x nj; with contacts: d a / d tau after the Schur step
+  // z = (M + A)^-1 (tau - nle) -> dtau[nj..2nj) (the acceleration without contacts);
+  // Y = Minv Jc^T
   ex.run([&](int lane) {
-    if (lane >= nj) return;
-    double s = 0.;
-    for (int k = 0; k < nj; ++k) s += Minv[(int64_t)k * nj + lane] * (u[k] - dtau[k]);
-    dtau[nj + lane] = ok ? s : NAN;
+    if (lane < nj) {
+      double s = 0.;
+      for (int k = 0; k < nj; ++k) s += Minv[(int64_t)k * nj + lane] * ((k < b.nun ? 0. : u[k - b.nun]) - dtau[k]);
+      dtau[nj + lane] = ok ? s : NAN;
+    }
+    for (int e = lane; e < nj * nc; e += ex.nt) {
+      const int k = e / nj, i = e % nj;
+      double s = 0.;
+      for (int r = 0; r < nj; ++r) s += Minv[(int64_t)r * nj + i] * Jc[(int64_t)k * nj + r];
+      Y[e] = s;
+    }
   });
+  if (nc > 0) {
+    // [S | I | Jc z + a0], S = Jc Y + damping I; Gauss-Jordan -> [. | S^-1 | S^-1 r]
+    ex.run([&](int lane) {
+      for (int e = lane; e < nc * (2 * nc + 1); e += ex.nt) {
+        const int col = e / nc, row = e % nc;
+        double v;
+        if (col < nc) {
+          double s = 0.;
+          for (int i = 0; i < nj; ++i) s += Jc[(int64_t)row * nj + i] * Y[(int64_t)col * nj + i];
+          v = s + (row == col ? b.damping : 0.);
+        } else if (col < 2 * nc) {
+          v = (col - nc == row) ? 1. : 0.;
+        } else {
+          double s = 0.;
+          for (int i = 0; i < nj; ++i) s += Jc[(int64_t)row * nj + i] * dtau[nj + i];
+          v = s + a0[row];
+        }
+        Sx[e] = v;
+      }
+    });
+    ok = gauss_jordan(ex, Sx, nc, 2 * nc + 1, flag) && ok;
+    // lambda = -S^-1 r, a = z + Y lambda, H = Y S^-1 (= Kinv top-right)
+    ex.run([&](int lane) {
+      const double* Sinv = Sx + (int64_t)nc * nc;
+      const double* sr = Sx + (int64_t)2 * nc * nc;
+      if (lane < nc) lam[lane] = -sr[lane];
+      if (lane < nj) {
+        double s = dtau[nj + lane];
+        for (int k = 0; k < nc; ++k) s -= Y[(int64_t)k * nj + lane] * sr[k];
+        dtau[nj + lane] = ok ? s : NAN;
+      }
+      for (int e = lane; e < nj * nc; e += ex.nt) {
+        const int k = e / nj, i = e % nj;
+        double s = 0.;
+        for (int m2 = 0; m2 < nc; ++m2) s += Y[(int64_t)m2 * nj + i] * Sinv[(int64_t)k * nc + m2];
+        H[e] = s;
+      }
+    });
+    // Kinv top-left Minv - H Y^T (in place); contact forces per joint (world)
+    ex.run([&](int lane) {
+      for (int e = lane; e < nj * nj; e += ex.nt) {
+        const int c = e / nj, i = e % nj;
+        double s = Minv[e];
+        for (int k = 0; k < nc; ++k) s -= H[(int64_t)k * nj + i] * Y[(int64_t)k * nj + c];
+        Minv[e] = s;
+      }
+      if (lane < nj) contact_joint_forces(b, W, lam, fx, lane);
+    });
+  }
   // accelerations and forces at the solved a (the linearisation point of
-  // computeABADerivatives); tau lands in dtau[2nj..3nj) and is not used
-  world_rnea(ex, b, W, x + nj, dtau + nj, dtau + 2 * nj);
+  // computeABADerivatives / computeRNEADerivatives with fext); tau lands in
+  // dtau[2nj..3nj) and is not used
+  world_rnea(ex, b, W, x + nj, dtau + nj, dtau + 2 * nj, nc > 0 ? fx : nullptr);
   // joint-frame values for the tangent recursion: liMi, oMi, and v, a, F moved
   // from world to joint coordinates (SE3::actInv of oMi)
   ex.run([&](int i) {
@@ -1103,7 +1404,7 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
         }
       }
       if (cost_out && !Fx && lane == 0) {  // calc only (with derivatives: from the residuals below)
-        const double cc = cost_value(b, W, x, u, nx, nj);
+        const double cc = cost_value(b, W, x, u, nx, nu);
         *cost_out = dt != 0. ? dt * cc : cc;
       }
     });
@@ -1111,7 +1412,10 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
   if (!Fx) return;  // calc only
   // tangents (lanes < 2 nj) and frame-cost residuals / Jacobian columns (lanes < nj)
   ex.run([&](int lane) {
-    if (lane < L) rnea_tangent(b, V, x + nj, lane < nj ? 0 : 1, lane % nj, T, L, lane, dtau);
+    if (lane < L) {
+      rnea_tangent(b, V, x + nj, lane < nj ? 0 : 1, lane % nj, T, L, lane, dtau);
+      if (nc > 0) contact_tangent(b, V, W, lane < nj ? 0 : 1, lane % nj, T, L, lane, da0);
+    }
     if (lane >= nj) return;
     const double* cr = b.C;
     int f = 0;
@@ -1144,6 +1448,7 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
       if (integ) {
         double s = 0.;
         for (int k = 0; k < nj; ++k) s += Minv[(int64_t)k * nj + r] * dtau[(int64_t)k * L + c];
+        for (int k = 0; k < nc; ++k) s += H[(int64_t)k * nj + r] * da0[(int64_t)k * L + c];
         const double da = ok ? -s : NAN;
         f = i < nj ? da * dt2 + (c == nj + i ? dt : 0.) + (c == i ? 1. : 0.) : da * dt + (c == i ? 1. : 0.);
       } else {
@@ -1151,12 +1456,12 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
       }
       Fx[e] = f;
     }
-    // Fu(i, c) = Minv(i mod nj, c) dt^2 | dt (ActuationModelFull: dtau/du = I); Lxu = 0
+    // Fu(i, c) = Minv(i mod nj, nun + c) dt^2 | dt (dtau/du = [0; I]); Lxu = 0
     for (int e = lane; e < n * m; e += ex.nt) {
       const int c = e / n, i = e % n;
       double f = 0.;
-      if (integ && c < nj) {
-        const double mi = ok ? Minv[(int64_t)c * nj + (i < nj ? i : i - nj)] : NAN;
+      if (integ && c < nu) {
+        const double mi = ok ? Minv[(int64_t)(b.nun + c) * nj + (i < nj ? i : i - nj)] : NAN;
         f = i < nj ? mi * dt2 : mi * dt;
       }
       Fu[e] = f;
@@ -1171,7 +1476,7 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
       for (int k = 0; k < b.ncost; ++k) {
         const CRec C{cr};
         const double wt = C.weight();
-        const double* wv = cost_weights(C, nx, nj);
+        const double* wv = cost_weights(C, nx, nu);
         if (C.type() == C_STATE) {
           if (i == j) l += wt * wv[j];
         } else if (C.type() == C_FRAME_PLACEMENT || C.type() == C_FRAME_TRANSLATION) {
@@ -1192,11 +1497,11 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
     for (int e = lane; e < m * m; e += ex.nt) {
       const int j = e / m, i = e % m;
       double l = 0.;
-      if (i == j && j < nj) {
+      if (i == j && j < nu) {
         const double* cr = b.C;
         for (int k = 0; k < b.ncost; ++k) {
           const CRec C{cr};
-          if (C.type() == C_CONTROL) l += C.weight() * cost_weights(C, nx, nj)[j];
+          if (C.type() == C_CONTROL) l += C.weight() * cost_weights(C, nx, nu)[j];
           cr += C.size();
         }
       }
@@ -1205,11 +1510,11 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
     if (lane < m) {
       const int j = lane;
       double lu = 0.;
-      if (j < nj) {
+      if (j < nu) {
         const double* cr = b.C;
         for (int k = 0; k < b.ncost; ++k) {
           const CRec C{cr};
-          if (C.type() == C_CONTROL) lu += C.weight() * cost_weights(C, nx, nj)[j] * (u[j] - C.d()[j]);
+          if (C.type() == C_CONTROL) lu += C.weight() * cost_weights(C, nx, nu)[j] * (u[j] - C.d()[j]);
           cr += C.size();
         }
       }
@@ -1224,7 +1529,7 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
         for (int k = 0; k < b.ncost; ++k) {
           const CRec C{cr};
           const double wt = C.weight();
-          const double* wv = cost_weights(C, nx, nj);
+          const double* wv = cost_weights(C, nx, nu);
           if (C.type() == C_STATE) {
             lx += wt * wv[j] * (x[j] - C.d()[j]);
           } else if (C.type() == C_FRAME_PLACEMENT || C.type() == C_FRAME_TRANSLATION) {
@@ -1247,12 +1552,12 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
       int f = 0;
       for (int k = 0; k < b.ncost; ++k) {
         const CRec C{cr};
-        const double* wv = cost_weights(C, nx, nj);
+        const double* wv = cost_weights(C, nx, nu);
         double a = 0.;
         if (C.type() == C_STATE) {
           for (int i = 0; i < nx; ++i) a += wv[i] * (x[i] - C.d()[i]) * (x[i] - C.d()[i]);
         } else if (C.type() == C_CONTROL) {
-          for (int i = 0; i < nj; ++i) a += wv[i] * (u[i] - C.d()[i]) * (u[i] - C.d()[i]);
+          for (int i = 0; i < nu; ++i) a += wv[i] * (u[i] - C.d()[i]) * (u[i] - C.d()[i]);
         } else {
           const int nr = C.type() == C_FRAME_PLACEMENT ? 6 : 3;
           for (int i = 0; i < nr; ++i) a += wv[i] * rf[6 * f + i] * rf[6 * f + i];

@@ -293,7 +293,9 @@ class IntegratedActionModelEuler(ActionModelAbstract):
                                       "and Euler(DifferentialActionModelFreeFwdDynamics) knots only; got "
                                       f"{type(diffModel).__name__}")
         if self._mb:
-            self.kind = _abi.KNOT_EULER_FREEFWD
+            from .multibody import DifferentialActionModelContactFwdDynamics
+            self.kind = (_abi.KNOT_EULER_CONTACTFWD if isinstance(diffModel, DifferentialActionModelContactFwdDynamics)
+                         else _abi.KNOT_EULER_FREEFWD)
         super().__init__(diffModel.state, diffModel.nu, diffModel.nr)
         # the integrated model copies the differential model's limits (euler.hxx:25-26)
         self.u_lb = diffModel.u_lb

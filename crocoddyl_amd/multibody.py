@@ -28,6 +28,8 @@ from . import _abi
 JOINT_REC = 26
 COST_HDR = 4
 COST_STATE, COST_CONTROL, COST_FRAME_PLACEMENT, COST_FRAME_TRANSLATION = 1, 2, 3, 4
+CONTACT_3D, CONTACT_6D = 5, 6
+MAX_CONTACT_ROWS = 24
 MAX_JOINTS = 32
 
 
@@ -241,6 +243,17 @@ class ActuationModelFull:
     def __init__(self, state):
         self.state = state
         self.nu = state.nv
+
+
+class ActuationModelFloatingBase:
+    """ActuationModelFloatingBase (actuations/floating-base.hpp:29-40): the
+    first joint's dofs are unactuated, tau = [0; u], nu = nv - nv(joint 1).
+    Over the revolute-only models covered here joint 1 has one dof."""
+
+    def __init__(self, state):
+        self.state = state
+        self.nun = 1
+        self.nu = state.nv - self.nun
 
 
 class ActivationModelQuad:
@@ -459,6 +472,9 @@ class DifferentialActionModelFreeFwdDynamics:
     def __init__(self, state, actuation, costs):
         if not isinstance(actuation, ActuationModelFull):
             raise NotImplementedError("crocoddyl_amd: the device path covers ActuationModelFull only")
+        self._init_dam(state, actuation, costs)
+
+    def _init_dam(self, state, actuation, costs):
         if costs.nu != actuation.nu:
             raise ValueError(f"Invalid argument: Costs doesn't have the same control dimension "
                              f"(it should be {actuation.nu})")
@@ -502,3 +518,172 @@ class DifferentialActionModelFreeFwdDynamics:
         hdr = np.array([[dt, model.nv, len(recs), size]])
         return np.ascontiguousarray(
             np.concatenate([np.broadcast_to(p, (Bm, p.shape[1])) for p in [hdr] + parts], axis=1))
+
+
+class _Contact:
+    """ContactModelAbstract (contact-base.hxx): state, nc, nu, gains (Baumgarte
+    position / velocity gains, default zero)."""
+
+    type = 0
+    nc = 0
+
+    def __init__(self, state, ref, args, kw):
+        nu = None
+        gains = None
+        for a in args:
+            if isinstance(a, (int, np.integer)) and not isinstance(a, bool) and nu is None and gains is None:
+                nu = int(a)
+            else:
+                gains = a
+        nu = kw.get("nu", nu)
+        gains = kw.get("gains", gains)
+        self.state = state
+        self.nu = state.nv if nu is None else int(nu)
+        g = np.zeros(2) if gains is None else np.array(gains, np.float64).reshape(-1)
+        if g.size != 2:
+            raise ValueError("Invalid argument: gains has wrong dimension (it should be 2)")
+        self.gains = g
+        self._ref = ref
+
+    def _frame(self, fid):
+        model = self.state.pinocchio
+        name, pj, pl = model.frames[fid]
+        if pj == 0:
+            raise ValueError("Invalid argument: frames attached to the universe are not supported")
+        return np.concatenate([[pj - 1], pl.rotation.T.reshape(-1), pl.translation])
+
+    def pack(self):
+        body = np.concatenate([self._frame(self._ref.id), self._ref_payload()])
+        return np.concatenate([[self.type, self.gains[0], self.gains[1], COST_HDR + body.size], body])
+
+
+class ContactModel3D(_Contact):
+    """ContactModel3D(state, xref, nu=nv, gains=[0, 0]) (contact-3d.hxx:12-43):
+    point contact on frame xref.id; a0 = classical acceleration of the frame
+    origin (LOCAL) + gains[0] (oMf.translation - xref.translation) + gains[1] v."""
+
+    type = CONTACT_3D
+    nc = 3
+
+    def __init__(self, state, xref, *args, **kw):
+        if not isinstance(xref, FrameTranslation):
+            raise TypeError("ContactModel3D needs a FrameTranslation reference")
+        super().__init__(state, xref, args, kw)
+        self.xref = xref
+
+    def _ref_payload(self):
+        t = np.asarray(self.xref.translation, np.float64).reshape(-1)
+        if t.size != 3:
+            raise ValueError("Invalid argument: contact references cannot vary over the batch")
+        return t
+
+
+class ContactModel6D(_Contact):
+    """ContactModel6D(state, Mref, nu=nv, gains=[0, 0]) (contact-6d.hxx:12-45):
+    rigid contact on frame Mref.id; a0 = frame spatial acceleration (LOCAL)
+    + gains[0] log6(Mref^-1 oMf) + gains[1] v."""
+
+    type = CONTACT_6D
+    nc = 6
+
+    def __init__(self, state, Mref, *args, **kw):
+        if not isinstance(Mref, FramePlacement):
+            raise TypeError("ContactModel6D needs a FramePlacement reference")
+        super().__init__(state, Mref, args, kw)
+        self.Mref = Mref
+
+    def _ref_payload(self):
+        Pinv = self.Mref.placement.inverse()
+        return np.concatenate([Pinv.rotation.T.reshape(-1), Pinv.translation])
+
+
+class ContactItem:
+    def __init__(self, name, contact, active=True):
+        self.name, self.contact, self.active = name, contact, bool(active)
+
+
+class ContactModelMultiple:
+    """ContactModelMultiple (multiple-contacts.hxx:14-88): named contacts in a
+    std::map; the active ones stack their rows (Jc, a0, lambda) in name order."""
+
+    def __init__(self, state, nu=None):
+        self.state = state
+        self.nu = state.nv if nu is None else int(nu)
+        self.contacts = {}
+        self._version = 0
+
+    def addContact(self, name, contact, active=True):
+        if contact.nu != self.nu:
+            raise ValueError(f"Invalid argument: {name} contact item doesn't have the same control dimension "
+                             f"({self.nu})")
+        if name in self.contacts:  # the reference prints a warning and keeps the old item
+            return
+        self.contacts[name] = ContactItem(name, contact, active)
+        self._version += 1
+
+    def removeContact(self, name):
+        if name in self.contacts:
+            del self.contacts[name]
+            self._version += 1
+
+    def changeContactStatus(self, name, active):
+        if name in self.contacts:
+            self.contacts[name].active = bool(active)
+            self._version += 1
+
+    @property
+    def nc(self):
+        return sum(c.contact.nc for c in self.contacts.values() if c.active)
+
+    @property
+    def nc_total(self):
+        return sum(c.contact.nc for c in self.contacts.values())
+
+    @property
+    def active(self):
+        return sorted(n for n, c in self.contacts.items() if c.active)
+
+    @property
+    def inactive(self):
+        return sorted(n for n, c in self.contacts.items() if not c.active)
+
+    def pack(self):
+        return [self.contacts[n].contact.pack() for n in self.active]
+
+
+class DifferentialActionModelContactFwdDynamics(DifferentialActionModelFreeFwdDynamics):
+    """contact-fwddyn.hxx:24-160: the KKT dynamics
+        [M  Jc^T ; Jc  0] [a ; -lambda] = [tau(u) - nle ; -a0]
+    (Schur complement with JMinvJt + inv_damping I), costs.calc(x, u).
+    ``enable_force`` only selects the force Jacobians, which no device-covered
+    cost reads."""
+
+    def __init__(self, state, actuation, contacts, costs, inv_damping=0.0, enable_force=False):
+        if not isinstance(actuation, ActuationModelFloatingBase):
+            raise TypeError("DifferentialActionModelContactFwdDynamics needs an ActuationModelFloatingBase")
+        if not isinstance(contacts, ContactModelMultiple):
+            raise TypeError("DifferentialActionModelContactFwdDynamics needs a ContactModelMultiple")
+        if contacts.nu != actuation.nu:
+            raise ValueError(f"Invalid argument: Contacts doesn't have the same control dimension "
+                             f"(it should be {actuation.nu})")
+        self._init_dam(state, actuation, costs)
+        self.contacts = contacts
+        self.JMinvJt_damping = abs(float(inv_damping))
+        self.enable_force = bool(enable_force)
+
+    def version(self):
+        return super().version() + (self.contacts._version, self.JMinvJt_damping,
+                                    tuple(c.contact.gains.tobytes() for c in self.contacts.contacts.values()))
+
+    def pack_body(self, dt):
+        """(Bm, size) rows of the FDDP_KNOT_EULER_CONTACTFWD block: the
+        FDDP_KNOT_EULER_FREEFWD layout, then [nun, damping, ncontact, 0] and the
+        active contact records in name order."""
+        recs = self.contacts.pack()
+        if self.contacts.nc > MAX_CONTACT_ROWS:
+            raise ValueError(f"Invalid argument: the device path holds at most {MAX_CONTACT_ROWS} contact rows")
+        base = super().pack_body(dt)
+        sec = np.concatenate([[self.actuation.nun, self.JMinvJt_damping, len(recs), 0.0]] + recs)
+        out = np.concatenate([base, np.broadcast_to(sec, (base.shape[0], sec.size))], axis=1)
+        out[:, 3] = out.shape[1]
+        return np.ascontiguousarray(out)

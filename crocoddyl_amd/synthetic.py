@@ -126,6 +126,58 @@ def build_hetero(name, T=None, B=None, seed=None, phase=10, impulse_every=7):
     return x0s, running, terminal
 
 
+def build_arm_contact(T=4, B=2, seed=0, robot=None, dt=1e-2, contact="6d", gains=(2.0, 1.5), damping=0.0,
+                      weighted=False, armature=None, inactive=False):
+    """Contact-dynamics knots on the arm: Euler(dt) ∘ DifferentialActionModelContactFwdDynamics
+    (contact-fwddyn.hxx) with ActuationModelFloatingBase (first joint unactuated)
+    and a ContactModelMultiple on the gripper frame ("6d": ContactModel6D, "3d":
+    ContactModel3D) and, for "6d+3d" / "3d+3d", a second 3D contact on a frame of
+    joint 4; costs xReg + uReg (+ a weighted xReg and an elbow FrameTranslation
+    when ``weighted``). ``inactive`` adds a contact item that is switched off
+    (ContactModelMultiple::changeContactStatus). The terminal model is the same
+    DAM with dt = 0. x0_b ~ U[-1,1]^(2 nv) per element (off the contact
+    manifold: the Baumgarte gains pull the frames back)."""
+    from . import multibody as mb
+    rng = np.random.default_rng(seed)
+    model = mb.sample_talos_arm() if robot is None else robot
+    if not model.existFrame("elbow_site"):
+        model.addFrame("elbow_site", min(4, model.nv), mb.SE3(np.eye(3), (0.0, 0.05, -0.1)))
+    state = mb.StateMultibody(model)
+    act = mb.ActuationModelFloatingBase(state)
+    nu = act.nu
+    fid = model.getFrameId("gripper_left_joint") if model.existFrame("gripper_left_joint") else model.getFrameId("tip")
+    eid = model.getFrameId("elbow_site")
+    contacts = mb.ContactModelMultiple(state, nu)
+    kinds = contact.split("+")
+    if kinds[0] == "6d":
+        contacts.addContact("gripper", mb.ContactModel6D(
+            state, mb.FramePlacement(fid, mb.SE3(np.eye(3), (0.1, 0.2, 0.3))), nu, gains))
+    else:
+        contacts.addContact("gripper", mb.ContactModel3D(state, mb.FrameTranslation(fid, (0.1, 0.2, 0.3)), nu, gains))
+    if len(kinds) > 1:
+        contacts.addContact("elbow", mb.ContactModel3D(state, mb.FrameTranslation(eid, (0.0, 0.1, 0.2)), nu,
+                                                       (gains[0] * 0.5, gains[1])))
+    if inactive:
+        contacts.addContact("aux", mb.ContactModel3D(state, mb.FrameTranslation(eid, (0.0, 0.0, 0.0)), nu, gains),
+                            active=False)
+    costs = mb.CostModelSum(state, nu)
+    if weighted:
+        costs.addCost("xReg", mb.CostModelState(state, mb.ActivationModelWeightedQuad(
+            np.linspace(0.5, 2.0, state.ndx)), nu), 1e-2)
+        costs.addCost("elbowTrans", mb.CostModelFrameTranslation(state, mb.FrameTranslation(eid, (0.1, 0.0, 0.2)),
+                                                                 nu), 0.3)
+    else:
+        costs.addCost("xReg", mb.CostModelState(state, nu), 1e-2)
+    costs.addCost("uReg", mb.CostModelControl(state, nu), 1e-3)
+    dam = mb.DifferentialActionModelContactFwdDynamics(state, act, contacts, costs, damping)
+    if armature is not None:
+        dam.armature = armature
+    running = IntegratedActionModelEuler(dam, dt)
+    terminal = IntegratedActionModelEuler(dam, 0.0)
+    x0s = np.hstack([rng.uniform(-1, 1, (B, state.nq)), rng.uniform(-1, 1, (B, state.nv))])
+    return x0s, [running] * T, terminal
+
+
 def build_arm(T=None, B=None, seed=None, robot=None, dt=1e-3, weighted=False, armature=None, w_x=1e-4, w_u=1e-4):
     """The reference's arm-manipulation problem (benchmark/factory/arm.hpp:31-96,
     benchmark/arm-manipulation-optctrl.cpp:20-40) on real multibody knots:

@@ -80,6 +80,21 @@ extern "C" {
  * At most 32 joints (fewer when the calcDiff LDS plan does not fit) and 8
  * frame costs per knot. */
 #define FDDP_KNOT_EULER_FREEFWD 4
+/* IntegratedActionModelEuler around DifferentialActionModelContactFwdDynamics
+ * (multibody/actions/contact-fwddyn.hxx:59-160) with ActuationModelFloatingBase
+ * (actuations/floating-base.hpp:29-40: tau = [0_nun; u], nu = nv - nun) and a
+ * ContactModelMultiple (contacts/multiple-contacts.hxx) of ContactModel3D /
+ * ContactModel6D (contacts/contact-{3d,6d}.hxx, LOCAL frame, Baumgarte gains),
+ * over the same fixed-base revolute trees. Block: the FDDP_KNOT_EULER_FREEFWD
+ * layout (header size covers everything), then
+ *   [nun, JMinvJt_damping, ncontact, 0]
+ *   ncontact active contact records in name order, each
+ *     [type (5: 3D, 6: 6D), gains[0], gains[1], size], frame joint, frame
+ *     placement in that joint R(9) p(3), then 3D: reference translation(3);
+ *     6D: Mref^-1 R(9) p(3)
+ * At most 24 stacked contact rows (nc); the Schur complement Jc M^-1 Jc^T +
+ * damping I must be positive definite (full-rank Jc or damping > 0). */
+#define FDDP_KNOT_EULER_CONTACTFWD 5
 
 #define FDDP_PARAM_HEADER 4 /* doubles of scalar header in front of every block */
 

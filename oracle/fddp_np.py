@@ -29,7 +29,7 @@ import math
 
 import numpy as np
 
-LQR, UNICYCLE, EULER_DIFFLQR, EULER_FREEFWD = 1, 2, 3, 4
+LQR, UNICYCLE, EULER_DIFFLQR, EULER_FREEFWD, EULER_CONTACTFWD = 1, 2, 3, 4, 5
 HDR = 4
 
 
@@ -167,6 +167,10 @@ def bind_problem(knot_descs, pool, b, nx):
         if kind == EULER_FREEFWD:  # variable-size multibody block (oracle/multibody_np.py)
             from oracle.multibody_np import FreeFwdKnot
             out.append(FreeFwdKnot(pool[o:o + int(pool[o + 3])], nx, nu))
+            continue
+        if kind == EULER_CONTACTFWD:
+            from oracle.multibody_np import ContactFwdKnot
+            out.append(ContactFwdKnot(pool[o:o + int(pool[o + 3])], nx, nu))
             continue
         size = block_size(kind, nx, nu)
         out.append(Knot(kind, nx, nu, pool[o:o + size]))

@@ -41,6 +41,7 @@ HDR = 4
 JOINT_REC = 26
 COST_HDR = 4
 STATE, CONTROL, FRAME_PLACEMENT, FRAME_TRANSLATION = 1, 2, 3, 4
+CONTACT_3D, CONTACT_6D = 5, 6  # contact records (FDDP_KNOT_EULER_CONTACTFWD)
 H_CS = 1e-30  # complex-step size
 
 
@@ -225,7 +226,7 @@ class Robot:
             lam = self.parent[i]
             if lam >= 0:
                 Ic[lam] = Ic[lam] + X[i].T @ Ic[i] @ X[i]
-        M = np.zeros((nj, nj))
+        M = np.zeros((nj, nj), dtype=np.result_type(q, float))
         for i in range(nj):
             F = Ic[i] @ self.S(i)
             M[i, i] = self.S(i) @ F
@@ -325,13 +326,13 @@ class Cost:
 class FreeFwdKnot:
     """Euler(dt) ∘ DifferentialActionModelFreeFwdDynamics, parsed from a block."""
 
-    def __init__(self, block, nx, nu):
+    def __init__(self, block, nx, nu, _contact=False):
         p = np.asarray(block, float)
         self.dt = float(p[0])
         nj = int(p[1])
         ncost = int(p[2])
         self.size = int(p[3])
-        assert nx == 2 * nj and nu == nj, "free-fwddyn knots: nx = 2 nv, nu = nv (full actuation)"
+        assert nx == 2 * nj and (_contact or nu == nj), "free-fwddyn knots: nx = 2 nv, nu = nv (full actuation)"
         self.nx, self.nu, self.nj = nx, nu, nj
         self.ndx = nx
         self.kind = 4
@@ -399,6 +400,143 @@ class FreeFwdKnot:
         s = dt if dt != 0 else 1.0
         return dict(Fx=Fx, Fu=Fu, Lx=s * Lz[:n], Lu=s * Lz[n:], Lxx=s * Lzz[:n, :n], Lxu=s * Lzz[:n, n:],
                     Luu=s * Lzz[n:, n:])
+
+
+class Contact:
+    """One active contact record (ContactModel3D / ContactModel6D, LOCAL frame)."""
+
+    def __init__(self, rec):
+        self.type = int(rec[0])
+        self.gains = (float(rec[1]), float(rec[2]))
+        d = rec[COST_HDR:]
+        self.joint = int(d[0])
+        self.Rf = d[1:10].reshape(3, 3).T  # frame placement in its joint
+        self.pf = d[10:13]
+        if self.type == CONTACT_3D:
+            self.pref = d[13:16]
+            self.nc = 3
+        elif self.type == CONTACT_6D:
+            self.Rri = d[13:22].reshape(3, 3).T  # Mref^-1
+            self.pri = d[22:25]
+            self.nc = 6
+        else:
+            raise ValueError(f"unknown contact type {self.type}")
+
+
+def local_motions(robot, q, v, qdd):
+    """Featherstone's forward recursion in joint frames WITHOUT gravity: spatial
+    velocity and acceleration of every joint (Pinocchio data.v / data.a after
+    computeAllTerms (qdd = 0) or forwardKinematics(q, v, qdd))."""
+    dt = np.result_type(q, v, qdd)
+    vs, as_ = [], []
+    for i in range(robot.nj):
+        X = motion_X(*robot.liMi(q, i))
+        lam = robot.parent[i]
+        S = robot.S(i)
+        vp = vs[lam] if lam >= 0 else np.zeros(6, dt)
+        ap = as_[lam] if lam >= 0 else np.zeros(6, dt)
+        vi = X @ vp + S * v[i]
+        vs.append(vi)
+        as_.append(X @ ap + S * qdd[i] + crm(vi) @ (S * v[i]))
+    return vs, as_
+
+
+class ContactFwdKnot(FreeFwdKnot):
+    """Euler(dt) ∘ DifferentialActionModelContactFwdDynamics
+    (multibody/actions/contact-fwddyn.hxx:59-160) with ActuationModelFloatingBase
+    (tau = [0_{nun}; u], actuations/floating-base.hpp:29-40) and a
+    ContactModelMultiple of ContactModel3D / ContactModel6D in name order
+    (contacts/{contact-3d,contact-6d,multiple-contacts}.hxx).
+
+    The constrained dynamics are solved as ONE KKT system
+        [M  Jc^T ; Jc  -damping I] [a ; -lambda] = [tau - nle ; -a0]
+    (pinocchio::forwardDynamics, contact-fwddyn.hxx:94-96, restated), where Jc
+    stacks the LOCAL frame Jacobians (3 linear rows for a 3D contact) and a0 the
+    frame drift accelerations with the Baumgarte terms (contact-3d.hxx:27-43,
+    contact-6d.hxx:27-45). Fx / Fu come from complex-step differentiation of
+    this calc: the reference's analytic KKT-inverse formula
+    (contact-fwddyn.hxx:127-140) is the implicit-function derivative of the
+    same map, so the two agree to rounding."""
+
+    def __init__(self, block, nx, nu):
+        p = np.asarray(block, float)
+        nj = int(p[1])
+        ncost = int(p[2])
+        body = p[HDR:]
+        o = 3 + nj + JOINT_REC * nj
+        for _ in range(ncost):
+            o += int(body[o + 3])
+        self.nun = int(body[o])
+        self.damping = float(body[o + 1])
+        ncon = int(body[o + 2])
+        o += 4
+        self.contacts = []
+        for _ in range(ncon):
+            rs = int(body[o + 3])
+            self.contacts.append(Contact(body[o:o + rs]))
+            o += rs
+        assert nu == nj - self.nun, "contact-fwddyn knots: nu = nv - (unactuated root dofs)"
+        super().__init__(block, nx, nu, _contact=True)
+        self.kind = 5
+        self.nc = sum(c.nc for c in self.contacts)
+
+    def contact_terms(self, x):
+        """(Jc (nc x nv), a0 (nc)) at ddq = 0 (ContactModelMultiple::calc)."""
+        nj = self.nj
+        q, v = x[:nj], x[nj:]
+        dt = np.result_type(x, float)
+        vs, as_ = local_motions(self.robot, q, v, np.zeros(nj, dt))
+        oM = self.robot.placements(q)
+        Js, a0s = [], []
+        for c in self.contacts:
+            Xf = motion_X(c.Rf, c.pf)  # joint -> frame (SE3::actInv by jMf)
+            vf = Xf @ vs[c.joint]
+            af = Xf @ as_[c.joint]
+            # LOCAL frame Jacobian: frame velocity per unit joint velocity
+            J = np.zeros((6, nj), dt)
+            for k in range(nj):
+                e = np.zeros(nj, dt)
+                e[k] = 1.0
+                J[:, k] = Xf @ local_motions(self.robot, q, e, np.zeros(nj, dt))[0][c.joint]
+            R0, p0 = oM[c.joint]
+            Rw, pw = R0 @ c.Rf, p0 + R0 @ c.pf  # oMf
+            kp, kd = c.gains
+            if c.type == CONTACT_3D:
+                a0 = af[:3] + np.cross(vf[3:], vf[:3])  # classical acceleration, contact-3d.hxx:37
+                if kp != 0.0:
+                    a0 = a0 + kp * (pw - c.pref)
+                if kd != 0.0:
+                    a0 = a0 + kd * vf[:3]
+                Js.append(J[:3])
+            else:
+                a0 = af.copy()
+                if kp != 0.0:
+                    a0 = a0 + kp * log6(c.Rri @ Rw, c.pri + c.Rri @ pw)
+                if kd != 0.0:
+                    a0 = a0 + kd * vf
+                Js.append(J)
+            a0s.append(a0)
+        if not Js:
+            return np.zeros((0, nj), dt), np.zeros(0, dt)
+        return np.vstack(Js), np.concatenate(a0s)
+
+    def accel_force(self, x, u):
+        nj, nc = self.nj, self.nc
+        q, v = x[:nj], x[nj:]
+        M = self.robot.crba(q) + np.diag(self.robot.armature)
+        nle = self.robot.rnea(q, v, np.zeros(nj, np.result_type(x, float)))
+        tau = np.concatenate([np.zeros(self.nun, np.result_type(u, float)), u])
+        Jc, a0 = self.contact_terms(x)
+        K = np.zeros((nj + nc, nj + nc), dtype=np.result_type(M, Jc))
+        K[:nj, :nj] = M
+        K[:nj, nj:] = Jc.T
+        K[nj:, :nj] = Jc
+        K[nj:, nj:] = -self.damping * np.eye(nc)
+        sol = np.linalg.solve(K, np.concatenate([tau - nle, -a0]))
+        return sol[:nj], -sol[nj:]
+
+    def accel(self, x, u):
+        return self.accel_force(x, u)[0]
 
 
 def block_size(block):

@@ -76,3 +76,48 @@ def test_device_code_vs_oracle(lib, case, terminal):
             got = a.reshape(-1, rows).T if q in ("Fx", "Fu", "Lxx", "Lxu", "Luu") else a
             scale = max(1.0, float(np.max(np.abs(ref[q]))))
             assert float(np.max(np.abs(got - ref[q]))) / scale < 1e-10, (q, case, terminal)
+
+
+CONTACT_CASES = [dict(contact="6d"), dict(contact="3d", weighted=True), dict(contact="3d+3d", armature=np.full(7, 0.02)),
+                 dict(contact="6d+3d", damping=1e-3, inactive=True),
+                 dict(contact="6d", gains=(0.0, 0.0)), dict(contact="3d", gains=(5.0, 0.0)),
+                 dict(contact="6d+3d", robot=mb.sample_tree(10, seed=5), damping=1e-2, weighted=True)]
+
+
+@pytest.mark.parametrize("case", range(len(CONTACT_CASES)))
+@pytest.mark.parametrize("terminal", [False, True])
+def test_contact_device_code_vs_oracle(lib, case, terminal):
+    """Euler∘ContactFwdDynamics: device KKT solve + analytic derivatives vs the
+    oracle's single KKT solve + complex-step derivatives."""
+    x0s, running, term = synthetic.build_arm_contact(T=2, B=1, **CONTACT_CASES[case])
+    em = term if terminal else running[0]
+    kind, nu, blk = em.pack()
+    assert kind == 5
+    blk = np.ascontiguousarray(blk[0])
+    nx = em.state.nx
+    k = onp.ContactFwdKnot(blk, nx, nu)
+    rng = np.random.default_rng(100 + case)
+    for _ in range(3):
+        x, u = rng.uniform(-1.5, 1.5, nx), rng.uniform(-3, 3, nu)
+        use_u = 0 if terminal else 1
+        uo = None if terminal else u
+        xn = np.zeros(nx)
+        c = lib.mb_host_calc(_p(blk), nx, _p(x), _p(u), use_u, _p(xn))
+        xo, co = k.calc(x, uo)
+        np.testing.assert_allclose(xn, xo, rtol=1e-10, atol=1e-10)
+        assert c == pytest.approx(co, rel=1e-12, abs=1e-14)
+        n, m = nx, nu
+        out = {q: np.zeros(s) for q, s in [("Fx", n * n), ("Fu", n * m), ("Lxx", n * n), ("Lxu", n * m),
+                                           ("Luu", m * m), ("Lx", n), ("Lu", m)]}
+        xn2, c2 = np.zeros(nx), np.zeros(1)
+        lib.mb_host_calc_diff(_p(blk), nx, m, _p(x), _p(u), use_u,
+                              *[_p(out[q]) for q in ["Fx", "Fu", "Lxx", "Lxu", "Luu", "Lx", "Lu"]], _p(xn2), _p(c2))
+        np.testing.assert_allclose(xn2, xo, rtol=1e-10, atol=1e-10)
+        assert c2[0] == pytest.approx(co, rel=1e-12, abs=1e-14)
+        ref = k.calc_diff(x, uo)
+        for q, a in out.items():
+            rows = m if q == "Luu" else n
+            got = a.reshape(-1, rows).T if q in ("Fx", "Fu", "Lxx", "Lxu", "Luu") else a
+            scale = max(1.0, float(np.max(np.abs(ref[q]))))
+            assert float(np.max(np.abs(got - ref[q]))) / scale < 1e-9, (q, case, terminal,
+                                                                        float(np.max(np.abs(got - ref[q]))))

@@ -232,3 +232,118 @@ def test_cpp_oracle_solve_vs_numpy(case):
         assert r[b].iter == n.iter
         assert r[b].cost == pytest.approx(n.cost, rel=1e-9)
         np.testing.assert_allclose(xs[b], np.array(n.xs), rtol=1e-8, atol=1e-9)
+
+
+# ---- contact dynamics (ContactFwdKnot) -------------------------------------
+CONTACT_KW = [dict(contact="6d"), dict(contact="3d", weighted=True), dict(contact="3d+3d"),
+              dict(contact="6d+3d", damping=1e-3, inactive=True)]
+
+
+@pytest.mark.parametrize("kw", CONTACT_KW)
+def test_contact_kkt_identities(kw):
+    """The constrained dynamics satisfy pinocchio::forwardDynamics' equations:
+    RNEA(q, v, a) - Jc^T lambda = tau(u) and Jc a + a0 = -damping lambda
+    (contact-fwddyn.hxx:94-96), and Gauss' principle: a minimises
+    (a - a_free)^T M (a - a_free) on the constraint set (damping 0)."""
+    from crocoddyl_amd import synthetic
+    _, running, _ = synthetic.build_arm_contact(T=1, B=1, **kw)
+    kind, nu, blk = running[0].pack()
+    assert kind == 5 and nu == 6
+    k = onp.ContactFwdKnot(blk[0], 14, nu)
+    assert k.nc == {"6d": 6, "3d": 3, "3d+3d": 6, "6d+3d": 9}[kw["contact"]]
+    rng = np.random.default_rng(4)
+    for _ in range(3):
+        x, u = rng.uniform(-1, 1, 14), rng.uniform(-2, 2, nu)
+        a, lam = k.accel_force(x, u)
+        J, a0 = k.contact_terms(x)
+        tau = np.concatenate([[0.0], u])
+        sc = 1e-12 * max(1.0, np.abs(lam).max(), np.abs(a).max()) * np.linalg.cond(J @ J.T)
+        np.testing.assert_allclose(k.robot.rnea(x[:7], x[7:], a) - J.T @ lam, tau, atol=sc)
+        np.testing.assert_allclose(J @ a + a0, -k.damping * lam, atol=sc)
+        if k.damping == 0:
+            M = k.robot.crba(x[:7])
+            a_free = k.robot.aba(x[:7], x[7:], tau)
+            # any feasible perturbation (null space of J) increases the Gauss cost
+            N = np.linalg.svd(J)[2][J.shape[0]:].T
+            f0 = (a - a_free) @ M @ (a - a_free)
+            for _ in range(5):
+                d = N @ rng.standard_normal(N.shape[1]) * 1e-3 * max(1.0, np.abs(a).max())
+                assert (a + d - a_free) @ M @ (a + d - a_free) > f0
+
+
+def test_contact_3d_drift_is_classical_acceleration():
+    """a0 of a 3D contact without gains is the classical acceleration of the
+    frame origin in the frame (contact-3d.hxx:37): d^2/dt^2 of oMf.translation
+    along the ddq = 0 motion, rotated into the frame."""
+    from crocoddyl_amd import synthetic
+    _, running, _ = synthetic.build_arm_contact(T=1, B=1, contact="3d", gains=(0.0, 0.0))
+    _, nu, blk = running[0].pack()
+    k = onp.ContactFwdKnot(blk[0], 14, nu)
+    rng = np.random.default_rng(2)
+    q, v = rng.uniform(-1, 1, 7), rng.uniform(-1, 1, 7)
+    c = k.contacts[0]
+
+    def pos(t):  # q(t) = q + v t (ddq = 0)
+        oM = k.robot.placements(q + v * t)
+        R0, p0 = oM[c.joint]
+        return R0 @ c.Rf, p0 + R0 @ c.pf
+
+    h = 1e-4
+    acc_w = (pos(h)[1] - 2 * pos(0.0)[1] + pos(-h)[1]) / (h * h)
+    Rf = pos(0.0)[0]
+    _, a0 = k.contact_terms(np.concatenate([q, v]))
+    np.testing.assert_allclose(a0, Rf.T @ acc_w, atol=1e-5)
+
+
+@pytest.mark.parametrize("kw", CONTACT_KW)
+def test_contact_knot_derivatives_vs_numdiff(kw):
+    """Complex-step derivatives of the contact knot vs central differences
+    (test_actions.cpp:70-110 design, tol 3e4 sqrt(2 eps))."""
+    from crocoddyl_amd import synthetic
+    _, running, _ = synthetic.build_arm_contact(T=1, B=1, **kw)
+    _, nu, blk = running[0].pack()
+    k = onp.ContactFwdKnot(blk[0], 14, nu)
+    rng = np.random.default_rng(7)
+    x, u = rng.uniform(-1, 1, 14), rng.uniform(-2, 2, nu)
+    d = k.calc_diff(x, u)
+    h = np.sqrt(2 * np.finfo(float).eps)
+    tol = 3e4 * h
+    nz = 14 + nu
+    z = np.concatenate([x, u])
+    F = np.zeros((14, nz))
+    for j in range(nz):
+        e = np.zeros(nz)
+        e[j] = h
+        F[:, j] = (k.calc(z[:14] + e[:14], z[14:] + e[14:])[0] - k.calc(z[:14] - e[:14], z[14:] - e[14:])[0]) / (2 * h)
+    np.testing.assert_allclose(d["Fx"], F[:, :14], atol=tol)
+    np.testing.assert_allclose(d["Fu"], F[:, 14:], atol=tol)
+
+
+def test_contact_api_validation_and_order():
+    model = mb.sample_talos_arm()
+    state = mb.StateMultibody(model)
+    act = mb.ActuationModelFloatingBase(state)
+    assert act.nu == 6
+    fid = model.getFrameId("gripper_left_joint")
+    contacts = mb.ContactModelMultiple(state, 6)
+    with pytest.raises(ValueError):  # nu mismatch (multiple-contacts.hxx:22-26)
+        contacts.addContact("c", mb.ContactModel3D(state, mb.FrameTranslation(fid, np.zeros(3))))
+    contacts.addContact("z", mb.ContactModel3D(state, mb.FrameTranslation(fid, np.zeros(3)), 6))
+    contacts.addContact("a", mb.ContactModel6D(state, mb.FramePlacement(fid, mb.SE3()), 6, [1.0, 2.0]))
+    contacts.addContact("m", mb.ContactModel3D(state, mb.FrameTranslation(fid, np.ones(3)), 6), False)
+    assert contacts.nc == 9 and contacts.nc_total == 12
+    assert contacts.active == ["a", "z"] and contacts.inactive == ["m"]
+    costs = mb.CostModelSum(state, 6)
+    costs.addCost("u", mb.CostModelControl(state, 6), 1.0)
+    with pytest.raises(TypeError):
+        mb.DifferentialActionModelContactFwdDynamics(state, mb.ActuationModelFull(state), contacts, costs)
+    dam = mb.DifferentialActionModelContactFwdDynamics(state, act, contacts, costs, -1e-3)
+    assert dam.JMinvJt_damping == 1e-3  # fabs (contact-fwddyn.hxx:35)
+    em = croc.IntegratedActionModelEuler(dam, 1e-2)
+    kind, nu, blk = em.pack()
+    k = onp.ContactFwdKnot(blk[0], 14, 6)
+    assert [c.type for c in k.contacts] == [onp.CONTACT_6D, onp.CONTACT_3D]  # name order
+    assert k.contacts[0].gains == (1.0, 2.0) and k.damping == 1e-3 and k.nun == 1
+    contacts.changeContactStatus("m", True)
+    kind2, _, blk2 = croc.IntegratedActionModelEuler(dam, 1e-2).pack()
+    assert onp.ContactFwdKnot(blk2[0], 14, 6).nc == 12
