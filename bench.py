@@ -167,7 +167,12 @@ def main():
     n, m, nx = problem.ndx, problem.nu_max, problem.nx
     mpc_iters = 2 if box else 1
 
-    solver.solve(maxiter=5)  # converge once from a cold start
+    if kind == "multibody_contact":
+        # warm start at x0: the default (state.zero(), the stretched arm) is a
+        # singular configuration of the gripper contact (rank-deficient Jc)
+        solver.solve(np.repeat(x0s[:, None, :], T + 1, axis=1), [], maxiter=5)
+    else:
+        solver.solve(maxiter=5)  # converge once from a cold start
 
     def step():  # one receding-horizon MPC solve, all elements
         solver.mpcShift()
@@ -226,6 +231,9 @@ def main():
             "data": ("synthetic: arm-manipulation problem of benchmark/factory/arm.hpp on real multibody knots "
                      "(Euler ∘ FreeFwdDynamics, 7-DoF Talos-class arm model built in code: the URDF is absent), "
                      "per-element x0" if kind == "multibody" else
+                     "synthetic: the 7-DoF arm on contact dynamics (Euler ∘ ContactFwdDynamics, gripper "
+                     "ContactModel6D with Baumgarte gains, ActuationModelFloatingBase), xReg + uReg costs, "
+                     "per-element x0 = bent posture + U[-0.3, 0.3]" if kind == "multibody_contact" else
                      "synthetic: seeded Euler(dt)∘DifferentialActionModelLQR knots at the config's (n, m, T); "
                      "per-element matrices (SURVEY §8d); no robot model (Pinocchio/URDF absent)"),
             "config": {"workload": f"{args.config}: n={n}, m={m}, T={T}, B={B} per GPU, warm-started "

@@ -22,6 +22,9 @@ CONFIGS = {
     "C5_talos_full": ("euler", 38, 32, 100, 1024, 1e-3),
     # C3 on real multibody knots: Euler ∘ FreeFwdDynamics of the 7-DoF arm (build_arm)
     "C3_arm_multibody": ("multibody", 7, 7, 250, 512, 1e-3),
+    # the same arm on contact dynamics: Euler ∘ ContactFwdDynamics, gripper 6D
+    # contact, floating-base actuation (nu = 6), build_arm_contact
+    "C3_arm_contact": ("multibody_contact", 7, 6, 250, 512, 1e-3),
 }
 
 
@@ -77,6 +80,9 @@ def build(name, T=None, B=None, seed=None, drift_free=True):
     B = B0 if B is None else B
     if kind == "multibody":
         return build_arm(T=T, B=B, seed=seed)
+    if kind == "multibody_contact":
+        return build_arm_contact(T=T, B=B, seed=seed_of(name) + 1 if seed is None else seed, dt=dt, contact="6d",
+                                 q_nominal=ARM_BENT, spread=0.3)
     rng = np.random.default_rng(seed_of(name) if seed is None else seed)
     if kind == "unicycle":
         model = ActionModelUnicycle()
@@ -127,7 +133,7 @@ def build_hetero(name, T=None, B=None, seed=None, phase=10, impulse_every=7):
 
 
 def build_arm_contact(T=4, B=2, seed=0, robot=None, dt=1e-2, contact="6d", gains=(2.0, 1.5), damping=0.0,
-                      weighted=False, armature=None, inactive=False):
+                      weighted=False, armature=None, inactive=False, q_nominal=None, spread=1.0):
     """Contact-dynamics knots on the arm: Euler(dt) ∘ DifferentialActionModelContactFwdDynamics
     (contact-fwddyn.hxx) with ActuationModelFloatingBase (first joint unactuated)
     and a ContactModelMultiple on the gripper frame ("6d": ContactModel6D, "3d":
@@ -136,7 +142,8 @@ def build_arm_contact(T=4, B=2, seed=0, robot=None, dt=1e-2, contact="6d", gains
     when ``weighted``). ``inactive`` adds a contact item that is switched off
     (ContactModelMultiple::changeContactStatus). The terminal model is the same
     DAM with dt = 0. x0_b ~ U[-1,1]^(2 nv) per element (off the contact
-    manifold: the Baumgarte gains pull the frames back)."""
+    manifold: the Baumgarte gains pull the frames back); with ``q_nominal``,
+    q0_b ~ q_nominal + U[-spread, spread]^nq and v0_b ~ U[-spread, spread]^nv."""
     from . import multibody as mb
     rng = np.random.default_rng(seed)
     model = mb.sample_talos_arm() if robot is None else robot
@@ -174,8 +181,17 @@ def build_arm_contact(T=4, B=2, seed=0, robot=None, dt=1e-2, contact="6d", gains
         dam.armature = armature
     running = IntegratedActionModelEuler(dam, dt)
     terminal = IntegratedActionModelEuler(dam, 0.0)
-    x0s = np.hstack([rng.uniform(-1, 1, (B, state.nq)), rng.uniform(-1, 1, (B, state.nv))])
+    if q_nominal is None:
+        x0s = np.hstack([rng.uniform(-1, 1, (B, state.nq)), rng.uniform(-1, 1, (B, state.nv))])
+    else:
+        x0s = np.hstack([np.asarray(q_nominal, float) + rng.uniform(-spread, spread, (B, state.nq)),
+                         rng.uniform(-spread, spread, (B, state.nv))])
     return x0s, [running] * T, terminal
+
+
+# a bent arm posture (elbow flexed, wrist pitched), away from the stretched
+# contact singularity: the contact bench's nominal configuration
+ARM_BENT = (0.3, 0.4, -0.2, -1.3, 0.1, 0.6, 0.0)
 
 
 def build_arm(T=None, B=None, seed=None, robot=None, dt=1e-3, weighted=False, armature=None, w_x=1e-4, w_u=1e-4):
