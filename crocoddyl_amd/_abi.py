@@ -14,7 +14,7 @@ FDDP_ERR_NO_DEVICE = -4
 
 STATUS_RUNNING, STATUS_CONVERGED, STATUS_REGMAX = 0, 1, 2
 
-KNOT_LQR, KNOT_UNICYCLE, KNOT_EULER_DIFFLQR, KNOT_EULER_FREEFWD, KNOT_EULER_CONTACTFWD = 1, 2, 3, 4, 5
+KNOT_LQR, KNOT_UNICYCLE, KNOT_EULER_DIFFLQR, KNOT_EULER_FREEFWD, KNOT_EULER_CONTACTFWD, KNOT_IMPULSEFWD = 1, 2, 3, 4, 5, 6
 PARAM_HEADER = 4
 
 Q_FX, Q_FU, Q_LXX, Q_LXU, Q_LUU, Q_LX, Q_LU, Q_XNEXT, Q_FS, Q_K, Q_KV = range(11)

@@ -11,7 +11,7 @@ namespace fddp {
 
 // Multibody knots (variable-size blocks, multibody.hpp): free and contact dynamics.
 __host__ __device__ inline bool is_mb_kind(int kind) {
-  return kind == FDDP_KNOT_EULER_FREEFWD || kind == FDDP_KNOT_EULER_CONTACTFWD;
+  return kind == FDDP_KNOT_EULER_FREEFWD || kind == FDDP_KNOT_EULER_CONTACTFWD || kind == FDDP_KNOT_IMPULSEFWD;
 }
 
 constexpr int kWave = 64;

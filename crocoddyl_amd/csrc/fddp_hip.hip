@@ -83,8 +83,10 @@ int64_t mb_block_check(const double* P, int64_t avail, int kind, int nx, int nu,
   if (!(dt >= 0.) || !std::isfinite(dt)) return why = "dt has positive value", -1;
   if ((double)nj != P[1] || nj < 1 || nj > kMaxJ) return why = "number of joints out of [1, 32]", -1;
   if (nx != 2 * nj) return why = "multibody knots need nx = 2 nv", -1;
-  const bool contact = kind == FDDP_KNOT_EULER_CONTACTFWD;
-  if (!contact && nu != nj) return why = "ActuationModelFull needs nu = nv", -1;
+  const bool contact = kind == FDDP_KNOT_EULER_CONTACTFWD, impulse = kind == FDDP_KNOT_IMPULSEFWD;
+  if (!contact && !impulse && nu != nj) return why = "ActuationModelFull needs nu = nv", -1;
+  if (impulse && nu != 0) return why = "impulse knots have nu = 0", -1;
+  if (impulse && dt != 0.) return why = "impulse blocks carry dt = 0 (no integrator)", -1;
   if ((double)ncost != P[2] || ncost < 0 || ncost > kMaxCosts) return why = "number of costs out of [0, 64]", -1;
   if (size > avail || (double)size != P[3]) return why = "block out of range", -1;
   int64_t o = FDDP_PARAM_HEADER + 3 + nj;
@@ -119,12 +121,17 @@ int64_t mb_block_check(const double* P, int64_t avail, int kind, int nx, int nu,
     o += rs;
   }
   int nc = 0;
-  if (contact) {  // [nun, damping, ncontact, 0] + contact records
+  if (contact || impulse) {  // [nun | r_coeff, damping, ncontact, 0 | 1] + contact / impulse records
     if (o + 4 > size) return why = "contact section out of range", -1;
     const int nun = (int)P[o], ncon = (int)P[o + 2];
     const double damping = P[o + 1];
-    if ((double)nun != P[o] || nun < 0 || nun >= nj) return why = "unactuated dofs out of [0, nv)", -1;
-    if (nu != nj - nun) return why = "ActuationModelFloatingBase needs nu = nv - nun", -1;
+    if (P[o + 3] != (impulse ? 1. : 0.)) return why = "contact / impulse section flag does not match the kind", -1;
+    if (impulse) {
+      if (!(P[o] >= 0.) || !std::isfinite(P[o])) return why = "The restitution coefficient has to be positive", -1;
+    } else {
+      if ((double)nun != P[o] || nun < 0 || nun >= nj) return why = "unactuated dofs out of [0, nv)", -1;
+      if (nu != nj - nun) return why = "ActuationModelFloatingBase needs nu = nv - nun", -1;
+    }
     if (!(damping >= 0.) || !std::isfinite(damping)) return why = "The damping factor has to be positive", -1;
     if ((double)ncon != P[o + 2] || ncon < 0) return why = "negative number of contacts", -1;
     o += 4;
@@ -134,8 +141,8 @@ int64_t mb_block_check(const double* P, int64_t avail, int kind, int nx, int nu,
       const int type = (int)C[0];
       const int64_t rs = (int64_t)C[3];
       int64_t want = -1;
-      if (type == C_CONTACT_3D) want = kCHdr + 16;
-      if (type == C_CONTACT_6D) want = kCHdr + 25;
+      if (type == C_CONTACT_3D) want = kCHdr + (impulse ? 13 : 16);
+      if (type == C_CONTACT_6D) want = kCHdr + (impulse ? 13 : 25);
       if (want < 0) return why = "unknown contact type " + std::to_string(type), -1;
       if (rs != want || o + rs > size) return why = "contact record of the wrong size", -1;
       const int fj = (int)C[kCHdr];

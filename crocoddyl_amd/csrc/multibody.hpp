@@ -53,6 +53,9 @@ struct Blk {
   int ncon, nc;       // active contact records, stacked rows
   double damping;     // JMinvJt_damping
   const double* K;    // contact records
+  // impulse section instead (ActionModelImpulseFwdDynamics, nu = 0)
+  bool impulse;
+  double r_coeff;     // restitution coefficient
 };
 
 MB_HD inline Blk parse(const double* P) {
@@ -70,8 +73,12 @@ MB_HD inline Blk parse(const double* P) {
   b.ncon = b.nc = 0;
   b.damping = 0.;
   b.K = e;
-  if (e - P < (int64_t)P[3]) {  // [nun, damping, ncontact, 0] + records
-    b.nun = (int)e[0];
+  b.impulse = false;
+  b.r_coeff = 0.;
+  if (e - P < (int64_t)P[3]) {  // [nun | r_coeff, damping, ncontact, 0 | 1] + records
+    b.impulse = (int)e[3] == 1;
+    b.nun = b.impulse ? b.nj : (int)e[0];
+    b.r_coeff = b.impulse ? e[0] : 0.;
     b.damping = e[1];
     b.ncon = (int)e[2];
     b.K = e + 4;
@@ -969,7 +976,8 @@ template <class X>
 MB_HD inline double knot_calc_x(const X& ex, const double* P, int nx, const double* x, const double* u, bool use_u,
                                 double* xnext, double* w) {
   const Blk b = parse(P);
-  const int nj = b.nj, nc = b.nc, nu = nj - b.nun, ncol = nj + nc + 1;
+  const bool imp = b.impulse;  // impulse: [M | Jc^T] only, z = v
+  const int nj = b.nj, nc = b.nc, nu = nj - b.nun, ncol = imp ? nj + nc : nj + nc + 1;
   const WVals W{w, nj};
   double* A = w + WVals::doubles(nj);  // nj x (nj + nc + 1), ld nj: [M | Jc^T | tau - nle]
   double* tau = A + (int64_t)nj * ncol;
@@ -993,14 +1001,14 @@ MB_HD inline double knot_calc_x(const X& ex, const double* P, int nx, const doub
       cr += C.size();
     }
   });
-  world_rnea(ex, b, W, x + nj, nullptr, tau);
+  if (!imp) world_rnea(ex, b, W, x + nj, nullptr, tau);
   ex.run([&](int lane) {
     if (lane < nj) {
       const double ti = lane < b.nun ? 0. : ub[lane - b.nun];  // ActuationModelFloatingBase: tau = [0; u]
-      A[(int64_t)nj * (nj + nc) + lane] = ti - tau[lane];
+      if (!imp) A[(int64_t)nj * (nj + nc) + lane] = ti - tau[lane];
       if (nc) contact_jac_lane(b, W, lane, Jc, A);
     }
-    if (lane >= 64 && lane < 64 + b.ncon) {
+    if (!imp && lane >= 64 && lane < 64 + b.ncon) {
       int row0;
       const CRec C{contact_rec(b, lane - 64, &row0)};
       contact_a0(b, W, C, a0 + row0);
@@ -1012,21 +1020,23 @@ MB_HD inline double knot_calc_x(const X& ex, const double* P, int nx, const doub
     }
   });
   bool ok = gauss_jordan(ex, A, nj, ncol, flag);
-  double* a = A + (int64_t)nj * (nj + nc);  // z, then a
+  // z, then a (impulse: v+, in tau's slot; z = M^-1 M v = v)
+  double* a = imp ? tau : A + (int64_t)nj * (nj + nc);
   if (nc > 0) {
     ex.run([&](int lane) {
       for (int e = lane; e < nc * (nc + 1); e += ex.nt) {
         const int col = e / nc, row = e % nc;
-        const double* yc = A + (int64_t)nj * (nj + col);  // column col of Y, or z
+        // column col of Y, or z (impulse: v, and the restitution term r Jc v)
+        const double* yc = (imp && col == nc) ? x + nj : A + (int64_t)nj * (nj + col);
         double s = 0.;
         for (int i = 0; i < nj; ++i) s += Jc[(int64_t)row * nj + i] * yc[i];
-        S[e] = col < nc ? s + (row == col ? b.damping : 0.) : s + a0[row];
+        S[e] = col < nc ? s + (row == col ? b.damping : 0.) : (imp ? (1. + b.r_coeff) * s : s + a0[row]);
       }
     });
     ok = gauss_jordan(ex, S, nc, nc + 1, flag) && ok;
     ex.run([&](int lane) {
       if (lane >= nj) return;
-      double s = a[lane];
+      double s = imp ? x[nj + lane] : a[lane];
       for (int k = 0; k < nc; ++k) s -= A[(int64_t)nj * (nj + k) + lane] * S[(int64_t)nc * nc + k];
       a[lane] = s;
     });
@@ -1035,6 +1045,11 @@ MB_HD inline double knot_calc_x(const X& ex, const double* P, int nx, const doub
   const double dt = b.dt;
   ex.run([&](int i) {
     if (i >= nj) return;
+    if (imp) {  // impulse-fwddyn.hxx:80-81: xnext = (q, v+)
+      xnext[i] = x[i];
+      xnext[nj + i] = ok ? (nc > 0 ? a[i] : x[nj + i]) : NAN;
+      return;
+    }
     const double ai = ok ? a[i] : NAN;  // a singular mass matrix surfaces as forward_error
     if (dt != 0.) {
       const double v = x[nj + i];
@@ -1062,7 +1077,7 @@ struct DiffLayout {
   int64_t wv, vals, A, tang, dtau, J, xu, red, ct, total;
   // contact area (nc > 0): Jc nc x nj, a0 nc, lambda nc, Y = Minv Jc^T and
   // H = Y S^-1 (nj x nc each), [S | I | r] nc x (2nc + 1), da0/dx nc x L, fx 6 nj
-  int64_t Jc, a0, lam, Y, H, Sx, da0, fx;
+  int64_t Jc, a0, lam, Y, H, Sx, da0, fx, zv;
 };
 __host__ __device__ inline DiffLayout diff_layout(int nj, int nframe, int nc = 0) {
   const int L = 2 * nj;
@@ -1084,7 +1099,8 @@ __host__ __device__ inline DiffLayout diff_layout(int nj, int nframe, int nc = 0
   l.Sx = l.H + (int64_t)nj * nc;
   l.da0 = l.Sx + (int64_t)nc * (2 * nc + 1);
   l.fx = l.da0 + (int64_t)nc * L;
-  l.total = nc > 0 ? l.fx + 6 * nj : l.ct;
+  l.zv = l.fx + 6 * nj;  // impulse: v+ - v
+  l.total = nc > 0 ? l.zv + nj : l.ct;
   return l;
 }
 
@@ -1218,6 +1234,43 @@ MB_HD inline void contact_tangent(const Blk& b, const Vals& V, const WVals& W, i
   }
 }
 
+// d(Jc v+)/dq_c for the impulse records (impulse-3d.hxx:33-39 / impulse-6d.hxx:30-36:
+// getJointVelocityDerivatives at v+, moved into the frame): the joint velocity
+// tangent along q_c walked from the root to each record's joint (vp: joint-frame
+// velocities at v+, 6 per joint; qdp = v+). dv0[row * L + lane].
+MB_HD inline void impulse_tangent(const Blk& b, const Vals& V, const WVals& W, const double* vp, const double* qdp,
+                                  int c, int L, int lane, double* dv0) {
+  const double* r = b.K;
+  int row = 0;
+  for (int k = 0; k < b.ncon; ++k) {
+    const CRec C{r};
+    const double* d = C.d();
+    const int j = (int)d[0];
+    const unsigned am = *W.anc(j);
+    double dv[6] = {0., 0., 0., 0., 0., 0.};
+    for (int i = 0; i <= j; ++i) {  // ancestors-or-self in root-to-j order (parents precede children)
+      if (!((am >> i) & 1u)) continue;
+      double t6[6];
+      motion_act_inv(V.R(i), V.p(i), dv, t6);
+      if (i == c) {  // d(X^-1 v_parent)/dq_i = -S x (X^-1 v_parent), X^-1 v_parent = v_i - S qd_i
+        const double* ax = JRec(b, i).axis();
+        const double S[6] = {0., 0., 0., ax[0], ax[1], ax[2]};
+        double u6[6], w6[6];
+        for (int e = 0; e < 6; ++e) u6[e] = vp[6 * i + e] - S[e] * qdp[i];
+        cross_m(S, u6, w6);
+        for (int e = 0; e < 6; ++e) t6[e] -= w6[e];
+      }
+      for (int e = 0; e < 6; ++e) dv[e] = t6[e];
+    }
+    double dvf[6];
+    motion_act_inv(d + 1, d + 10, dv, dvf);
+    const int n = C.type() == C_CONTACT_3D ? 3 : 6;
+    for (int e = 0; e < n; ++e) dv0[(int64_t)(row + e) * L + lane] = dvf[e];
+    row += n;
+    r += C.size();
+  }
+}
+
 // model->calcDiff for one knot by one 64-thread workgroup (euler.hxx:83-131,
 // free-fwddyn.hxx:82-118, cost-sum.hxx:122-160). Writes full blocks (entries
 // beyond nu zero); Lxu is zero (no cost couples x and u). A mass matrix that is
@@ -1231,6 +1284,7 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
                                    double* Luu, double* Lx, double* Lu, double* xnext_out = nullptr,
                                    double* cost_out = nullptr) {
   const Blk b = parse(P);
+  const bool imp = b.impulse;  // ActionModelImpulseFwdDynamics (impulse-fwddyn.hxx:53-127)
   const int nj = b.nj, n = nx, L = 2 * nj, nc = b.nc, nu = nj - b.nun;
   int nframe = 0;
   {
@@ -1261,9 +1315,10 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
   double* Sx = w + l.Sx;
   double* da0 = w + l.da0;
   double* fx = w + l.fx;
+  double* zv = w + l.zv;
   ex.run([&](int lane) {
     if (lane < nx) x[lane] = xg[lane];
-    if (lane < nu) u[lane] = use_u ? ug[lane] : 0.;
+    if (lane < nj) u[lane] = (use_u && lane < nu) ? ug[lane] : 0.;  // (impulse: a zero velocity)
     for (int e = lane; e < 2 * nj * nj; e += ex.nt) {
       const int c = e / nj, r = e % nj;
       A[e] = (c == nj + r) ? 1. : 0.;
@@ -1271,11 +1326,11 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
   });
   // world-frame kinematics, M into the left half of [M | I], nle -> dtau[0..nj)
   world_kinematics(ex, b, W, x, A, [](int, int) {});
-  world_rnea(ex, b, W, x + nj, nullptr, dtau);
+  if (!imp) world_rnea(ex, b, W, x + nj, nullptr, dtau);
   if (nc > 0)  // contact rows at the drift (ddq = 0; ContactModelMultiple::calc)
     ex.run([&](int lane) {
       if (lane < nj) contact_jac_lane(b, W, lane, Jc, nullptr);
-      for (int k = lane; k < b.ncon; k += ex.nt) {
+      for (int k = lane; k < (imp ? 0 : b.ncon); k += ex.nt) {
         int row0;
         const CRec C{contact_rec(b, k, &row0)};
         contact_a0(b, W, C, a0 + row0);
@@ -1286,7 +1341,12 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
   // z = (M + A)^-1 (tau - nle) -> dtau[nj..2nj) (the acceleration without contacts);
   // Y = Minv Jc^T
   ex.run([&](int lane) {
-    if (lane < nj) {
+    if (lane < nj && imp) {
+      dtau[nj + lane] = x[nj + lane];  // z = M^-1 (M v) = v
+      zv[lane] = 0.;
+      if (lane == 0)
+        for (int e = 0; e < 6; ++e) W.root_a()[e] = 0.;  // the impulse RNEA has no gravity
+    } else if (lane < nj) {
       double s = 0.;
       for (int k = 0; k < nj; ++k) s += Minv[(int64_t)k * nj + lane] * ((k < b.nun ? 0. : u[k - b.nun]) - dtau[k]);
       dtau[nj + lane] = ok ? s : NAN;
@@ -1313,7 +1373,7 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
         } else {
           double s = 0.;
           for (int i = 0; i < nj; ++i) s += Jc[(int64_t)row * nj + i] * dtau[nj + i];
-          v = s + a0[row];
+          v = imp ? (1. + b.r_coeff) * s : s + a0[row];  // impulse: Jc v+ = -r Jc v
         }
         Sx[e] = v;
       }
@@ -1344,20 +1404,24 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
         for (int k = 0; k < nc; ++k) s -= H[(int64_t)k * nj + i] * Y[(int64_t)k * nj + c];
         Minv[e] = s;
       }
-      if (lane < nj) contact_joint_forces(b, W, lam, fx, lane);
+      if (lane < nj) {
+        contact_joint_forces(b, W, lam, fx, lane);
+        if (imp) zv[lane] = dtau[nj + lane] - x[nj + lane];  // v+ - v
+      }
     });
   }
   // accelerations and forces at the solved a (the linearisation point of
   // computeABADerivatives / computeRNEADerivatives with fext); tau lands in
   // dtau[2nj..3nj) and is not used
-  world_rnea(ex, b, W, x + nj, dtau + nj, dtau + 2 * nj, nc > 0 ? fx : nullptr);
+  // (impulse: RNEA(q, 0, v+ - v) without gravity, impulse-fwddyn.hxx:102-104)
+  world_rnea(ex, b, W, imp ? u : x + nj, imp ? zv : dtau + nj, dtau + 2 * nj, nc > 0 ? fx : nullptr);
   // joint-frame values for the tangent recursion: liMi, oMi, and v, a, F moved
   // from world to joint coordinates (SE3::actInv of oMi)
   ex.run([&](int i) {
     if (i == 0)
       for (int e = 0; e < 6; ++e) {
         V.root_v()[e] = 0.;
-        V.root_a()[e] = e < 3 ? -b.g[e] : 0.;
+        V.root_a()[e] = (e < 3 && !imp) ? -b.g[e] : 0.;
       }
     if (i >= nj) return;
     double oR[9], op[3], t6[6], m6[6];
@@ -1392,7 +1456,10 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
   if (xnext_out || cost_out) {  // the knot's calc, fused (iteration 0 of a solve, or calc only)
     ex.run([&](int lane) {
       const double dt = b.dt;
-      if (xnext_out && lane < nj) {
+      if (xnext_out && lane < nj && imp) {
+        xnext_out[lane] = x[lane];
+        xnext_out[nj + lane] = dtau[nj + lane];
+      } else if (xnext_out && lane < nj) {
         const double ai = dtau[nj + lane];
         if (dt != 0.) {
           const double v = x[nj + lane];
@@ -1410,11 +1477,23 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
     });
   }
   if (!Fx) return;  // calc only
-  // tangents (lanes < 2 nj) and frame-cost residuals / Jacobian columns (lanes < nj)
+  if (imp && nc > 0)  // joint-frame velocities at v+ (into fx, free after the RNEA); zv = v+
+    ex.run([&](int lane) {
+      if (lane >= nj) return;
+      w_velocity(W, dtau + nj, lane);
+      double m6[6], t6[6];
+      for (int e = 0; e < 6; ++e) m6[e] = W.v(lane)[e];
+      motion_act_inv(W.oR(lane), W.op(lane), m6, t6);
+      for (int e = 0; e < 6; ++e) fx[6 * lane + e] = t6[e];
+      zv[lane] = dtau[nj + lane];
+    });
+  // tangents (lanes < 2 nj; impulse: q directions only) and frame-cost residuals /
+  // Jacobian columns (lanes < nj)
   ex.run([&](int lane) {
-    if (lane < L) {
-      rnea_tangent(b, V, x + nj, lane < nj ? 0 : 1, lane % nj, T, L, lane, dtau);
-      if (nc > 0) contact_tangent(b, V, W, lane < nj ? 0 : 1, lane % nj, T, L, lane, da0);
+    if (lane < (imp ? nj : L)) {
+      rnea_tangent(b, V, imp ? u : x + nj, lane < nj ? 0 : 1, lane % nj, T, L, lane, dtau);
+      if (nc > 0 && imp) impulse_tangent(b, V, W, fx, zv, lane, L, lane, da0);
+      else if (nc > 0) contact_tangent(b, V, W, lane < nj ? 0 : 1, lane % nj, T, L, lane, da0);
     }
     if (lane >= nj) return;
     const double* cr = b.C;
@@ -1445,7 +1524,20 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
     for (int e = lane; e < n * n; e += ex.nt) {
       const int c = e / n, i = e % n, r = i < nj ? i : i - nj;
       double f;
-      if (integ) {
+      if (imp) {  // [[I, 0], [-G dtau_dq - H dv0_dq, G M = I - H Jc]] (impulse-fwddyn.hxx:111-115)
+        if (i < nj) {
+          f = c == i ? 1. : 0.;
+        } else if (c < nj) {
+          double s = 0.;
+          for (int k = 0; k < nj; ++k) s += Minv[(int64_t)k * nj + r] * dtau[(int64_t)k * L + c];
+          for (int k = 0; k < nc; ++k) s += H[(int64_t)k * nj + r] * da0[(int64_t)k * L + c];
+          f = ok ? -s : NAN;
+        } else {
+          double s = 0.;
+          for (int k = 0; k < nc; ++k) s += H[(int64_t)k * nj + r] * Jc[(int64_t)k * nj + (c - nj)];
+          f = ok ? (c - nj == r ? 1. : 0.) - s : NAN;
+        }
+      } else if (integ) {
         double s = 0.;
         for (int k = 0; k < nj; ++k) s += Minv[(int64_t)k * nj + r] * dtau[(int64_t)k * L + c];
         for (int k = 0; k < nc; ++k) s += H[(int64_t)k * nj + r] * da0[(int64_t)k * L + c];

@@ -509,15 +509,21 @@ class DifferentialActionModelFreeFwdDynamics:
 
     def pack_body(self, dt):
         """(Bm, size) rows of the FDDP_KNOT_EULER_FREEFWD block for step dt."""
-        model = self.state.pinocchio
-        robot = model.pack_robot(self._armature).reshape(1, -1)
-        recs = self.costs.pack()
-        parts = [robot] + recs
-        Bm = max(p.shape[0] for p in parts)
-        size = _abi.PARAM_HEADER + sum(p.shape[1] for p in parts)
-        hdr = np.array([[dt, model.nv, len(recs), size]])
-        return np.ascontiguousarray(
-            np.concatenate([np.broadcast_to(p, (Bm, p.shape[1])) for p in [hdr] + parts], axis=1))
+        return _pack_mb(self.state, self._armature, self.costs, dt)
+
+
+def _pack_mb(state, armature, costs, dt, section=None):
+    """(Bm, size) rows of a multibody block: header [dt, nv, ncost, size], robot,
+    cost records, then the optional contact / impulse section."""
+    model = state.pinocchio
+    robot = model.pack_robot(armature).reshape(1, -1)
+    recs = costs.pack()
+    parts = [robot] + recs + ([np.asarray(section, float).reshape(1, -1)] if section is not None else [])
+    Bm = max(p.shape[0] for p in parts)
+    size = _abi.PARAM_HEADER + sum(p.shape[1] for p in parts)
+    hdr = np.array([[dt, model.nv, len(recs), size]])
+    return np.ascontiguousarray(
+        np.concatenate([np.broadcast_to(p, (Bm, p.shape[1])) for p in [hdr] + parts], axis=1))
 
 
 class _Contact:
@@ -682,8 +688,158 @@ class DifferentialActionModelContactFwdDynamics(DifferentialActionModelFreeFwdDy
         recs = self.contacts.pack()
         if self.contacts.nc > MAX_CONTACT_ROWS:
             raise ValueError(f"Invalid argument: the device path holds at most {MAX_CONTACT_ROWS} contact rows")
-        base = super().pack_body(dt)
         sec = np.concatenate([[self.actuation.nun, self.JMinvJt_damping, len(recs), 0.0]] + recs)
-        out = np.concatenate([base, np.broadcast_to(sec, (base.shape[0], sec.size))], axis=1)
-        out[:, 3] = out.shape[1]
-        return np.ascontiguousarray(out)
+        return _pack_mb(self.state, self._armature, self.costs, dt, sec)
+
+
+class _Impulse:
+    """ImpulseModelAbstract (impulse-base.hxx): an impulse on a frame (LOCAL)."""
+
+    type = 0
+    ni = 0
+
+    def __init__(self, state, frame):
+        self.state = state
+        self.frame = int(frame)
+        model = state.pinocchio
+        if not 0 <= self.frame < len(model.frames):
+            raise ValueError("Invalid argument: unknown frame")
+
+    def pack(self):
+        name, pj, pl = self.state.pinocchio.frames[self.frame]
+        if pj == 0:
+            raise ValueError("Invalid argument: frames attached to the universe are not supported")
+        body = np.concatenate([[pj - 1], pl.rotation.T.reshape(-1), pl.translation])
+        return np.concatenate([[self.type, 0.0, 0.0, COST_HDR + body.size], body])
+
+
+class ImpulseModel3D(_Impulse):
+    """ImpulseModel3D(state, frame) (impulses/impulse-3d.hxx): point impulse,
+    Jc = the 3 linear rows of the LOCAL frame Jacobian."""
+
+    type = CONTACT_3D
+    ni = 3
+
+
+class ImpulseModel6D(_Impulse):
+    """ImpulseModel6D(state, frame) (impulses/impulse-6d.hxx): rigid impulse,
+    Jc = the LOCAL frame Jacobian."""
+
+    type = CONTACT_6D
+    ni = 6
+
+
+class ImpulseItem:
+    def __init__(self, name, impulse, active=True):
+        self.name, self.impulse, self.active = name, impulse, bool(active)
+
+
+class ImpulseModelMultiple:
+    """ImpulseModelMultiple (impulses/multiple-impulses.hxx): named impulses in a
+    std::map; the active ones stack their rows in name order."""
+
+    def __init__(self, state):
+        self.state = state
+        self.impulses = {}
+        self._version = 0
+
+    def addImpulse(self, name, impulse, active=True):
+        if name in self.impulses:  # the reference prints a warning and keeps the old item
+            return
+        self.impulses[name] = ImpulseItem(name, impulse, active)
+        self._version += 1
+
+    def removeImpulse(self, name):
+        if name in self.impulses:
+            del self.impulses[name]
+            self._version += 1
+
+    def changeImpulseStatus(self, name, active):
+        if name in self.impulses:
+            self.impulses[name].active = bool(active)
+            self._version += 1
+
+    @property
+    def ni(self):
+        return sum(c.impulse.ni for c in self.impulses.values() if c.active)
+
+    @property
+    def ni_total(self):
+        return sum(c.impulse.ni for c in self.impulses.values())
+
+    @property
+    def active(self):
+        return sorted(n for n, c in self.impulses.items() if c.active)
+
+    @property
+    def inactive(self):
+        return sorted(n for n, c in self.impulses.items() if not c.active)
+
+    def pack(self):
+        return [self.impulses[n].impulse.pack() for n in self.active]
+
+
+def _impulse_model_base():
+    from .models import ActionModelAbstract
+    return ActionModelAbstract
+
+
+class ActionModelImpulseFwdDynamics(_impulse_model_base()):
+    """ActionModelImpulseFwdDynamics(state, impulses, costs, r_coeff=0.,
+    inv_damping=0., enable_force=False) (multibody/actions/impulse-fwddyn.hxx:15-127):
+    nu = 0, xnext = (q, v+) with
+        [M  Jc^T ; Jc  0] [v+ ; -Lambda] = [M v ; -r_coeff Jc v]
+    (Schur complement with JMinvJt + inv_damping I), cost = costs.calc(x).
+    An action model itself (no integrator): a running knot of the ShootingProblem."""
+
+    kind = _abi.KNOT_IMPULSEFWD
+
+    def __init__(self, state, impulses, costs, r_coeff=0.0, inv_damping=0.0, enable_force=False):
+        if not isinstance(impulses, ImpulseModelMultiple):
+            raise TypeError("ActionModelImpulseFwdDynamics needs an ImpulseModelMultiple")
+        if r_coeff < 0.0:
+            raise ValueError("Invalid argument: The restitution coefficient has to be positive, set to 0")
+        if inv_damping < 0.0:
+            raise ValueError("Invalid argument: The damping factor has to be positive, set to 0")
+        if costs.nu != 0:
+            raise ValueError("Invalid argument: impulse knots have no controls (CostModelSum(state, 0))")
+        super().__init__(state, 0, costs.nr)
+        self.impulses = impulses
+        self.costs = costs
+        self.r_coeff = float(r_coeff)
+        self.JMinvJt_damping = float(inv_damping)
+        self.enable_force = bool(enable_force)
+        self._armature = np.zeros(state.nv)
+        self._arm_version = 0
+
+    @property
+    def armature(self):
+        return self._armature.copy()
+
+    @armature.setter
+    def armature(self, a):
+        a = np.array(a, np.float64).reshape(-1)
+        if a.size != self.state.nv:
+            raise ValueError(f"Invalid argument: The armature dimension is wrong (it should be {self.state.nv})")
+        self._armature = a
+        self._arm_version += 1
+
+    @property
+    def _version(self):
+        return (self.__dict__.get("_own_version", 0), self.state.pinocchio._version, self.costs._version,
+                self.impulses._version, self._arm_version, self.r_coeff, self.JMinvJt_damping,
+                tuple(getattr(c.cost, "_version", 0) for c in self.costs.costs.values()))
+
+    @_version.setter
+    def _version(self, v):
+        self.__dict__["_own_version"] = v if not isinstance(v, tuple) else v[0]
+
+    def _touch(self):
+        self.__dict__["_own_version"] = self.__dict__.get("_own_version", 0) + 1
+
+    def pack(self):
+        recs = self.impulses.pack()
+        if self.impulses.ni > MAX_CONTACT_ROWS:
+            raise ValueError(f"Invalid argument: the device path holds at most {MAX_CONTACT_ROWS} impulse rows")
+        sec = np.concatenate([[self.r_coeff, self.JMinvJt_damping, len(recs), 1.0]] + recs)
+        return self.kind, 0, _pack_mb(self.state, self._armature, self.costs, 0.0, sec)

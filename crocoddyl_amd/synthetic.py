@@ -189,6 +189,47 @@ def build_arm_contact(T=4, B=2, seed=0, robot=None, dt=1e-2, contact="6d", gains
     return x0s, [running] * T, terminal
 
 
+def impulse_model(robot=None, kind="6d", r_coeff=0.0, damping=0.0, weighted=False, armature=None, inactive=False):
+    """ActionModelImpulseFwdDynamics on the arm's gripper ("6d": ImpulseModel6D,
+    "3d": ImpulseModel3D, "6d+3d": plus a 3D impulse on the elbow frame),
+    costs xReg (+ an elbow FrameTranslation when ``weighted``)."""
+    from . import multibody as mb
+    model = mb.sample_talos_arm() if robot is None else robot
+    if not model.existFrame("elbow_site"):
+        model.addFrame("elbow_site", min(4, model.nv), mb.SE3(np.eye(3), (0.0, 0.05, -0.1)))
+    state = mb.StateMultibody(model)
+    fid = model.getFrameId("gripper_left_joint") if model.existFrame("gripper_left_joint") else model.getFrameId("tip")
+    eid = model.getFrameId("elbow_site")
+    imps = mb.ImpulseModelMultiple(state)
+    kinds = kind.split("+")
+    imps.addImpulse("gripper", mb.ImpulseModel6D(state, fid) if kinds[0] == "6d" else mb.ImpulseModel3D(state, fid))
+    if len(kinds) > 1:
+        imps.addImpulse("elbow", mb.ImpulseModel3D(state, eid))
+    if inactive:
+        imps.addImpulse("aux", mb.ImpulseModel3D(state, eid), active=False)
+    costs = mb.CostModelSum(state, 0)
+    costs.addCost("xReg", mb.CostModelState(state, 0), 1e-2)
+    if weighted:
+        costs.addCost("elbowTrans", mb.CostModelFrameTranslation(state, mb.FrameTranslation(eid, (0.1, 0.0, 0.2)),
+                                                                 0), 0.3)
+    am = mb.ActionModelImpulseFwdDynamics(state, imps, costs, r_coeff, damping)
+    if armature is not None:
+        am.armature = armature
+    return am
+
+
+def build_arm_impact(T=8, B=2, seed=0, dt=1e-2, r_coeff=0.0):
+    """A contact-switch horizon (the pattern of the reference's gait / jumping
+    problems): free-flight knots (Euler ∘ FreeFwdDynamics, nu = 7) up to T/2,
+    an impulse knot (ActionModelImpulseFwdDynamics, nu = 0) on the gripper at
+    T/2, then gripper-contact knots (Euler ∘ ContactFwdDynamics, nu = 6)."""
+    x0s, run_c, term_c = build_arm_contact(T=T, B=B, seed=seed, dt=dt, contact="6d", q_nominal=ARM_BENT, spread=0.3)
+    _, run_f, _ = build_arm(T=T, B=B, dt=dt, w_x=1e-2, w_u=1e-2)
+    imp = impulse_model(robot=run_c[0].differential.state.pinocchio, kind="6d", r_coeff=r_coeff)
+    h = T // 2
+    return x0s, run_f[:h] + [imp] + run_c[h + 1:], term_c
+
+
 # a bent arm posture (elbow flexed, wrist pitched), away from the stretched
 # contact singularity: the contact bench's nominal configuration
 ARM_BENT = (0.3, 0.4, -0.2, -1.3, 0.1, 0.6, 0.0)

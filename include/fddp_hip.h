@@ -95,6 +95,17 @@ extern "C" {
  * At most 24 stacked contact rows (nc); the Schur complement Jc M^-1 Jc^T +
  * damping I must be positive definite (full-rank Jc or damping > 0). */
 #define FDDP_KNOT_EULER_CONTACTFWD 5
+/* ActionModelImpulseFwdDynamics (multibody/actions/impulse-fwddyn.hxx:53-127): an
+ * action model (no integrator), nu = 0, xnext = (q, v+) with the impulse
+ * dynamics [M Jc^T; Jc 0][v+; -Lambda] = [M v; -r_coeff Jc v], cost = costs(x);
+ * ImpulseModelMultiple of ImpulseModel3D / 6D (impulses/impulse-{3d,6d}.hxx).
+ * Block: the FDDP_KNOT_EULER_FREEFWD layout with dt = 0, then
+ *   [r_coeff, JMinvJt_damping, nimpulse, 1]
+ *   nimpulse active impulse records in name order, each
+ *     [type (5: 3D, 6: 6D), 0, 0, size = 17], frame joint, frame placement R(9) p(3)
+ * calcDiff follows the reference's formula (restitution terms left out of Fx, as
+ * impulse-fwddyn.hxx:111-115). At most 24 stacked impulse rows. */
+#define FDDP_KNOT_IMPULSEFWD 6
 
 #define FDDP_PARAM_HEADER 4 /* doubles of scalar header in front of every block */
 

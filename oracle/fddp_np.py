@@ -29,7 +29,7 @@ import math
 
 import numpy as np
 
-LQR, UNICYCLE, EULER_DIFFLQR, EULER_FREEFWD, EULER_CONTACTFWD = 1, 2, 3, 4, 5
+LQR, UNICYCLE, EULER_DIFFLQR, EULER_FREEFWD, EULER_CONTACTFWD, IMPULSEFWD = 1, 2, 3, 4, 5, 6
 HDR = 4
 
 
@@ -171,6 +171,10 @@ def bind_problem(knot_descs, pool, b, nx):
         if kind == EULER_CONTACTFWD:
             from oracle.multibody_np import ContactFwdKnot
             out.append(ContactFwdKnot(pool[o:o + int(pool[o + 3])], nx, nu))
+            continue
+        if kind == IMPULSEFWD:
+            from oracle.multibody_np import ImpulseFwdKnot
+            out.append(ImpulseFwdKnot(pool[o:o + int(pool[o + 3])], nx, nu))
             continue
         size = block_size(kind, nx, nu)
         out.append(Knot(kind, nx, nu, pool[o:o + size]))

@@ -195,12 +195,13 @@ class Robot:
         return out
 
     # Featherstone Table 5.1 (Pinocchio rnea)
-    def rnea(self, q, v, a):
+    def rnea(self, q, v, a, gravity=None):
         dt = np.result_type(q, v, a)
         nj = self.nj
         X = [motion_X(*self.liMi(q, i)) for i in range(nj)]
         vs, as_, fs = [None] * nj, [None] * nj, [None] * nj
-        a0 = np.concatenate([-self.gravity, np.zeros(3)]).astype(dt)
+        g = self.gravity if gravity is None else np.asarray(gravity, float)
+        a0 = np.concatenate([-g, np.zeros(3)]).astype(dt)
         for i in range(nj):
             lam = self.parent[i]
             S = self.S(i)
@@ -413,11 +414,12 @@ class Contact:
         self.Rf = d[1:10].reshape(3, 3).T  # frame placement in its joint
         self.pf = d[10:13]
         if self.type == CONTACT_3D:
-            self.pref = d[13:16]
+            self.pref = d[13:16]  # (empty for an impulse record)
             self.nc = 3
         elif self.type == CONTACT_6D:
-            self.Rri = d[13:22].reshape(3, 3).T  # Mref^-1
-            self.pri = d[22:25]
+            if d.size >= 25:
+                self.Rri = d[13:22].reshape(3, 3).T  # Mref^-1
+                self.pri = d[22:25]
             self.nc = 6
         else:
             raise ValueError(f"unknown contact type {self.type}")
@@ -537,6 +539,115 @@ class ContactFwdKnot(FreeFwdKnot):
 
     def accel(self, x, u):
         return self.accel_force(x, u)[0]
+
+
+class ImpulseFwdKnot(FreeFwdKnot):
+    """ActionModelImpulseFwdDynamics (multibody/actions/impulse-fwddyn.hxx:53-127)
+    with an ImpulseModelMultiple of ImpulseModel3D / 6D (impulses/impulse-{3d,6d}.hxx,
+    LOCAL frame), nu = 0:
+        [M  Jc^T ; Jc  -damping I] [v+ ; -Lambda] = [M v ; -r Jc v]
+    (pinocchio::impulseDynamics restated), xnext = (q, v+), cost = costs(x).
+    calcDiff restates the reference's formula (impulse-fwddyn.hxx:111-119):
+    Fx = [[I, 0], [-G dtau_dq - H dv0_dq, G M]] with G, H the KKT-inverse blocks,
+    dtau_dq = d/dq [RNEA(q, 0, v+ - v) - Jc^T Lambda] without gravity (fext fixed
+    in their frames) and dv0_dq = d/dq (Jc v+), each by complex step of that
+    sub-function. For r = 0 this is the exact derivative of calc (tested); for
+    r > 0 the reference drops the restitution terms, and so does this."""
+
+    def __init__(self, block, nx, nu):
+        p = np.asarray(block, float)
+        nj = int(p[1])
+        ncost = int(p[2])
+        body = p[HDR:]
+        o = 3 + nj + JOINT_REC * nj
+        for _ in range(ncost):
+            o += int(body[o + 3])
+        self.r_coeff = float(body[o])
+        self.damping = float(body[o + 1])
+        nimp = int(body[o + 2])
+        assert int(body[o + 3]) == 1, "impulse section flag"
+        o += 4
+        self.contacts = []
+        for _ in range(nimp):
+            rs = int(body[o + 3])
+            self.contacts.append(Contact(body[o:o + rs]))
+            o += rs
+        assert nu == 0, "impulse knots have no controls"
+        super().__init__(block, nx, nu, _contact=True)
+        self.kind = 6
+        self.nun = nj
+        self.nc = sum(c.nc for c in self.contacts)
+
+    def jac(self, q):
+        nj = self.nj
+        dt = np.result_type(q, float)
+        Js = []
+        for c in self.contacts:
+            Xf = motion_X(c.Rf, c.pf)
+            J = np.zeros((6, nj), dt)
+            for k in range(nj):
+                e = np.zeros(nj, dt)
+                e[k] = 1.0
+                J[:, k] = Xf @ local_motions(self.robot, q, e, np.zeros(nj, dt))[0][c.joint]
+            Js.append(J[:3] if c.type == CONTACT_3D else J)
+        return np.vstack(Js) if Js else np.zeros((0, nj), dt)
+
+    def kkt(self, q):
+        nj, nc = self.nj, self.nc
+        M = self.robot.crba(q) + np.diag(self.robot.armature)
+        J = self.jac(q)
+        K = np.zeros((nj + nc, nj + nc), dtype=np.result_type(M, J))
+        K[:nj, :nj] = M
+        K[:nj, nj:] = J.T
+        K[nj:, :nj] = J
+        K[nj:, nj:] = -self.damping * np.eye(nc)
+        return M, J, K
+
+    def impulse(self, x):
+        nj = self.nj
+        q, v = x[:nj], x[nj:]
+        M, J, K = self.kkt(q)
+        sol = np.linalg.solve(K, np.concatenate([M @ v, -self.r_coeff * (J @ v)]))
+        return sol[:nj], -sol[nj:]
+
+    def calc(self, x, u=None):
+        nj = self.nj
+        vp, _ = self.impulse(x)
+        xn = np.concatenate([x[:nj] + 0 * vp, vp])
+        return xn, self.cost_c(x, np.zeros(0))
+
+    def calc_diff(self, x, u=None):
+        n, nj = self.nx, self.nj
+        x = np.asarray(x, float)
+        q, v = x[:nj], x[nj:]
+        vp, lam = self.impulse(x)
+        M, J, _ = self.kkt(q)
+        Minv = np.linalg.inv(M)
+        Y = Minv @ J.T
+        S = J @ Y + self.damping * np.eye(self.nc)
+        H = Y @ np.linalg.inv(S)
+        G = Minv - H @ Y.T
+        dv = vp - v
+
+        def tau(qq):  # RNEA(q, 0, dv) - Jc^T lambda, no gravity, lambda fixed in the frames
+            return self.robot.rnea(qq, np.zeros(nj), dv, gravity=np.zeros(3)) - self.jac(qq).T @ lam
+
+        dtau = self._cs_jac(tau, q, nj)
+        dv0 = self._cs_jac(lambda qq: self.jac(qq) @ vp, q, self.nc)
+        Fx = np.zeros((n, n))
+        Fx[:nj, :nj] = np.eye(nj)
+        Fx[nj:, :nj] = -G @ dtau - H @ dv0
+        Fx[nj:, nj:] = G @ M
+        Lx = np.zeros(n)
+        Lxx = np.zeros((n, n))
+        u0 = np.zeros(0)
+        for k in self.costs:
+            r = k.residual(self.robot, x, u0)
+            Rx = self._cs_jac(lambda xx: k.residual(self.robot, xx, u0), x, r.size)
+            Lx += k.weight * Rx.T @ (k.w * r)
+            Lxx += k.weight * Rx.T @ (k.w[:, None] * Rx)
+        return dict(Fx=Fx, Fu=np.zeros((n, 0)), Lx=Lx, Lu=np.zeros(0), Lxx=Lxx, Lxu=np.zeros((n, 0)),
+                    Luu=np.zeros((0, 0)))
 
 
 def block_size(block):

@@ -121,3 +121,47 @@ def test_contact_device_code_vs_oracle(lib, case, terminal):
             scale = max(1.0, float(np.max(np.abs(ref[q]))))
             assert float(np.max(np.abs(got - ref[q]))) / scale < 1e-9, (q, case, terminal,
                                                                         float(np.max(np.abs(got - ref[q]))))
+
+
+IMPULSE_CASES = [dict(kind="6d"), dict(kind="3d", weighted=True), dict(kind="6d+3d", damping=1e-3, inactive=True),
+                 dict(kind="6d", r_coeff=0.5, armature=np.full(7, 0.02)),
+                 dict(kind="6d+3d", robot=mb.sample_tree(10, seed=5), damping=1e-2, weighted=True, r_coeff=0.2)]
+
+
+@pytest.mark.parametrize("case", range(len(IMPULSE_CASES)))
+def test_impulse_device_code_vs_oracle(lib, case):
+    """ActionModelImpulseFwdDynamics: device impulse solve + the reference's
+    derivative formula vs the oracle's KKT solve + complex-step pieces."""
+    am = synthetic.impulse_model(**IMPULSE_CASES[case])
+    kind, nu, blk = am.pack()
+    assert kind == 6 and nu == 0
+    blk = np.ascontiguousarray(blk[0])
+    nx = am.state.nx
+    k = onp.ImpulseFwdKnot(blk, nx, 0)
+    rng = np.random.default_rng(200 + case)
+    u = np.zeros(1)
+    for _ in range(3):
+        x = rng.uniform(-1.5, 1.5, nx)
+        xn = np.zeros(nx)
+        c = lib.mb_host_calc(_p(blk), nx, _p(x), _p(u), 0, _p(xn))
+        xo, co = k.calc(x)
+        np.testing.assert_allclose(xn, xo, rtol=1e-10, atol=1e-10)
+        assert c == pytest.approx(co, rel=1e-12, abs=1e-14)
+        n, m = nx, 1  # one padded control column (nu_max of a mixed horizon)
+        out = {q: np.zeros(s) for q, s in [("Fx", n * n), ("Fu", n * m), ("Lxx", n * n), ("Lxu", n * m),
+                                           ("Luu", m * m), ("Lx", n), ("Lu", m)]}
+        xn2, c2 = np.zeros(nx), np.zeros(1)
+        lib.mb_host_calc_diff(_p(blk), nx, m, _p(x), _p(u), 0,
+                              *[_p(out[q]) for q in ["Fx", "Fu", "Lxx", "Lxu", "Luu", "Lx", "Lu"]], _p(xn2), _p(c2))
+        np.testing.assert_allclose(xn2, xo, rtol=1e-10, atol=1e-10)
+        assert c2[0] == pytest.approx(co, rel=1e-12, abs=1e-14)
+        ref = k.calc_diff(x)
+        Fx = out["Fx"].reshape(n, n).T
+        scale = max(1.0, float(np.max(np.abs(ref["Fx"]))))
+        # 1e-8: G and H come from S = Jc M^-1 Jc^T, whose condition number reaches
+        # 2e7 on these random states (Gauss-Jordan here, LAPACK inverses there)
+        assert float(np.max(np.abs(Fx - ref["Fx"]))) / scale < 1e-8, (case, float(np.max(np.abs(Fx - ref["Fx"]))))
+        for q in ("Lxx", "Lx"):
+            got = out[q].reshape(n, n).T if q == "Lxx" else out[q]
+            assert float(np.max(np.abs(got - ref[q]))) / max(1.0, float(np.max(np.abs(ref[q])))) < 1e-10, q
+        assert not out["Fu"].any() and not out["Lxu"].any() and not out["Luu"].any() and not out["Lu"].any()

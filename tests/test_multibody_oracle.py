@@ -347,3 +347,51 @@ def test_contact_api_validation_and_order():
     contacts.changeContactStatus("m", True)
     kind2, _, blk2 = croc.IntegratedActionModelEuler(dam, 1e-2).pack()
     assert onp.ContactFwdKnot(blk2[0], 14, 6).nc == 12
+
+
+# ---- impulse dynamics (ImpulseFwdKnot) -------------------------------------
+@pytest.mark.parametrize("kw", [dict(kind="6d"), dict(kind="3d"), dict(kind="6d+3d", damping=1e-3),
+                                dict(kind="6d", r_coeff=0.5)])
+def test_impulse_identities_and_derivatives(kw):
+    """pinocchio::impulseDynamics' equations: M (v+ - v) = Jc^T Lambda and
+    Jc v+ = -r Jc v - damping Lambda; the reference's derivative formula equals the
+    exact derivative of calc when r = 0 (impulse-fwddyn.hxx:111-115)."""
+    from crocoddyl_amd import synthetic
+    am = synthetic.impulse_model(**kw)
+    kind, nu, blk = am.pack()
+    assert kind == 6 and nu == 0
+    k = onp.ImpulseFwdKnot(blk[0], 14, 0)
+    rng = np.random.default_rng(3)
+    for _ in range(3):
+        x = rng.uniform(-1, 1, 14)
+        vp, lam = k.impulse(x)
+        M, J, _ = k.kkt(x[:7])
+        sc = 1e-12 * max(1.0, np.abs(lam).max()) * np.linalg.cond(J @ J.T)
+        np.testing.assert_allclose(M @ (vp - x[7:]), J.T @ lam, atol=sc)
+        np.testing.assert_allclose(J @ vp, -k.r_coeff * (J @ x[7:]) - k.damping * lam, atol=sc)
+        xn, c = k.calc(x)
+        np.testing.assert_array_equal(xn[:7], x[:7])
+        if k.r_coeff == 0.0:
+            d = k.calc_diff(x)
+            F = k._cs_jac(lambda xx: k.calc(xx)[0], x, 14)
+            np.testing.assert_allclose(d["Fx"], F, atol=1e-8 * max(1.0, np.abs(F).max()))
+
+
+def test_impulse_api_validation():
+    model = mb.sample_talos_arm()
+    state = mb.StateMultibody(model)
+    fid = model.getFrameId("gripper_left_joint")
+    imps = mb.ImpulseModelMultiple(state)
+    imps.addImpulse("b", mb.ImpulseModel3D(state, fid))
+    imps.addImpulse("a", mb.ImpulseModel6D(state, fid))
+    imps.addImpulse("c", mb.ImpulseModel3D(state, fid), False)
+    assert imps.ni == 9 and imps.ni_total == 12 and imps.active == ["a", "b"]
+    costs = mb.CostModelSum(state, 0)
+    costs.addCost("x", mb.CostModelState(state, 0), 1.0)
+    with pytest.raises(ValueError):
+        mb.ActionModelImpulseFwdDynamics(state, imps, costs, -0.1)
+    with pytest.raises(ValueError):
+        mb.ActionModelImpulseFwdDynamics(state, imps, mb.CostModelSum(state), 0.0)  # nu must be 0
+    am = mb.ActionModelImpulseFwdDynamics(state, imps, costs, 0.3, 1e-4)
+    k = onp.ImpulseFwdKnot(am.pack()[2][0], 14, 0)
+    assert [c.type for c in k.contacts] == [onp.CONTACT_6D, onp.CONTACT_3D] and k.r_coeff == 0.3 and k.nc == 9
