@@ -87,7 +87,7 @@ def _cpu_baseline_child(cfg, T, seed, target_s, box, arch):
         cores = os.cpu_count() or 1
     threads = max(1, min(16, cores))
 
-    from crocoddyl_amd import _abi
+    from crocoddyl_amd import _abi, synthetic
 
     def run(Bs, steps):
         S = helpers.setup(cfg, T=T, B=Bs, seed=seed)
@@ -99,7 +99,10 @@ def _cpu_baseline_child(cfg, T, seed, target_s, box, arch):
             p = oracle_lib.default_params()
             p.th_stop = 5e-5
             o.set_params(p)
-        o.set_candidate(None, None, False)
+        if synthetic.CONFIGS[cfg][0] == "multibody_contact":  # as the GPU run: warm start at x0
+            o.set_candidate(np.repeat(S["x0s"][:, None, :], T + 1, axis=1), None, False)
+        else:
+            o.set_candidate(None, None, False)
         o.solve(maxiter=2)
         t0 = time.perf_counter()
         it = 0

@@ -259,7 +259,8 @@ static void calc(const Model& m, Data& d, const double* x, const double* u_in) {
       }
       break;
     }
-    case FDDP_KNOT_EULER_FREEFWD: {  // euler.hxx:41-80 around free-fwddyn.hxx:44-79 (multibody_oracle.hpp)
+    case FDDP_KNOT_EULER_FREEFWD:     // euler.hxx:41-80 around free-fwddyn.hxx:44-79 (multibody_oracle.hpp)
+    case FDDP_KNOT_EULER_CONTACTFWD: {  // ... or contact-fwddyn.hxx:59-104
       mbo::Knot k;
       k.parse(m.p);
       k.calc(x, u, d.xnext.data(), &d.cost);
@@ -342,7 +343,8 @@ static void calcDiff(const Model& m, Data& d, const double* x, const double* u_i
       }
       break;
     }
-    case FDDP_KNOT_EULER_FREEFWD: {  // euler.hxx:83-131 around free-fwddyn.hxx:82-118 (multibody_oracle.hpp)
+    case FDDP_KNOT_EULER_FREEFWD:     // euler.hxx:83-131 around free-fwddyn.hxx:82-118 (multibody_oracle.hpp)
+    case FDDP_KNOT_EULER_CONTACTFWD: {  // ... or contact-fwddyn.hxx:107-160
       mbo::Knot k;
       k.parse(m.p);
       k.calc_diff(x, u, m.nu, d.Fx.a.data(), d.Fu.a.data(), d.Lxx.a.data(), d.Lxu.a.data(), d.Luu.a.data(),

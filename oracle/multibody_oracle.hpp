@@ -223,7 +223,9 @@ inline void aba(const Robot& rb, const Kin& K, const double* qd, const double* t
 struct Rnea {
   double v[kMaxJ][6], a[kMaxJ][6], F[kMaxJ][6];
 };
-inline void rnea(const Robot& rb, const Kin& K, const double* qd, const double* qdd, Rnea& Rv, double* tau) {
+// fext (may be null): external forces in the joint frames (pinocchio's fext)
+inline void rnea(const Robot& rb, const Kin& K, const double* qd, const double* qdd, Rnea& Rv, double* tau,
+                 const double* fext = nullptr) {
   const int nj = rb.nj;
   const double a0[6] = {-rb.g[0], -rb.g[1], -rb.g[2], 0., 0., 0.}, z6[6] = {0., 0., 0., 0., 0., 0.};
   for (int i = 0; i < nj; ++i) {
@@ -241,7 +243,7 @@ inline void rnea(const Robot& rb, const Kin& K, const double* qd, const double* 
     m6v(rb.I6[i], Rv.a[i], Ia);
     m6v(rb.I6[i], Rv.v[i], Iv);
     crf(Rv.v[i], Iv, t6);
-    for (int e = 0; e < 6; ++e) Rv.F[i][e] = Ia[e] + t6[e];
+    for (int e = 0; e < 6; ++e) Rv.F[i][e] = Ia[e] + t6[e] - (fext ? fext[6 * i + e] : 0.);
   }
   for (int i = nj - 1; i >= 0; --i) {
     const double* ax = rb.axis(i);
@@ -255,7 +257,9 @@ inline void rnea(const Robot& rb, const Kin& K, const double* qd, const double* 
 }
 
 // dRNEA/dq_j (dir 0) or dRNEA/dqd_j (dir 1) at the values in Rv -> dtau
-inline void rnea_dir(const Robot& rb, const Kin& K, const Rnea& Rv, const double* qd, int dir, int j, double* dtau) {
+// (tv / ta, may be null: the joint velocity / acceleration tangents, 6 per joint)
+inline void rnea_dir(const Robot& rb, const Kin& K, const Rnea& Rv, const double* qd, int dir, int j, double* dtau,
+                     double* tv = nullptr, double* ta = nullptr) {
   const int nj = rb.nj;
   const double a0[6] = {-rb.g[0], -rb.g[1], -rb.g[2], 0., 0., 0.}, z6[6] = {0., 0., 0., 0., 0., 0.};
   double dv[kMaxJ][6], da[kMaxJ][6], dF[kMaxJ][6];
@@ -290,6 +294,8 @@ inline void rnea_dir(const Robot& rb, const Kin& K, const Rnea& Rv, const double
     crf(dv[i], Iv, t6);
     crf(Rv.v[i], Idv, u6);
     for (int e = 0; e < 6; ++e) dF[i][e] = Ida[e] + t6[e] + u6[e];
+    if (tv)
+      for (int e = 0; e < 6; ++e) tv[6 * i + e] = dv[i][e], ta[6 * i + e] = da[i][e];
   }
   for (int i = nj - 1; i >= 0; --i) {
     const double* ax = rb.axis(i);
@@ -513,6 +519,11 @@ struct Knot {
   double dt = 0.;
   Robot rb;
   Costs cs;
+  // contact section (Euler ∘ ContactFwdDynamics; contact-fwddyn.hxx:59-160)
+  int nun = 0, ncon = 0, nc = 0;
+  bool contact = false;
+  double damping = 0.;
+  const double* crec[kMaxJ];
   void parse(const double* P) {
     dt = P[0];
     const int nj = (int)P[1];
@@ -523,20 +534,174 @@ struct Knot {
       cs.rec[k] = c;
       c += (int)c[3];
     }
+    if (c - P < (long)P[3]) {  // [nun, damping, ncontact, 0] + records
+      contact = true;
+      nun = (int)c[0];
+      damping = c[1];
+      ncon = (int)c[2];
+      c += 4;
+      for (int k = 0; k < ncon; ++k) {
+        crec[k] = c;
+        nc += (int)c[0] == 5 ? 3 : 6;
+        c += (int)c[3];
+      }
+    }
+  }
+  int nu() const { return rb.nj - nun; }
+  // LOCAL frame Jacobians stacked (nc x nj, row-major) and a0 at the drift
+  // (Rv from RNEA(q, v, 0): joint-frame v, gravity-including a)
+  void contact_terms(const Kin& K, const Rnea& Rv, double* Jc, double* a0) const {
+    const int nj = rb.nj;
+    int row = 0;
+    for (int k = 0; k < ncon; ++k) {
+      const double* rc = crec[k];
+      const double* d = rc + 4;
+      const int j = (int)d[0], n = (int)rc[0] == 5 ? 3 : 6;
+      for (int c = 0; c < nj; ++c) {  // S_c moved from joint c to the frame
+        bool sup = false;
+        for (int i = j; i >= 0; i = rb.parent[i]) sup |= i == c;
+        double o[6] = {0., 0., 0., 0., 0., 0.};
+        if (sup) {  // X_{f <- c} S_c = actInv(oMf) oMc S_c
+          double w[3], ow[3], Rf[9], pf[3], t[3], Sw[6];
+          mv(K.oR[c], rb.axis(c), w);
+          cr(K.op[c], w, ow);  // world motion at the origin: (op x w, w)
+          mm(K.oR[j], d + 1, Rf);
+          mv(K.oR[j], d + 10, t);
+          for (int e = 0; e < 3; ++e) pf[e] = K.op[j][e] + t[e], Sw[e] = ow[e], Sw[3 + e] = w[e];
+          act_inv(Rf, pf, Sw, o);
+        }
+        for (int e = 0; e < n; ++e) Jc[(row + e) * nj + c] = o[e];
+      }
+      double vf[6], af[6], ag[6], gl[3];
+      act_inv(d + 1, d + 10, Rv.v[j], vf);
+      mtv(K.oR[j], rb.g, gl);  // remove the gravity RNEA carries: a + (R^T g, 0)
+      for (int e = 0; e < 6; ++e) ag[e] = Rv.a[j][e] + (e < 3 ? gl[e] : 0.);
+      act_inv(d + 1, d + 10, ag, af);
+      const double kp = rc[1], kd = rc[2];
+      double r[6] = {0., 0., 0., 0., 0., 0.};
+      if (kp != 0.) frame_residual(rb, K, d, n == 3 ? C_FRAME_TRANSLATION : C_FRAME_PLACEMENT, -1, r, nullptr);
+      if (n == 3) {
+        double wxv[3];
+        cr(vf + 3, vf, wxv);
+        for (int e = 0; e < 3; ++e) a0[row + e] = af[e] + wxv[e] + kp * r[e] + kd * vf[e];
+      } else {
+        for (int e = 0; e < 6; ++e) a0[row + e] = af[e] + kp * r[e] + kd * vf[e];
+      }
+      row += n;
+    }
+  }
+  // forwardDynamics by the Schur complement: a, lambda; Y = Minv Jc^T (nj x nc),
+  // Sinv (nc x nc). false if M or S is not positive definite.
+  bool contact_solve(const Kin& K, const double* x, const double* u, double* a, double* lam, double* Jc, double* Mi,
+                     double* Y, double* Si, Rnea& Rv) const {
+    const int nj = rb.nj;
+    double M[kMaxJ * kMaxJ], nle[kMaxJ], a0[kMaxJ], z6[kMaxJ] = {0.};
+    crba(rb, K, M);
+    bool ok = spd_inverse(M, nj, Mi);
+    rnea(rb, K, x + nj, z6, Rv, nle);
+    contact_terms(K, Rv, Jc, a0);
+    double z[kMaxJ];
+    for (int i = 0; i < nj; ++i) {
+      double s = 0.;
+      for (int k = 0; k < nj; ++k) s += Mi[k * nj + i] * ((k < nun ? 0. : u[k - nun]) - nle[k]);
+      z[i] = s;
+    }
+    for (int c = 0; c < nc; ++c)
+      for (int i = 0; i < nj; ++i) {
+        double s = 0.;
+        for (int k = 0; k < nj; ++k) s += Mi[k * nj + i] * Jc[c * nj + k];
+        Y[c * nj + i] = s;
+      }
+    double S[kMaxJ * kMaxJ], r[kMaxJ];
+    for (int c = 0; c < nc; ++c) {
+      for (int rr = 0; rr < nc; ++rr) {
+        double s = 0.;
+        for (int i = 0; i < nj; ++i) s += Jc[rr * nj + i] * Y[c * nj + i];
+        S[c * nc + rr] = s + (rr == c ? damping : 0.);
+      }
+      double s = 0.;
+      for (int i = 0; i < nj; ++i) s += Jc[c * nj + i] * z[i];
+      r[c] = s + a0[c];
+    }
+    if (nc > 0) ok = spd_inverse(S, nc, Si) && ok;
+    for (int c = 0; c < nc; ++c) {
+      double s = 0.;
+      for (int k = 0; k < nc; ++k) s += Si[k * nc + c] * r[k];
+      lam[c] = -s;
+    }
+    for (int i = 0; i < nj; ++i) {
+      double s = z[i];
+      for (int c = 0; c < nc; ++c) s += Y[c * nj + i] * lam[c];
+      a[i] = s;
+    }
+    return ok;
+  }
+  // da0/dx along q_c (dir 0) / v_c (dir 1) from the joint tangents tv / ta
+  // (contact-3d.hxx:46-71, contact-6d.hxx:48-66)
+  void contact_dir(const Kin& K, const Rnea& Rv, int dir, int c, const double* tv, const double* ta,
+                   double* da0) const {
+    int row = 0;
+    for (int k = 0; k < ncon; ++k) {
+      const double* rc = crec[k];
+      const double* d = rc + 4;
+      const int j = (int)d[0], n = (int)rc[0] == 5 ? 3 : 6;
+      double dv[6], da[6];
+      for (int e = 0; e < 6; ++e) dv[e] = tv[6 * j + e], da[e] = ta[6 * j + e];
+      bool sup = false;
+      for (int i = j; i >= 0; i = rb.parent[i]) sup |= i == c;
+      if (dir == 0 && sup) {  // gravity tangent: d(-R_j^T g)/dq_c = R_j^T (w_c x g)
+        double wc[3], wg[3], t[3];
+        mv(K.oR[c], rb.axis(c), wc);
+        cr(wc, rb.g, wg);
+        mtv(K.oR[j], wg, t);
+        for (int e = 0; e < 3; ++e) da[e] -= t[e];
+      }
+      double dvf[6], daf[6], vf[6];
+      act_inv(d + 1, d + 10, dv, dvf);
+      act_inv(d + 1, d + 10, da, daf);
+      act_inv(d + 1, d + 10, Rv.v[j], vf);
+      const double kp = rc[1], kd = rc[2];
+      double rr[6], Jk[6] = {0., 0., 0., 0., 0., 0.};
+      if (kp != 0. && dir == 0 && sup)
+        frame_residual(rb, K, d, n == 3 ? C_FRAME_TRANSLATION : C_FRAME_PLACEMENT, c, rr, Jk);
+      if (n == 3) {
+        double t1[3], t2[3];
+        cr(dvf + 3, vf, t1);
+        cr(vf + 3, dvf, t2);
+        for (int e = 0; e < 3; ++e) da0[row + e] = daf[e] + t1[e] + t2[e] + kd * dvf[e] + kp * Jk[e];
+      } else {
+        for (int e = 0; e < 6; ++e) da0[row + e] = daf[e] + kd * dvf[e] + kp * Jk[e];
+      }
+      row += n;
+    }
+  }
+  // joint-frame external forces of the multipliers (updateForce: jMf.act(lambda))
+  void contact_fext(const double* lam, double* fext) const {
+    std::memset(fext, 0, sizeof(double) * 6 * rb.nj);
+    int row = 0;
+    for (int k = 0; k < ncon; ++k) {
+      const double* d = crec[k] + 4;
+      const int j = (int)d[0], n = (int)crec[k][0] == 5 ? 3 : 6;
+      double f[6] = {0., 0., 0., 0., 0., 0.}, o[6];
+      for (int e = 0; e < n; ++e) f[e] = lam[row + e];
+      act_force(d + 1, d + 10, f, o);
+      for (int e = 0; e < 6; ++e) fext[6 * j + e] += o[e];
+      row += n;
+    }
   }
   double cost_c(const Kin& K, const double* x, const double* u) const {
     const int nj = rb.nj, nx = 2 * nj;
     double total = 0.;
     for (int k = 0; k < cs.n; ++k) {
       const double* rc = cs.rec[k];
-      const int type = (int)rc[0], nr = cost_nr(rc, nx, nj);
+      const int type = (int)rc[0], nr = cost_nr(rc, nx, nu());
       const double* w = cost_w(rc, nr);
       const double* d = rc + 4;
       double r[6], a = 0.;
       if (type == C_STATE) {
         for (int i = 0; i < nx; ++i) a += w[i] * (x[i] - d[i]) * (x[i] - d[i]);
       } else if (type == C_CONTROL) {
-        for (int i = 0; i < nj; ++i) a += w[i] * (u[i] - d[i]) * (u[i] - d[i]);
+        for (int i = 0; i < nu(); ++i) a += w[i] * (u[i] - d[i]) * (u[i] - d[i]);
       } else {
         frame_residual(rb, K, d, type, -1, r, nullptr);
         for (int i = 0; i < nr; ++i) a += w[i] * r[i] * r[i];
@@ -551,7 +716,14 @@ struct Knot {
     Kin K;
     kinematics(rb, x, K);
     double qdd[kMaxJ];
-    aba(rb, K, x + nj, u, qdd);
+    if (contact) {
+      double lam[kMaxJ], Jc[kMaxJ * kMaxJ], Mi[kMaxJ * kMaxJ], Y[kMaxJ * kMaxJ], Si[kMaxJ * kMaxJ];
+      Rnea Rv;
+      if (!contact_solve(K, x, u, qdd, lam, Jc, Mi, Y, Si, Rv))
+        for (int i = 0; i < nj; ++i) qdd[i] = NAN;
+    } else {
+      aba(rb, K, x + nj, u, qdd);
+    }
     const double cc = cost_c(K, x, u);
     if (dt != 0.) {
       for (int i = 0; i < nj; ++i) {
@@ -571,20 +743,43 @@ struct Knot {
     Kin K;
     kinematics(rb, x, K);
     double qdd[kMaxJ], M[kMaxJ * kMaxJ], Mi[kMaxJ * kMaxJ], tau[kMaxJ];
-    aba(rb, K, x + nj, u, qdd);  // computeABADerivatives evaluates ABA first
-    crba(rb, K, M);
-    const bool ok = spd_inverse(M, nj, Mi);
+    double Jc[kMaxJ * kMaxJ], Y[kMaxJ * kMaxJ], Si[kMaxJ * kMaxJ], H[kMaxJ * kMaxJ], lam[kMaxJ], fext[6 * kMaxJ];
+    bool ok;
+    if (contact) {  // contact-fwddyn.hxx:107-140: Kinv blocks G = Minv - H Y^T, H = Y S^-1
+      Rnea R0;
+      ok = contact_solve(K, x, u, qdd, lam, Jc, Mi, Y, Si, R0);
+      contact_fext(lam, fext);
+      for (int c = 0; c < nc; ++c)
+        for (int i = 0; i < nj; ++i) {
+          double s = 0.;
+          for (int k = 0; k < nc; ++k) s += Y[k * nj + i] * Si[c * nc + k];
+          H[c * nj + i] = s;
+        }
+      for (int c = 0; c < nj; ++c)
+        for (int i = 0; i < nj; ++i) {
+          double s = 0.;
+          for (int k = 0; k < nc; ++k) s += H[k * nj + i] * Y[k * nj + c];
+          Mi[c * nj + i] -= s;
+        }
+    } else {
+      aba(rb, K, x + nj, u, qdd);  // computeABADerivatives evaluates ABA first
+      crba(rb, K, M);
+      ok = spd_inverse(M, nj, Mi);
+    }
     Rnea Rv;
-    rnea(rb, K, x + nj, qdd, Rv, tau);
+    rnea(rb, K, x + nj, qdd, Rv, tau, contact ? fext : nullptr);
     std::memset(Fx, 0, sizeof(double) * n * n);
     std::memset(Fu, 0, sizeof(double) * n * m);
     const double dt2 = dt * dt;
     for (int c = 0; c < n; ++c) {  // da/dx column c
-      double dt_[kMaxJ], da[kMaxJ];
-      rnea_dir(rb, K, Rv, x + nj, c < nj ? 0 : 1, c % nj, dt_);
+      double dt_[kMaxJ], da[kMaxJ], tv[6 * kMaxJ], ta[6 * kMaxJ], da0[kMaxJ];
+      rnea_dir(rb, K, Rv, x + nj, c < nj ? 0 : 1, c % nj, dt_, tv, ta);
+      if (contact) contact_dir(K, Rv, c < nj ? 0 : 1, c % nj, tv, ta, da0);
       for (int i = 0; i < nj; ++i) {
         double s = 0.;
         for (int k = 0; k < nj; ++k) s += Mi[k * nj + i] * dt_[k];
+        if (contact)
+          for (int k = 0; k < nc; ++k) s += H[k * nj + i] * da0[k];
         da[i] = ok ? -s : NAN;
       }
       for (int i = 0; i < nj; ++i) {
@@ -598,10 +793,10 @@ struct Knot {
       }
     }
     if (dt != 0.)
-      for (int c = 0; c < nj; ++c)
+      for (int c = 0; c < nu(); ++c)
         for (int i = 0; i < nj; ++i) {
-          Fu[c * n + i] = (ok ? Mi[c * nj + i] : NAN) * dt2;
-          Fu[c * n + nj + i] = (ok ? Mi[c * nj + i] : NAN) * dt;
+          Fu[c * n + i] = (ok ? Mi[(nun + c) * nj + i] : NAN) * dt2;
+          Fu[c * n + nj + i] = (ok ? Mi[(nun + c) * nj + i] : NAN) * dt;
         }
     // cost derivatives: Gauss-Newton, cost-sum.hxx:122-160
     std::memset(Lxx, 0, sizeof(double) * n * n);
@@ -611,7 +806,7 @@ struct Knot {
     std::memset(Lu, 0, sizeof(double) * m);
     for (int k = 0; k < cs.n; ++k) {
       const double* rc = cs.rec[k];
-      const int type = (int)rc[0], nr = cost_nr(rc, n, nj);
+      const int type = (int)rc[0], nr = cost_nr(rc, n, nu());
       const double* w = cost_w(rc, nr);
       const double* d = rc + 4;
       const double wt = rc[1];
@@ -621,7 +816,7 @@ struct Knot {
           Lxx[i * n + i] += wt * w[i];
         }
       } else if (type == C_CONTROL) {
-        for (int i = 0; i < nj; ++i) {
+        for (int i = 0; i < nu(); ++i) {
           Lu[i] += wt * w[i] * (u[i] - d[i]);
           Luu[i * m + i] += wt * w[i];
         }
