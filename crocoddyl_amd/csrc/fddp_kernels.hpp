@@ -696,7 +696,7 @@ __host__ __device__ inline int64_t fwd_lds_doubles(int64_t sX, int64_t sN, int64
 }
 
 template <int NT, bool FAST>
-__global__ __launch_bounds__(NT) void forward_kernel(Dev D, Prm prm, int mode, double alpha1, int* active_count,
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2))) void forward_kernel(Dev D, Prm prm, int mode, double alpha1, int* active_count,
                                                      int64_t pcap) {
   const int b = blockIdx.x;
   ElemState* st = D.st + b;

@@ -243,7 +243,10 @@ MB_HD inline void joint_rotation(const double* Rpl, const double* ax, double q, 
 // Phase executor: run(f) calls f(lane) for every thread of the workgroup and
 // then synchronises (device), or for lanes 0..nt-1 in order (host emulation,
 // tests/test_multibody_host.py). Within one phase no lane reads what another
-// lane writes, so both orders give the same result.
+// lane writes, so both orders give the same result. run_w0(f): a phase only
+// wave 0 works in, closed by a wave-level fence instead of a workgroup barrier
+// (the other waves skip ahead to the next sync()); sync(): the barrier that
+// hands wave-0 results back to the whole workgroup.
 struct DevExec {
   int nt;
   template <class F>
@@ -251,6 +254,16 @@ struct DevExec {
     f((int)threadIdx.x);
     __syncthreads();
   }
+  template <class F>
+  __device__ void run_w0(F f) const {
+    if (threadIdx.x < 64) {
+      f((int)threadIdx.x);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+  }
+  __device__ void sync() const { __syncthreads(); }
 };
 struct HostExec {
   int nt;
@@ -258,19 +271,27 @@ struct HostExec {
   void run(F f) const {
     for (int l = 0; l < nt; ++l) f(l);
   }
+  template <class F>
+  void run_w0(F f) const {
+    for (int l = 0; l < 64 && l < nt; ++l) f(l);
+  }
+  void sync() const {}
 };
 
 // Gauss-Jordan on the column-major nr x nc matrix A (ld nr) without pivoting
 // (the left nr x nr block is SPD): one column per lane (lane < nc), one pivot
 // per phase; the left block's pivot column is only read in its step. Returns
 // false if a pivot is not positive.
+// Runs on wave 0 (nc <= 64 columns) between wave-level fences; the caller's
+// preceding phase must have ended in a workgroup barrier.
 template <class X>
-MB_HD inline bool gauss_jordan(const X& ex, double* A, int nr, int nc, int* flag) {
-  ex.run([&](int lane) {
+MB_HD __attribute__((noinline)) bool gauss_jordan(const X& ex, double* A, int nr, int nc, int* flag) {
+  ex.run_w0([&](int lane) {
     if (lane == 0) *flag = 0;
   });
+#pragma unroll 1
   for (int k = 0; k < nr; ++k) {
-    ex.run([&](int lane) {
+    ex.run_w0([&](int lane) {
       const double piv = A[(int64_t)k * nr + k];
       if (!(piv > 0.)) {
         if (lane == 0) *flag = 1;
@@ -280,6 +301,7 @@ MB_HD inline bool gauss_jordan(const X& ex, double* A, int nr, int nc, int* flag
         double* col = A + (int64_t)lane * nr;
         const double* pc = A + (int64_t)k * nr;
         const double akc = col[k] / piv;
+#pragma unroll 1
         for (int r0 = 0; r0 < nr; r0 += 8) {
           double pv[8], cv[8];
 #pragma unroll
@@ -295,6 +317,7 @@ MB_HD inline bool gauss_jordan(const X& ex, double* A, int nr, int nc, int* flag
       }
     });
   }
+  ex.sync();
   return *flag == 0;
 }
 
@@ -833,9 +856,19 @@ MB_HD inline void contact_jac_col(const VT& V, const unsigned* anc_j, const doub
   motion_act_inv(Rf, pf, Sc, o);
 }
 
-// a0 of a contact (contact-3d.hxx:35-43, contact-6d.hxx:31-44) from the world
-// velocity / drift acceleration (gravity included, as RNEA) of its joint.
-MB_HD inline int contact_a0(const Blk& b, const WVals& W, const CRec& C, double* a0) {
+// a0 of a contact (contact-3d.hxx:35-43, contact-6d.hxx:31-44) in two parts,
+// so that neither holds log6 and the frame motions live at once: the
+// Baumgarte position term kp * (p - p_ref) | kp * log6(Mref^-1 oMf) (needs only
+// the placements), then the frame drift acceleration (classical for 3D, gravity
+// removed) + kd * v from the world velocity / acceleration of the joint.
+MB_HD __attribute__((noinline)) void contact_a0_position(const WVals& W, const CRec& C, double* a0) {
+  const double kp = C.r[1];
+  double r[6] = {0., 0., 0., 0., 0., 0.};
+  if (kp != 0.) frame_residual_value(W, C, r);
+  const int n = C.type() == C_CONTACT_3D ? 3 : 6;
+  for (int e = 0; e < n; ++e) a0[e] = kp * r[e];
+}
+MB_HD __attribute__((noinline)) void contact_a0_drift(const WVals& W, const CRec& C, double* a0) {
   const double* d = C.d();
   const int j = (int)d[0];
   double Rf[9], pf[3], m6[6], vf[6], af[6];
@@ -844,17 +877,14 @@ MB_HD inline int contact_a0(const Blk& b, const WVals& W, const CRec& C, double*
   motion_act_inv(Rf, pf, m6, vf);
   for (int e = 0; e < 6; ++e) m6[e] = W.a(j)[e] - W.root_a()[e];  // data.a has no gravity
   motion_act_inv(Rf, pf, m6, af);
-  const double kp = C.r[1], kd = C.r[2];
-  double r[6] = {0., 0., 0., 0., 0., 0.};
-  if (kp != 0.) frame_residual_value(W, C, r);
+  const double kd = C.r[2];
   if (C.type() == C_CONTACT_3D) {
     double wxv[3];
     cross3(vf + 3, vf, wxv);
-    for (int e = 0; e < 3; ++e) a0[e] = af[e] + wxv[e] + kp * r[e] + kd * vf[e];
-    return 3;
+    for (int e = 0; e < 3; ++e) a0[e] += af[e] + wxv[e] + kd * vf[e];
+  } else {
+    for (int e = 0; e < 6; ++e) a0[e] += af[e] + kd * vf[e];
   }
-  for (int e = 0; e < 6; ++e) a0[e] = af[e] + kp * r[e] + kd * vf[e];
-  return 6;
 }
 
 // World force (at the origin) of contact record C for the multipliers lam
@@ -887,7 +917,7 @@ MB_HD inline void contact_joint_forces(const Blk& b, const WVals& W, const doubl
 
 // lane c < nj: column c of the stacked contact Jacobian Jc (nc x nj,
 // Jc[row * nj + c]); with At != null also into the columns [nj + row] of A (ld nj).
-MB_HD inline void contact_jac_lane(const Blk& b, const WVals& W, int c, double* Jc, double* At) {
+MB_HD __attribute__((noinline)) void contact_jac_lane(const Blk& b, const WVals& W, int c, double* Jc, double* At) {
   double Sc[6];
   for (int e = 0; e < 6; ++e) Sc[e] = W.S(c)[e];
   const double* r = b.K;
@@ -1000,6 +1030,12 @@ MB_HD inline double knot_calc_x(const X& ex, const double* P, int nx, const doub
       if (wave == 2 + (k & 1) && l == (k >> 1)) cv[k] = C.weight() * cost_activation(W, C, x, ub, nx, nu);
       cr += C.size();
     }
+    const int kc = l - 32;  // contact position terms on the upper half of wave 2
+    if (!imp && wave == 2 && kc >= 0 && kc < b.ncon) {
+      int row0;
+      const CRec C{contact_rec(b, kc, &row0)};
+      contact_a0_position(W, C, a0 + row0);
+    }
   });
   if (!imp) world_rnea(ex, b, W, x + nj, nullptr, tau);
   ex.run([&](int lane) {
@@ -1011,7 +1047,7 @@ MB_HD inline double knot_calc_x(const X& ex, const double* P, int nx, const doub
     if (!imp && lane >= 64 && lane < 64 + b.ncon) {
       int row0;
       const CRec C{contact_rec(b, lane - 64, &row0)};
-      contact_a0(b, W, C, a0 + row0);
+      contact_a0_drift(W, C, a0 + row0);
     }
     if (lane == 128) {
       double total = 0.;
@@ -1333,7 +1369,8 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
       for (int k = lane; k < (imp ? 0 : b.ncon); k += ex.nt) {
         int row0;
         const CRec C{contact_rec(b, k, &row0)};
-        contact_a0(b, W, C, a0 + row0);
+        contact_a0_position(W, C, a0 + row0);
+        contact_a0_drift(W, C, a0 + row0);
       }
     });
   bool ok = gauss_jordan(ex, A, nj, 2 * nj, flag);
