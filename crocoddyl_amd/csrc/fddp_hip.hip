@@ -90,6 +90,7 @@ int64_t mb_block_check(const double* P, int64_t avail, int kind, int nx, int nu,
   if ((double)ncost != P[2] || ncost < 0 || ncost > kMaxCosts) return why = "number of costs out of [0, 64]", -1;
   if (size > avail || (double)size != P[3]) return why = "block out of range", -1;
   int64_t o = FDDP_PARAM_HEADER + 3 + nj;
+  int force_rows = 0;  // rows the contact-force costs read
   if (o + (int64_t)kJRec * nj > size) return why = "block too small for its joints", -1;
   for (int i = 0; i < nj; ++i) {
     const double* J = P + o + (int64_t)kJRec * i;
@@ -111,6 +112,14 @@ int64_t mb_block_check(const double* P, int64_t avail, int kind, int nx, int nu,
     if (type == C_CONTROL) want = kCHdr + 2 * (int64_t)nu;
     if (type == C_FRAME_PLACEMENT) want = kCHdr + 31;
     if (type == C_FRAME_TRANSLATION) want = kCHdr + 19;
+    if (type == C_CONTACT_FORCE) {  // [row0, nr, fref(6)] + w(nr); rows checked against the contacts below
+      const int nrf = o + kCHdr + 1 < size ? (int)C[kCHdr + 1] : 0;
+      if (kind != FDDP_KNOT_EULER_CONTACTFWD || (nrf != 3 && nrf != 6))
+        return why = "contact-force costs need contact knots and a 3- or 6-row force", -1;
+      want = kCHdr + 8 + nrf;
+      force_rows = std::max(force_rows, (int)C[kCHdr] + nrf);
+      if ((int)C[kCHdr] < 0) return why = "contact-force cost row out of range", -1;
+    }
     if (want < 0) return why = "unknown cost type " + std::to_string(type), -1;
     if (rs != want || o + rs > size) return why = "cost record of the wrong size", -1;
     if (type == C_FRAME_PLACEMENT || type == C_FRAME_TRANSLATION) {
@@ -125,7 +134,8 @@ int64_t mb_block_check(const double* P, int64_t avail, int kind, int nx, int nu,
     if (o + 4 > size) return why = "contact section out of range", -1;
     const int nun = (int)P[o], ncon = (int)P[o + 2];
     const double damping = P[o + 1];
-    if (P[o + 3] != (impulse ? 1. : 0.)) return why = "contact / impulse section flag does not match the kind", -1;
+    if (impulse ? P[o + 3] != 1. : (P[o + 3] != 0. && P[o + 3] != 2.))
+      return why = "contact / impulse section flag does not match the kind", -1;
     if (impulse) {
       if (!(P[o] >= 0.) || !std::isfinite(P[o])) return why = "The restitution coefficient has to be positive", -1;
     } else {
@@ -153,6 +163,7 @@ int64_t mb_block_check(const double* P, int64_t avail, int kind, int nx, int nu,
     }
     if (nc > kMaxNc) return why = "more than 24 contact rows in one knot", -1;
   }
+  if (force_rows > nc) return why = "contact-force cost reads rows beyond the contacts", -1;
   if (o != size) return why = "block size does not match its records", -1;
   if (nframe > kMaxFrameCosts) return why = "more than 8 frame costs in one knot", -1;
   if ((pad2(diff_layout(nj, nframe, nc).total) + pad2(size)) * 8 > 160 * 1024)

@@ -39,7 +39,15 @@ constexpr int kValsPerJoint = 52;  // R 9, p 3, oR 9, op 3, v 6, a 6, F 6, compo
 constexpr int kMaxNc = 24;         // stacked contact rows (FDDP_KNOT_EULER_CONTACTFWD)
 // Cost record types; contact records (after the costs) use 5 / 6 and the same
 // frame payload as the frame costs, so frame_residual serves both.
-enum { C_STATE = 1, C_CONTROL = 2, C_FRAME_PLACEMENT = 3, C_FRAME_TRANSLATION = 4, C_CONTACT_3D = 5, C_CONTACT_6D = 6 };
+enum {
+  C_STATE = 1,
+  C_CONTROL = 2,
+  C_FRAME_PLACEMENT = 3,
+  C_FRAME_TRANSLATION = 4,
+  C_CONTACT_3D = 5,
+  C_CONTACT_6D = 6,
+  C_CONTACT_FORCE = 7  // cost on a contact's force: payload [row0, nr, fref(6)] (contact-force.hxx)
+};
 
 struct Blk {
   double dt;
@@ -56,6 +64,7 @@ struct Blk {
   // impulse section instead (ActionModelImpulseFwdDynamics, nu = 0)
   bool impulse;
   double r_coeff;     // restitution coefficient
+  bool enable_force;  // contact section flag 2: force Jacobians for CostModelContactForce
 };
 
 MB_HD inline Blk parse(const double* P) {
@@ -74,9 +83,11 @@ MB_HD inline Blk parse(const double* P) {
   b.damping = 0.;
   b.K = e;
   b.impulse = false;
+  b.enable_force = false;
   b.r_coeff = 0.;
   if (e - P < (int64_t)P[3]) {  // [nun | r_coeff, damping, ncontact, 0 | 1] + records
     b.impulse = (int)e[3] == 1;
+    b.enable_force = (int)e[3] == 2;
     b.nun = b.impulse ? b.nj : (int)e[0];
     b.r_coeff = b.impulse ? e[0] : 0.;
     b.damping = e[1];
@@ -514,9 +525,23 @@ MB_HD inline int frame_residual(const Blk& b, const Vals& V, const CRec& C, int 
 // doubles of the record).
 MB_HD inline int cost_nr(const CRec& C, int nx, int nu) {
   const int t = C.type();
+  if (t == C_CONTACT_FORCE) return (int)C.d()[1];
   return t == C_STATE ? nx : (t == C_CONTROL ? nu : (t == C_FRAME_PLACEMENT ? 6 : 3));
 }
 MB_HD inline const double* cost_weights(const CRec& C, int nx, int nu) { return C.r + C.size() - cost_nr(C, nx, nu); }
+// 0.5 r^T W r of a contact-force cost, r = lambda[row0 .. row0 + nr) - fref
+// (contact-force.hxx:33-50: jMf.actInv(f) is the multiplier itself).
+MB_HD inline double force_cost_activation(const CRec& C, const double* lam, int nx, int nu) {
+  const double* d = C.d();
+  const int row0 = (int)d[0], nr = (int)d[1];
+  const double* w = cost_weights(C, nx, nu);
+  double a = 0.;
+  for (int e = 0; e < nr; ++e) {
+    const double r = lam[row0 + e] - d[2 + e];
+    a += w[e] * r * r;
+  }
+  return 0.5 * a;
+}
 
 // Residual of a frame cost, value only (calc). Returns the residual size.
 template <class VT>
@@ -551,6 +576,8 @@ MB_HD __forceinline__ double cost_activation(const VT& V, const CRec& C, const d
       const double r = u[i] - C.d()[i];
       a += w[i] * r * r;
     }
+  } else if (C.type() == C_CONTACT_FORCE) {
+    return 0.;  // needs the multipliers: added after the contact solve
   } else {
     double r[6] = {0., 0., 0., 0., 0., 0.};
     const int nr = frame_residual_value(V, C, r);
@@ -1071,6 +1098,18 @@ MB_HD inline double knot_calc_x(const X& ex, const double* P, int nx, const doub
     });
     ok = gauss_jordan(ex, S, nc, nc + 1, flag) && ok;
     ex.run([&](int lane) {
+      if (lane == 64 && !imp) {  // contact-force costs (lambda = -S^-1 r, in S's last column, negated)
+        double lamv[kMaxNc];
+        for (int k = 0; k < nc; ++k) lamv[k] = -S[(int64_t)nc * nc + k];
+        double add = 0.;
+        const double* cr = b.C;
+        for (int k = 0; k < b.ncost; ++k) {
+          const CRec C{cr};
+          if (C.type() == C_CONTACT_FORCE) add += C.weight() * force_cost_activation(C, lamv, nx, nu);
+          cr += C.size();
+        }
+        red[0] += add;
+      }
       if (lane >= nj) return;
       double s = imp ? x[nj + lane] : a[lane];
       for (int k = 0; k < nc; ++k) s -= A[(int64_t)nj * (nj + k) + lane] * S[(int64_t)nc * nc + k];
@@ -1113,7 +1152,7 @@ struct DiffLayout {
   int64_t wv, vals, A, tang, dtau, J, xu, red, ct, total;
   // contact area (nc > 0): Jc nc x nj, a0 nc, lambda nc, Y = Minv Jc^T and
   // H = Y S^-1 (nj x nc each), [S | I | r] nc x (2nc + 1), da0/dx nc x L, fx 6 nj
-  int64_t Jc, a0, lam, Y, H, Sx, da0, fx, zv;
+  int64_t Jc, a0, lam, Y, H, Sx, da0, fx, zv, dfx, dfu;
 };
 __host__ __device__ inline DiffLayout diff_layout(int nj, int nframe, int nc = 0) {
   const int L = 2 * nj;
@@ -1136,7 +1175,9 @@ __host__ __device__ inline DiffLayout diff_layout(int nj, int nframe, int nc = 0
   l.da0 = l.Sx + (int64_t)nc * (2 * nc + 1);
   l.fx = l.da0 + (int64_t)nc * L;
   l.zv = l.fx + 6 * nj;  // impulse: v+ - v
-  l.total = nc > 0 ? l.zv + nj : l.ct;
+  l.dfx = l.zv + nj;     // d lambda / dx (nc x L), d lambda / du (nc x nj): CostModelContactForce
+  l.dfu = l.dfx + (int64_t)nc * L;
+  l.total = nc > 0 ? l.dfu + (int64_t)nc * nj : l.ct;
   return l;
 }
 
@@ -1508,7 +1549,13 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
         }
       }
       if (cost_out && !Fx && lane == 0) {  // calc only (with derivatives: from the residuals below)
-        const double cc = cost_value(b, W, x, u, nx, nu);
+        double cc = cost_value(b, W, x, u, nx, nu);
+        const double* cr = b.C;
+        for (int k = 0; k < b.ncost; ++k) {
+          const CRec C{cr};
+          if (C.type() == C_CONTACT_FORCE && nc > 0) cc += C.weight() * force_cost_activation(C, lam, nx, nu);
+          cr += C.size();
+        }
         *cost_out = dt != 0. ? dt * cc : cc;
       }
     });
@@ -1551,6 +1598,26 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
       cr += C.size();
     }
   });
+  // d lambda / dx, d lambda / du for CostModelContactForce (contact-fwddyn.hxx:131-137, with
+  // enable_force): Kinv bottom-left = H^T, bottom-right = -S^-1; dtau/du = [0; I]
+  const bool fd = b.enable_force && nc > 0 && !imp;
+  double* dfx = w + l.dfx;
+  double* dfu = w + l.dfu;
+  if (fd)
+    ex.run([&](int lane) {
+      const double* Sinv = Sx + (int64_t)nc * nc;
+      for (int e = lane; e < nc * L; e += ex.nt) {
+        const int k = e / L, c = e % L;
+        double s = 0.;
+        for (int i = 0; i < nj; ++i) s += H[(int64_t)k * nj + i] * dtau[(int64_t)i * L + c];
+        for (int m2 = 0; m2 < nc; ++m2) s -= Sinv[(int64_t)m2 * nc + k] * da0[(int64_t)m2 * L + c];
+        dfx[e] = s;
+      }
+      for (int e = lane; e < nc * nj; e += ex.nt) {
+        const int k = e / nj, c = e % nj;
+        dfu[e] = c < nu ? -H[(int64_t)k * nj + b.nun + c] : 0.;
+      }
+    });
   const double dt = b.dt, dt2 = dt * dt;
   const bool integ = dt != 0.;
   const double sc = integ ? dt : 1.;
@@ -1594,7 +1661,23 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
         f = i < nj ? mi * dt2 : mi * dt;
       }
       Fu[e] = f;
-      Lxu[e] = 0.;
+      double lxu = 0.;  // only contact-force costs couple x and u
+      if (fd && c < nu) {
+        const double* cr = b.C;
+        for (int k = 0; k < b.ncost; ++k) {
+          const CRec C{cr};
+          if (C.type() == C_CONTACT_FORCE) {
+            const int row0 = (int)C.d()[0], nr = (int)C.d()[1];
+            const double* wv = cost_weights(C, nx, nu);
+            double s2 = 0.;
+            for (int r = 0; r < nr; ++r)
+              s2 += dfx[(int64_t)(row0 + r) * L + i] * wv[r] * dfu[(int64_t)(row0 + r) * nj + c];
+            lxu += C.weight() * s2;
+          }
+          cr += C.size();
+        }
+      }
+      Lxu[e] = sc * lxu;
     }
     // Lxx(i, j): Gauss-Newton, cost-sum.hxx:122-160
     for (int e = lane; e < n * n; e += ex.nt) {
@@ -1617,6 +1700,12 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
             l += wt * s2;
           }
           ++f;
+        } else if (C.type() == C_CONTACT_FORCE && fd) {
+          const int row0 = (int)C.d()[0], nr = (int)C.d()[1];
+          double s2 = 0.;
+          for (int r = 0; r < nr; ++r)
+            s2 += dfx[(int64_t)(row0 + r) * L + i] * wv[r] * dfx[(int64_t)(row0 + r) * L + j];
+          l += wt * s2;
         }
         cr += C.size();
       }
@@ -1626,11 +1715,19 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
     for (int e = lane; e < m * m; e += ex.nt) {
       const int j = e / m, i = e % m;
       double l = 0.;
-      if (i == j && j < nu) {
+      if (i < nu && j < nu) {
         const double* cr = b.C;
         for (int k = 0; k < b.ncost; ++k) {
           const CRec C{cr};
-          if (C.type() == C_CONTROL) l += C.weight() * cost_weights(C, nx, nu)[j];
+          if (C.type() == C_CONTROL && i == j) l += C.weight() * cost_weights(C, nx, nu)[j];
+          if (C.type() == C_CONTACT_FORCE && fd) {
+            const int row0 = (int)C.d()[0], nr = (int)C.d()[1];
+            const double* wv = cost_weights(C, nx, nu);
+            double s2 = 0.;
+            for (int r = 0; r < nr; ++r)
+              s2 += dfu[(int64_t)(row0 + r) * nj + i] * wv[r] * dfu[(int64_t)(row0 + r) * nj + j];
+            l += C.weight() * s2;
+          }
           cr += C.size();
         }
       }
@@ -1644,6 +1741,12 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
         for (int k = 0; k < b.ncost; ++k) {
           const CRec C{cr};
           if (C.type() == C_CONTROL) lu += C.weight() * cost_weights(C, nx, nu)[j] * (u[j] - C.d()[j]);
+          if (C.type() == C_CONTACT_FORCE && fd) {
+            const int row0 = (int)C.d()[0], nr = (int)C.d()[1];
+            const double* wv = cost_weights(C, nx, nu);
+            for (int r = 0; r < nr; ++r)
+              lu += C.weight() * dfu[(int64_t)(row0 + r) * nj + j] * wv[r] * (lam[row0 + r] - C.d()[2 + r]);
+          }
           cr += C.size();
         }
       }
@@ -1668,6 +1771,10 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
               for (int r = 0; r < nr; ++r) lx += wt * Jk[(int64_t)r * nj + j] * wv[r] * rf[6 * f + r];
             }
             ++f;
+          } else if (C.type() == C_CONTACT_FORCE && fd) {
+            const int row0 = (int)C.d()[0], nr = (int)C.d()[1];
+            for (int r = 0; r < nr; ++r)
+              lx += wt * dfx[(int64_t)(row0 + r) * L + j] * wv[r] * (lam[row0 + r] - C.d()[2 + r]);
           }
           cr += C.size();
         }
@@ -1687,6 +1794,8 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
           for (int i = 0; i < nx; ++i) a += wv[i] * (x[i] - C.d()[i]) * (x[i] - C.d()[i]);
         } else if (C.type() == C_CONTROL) {
           for (int i = 0; i < nu; ++i) a += wv[i] * (u[i] - C.d()[i]) * (u[i] - C.d()[i]);
+        } else if (C.type() == C_CONTACT_FORCE) {
+          if (nc > 0) a = 2. * force_cost_activation(C, lam, nx, nu);
         } else {
           const int nr = C.type() == C_FRAME_PLACEMENT ? 6 : 3;
           for (int i = 0; i < nr; ++i) a += wv[i] * rf[6 * f + i] * rf[6 * f + i];

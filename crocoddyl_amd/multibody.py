@@ -29,6 +29,7 @@ JOINT_REC = 26
 COST_HDR = 4
 COST_STATE, COST_CONTROL, COST_FRAME_PLACEMENT, COST_FRAME_TRANSLATION = 1, 2, 3, 4
 CONTACT_3D, CONTACT_6D = 5, 6
+COST_CONTACT_FORCE = 7
 MAX_CONTACT_ROWS = 24
 MAX_JOINTS = 32
 
@@ -413,6 +414,53 @@ class CostModelFrameTranslation(_Cost):
         return [frame, _rows(self.xref.translation, 3)]
 
 
+class FrameForce:
+    """FrameForce (multibody/frames.hpp): frame id and a spatial force (linear, angular)."""
+
+    def __init__(self, id, force):
+        self.id = int(id)
+        self.force = np.array(force, np.float64).reshape(6)
+
+
+class CostModelContactForce(_Cost):
+    """r = jMf.actInv(f) - fref = lambda_contact - fref (contact-force.hxx:33-74): the
+    force of the contact defined on frame fref.id (3 linear rows for a 3D contact, 6
+    for a 6D one). Its derivatives are the force Jacobians of the contact dynamics,
+    which the DAM computes only with enable_force=True (otherwise Rx = Ru = 0, as in
+    the reference)."""
+
+    type = COST_CONTACT_FORCE
+
+    def __init__(self, state, *args, **kw):
+        act = None
+        fref = None
+        ints = []
+        for a in args:
+            if isinstance(a, (ActivationModelQuad, ActivationModelWeightedQuad)):
+                act = a
+            elif isinstance(a, FrameForce):
+                fref = a
+            elif isinstance(a, (int, np.integer)) and not isinstance(a, bool):
+                ints.append(int(a))
+        act = kw.get("activation", act)
+        fref = kw.get("fref", fref)
+        if not isinstance(fref, FrameForce):
+            raise TypeError("CostModelContactForce needs a FrameForce reference")
+        if act is not None:  # (state, activation, fref[, nu])
+            nr, nu = act.nr, (ints[0] if ints else None)
+        else:  # (state, fref[, nc[, nu]])
+            nr = ints[0] if ints else 3
+            nu = ints[1] if len(ints) > 1 else None
+        nu = kw.get("nu", nu)
+        if nr not in (3, 6):
+            raise ValueError("Invalid argument: nr has to be 3 or 6 (the contact's force)")
+        super().__init__(state, act, nr, nu)
+        self.fref = fref
+
+    def _payload(self):  # the contact row offset is resolved by the DAM (pack_body)
+        return [np.concatenate([[-1.0, self.activation.nr], self.fref.force]).reshape(1, -1)]
+
+
 class CostItem:
     def __init__(self, name, cost, weight, active=True):
         self.name, self.cost, self.weight, self.active = name, cost, float(weight), bool(active)
@@ -688,8 +736,31 @@ class DifferentialActionModelContactFwdDynamics(DifferentialActionModelFreeFwdDy
         recs = self.contacts.pack()
         if self.contacts.nc > MAX_CONTACT_ROWS:
             raise ValueError(f"Invalid argument: the device path holds at most {MAX_CONTACT_ROWS} contact rows")
-        sec = np.concatenate([[self.actuation.nun, self.JMinvJt_damping, len(recs), 0.0]] + recs)
-        return _pack_mb(self.state, self._armature, self.costs, dt, sec)
+        sec = np.concatenate([[self.actuation.nun, self.JMinvJt_damping, len(recs), 2.0 if self.enable_force else 0.0]]
+                             + recs)
+        out = _pack_mb(self.state, self._armature, self.costs, dt, sec)
+        # contact-force costs: the row offset of the active contact on fref.id (contact-force.hxx createData)
+        rows, r0 = {}, 0
+        for n in self.contacts.active:
+            c = self.contacts.contacts[n].contact
+            rows[c._ref.id] = (r0, c.nc)
+            r0 += c.nc
+        o = _abi.PARAM_HEADER + 3 + self.state.nv + JOINT_REC * self.state.nv
+        for name in sorted(self.costs.costs):
+            it = self.costs.costs[name]
+            if not it.active:
+                continue
+            size = int(out[0, o + 3])
+            if it.cost.type == COST_CONTACT_FORCE:
+                fid = it.cost.fref.id
+                if fid not in rows:
+                    raise ValueError(f"Invalid argument: there is not contact defined for frame {fid}")
+                row0, nci = rows[fid]
+                if nci != it.cost.activation.nr:
+                    raise ValueError("Invalid argument: the contact-force cost and its contact differ in size")
+                out[:, o + COST_HDR] = row0
+            o += size
+        return out
 
 
 class _Impulse:

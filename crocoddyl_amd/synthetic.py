@@ -133,7 +133,8 @@ def build_hetero(name, T=None, B=None, seed=None, phase=10, impulse_every=7):
 
 
 def build_arm_contact(T=4, B=2, seed=0, robot=None, dt=1e-2, contact="6d", gains=(2.0, 1.5), damping=0.0,
-                      weighted=False, armature=None, inactive=False, q_nominal=None, spread=1.0):
+                      weighted=False, armature=None, inactive=False, q_nominal=None, spread=1.0, force_costs=False,
+                      enable_force=None):
     """Contact-dynamics knots on the arm: Euler(dt) ∘ DifferentialActionModelContactFwdDynamics
     (contact-fwddyn.hxx) with ActuationModelFloatingBase (first joint unactuated)
     and a ContactModelMultiple on the gripper frame ("6d": ContactModel6D, "3d":
@@ -143,7 +144,9 @@ def build_arm_contact(T=4, B=2, seed=0, robot=None, dt=1e-2, contact="6d", gains
     (ContactModelMultiple::changeContactStatus). The terminal model is the same
     DAM with dt = 0. x0_b ~ U[-1,1]^(2 nv) per element (off the contact
     manifold: the Baumgarte gains pull the frames back); with ``q_nominal``,
-    q0_b ~ q_nominal + U[-spread, spread]^nq and v0_b ~ U[-spread, spread]^nv."""
+    q0_b ~ q_nominal + U[-spread, spread]^nq and v0_b ~ U[-spread, spread]^nv.
+    ``force_costs`` adds a CostModelContactForce per contact (a weighted one on the
+    elbow); ``enable_force`` defaults to ``force_costs``."""
     from . import multibody as mb
     rng = np.random.default_rng(seed)
     model = mb.sample_talos_arm() if robot is None else robot
@@ -176,7 +179,15 @@ def build_arm_contact(T=4, B=2, seed=0, robot=None, dt=1e-2, contact="6d", gains
     else:
         costs.addCost("xReg", mb.CostModelState(state, nu), 1e-2)
     costs.addCost("uReg", mb.CostModelControl(state, nu), 1e-3)
-    dam = mb.DifferentialActionModelContactFwdDynamics(state, act, contacts, costs, damping)
+    if force_costs:
+        costs.addCost("gripperForce", mb.CostModelContactForce(
+            state, mb.FrameForce(fid, (1.0, 2.0, 3.0, 0.1, 0.2, 0.3)), 6 if kinds[0] == "6d" else 3, nu), 1e-3)
+        if len(kinds) > 1:
+            costs.addCost("elbowForce", mb.CostModelContactForce(
+                state, mb.ActivationModelWeightedQuad(np.array([1.0, 2.0, 3.0])), mb.FrameForce(eid, np.zeros(6)), nu),
+                1e-2)
+    dam = mb.DifferentialActionModelContactFwdDynamics(state, act, contacts, costs, damping,
+                                                       force_costs if enable_force is None else enable_force)
     if armature is not None:
         dam.armature = armature
     running = IntegratedActionModelEuler(dam, dt)

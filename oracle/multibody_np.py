@@ -42,6 +42,7 @@ JOINT_REC = 26
 COST_HDR = 4
 STATE, CONTROL, FRAME_PLACEMENT, FRAME_TRANSLATION = 1, 2, 3, 4
 CONTACT_3D, CONTACT_6D = 5, 6  # contact records (FDDP_KNOT_EULER_CONTACTFWD)
+CONTACT_FORCE = 7  # CostModelContactForce: r = lambda[row0:row0+nr] - fref (contact-force.hxx:33-50)
 H_CS = 1e-30  # complex-step size
 
 
@@ -305,6 +306,12 @@ class Cost:
             else:
                 self.pref = d[13:16]
                 w, nr = d[16:19], 3
+        elif self.type == CONTACT_FORCE:
+            self.row0, nr = int(d[0]), int(d[1])
+            self.fref = d[2:2 + nr]
+            w = d[8:8 + nr]
+            self.force_fn = None  # set by ContactFwdKnot: (x, u) -> lambda
+            self.zero_jac = False  # reference: Rx = Ru = 0 unless enable_force
         else:
             raise ValueError(f"unknown cost type {self.type}")
         self.w = np.asarray(w, float) if weighted else np.ones(nr)
@@ -315,6 +322,8 @@ class Cost:
             return x - self.xref  # diff(xref, x), state.hxx:136
         if self.type == CONTROL:
             return u - self.uref  # control.hxx:67
+        if self.type == CONTACT_FORCE:
+            return self.force_fn(x, u)[self.row0:self.row0 + len(self.fref)] - self.fref
         if oM is None:
             oM = robot.placements(x[:nj])
         R0, p0 = oM[self.joint]
@@ -396,6 +405,8 @@ class FreeFwdKnot:
         for k in self.costs:
             r = k.residual(self.robot, x, u)
             Rz = self._cs_jac(lambda zz: k.residual(self.robot, zz[:n], zz[n:]), z, r.size)
+            if getattr(k, "zero_jac", False):
+                Rz[:] = 0.0
             Lz += k.weight * Rz.T @ (k.w * r)
             Lzz += k.weight * Rz.T @ (k.w[:, None] * Rz)
         s = dt if dt != 0 else 1.0
@@ -471,6 +482,7 @@ class ContactFwdKnot(FreeFwdKnot):
         self.nun = int(body[o])
         self.damping = float(body[o + 1])
         ncon = int(body[o + 2])
+        self.enable_force = int(body[o + 3]) == 2
         o += 4
         self.contacts = []
         for _ in range(ncon):
@@ -481,6 +493,10 @@ class ContactFwdKnot(FreeFwdKnot):
         super().__init__(block, nx, nu, _contact=True)
         self.kind = 5
         self.nc = sum(c.nc for c in self.contacts)
+        for c in self.costs:
+            if c.type == CONTACT_FORCE:
+                c.force_fn = lambda xx, uu: self.accel_force(xx, uu)[1]
+                c.zero_jac = not self.enable_force
 
     def contact_terms(self, x):
         """(Jc (nc x nv), a0 (nc)) at ddq = 0 (ContactModelMultiple::calc)."""

@@ -511,6 +511,7 @@ struct Costs {  // record pointers in name order
 inline const double* cost_w(const double* rc, int nr) { return rc + (int)rc[3] - nr; }
 inline int cost_nr(const double* rc, int nx, int nu) {
   const int t = (int)rc[0];
+  if (t == 7) return (int)rc[5];
   return t == C_STATE ? nx : (t == C_CONTROL ? nu : (t == C_FRAME_PLACEMENT ? 6 : 3));
 }
 
@@ -702,6 +703,8 @@ struct Knot {
         for (int i = 0; i < nx; ++i) a += w[i] * (x[i] - d[i]) * (x[i] - d[i]);
       } else if (type == C_CONTROL) {
         for (int i = 0; i < nu(); ++i) a += w[i] * (u[i] - d[i]) * (u[i] - d[i]);
+      } else if (type == 7) {  // CostModelContactForce: not restated in this port (numpy oracle only)
+        a = NAN;
       } else {
         frame_residual(rb, K, d, type, -1, r, nullptr);
         for (int i = 0; i < nr; ++i) a += w[i] * r[i] * r[i];
@@ -815,6 +818,8 @@ struct Knot {
           Lx[i] += wt * w[i] * (x[i] - d[i]);
           Lxx[i * n + i] += wt * w[i];
         }
+      } else if (type == 7) {
+        for (int i = 0; i < n; ++i) Lx[i] = NAN;
       } else if (type == C_CONTROL) {
         for (int i = 0; i < nu(); ++i) {
           Lu[i] += wt * w[i] * (u[i] - d[i]);

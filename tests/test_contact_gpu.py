@@ -46,7 +46,8 @@ def _setup(T, B, mixed=False, impact=None, **kw):
 CASES = [dict(contact="6d"), dict(contact="3d", weighted=True), dict(contact="3d+3d", armature=np.full(7, 0.02)),
          dict(contact="6d+3d", damping=1e-3, inactive=True), dict(contact="6d", gains=(0.0, 0.0)),
          dict(contact="6d+3d", robot=mb.sample_tree(10, seed=5), damping=1e-2, weighted=True), dict(mixed=True),
-         dict(impact=0.0), dict(impact=0.5)]
+         dict(impact=0.0), dict(impact=0.5),
+         dict(contact="6d+3d", damping=1e-3, force_costs=True), dict(contact="3d", force_costs=True, weighted=True)]
 
 
 @pytest.mark.parametrize("case", range(len(CASES)))
@@ -94,7 +95,7 @@ def test_calc_and_calc_diff(case):
         assert abs(cost[b] - ctot) <= 1e-10 * max(1.0, abs(ctot)), (b, cost[b], ctot)
 
 
-@pytest.mark.parametrize("case", [0, 1, 3, 6, 7, 8])
+@pytest.mark.parametrize("case", [0, 1, 3, 6, 7, 8, 9, 10])
 def test_solve_vs_oracle(case):
     """Full solves to convergence: identical iteration counts, xs / us / cost within 1e-6."""
     T, B = 16, 2

@@ -409,3 +409,47 @@ def test_impulse_api_validation():
     am = mb.ActionModelImpulseFwdDynamics(state, imps, costs, 0.3, 1e-4)
     k = onp.ImpulseFwdKnot(am.pack()[2][0], 14, 0)
     assert [c.type for c in k.contacts] == [onp.CONTACT_6D, onp.CONTACT_3D] and k.r_coeff == 0.3 and k.nc == 9
+
+
+def test_contact_force_cost_packing_and_derivatives():
+    """CostModelContactForce (contact-force.hxx): r = lambda of the contact on fref.id
+    minus fref; packed with the contact's row offset (name order of the active
+    contacts); derivatives vs central differences of the cost with enable_force,
+    zero Jacobians without it (the reference's df_dx stays unset)."""
+    from crocoddyl_amd import synthetic
+    _, running, _ = synthetic.build_arm_contact(T=1, B=1, contact="6d+3d", damping=1e-3, force_costs=True)
+    _, nu, blk = running[0].pack()
+    k = onp.ContactFwdKnot(blk[0], 14, nu)
+    fc = {c.row0: c for c in k.costs if c.type == onp.CONTACT_FORCE}
+    assert sorted(fc) == [0, 3] and len(fc[0].fref) == 3 and len(fc[3].fref) == 6  # elbow 3D first, then gripper
+    rng = np.random.default_rng(11)
+    x, u = rng.uniform(-1, 1, 14), rng.uniform(-1, 1, nu)
+    d = k.calc_diff(x, u)
+    h = np.sqrt(2 * np.finfo(float).eps)
+    z = np.concatenate([x, u])
+    g = np.zeros(z.size)
+    for j in range(z.size):
+        e = np.zeros(z.size)
+        e[j] = h
+        g[j] = (k.calc(z[:14] + e[:14], z[14:] + e[14:])[1] - k.calc(z[:14] - e[:14], z[14:] - e[14:])[1]) / (2 * h)
+    scale = max(1.0, np.abs(g).max())
+    np.testing.assert_allclose(d["Lx"], g[:14], atol=3e4 * h * scale)
+    np.testing.assert_allclose(d["Lu"], g[14:], atol=3e4 * h * scale)
+    assert np.abs(d["Lxu"]).max() > 0
+    _, running2, _ = synthetic.build_arm_contact(T=1, B=1, contact="6d", force_costs=True, enable_force=False)
+    _, nu2, blk2 = running2[0].pack()
+    d2 = onp.ContactFwdKnot(blk2[0], 14, nu2).calc_diff(x, u)
+    assert not d2["Lxu"].any()
+    # no contact on the cost's frame -> the reference throws at createData
+    model = mb.sample_talos_arm()
+    other = model.addFrame("other", 3, mb.SE3())
+    state = mb.StateMultibody(model)
+    act = mb.ActuationModelFloatingBase(state)
+    contacts = mb.ContactModelMultiple(state, act.nu)
+    fid = model.getFrameId("gripper_left_joint")
+    contacts.addContact("g", mb.ContactModel3D(state, mb.FrameTranslation(fid, np.zeros(3)), act.nu))
+    costs = mb.CostModelSum(state, act.nu)
+    costs.addCost("f", mb.CostModelContactForce(state, mb.FrameForce(other, np.zeros(6)), 3, act.nu), 1.0)
+    dam = mb.DifferentialActionModelContactFwdDynamics(state, act, contacts, costs, 0.0, True)
+    with pytest.raises(ValueError):
+        croc.IntegratedActionModelEuler(dam, 1e-2).pack()
