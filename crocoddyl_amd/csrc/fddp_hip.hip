@@ -69,68 +69,84 @@ int64_t block_doubles(int kind, int nx, int nu) {
 }
 
 
-// Checks one FDDP_KNOT_EULER_FREEFWD / _CONTACTFWD block (layouts in
-// include/fddp_hip.h) against nx / nu and the space left in the pool. Returns
-// its size in doubles, or -1 with `why` set. nj / nframe / nc: joints, frame
-// costs and contact rows (LDS sizing).
+// Checks one FDDP_KNOT_EULER_FREEFWD / _CONTACTFWD / FDDP_KNOT_IMPULSEFWD block
+// (layouts in include/fddp_hip.h) against nx / nu and the space left in the
+// pool. Returns its size in doubles, or -1 with `why` set. nj / njac / nc:
+// dofs, jac costs and contact rows (LDS sizing).
 int64_t mb_block_check(const double* P, int64_t avail, int kind, int nx, int nu, std::string& why, int* nj_out,
-                       int* nframe_out, int* nc_out) {
+                       int* njac_out, int* nc_out) {
   using namespace fddp::mb;
   if (avail < FDDP_PARAM_HEADER) return why = "block out of range", -1;
   const double dt = P[0];
   const int nj = (int)P[1], ncost = (int)P[2];
   const int64_t size = (int64_t)P[3];
   if (!(dt >= 0.) || !std::isfinite(dt)) return why = "dt has positive value", -1;
-  if ((double)nj != P[1] || nj < 1 || nj > kMaxJ) return why = "number of joints out of [1, 32]", -1;
-  if (nx != 2 * nj) return why = "multibody knots need nx = 2 nv", -1;
+  if ((double)nj != P[1] || nj < 1 || nj > kMaxJ) return why = "number of dofs out of [1, 64]", -1;
+  if (size > avail || (double)size != P[3]) return why = "block out of range", -1;
+  int64_t o = FDDP_PARAM_HEADER + 3 + nj;
+  if (o + kJRec > size) return why = "block too small for its joints", -1;
+  const bool ff = (int)P[o] == J_FREEFLYER;
+  if (ff && nj < 6) return why = "a free-flyer root needs nv >= 6", -1;
+  const int nb = ff ? nj - 5 : nj, nq = ff ? nj + 1 : nj;
+  if (nx != nq + nj) return why = "multibody knots need nx = nq + nv", -1;
   const bool contact = kind == FDDP_KNOT_EULER_CONTACTFWD, impulse = kind == FDDP_KNOT_IMPULSEFWD;
-  if (!contact && !impulse && nu != nj) return why = "ActuationModelFull needs nu = nv", -1;
+  if (!contact && !impulse && (nu != nj || ff)) return why = "ActuationModelFull needs nu = nv and no free-flyer", -1;
   if (impulse && nu != 0) return why = "impulse knots have nu = 0", -1;
   if (impulse && dt != 0.) return why = "impulse blocks carry dt = 0 (no integrator)", -1;
   if ((double)ncost != P[2] || ncost < 0 || ncost > kMaxCosts) return why = "number of costs out of [0, 64]", -1;
-  if (size > avail || (double)size != P[3]) return why = "block out of range", -1;
-  int64_t o = FDDP_PARAM_HEADER + 3 + nj;
   int force_rows = 0;  // rows the contact-force costs read
-  if (o + (int64_t)kJRec * nj > size) return why = "block too small for its joints", -1;
-  for (int i = 0; i < nj; ++i) {
+  if (o + (int64_t)kJRec * nb > size) return why = "block too small for its joints", -1;
+  for (int i = 0; i < nb; ++i) {
     const double* J = P + o + (int64_t)kJRec * i;
-    const int par = (int)J[0];
-    if ((double)par != J[0] || par < -1 || par >= i) return why = "joint parents must precede their children", -1;
-    const double an = std::sqrt(J[1] * J[1] + J[2] * J[2] + J[3] * J[3]);
-    if (!(std::fabs(an - 1.) < 1e-9)) return why = "joint axes must be unit vectors", -1;
-    if (!(J[16] >= 0.)) return why = "negative body mass", -1;
+    const int type = (int)J[0], par = (int)J[1];
+    if ((double)type != J[0] || (type != J_REVOLUTE && type != J_FREEFLYER)) return why = "unknown joint type", -1;
+    if (type == J_FREEFLYER && (i != 0 || par != -1)) return why = "a free-flyer may only be the root joint", -1;
+    if ((double)par != J[1] || par < -1 || par >= i) return why = "joint parents must precede their children", -1;
+    if (type == J_REVOLUTE) {
+      const double an = std::sqrt(J[2] * J[2] + J[3] * J[3] + J[4] * J[4]);
+      if (!(std::fabs(an - 1.) < 1e-9)) return why = "joint axes must be unit vectors", -1;
+    }
+    if (!(J[17] >= 0.)) return why = "negative body mass", -1;
   }
-  o += (int64_t)kJRec * nj;
-  int nframe = 0;
+  o += (int64_t)kJRec * nb;
+  int njac = 0;
   for (int k = 0; k < ncost; ++k) {
     if (o + kCHdr > size) return why = "cost records out of range", -1;
     const double* C = P + o;
     const int type = (int)C[0];
     const int64_t rs = (int64_t)C[3];
     int64_t want = -1;
-    if (type == C_STATE) want = kCHdr + 2 * nx;
+    if (type == C_STATE) want = kCHdr + nx + 2 * nj;
     if (type == C_CONTROL) want = kCHdr + 2 * (int64_t)nu;
     if (type == C_FRAME_PLACEMENT) want = kCHdr + 31;
     if (type == C_FRAME_TRANSLATION) want = kCHdr + 19;
+    if (type == C_COM_POSITION) want = kCHdr + 6;
     if (type == C_CONTACT_FORCE) {  // [row0, nr, fref(6)] + w(nr); rows checked against the contacts below
       const int nrf = o + kCHdr + 1 < size ? (int)C[kCHdr + 1] : 0;
       if (kind != FDDP_KNOT_EULER_CONTACTFWD || (nrf != 3 && nrf != 6))
         return why = "contact-force costs need contact knots and a 3- or 6-row force", -1;
       want = kCHdr + 8 + nrf;
-      force_rows = std::max(force_rows, (int)C[kCHdr] + nrf);
-      if ((int)C[kCHdr] < 0) return why = "contact-force cost row out of range", -1;
+      const int row0 = (int)C[kCHdr];
+      if ((double)row0 != C[kCHdr] || (row0 < 0 && row0 != kInactiveForceRow))
+        return why = "contact-force cost row out of range", -1;
+      if (row0 >= 0) force_rows = std::max(force_rows, row0 + nrf);
     }
     if (want < 0) return why = "unknown cost type " + std::to_string(type), -1;
     if (rs != want || o + rs > size) return why = "cost record of the wrong size", -1;
     if (type == C_FRAME_PLACEMENT || type == C_FRAME_TRANSLATION) {
       const int fj = (int)C[kCHdr];
-      if ((double)fj != C[kCHdr] || fj < 0 || fj >= nj) return why = "frame attached to an unknown joint", -1;
-      ++nframe;
+      if ((double)fj != C[kCHdr] || fj < 0 || fj >= nb) return why = "frame attached to an unknown joint", -1;
     }
+    if (type == C_STATE && ff)  // the reference state's free-flyer pose must be finite
+      for (int e = 0; e < 7; ++e)
+        if (!std::isfinite(C[kCHdr + e])) return why = "non-finite reference state", -1;
+    if (type == C_FRAME_PLACEMENT || type == C_FRAME_TRANSLATION || type == C_COM_POSITION || (type == C_STATE && ff))
+      ++njac;
     o += rs;
   }
   int nc = 0;
-  if (contact || impulse) {  // [nun | r_coeff, damping, ncontact, 0 | 1] + contact / impulse records
+  std::vector<std::pair<int, int>> crow;  // (row0, rows) of every contact record
+  if (contact || impulse) {  // [nun | r_coeff, damping, ncontact, 0 | 1 | 2] + contact / impulse records
     if (o + 4 > size) return why = "contact section out of range", -1;
     const int nun = (int)P[o], ncon = (int)P[o + 2];
     const double damping = P[o + 1];
@@ -140,6 +156,7 @@ int64_t mb_block_check(const double* P, int64_t avail, int kind, int nx, int nu,
       if (!(P[o] >= 0.) || !std::isfinite(P[o])) return why = "The restitution coefficient has to be positive", -1;
     } else {
       if ((double)nun != P[o] || nun < 0 || nun >= nj) return why = "unactuated dofs out of [0, nv)", -1;
+      if (ff && nun != 6) return why = "ActuationModelFloatingBase on a free-flyer leaves 6 dofs unactuated", -1;
       if (nu != nj - nun) return why = "ActuationModelFloatingBase needs nu = nv - nun", -1;
     }
     if (!(damping >= 0.) || !std::isfinite(damping)) return why = "The damping factor has to be positive", -1;
@@ -156,20 +173,34 @@ int64_t mb_block_check(const double* P, int64_t avail, int kind, int nx, int nu,
       if (want < 0) return why = "unknown contact type " + std::to_string(type), -1;
       if (rs != want || o + rs > size) return why = "contact record of the wrong size", -1;
       const int fj = (int)C[kCHdr];
-      if ((double)fj != C[kCHdr] || fj < 0 || fj >= nj) return why = "contact frame attached to an unknown joint", -1;
+      if ((double)fj != C[kCHdr] || fj < 0 || fj >= nb) return why = "contact frame attached to an unknown joint", -1;
       if (!std::isfinite(C[1]) || !std::isfinite(C[2])) return why = "non-finite contact gains", -1;
-      nc += type == C_CONTACT_3D ? 3 : 6;
+      const int rows = type == C_CONTACT_3D ? 3 : 6;
+      crow.emplace_back(nc, rows);
+      nc += rows;
       o += rs;
     }
     if (nc > kMaxNc) return why = "more than 24 contact rows in one knot", -1;
   }
   if (force_rows > nc) return why = "contact-force cost reads rows beyond the contacts", -1;
+  if (force_rows > 0) {  // each contact-force cost reads exactly one contact of its size
+    int64_t oc = FDDP_PARAM_HEADER + 3 + nj + (int64_t)kJRec * nb;
+    for (int k = 0; k < ncost; ++k) {
+      const double* C = P + oc;
+      if ((int)C[0] == C_CONTACT_FORCE && (int)C[kCHdr] >= 0) {
+        bool hit = false;
+        for (const auto& r : crow) hit = hit || (r.first == (int)C[kCHdr] && r.second == (int)C[kCHdr + 1]);
+        if (!hit) return why = "a contact-force cost must read one whole contact of its size", -1;
+      }
+      oc += (int64_t)C[3];
+    }
+  }
   if (o != size) return why = "block size does not match its records", -1;
-  if (nframe > kMaxFrameCosts) return why = "more than 8 frame costs in one knot", -1;
-  if ((pad2(diff_layout(nj, nframe, nc).total) + pad2(size)) * 8 > 160 * 1024)
-    return why = "too many joints for the calcDiff LDS plan", -1;
+  if (njac > kMaxJacCosts) return why = "more than 8 frame / CoM / free-flyer state costs in one knot", -1;
+  if ((pad2(diff_layout(nj, njac, nc).total) + pad2(size)) * 8 > 160 * 1024)
+    return why = "too many dofs for the calcDiff LDS plan", -1;
   if (nj_out) *nj_out = std::max(*nj_out, nj);
-  if (nframe_out) *nframe_out = std::max(*nframe_out, nframe);
+  if (njac_out) *njac_out = std::max(*njac_out, njac);
   if (nc_out) *nc_out = std::max(*nc_out, nc);
   return size;
 }
@@ -187,6 +218,8 @@ int check_knots(const fddp_dims& d, const fddp_knot_desc* knots, const double* p
     const fddp_knot_desc& k = knots[t];
     if (k.nu < 0) return fail(FDDP_ERR_INVALID_ARG, w + ": negative nu");
     if (t < d.T && k.nu > nu_max) nu_max = k.nu;
+    if (d.nx != d.ndx && !is_mb_kind(k.kind))
+      return fail(FDDP_ERR_INVALID_ARG, w + ": a free-flyer state needs multibody knots");
     if (k.kind == FDDP_KNOT_UNICYCLE && (d.nx != 3 || k.nu != 2))
       return fail(FDDP_ERR_INVALID_ARG, w + ": unicycle knots need nx=3, nu=2");
     if (k.kind == FDDP_KNOT_EULER_DIFFLQR && (d.nx % 2))
@@ -356,7 +389,7 @@ int launch_fused(fddp_handle* h, int sel_calc, int sel_diff, int gaps) {
 // Multibody knots (knot-parallel): calc for sel_calc, calcDiff for sel_diff (-1: none).
 int launch_mb(fddp_handle* h, int sel_calc, int sel_diff) {
   const Dev& D = h->D;
-  hipLaunchKernelGGL(mb_knot_kernel, dim3(D.T + 1, D.B), dim3(64), h->mb_diff_smem, h->stream, D, sel_calc, sel_diff);
+  hipLaunchKernelGGL(mb_knot_kernel, dim3(D.T + 1, D.B), dim3(mb::kMbDiffNT), h->mb_diff_smem, h->stream, D, sel_calc, sel_diff);
   LAUNCH_CHECK();
   return FDDP_OK;
 }
@@ -577,7 +610,7 @@ int apply_knots(fddp_handle* h, const fddp_knot_desc* knots, const double* param
   h->knots.assign(knots, knots + K1);
   {
     int64_t pmax = 0;
-    int mb_nj = 0, mb_nframe = 0, mb_nc = 0;
+    int mb_nj = 0, mb_njac = 0, mb_nc = 0;
     h->has_mb = false;
     for (int t = 0; t <= d.T; ++t) {
       int64_t sz;
@@ -589,7 +622,7 @@ int apply_knots(fddp_handle* h, const fddp_knot_desc* knots, const double* param
           const int64_t off = knots[t].param_offset + (int64_t)b * knots[t].param_stride;
           std::string why;
           sz = std::max(sz, mb_block_check(params + off, n_params - off, knots[t].kind, d.nx, knots[t].nu, why, &mb_nj,
-                                           &mb_nframe, &mb_nc));
+                                           &mb_njac, &mb_nc));
         }
       } else {
         sz = block_doubles(knots[t].kind, d.nx, knots[t].nu);
@@ -606,9 +639,9 @@ int apply_knots(fddp_handle* h, const fddp_knot_desc* knots, const double* param
         for (int b = 0; b < nb; ++b)
           mb_pmax = std::max<int64_t>(mb_pmax, (int64_t)params[knots[t].param_offset + (int64_t)b * knots[t].param_stride + 3]);
       }
-    D.mbd = h->has_mb ? pad2(fddp::mb::diff_layout(mb_nj, mb_nframe, mb_nc).total) : 0;
+    D.mbd = h->has_mb ? pad2(fddp::mb::diff_layout(mb_nj, mb_njac, mb_nc).total) : 0;
     h->mb_diff_smem = h->has_mb ? sizeof(double) * (D.mbd + pad2(mb_pmax)) : 0;
-    const int64_t budget = (150 * 1024) / 8 - (2 * D.sX + D.sM + 5 * (kNT / kWave) + 16) - D.mbw;
+    const int64_t budget = (150 * 1024) / 8 - (2 * D.sX + D.sM + 2 * D.sN + 5 * (kNT / kWave) + 16) - D.mbw;
     h->pcap = pmax <= budget ? pad2(pmax) : 0;
   }
   h->fwd_smem = sizeof(double) * (h->pcap + fwd_lds_doubles<kNT, false>(D.sX, D.sN, D.sM) + D.mbw);
@@ -700,7 +733,13 @@ int fddp_create(const fddp_dims* dims, const fddp_knot_desc* knots, const double
   const fddp_dims d = *dims;
   if (d.T < 1 || d.B < 1 || d.nx < 1 || d.nu_max < 0)
     return fail(FDDP_ERR_INVALID_ARG, "fddp_create: T, B, nx must be positive");
-  if (d.nx != d.ndx) return fail(FDDP_ERR_UNSUPPORTED, "fddp_create: only Euclidean states (nx == ndx) are supported");
+  if (d.nx != d.ndx) {  // StateMultibody with a free-flyer root: nq = nv + 1, ndx = 2 nv (multibody.hxx:16-17)
+    if (d.nx != d.ndx + 1 || d.ndx % 2 || d.ndx < 12)
+      return fail(FDDP_ERR_UNSUPPORTED, "fddp_create: nx != ndx is supported for free-flyer states (nx = ndx + 1)");
+    for (int t = 0; t <= d.T; ++t)
+      if (!is_mb_kind(knots[t].kind))
+        return fail(FDDP_ERR_INVALID_ARG, "fddp_create: a free-flyer state needs multibody knots");
+  }
   if (d.B > 65535) return fail(FDDP_ERR_INVALID_ARG, "fddp_create: B > 65535 per handle");
   {
     const int rc0 = check_knots(d, knots, params, n_params, "fddp_create", true);

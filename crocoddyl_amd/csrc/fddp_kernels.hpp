@@ -20,6 +20,54 @@ __device__ inline int64_t block_doubles_dev(int kind, int nx, int nu, const doub
          nu;
 }
 
+// StateMultibody with a free-flyer root (nx = ndx + 1: x = (p, quat xyzw, q_rest, v)),
+// otherwise a Euclidean state (StateVector, or StateMultibody over revolute joints).
+// diff(x0, x1) / integrate(x, dx) (multibody.hxx:54-91, euclidean.hxx:28-61) over the
+// threads of a workgroup; thread 0 does the free-flyer's SE(3) part. out may not
+// alias the inputs. No barrier inside.
+template <int NT>
+__device__ __forceinline__ void state_diff_wg(const Dev& D, const double* x0, const double* x1, double* out) {
+  const int n = D.n;
+  if (D.nx == n) {
+    for (int i = threadIdx.x; i < n; i += NT) out[i] = x1[i] - x0[i];
+    return;
+  }
+  const int nv = n / 2, nq = D.nx - nv;
+  for (int i = threadIdx.x; i < n; i += NT) {
+    if (i < 6) {
+      if (i == 0) mb::ff_difference(x0, x1, out);
+    } else if (i < nv) {
+      out[i] = x1[i + 1] - x0[i + 1];
+    } else {
+      out[i] = x1[nq + i - nv] - x0[nq + i - nv];
+    }
+  }
+}
+// integrate(x, s * dx)
+template <int NT>
+__device__ __forceinline__ void state_integrate_wg(const Dev& D, const double* x, const double* dx, double s,
+                                                   double* out) {
+  const int n = D.n;
+  if (D.nx == n) {
+    for (int i = threadIdx.x; i < n; i += NT) out[i] = x[i] + dx[i] * s;
+    return;
+  }
+  const int nv = n / 2, nq = D.nx - nv;
+  for (int i = threadIdx.x; i < n; i += NT) {
+    if (i < 6) {
+      if (i == 0) {
+        double d6[6];
+        for (int e = 0; e < 6; ++e) d6[e] = dx[e] * s;
+        mb::ff_integrate(x, d6, out);
+      }
+    } else if (i < nv) {
+      out[i + 1] = x[i + 1] + dx[i] * s;
+    } else {
+      out[nq + i - nv] = x[nq + i - nv] + dx[i] * s;
+    }
+  }
+}
+
 // Keep one knot parameter block resident in LDS across consecutive knots that
 // share it (a reference model object shared by several knots, or one
 // element's perturbed model used at every t). Returns the pointer to read the
@@ -179,17 +227,10 @@ __global__ __launch_bounds__(NT) void calc_diff_kernel(Dev D, int sel, int gaps,
     if (gaps) {
       if (!s.is_feasible) {
         // fs[0] = diff(xs[0], x0) = x0 - xs[0]; fs[t+1] = diff(xs[t+1], data[t].xnext)
-        if (t == 0) {
-          double* f = D.fs + D.knot(b, 0) * D.sN;
-          const double* x0 = D.x0 + (int64_t)b * D.sX;
-          for (int i = threadIdx.x; i < D.n; i += NT) f[i] = x0[i] - x[i];
-        }
-        if (running) {
-          double* f = D.fs + D.knot(b, t + 1) * D.sN;
-          const double* xn = D.xnext[c] + D.run(b, t) * D.sX;
-          const double* x1 = D.xs[c] + D.knot(b, t + 1) * D.sX;
-          for (int i = threadIdx.x; i < D.n; i += NT) f[i] = xn[i] - x1[i];
-        }
+        if (t == 0) state_diff_wg<NT>(D, x, D.x0 + (int64_t)b * D.sX, D.fs + D.knot(b, 0) * D.sN);
+        if (running)
+          state_diff_wg<NT>(D, D.xs[c] + D.knot(b, t + 1) * D.sX, D.xnext[c] + D.run(b, t) * D.sX,
+                            D.fs + D.knot(b, t + 1) * D.sN);
       } else if (!s.was_feasible) {  // closing the gaps
         double* f = D.fs + kk * D.sN;
         for (int i = threadIdx.x; i < D.n; i += NT) f[i] = 0.;
@@ -199,13 +240,13 @@ __global__ __launch_bounds__(NT) void calc_diff_kernel(Dev D, int sel, int gaps,
   }
 }
 
-// Multibody knots (multibody.hpp), knot-parallel: one 64-thread workgroup per
+// Multibody knots (multibody.hpp), knot-parallel: one mb::kMbDiffNT-thread workgroup per
 // (knot t = blockIdx.x, element b = blockIdx.y); knots of other kinds return.
 // calc (xnext, knot cost) for elements selected by sel_calc and calcDiff
 // (derivative blocks) for those selected by sel_diff (-1: none), fused: the
 // calcDiff evaluates the dynamics the calc needs anyway. The gaps of these
 // knots are written by calc_diff_kernel as for any knot.
-__global__ __launch_bounds__(64) void mb_knot_kernel(Dev D, int sel_calc, int sel_diff) {
+__global__ __launch_bounds__(mb::kMbDiffNT) void mb_knot_kernel(Dev D, int sel_calc, int sel_diff) {
   const int t = blockIdx.x, b = blockIdx.y;
   const fddp_knot_desc kd = D.knots[t];
   if (!is_mb_kind(kd.kind)) return;
@@ -225,7 +266,7 @@ __global__ __launch_bounds__(64) void mb_knot_kernel(Dev D, int sel_calc, int se
   const double* Pg = D.pblock(b, t);
   double* P = sm + D.mbd;
   const int psz = (int)Pg[3];
-  for (int e = threadIdx.x; e < psz; e += 64) P[e] = Pg[e];
+  for (int e = threadIdx.x; e < psz; e += mb::kMbDiffNT) P[e] = Pg[e];
   __syncthreads();
   if (do_diff)
     mb::knot_calc_diff(P, D.nx, D.m, xg, ug, running && kd.nu > 0, sm, D.Fx + kk * D.sNN, D.Fu + kk * D.sNM,
@@ -599,11 +640,12 @@ __global__ __launch_bounds__(NT) void backward_kernel(Dev D, Prm prm, int mode) 
 template <int NT>
 __device__ __forceinline__ bool fwd_trial(const Dev& D, int b, const ElemState& s, double alpha, double* xv, double* uv, double* xn,
                           double* red, int* flag, double& cost_try, double& dv, double* pl, int64_t pcap,
-                          const double*& cached, double* mbw) {
+                          const double*& cached, double* mbw, double* dxv) {
   const int n = D.n, nx = D.nx, m = D.m, T = D.T, tid = threadIdx.x;
   const int c = s.cur, o = 1 - c;
   const bool feas = s.is_feasible != 0;
   const bool full = feas || alpha == 1.;
+  const bool ff = nx != n;  // free-flyer state (dxv: 2 sN doubles of LDS)
   const double* x0 = D.x0 + (int64_t)b * D.sX;
   for (int i = tid; i < nx; i += NT) xn[i] = x0[i];
   cost_try = 0.;
@@ -616,13 +658,27 @@ __device__ __forceinline__ bool fwd_trial(const Dev& D, int b, const ElemState& 
     double* xt = D.xs[o] + kk * D.sX;
     // xs_try[t] = xnext  or  integrate(xnext, fs[t] * (alpha - 1))
     double pd = 0.;
-    for (int i = tid; i < nx; i += NT) {
-      const double v = full ? xn[i] : xn[i] + fs[i] * (alpha - 1);
-      xv[i] = v;
-      xt[i] = v;
-      if (!feas) pd += (v - xs[i]) * D.Vxxfs[kk * D.sN + i];  // -fs^T Vxx diff(xs_try, xs)
+    if (!ff) {
+      for (int i = tid; i < nx; i += NT) {
+        const double v = full ? xn[i] : xn[i] + fs[i] * (alpha - 1);
+        xv[i] = v;
+        xt[i] = v;
+        if (!feas) pd += (v - xs[i]) * D.Vxxfs[kk * D.sN + i];  // -fs^T Vxx diff(xs_try, xs)
+      }
+      __syncthreads();
+    } else {  // on the manifold: dx = diff(xs, xs_try) for the gains, diff(xs_try, xs) for dv
+      if (full)
+        for (int i = tid; i < nx; i += NT) xv[i] = xn[i];
+      else
+        state_integrate_wg<NT>(D, xn, fs, alpha - 1, xv);
+      __syncthreads();
+      for (int i = tid; i < nx; i += NT) xt[i] = xv[i];
+      state_diff_wg<NT>(D, xs, xv, dxv);
+      if (!feas) state_diff_wg<NT>(D, xv, xs, dxv + D.sN);
+      __syncthreads();
+      if (!feas)
+        for (int i = tid; i < n; i += NT) pd -= dxv[D.sN + i] * D.Vxxfs[kk * D.sN + i];
     }
-    __syncthreads();
     const bool running = t < T;
     const fddp_knot_desc kd = D.knots[t];
     const double* P = stage_params<NT>(D.pblock(b, t), block_doubles_dev(kd.kind, nx, kd.nu, D.pblock(b, t)), pl, pcap, cached);
@@ -637,7 +693,10 @@ __device__ __forceinline__ bool fwd_trial(const Dev& D, int b, const ElemState& 
         double v = 0.;
         if (i < nu) {
           double kd2 = 0.;
-          for (int j = 0; j < n; ++j) kd2 += K[(int64_t)j * m + i] * (xv[j] - xs[j]);
+          if (ff)
+            for (int j = 0; j < n; ++j) kd2 += K[(int64_t)j * m + i] * dxv[j];
+          else
+            for (int j = 0; j < n; ++j) kd2 += K[(int64_t)j * m + i] * (xv[j] - xs[j]);
           v = (us[i] - kv[i] * alpha) - kd2;
           // SolverBoxFDDP::forwardPass: cwiseMax(u_lb).cwiseMin(u_ub) (box-fddp.cpp:100-102)
           if (D.box_knot(b, t)) v = std_min(std_max(v, D.ulb[D.run(b, t) * D.sM + i]), D.uub[D.run(b, t) * D.sM + i]);
@@ -688,11 +747,11 @@ __device__ __forceinline__ bool fwd_trial_fast(const Dev& D, int b, const ElemSt
                                                const double*& cached);
 
 // Forward-pass LDS beyond the parameter block (doubles): generic trial
-// [xv sX | uv sM | xn sX | red 5*NW+8 | flag | multibody scratch D.mbw], fast trial
+// [xv sX | uv sM | xn sX | red 5*NW+8 | flag 2 | dxv 2 sN | multibody scratch D.mbw], fast trial
 // [xu sX+sM | dxv sN | xn sX | pa NT | pdyn NT | red 24 | flag].
 template <int NT, bool FAST>
 __host__ __device__ inline int64_t fwd_lds_doubles(int64_t sX, int64_t sN, int64_t sM) {
-  return FAST ? (sX + sM) + sN + sX + 2 * NT + 24 + 2 : 2 * sX + sM + 5 * (NT / 64) + 8 + 2;
+  return FAST ? (sX + sM) + sN + sX + 2 * NT + 24 + 2 : 2 * sX + sM + 5 * (NT / 64) + 8 + 2 + 2 * sN;
 }
 
 template <int NT, bool FAST>
@@ -727,7 +786,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2))) void fo
     if constexpr (FAST)
       return fwd_trial_fast<NT, true>(D, b, s, alpha, xv, dxv, xn, pa, pdyn, red, flag, ct, dv, pl, pcap, cached);
     else
-      return fwd_trial<NT>(D, b, s, alpha, xv, uv, xn, red, flag, ct, dv, pl, pcap, cached, (double*)flag + 2);
+      return fwd_trial<NT>(D, b, s, alpha, xv, uv, xn, red, flag, ct, dv, pl, pcap, cached, (double*)flag + 2 + 2 * D.sN,
+                           (double*)flag + 2);
   };
   if (mode == 1) {
     double ct, dv;
@@ -861,8 +921,10 @@ __global__ void scatter_traj_kernel(Dev D, int which, const double* in, int use_
   const int64_t sw = which == 0 ? D.sX : D.sM;
   double* dst = (which == 0 ? D.xs[c] : D.us[c]) + (int64_t)b * rows * sw;
   const double* src = in + (int64_t)b * rows * w;
+  // state.zero() of a free-flyer state: the identity quaternion (pinocchio::neutral)
+  const int qw = (which == 0 && D.nx != D.n) ? 6 : -1;
   for (int64_t e = blockIdx.x * blockDim.x + threadIdx.x; e < rows * w; e += (int64_t)gridDim.x * blockDim.x)
-    dst[(e / w) * sw + e % w] = use_zero ? 0. : src[e];
+    dst[(e / w) * sw + e % w] = use_zero ? ((e % w) == qw ? 1. : 0.) : src[e];
 }
 
 

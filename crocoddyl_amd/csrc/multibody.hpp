@@ -1,23 +1,32 @@
 // Multibody knots on the device: IntegratedActionModelEuler ∘
-// DifferentialActionModelFreeFwdDynamics (ActuationModelFull, CostModelSum of
-// State / Control / FramePlacement / FrameTranslation costs) over a fixed-base
-// kinematic tree of revolute joints.
+// DifferentialAction{Free,Contact}FwdDynamics and ActionModelImpulseFwdDynamics
+// (CostModelSum of State / Control / FramePlacement / FrameTranslation / CoMPosition /
+// ContactForce costs) over a kinematic tree of revolute joints below either the
+// universe or a free-flyer root (StateMultibody on SE(3) x R^n).
 //
 // Reference: include/crocoddyl/core/integrator/euler.hxx:41-131,
-//   multibody/actions/free-fwddyn.hxx:44-118, multibody/costs/cost-sum.hxx:89-160,
-//   multibody/costs/{state,control,frame-placement,frame-translation}.hxx; the rigid-body
-//   arithmetic the reference takes from Pinocchio (aba, computeABADerivatives,
-//   updateFramePlacement, getFrameJacobian, log6, Jlog6) is computed here as:
+//   multibody/actions/{free,contact,impulse}-fwddyn.hxx, multibody/costs/cost-sum.hxx:89-160,
+//   multibody/costs/*.hxx, multibody/states/multibody.hxx:54-240; the rigid-body
+//   arithmetic the reference takes from Pinocchio (aba, computeRNEADerivatives,
+//   updateFramePlacement, getFrameJacobian, integrate / difference / dIntegrate /
+//   dIntegrateTransport / dDifference, exp6, log6, Jexp6, Jlog6) is computed here as:
 //   * forward dynamics: a = (M + diag(armature))^-1 (tau - nle), with RNEA and the
 //     composite-rigid-body algorithm in world coordinates, where every recursion is
-//     an ancestor / subtree sum evaluated one joint per lane, and the solve by
-//     Gauss-Jordan with one column per lane. (The reference's default path is ABA,
-//     the same function.)
-//   * derivatives: the RNEA linearised along each state direction (one lane per
-//     q_j / v_j direction, tangents kept in LDS), da/dx = -(M + A)^-1 dtau/dx — the
-//     identity computeABADerivatives implements;
-//   * frame-cost Jacobians: the local frame Jacobian column of joint j pushed through
-//     log6 in dual numbers, which is Jlog6(rMf) * fJf (frame-placement.hxx:63-66).
+//     an ancestor / subtree sum evaluated one dof per lane (a free-flyer is six dofs
+//     that share one body), and the solve by Gauss-Jordan with one column per lane.
+//     (The reference's default path is ABA, the same function.)
+//   * derivatives: the world-frame analytic RNEA derivatives, one lane per tangent
+//     direction (q_j or v_j): every world quantity of the subtree moved by q_j is
+//     transported by the joint motion S_j, and what is left reduces to the
+//     subtree composites (composite inertia, and P_k = sum_b dY_b-like terms), so
+//     d tau_k / d q_j is a 6-vector dot product per pair (see dtau_direction);
+//     da/dx = -Kinv (dtau/dx; da0/dx) as computeABADerivatives /
+//     the contact KKT inverse (contact-fwddyn.hxx:127-140).
+//   * frame-cost Jacobians: the frame's motion under S_j pushed through log6 in dual
+//     numbers, which is Jlog6(rMf) * fJf (frame-placement.hxx:63-66);
+//   * free-flyer state: M exp6(dq) with Eigen's quaternion extraction, log6(M0^-1 M1),
+//     Jexp6 / Jlog6 columns in dual numbers, Ad(exp6(dq)^-1) (pinocchio's
+//     SpecialEuclideanOperationTpl<3>).
 // Parameter-block layout: include/fddp_hip.h (FDDP_KNOT_EULER_FREEFWD).
 #pragma once
 
@@ -31,12 +40,14 @@
 namespace fddp {
 namespace mb {
 
-constexpr int kMaxJ = 32;       // joints (2 nv directions <= 64 lanes)
-constexpr int kJRec = 26;       // doubles per joint record
-constexpr int kCHdr = 4;        // doubles of a cost record's header
-constexpr int kMaxFrameCosts = 8;
-constexpr int kValsPerJoint = 52;  // R 9, p 3, oR 9, op 3, v 6, a 6, F 6, composite m 1, c 3, I 6
-constexpr int kMaxNc = 24;         // stacked contact rows (FDDP_KNOT_EULER_CONTACTFWD)
+typedef unsigned long long Mask;  // one bit per dof
+constexpr int kMaxJ = 64;         // dofs (nv)
+constexpr int kJRec = 27;         // doubles per joint record
+constexpr int kCHdr = 4;          // doubles of a cost record's header
+constexpr int kMaxJacCosts = 8;   // costs with a dense residual Jacobian (frame, CoM, free-flyer state)
+constexpr int kMaxNc = 24;        // stacked contact rows (FDDP_KNOT_EULER_CONTACTFWD)
+constexpr int kMbDiffNT = 128;    // threads of the knot-parallel calcDiff workgroup
+enum { J_REVOLUTE = 0, J_FREEFLYER = 1 };
 // Cost record types; contact records (after the costs) use 5 / 6 and the same
 // frame payload as the frame costs, so frame_residual serves both.
 enum {
@@ -46,14 +57,20 @@ enum {
   C_FRAME_TRANSLATION = 4,
   C_CONTACT_3D = 5,
   C_CONTACT_6D = 6,
-  C_CONTACT_FORCE = 7  // cost on a contact's force: payload [row0, nr, fref(6)] (contact-force.hxx)
+  C_CONTACT_FORCE = 7,  // cost on a contact's force: payload [row0, nr, fref(6)] (contact-force.hxx)
+  C_COM_POSITION = 8    // r = com(q) - cref: payload [cref(3)] (com-position.hxx:49-75)
 };
+constexpr int kInactiveForceRow = -2;  // contact-force cost on an inactive contact: lambda = 0, no Jacobians
 
 struct Blk {
   double dt;
-  int nj, ncost;
+  int nj;   // nv: dofs
+  int nq;   // nv + 1 with a free-flyer root
+  int nb;   // joint records (pinocchio joints)
+  bool ff;  // record 0 is a free-flyer (dofs 0..5: base twist, body on dof 5)
+  int ncost;
   const double* g;    // gravity (3)
-  const double* arm;  // armature (nj)
+  const double* arm;  // armature (nv)
   const double* J;    // joint records
   const double* C;    // cost records
   // contact section (DifferentialActionModelContactFwdDynamics); ncon == 0 without
@@ -75,7 +92,10 @@ MB_HD inline Blk parse(const double* P) {
   b.g = P + FDDP_PARAM_HEADER;
   b.arm = b.g + 3;
   b.J = b.arm + b.nj;
-  b.C = b.J + (int64_t)kJRec * b.nj;
+  b.ff = (int)b.J[0] == J_FREEFLYER;
+  b.nb = b.ff ? b.nj - 5 : b.nj;
+  b.nq = b.ff ? b.nj + 1 : b.nj;
+  b.C = b.J + (int64_t)kJRec * b.nb;
   const double* e = b.C;
   for (int k = 0; k < b.ncost; ++k) e += (int)e[3];
   b.nun = 0;
@@ -85,7 +105,7 @@ MB_HD inline Blk parse(const double* P) {
   b.impulse = false;
   b.enable_force = false;
   b.r_coeff = 0.;
-  if (e - P < (int64_t)P[3]) {  // [nun | r_coeff, damping, ncontact, 0 | 1] + records
+  if (e - P < (int64_t)P[3]) {  // [nun | r_coeff, damping, ncontact, 0 | 1 | 2] + records
     b.impulse = (int)e[3] == 1;
     b.enable_force = (int)e[3] == 2;
     b.nun = b.impulse ? b.nj : (int)e[0];
@@ -129,10 +149,12 @@ MB_HD __forceinline__ void matTvec3(const double* R, const double* v, double* o)
 MB_HD __forceinline__ void matmul3(const double* A, const double* B, double* O) {  // O = A B
   for (int c = 0; c < 3; ++c) matvec3(A, B + 3 * c, O + 3 * c);
 }
+MB_HD __forceinline__ void matTmul3(const double* A, const double* B, double* O) {  // O = A^T B
+  for (int c = 0; c < 3; ++c) matTvec3(A, B + 3 * c, O + 3 * c);
+}
 
 // Spatial algebra in (linear, angular) order, as Pinocchio's Motion / Force.
-// liMi = (R, p): pose of the child joint frame in the parent frame.
-// actInv on a motion (child <- parent): lin' = R^T (v - p x w), ang' = R^T w.
+// actInv on a motion by M = (R, p): lin' = R^T (v - p x w), ang' = R^T w.
 MB_HD __forceinline__ void motion_act_inv(const double* R, const double* p, const double* m, double* o) {
   double t[3];
   cross3(p, m + 3, t);
@@ -200,38 +222,65 @@ MB_HD __forceinline__ void inertia_mul(double m, const double* c, const double* 
   o[4] = n1 + t[1];
   o[5] = n2 + t[2];
 }
+MB_HD __forceinline__ double dot6(const double* a, const double* b) {
+  return a[0] * b[0] + a[1] * b[1] + a[2] * b[2] + a[3] * b[3] + a[4] * b[4] + a[5] * b[5];
+}
 
-// Joint record accessors
+// Joint record accessors: [type, parent record (-1 universe), axis(3), placement
+// R(9) p(3), mass, CoM(3), I(6)]
 struct JRec {
   const double* r;
   MB_HD JRec(const Blk& b, int i) : r(b.J + (int64_t)kJRec * i) {}
-  MB_HD int parent() const { return (int)r[0]; }
-  MB_HD const double* axis() const { return r + 1; }
-  MB_HD const double* Rpl() const { return r + 4; }
-  MB_HD const double* ppl() const { return r + 13; }
-  MB_HD double mass() const { return r[16]; }
-  MB_HD const double* com() const { return r + 17; }
-  MB_HD const double* I6() const { return r + 20; }
+  MB_HD int type() const { return (int)r[0]; }
+  MB_HD int parent() const { return (int)r[1]; }
+  MB_HD const double* axis() const { return r + 2; }
+  MB_HD const double* Rpl() const { return r + 5; }
+  MB_HD const double* ppl() const { return r + 14; }
+  MB_HD double mass() const { return r[17]; }
+  MB_HD const double* com() const { return r + 18; }
+  MB_HD const double* I6() const { return r + 21; }
 };
 
-// Per-knot value storage (LDS), kValsPerJoint doubles per joint, then the
-// universe's velocity (0) and acceleration (-gravity) as the root's parent.
-struct Vals {
-  double* base;
-  int nj;
-  MB_HD double* root_v() const { return base + kValsPerJoint * nj; }
-  MB_HD double* root_a() const { return root_v() + 6; }
-  MB_HD double* R(int i) const { return base + kValsPerJoint * i; }
-  MB_HD double* p(int i) const { return R(i) + 9; }
-  MB_HD double* oR(int i) const { return R(i) + 12; }
-  MB_HD double* op(int i) const { return R(i) + 21; }
-  MB_HD double* v(int i) const { return R(i) + 24; }
-  MB_HD double* a(int i) const { return R(i) + 30; }
-  MB_HD double* F(int i) const { return R(i) + 36; }
-  MB_HD double* cm(int i) const { return R(i) + 42; }   // composite mass
-  MB_HD double* cc(int i) const { return R(i) + 43; }   // composite CoM
-  MB_HD double* cI(int i) const { return R(i) + 46; }   // composite inertia about its CoM (6)
-};
+// ---- dofs and bodies --------------------------------------------------------
+// Dof d is one lane. A free-flyer record expands into dofs 0..5 (base twist:
+// linear 0..2 along, angular 3..5 about the base axes) that share one body, whose
+// inertia sits on dof 5; placements compose along 0 -> 1 -> .. -> 5 with the base
+// pose on dof 0 and identities after it. Every other record is one revolute dof.
+MB_HD __forceinline__ int rec_of(const Blk& b, int d) { return b.ff ? (d < 6 ? 0 : d - 5) : d; }
+// the dof that carries record r's body (and its frames)
+MB_HD __forceinline__ int dof_of_rec(const Blk& b, int r) { return b.ff ? (r == 0 ? 5 : r + 5) : r; }
+// configuration index of a revolute dof
+MB_HD __forceinline__ int qof(const Blk& b, int d) { return b.ff ? d + 1 : d; }
+// the dof carrying the parent body (-1: universe)
+MB_HD __forceinline__ int body_parent(const Blk& b, int d) {
+  if (b.ff && d < 6) return -1;
+  const int pr = JRec(b, rec_of(b, d)).parent();
+  return pr < 0 ? -1 : dof_of_rec(b, pr);
+}
+// placement composition parent (free-flyer dofs chain 0 -> 5)
+MB_HD __forceinline__ int chain_parent(const Blk& b, int d) { return (b.ff && d < 6) ? d - 1 : body_parent(b, d); }
+MB_HD __forceinline__ Mask own_mask(const Blk& b, int d) { return (b.ff && d < 6) ? Mask(0x3F) : (Mask(1) << d); }
+// dofs whose body is an ancestor-or-self of d's body
+MB_HD inline Mask anc_mask(const Blk& b, int d) {
+  Mask m = own_mask(b, d);
+  for (int k = body_parent(b, d); k >= 0; k = body_parent(b, k)) m |= own_mask(b, k);
+  return m;
+}
+MB_HD __forceinline__ bool carries_body(const Blk& b, int d) { return !(b.ff && d < 5); }
+// joint-frame axis of dof d; prismatic: translation along it (free-flyer 0..2)
+MB_HD __forceinline__ bool dof_prismatic(const Blk& b, int d) { return b.ff && d < 3; }
+MB_HD __forceinline__ void dof_axis(const Blk& b, int d, double* ax) {
+  if (b.ff && d < 6) {
+    ax[0] = d % 3 == 0 ? 1. : 0.;
+    ax[1] = d % 3 == 1 ? 1. : 0.;
+    ax[2] = d % 3 == 2 ? 1. : 0.;
+  } else {
+    const double* a = JRec(b, rec_of(b, d)).axis();
+    ax[0] = a[0];
+    ax[1] = a[1];
+    ax[2] = a[2];
+  }
+}
 
 // R = Rpl * exp(q [axis]x)  (Rodrigues: c I + s [a]x + (1 - c) a a^T)
 MB_HD inline void joint_rotation(const double* Rpl, const double* ax, double q, double* R) {
@@ -249,6 +298,65 @@ MB_HD inline void joint_rotation(const double* Rpl, const double* ax, double q, 
   Rj[7] = oc * ax[1] * ax[2] - s * ax[0];
   Rj[8] = c + oc * ax[2] * ax[2];
   matmul3(Rpl, Rj, R);
+}
+
+// Eigen QuaternionBase::toRotationMatrix, quaternion (x, y, z, w); column-major R
+MB_HD inline void quat_to_R(const double* qv, double* R) {
+  const double x = qv[0], y = qv[1], z = qv[2], w = qv[3];
+  const double tx = 2. * x, ty = 2. * y, tz = 2. * z;
+  const double twx = tx * w, twy = ty * w, twz = tz * w;
+  const double txx = tx * x, txy = ty * x, txz = tz * x;
+  const double tyy = ty * y, tyz = tz * y, tzz = tz * z;
+  R[0] = 1. - (tyy + tzz);
+  R[1] = txy + twz;
+  R[2] = txz - twy;
+  R[3] = txy - twz;
+  R[4] = 1. - (txx + tzz);
+  R[5] = tyz + twx;
+  R[6] = txz + twy;
+  R[7] = tyz - twx;
+  R[8] = 1. - (txx + tyy);
+}
+
+// Eigen's quaternion from a rotation matrix (quaternionbase_assign_impl), with the
+// index selection written as explicit selects (no runtime-indexed arrays).
+MB_HD inline void R_to_quat(const double* R, double* q) {
+  auto at = [&](int r, int c) { return R[c * 3 + r]; };
+  const double t = at(0, 0) + at(1, 1) + at(2, 2);
+  if (t > 0.) {
+    double s = sqrt(t + 1.);
+    q[3] = 0.5 * s;
+    s = 0.5 / s;
+    q[0] = (at(2, 1) - at(1, 2)) * s;
+    q[1] = (at(0, 2) - at(2, 0)) * s;
+    q[2] = (at(1, 0) - at(0, 1)) * s;
+    return;
+  }
+  int i = 0;
+  if (at(1, 1) > at(0, 0)) i = 1;
+  if (at(2, 2) > (i == 0 ? at(0, 0) : at(1, 1))) i = 2;
+  if (i == 0) {
+    double s = sqrt(at(0, 0) - at(1, 1) - at(2, 2) + 1.);
+    q[0] = 0.5 * s;
+    s = 0.5 / s;
+    q[3] = (at(2, 1) - at(1, 2)) * s;
+    q[1] = (at(1, 0) + at(0, 1)) * s;
+    q[2] = (at(2, 0) + at(0, 2)) * s;
+  } else if (i == 1) {
+    double s = sqrt(at(1, 1) - at(2, 2) - at(0, 0) + 1.);
+    q[1] = 0.5 * s;
+    s = 0.5 / s;
+    q[3] = (at(0, 2) - at(2, 0)) * s;
+    q[2] = (at(2, 1) + at(1, 2)) * s;
+    q[0] = (at(0, 1) + at(1, 0)) * s;
+  } else {
+    double s = sqrt(at(2, 2) - at(0, 0) - at(1, 1) + 1.);
+    q[2] = 0.5 * s;
+    s = 0.5 / s;
+    q[3] = (at(1, 0) - at(0, 1)) * s;
+    q[0] = (at(0, 2) + at(2, 0)) * s;
+    q[1] = (at(1, 2) + at(2, 1)) * s;
+  }
 }
 
 // Phase executor: run(f) calls f(lane) for every thread of the workgroup and
@@ -292,9 +400,10 @@ struct HostExec {
 // Gauss-Jordan on the column-major nr x nc matrix A (ld nr) without pivoting
 // (the left nr x nr block is SPD): one column per lane (lane < nc), one pivot
 // per phase; the left block's pivot column is only read in its step. Returns
-// false if a pivot is not positive.
-// Runs on wave 0 (nc <= 64 columns) between wave-level fences; the caller's
-// preceding phase must have ended in a workgroup barrier.
+// false if a pivot is not positive. Columns beyond 64 are taken by the same
+// lanes in a second pass of each pivot step.
+// Runs on wave 0 between wave-level fences; the caller's preceding phase must
+// have ended in a workgroup barrier.
 template <class X>
 MB_HD __attribute__((noinline)) bool gauss_jordan(const X& ex, double* A, int nr, int nc, int* flag) {
   ex.run_w0([&](int lane) {
@@ -306,10 +415,14 @@ MB_HD __attribute__((noinline)) bool gauss_jordan(const X& ex, double* A, int nr
       const double piv = A[(int64_t)k * nr + k];
       if (!(piv > 0.)) {
         if (lane == 0) *flag = 1;
-      } else if (lane < nc && lane > k) {
+        return;
+      }
+#pragma unroll 1
+      for (int cc = lane; cc < nc; cc += 64) {
+        if (cc <= k) continue;
         // pivot column and own column in chunks of 8 rows through registers
         // (independent loads, then the updates): no LDS round trip per row
-        double* col = A + (int64_t)lane * nr;
+        double* col = A + (int64_t)cc * nr;
         const double* pc = A + (int64_t)k * nr;
         const double akc = col[k] / piv;
 #pragma unroll 1
@@ -332,7 +445,7 @@ MB_HD __attribute__((noinline)) bool gauss_jordan(const X& ex, double* A, int nr
   return *flag == 0;
 }
 
-// ---- dual numbers for the log6 Jacobian -----------------------------------
+// ---- dual numbers for the exp6 / log6 Jacobians ----------------------------
 struct Dual {
   double v, d;
   Dual() = default;
@@ -432,187 +545,122 @@ MB_HD inline void log6_t(const T* R, const T* p, T* out) {
   }
 }
 
-// Cost records
-struct CRec {
-  const double* r;
-  MB_HD int type() const { return (int)r[0]; }
-  MB_HD double weight() const { return r[1]; }
-  MB_HD int size() const { return (int)r[3]; }
-  MB_HD const double* d() const { return r + kCHdr; }
-};
-
-// oMf of a frame record d = [joint, R 9, p 3, ...]; VT: any values type with oR(i), op(i)
-template <class VT>
-MB_HD inline void frame_placement(const VT& V, const double* d, double* R, double* p) {
-  const int j = (int)d[0];
-  matmul3(V.oR(j), d + 1, R);
-  matvec3(V.oR(j), d + 10, p);
-  p[0] += V.op(j)[0];
-  p[1] += V.op(j)[1];
-  p[2] += V.op(j)[2];
-}
-
-// Residual of a frame cost (and, with jcol >= 0, its Jacobian column d r / d q_jcol).
-// Returns the residual size (6 placement, 3 translation).
-MB_HD inline int frame_residual(const Blk& b, const Vals& V, const CRec& C, int jcol, double* r, double* Jc) {
-  const double* d = C.d();
-  double Rf[9], pf[3];
-  frame_placement(V, d, Rf, pf);
-  double dR[9] = {0., 0., 0., 0., 0., 0., 0., 0., 0.}, dp[3] = {0., 0., 0.};
-  bool sup = false;
-  if (jcol >= 0) {  // is jcol an ancestor-or-self of the frame's joint?
-    for (int i = (int)d[0]; i >= 0; i = JRec(b, i).parent())
-      if (i == jcol) {
-        sup = true;
-        break;
-      }
-    if (sup) {  // world axis w, velocity of the frame origin w x (op_f - op_j)
-      double w[3], dd[3], vl[3];
-      matvec3(V.oR(jcol), JRec(b, jcol).axis(), w);
-      dd[0] = pf[0] - V.op(jcol)[0];
-      dd[1] = pf[1] - V.op(jcol)[1];
-      dd[2] = pf[2] - V.op(jcol)[2];
-      cross3(w, dd, vl);
-      dp[0] = vl[0];
-      dp[1] = vl[1];
-      dp[2] = vl[2];
-      // dR = R_f [xi_ang]x with xi_ang = R_f^T w, i.e. [w]x R_f
-      for (int c = 0; c < 3; ++c) {
-        const double* Rc = Rf + 3 * c;
-        double t[3];
-        cross3(w, Rc, t);
-        dR[3 * c] = t[0];
-        dR[3 * c + 1] = t[1];
-        dR[3 * c + 2] = t[2];
-      }
-    }
-  }
-  if (C.type() == C_FRAME_TRANSLATION || C.type() == C_CONTACT_3D) {
-    const double* pref = d + 13;
-    for (int e = 0; e < 3; ++e) {
-      r[e] = pf[e] - pref[e];
-      if (Jc) Jc[e] = dp[e];
-    }
-    for (int e = 3; e < 6; ++e) {
-      r[e] = 0.;
-      if (Jc) Jc[e] = 0.;
-    }
-    return 3;
-  }
-  // rMf = Mref^-1 oMf
-  const double* Rri = d + 13;
-  const double* pri = d + 22;
-  double Rr[9], pr[3], dRr[9], dpr[3];
-  matmul3(Rri, Rf, Rr);
-  matvec3(Rri, pf, pr);
-  pr[0] += pri[0];
-  pr[1] += pri[1];
-  pr[2] += pri[2];
-  matmul3(Rri, dR, dRr);
-  matvec3(Rri, dp, dpr);
-  Dual RD[9], PD[3], o[6];
-  for (int e = 0; e < 9; ++e) RD[e] = Dual{Rr[e], dRr[e]};
-  for (int e = 0; e < 3; ++e) PD[e] = Dual{pr[e], dpr[e]};
-  log6_t<Dual>(RD, PD, o);
-  for (int e = 0; e < 6; ++e) {
-    r[e] = o[e].v;
-    if (Jc) Jc[e] = sup ? o[e].d : 0.;
-  }
-  return 6;
-}
-
-// Residual size of a cost record, and its activation weights (the last nr
-// doubles of the record).
-MB_HD inline int cost_nr(const CRec& C, int nx, int nu) {
-  const int t = C.type();
-  if (t == C_CONTACT_FORCE) return (int)C.d()[1];
-  return t == C_STATE ? nx : (t == C_CONTROL ? nu : (t == C_FRAME_PLACEMENT ? 6 : 3));
-}
-MB_HD inline const double* cost_weights(const CRec& C, int nx, int nu) { return C.r + C.size() - cost_nr(C, nx, nu); }
-// 0.5 r^T W r of a contact-force cost, r = lambda[row0 .. row0 + nr) - fref
-// (contact-force.hxx:33-50: jMf.actInv(f) is the multiplier itself).
-MB_HD inline double force_cost_activation(const CRec& C, const double* lam, int nx, int nu) {
-  const double* d = C.d();
-  const int row0 = (int)d[0], nr = (int)d[1];
-  const double* w = cost_weights(C, nx, nu);
-  double a = 0.;
-  for (int e = 0; e < nr; ++e) {
-    const double r = lam[row0 + e] - d[2 + e];
-    a += w[e] * r * r;
-  }
-  return 0.5 * a;
-}
-
-// Residual of a frame cost, value only (calc). Returns the residual size.
-template <class VT>
-MB_HD __forceinline__ int frame_residual_value(const VT& V, const CRec& C, double* r) {
-  const double* d = C.d();
-  double Rf[9], pf[3];
-  frame_placement(V, d, Rf, pf);
-  if (C.type() == C_FRAME_TRANSLATION || C.type() == C_CONTACT_3D) {
-    for (int e = 0; e < 3; ++e) r[e] = pf[e] - d[13 + e];
-    return 3;
-  }
-  double Rr[9], pr[3];
-  matmul3(d + 13, Rf, Rr);
-  matvec3(d + 13, pf, pr);
-  for (int e = 0; e < 3; ++e) pr[e] += d[22 + e];
-  log6_t<double>(Rr, pr, r);
-  return 6;
-}
-
-// 0.5 r^T W r of one cost record (kinematics in V).
-template <class VT>
-MB_HD __forceinline__ double cost_activation(const VT& V, const CRec& C, const double* x, const double* u, int nx, int nu) {
-  const double* w = cost_weights(C, nx, nu);
-  double a = 0.;
-  if (C.type() == C_STATE) {
-    for (int i = 0; i < nx; ++i) {
-      const double r = x[i] - C.d()[i];
-      a += w[i] * r * r;
-    }
-  } else if (C.type() == C_CONTROL) {
-    for (int i = 0; i < nu; ++i) {
-      const double r = u[i] - C.d()[i];
-      a += w[i] * r * r;
-    }
-  } else if (C.type() == C_CONTACT_FORCE) {
-    return 0.;  // needs the multipliers: added after the contact solve
+// exp6(nu) -> (R, p) (pinocchio::exp6): R = cos t I + (1 - cos t)/t^2 w w^T +
+// sin t / t [w]x, p = sin t / t v + (1 - sin t / t)/t^2 (w.v) w + (1 - cos t)/t^2 w x v,
+// Taylor branch for t^2 < 1e-8 (as oracle/multibody_np.py:exp6). T = double or Dual.
+template <class T>
+MB_HD inline void exp6_t(const T* nu, T* R, T* p) {
+  const T* v = nu;
+  const T* w = nu + 3;
+  const T t2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+  T ct, st_t, a_wxv, a_w;
+  if (mval(t2) < 1e-8) {
+    ct = T(1.) - 0.5 * t2 + (1. / 24.) * (t2 * t2);
+    st_t = T(1.) - (1. / 6.) * t2 + (1. / 120.) * (t2 * t2);
+    a_wxv = T(0.5) - (1. / 24.) * t2 + (1. / 720.) * (t2 * t2);
+    a_w = T(1. / 6.) - (1. / 120.) * t2 + (1. / 5040.) * (t2 * t2);
   } else {
-    double r[6] = {0., 0., 0., 0., 0., 0.};
-    const int nr = frame_residual_value(V, C, r);
-#pragma unroll
-    for (int i = 0; i < 6; ++i)  // fixed trip count: r stays in registers
-      if (i < nr) a += w[i] * r[i] * r[i];
+    const T t = msqrt(t2);
+    ct = mcos(t);
+    st_t = msin(t) / t;
+    a_wxv = (T(1.) - ct) / t2;
+    a_w = (T(1.) - st_t) / t2;
   }
-  return 0.5 * a;
+  // column-major R[c*3 + r] = ct d_rc + a_wxv w_r w_c + st_t [w]x(r, c)
+  R[0] = ct + a_wxv * (w[0] * w[0]);
+  R[1] = a_wxv * (w[1] * w[0]) + st_t * w[2];
+  R[2] = a_wxv * (w[2] * w[0]) - st_t * w[1];
+  R[3] = a_wxv * (w[0] * w[1]) - st_t * w[2];
+  R[4] = ct + a_wxv * (w[1] * w[1]);
+  R[5] = a_wxv * (w[2] * w[1]) + st_t * w[0];
+  R[6] = a_wxv * (w[0] * w[2]) + st_t * w[1];
+  R[7] = a_wxv * (w[1] * w[2]) - st_t * w[0];
+  R[8] = ct + a_wxv * (w[2] * w[2]);
+  const T wv = w[0] * v[0] + w[1] * v[1] + w[2] * v[2];
+  const T wxv[3] = {w[1] * v[2] - w[2] * v[1], w[2] * v[0] - w[0] * v[2], w[0] * v[1] - w[1] * v[0]};
+  for (int e = 0; e < 3; ++e) p[e] = st_t * v[e] + a_w * wv * w[e] + a_wxv * wxv[e];
 }
 
-// Cost value of the DAM (one thread; kinematics in V): sum of weight * 0.5 r^T W r
-// in record (name) order (cost-sum.hxx:89-117).
-template <class VT>
-MB_HD inline double cost_value(const Blk& b, const VT& V, const double* x, const double* u, int nx, int nu) {
-  double total = 0.;
-  const double* cr = b.C;
-  for (int k = 0; k < b.ncost; ++k) {
-    const CRec C{cr};
-    total += C.weight() * cost_activation(V, C, x, u, nx, nu);
-    cr += C.size();
+// pinocchio SpecialEuclideanOperationTpl<3>::integrate: M1 = M0 exp6(dq); the
+// quaternion re-extracted from M1's rotation, flipped into q0's hemisphere and
+// first-order normalised. q7 = (p, quat xyzw); out may not alias q7.
+MB_HD inline void ff_integrate(const double* q7, const double* dq, double* out) {
+  double R0[9], Re[9], pe[3], R1[9], t[3];
+  quat_to_R(q7 + 3, R0);
+  exp6_t<double>(dq, Re, pe);
+  matmul3(R0, Re, R1);
+  matvec3(R0, pe, t);
+  out[0] = q7[0] + t[0];
+  out[1] = q7[1] + t[1];
+  out[2] = q7[2] + t[2];
+  double qn[4];
+  R_to_quat(R1, qn);
+  const double dd = qn[0] * q7[3] + qn[1] * q7[4] + qn[2] * q7[5] + qn[3] * q7[6];
+  const double sg = dd < 0. ? -1. : 1.;
+  const double n2 = qn[0] * qn[0] + qn[1] * qn[1] + qn[2] * qn[2] + qn[3] * qn[3];
+  const double al = sg * (3. - n2) * 0.5;
+  for (int e = 0; e < 4; ++e) out[3 + e] = qn[e] * al;
+}
+// pinocchio SpecialEuclideanOperationTpl<3>::difference: log6(M0^-1 M1).
+MB_HD inline void ff_difference(const double* q0, const double* q1, double* out) {
+  double R0[9], R1[9], Rr[9], dp[3], pr[3];
+  quat_to_R(q0 + 3, R0);
+  quat_to_R(q1 + 3, R1);
+  matTmul3(R0, R1, Rr);
+  dp[0] = q1[0] - q0[0];
+  dp[1] = q1[1] - q0[1];
+  dp[2] = q1[2] - q0[2];
+  matTvec3(R0, dp, pr);
+  log6_t<double>(Rr, pr, out);
+}
+// column k of Jexp6(nu) (pinocchio Jexp6, the right Jacobian: exp6(nu + e eps)
+// = exp6(nu) exp6(J e eps)): the twist of exp6(nu)^-1 d exp6(nu + eps e_k).
+MB_HD inline void jexp6_col(const double* nu, int k, double* col) {
+  Dual n[6], R[9], p[3];
+  for (int e = 0; e < 6; ++e) n[e] = Dual{nu[e], e == k ? 1. : 0.};
+  exp6_t<Dual>(n, R, p);
+  double Rv[9], dR[9], dp[3], Om[9];
+  for (int e = 0; e < 9; ++e) {
+    Rv[e] = R[e].v;
+    dR[e] = R[e].d;
   }
-  return total;
+  for (int e = 0; e < 3; ++e) dp[e] = p[e].d;
+  matTvec3(Rv, dp, col);
+  matTmul3(Rv, dR, Om);  // [xi_ang]x
+  col[3] = Om[5];        // (2,1)
+  col[4] = Om[6];        // (0,2)
+  col[5] = Om[1];        // (1,0)
+}
+// column k of Jlog6(M) (pinocchio Jlog6: log6(M exp6(e eps)) = log6(M) + J e eps)
+MB_HD inline void jlog6_col(const double* R, const double* p, int k, double* col) {
+  double xi[6] = {0., 0., 0., 0., 0., 0.};
+  xi[k] = 1.;
+  double dR[9], dp[3];
+  for (int c = 0; c < 3; ++c) {  // dR = R [xi_ang]x
+    double t[3];
+    const double e[3] = {c == 0 ? 1. : 0., c == 1 ? 1. : 0., c == 2 ? 1. : 0.};
+    cross3(xi + 3, e, t);
+    matvec3(R, t, dR + 3 * c);
+  }
+  matvec3(R, xi, dp);
+  Dual RD[9], PD[3], o[6];
+  for (int e = 0; e < 9; ++e) RD[e] = Dual{R[e], dR[e]};
+  for (int e = 0; e < 3; ++e) PD[e] = Dual{p[e], dp[e]};
+  log6_t<Dual>(RD, PD, o);
+  for (int e = 0; e < 6; ++e) col[e] = o[e].d;
 }
 
 // ---------------------------------------------------------------------------
-// World-frame dynamics (the calc path). Spatial quantities are expressed at
-// the world origin in world axes, so every recursion of RNEA/CRBA becomes a
-// sum over the ancestors or the subtree of a joint
-//   v_i = sum_{k <= i} S_k qd_k,  a_i = -g + sum_{k <= i} (S_k qdd_k + v_k x S_k qd_k),
-//   tau_i = S_i . sum_{k in subtree(i)} f_k,  Ic_i = sum_{k in subtree(i)} I_k,
-//   M_ij = S_i . (Ic_j S_j)  (i ancestor of j),
-// which each lane evaluates for its own joint: no serial chain through LDS.
-// The placements oMi = oMparent * liMi are composed by pointer jumping
-// (ceil(log2 nj) rounds). Same functions as the local-frame value_pass,
-// rounded differently (tests/test_multibody_host.py checks both vs the oracle).
+// World-frame values. Spatial quantities are expressed at the world origin in
+// world axes, so every recursion of RNEA/CRBA becomes a sum over the ancestors or
+// the subtree of a dof
+//   v_i = sum_{k in anc(i)} S_k qd_k,  a_i = -g + sum_{k in anc(i)} (S_k qdd_k + v_k x S_k qd_k),
+//   tau_i = S_i . sum_{k in sub(i)} f_k,  Ic_i = sum_{k in sub(i)} I_k,
+//   M_ij = S_i . (Ic_j S_j)  (i in anc(j)),
+// which each lane evaluates for its own dof: no serial chain through LDS.
+// anc(i) holds every dof of the ancestor-or-self bodies (all six free-flyer
+// dofs for the base), so v_k is the full body velocity. The placements
+// oMi = oMparent * liMi are composed by pointer jumping (ceil(log2 nj) rounds).
 // ---------------------------------------------------------------------------
 constexpr int kWPerJoint = 96;
 constexpr int kMaxCosts = 64;
@@ -623,8 +671,8 @@ struct WVals {
   MB_HD double* p(int i) const { return R(i) + 9; }
   MB_HD double* oR(int i) const { return R(i) + 12; }  // oMi (also pointer-jumping buffer A)
   MB_HD double* op(int i) const { return R(i) + 21; }
-  MB_HD double* S(int i) const { return R(i) + 24; }   // joint motion subspace (world)
-  MB_HD double* m(int i) const { return R(i) + 30; }   // body mass
+  MB_HD double* S(int i) const { return R(i) + 24; }   // dof motion subspace (world)
+  MB_HD double* m(int i) const { return R(i) + 30; }   // body mass (0 on the massless free-flyer dofs)
   MB_HD double* c(int i) const { return R(i) + 31; }   // body CoM (world)
   MB_HD double* Ic(int i) const { return R(i) + 34; }  // body inertia about its CoM, world axes (6)
   MB_HD double* v(int i) const { return R(i) + 40; }
@@ -639,9 +687,9 @@ struct WVals {
   MB_HD double* jA(int i) const { return R(i) + 86; }  // jump targets of buffers A / B
   MB_HD double* jB(int i) const { return R(i) + 87; }
   MB_HD double* fb(int i) const { return R(i) + 90; }  // body force I a + v x* I v
-  MB_HD unsigned* anc(int i) const { return (unsigned*)(base + kWPerJoint * nj) + i; }  // ancestors-or-self bits
-  MB_HD double* root_a() const { return base + kWPerJoint * nj + (nj + 1) / 2 + 1; }
-  MB_HD static int64_t doubles(int nj) { return (int64_t)kWPerJoint * nj + (nj + 1) / 2 + 1 + 6; }
+  MB_HD Mask* anc(int i) const { return (Mask*)(base + kWPerJoint * nj) + i; }  // ancestors-or-self dofs
+  MB_HD double* root_a() const { return base + kWPerJoint * nj + nj; }
+  MB_HD static int64_t doubles(int nj) { return (int64_t)kWPerJoint * nj + nj + 6; }
 };
 
 MB_HD inline int jump_rounds(int nj) {
@@ -650,32 +698,42 @@ MB_HD inline int jump_rounds(int nj) {
   return r;
 }
 
-MB_HD __forceinline__ double dot6(const double* a, const double* b) {
-  return a[0] * b[0] + a[1] * b[1] + a[2] * b[2] + a[3] * b[3] + a[4] * b[4] + a[5] * b[5];
-}
-
 // lane i < nj: local placement (buffer A starts as liMi), ancestor bits.
 MB_HD inline void w_joint_local(const Blk& b, const WVals& W, const double* q, int i) {
-  const JRec J(b, i);
-  double ax[3], Rpl[9], R[9];
-  for (int e = 0; e < 3; ++e) ax[e] = J.axis()[e];
-  for (int e = 0; e < 9; ++e) Rpl[e] = J.Rpl()[e];
-  joint_rotation(Rpl, ax, q[i], R);
+  double R[9], p[3];
+  if (b.ff && i < 6) {
+    if (i == 0) {  // base pose: root placement * (R(quat), p)
+      const JRec J(b, 0);
+      double Rq[9], t[3];
+      quat_to_R(q + 3, Rq);
+      matmul3(J.Rpl(), Rq, R);
+      matvec3(J.Rpl(), q, t);
+      for (int e = 0; e < 3; ++e) p[e] = J.ppl()[e] + t[e];
+    } else {
+      for (int e = 0; e < 9; ++e) R[e] = (e % 4 == 0) ? 1. : 0.;
+      for (int e = 0; e < 3; ++e) p[e] = 0.;
+    }
+  } else {
+    const JRec J(b, rec_of(b, i));
+    double ax[3], Rpl[9];
+    for (int e = 0; e < 3; ++e) ax[e] = J.axis()[e];
+    for (int e = 0; e < 9; ++e) Rpl[e] = J.Rpl()[e];
+    joint_rotation(Rpl, ax, q[qof(b, i)], R);
+    for (int e = 0; e < 3; ++e) p[e] = J.ppl()[e];
+  }
   for (int e = 0; e < 9; ++e) {
     W.R(i)[e] = R[e];
     W.oR(i)[e] = R[e];
   }
   for (int e = 0; e < 3; ++e) {
-    W.p(i)[e] = J.ppl()[e];
-    W.op(i)[e] = J.ppl()[e];
+    W.p(i)[e] = p[e];
+    W.op(i)[e] = p[e];
   }
-  *W.jA(i) = (double)J.parent();
+  *W.jA(i) = (double)chain_parent(b, i);
   if (i == 0) {
     for (int e = 0; e < 6; ++e) W.root_a()[e] = e < 3 ? -b.g[e] : 0.;
   }
-  unsigned m = 1u << i;
-  for (int k = J.parent(); k >= 0; k = JRec(b, k).parent()) m |= 1u << k;
-  *W.anc(i) = m;
+  *W.anc(i) = anc_mask(b, i);
 }
 
 // lane i < nj, round r: T_i <- T_j(i) o T_i, j(i) <- j(j(i)) (A -> B on even
@@ -711,16 +769,37 @@ MB_HD inline void w_jump(const WVals& W, int i, int r) {
 // lane i < nj: oMi into oR/op (from buffer B after an odd number of rounds),
 // world motion subspace and body inertia.
 MB_HD inline void w_joint_world(const Blk& b, const WVals& W, int i, bool from_b) {
-  const JRec J(b, i);
-  double oR[9], op[3], w[3], vl[3], c[3], t[3];
+  double oR[9], op[3], w[3], ax[3];
   for (int e = 0; e < 9; ++e) oR[e] = from_b ? W.Rb(i)[e] : W.oR(i)[e];
   for (int e = 0; e < 3; ++e) op[e] = from_b ? W.pb(i)[e] : W.op(i)[e];
   if (from_b) {
     for (int e = 0; e < 9; ++e) W.oR(i)[e] = oR[e];
     for (int e = 0; e < 3; ++e) W.op(i)[e] = op[e];
   }
-  matvec3(oR, J.axis(), w);
-  cross3(op, w, vl);  // velocity of the world origin: w x (0 - op) = op x w
+  dof_axis(b, i, ax);
+  matvec3(oR, ax, w);
+  if (dof_prismatic(b, i)) {
+    for (int e = 0; e < 3; ++e) {
+      W.S(i)[e] = w[e];
+      W.S(i)[3 + e] = 0.;
+    }
+  } else {
+    double vl[3];
+    cross3(op, w, vl);  // velocity of the world origin: w x (0 - op) = op x w
+    for (int e = 0; e < 3; ++e) {
+      W.S(i)[e] = vl[e];
+      W.S(i)[3 + e] = w[e];
+    }
+  }
+  double* o = W.Ic(i);
+  if (!carries_body(b, i)) {
+    *W.m(i) = 0.;
+    for (int e = 0; e < 3; ++e) W.c(i)[e] = op[e];
+    for (int e = 0; e < 6; ++e) o[e] = 0.;
+    return;
+  }
+  const JRec J(b, rec_of(b, i));
+  double c[3], t[3];
   matvec3(oR, J.com(), t);
   for (int e = 0; e < 3; ++e) c[e] = op[e] + t[e];
   // Ic_w = oR Ic oR^T
@@ -730,13 +809,8 @@ MB_HD inline void w_joint_world(const Blk& b, const WVals& W, int i, bool from_b
   matmul3(oR, Is, tmp);
   for (int r = 0; r < 3; ++r)
     for (int cc = 0; cc < 3; ++cc) Iw[cc * 3 + r] = tmp[r] * oR[cc] + tmp[3 + r] * oR[3 + cc] + tmp[6 + r] * oR[6 + cc];
-  for (int e = 0; e < 3; ++e) {
-    W.S(i)[e] = vl[e];
-    W.S(i)[3 + e] = w[e];
-    W.c(i)[e] = c[e];
-  }
+  for (int e = 0; e < 3; ++e) W.c(i)[e] = c[e];
   *W.m(i) = J.mass();
-  double* o = W.Ic(i);
   o[0] = Iw[0];
   o[1] = Iw[4];
   o[2] = Iw[8];
@@ -749,8 +823,8 @@ MB_HD inline void w_joint_world(const Blk& b, const WVals& W, int i, bool from_b
 // (m, h = m c, I_O = Ic + m (|c|^2 I - c c^T)): additive over the subtree.
 MB_HD inline void w_composite(const Blk& b, const WVals& W, int i) {
   double m = 0., h[3] = {0., 0., 0.}, I[6] = {0., 0., 0., 0., 0., 0.};
-  for (int k = i; k < b.nj; ++k) {
-    if (!((*W.anc(k) >> i) & 1u)) continue;
+  for (int k = 0; k < b.nj; ++k) {
+    if (!((*W.anc(k) >> i) & 1ull) || !carries_body(b, k)) continue;
     const double mk = *W.m(k);
     double c[3], Ic[6];
     for (int e = 0; e < 3; ++e) c[e] = W.c(k)[e];
@@ -770,12 +844,26 @@ MB_HD inline void w_composite(const Blk& b, const WVals& W, int i) {
   for (int e = 0; e < 6; ++e) W.cI(i)[e] = I[e];
 }
 
+// composite inertia of dof i's subtree times a motion x: (m v - h x w, I_O w + h x v)
+MB_HD __forceinline__ void comp_mul(const WVals& W, int i, const double* x, double* o) {
+  const double m = *W.cm(i);
+  const double* h = W.ch(i);
+  const double* I = W.cI(i);
+  double t[3];
+  cross3(h, x + 3, t);
+  for (int e = 0; e < 3; ++e) o[e] = m * x[e] - t[e];
+  cross3(h, x, t);
+  o[3] = I[0] * x[3] + I[3] * x[4] + I[4] * x[5] + t[0];
+  o[4] = I[3] * x[3] + I[1] * x[4] + I[5] * x[5] + t[1];
+  o[5] = I[4] * x[3] + I[5] * x[4] + I[2] * x[5] + t[2];
+}
+
 // lane i < nj: v_i = sum over ancestors-or-self of S_k qd_k
 MB_HD inline void w_velocity(const WVals& W, const double* qd, int i) {
   double v[6] = {0., 0., 0., 0., 0., 0.};
-  const unsigned am = *W.anc(i);
-  for (int k = 0; k <= i; ++k) {
-    if (!((am >> k) & 1u)) continue;
+  const Mask am = *W.anc(i);
+  for (int k = 0; k < W.nj; ++k) {
+    if (!((am >> k) & 1ull)) continue;
     const double w = qd[k];
     for (int e = 0; e < 6; ++e) v[e] += W.S(k)[e] * w;
   }
@@ -796,13 +884,13 @@ MB_HD inline void w_accel_term(const WVals& W, const double* qd, const double* q
 }
 
 // lane i < nj: a_i = -g + sum over ancestors-or-self of cq_k, then the body
-// force f_i = I_i a_i + v_i x* (I_i v_i)
+// force f_i = I_i a_i + v_i x* (I_i v_i) - fext_i
 MB_HD inline void w_accel_force(const WVals& W, int i, const double* fx = nullptr) {
   double a[6];
   for (int e = 0; e < 6; ++e) a[e] = W.root_a()[e];
-  const unsigned am = *W.anc(i);
-  for (int k = 0; k <= i; ++k) {
-    if (!((am >> k) & 1u)) continue;
+  const Mask am = *W.anc(i);
+  for (int k = 0; k < W.nj; ++k) {
+    if (!((am >> k) & 1ull)) continue;
     for (int e = 0; e < 6; ++e) a[e] += W.cq(k)[e];
   }
   double v[6], f[6], Iv[6], t6[6], c[3], I6[6];
@@ -822,8 +910,8 @@ MB_HD inline void w_accel_force(const WVals& W, int i, const double* fx = nullpt
 // lane i < nj: F_i = sum over the subtree of the body forces, tau_i = S_i . F_i
 MB_HD inline void w_joint_force(const Blk& b, const WVals& W, double* tau, int i) {
   double F[6] = {0., 0., 0., 0., 0., 0.};
-  for (int k = i; k < b.nj; ++k) {
-    if (!((*W.anc(k) >> i) & 1u)) continue;
+  for (int k = 0; k < b.nj; ++k) {
+    if (!((*W.anc(k) >> i) & 1ull)) continue;
     for (int e = 0; e < 6; ++e) F[e] += W.fb(k)[e];
   }
   for (int e = 0; e < 6; ++e) W.F(i)[e] = F[e];
@@ -831,28 +919,236 @@ MB_HD inline void w_joint_force(const Blk& b, const WVals& W, double* tau, int i
 }
 
 // lane j < nj: CRBA column j in world frame: F = Ic_j S_j, M_ij = S_i . F for
-// the ancestors-or-self i of j (+ armature on the diagonal). A: ld lda, zeroed.
+// the ancestors-or-self i < j of j (+ armature on the diagonal). A: ld lda, zeroed.
 MB_HD inline void w_crba_column(const Blk& b, const WVals& W, int j, double* A, int lda) {
-  double S[6], F[6], t[3];
-  for (int e = 0; e < 6; ++e) S[e] = W.S(j)[e];
-  const double m = *W.cm(j);
-  const double* h = W.ch(j);
-  const double* I = W.cI(j);
-  // (m v - h x w, I_O w + h x v)
-  cross3(h, S + 3, t);
-  for (int e = 0; e < 3; ++e) F[e] = m * S[e] - t[e];
-  cross3(h, S, t);
-  F[3] = I[0] * S[3] + I[3] * S[4] + I[4] * S[5] + t[0];
-  F[4] = I[3] * S[3] + I[1] * S[4] + I[5] * S[5] + t[1];
-  F[5] = I[4] * S[3] + I[5] * S[4] + I[2] * S[5] + t[2];
-  A[(int64_t)j * lda + j] = dot6(S, F) + b.arm[j];
-  const unsigned am = *W.anc(j);
+  double F[6];
+  comp_mul(W, j, W.S(j), F);
+  A[(int64_t)j * lda + j] = dot6(W.S(j), F) + b.arm[j];
+  const Mask am = *W.anc(j);
   for (int i = 0; i < j; ++i) {
-    if (!((am >> i) & 1u)) continue;
+    if (!((am >> i) & 1ull)) continue;
     const double Mij = dot6(W.S(i), F);
     A[(int64_t)j * lda + i] = Mij;
     A[(int64_t)i * lda + j] = Mij;
   }
+}
+
+// Cost records
+struct CRec {
+  const double* r;
+  MB_HD int type() const { return (int)r[0]; }
+  MB_HD double weight() const { return r[1]; }
+  MB_HD int size() const { return (int)r[3]; }
+  MB_HD const double* d() const { return r + kCHdr; }
+};
+
+// dof carrying the frame of a frame / contact payload d = [joint record, R 9, p 3, ...]
+MB_HD __forceinline__ int frame_dof(const Blk& b, const double* d) { return dof_of_rec(b, (int)d[0]); }
+
+// oMf of a frame payload
+MB_HD inline void frame_placement(const Blk& b, const WVals& V, const double* d, double* R, double* p) {
+  const int j = frame_dof(b, d);
+  matmul3(V.oR(j), d + 1, R);
+  matvec3(V.oR(j), d + 10, p);
+  p[0] += V.op(j)[0];
+  p[1] += V.op(j)[1];
+  p[2] += V.op(j)[2];
+}
+
+// Residual of a frame cost and, with S != null (the world motion of a dof that
+// moves the frame), its Jacobian column. Returns the residual size (6 placement,
+// 3 translation).
+MB_HD inline int frame_residual(const Blk& b, const WVals& V, const CRec& C, const double* S, double* r, double* Jc) {
+  const double* d = C.d();
+  double Rf[9], pf[3];
+  frame_placement(b, V, d, Rf, pf);
+  double dR[9] = {0., 0., 0., 0., 0., 0., 0., 0., 0.}, dp[3] = {0., 0., 0.};
+  if (S) {  // motion of oMf under S: dp = S_lin + S_ang x pf, dR = [S_ang]x Rf
+    double t[3];
+    cross3(S + 3, pf, t);
+    for (int e = 0; e < 3; ++e) dp[e] = S[e] + t[e];
+    for (int c = 0; c < 3; ++c) cross3(S + 3, Rf + 3 * c, dR + 3 * c);
+  }
+  if (C.type() == C_FRAME_TRANSLATION || C.type() == C_CONTACT_3D) {
+    const double* pref = d + 13;
+    for (int e = 0; e < 3; ++e) {
+      r[e] = pf[e] - pref[e];
+      if (Jc) Jc[e] = dp[e];
+    }
+    for (int e = 3; e < 6; ++e) {
+      r[e] = 0.;
+      if (Jc) Jc[e] = 0.;
+    }
+    return 3;
+  }
+  // rMf = Mref^-1 oMf
+  const double* Rri = d + 13;
+  const double* pri = d + 22;
+  double Rr[9], pr[3], dRr[9], dpr[3];
+  matmul3(Rri, Rf, Rr);
+  matvec3(Rri, pf, pr);
+  pr[0] += pri[0];
+  pr[1] += pri[1];
+  pr[2] += pri[2];
+  matmul3(Rri, dR, dRr);
+  matvec3(Rri, dp, dpr);
+  Dual RD[9], PD[3], o[6];
+  for (int e = 0; e < 9; ++e) RD[e] = Dual{Rr[e], dRr[e]};
+  for (int e = 0; e < 3; ++e) PD[e] = Dual{pr[e], dpr[e]};
+  log6_t<Dual>(RD, PD, o);
+  for (int e = 0; e < 6; ++e) {
+    r[e] = o[e].v;
+    if (Jc) Jc[e] = S ? o[e].d : 0.;
+  }
+  return 6;
+}
+
+// Residual size of a cost record, and its activation weights (the last nr
+// doubles of the record).
+MB_HD inline int cost_nr(const Blk& b, const CRec& C, int nu) {
+  const int t = C.type();
+  if (t == C_CONTACT_FORCE) return (int)C.d()[1];
+  if (t == C_STATE) return 2 * b.nj;
+  if (t == C_CONTROL) return nu;
+  return t == C_FRAME_PLACEMENT ? 6 : 3;
+}
+MB_HD inline const double* cost_weights(const Blk& b, const CRec& C, int nu) {
+  return C.r + C.size() - cost_nr(b, C, nu);
+}
+// costs whose residual Jacobian is dense over the configuration tangent (stored
+// per cost: rows x nj): frame costs, CoM, and the free-flyer block of a state cost
+MB_HD __forceinline__ bool jac_cost(const Blk& b, int type) {
+  return type == C_FRAME_PLACEMENT || type == C_FRAME_TRANSLATION || type == C_COM_POSITION ||
+         (type == C_STATE && b.ff);
+}
+MB_HD __forceinline__ int jac_rows(int type) {
+  return (type == C_FRAME_TRANSLATION || type == C_COM_POSITION) ? 3 : 6;
+}
+MB_HD inline int count_jac_costs(const Blk& b) {
+  int n = 0;
+  const double* cr = b.C;
+  for (int k = 0; k < b.ncost; ++k) {
+    const CRec C{cr};
+    if (jac_cost(b, C.type())) ++n;
+    cr += C.size();
+  }
+  return n;
+}
+
+// 0.5 r^T W r of a contact-force cost, r = lambda[row0 .. row0 + nr) - fref
+// (contact-force.hxx:33-50: jMf.actInv(f) is the multiplier itself); an
+// inactive contact has lambda = 0.
+MB_HD inline double force_cost_activation(const Blk& b, const CRec& C, const double* lam, int nu) {
+  const double* d = C.d();
+  const int row0 = (int)d[0], nr = (int)d[1];
+  const double* w = cost_weights(b, C, nu);
+  double a = 0.;
+  for (int e = 0; e < nr; ++e) {
+    const double r = (row0 >= 0 ? lam[row0 + e] : 0.) - d[2 + e];
+    a += w[e] * r * r;
+  }
+  return 0.5 * a;
+}
+
+// Residual of a frame cost, value only (calc). Returns the residual size.
+MB_HD __forceinline__ int frame_residual_value(const Blk& b, const WVals& V, const CRec& C, double* r) {
+  const double* d = C.d();
+  double Rf[9], pf[3];
+  frame_placement(b, V, d, Rf, pf);
+  if (C.type() == C_FRAME_TRANSLATION || C.type() == C_CONTACT_3D) {
+    for (int e = 0; e < 3; ++e) r[e] = pf[e] - d[13 + e];
+    return 3;
+  }
+  double Rr[9], pr[3];
+  matmul3(d + 13, Rf, Rr);
+  matvec3(d + 13, pf, pr);
+  for (int e = 0; e < 3; ++e) pr[e] += d[22 + e];
+  log6_t<double>(Rr, pr, r);
+  return 6;
+}
+
+// Centre of mass (pinocchio::centerOfMass) from the world body CoMs
+MB_HD inline void com_value(const Blk& b, const WVals& W, double* c) {
+  double m = 0., h[3] = {0., 0., 0.};
+  for (int k = 0; k < b.nj; ++k) {
+    if (!carries_body(b, k)) continue;
+    const double mk = *W.m(k);
+    m += mk;
+    for (int e = 0; e < 3; ++e) h[e] += mk * W.c(k)[e];
+  }
+  for (int e = 0; e < 3; ++e) c[e] = h[e] / m;
+}
+
+// free-flyer block of a state residual: log6(Mref^-1 M) (multibody.hxx:69)
+MB_HD inline void ff_rel(const double* xref, const double* x, double* Rr, double* pr) {
+  double R0[9], R1[9], dp[3];
+  quat_to_R(xref + 3, R0);
+  quat_to_R(x + 3, R1);
+  matTmul3(R0, R1, Rr);
+  for (int e = 0; e < 3; ++e) dp[e] = x[e] - xref[e];
+  matTvec3(R0, dp, pr);
+}
+
+// entry i of the state residual diff(xref, x) beyond the free-flyer block
+MB_HD __forceinline__ double state_res(const Blk& b, const double* xref, const double* x, int i) {
+  if (i < b.nj) return x[qof(b, i)] - xref[qof(b, i)];
+  return x[b.nq + i - b.nj] - xref[b.nq + i - b.nj];
+}
+
+// 0.5 r^T W r of one cost record (kinematics in V).
+MB_HD __forceinline__ double cost_activation(const Blk& b, const WVals& V, const CRec& C, const double* x,
+                                             const double* u, int nu) {
+  const double* w = cost_weights(b, C, nu);
+  double a = 0.;
+  if (C.type() == C_STATE) {
+    const int ndx = 2 * b.nj;
+    int i0 = 0;
+    if (b.ff) {
+      double Rr[9], pr[3], r[6];
+      ff_rel(C.d(), x, Rr, pr);
+      log6_t<double>(Rr, pr, r);
+      for (int e = 0; e < 6; ++e) a += w[e] * r[e] * r[e];
+      i0 = 6;
+    }
+    for (int i = i0; i < ndx; ++i) {
+      const double r = state_res(b, C.d(), x, i);
+      a += w[i] * r * r;
+    }
+  } else if (C.type() == C_CONTROL) {
+    for (int i = 0; i < nu; ++i) {
+      const double r = u[i] - C.d()[i];
+      a += w[i] * r * r;
+    }
+  } else if (C.type() == C_CONTACT_FORCE) {
+    return 0.;  // needs the multipliers: added after the contact solve
+  } else if (C.type() == C_COM_POSITION) {
+    double c[3];
+    com_value(b, V, c);
+    for (int i = 0; i < 3; ++i) {
+      const double r = c[i] - C.d()[i];
+      a += w[i] * r * r;
+    }
+  } else {
+    double r[6] = {0., 0., 0., 0., 0., 0.};
+    const int nr = frame_residual_value(b, V, C, r);
+#pragma unroll
+    for (int i = 0; i < 6; ++i)  // fixed trip count: r stays in registers
+      if (i < nr) a += w[i] * r[i] * r[i];
+  }
+  return 0.5 * a;
+}
+
+// Cost value of the DAM (one thread; kinematics in V): sum of weight * 0.5 r^T W r
+// in record (name) order (cost-sum.hxx:89-117).
+MB_HD inline double cost_value(const Blk& b, const WVals& V, const double* x, const double* u, int nu) {
+  double total = 0.;
+  const double* cr = b.C;
+  for (int k = 0; k < b.ncost; ++k) {
+    const CRec C{cr};
+    total += C.weight() * cost_activation(b, V, C, x, u, nu);
+    cr += C.size();
+  }
+  return total;
 }
 
 // ---- contacts (ContactModel3D / 6D in the LOCAL frame) ----------------------
@@ -868,38 +1164,23 @@ MB_HD inline const double* contact_rec(const Blk& b, int k, int* row0) {
   return r;
 }
 
-// Column c of the contact's LOCAL frame Jacobian (pinocchio getFrameJacobian
-// LOCAL, contact-3d.hxx:29 / contact-6d.hxx:29): the world motion S_c moved to
-// the frame (SE3::actInv of oMf), zero unless c supports the frame's joint.
-template <class VT>
-MB_HD inline void contact_jac_col(const VT& V, const unsigned* anc_j, const double* d, int c, const double* Sc,
-                                  double* o) {
-  if (!((*anc_j >> c) & 1u)) {
-    for (int e = 0; e < 6; ++e) o[e] = 0.;
-    return;
-  }
-  double Rf[9], pf[3];
-  frame_placement(V, d, Rf, pf);
-  motion_act_inv(Rf, pf, Sc, o);
-}
-
 // a0 of a contact (contact-3d.hxx:35-43, contact-6d.hxx:31-44) in two parts,
 // so that neither holds log6 and the frame motions live at once: the
 // Baumgarte position term kp * (p - p_ref) | kp * log6(Mref^-1 oMf) (needs only
 // the placements), then the frame drift acceleration (classical for 3D, gravity
-// removed) + kd * v from the world velocity / acceleration of the joint.
-MB_HD __attribute__((noinline)) void contact_a0_position(const WVals& W, const CRec& C, double* a0) {
+// removed) + kd * v from the world velocity / acceleration of the body.
+MB_HD __attribute__((noinline)) void contact_a0_position(const Blk& b, const WVals& W, const CRec& C, double* a0) {
   const double kp = C.r[1];
   double r[6] = {0., 0., 0., 0., 0., 0.};
-  if (kp != 0.) frame_residual_value(W, C, r);
+  if (kp != 0.) frame_residual_value(b, W, C, r);
   const int n = C.type() == C_CONTACT_3D ? 3 : 6;
   for (int e = 0; e < n; ++e) a0[e] = kp * r[e];
 }
-MB_HD __attribute__((noinline)) void contact_a0_drift(const WVals& W, const CRec& C, double* a0) {
+MB_HD __attribute__((noinline)) void contact_a0_drift(const Blk& b, const WVals& W, const CRec& C, double* a0) {
   const double* d = C.d();
-  const int j = (int)d[0];
+  const int j = frame_dof(b, d);
   double Rf[9], pf[3], m6[6], vf[6], af[6];
-  frame_placement(W, d, Rf, pf);
+  frame_placement(b, W, d, Rf, pf);
   for (int e = 0; e < 6; ++e) m6[e] = W.v(j)[e];
   motion_act_inv(Rf, pf, m6, vf);
   for (int e = 0; e < 6; ++e) m6[e] = W.a(j)[e] - W.root_a()[e];  // data.a has no gravity
@@ -916,24 +1197,24 @@ MB_HD __attribute__((noinline)) void contact_a0_drift(const WVals& W, const CRec
 
 // World force (at the origin) of contact record C for the multipliers lam
 // (updateForce: jMf.act(Force(lambda[, 0])), contact-3d.hxx:59-67).
-MB_HD inline void contact_world_force(const WVals& W, const CRec& C, const double* lam, double* o) {
+MB_HD inline void contact_world_force(const Blk& b, const WVals& W, const CRec& C, const double* lam, double* o) {
   double Rf[9], pf[3], f[6];
-  frame_placement(W, C.d(), Rf, pf);
+  frame_placement(b, W, C.d(), Rf, pf);
   const bool c3 = C.type() == C_CONTACT_3D;
   for (int e = 0; e < 6; ++e) f[e] = (c3 && e >= 3) ? 0. : lam[e];
   force_act(Rf, pf, f, o);
 }
 
-// lane j < nj: sum of the contact forces acting on joint j (world) into fx[6j..]
+// lane j < nj: sum of the contact forces acting on dof j's body (world) into fx[6j..]
 MB_HD inline void contact_joint_forces(const Blk& b, const WVals& W, const double* lam, double* fx, int j) {
   double F[6] = {0., 0., 0., 0., 0., 0.};
   const double* r = b.K;
   int row = 0;
   for (int k = 0; k < b.ncon; ++k) {
     const CRec C{r};
-    if ((int)C.d()[0] == j) {
+    if (frame_dof(b, C.d()) == j) {
       double o[6];
-      contact_world_force(W, C, lam + row, o);
+      contact_world_force(b, W, C, lam + row, o);
       for (int e = 0; e < 6; ++e) F[e] += o[e];
     }
     row += C.type() == C_CONTACT_3D ? 3 : 6;
@@ -943,7 +1224,10 @@ MB_HD inline void contact_joint_forces(const Blk& b, const WVals& W, const doubl
 }
 
 // lane c < nj: column c of the stacked contact Jacobian Jc (nc x nj,
-// Jc[row * nj + c]); with At != null also into the columns [nj + row] of A (ld nj).
+// Jc[row * nj + c]) — the LOCAL frame Jacobian (pinocchio getFrameJacobian LOCAL,
+// contact-3d.hxx:29 / contact-6d.hxx:29): the world motion S_c moved to the frame
+// (SE3::actInv of oMf), zero unless c moves the frame's body; with At != null also
+// into the columns [nj + row] of A (ld nj).
 MB_HD __attribute__((noinline)) void contact_jac_lane(const Blk& b, const WVals& W, int c, double* Jc, double* At) {
   double Sc[6];
   for (int e = 0; e < 6; ++e) Sc[e] = W.S(c)[e];
@@ -951,9 +1235,13 @@ MB_HD __attribute__((noinline)) void contact_jac_lane(const Blk& b, const WVals&
   int row = 0;
   for (int k = 0; k < b.ncon; ++k) {
     const CRec C{r};
-    const int j = (int)C.d()[0];
-    double o[6];
-    contact_jac_col(W, W.anc(j), C.d(), c, Sc, o);
+    const int j = frame_dof(b, C.d());
+    double o[6] = {0., 0., 0., 0., 0., 0.};
+    if ((*W.anc(j) >> c) & 1ull) {
+      double Rf[9], pf[3];
+      frame_placement(b, W, C.d(), Rf, pf);
+      motion_act_inv(Rf, pf, Sc, o);
+    }
     const int n = C.type() == C_CONTACT_3D ? 3 : 6;
     for (int e = 0; e < n; ++e) {
       Jc[(int64_t)(row + e) * b.nj + c] = o[e];
@@ -992,7 +1280,7 @@ MB_HD inline void world_kinematics(const X& ex, const Blk& b, const WVals& W, co
 }
 
 // Joint torques of RNEA(q, qd, qdd) (qdd == nullptr: 0) with the kinematics in W;
-// fx (6 per joint, world frame at the origin, may be null): external forces,
+// fx (6 per dof, world frame at the origin, may be null): external forces,
 // as pinocchio::rnea(model, data, q, v, a, fext).
 template <class X>
 MB_HD inline void world_rnea(const X& ex, const Blk& b, const WVals& W, const double* qd, const double* qdd,
@@ -1012,9 +1300,28 @@ MB_HD inline void world_rnea(const X& ex, const Blk& b, const WVals& W, const do
   });
 }
 
-// LDS (doubles) of the calc scratch for nj joints and nc contact rows.
+// Euler step of the state (euler.hxx:64-68 + StateMultibody::integrate): lane i < nj
+// writes v_next[i] and the configuration entries of dof i (lane 0 the free-flyer's
+// seven: M exp6(v dt + a dt^2)). a: the acceleration (every lane reads a[0..5]).
+MB_HD inline void euler_step(const Blk& b, const double* x, const double* a, double dt, double* xnext, int i) {
+  const int nq = b.nq;
+  const double v = x[nq + i], ai = a[i];
+  xnext[nq + i] = v + ai * dt;
+  if (b.ff && i < 6) {
+    if (i == 0) {
+      double dq[6];
+      for (int e = 0; e < 6; ++e) dq[e] = x[nq + e] * dt + a[e] * (dt * dt);
+      ff_integrate(x, dq, xnext);
+    }
+  } else {
+    const int qi = qof(b, i);
+    xnext[qi] = x[qi] + (v * dt + ai * dt * dt);
+  }
+}
+
+// LDS (doubles) of the calc scratch for nj dofs and nc contact rows.
 MB_HD inline int64_t calc_work_doubles(int nj, int nc = 0) {
-  return WVals::doubles(nj) + (int64_t)nj * (nj + nc + 1) + 2 * nj + kMaxCosts + 8 + (int64_t)nc * nj + nc +
+  return pad2(WVals::doubles(nj)) + (int64_t)nj * (nj + nc + 1) + 2 * nj + kMaxCosts + 8 + (int64_t)nc * nj + nc +
          (int64_t)nc * (nc + 1);
 }
 
@@ -1034,9 +1341,9 @@ MB_HD inline double knot_calc_x(const X& ex, const double* P, int nx, const doub
                                 double* xnext, double* w) {
   const Blk b = parse(P);
   const bool imp = b.impulse;  // impulse: [M | Jc^T] only, z = v
-  const int nj = b.nj, nc = b.nc, nu = nj - b.nun, ncol = imp ? nj + nc : nj + nc + 1;
+  const int nj = b.nj, nq = b.nq, nc = b.nc, nu = nj - b.nun, ncol = imp ? nj + nc : nj + nc + 1;
   const WVals W{w, nj};
-  double* A = w + WVals::doubles(nj);  // nj x (nj + nc + 1), ld nj: [M | Jc^T | tau - nle]
+  double* A = w + pad2(WVals::doubles(nj));  // nj x (nj + nc + 1), ld nj: [M | Jc^T | tau - nle]
   double* tau = A + (int64_t)nj * ncol;
   double* ub = tau + nj;  // u (zero if !use_u)
   double* cv = ub + nj;   // per-cost activations
@@ -1054,17 +1361,17 @@ MB_HD inline double knot_calc_x(const X& ex, const double* P, int nx, const doub
     const double* cr = b.C;
     for (int k = 0; k < b.ncost; ++k) {
       const CRec C{cr};
-      if (wave == 2 + (k & 1) && l == (k >> 1)) cv[k] = C.weight() * cost_activation(W, C, x, ub, nx, nu);
+      if (wave == 2 + (k & 1) && l == (k >> 1)) cv[k] = C.weight() * cost_activation(b, W, C, x, ub, nu);
       cr += C.size();
     }
     const int kc = l - 32;  // contact position terms on the upper half of wave 2
     if (!imp && wave == 2 && kc >= 0 && kc < b.ncon) {
       int row0;
       const CRec C{contact_rec(b, kc, &row0)};
-      contact_a0_position(W, C, a0 + row0);
+      contact_a0_position(b, W, C, a0 + row0);
     }
   });
-  if (!imp) world_rnea(ex, b, W, x + nj, nullptr, tau);
+  if (!imp) world_rnea(ex, b, W, x + nq, nullptr, tau);
   ex.run([&](int lane) {
     if (lane < nj) {
       const double ti = lane < b.nun ? 0. : ub[lane - b.nun];  // ActuationModelFloatingBase: tau = [0; u]
@@ -1074,11 +1381,18 @@ MB_HD inline double knot_calc_x(const X& ex, const double* P, int nx, const doub
     if (!imp && lane >= 64 && lane < 64 + b.ncon) {
       int row0;
       const CRec C{contact_rec(b, lane - 64, &row0)};
-      contact_a0_drift(W, C, a0 + row0);
+      contact_a0_drift(b, W, C, a0 + row0);
     }
     if (lane == 128) {
       double total = 0.;
-      for (int k = 0; k < b.ncost; ++k) total += cv[k];
+      const double* cr = b.C;
+      for (int k = 0; k < b.ncost; ++k) {
+        const CRec C{cr};
+        total += cv[k];
+        // contact-force costs without active contact rows (lambda = 0)
+        if (C.type() == C_CONTACT_FORCE && nc == 0) total += C.weight() * force_cost_activation(b, C, nullptr, nu);
+        cr += C.size();
+      }
       red[0] = total;
     }
   });
@@ -1090,7 +1404,7 @@ MB_HD inline double knot_calc_x(const X& ex, const double* P, int nx, const doub
       for (int e = lane; e < nc * (nc + 1); e += ex.nt) {
         const int col = e / nc, row = e % nc;
         // column col of Y, or z (impulse: v, and the restitution term r Jc v)
-        const double* yc = (imp && col == nc) ? x + nj : A + (int64_t)nj * (nj + col);
+        const double* yc = (imp && col == nc) ? x + nq : A + (int64_t)nj * (nj + col);
         double s = 0.;
         for (int i = 0; i < nj; ++i) s += Jc[(int64_t)row * nj + i] * yc[i];
         S[e] = col < nc ? s + (row == col ? b.damping : 0.) : (imp ? (1. + b.r_coeff) * s : s + a0[row]);
@@ -1105,36 +1419,41 @@ MB_HD inline double knot_calc_x(const X& ex, const double* P, int nx, const doub
         const double* cr = b.C;
         for (int k = 0; k < b.ncost; ++k) {
           const CRec C{cr};
-          if (C.type() == C_CONTACT_FORCE) add += C.weight() * force_cost_activation(C, lamv, nx, nu);
+          if (C.type() == C_CONTACT_FORCE) add += C.weight() * force_cost_activation(b, C, lamv, nu);
           cr += C.size();
         }
         red[0] += add;
       }
       if (lane >= nj) return;
-      double s = imp ? x[nj + lane] : a[lane];
+      double s = imp ? x[nq + lane] : a[lane];
       for (int k = 0; k < nc; ++k) s -= A[(int64_t)nj * (nj + k) + lane] * S[(int64_t)nc * nc + k];
       a[lane] = s;
     });
   }
   const double cc = red[0];
   const double dt = b.dt;
+  if (!ok)  // a singular mass matrix / Schur complement surfaces as forward_error
+    ex.run([&](int i) {
+      if (i < nj) a[i] = NAN;
+    });
   ex.run([&](int i) {
     if (i >= nj) return;
     if (imp) {  // impulse-fwddyn.hxx:80-81: xnext = (q, v+)
+      xnext[nq + i] = nc > 0 ? a[i] : x[nq + i];
+      if (!ok) xnext[nq + i] = NAN;
       xnext[i] = x[i];
-      xnext[nj + i] = ok ? (nc > 0 ? a[i] : x[nj + i]) : NAN;
+      if (i == nj - 1 && b.ff) xnext[nq - 1] = x[nq - 1];
       return;
     }
-    const double ai = ok ? a[i] : NAN;  // a singular mass matrix surfaces as forward_error
     if (dt != 0.) {
-      const double v = x[nj + i];
-      xnext[i] = x[i] + (v * dt + ai * dt * dt);
-      xnext[nj + i] = v + ai * dt;
+      euler_step(b, x, a, dt, xnext, i);
     } else {
       xnext[i] = x[i];
-      xnext[nj + i] = x[nj + i];
+      xnext[nq + i] = x[nq + i];
+      if (i == nj - 1 && b.ff) xnext[nq - 1] = x[nq - 1];
     }
   });
+  (void)nx;
   return dt != 0. ? dt * cc : cc;
 }
 
@@ -1146,27 +1465,46 @@ __device__ inline double knot_calc(const double* P, int nx, const double* x, con
 }
 
 // ---------------------------------------------------------------------------
-// calcDiff: one 64-thread workgroup per (element, knot).
+// calcDiff: one kMbDiffNT-thread workgroup per (element, knot).
+//
+// World-frame RNEA derivatives. Perturbing q_j moves the whole subtree of dof j's
+// body rigidly by S_j, so every world quantity X of that subtree changes by the
+// transport S_j x X (x* for forces) plus an intrinsic part; with
+//   V_P, A_P: velocity / acceleration (gravity included) of the parent body of j,
+//   u_j = S_j x V_P,  c_j = -S_j x A_P + u_j x V_P,  w_j = (V_b(j) + V_P) x S_j,
+// the body accelerations and velocities change by
+//   dA_b/dq_j = S_j x A_b + c_j - u_j x V_b,  dV_b/dq_j = S_j x V_b - u_j,
+//   dA_b/dv_j = w_j + S_j x V_b,              dV_b/dv_j = S_j,
+// for every body b below j, and the transport cancels in tau_k = S_k . F_k, so
+//   k below j (incl. j's body):   dtau_k/dq_j = Q_k . c_j - P_k . u_j,   dtau_k/dv_j = Q_k . w_j + P_k . S_j
+//   k strict ancestor of j:       dtau_k/dx_j = S_k . G_j
+// with Q_k = Ycrb_k S_k (composite inertia), P_k = sum_{b in sub(k)} [V_b x* (Y_b S_k)
+// - Y_b (V_b x S_k)] - S_k x* sum_{b in sub(k)} Y_b V_b, and G_j = S_j x* F_j +
+// Ycrb_j c_j - B_j u_j (q) / Ycrb_j w_j + B_j S_j (v), B_j x = sum_{b in sub(j)}
+// [-Y_b (V_b x x) + x x* (Y_b V_b) + V_b x* (Y_b x)]. Contact forces are fixed in
+// their frames (computeRNEADerivatives with fext) and enter through F.
 // ---------------------------------------------------------------------------
 struct DiffLayout {
-  int64_t wv, vals, A, tang, dtau, J, xu, red, ct, total;
+  int64_t wv, A, dtau, da, qp, vec, J, red, total;
   // contact area (nc > 0): Jc nc x nj, a0 nc, lambda nc, Y = Minv Jc^T and
   // H = Y S^-1 (nj x nc each), [S | I | r] nc x (2nc + 1), da0/dx nc x L, fx 6 nj
   int64_t Jc, a0, lam, Y, H, Sx, da0, fx, zv, dfx, dfu;
 };
-__host__ __device__ inline DiffLayout diff_layout(int nj, int nframe, int nc = 0) {
+// vec area: x (nq + nj <= 2 nj + 1), u (nj), nle / z / a / tau (3 nj), jac-cost
+// residuals (6 per cost), Jexp6 / Ad(exp6^-1) (72)
+__host__ __device__ inline DiffLayout diff_layout(int nj, int njac, int nc = 0) {
   const int L = 2 * nj;
   DiffLayout l;
   l.wv = 0;
-  l.vals = l.wv + pad2(WVals::doubles(nj));
-  l.A = l.vals + (int64_t)kValsPerJoint * nj + 12;
-  l.tang = l.A + (int64_t)nj * 2 * nj;          // [M | I] -> [. | Minv]
-  l.dtau = l.tang + (int64_t)18 * nj * L;       // per lane: dv, da, df per joint, [i][c][L]
-  l.J = l.dtau + ((int64_t)nj * L > 3 * nj ? (int64_t)nj * L : 3 * nj);  // dtau [i][L] (nle, a first)
-  l.xu = l.J + (int64_t)6 * nj * (nframe > 0 ? nframe : 1);  // frame-cost Jacobians [cost][6][nj] + residuals
-  l.red = l.xu + 3 * nj + 6 * kMaxFrameCosts + 8;  // x (2nj), u (nj), frame residuals
-  l.ct = l.red + 8;  // red: flag
-  l.Jc = l.ct;
+  l.A = l.wv + pad2(WVals::doubles(nj));
+  l.dtau = l.A + (int64_t)nj * 2 * nj;  // [M | I] -> [. | Minv]
+  l.da = l.dtau + (int64_t)nj * L;      // dtau [k][L]
+  l.qp = l.da + (int64_t)nj * L;        // da = -Kinv (dtau; da0) [r][L]
+  l.vec = l.qp + (int64_t)12 * nj;      // Q_k, P_k
+  l.J = l.vec + pad2(6 * nj + 1 + 6 * kMaxJacCosts + 72);
+  l.red = l.J + (int64_t)6 * nj * (njac > 0 ? njac : 1);  // jac-cost Jacobians [cost][6][nj]
+  l.total = l.red + 8;
+  l.Jc = l.total;
   l.a0 = l.Jc + (int64_t)nc * nj;
   l.lam = l.a0 + nc;
   l.Y = l.lam + nc;
@@ -1177,182 +1515,295 @@ __host__ __device__ inline DiffLayout diff_layout(int nj, int nframe, int nc = 0
   l.zv = l.fx + 6 * nj;  // impulse: v+ - v
   l.dfx = l.zv + nj;     // d lambda / dx (nc x L), d lambda / du (nc x nj): CostModelContactForce
   l.dfu = l.dfx + (int64_t)nc * L;
-  l.total = nc > 0 ? l.dfu + (int64_t)nc * nj : l.ct;
+  l.total = nc > 0 ? l.dfu + (int64_t)nc * nj : l.total;
   return l;
 }
 
-// Linearised RNEA along direction (q_j if dir == 0, v_j if dir == 1), values in V.
-// Tangents kept at T[(i*18 + c)*L + lane]. Writes dtau[i*L + lane].
-MB_HD inline void rnea_tangent(const Blk& b, const Vals& V, const double* qd, int dir, int j, double* T, int L,
-                                    int lane, double* dtau) {
-  const int nj = b.nj;
-  auto slot = [&](int i, int c) -> double& { return T[((int64_t)i * 18 + c) * L + lane]; };
-  for (int i = 0; i < nj; ++i) {
-    const JRec J(b, i);
-    const int lam = J.parent();
-    const double* ax = J.axis();
-    const double* R = V.R(i);
-    const double* p = V.p(i);
-    double dv[6], da[6], t6[6], u6[6];
-    if (lam >= 0) {
-      double pv[6], pa[6];
-      for (int e = 0; e < 6; ++e) {
-        pv[e] = slot(lam, e);
-        pa[e] = slot(lam, 6 + e);
-      }
-      motion_act_inv(R, p, pv, dv);
-      motion_act_inv(R, p, pa, da);
-    } else {
-      for (int e = 0; e < 6; ++e) dv[e] = da[e] = 0.;
-    }
-    const double S[6] = {0., 0., 0., ax[0], ax[1], ax[2]};
-    if (i == j) {
-      if (dir == 0) {  // d(X^-1 m)/dq = -S x (X^-1 m)
-        motion_act_inv(R, p, lam >= 0 ? V.v(lam) : V.root_v(), u6);
-        cross_m(S, u6, t6);
-        for (int e = 0; e < 6; ++e) dv[e] -= t6[e];
-        motion_act_inv(R, p, lam >= 0 ? V.a(lam) : V.root_a(), u6);
-        cross_m(S, u6, t6);
-        for (int e = 0; e < 6; ++e) da[e] -= t6[e];
-      } else {
-        dv[3] += ax[0];
-        dv[4] += ax[1];
-        dv[5] += ax[2];
-      }
-    }
-    // d(v x S qd) = dv x S qd  (+ v x S when dir == v, i == j)
-    const double w = qd[i];
-    const double Sw[6] = {0., 0., 0., ax[0] * w, ax[1] * w, ax[2] * w};
-    cross_m(dv, Sw, t6);
-    for (int e = 0; e < 6; ++e) da[e] += t6[e];
-    if (dir == 1 && i == j) {
-      cross_m(V.v(i), S, t6);
-      for (int e = 0; e < 6; ++e) da[e] += t6[e];
-    }
-    // df = I da + dv x* (I v) + v x* (I dv)
-    double df[6], Iv[6], Idv[6];
-    inertia_mul(J.mass(), J.com(), J.I6(), da, df);
-    inertia_mul(J.mass(), J.com(), J.I6(), V.v(i), Iv);
-    inertia_mul(J.mass(), J.com(), J.I6(), dv, Idv);
-    cross_f(dv, Iv, t6);
-    cross_f(V.v(i), Idv, u6);
+// lane k < nj: Q_k = Ycrb_k S_k, P_k (header comment). qp[12 k ..].
+MB_HD inline void qp_lane(const Blk& b, const WVals& W, int k, double* qp) {
+  double S[6], Q[6], P[6] = {0., 0., 0., 0., 0., 0.}, Hc[6] = {0., 0., 0., 0., 0., 0.};
+  for (int e = 0; e < 6; ++e) S[e] = W.S(k)[e];
+  comp_mul(W, k, S, Q);
+  for (int bb = 0; bb < b.nj; ++bb) {
+    if (!((*W.anc(bb) >> k) & 1ull) || !carries_body(b, bb)) continue;
+    const double m = *W.m(bb);
+    double c[3], I6[6], V[6], YS[6], VxS[6], YVxS[6], t6[6], h[6];
+    for (int e = 0; e < 3; ++e) c[e] = W.c(bb)[e];
     for (int e = 0; e < 6; ++e) {
-      slot(i, e) = dv[e];
-      slot(i, 6 + e) = da[e];
-      slot(i, 12 + e) = df[e] + t6[e] + u6[e];
+      I6[e] = W.Ic(bb)[e];
+      V[e] = W.v(bb)[e];
+    }
+    inertia_mul(m, c, I6, S, YS);
+    cross_m(V, S, VxS);
+    inertia_mul(m, c, I6, VxS, YVxS);
+    cross_f(V, YS, t6);
+    inertia_mul(m, c, I6, V, h);
+    for (int e = 0; e < 6; ++e) {
+      P[e] += t6[e] - YVxS[e];
+      Hc[e] += h[e];
     }
   }
-  for (int i = nj - 1; i >= 0; --i) {
-    const JRec J(b, i);
-    double F[6];
-    for (int e = 0; e < 6; ++e) F[e] = slot(i, 12 + e);
-    dtau[(int64_t)i * L + lane] = dot3(J.axis(), F + 3);
-    const int lam = J.parent();
-    if (lam < 0) continue;
-    if (dir == 0 && i == j) {  // d(X F)/dq = X (S x* F)
-      const double S[6] = {0., 0., 0., J.axis()[0], J.axis()[1], J.axis()[2]};
-      double t6[6];
-      cross_f(S, V.F(i), t6);
-      for (int e = 0; e < 6; ++e) F[e] += t6[e];
-    }
-    double t6[6];
-    force_act(V.R(i), V.p(i), F, t6);
-    for (int e = 0; e < 6; ++e) slot(lam, 12 + e) += t6[e];
+  double t6[6];
+  cross_f(S, Hc, t6);
+  for (int e = 0; e < 6; ++e) {
+    qp[12 * k + e] = Q[e];
+    qp[12 * k + 6 + e] = P[e] - t6[e];
   }
 }
 
-// da0/dx along the tangent direction of this lane (q_c if dir == 0, v_c if
-// dir == 1), from the joint tangents of rnea_tangent (at ddq = a fixed, as
-// getJointAccelerationDerivatives after computeRNEADerivatives): the frame
-// motion tangents (jMf.actInv), the classical-acceleration term of a 3D
-// contact, the gravity that RNEA's tangents carry removed, and the Baumgarte
-// terms (contact-3d.hxx:46-71, contact-6d.hxx:48-66). da0[row * L + lane].
-MB_HD inline void contact_tangent(const Blk& b, const Vals& V, const WVals& W, int dir, int c, const double* T,
-                                  int L, int lane, double* da0) {
+// B_j x = sum_{b in sub(j)} [-Y_b (V_b x x) + x x* (Y_b V_b) + V_b x* (Y_b x)]
+MB_HD inline void bsub_mul(const Blk& b, const WVals& W, int j, const double* x, double* o) {
+  for (int e = 0; e < 6; ++e) o[e] = 0.;
+  for (int bb = 0; bb < b.nj; ++bb) {
+    if (!((*W.anc(bb) >> j) & 1ull) || !carries_body(b, bb)) continue;
+    const double m = *W.m(bb);
+    double c[3], I6[6], V[6], t[6], Yt[6], h[6], s1[6], Yx[6], s2[6];
+    for (int e = 0; e < 3; ++e) c[e] = W.c(bb)[e];
+    for (int e = 0; e < 6; ++e) {
+      I6[e] = W.Ic(bb)[e];
+      V[e] = W.v(bb)[e];
+    }
+    cross_m(V, x, t);
+    inertia_mul(m, c, I6, t, Yt);
+    inertia_mul(m, c, I6, V, h);
+    cross_f(x, h, s1);
+    inertia_mul(m, c, I6, x, Yx);
+    cross_f(V, Yx, s2);
+    for (int e = 0; e < 6; ++e) o[e] += s1[e] + s2[e] - Yt[e];
+  }
+}
+
+// Direction dd (q_j for dd < nj, v_j otherwise): column dd of dtau/dx
+// (dtau[k * L + dd]), and the motion derivatives of the contact / impulse frames.
+// Parent-body quantities: V_P, A_P (gravity included; the root: 0, root_a).
+MB_HD inline void parent_motion(const Blk& b, const WVals& W, int j, double* VP, double* AP) {
+  const int p = body_parent(b, j);
+  for (int e = 0; e < 6; ++e) {
+    VP[e] = p >= 0 ? W.v(p)[e] : 0.;
+    AP[e] = p >= 0 ? W.a(p)[e] : W.root_a()[e];
+  }
+}
+
+MB_HD inline void dtau_direction(const Blk& b, const WVals& W, const double* qp, int dd, int L, double* dtau) {
+  const int nj = b.nj, j = dd < nj ? dd : dd - nj;
+  const bool isq = dd < nj;
+  double S[6], VP[6], AP[6], u[6], cj[6], G[6], t6[6], t7[6];
+  for (int e = 0; e < 6; ++e) S[e] = W.S(j)[e];
+  parent_motion(b, W, j, VP, AP);
+  if (isq) {
+    cross_m(S, VP, u);
+    cross_m(S, AP, t6);
+    cross_m(u, VP, t7);
+    for (int e = 0; e < 6; ++e) cj[e] = t7[e] - t6[e];
+    // G_j = S_j x* F_j + Ycrb_j c_j - B_j u_j
+    double F[6], Bu[6];
+    for (int e = 0; e < 6; ++e) F[e] = W.F(j)[e];
+    cross_f(S, F, G);
+    comp_mul(W, j, cj, t6);
+    bsub_mul(b, W, j, u, Bu);
+    for (int e = 0; e < 6; ++e) G[e] += t6[e] - Bu[e];
+  } else {
+    // w_j = (V_b(j) + V_P) x S_j ; G_j = Ycrb_j w_j + B_j S_j
+    double Vs[6], BS[6];
+    for (int e = 0; e < 6; ++e) Vs[e] = W.v(j)[e] + VP[e];
+    cross_m(Vs, S, cj);  // (w_j in cj)
+    comp_mul(W, j, cj, G);
+    bsub_mul(b, W, j, S, BS);
+    for (int e = 0; e < 6; ++e) G[e] += BS[e];
+    for (int e = 0; e < 6; ++e) u[e] = S[e];  // P_k . S_j
+  }
+  const Mask aj = *W.anc(j);
+  for (int k = 0; k < nj; ++k) {
+    double val = 0.;
+    if ((*W.anc(k) >> j) & 1ull) {  // k's body below j's (or the same body)
+      const double* Q = qp + 12 * k;
+      const double* P = Q + 6;
+      val = isq ? dot6(Q, cj) - dot6(P, u) : dot6(Q, cj) + dot6(P, u);
+    } else if ((aj >> k) & 1ull) {  // k's body a strict ancestor of j's
+      val = dot6(W.S(k), G);
+    }
+    dtau[(int64_t)k * L + dd] = val;
+  }
+}
+
+// Direction dd: da0/dx column (contact-3d.hxx:46-71, contact-6d.hxx:48-66) at the
+// solved acceleration (getJointAccelerationDerivatives after computeRNEADerivatives):
+// the frame motion derivative moved to the frame, the classical term of a 3D
+// contact, the Baumgarte terms. da0[row * L + dd].
+MB_HD inline void contact_direction(const Blk& b, const WVals& W, int dd, int L, double* da0) {
+  const int nj = b.nj, j = dd < nj ? dd : dd - nj;
+  const bool isq = dd < nj;
+  double S[6], VP[6], AP[6], u[6], c0[6], t6[6], t7[6];
+  for (int e = 0; e < 6; ++e) S[e] = W.S(j)[e];
+  parent_motion(b, W, j, VP, AP);
+  for (int e = 0; e < 6; ++e) AP[e] -= W.root_a()[e];  // gravity-free (data.a)
+  if (isq) {
+    cross_m(S, VP, u);
+    cross_m(S, AP, t6);
+    cross_m(u, VP, t7);
+    for (int e = 0; e < 6; ++e) c0[e] = t7[e] - t6[e];
+  } else {
+    double Vs[6];
+    for (int e = 0; e < 6; ++e) Vs[e] = W.v(j)[e] + VP[e];
+    cross_m(Vs, S, c0);  // w_j
+  }
   const double* r = b.K;
   int row = 0;
   for (int k = 0; k < b.ncon; ++k) {
     const CRec C{r};
     const double* d = C.d();
-    const int j = (int)d[0];
-    double dv[6], da[6];
-    for (int e = 0; e < 6; ++e) {
-      dv[e] = T[((int64_t)j * 18 + e) * L + lane];
-      da[e] = T[((int64_t)j * 18 + 6 + e) * L + lane];
+    const int fb = frame_dof(b, d);
+    const int n = C.type() == C_CONTACT_3D ? 3 : 6;
+    if (!((*W.anc(fb) >> j) & 1ull)) {
+      for (int e = 0; e < n; ++e) da0[(int64_t)(row + e) * L + dd] = 0.;
+      row += n;
+      r += C.size();
+      continue;
     }
-    const bool sup = (*W.anc(j) >> c) & 1u;
-    if (dir == 0 && sup) {  // d(-R_j^T g)/dq_c = R_j^T (w_c x g)
-      double wc[3], wg[3], t[3];
-      matvec3(V.oR(c), JRec(b, c).axis(), wc);
-      cross3(wc, b.g, wg);
-      matTvec3(V.oR(j), wg, t);
-      for (int e = 0; e < 3; ++e) da[e] -= t[e];
+    double Rf[9], pf[3], V[6], dV[6], dA[6], vf[6], dvf[6], daf[6];
+    frame_placement(b, W, d, Rf, pf);
+    for (int e = 0; e < 6; ++e) V[e] = W.v(fb)[e];
+    if (isq) {  // dV = -u_j, dA = c0_j - u_j x V_b (intrinsic parts)
+      cross_m(u, V, t6);
+      for (int e = 0; e < 6; ++e) {
+        dV[e] = -u[e];
+        dA[e] = c0[e] - t6[e];
+      }
+    } else {  // dV = S_j, dA = w_j + S_j x V_b
+      cross_m(S, V, t6);
+      for (int e = 0; e < 6; ++e) {
+        dV[e] = S[e];
+        dA[e] = c0[e] + t6[e];
+      }
     }
-    double dvf[6], daf[6], vf[6], vj[6];
-    for (int e = 0; e < 6; ++e) vj[e] = V.v(j)[e];
-    motion_act_inv(d + 1, d + 10, dv, dvf);
-    motion_act_inv(d + 1, d + 10, da, daf);
-    motion_act_inv(d + 1, d + 10, vj, vf);
+    motion_act_inv(Rf, pf, V, vf);
+    motion_act_inv(Rf, pf, dV, dvf);
+    motion_act_inv(Rf, pf, dA, daf);
     const double kp = C.r[1], kd = C.r[2];
-    double rr[6], Jk[6] = {0., 0., 0., 0., 0., 0.};
-    if (kp != 0. && dir == 0 && sup) frame_residual(b, V, C, c, rr, Jk);
     if (C.type() == C_CONTACT_3D) {
-      double t1[3], t2[3];
+      double t1[3], t2[3], pv[3] = {0., 0., 0.};
       cross3(dvf + 3, vf, t1);
       cross3(vf + 3, dvf, t2);
-      for (int e = 0; e < 3; ++e)
-        da0[(int64_t)(row + e) * L + lane] = daf[e] + t1[e] + t2[e] + kd * dvf[e] + kp * Jk[e];
-      row += 3;
-    } else {
-      for (int e = 0; e < 6; ++e) da0[(int64_t)(row + e) * L + lane] = daf[e] + kd * dvf[e] + kp * Jk[e];
-      row += 6;
-    }
-    r += C.size();
-  }
-}
-
-// d(Jc v+)/dq_c for the impulse records (impulse-3d.hxx:33-39 / impulse-6d.hxx:30-36:
-// getJointVelocityDerivatives at v+, moved into the frame): the joint velocity
-// tangent along q_c walked from the root to each record's joint (vp: joint-frame
-// velocities at v+, 6 per joint; qdp = v+). dv0[row * L + lane].
-MB_HD inline void impulse_tangent(const Blk& b, const Vals& V, const WVals& W, const double* vp, const double* qdp,
-                                  int c, int L, int lane, double* dv0) {
-  const double* r = b.K;
-  int row = 0;
-  for (int k = 0; k < b.ncon; ++k) {
-    const CRec C{r};
-    const double* d = C.d();
-    const int j = (int)d[0];
-    const unsigned am = *W.anc(j);
-    double dv[6] = {0., 0., 0., 0., 0., 0.};
-    for (int i = 0; i <= j; ++i) {  // ancestors-or-self in root-to-j order (parents precede children)
-      if (!((am >> i) & 1u)) continue;
-      double t6[6];
-      motion_act_inv(V.R(i), V.p(i), dv, t6);
-      if (i == c) {  // d(X^-1 v_parent)/dq_i = -S x (X^-1 v_parent), X^-1 v_parent = v_i - S qd_i
-        const double* ax = JRec(b, i).axis();
-        const double S[6] = {0., 0., 0., ax[0], ax[1], ax[2]};
-        double u6[6], w6[6];
-        for (int e = 0; e < 6; ++e) u6[e] = vp[6 * i + e] - S[e] * qdp[i];
-        cross_m(S, u6, w6);
-        for (int e = 0; e < 6; ++e) t6[e] -= w6[e];
+      if (isq && kp != 0.) {  // world velocity of the frame origin: oRf Jc
+        cross3(S + 3, pf, pv);
+        for (int e = 0; e < 3; ++e) pv[e] += S[e];
       }
-      for (int e = 0; e < 6; ++e) dv[e] = t6[e];
+      for (int e = 0; e < 3; ++e)
+        da0[(int64_t)(row + e) * L + dd] = daf[e] + t1[e] + t2[e] + kd * dvf[e] + kp * pv[e];
+    } else {
+      double rr[6], Jk[6] = {0., 0., 0., 0., 0., 0.};
+      if (isq && kp != 0.) frame_residual(b, W, C, S, rr, Jk);
+      for (int e = 0; e < 6; ++e) da0[(int64_t)(row + e) * L + dd] = daf[e] + kd * dvf[e] + kp * Jk[e];
     }
-    double dvf[6];
-    motion_act_inv(d + 1, d + 10, dv, dvf);
-    const int n = C.type() == C_CONTACT_3D ? 3 : 6;
-    for (int e = 0; e < n; ++e) dv0[(int64_t)(row + e) * L + lane] = dvf[e];
     row += n;
     r += C.size();
   }
 }
 
-// model->calcDiff for one knot by one 64-thread workgroup (euler.hxx:83-131,
-// free-fwddyn.hxx:82-118, cost-sum.hxx:122-160). Writes full blocks (entries
-// beyond nu zero); Lxu is zero (no cost couples x and u). A mass matrix that is
-// not positive definite leaves NaN in Fx/Fu, which the backward pass reports
-// as backward_error. `w`: diff_layout(nj, nframe).total doubles of LDS.
+// d(Jc v+)/dq_j for the impulse records (impulse-3d.hxx:33-39 / impulse-6d.hxx:30-36:
+// getJointVelocityDerivatives at v+, moved into the frame): -Ad(oMf)^-1 (S_j x V+_P)
+// with W.v holding the velocities at v+. dv0[row * L + j].
+MB_HD inline void impulse_direction(const Blk& b, const WVals& W, int j, int L, double* dv0) {
+  double S[6], VP[6], AP[6], u[6];
+  for (int e = 0; e < 6; ++e) S[e] = W.S(j)[e];
+  parent_motion(b, W, j, VP, AP);
+  cross_m(S, VP, u);
+  for (int e = 0; e < 6; ++e) u[e] = -u[e];
+  const double* r = b.K;
+  int row = 0;
+  for (int k = 0; k < b.ncon; ++k) {
+    const CRec C{r};
+    const int fb = frame_dof(b, C.d());
+    const int n = C.type() == C_CONTACT_3D ? 3 : 6;
+    double o[6] = {0., 0., 0., 0., 0., 0.};
+    if ((*W.anc(fb) >> j) & 1ull) {
+      double Rf[9], pf[3];
+      frame_placement(b, W, C.d(), Rf, pf);
+      motion_act_inv(Rf, pf, u, o);
+    }
+    for (int e = 0; e < n; ++e) dv0[(int64_t)(row + e) * L + j] = o[e];
+    row += n;
+    r += C.size();
+  }
+}
+
+// lane j < nj: column j of every jac-cost Jacobian (Jf[(f*6 + e)*nj + j]) and, on
+// lane 0, their residuals (rf[6 f + e]); lanes j < 6 of a free-flyer knot also the
+// Euler step's Jexp6(dq) column j (Je, col-major 6x6) and, on lane 0, Ad(exp6(dq)^-1) (Ai).
+MB_HD inline void jac_lane(const Blk& b, const WVals& W, const double* x, int j, double* Jf, double* rf,
+                           const double* dqff, double* Je, double* Ai) {
+  const int nj = b.nj;
+  double S[6];
+  for (int e = 0; e < 6; ++e) S[e] = W.S(j)[e];
+  const double* cr = b.C;
+  int f = 0;
+  for (int k = 0; k < b.ncost; ++k) {
+    const CRec C{cr};
+    const int t = C.type();
+    if (jac_cost(b, t)) {
+      double r[6] = {0., 0., 0., 0., 0., 0.}, Jc[6] = {0., 0., 0., 0., 0., 0.};
+      if (t == C_FRAME_PLACEMENT || t == C_FRAME_TRANSLATION) {
+        const bool sup = (*W.anc(frame_dof(b, C.d())) >> j) & 1ull;
+        frame_residual(b, W, C, sup ? S : nullptr, r, Jc);
+      } else if (t == C_COM_POSITION) {  // Jcom col j = (m_sub S_lin + S_ang x h_sub) / m_total
+        double mt = 0.;
+        for (int bb = 0; bb < nj; ++bb)
+          if (carries_body(b, bb)) mt += *W.m(bb);
+        double tt[3];
+        cross3(S + 3, W.ch(j), tt);
+        const double m = *W.cm(j);
+        for (int e = 0; e < 3; ++e) Jc[e] = (m * S[e] + tt[e]) / mt;
+        if (j == 0) {
+          double c[3];
+          com_value(b, W, c);
+          for (int e = 0; e < 3; ++e) r[e] = c[e] - C.d()[e];
+        }
+      } else {  // free-flyer block of a state cost: Jlog6(Mref^-1 M) (Jdiff second, multibody.hxx:118-126)
+        double Rr[9], pr[3];
+        ff_rel(C.d(), x, Rr, pr);
+        if (j < 6) jlog6_col(Rr, pr, j, Jc);
+        if (j == 0) log6_t<double>(Rr, pr, r);
+      }
+      const int nr = jac_rows(t);
+#pragma unroll
+      for (int e = 0; e < 6; ++e)
+        if (e < nr) {
+          Jf[((int64_t)f * 6 + e) * nj + j] = Jc[e];
+          if (j == 0) rf[6 * f + e] = r[e];
+        }
+      ++f;
+    }
+    cr += C.size();
+  }
+  if (dqff && j < 6) {
+    jexp6_col(dqff, j, Je + 6 * j);
+    if (j == 0) {  // Ad(M^-1) of M = exp6(dq): [[R^T, -R^T [p]x], [0, R^T]]
+      double R[9], p[3];
+      exp6_t<double>(dqff, R, p);
+      for (int c = 0; c < 6; ++c)
+        for (int r = 0; r < 6; ++r) Ai[c * 6 + r] = 0.;
+      for (int c = 0; c < 3; ++c)
+        for (int r = 0; r < 3; ++r) {
+          const double Rt = R[r * 3 + c];  // (R^T)(r, c)
+          Ai[c * 6 + r] = Rt;
+          Ai[(c + 3) * 6 + r + 3] = Rt;
+        }
+      for (int c = 0; c < 3; ++c) {  // -R^T [p]x, column c: -R^T (p x e_c)
+        const double e[3] = {c == 0 ? 1. : 0., c == 1 ? 1. : 0., c == 2 ? 1. : 0.};
+        double t[3], o[3];
+        cross3(p, e, t);
+        matTvec3(R, t, o);
+        for (int r = 0; r < 3; ++r) Ai[(c + 3) * 6 + r] = -o[r];
+      }
+    }
+  }
+}
+
+// model->calcDiff for one knot by one workgroup (euler.hxx:83-131,
+// free-fwddyn.hxx:82-118, contact-fwddyn.hxx:107-160, impulse-fwddyn.hxx:85-127,
+// cost-sum.hxx:122-160). Writes full blocks (entries beyond nu zero). A mass
+// matrix that is not positive definite leaves NaN in Fx/Fu, which the backward
+// pass reports as backward_error. `w`: diff_layout(nj, njac, nc).total doubles of LDS.
 // xnext_out / cost_out (may be null): the knot's calc (xnext, cost) as well;
 // Fx == nullptr: calc only (no derivative block is written).
 template <class X>
@@ -1362,26 +1813,22 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
                                    double* cost_out = nullptr) {
   const Blk b = parse(P);
   const bool imp = b.impulse;  // ActionModelImpulseFwdDynamics (impulse-fwddyn.hxx:53-127)
-  const int nj = b.nj, n = nx, L = 2 * nj, nc = b.nc, nu = nj - b.nun;
-  int nframe = 0;
-  {
-    const double* cr = b.C;
-    for (int k = 0; k < b.ncost; ++k) {
-      const CRec C{cr};
-      if (C.type() == C_FRAME_PLACEMENT || C.type() == C_FRAME_TRANSLATION) ++nframe;
-      cr += C.size();
-    }
-  }
-  const DiffLayout l = diff_layout(nj, nframe, nc);
+  const int nj = b.nj, nq = b.nq, n = 2 * nj, L = 2 * nj, nc = b.nc, nu = nj - b.nun;
+  const int njac = count_jac_costs(b);
+  const DiffLayout l = diff_layout(nj, njac, nc);
   const WVals W{w + l.wv, nj};
-  const Vals V{w + l.vals, nj};
   double* A = w + l.A;
-  double* T = w + l.tang;
   double* dtau = w + l.dtau;
+  double* da = w + l.da;
+  double* qp = w + l.qp;
+  double* x = w + l.vec;
+  double* u = x + nq + nj;
+  double* nle = u + nj;   // nle, then RNEA's tau (unused)
+  double* av = nle + nj;  // z, then a (impulse: v+)
+  double* rf = av + nj;   // jac-cost residuals, 6 per cost
+  double* Je = rf + 6 * kMaxJacCosts;  // Jexp6(dq) 6x6
+  double* Ai = Je + 36;                // Ad(exp6(dq)^-1) 6x6
   double* Jf = w + l.J;
-  double* x = w + l.xu;
-  double* u = x + 2 * nj;
-  double* rf = u + nj;  // frame residuals, 6 per frame cost
   double* red = w + l.red;
   int* flag = (int*)(red + 4);
   double* Jc = w + l.Jc;
@@ -1394,40 +1841,39 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
   double* fx = w + l.fx;
   double* zv = w + l.zv;
   ex.run([&](int lane) {
-    if (lane < nx) x[lane] = xg[lane];
+    for (int e = lane; e < nq + nj; e += ex.nt) x[e] = xg[e];
     if (lane < nj) u[lane] = (use_u && lane < nu) ? ug[lane] : 0.;  // (impulse: a zero velocity)
     for (int e = lane; e < 2 * nj * nj; e += ex.nt) {
       const int c = e / nj, r = e % nj;
       A[e] = (c == nj + r) ? 1. : 0.;
     }
   });
-  // world-frame kinematics, M into the left half of [M | I], nle -> dtau[0..nj)
+  // world-frame kinematics, M into the left half of [M | I], nle
   world_kinematics(ex, b, W, x, A, [](int, int) {});
-  if (!imp) world_rnea(ex, b, W, x + nj, nullptr, dtau);
+  if (!imp) world_rnea(ex, b, W, x + nq, nullptr, nle);
   if (nc > 0)  // contact rows at the drift (ddq = 0; ContactModelMultiple::calc)
     ex.run([&](int lane) {
       if (lane < nj) contact_jac_lane(b, W, lane, Jc, nullptr);
       for (int k = lane; k < (imp ? 0 : b.ncon); k += ex.nt) {
         int row0;
         const CRec C{contact_rec(b, k, &row0)};
-        contact_a0_position(W, C, a0 + row0);
-        contact_a0_drift(W, C, a0 + row0);
+        contact_a0_position(b, W, C, a0 + row0);
+        contact_a0_drift(b, W, C, a0 + row0);
       }
     });
   bool ok = gauss_jordan(ex, A, nj, 2 * nj, flag);
   double* Minv = A + (int64_t)nj * nj;  // column-major nj x nj; with contacts: d a / d tau after the Schur step
-  // z = (M + A)^-1 (tau - nle) -> dtau[nj..2nj) (the acceleration without contacts);
-  // Y = Minv Jc^T
+  // z = (M + A)^-1 (tau - nle) (the acceleration without contacts); Y = Minv Jc^T
   ex.run([&](int lane) {
     if (lane < nj && imp) {
-      dtau[nj + lane] = x[nj + lane];  // z = M^-1 (M v) = v
+      av[lane] = x[nq + lane];  // z = M^-1 (M v) = v
       zv[lane] = 0.;
       if (lane == 0)
         for (int e = 0; e < 6; ++e) W.root_a()[e] = 0.;  // the impulse RNEA has no gravity
     } else if (lane < nj) {
       double s = 0.;
-      for (int k = 0; k < nj; ++k) s += Minv[(int64_t)k * nj + lane] * ((k < b.nun ? 0. : u[k - b.nun]) - dtau[k]);
-      dtau[nj + lane] = ok ? s : NAN;
+      for (int k = 0; k < nj; ++k) s += Minv[(int64_t)k * nj + lane] * ((k < b.nun ? 0. : u[k - b.nun]) - nle[k]);
+      av[lane] = ok ? s : NAN;
     }
     for (int e = lane; e < nj * nc; e += ex.nt) {
       const int k = e / nj, i = e % nj;
@@ -1450,7 +1896,7 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
           v = (col - nc == row) ? 1. : 0.;
         } else {
           double s = 0.;
-          for (int i = 0; i < nj; ++i) s += Jc[(int64_t)row * nj + i] * dtau[nj + i];
+          for (int i = 0; i < nj; ++i) s += Jc[(int64_t)row * nj + i] * av[i];
           v = imp ? (1. + b.r_coeff) * s : s + a0[row];  // impulse: Jc v+ = -r Jc v
         }
         Sx[e] = v;
@@ -1463,9 +1909,9 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
       const double* sr = Sx + (int64_t)2 * nc * nc;
       if (lane < nc) lam[lane] = -sr[lane];
       if (lane < nj) {
-        double s = dtau[nj + lane];
+        double s = av[lane];
         for (int k = 0; k < nc; ++k) s -= Y[(int64_t)k * nj + lane] * sr[k];
-        dtau[nj + lane] = ok ? s : NAN;
+        av[lane] = ok ? s : NAN;
       }
       for (int e = lane; e < nj * nc; e += ex.nt) {
         const int k = e / nj, i = e % nj;
@@ -1474,7 +1920,7 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
         H[e] = s;
       }
     });
-    // Kinv top-left Minv - H Y^T (in place); contact forces per joint (world)
+    // Kinv top-left Minv - H Y^T (in place); contact forces per dof (world)
     ex.run([&](int lane) {
       for (int e = lane; e < nj * nj; e += ex.nt) {
         const int c = e / nj, i = e % nj;
@@ -1484,76 +1930,36 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
       }
       if (lane < nj) {
         contact_joint_forces(b, W, lam, fx, lane);
-        if (imp) zv[lane] = dtau[nj + lane] - x[nj + lane];  // v+ - v
+        if (imp) zv[lane] = av[lane] - x[nq + lane];  // v+ - v
       }
     });
   }
-  // accelerations and forces at the solved a (the linearisation point of
-  // computeABADerivatives / computeRNEADerivatives with fext); tau lands in
-  // dtau[2nj..3nj) and is not used
+  // velocities, accelerations and forces at the solved a (the linearisation point
+  // of computeABADerivatives / computeRNEADerivatives with fext)
   // (impulse: RNEA(q, 0, v+ - v) without gravity, impulse-fwddyn.hxx:102-104)
-  world_rnea(ex, b, W, imp ? u : x + nj, imp ? zv : dtau + nj, dtau + 2 * nj, nc > 0 ? fx : nullptr);
-  // joint-frame values for the tangent recursion: liMi, oMi, and v, a, F moved
-  // from world to joint coordinates (SE3::actInv of oMi)
-  ex.run([&](int i) {
-    if (i == 0)
-      for (int e = 0; e < 6; ++e) {
-        V.root_v()[e] = 0.;
-        V.root_a()[e] = (e < 3 && !imp) ? -b.g[e] : 0.;
-      }
-    if (i >= nj) return;
-    double oR[9], op[3], t6[6], m6[6];
-    for (int e = 0; e < 9; ++e) {
-      oR[e] = W.oR(i)[e];
-      V.R(i)[e] = W.R(i)[e];
-      V.oR(i)[e] = oR[e];
-    }
-    for (int e = 0; e < 3; ++e) {
-      op[e] = W.op(i)[e];
-      V.p(i)[e] = W.p(i)[e];
-      V.op(i)[e] = op[e];
-    }
-    for (int e = 0; e < 6; ++e) m6[e] = W.v(i)[e];
-    motion_act_inv(oR, op, m6, t6);
-    for (int e = 0; e < 6; ++e) V.v(i)[e] = t6[e];
-    for (int e = 0; e < 6; ++e) m6[e] = W.a(i)[e];
-    motion_act_inv(oR, op, m6, t6);
-    for (int e = 0; e < 6; ++e) V.a(i)[e] = t6[e];
-    // force actInv: f' = R^T f, n' = R^T (n - p x f)
-    double f[3], nn[3], c[3];
-    for (int e = 0; e < 3; ++e) {
-      f[e] = W.F(i)[e];
-      nn[e] = W.F(i)[3 + e];
-    }
-    cross3(op, f, c);
-    for (int e = 0; e < 3; ++e) nn[e] -= c[e];
-    matTvec3(oR, f, t6);
-    matTvec3(oR, nn, t6 + 3);
-    for (int e = 0; e < 6; ++e) V.F(i)[e] = t6[e];
-  });
+  world_rnea(ex, b, W, imp ? u : x + nq, imp ? zv : av, nle, nc > 0 ? fx : nullptr);
   if (xnext_out || cost_out) {  // the knot's calc, fused (iteration 0 of a solve, or calc only)
     ex.run([&](int lane) {
       const double dt = b.dt;
-      if (xnext_out && lane < nj && imp) {
-        xnext_out[lane] = x[lane];
-        xnext_out[nj + lane] = dtau[nj + lane];
-      } else if (xnext_out && lane < nj) {
-        const double ai = dtau[nj + lane];
-        if (dt != 0.) {
-          const double v = x[nj + lane];
-          xnext_out[lane] = x[lane] + (v * dt + ai * dt * dt);
-          xnext_out[nj + lane] = v + ai * dt;
+      if (xnext_out && lane < nj) {
+        if (imp) {
+          xnext_out[lane] = x[lane];
+          if (lane == nj - 1 && b.ff) xnext_out[nq - 1] = x[nq - 1];
+          xnext_out[nq + lane] = av[lane];
+        } else if (dt != 0.) {
+          euler_step(b, x, av, dt, xnext_out, lane);
         } else {
           xnext_out[lane] = x[lane];
-          xnext_out[nj + lane] = x[nj + lane];
+          if (lane == nj - 1 && b.ff) xnext_out[nq - 1] = x[nq - 1];
+          xnext_out[nq + lane] = x[nq + lane];
         }
       }
       if (cost_out && !Fx && lane == 0) {  // calc only (with derivatives: from the residuals below)
-        double cc = cost_value(b, W, x, u, nx, nu);
+        double cc = cost_value(b, W, x, u, nu);
         const double* cr = b.C;
         for (int k = 0; k < b.ncost; ++k) {
           const CRec C{cr};
-          if (C.type() == C_CONTACT_FORCE && nc > 0) cc += C.weight() * force_cost_activation(C, lam, nx, nu);
+          if (C.type() == C_CONTACT_FORCE) cc += C.weight() * force_cost_activation(b, C, lam, nu);
           cr += C.size();
         }
         *cost_out = dt != 0. ? dt * cc : cc;
@@ -1561,50 +1967,58 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
     });
   }
   if (!Fx) return;  // calc only
-  if (imp && nc > 0)  // joint-frame velocities at v+ (into fx, free after the RNEA); zv = v+
+  const double dt = b.dt, dt2 = dt * dt;
+  const bool integ = dt != 0.;
+  const bool ffe = b.ff && integ && !imp;  // Euler on the free-flyer: Jexp6 / Ad(exp6^-1)
+  // per-dof Q_k, P_k (lanes < nj) and the jac-cost Jacobians / residuals; the
+  // free-flyer Euler step's Jexp6 and Ad(exp6(dq)^-1) (dq = v dt + a dt^2)
+  ex.run([&](int lane) {
+    if (lane >= nj) return;
+    if (!imp) qp_lane(b, W, lane, qp);
+    double dq[6];
+    if (ffe)
+      for (int e = 0; e < 6; ++e) dq[e] = x[nq + e] * dt + av[e] * dt2;
+    jac_lane(b, W, x, lane, Jf, rf, ffe ? dq : nullptr, Je, Ai);
+  });
+  if (imp) {  // V = 0 in the impulse RNEA: P_k = 0, Q_k = Ycrb_k S_k
     ex.run([&](int lane) {
       if (lane >= nj) return;
-      w_velocity(W, dtau + nj, lane);
-      double m6[6], t6[6];
-      for (int e = 0; e < 6; ++e) m6[e] = W.v(lane)[e];
-      motion_act_inv(W.oR(lane), W.op(lane), m6, t6);
-      for (int e = 0; e < 6; ++e) fx[6 * lane + e] = t6[e];
-      zv[lane] = dtau[nj + lane];
+      comp_mul(W, lane, W.S(lane), qp + 12 * lane);
+      for (int e = 0; e < 6; ++e) qp[12 * lane + 6 + e] = 0.;
     });
-  // tangents (lanes < 2 nj; impulse: q directions only) and frame-cost residuals /
-  // Jacobian columns (lanes < nj)
+  }
+  // tangent directions: dtau/dx (impulse: q only) and da0/dx
   ex.run([&](int lane) {
-    if (lane < (imp ? nj : L)) {
-      rnea_tangent(b, V, imp ? u : x + nj, lane < nj ? 0 : 1, lane % nj, T, L, lane, dtau);
-      if (nc > 0 && imp) impulse_tangent(b, V, W, fx, zv, lane, L, lane, da0);
-      else if (nc > 0) contact_tangent(b, V, W, lane < nj ? 0 : 1, lane % nj, T, L, lane, da0);
-    }
-    if (lane >= nj) return;
-    const double* cr = b.C;
-    int f = 0;
-    for (int k = 0; k < b.ncost; ++k) {
-      const CRec C{cr};
-      if (C.type() == C_FRAME_PLACEMENT || C.type() == C_FRAME_TRANSLATION) {
-        double r[6], Jc[6];
-        const int nr = frame_residual(b, V, C, lane, r, Jc);
-#pragma unroll
-        for (int e = 0; e < 6; ++e)
-          if (e < nr) {
-            Jf[((int64_t)f * 6 + e) * nj + lane] = Jc[e];
-            if (lane == 0) rf[6 * f + e] = r[e];
-          }
-        ++f;
-      }
-      cr += C.size();
+    for (int dd = lane; dd < (imp ? nj : L); dd += ex.nt) {
+      dtau_direction(b, W, qp, dd, L, dtau);
+      if (nc > 0 && !imp) contact_direction(b, W, dd, L, da0);
     }
   });
+  if (imp && nc > 0) {  // velocities at v+, then d(Jc v+)/dq
+    ex.run([&](int lane) {
+      if (lane < nj) w_velocity(W, av, lane);
+    });
+    ex.run([&](int lane) {
+      for (int j = lane; j < nj; j += ex.nt) impulse_direction(b, W, j, L, da0);
+    });
+  }
   // d lambda / dx, d lambda / du for CostModelContactForce (contact-fwddyn.hxx:131-137, with
   // enable_force): Kinv bottom-left = H^T, bottom-right = -S^-1; dtau/du = [0; I]
   const bool fd = b.enable_force && nc > 0 && !imp;
   double* dfx = w + l.dfx;
   double* dfu = w + l.dfu;
-  if (fd)
-    ex.run([&](int lane) {
+  // da = -Kinv_tl dtau - H da0 (impulse: -G dtau_dq - H dv0_dq on the q columns)
+  ex.run([&](int lane) {
+    for (int e = lane; e < nj * L; e += ex.nt) {
+      const int r = e / L, c = e % L;
+      double s = 0.;
+      if (!imp || c < nj) {
+        for (int k = 0; k < nj; ++k) s += Minv[(int64_t)k * nj + r] * dtau[(int64_t)k * L + c];
+        for (int k = 0; k < nc; ++k) s += H[(int64_t)k * nj + r] * da0[(int64_t)k * L + c];
+      }
+      da[e] = ok ? -s : NAN;
+    }
+    if (fd) {
       const double* Sinv = Sx + (int64_t)nc * nc;
       for (int e = lane; e < nc * L; e += ex.nt) {
         const int k = e / L, c = e % L;
@@ -1617,48 +2031,56 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
         const int k = e / nj, c = e % nj;
         dfu[e] = c < nu ? -H[(int64_t)k * nj + b.nun + c] : 0.;
       }
-    });
-  const double dt = b.dt, dt2 = dt * dt;
-  const bool integ = dt != 0.;
+    }
+  });
   const double sc = integ ? dt : 1.;
   // Output blocks, entry by entry over all lanes (consecutive lanes write
   // consecutive addresses of the column-major blocks).
   ex.run([&](int lane) {
-    // Fx(i, c): da/dx = -Minv dtau(:, c), Euler assembly (euler.hxx:100-112)
+    // Fx(i, c): Euler assembly (euler.hxx:100-112) with JintegrateTransport / Jintegrate
     for (int e = lane; e < n * n; e += ex.nt) {
-      const int c = e / n, i = e % n, r = i < nj ? i : i - nj;
+      const int c = e / n, i = e % n;
       double f;
       if (imp) {  // [[I, 0], [-G dtau_dq - H dv0_dq, G M = I - H Jc]] (impulse-fwddyn.hxx:111-115)
         if (i < nj) {
           f = c == i ? 1. : 0.;
         } else if (c < nj) {
-          double s = 0.;
-          for (int k = 0; k < nj; ++k) s += Minv[(int64_t)k * nj + r] * dtau[(int64_t)k * L + c];
-          for (int k = 0; k < nc; ++k) s += H[(int64_t)k * nj + r] * da0[(int64_t)k * L + c];
-          f = ok ? -s : NAN;
+          f = da[(int64_t)(i - nj) * L + c];
         } else {
           double s = 0.;
-          for (int k = 0; k < nc; ++k) s += H[(int64_t)k * nj + r] * Jc[(int64_t)k * nj + (c - nj)];
-          f = ok ? (c - nj == r ? 1. : 0.) - s : NAN;
+          for (int k = 0; k < nc; ++k) s += H[(int64_t)k * nj + (i - nj)] * Jc[(int64_t)k * nj + (c - nj)];
+          f = ok ? (c - nj == i - nj ? 1. : 0.) - s : NAN;
         }
       } else if (integ) {
-        double s = 0.;
-        for (int k = 0; k < nj; ++k) s += Minv[(int64_t)k * nj + r] * dtau[(int64_t)k * L + c];
-        for (int k = 0; k < nc; ++k) s += H[(int64_t)k * nj + r] * da0[(int64_t)k * L + c];
-        const double da = ok ? -s : NAN;
-        f = i < nj ? da * dt2 + (c == nj + i ? dt : 0.) + (c == i ? 1. : 0.) : da * dt + (c == i ? 1. : 0.);
+        if (i < nj && ffe && i < 6) {  // Jexp6(dq) (da dt^2 + [0 dt I]) + Ad(exp6(dq)^-1)
+          double s = c < 6 ? Ai[c * 6 + i] : 0.;
+          for (int r = 0; r < 6; ++r)
+            s += Je[r * 6 + i] * (da[(int64_t)r * L + c] * dt2 + (c == nj + r ? dt : 0.));
+          f = s;
+        } else if (i < nj) {
+          f = da[(int64_t)i * L + c] * dt2 + (c == nj + i ? dt : 0.) + (c == i ? 1. : 0.);
+        } else {
+          f = da[(int64_t)(i - nj) * L + c] * dt + (c == i ? 1. : 0.);
+        }
       } else {
         f = c == i ? 1. : 0.;
       }
       Fx[e] = f;
     }
-    // Fu(i, c) = Minv(i mod nj, nun + c) dt^2 | dt (dtau/du = [0; I]); Lxu = 0
+    // Fu(i, c) = Kinv_tl(i mod nj, nun + c) dt^2 | dt (dtau/du = [0; I]), Jexp6 on
+    // the free-flyer rows; Lxu from the contact-force costs
     for (int e = lane; e < n * m; e += ex.nt) {
       const int c = e / n, i = e % n;
       double f = 0.;
-      if (integ && c < nu) {
-        const double mi = ok ? Minv[(int64_t)(b.nun + c) * nj + (i < nj ? i : i - nj)] : NAN;
-        f = i < nj ? mi * dt2 : mi * dt;
+      if (integ && c < nu && !imp) {
+        if (i < nj && ffe && i < 6) {
+          double s = 0.;
+          for (int r = 0; r < 6; ++r) s += Je[r * 6 + i] * Minv[(int64_t)(b.nun + c) * nj + r];
+          f = ok ? s * dt2 : NAN;
+        } else {
+          const double mi = ok ? Minv[(int64_t)(b.nun + c) * nj + (i < nj ? i : i - nj)] : NAN;
+          f = i < nj ? mi * dt2 : mi * dt;
+        }
       }
       Fu[e] = f;
       double lxu = 0.;  // only contact-force costs couple x and u
@@ -1666,9 +2088,9 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
         const double* cr = b.C;
         for (int k = 0; k < b.ncost; ++k) {
           const CRec C{cr};
-          if (C.type() == C_CONTACT_FORCE) {
+          if (C.type() == C_CONTACT_FORCE && (int)C.d()[0] >= 0) {
             const int row0 = (int)C.d()[0], nr = (int)C.d()[1];
-            const double* wv = cost_weights(C, nx, nu);
+            const double* wv = cost_weights(b, C, nu);
             double s2 = 0.;
             for (int r = 0; r < nr; ++r)
               s2 += dfx[(int64_t)(row0 + r) * L + i] * wv[r] * dfu[(int64_t)(row0 + r) * nj + c];
@@ -1682,56 +2104,57 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
     // Lxx(i, j): Gauss-Newton, cost-sum.hxx:122-160
     for (int e = lane; e < n * n; e += ex.nt) {
       const int j = e / n, i = e % n;
-      double l = 0.;
+      double lv = 0.;
       const double* cr = b.C;
       int f = 0;
       for (int k = 0; k < b.ncost; ++k) {
         const CRec C{cr};
+        const int t = C.type();
         const double wt = C.weight();
-        const double* wv = cost_weights(C, nx, nu);
-        if (C.type() == C_STATE) {
-          if (i == j) l += wt * wv[j];
-        } else if (C.type() == C_FRAME_PLACEMENT || C.type() == C_FRAME_TRANSLATION) {
+        const double* wv = cost_weights(b, C, nu);
+        if (jac_cost(b, t)) {
           if (i < nj && j < nj) {
-            const int nr = C.type() == C_FRAME_PLACEMENT ? 6 : 3;
+            const int nr = jac_rows(t);
             const double* Jk = Jf + (int64_t)f * 6 * nj;
             double s2 = 0.;
             for (int r = 0; r < nr; ++r) s2 += Jk[(int64_t)r * nj + i] * wv[r] * Jk[(int64_t)r * nj + j];
-            l += wt * s2;
+            lv += wt * s2;
           }
           ++f;
-        } else if (C.type() == C_CONTACT_FORCE && fd) {
+        }
+        if (t == C_STATE && i == j && !(b.ff && i < 6)) lv += wt * wv[j];
+        if (t == C_CONTACT_FORCE && fd && (int)C.d()[0] >= 0) {
           const int row0 = (int)C.d()[0], nr = (int)C.d()[1];
           double s2 = 0.;
           for (int r = 0; r < nr; ++r)
             s2 += dfx[(int64_t)(row0 + r) * L + i] * wv[r] * dfx[(int64_t)(row0 + r) * L + j];
-          l += wt * s2;
+          lv += wt * s2;
         }
         cr += C.size();
       }
-      Lxx[e] = integ ? sc * l : l;
+      Lxx[e] = integ ? sc * lv : lv;
     }
-    // Luu (diagonal), Lu, Lx
+    // Luu, Lu, Lx
     for (int e = lane; e < m * m; e += ex.nt) {
       const int j = e / m, i = e % m;
-      double l = 0.;
+      double lv = 0.;
       if (i < nu && j < nu) {
         const double* cr = b.C;
         for (int k = 0; k < b.ncost; ++k) {
           const CRec C{cr};
-          if (C.type() == C_CONTROL && i == j) l += C.weight() * cost_weights(C, nx, nu)[j];
-          if (C.type() == C_CONTACT_FORCE && fd) {
+          if (C.type() == C_CONTROL && i == j) lv += C.weight() * cost_weights(b, C, nu)[j];
+          if (C.type() == C_CONTACT_FORCE && fd && (int)C.d()[0] >= 0) {
             const int row0 = (int)C.d()[0], nr = (int)C.d()[1];
-            const double* wv = cost_weights(C, nx, nu);
+            const double* wv = cost_weights(b, C, nu);
             double s2 = 0.;
             for (int r = 0; r < nr; ++r)
               s2 += dfu[(int64_t)(row0 + r) * nj + i] * wv[r] * dfu[(int64_t)(row0 + r) * nj + j];
-            l += C.weight() * s2;
+            lv += C.weight() * s2;
           }
           cr += C.size();
         }
       }
-      Luu[e] = integ ? sc * l : l;
+      Luu[e] = integ ? sc * lv : lv;
     }
     if (lane < m) {
       const int j = lane;
@@ -1740,10 +2163,10 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
         const double* cr = b.C;
         for (int k = 0; k < b.ncost; ++k) {
           const CRec C{cr};
-          if (C.type() == C_CONTROL) lu += C.weight() * cost_weights(C, nx, nu)[j] * (u[j] - C.d()[j]);
-          if (C.type() == C_CONTACT_FORCE && fd) {
+          if (C.type() == C_CONTROL) lu += C.weight() * cost_weights(b, C, nu)[j] * (u[j] - C.d()[j]);
+          if (C.type() == C_CONTACT_FORCE && fd && (int)C.d()[0] >= 0) {
             const int row0 = (int)C.d()[0], nr = (int)C.d()[1];
-            const double* wv = cost_weights(C, nx, nu);
+            const double* wv = cost_weights(b, C, nu);
             for (int r = 0; r < nr; ++r)
               lu += C.weight() * dfu[(int64_t)(row0 + r) * nj + j] * wv[r] * (lam[row0 + r] - C.d()[2 + r]);
           }
@@ -1752,54 +2175,57 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
       }
       Lu[j] = integ ? sc * lu : lu;
     }
-    {
-      const int j = lane;
-      if (j < n) {
-        double lx = 0.;
-        const double* cr = b.C;
-        int f = 0;
-        for (int k = 0; k < b.ncost; ++k) {
-          const CRec C{cr};
-          const double wt = C.weight();
-          const double* wv = cost_weights(C, nx, nu);
-          if (C.type() == C_STATE) {
-            lx += wt * wv[j] * (x[j] - C.d()[j]);
-          } else if (C.type() == C_FRAME_PLACEMENT || C.type() == C_FRAME_TRANSLATION) {
-            const int nr = C.type() == C_FRAME_PLACEMENT ? 6 : 3;
-            if (j < nj) {
-              const double* Jk = Jf + (int64_t)f * 6 * nj;
-              for (int r = 0; r < nr; ++r) lx += wt * Jk[(int64_t)r * nj + j] * wv[r] * rf[6 * f + r];
-            }
-            ++f;
-          } else if (C.type() == C_CONTACT_FORCE && fd) {
-            const int row0 = (int)C.d()[0], nr = (int)C.d()[1];
-            for (int r = 0; r < nr; ++r)
-              lx += wt * dfx[(int64_t)(row0 + r) * L + j] * wv[r] * (lam[row0 + r] - C.d()[2 + r]);
+    for (int j = lane; j < n; j += ex.nt) {
+      double lx = 0.;
+      const double* cr = b.C;
+      int f = 0;
+      for (int k = 0; k < b.ncost; ++k) {
+        const CRec C{cr};
+        const int t = C.type();
+        const double wt = C.weight();
+        const double* wv = cost_weights(b, C, nu);
+        if (jac_cost(b, t)) {
+          if (j < nj) {
+            const int nr = jac_rows(t);
+            const double* Jk = Jf + (int64_t)f * 6 * nj;
+            for (int r = 0; r < nr; ++r) lx += wt * Jk[(int64_t)r * nj + j] * wv[r] * rf[6 * f + r];
           }
-          cr += C.size();
+          ++f;
         }
-        Lx[j] = integ ? sc * lx : lx;
+        if (t == C_STATE && !(b.ff && j < 6)) lx += wt * wv[j] * state_res(b, C.d(), x, j);
+        if (t == C_CONTACT_FORCE && fd && (int)C.d()[0] >= 0) {
+          const int row0 = (int)C.d()[0], nr = (int)C.d()[1];
+          for (int r = 0; r < nr; ++r)
+            lx += wt * dfx[(int64_t)(row0 + r) * L + j] * wv[r] * (lam[row0 + r] - C.d()[2 + r]);
+        }
+        cr += C.size();
       }
+      Lx[j] = integ ? sc * lx : lx;
     }
-    // the fused calc's cost: frame residuals from the Jacobian phase (cost-sum.hxx:89-117)
+    // the fused calc's cost: jac-cost residuals from the Jacobian phase (cost-sum.hxx:89-117)
     if (cost_out && lane == 0) {
       double total = 0.;
       const double* cr = b.C;
       int f = 0;
       for (int k = 0; k < b.ncost; ++k) {
         const CRec C{cr};
-        const double* wv = cost_weights(C, nx, nu);
+        const int t = C.type();
+        const double* wv = cost_weights(b, C, nu);
         double a = 0.;
-        if (C.type() == C_STATE) {
-          for (int i = 0; i < nx; ++i) a += wv[i] * (x[i] - C.d()[i]) * (x[i] - C.d()[i]);
-        } else if (C.type() == C_CONTROL) {
-          for (int i = 0; i < nu; ++i) a += wv[i] * (u[i] - C.d()[i]) * (u[i] - C.d()[i]);
-        } else if (C.type() == C_CONTACT_FORCE) {
-          if (nc > 0) a = 2. * force_cost_activation(C, lam, nx, nu);
-        } else {
-          const int nr = C.type() == C_FRAME_PLACEMENT ? 6 : 3;
+        if (jac_cost(b, t)) {
+          const int nr = jac_rows(t);
           for (int i = 0; i < nr; ++i) a += wv[i] * rf[6 * f + i] * rf[6 * f + i];
           ++f;
+        }
+        if (t == C_STATE) {
+          for (int i = b.ff ? 6 : 0; i < n; ++i) {
+            const double r = state_res(b, C.d(), x, i);
+            a += wv[i] * r * r;
+          }
+        } else if (t == C_CONTROL) {
+          for (int i = 0; i < nu; ++i) a += wv[i] * (u[i] - C.d()[i]) * (u[i] - C.d()[i]);
+        } else if (t == C_CONTACT_FORCE) {
+          a = 2. * force_cost_activation(b, C, lam, nu);
         }
         total += C.weight() * (0.5 * a);
         cr += C.size();
@@ -1807,12 +2233,13 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
       *cost_out = integ ? dt * total : total;
     }
   });
+  (void)nx;
 }
 
 __device__ inline void knot_calc_diff(const double* P, int nx, int m, const double* xg, const double* ug, bool use_u,
                                       double* w, double* Fx, double* Fu, double* Lxx, double* Lxu, double* Luu,
                                       double* Lx, double* Lu, double* xnext_out, double* cost_out) {
-  knot_calc_diff_x(DevExec{64}, P, nx, m, xg, ug, use_u, w, Fx, Fu, Lxx, Lxu, Luu, Lx, Lu, xnext_out, cost_out);
+  knot_calc_diff_x(DevExec{kMbDiffNT}, P, nx, m, xg, ug, use_u, w, Fx, Fu, Lxx, Lxu, Luu, Lx, Lu, xnext_out, cost_out);
 }
 
 }  // namespace mb

@@ -293,9 +293,7 @@ class IntegratedActionModelEuler(ActionModelAbstract):
                                       "and Euler(DifferentialActionModelFreeFwdDynamics) knots only; got "
                                       f"{type(diffModel).__name__}")
         if self._mb:
-            from .multibody import DifferentialActionModelContactFwdDynamics
-            self.kind = (_abi.KNOT_EULER_CONTACTFWD if isinstance(diffModel, DifferentialActionModelContactFwdDynamics)
-                         else _abi.KNOT_EULER_FREEFWD)
+            self.kind = diffModel.knot_kind
         super().__init__(diffModel.state, diffModel.nu, diffModel.nr)
         # the integrated model copies the differential model's limits (euler.hxx:25-26)
         self.u_lb = diffModel.u_lb
@@ -337,6 +335,7 @@ class IntegratedActionModelEuler(ActionModelAbstract):
     def pack(self):
         d = self.differential
         if self._mb:
+            self.kind = d.knot_kind
             return self.kind, d.nu, d.pack_body(self._dt)
         nq, nu, nx = d.nq, d.nu, d.state.nx
         parts = [_colmajor(d._Fq, nq, nq, "Fq"), _colmajor(d._Fv, nq, nq, "Fv"), _colmajor(d._Fu, nq, nu, "Fu"),

@@ -2,36 +2,42 @@
 
 The device computes these knots (crocoddyl_amd/csrc/multibody.hpp); the
 classes here hold the parameters, validate them like the reference, and pack
-the FDDP_KNOT_EULER_FREEFWD parameter block declared in include/fddp_hip.h.
+the multibody parameter blocks declared in include/fddp_hip.h.
 
 Reference API mirrored:
   StateMultibody(model)                         multibody/states/multibody.hxx
   ActuationModelFull(state)                     multibody/actuations/full.hpp
+  ActuationModelFloatingBase(state)             multibody/actuations/floating-base.hpp
   ActivationModelQuad(nr), ActivationModelWeightedQuad(weights)
                                                 core/activations/{quadratic,weighted-quadratic}.hpp
   CostModelSum(state, nu).addCost(name, cost, weight)   multibody/costs/cost-sum.hxx:18-85
   CostModelState / CostModelControl / CostModelFramePlacement / CostModelFrameTranslation
-                                                multibody/costs/{state,control,frame-placement,frame-translation}.hxx
+  / CostModelCoMPosition / CostModelContactForce / CostModelContactFrictionCone
+                                                multibody/costs/*.hxx
   FramePlacement(id, SE3), FrameTranslation(id, p)      multibody/frames.hpp
   DifferentialActionModelFreeFwdDynamics(state, actuation, costs)  .armature
                                                 multibody/actions/free-fwddyn.hxx:24-160
 Pinocchio is not available offline, so ``RobotModel`` stands in for
-``pinocchio.Model`` over the subset the device covers: a fixed-base
-kinematic tree of revolute joints (any unit axis), with joint placements,
-body inertias, operational frames and gravity. Joint and frame indices
-follow Pinocchio's (joint 0 / frame 0 = universe).
+``pinocchio.Model`` over the subset the device covers: a kinematic tree of
+revolute joints (any unit axis) below either the universe or a free-flyer root
+(JointModelFreeFlyer: q = (p, quat xyzw), v = base twist), with joint
+placements, body inertias, operational frames and gravity. Joint and frame
+indices follow Pinocchio's (joint 0 / frame 0 = universe).
 """
 import numpy as np
 
 from . import _abi
 
-JOINT_REC = 26
+JOINT_REC = 27
+JOINT_REVOLUTE, JOINT_FREEFLYER = 0, 1
 COST_HDR = 4
 COST_STATE, COST_CONTROL, COST_FRAME_PLACEMENT, COST_FRAME_TRANSLATION = 1, 2, 3, 4
 CONTACT_3D, CONTACT_6D = 5, 6
 COST_CONTACT_FORCE = 7
+COST_COM_POSITION = 8
+COST_FRICTION_CONE = 9
 MAX_CONTACT_ROWS = 24
-MAX_JOINTS = 32
+MAX_DOFS = 64  # nv of the device path (one lane per tangent direction of a wave pair)
 
 
 class SE3:
@@ -89,18 +95,52 @@ class Inertia:
         return Inertia(m, c, shift(self.inertia, self.mass, self.lever) + shift(o.inertia, o.mass, o.lever))
 
 
-class RobotModel:
-    """Stand-in for pinocchio.Model over fixed-base revolute trees."""
+class JointModelFreeFlyer:
+    """pinocchio::JointModelFreeFlyer: 6 dofs, q = (p, quaternion x y z w)."""
+    nq, nv = 7, 6
 
-    def __init__(self):
+
+class JointModelRevoluteUnaligned:
+    """pinocchio::JointModelRevoluteUnaligned(axis)."""
+    nq, nv = 1, 1
+
+    def __init__(self, *axis):
+        ax = np.array(axis[0] if len(axis) == 1 else axis, np.float64).reshape(3)
+        n = np.linalg.norm(ax)
+        if n == 0:
+            raise ValueError("Invalid argument: zero joint axis")
+        self.axis = ax / n
+
+
+def JointModelRX():
+    return JointModelRevoluteUnaligned((1.0, 0.0, 0.0))
+
+
+def JointModelRY():
+    return JointModelRevoluteUnaligned((0.0, 1.0, 0.0))
+
+
+def JointModelRZ():
+    return JointModelRevoluteUnaligned((0.0, 0.0, 1.0))
+
+
+class RobotModel:
+    """Stand-in for pinocchio.Model: revolute trees, optionally below a
+    free-flyer root (the only joint allowed to be a JointModelFreeFlyer)."""
+
+    def __init__(self, root_joint=None):
         self.names = ["universe"]
         self.parents = [0]
+        self.kinds = [JOINT_REVOLUTE]
         self.axes = [np.zeros(3)]
         self.jointPlacements = [SE3()]
         self.inertias = [Inertia.Zero()]
         self.frames = [("universe", 0, SE3())]
         self.gravity = np.array([0.0, 0.0, -9.81])  # pinocchio Model::gravity981
+        self.referenceConfigurations = {}
         self._version = 0
+        if root_joint is not None:  # pinocchio::buildModel(urdf, JointModelFreeFlyer(), model)
+            self.addJoint(0, root_joint, SE3(), "root_joint")
 
     @property
     def njoints(self):
@@ -108,29 +148,55 @@ class RobotModel:
 
     @property
     def nq(self):
-        return self.njoints - 1
+        return sum(7 if k == JOINT_FREEFLYER else 1 for k in self.kinds[1:])
 
-    nv = nq
+    @property
+    def nv(self):
+        return sum(6 if k == JOINT_FREEFLYER else 1 for k in self.kinds[1:])
 
-    def addJoint(self, parent_id, axis, placement, name):
-        """Revolute joint about the unit ``axis`` (joint frame), placed at
-        ``placement`` in the parent joint's frame. Returns its index."""
+    @property
+    def has_freeflyer(self):
+        return self.njoints > 1 and self.kinds[1] == JOINT_FREEFLYER
+
+    def idx_q(self, j):
+        """Model::idx_qs[j]: first configuration index of joint j."""
+        return sum(7 if k == JOINT_FREEFLYER else 1 for k in self.kinds[1:j])
+
+    def idx_v(self, j):
+        """Model::idx_vs[j]: first velocity index of joint j."""
+        return sum(6 if k == JOINT_FREEFLYER else 1 for k in self.kinds[1:j])
+
+    def addJoint(self, parent_id, joint, placement, name):
+        """pinocchio Model::addJoint(parent, joint_model, placement, name):
+        ``joint`` is a JointModelFreeFlyer / JointModelRevoluteUnaligned (or a
+        bare axis, a revolute joint about it), placed at ``placement`` in the
+        parent joint's frame. Returns its index."""
         parent_id = int(parent_id)
         if not 0 <= parent_id < self.njoints:
             raise ValueError("Invalid argument: unknown parent joint")
-        if self.nq >= MAX_JOINTS:
-            raise ValueError(f"Invalid argument: the device path holds at most {MAX_JOINTS} joints")
-        ax = np.array(axis, np.float64).reshape(3)
-        nrm = np.linalg.norm(ax)
-        if nrm == 0:
-            raise ValueError("Invalid argument: zero joint axis")
+        if isinstance(joint, JointModelFreeFlyer) or joint is JointModelFreeFlyer:
+            if self.njoints != 1 or parent_id != 0:
+                raise ValueError("Invalid argument: the device path takes a free-flyer as the root joint only")
+            kind, ax, nvj = JOINT_FREEFLYER, np.zeros(3), 6
+        else:
+            if not isinstance(joint, JointModelRevoluteUnaligned):
+                joint = JointModelRevoluteUnaligned(joint)
+            kind, ax, nvj = JOINT_REVOLUTE, joint.axis, 1
+        if self.nv + nvj > MAX_DOFS:
+            raise ValueError(f"Invalid argument: the device path holds at most {MAX_DOFS} dofs")
         self.names.append(str(name))
         self.parents.append(parent_id)
-        self.axes.append(ax / nrm)
+        self.kinds.append(kind)
+        self.axes.append(ax)
         self.jointPlacements.append(placement if placement is not None else SE3())
         self.inertias.append(Inertia.Zero())
         self._version += 1
         return self.njoints - 1
+
+    def getJointId(self, name):
+        if name in self.names:
+            return self.names.index(name)
+        return self.njoints
 
     def appendBodyToJoint(self, joint_id, inertia, placement=None):
         """pinocchio Model::appendBodyToJoint: add a body (inertia given in
@@ -153,18 +219,123 @@ class RobotModel:
     def existFrame(self, name):
         return any(f[0] == name for f in self.frames)
 
+    def neutral(self):
+        """pinocchio::neutral: identity quaternion for the free-flyer, zeros else."""
+        q = np.zeros(self.nq)
+        if self.has_freeflyer:
+            q[6] = 1.0
+        return q
+
+    def placements(self, q):
+        """oMi of every joint (pinocchio::forwardKinematics, host side)."""
+        q = np.asarray(q, float)
+        out = [SE3()]
+        for j in range(1, self.njoints):
+            iq = self.idx_q(j)
+            if self.kinds[j] == JOINT_FREEFLYER:
+                Mj = SE3(_quat_to_R(q[iq + 3:iq + 7]), q[iq:iq + 3])
+            else:
+                Mj = SE3(_rot_axis(self.axes[j], q[iq]))
+            out.append(out[self.parents[j]] * (self.jointPlacements[j] * Mj))
+        return out
+
+    def framePlacement(self, q, frame_id):
+        name, pj, pl = self.frames[frame_id]
+        return self.placements(q)[pj] * pl
+
+    def centerOfMass(self, q):
+        oM = self.placements(q)
+        mt = sum(I.mass for I in self.inertias)
+        c = sum(I.mass * (oM[j].translation + oM[j].rotation @ I.lever) for j, I in enumerate(self.inertias))
+        return c / mt
+
     def pack_robot(self, armature):
-        """gravity(3) armature(nv) then one 26-double record per joint."""
+        """gravity(3) armature(nv) then one 27-double record per joint:
+        [type, parent record (-1 universe), axis(3), placement R(9) p(3), mass, CoM(3), I(6)]."""
         nv = self.nv
         rows = [self.gravity, np.asarray(armature, float).reshape(nv)]
         for j in range(1, self.njoints):
             P = self.jointPlacements[j]
             I = self.inertias[j]
             Ic = I.inertia
-            rows.append(np.concatenate([[self.parents[j] - 1], self.axes[j], P.rotation.T.reshape(-1),
-                                        P.translation, [I.mass], I.lever,
+            rows.append(np.concatenate([[self.kinds[j], self.parents[j] - 1], self.axes[j],
+                                        P.rotation.T.reshape(-1), P.translation, [I.mass], I.lever,
                                         [Ic[0, 0], Ic[1, 1], Ic[2, 2], Ic[0, 1], Ic[0, 2], Ic[1, 2]]]))
         return np.concatenate(rows)
+
+
+def _skew(w):
+    return np.array([[0.0, -w[2], w[1]], [w[2], 0.0, -w[0]], [-w[1], w[0], 0.0]])
+
+
+def _rot_axis(ax, q):
+    K = _skew(ax)
+    return np.eye(3) + np.sin(q) * K + (1 - np.cos(q)) * (K @ K)
+
+
+def _quat_to_R(qv):
+    x, y, z, w = qv
+    return np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w)],
+                     [2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w)],
+                     [2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)]])
+
+
+def _R_to_quat(R):
+    t = np.trace(R)
+    if t > 0:
+        s = np.sqrt(t + 1.0)
+        w = 0.5 * s
+        s = 0.5 / s
+        return np.array([(R[2, 1] - R[1, 2]) * s, (R[0, 2] - R[2, 0]) * s, (R[1, 0] - R[0, 1]) * s, w])
+    i = int(np.argmax([R[0, 0], R[1, 1], R[2, 2]]))
+    j, k = (i + 1) % 3, (i + 2) % 3
+    s = np.sqrt(R[i, i] - R[j, j] - R[k, k] + 1.0)
+    q = np.zeros(4)
+    q[i] = 0.5 * s
+    s = 0.5 / s
+    q[3] = (R[k, j] - R[j, k]) * s
+    q[j] = (R[j, i] + R[i, j]) * s
+    q[k] = (R[k, i] + R[i, k]) * s
+    return q
+
+
+def _exp6(nu):
+    v, w = np.asarray(nu[:3], float), np.asarray(nu[3:], float)
+    t2 = w @ w
+    if t2 < 1e-8:
+        ct, st_t = 1 - t2 / 2 + t2 * t2 / 24, 1 - t2 / 6 + t2 * t2 / 120
+        a_wxv, a_w = 0.5 - t2 / 24 + t2 * t2 / 720, 1.0 / 6 - t2 / 120 + t2 * t2 / 5040
+    else:
+        t = np.sqrt(t2)
+        ct, st_t = np.cos(t), np.sin(t) / t
+        a_wxv, a_w = (1 - ct) / t2, (1 - st_t) / t2
+    R = ct * np.eye(3) + a_wxv * np.outer(w, w) + st_t * _skew(w)
+    return R, st_t * v + a_w * (w @ v) * w + a_wxv * np.cross(w, v)
+
+
+def _log6(R, p):
+    c = 0.5 * (np.trace(R) - 1)
+    wv = np.array([R[2, 1] - R[1, 2], R[0, 2] - R[2, 0], R[1, 0] - R[0, 1]])
+    s = 0.5 * np.linalg.norm(wv)
+    th = np.arctan2(s, c)
+    if s < 1e-8 and c > 0:
+        w = 0.5 * (1 + s * s / 6) * wv
+    elif s < 1e-8:
+        th = np.arccos(max(-1.0, min(1.0, c)))
+        ax = np.sqrt(np.maximum((np.diag(R) - c) / (1 - c), 0))
+        i0 = int(np.argmax(ax))
+        sg = np.array([1.0 if j == i0 else (1.0 if R[i0, j] + R[j, i0] >= 0 else -1.0) for j in range(3)])
+        w = (th if wv[i0] >= 0 else -th) * sg * ax
+    else:
+        w = th / (2 * s) * wv
+    t2 = w @ w
+    if t2 < 1e-2:
+        beta = 1.0 / 12 + t2 / 720 + t2 * t2 / 30240
+    else:
+        t = np.sqrt(t2)
+        beta = 1 / t2 - np.sin(t) / (2 * t * (1 - np.cos(t)))
+    W = _skew(w)
+    return np.concatenate([(np.eye(3) - 0.5 * W + beta * W @ W) @ p, w])
 
 
 def sample_talos_arm():
@@ -192,12 +363,18 @@ def sample_talos_arm():
     return m
 
 
-def sample_tree(nj, seed=0, branching=True):
-    """Random kinematic tree (tests): random axes, placements and inertias."""
+def sample_tree(nj, seed=0, branching=True, freeflyer=False):
+    """Random kinematic tree (tests): random axes, placements and inertias; with
+    ``freeflyer`` the nj revolute joints hang below a free-flyer base (joint 1)."""
     rng = np.random.default_rng(seed)
-    m = RobotModel()
-    for j in range(1, nj + 1):
-        parent = int(rng.integers(0, j)) if branching else j - 1
+    m = RobotModel(JointModelFreeFlyer() if freeflyer else None)
+    if freeflyer:
+        A = rng.normal(size=(3, 3)) * 0.1
+        m.appendBodyToJoint(1, Inertia(rng.uniform(2.0, 6.0), rng.uniform(-0.05, 0.05, 3), A @ A.T + 0.05 * np.eye(3)))
+    first = m.njoints
+    for j in range(first, first + nj):
+        lo = 1 if freeflyer else 0
+        parent = int(rng.integers(lo, j)) if branching else j - 1
         ax = rng.normal(size=3)
         ang = rng.normal(size=3) * 0.5
         t = np.linalg.norm(ang)
@@ -207,14 +384,15 @@ def sample_tree(nj, seed=0, branching=True):
         A = rng.normal(size=(3, 3)) * 0.05
         m.appendBodyToJoint(jid, Inertia(rng.uniform(0.3, 3.0), rng.uniform(-0.1, 0.1, 3),
                                          A @ A.T + 0.01 * np.eye(3)))
-    m.addFrame("tip", nj, SE3(np.eye(3), (0.0, 0.0, -0.1)))
+    m.addFrame("tip", m.njoints - 1, SE3(np.eye(3), (0.0, 0.0, -0.1)))
     return m
 
 
 class StateMultibody:
-    """StateMultibody over a revolute-only model: q and v spaces coincide,
-    so diff / integrate are Euclidean (multibody.hxx:54-91 with Pinocchio's
-    revolute difference / integrate)."""
+    """StateMultibody (multibody.hxx:14-240): x = (q, v), nx = nq + nv,
+    ndx = 2 nv; diff / integrate are pinocchio::difference / integrate
+    (multibody.hxx:54-91): Euclidean on revolute joints, SE(3) (M0^-1 M1 ->
+    log6, M exp6(dq)) on a free-flyer root."""
 
     def __init__(self, model):
         if not isinstance(model, RobotModel):
@@ -226,34 +404,60 @@ class StateMultibody:
         self.ndx = 2 * self.nv
 
     def zero(self):
-        return np.zeros(self.nx)
+        return np.concatenate([self.pinocchio.neutral(), np.zeros(self.nv)])
 
     def rand(self):
-        return np.concatenate([np.random.uniform(-np.pi, np.pi, self.nq), np.random.uniform(-1, 1, self.nv)])
+        q = np.random.uniform(-np.pi, np.pi, self.nq)
+        if self.pinocchio.has_freeflyer:
+            q[:3] = np.random.uniform(-1, 1, 3)
+            qq = np.random.normal(size=4)
+            q[3:7] = qq / np.linalg.norm(qq)
+        return np.concatenate([q, np.random.uniform(-1, 1, self.nv)])
 
     def diff(self, x0, x1):
-        return np.asarray(x1, float) - np.asarray(x0, float)
+        x0, x1 = np.asarray(x0, float), np.asarray(x1, float)
+        nq = self.nq
+        dq = x1[:nq] - x0[:nq]
+        if self.pinocchio.has_freeflyer:
+            R0, R1 = _quat_to_R(x0[3:7]), _quat_to_R(x1[3:7])
+            dq = np.concatenate([_log6(R0.T @ R1, R0.T @ (x1[:3] - x0[:3])), dq[7:]])
+        return np.concatenate([dq, x1[nq:] - x0[nq:]])
 
     def integrate(self, x, dx):
-        return np.asarray(x, float) + np.asarray(dx, float)
+        x, dx = np.asarray(x, float), np.asarray(dx, float)
+        nq, nv = self.nq, self.nv
+        if self.pinocchio.has_freeflyer:
+            R0 = _quat_to_R(x[3:7])
+            Re, pe = _exp6(dx[:6])
+            qn = _R_to_quat(R0 @ Re)
+            if qn @ x[3:7] < 0:
+                qn = -qn
+            qn *= (3 - qn @ qn) / 2
+            q = np.concatenate([x[:3] + R0 @ pe, qn, x[7:nq] + dx[6:nv]])
+        else:
+            q = x[:nq] + dx[:nv]
+        return np.concatenate([q, x[nq:] + dx[nv:]])
 
 
 class ActuationModelFull:
     """ActuationModelFull: tau = u, nu = nv."""
 
     def __init__(self, state):
+        if state.pinocchio.has_freeflyer:
+            raise ValueError("Invalid argument: the first joint cannot be a free-flyer")
         self.state = state
         self.nu = state.nv
 
 
 class ActuationModelFloatingBase:
-    """ActuationModelFloatingBase (actuations/floating-base.hpp:29-40): the
-    first joint's dofs are unactuated, tau = [0; u], nu = nv - nv(joint 1).
-    Over the revolute-only models covered here joint 1 has one dof."""
+    """ActuationModelFloatingBase (actuations/floating-base.hpp:29-61): the
+    root joint's dofs are unactuated, tau = [0; u], nu = nv - nv(joint 1)
+    (6 for a free-flyer root, 1 for a revolute one)."""
 
     def __init__(self, state):
         self.state = state
-        self.nun = 1
+        model = state.pinocchio
+        self.nun = 6 if model.has_freeflyer else 1
         self.nu = state.nv - self.nun
 
 
@@ -414,6 +618,25 @@ class CostModelFrameTranslation(_Cost):
         return [frame, _rows(self.xref.translation, 3)]
 
 
+class CostModelCoMPosition(_Cost):
+    """r = com(q) - cref (com-position.hxx:49-75): Rx = [Jcom, 0]."""
+
+    type = COST_COM_POSITION
+
+    def __init__(self, state, *args, **kw):
+        act, ref, nu = _cost_args(args, kw)
+        ref = kw.get("cref", ref)
+        if ref is None:
+            raise TypeError("CostModelCoMPosition needs a reference position cref")
+        super().__init__(state, act, 3, nu)
+        self.cref = np.array(ref, np.float64)
+        if self.cref.shape[-1] != 3:
+            raise ValueError("Invalid argument: cref has wrong dimension (it should be 3)")
+
+    def _payload(self):
+        return [_rows(self.cref, 3)]
+
+
 class FrameForce:
     """FrameForce (multibody/frames.hpp): frame id and a spatial force (linear, angular)."""
 
@@ -448,14 +671,18 @@ class CostModelContactForce(_Cost):
             raise TypeError("CostModelContactForce needs a FrameForce reference")
         if act is not None:  # (state, activation, fref[, nu])
             nr, nu = act.nr, (ints[0] if ints else None)
-        else:  # (state, fref[, nc[, nu]])
-            nr = ints[0] if ints else 3
+        else:  # (state, fref[, nc[, nu]]): ActivationModelQuad(6) by default (contact-force.hxx:57-59)
+            nr = ints[0] if ints else 6
             nu = ints[1] if len(ints) > 1 else None
         nu = kw.get("nu", nu)
         if nr not in (3, 6):
             raise ValueError("Invalid argument: nr has to be 3 or 6 (the contact's force)")
         super().__init__(state, act, nr, nu)
         self.fref = fref
+
+    @property
+    def frame_id(self):
+        return self.fref.id
 
     def _payload(self):  # the contact row offset is resolved by the DAM (pack_body)
         return [np.concatenate([[-1.0, self.activation.nr], self.fref.force]).reshape(1, -1)]
@@ -518,9 +745,17 @@ class DifferentialActionModelFreeFwdDynamics:
     (tau - nle) once an armature is set), cost = costs.calc(x, u)."""
 
     def __init__(self, state, actuation, costs):
-        if not isinstance(actuation, ActuationModelFull):
-            raise NotImplementedError("crocoddyl_amd: the device path covers ActuationModelFull only")
+        if not isinstance(actuation, (ActuationModelFull, ActuationModelFloatingBase)):
+            raise NotImplementedError("crocoddyl_amd: the device path covers ActuationModelFull and "
+                                      "ActuationModelFloatingBase only")
         self._init_dam(state, actuation, costs)
+
+    @property
+    def knot_kind(self):
+        """Device knot kind of Euler(this DAM): free dynamics with a floating-base
+        actuation is the contact knot with an empty ContactModelMultiple."""
+        return _abi.KNOT_EULER_FREEFWD if isinstance(self.actuation, ActuationModelFull) else \
+            _abi.KNOT_EULER_CONTACTFWD
 
     def _init_dam(self, state, actuation, costs):
         if costs.nu != actuation.nu:
@@ -556,7 +791,10 @@ class DifferentialActionModelFreeFwdDynamics:
                 tuple(getattr(c.cost, "_version", 0) for c in self.costs.costs.values()))
 
     def pack_body(self, dt):
-        """(Bm, size) rows of the FDDP_KNOT_EULER_FREEFWD block for step dt."""
+        """(Bm, size) rows of the FDDP_KNOT_EULER_FREEFWD block for step dt (with a
+        floating-base actuation: the FDDP_KNOT_EULER_CONTACTFWD block, no contacts)."""
+        if isinstance(self.actuation, ActuationModelFloatingBase):
+            return _pack_mb(self.state, self._armature, self.costs, dt, [self.actuation.nun, 0.0, 0.0, 0.0])
         return _pack_mb(self.state, self._armature, self.costs, dt)
 
 
@@ -729,9 +967,11 @@ class DifferentialActionModelContactFwdDynamics(DifferentialActionModelFreeFwdDy
         return super().version() + (self.contacts._version, self.JMinvJt_damping,
                                     tuple(c.contact.gains.tobytes() for c in self.contacts.contacts.values()))
 
+    knot_kind = _abi.KNOT_EULER_CONTACTFWD
+
     def pack_body(self, dt):
         """(Bm, size) rows of the FDDP_KNOT_EULER_CONTACTFWD block: the
-        FDDP_KNOT_EULER_FREEFWD layout, then [nun, damping, ncontact, 0] and the
+        FDDP_KNOT_EULER_FREEFWD layout, then [nun, damping, ncontact, flag] and the
         active contact records in name order."""
         recs = self.contacts.pack()
         if self.contacts.nc > MAX_CONTACT_ROWS:
@@ -739,28 +979,39 @@ class DifferentialActionModelContactFwdDynamics(DifferentialActionModelFreeFwdDy
         sec = np.concatenate([[self.actuation.nun, self.JMinvJt_damping, len(recs), 2.0 if self.enable_force else 0.0]]
                              + recs)
         out = _pack_mb(self.state, self._armature, self.costs, dt, sec)
-        # contact-force costs: the row offset of the active contact on fref.id (contact-force.hxx createData)
+        # costs on a contact's force: the row offset of the contact on fref.id among the
+        # active contacts; a contact that exists but is inactive has f = 0 and zero force
+        # Jacobians (contact-force.hxx createData looks the frame up among all contacts,
+        # the first match in name order; updateForce / setZeroForceDiff)
         rows, r0 = {}, 0
         for n in self.contacts.active:
             c = self.contacts.contacts[n].contact
-            rows[c._ref.id] = (r0, c.nc)
+            rows.setdefault(c._ref.id, (r0, c.nc))
             r0 += c.nc
-        o = _abi.PARAM_HEADER + 3 + self.state.nv + JOINT_REC * self.state.nv
+        for n in self.contacts.inactive:
+            c = self.contacts.contacts[n].contact
+            rows.setdefault(c._ref.id, (INACTIVE_FORCE_ROW, c.nc))
+        o = _abi.PARAM_HEADER + 3 + self.state.nv + JOINT_REC * (self.state.pinocchio.njoints - 1)
         for name in sorted(self.costs.costs):
             it = self.costs.costs[name]
             if not it.active:
                 continue
             size = int(out[0, o + 3])
-            if it.cost.type == COST_CONTACT_FORCE:
-                fid = it.cost.fref.id
+            if it.cost.type in (COST_CONTACT_FORCE, COST_FRICTION_CONE):
+                fid = it.cost.frame_id
                 if fid not in rows:
                     raise ValueError(f"Invalid argument: there is not contact defined for frame {fid}")
                 row0, nci = rows[fid]
-                if nci != it.cost.activation.nr:
+                if it.cost.type == COST_CONTACT_FORCE and nci != it.cost.activation.nr:
                     raise ValueError("Invalid argument: the contact-force cost and its contact differ in size")
                 out[:, o + COST_HDR] = row0
+                if it.cost.type == COST_FRICTION_CONE:
+                    out[:, o + COST_HDR + 1] = nci
             o += size
         return out
+
+
+INACTIVE_FORCE_ROW = -2  # contact exists but is inactive: lambda = 0, zero force Jacobians
 
 
 class _Impulse:

@@ -284,3 +284,75 @@ def build_arm(T=None, B=None, seed=None, robot=None, dt=1e-3, weighted=False, ar
     terminal = IntegratedActionModelEuler(dam, 0.0)
     x0s = np.hstack([rng.uniform(-1, 1, (B, state.nq)), rng.uniform(-1, 1, (B, state.nv))])
     return x0s, [running] * T, terminal
+
+
+def random_floating_state(model, rng, B, spread=0.3, v_spread=0.5):
+    """(B, nq + nv) states around the neutral configuration: the free-flyer pose
+    integrated along a random twist (unit quaternion), joint angles and velocities
+    uniform in [-spread, spread] / [-v_spread, v_spread]."""
+    from . import multibody as mb
+    state = mb.StateMultibody(model)
+    x0 = state.zero()
+    out = np.zeros((B, state.nx))
+    for b in range(B):
+        dx = np.concatenate([rng.uniform(-spread, spread, state.nv), rng.uniform(-v_spread, v_spread, state.nv)])
+        out[b] = state.integrate(x0, dx)
+    return out
+
+
+def build_floating(T=4, B=2, seed=0, robot=None, dt=1e-2, contacts=(), gains=(2.0, 1.5), damping=0.0,
+                   weighted=False, com=False, force_costs=False, enable_force=None, armature=None, spread=0.3):
+    """Floating-base knots (the reference's legged-robot models, on a tree below a
+    free-flyer root): Euler(dt) ∘ DifferentialAction{Free,Contact}FwdDynamics with
+    ActuationModelFloatingBase (nu = nv - 6). ``contacts``: ("6d" | "3d", frame
+    name) pairs -> ContactModel6D / 3D; none: free dynamics. Costs: xReg (to a
+    non-neutral reference state, weighted with ``weighted``), uReg, a tip
+    FramePlacement (+ a FrameTranslation when ``weighted``), CoMPosition with
+    ``com``, a CostModelContactForce per contact with ``force_costs``. The
+    terminal model is the same DAM with dt = 0."""
+    from . import multibody as mb
+    rng = np.random.default_rng(seed)
+    model = mb.sample_tree(5, seed=3, freeflyer=True) if robot is None else robot
+    if not model.existFrame("mid_site"):
+        model.addFrame("mid_site", min(3, model.njoints - 1), mb.SE3(np.eye(3), (0.0, 0.05, -0.1)))
+    state = mb.StateMultibody(model)
+    act = mb.ActuationModelFloatingBase(state)
+    nu = act.nu
+    tip = model.getFrameId("tip")
+    xref = random_floating_state(model, rng, 1, spread=0.5, v_spread=0.2)[0]
+    costs = mb.CostModelSum(state, nu)
+    if weighted:
+        costs.addCost("xReg", mb.CostModelState(state, mb.ActivationModelWeightedQuad(
+            np.linspace(0.5, 2.0, state.ndx)), xref, nu), 1e-2)
+        costs.addCost("midTrans", mb.CostModelFrameTranslation(state, mb.FrameTranslation(
+            model.getFrameId("mid_site"), (0.1, 0.0, 0.2)), nu), 0.3)
+    else:
+        costs.addCost("xReg", mb.CostModelState(state, xref, nu), 1e-2)
+    costs.addCost("uReg", mb.CostModelControl(state, nu), 1e-3)
+    costs.addCost("tipPose", mb.CostModelFramePlacement(state, mb.FramePlacement(
+        tip, mb.SE3(mb._rot_axis(np.array([0.0, 0.6, 0.8]), 0.4), (0.2, -0.1, 0.3))), nu), 0.5)
+    if com:
+        costs.addCost("comTrack", mb.CostModelCoMPosition(state, (0.05, -0.02, 0.1), nu), 2.0)
+    if contacts:
+        cm = mb.ContactModelMultiple(state, nu)
+        for i, (kind, fname) in enumerate(contacts):
+            fid = model.getFrameId(fname)
+            if kind == "6d":
+                c = mb.ContactModel6D(state, mb.FramePlacement(fid, mb.SE3(np.eye(3), (0.1, 0.2, 0.3))), nu, gains)
+            else:
+                c = mb.ContactModel3D(state, mb.FrameTranslation(fid, (0.1, 0.2, 0.3)), nu, gains)
+            cm.addContact(f"c{i}_{fname}", c)
+            if force_costs:
+                nr = 6 if kind == "6d" else 3
+                costs.addCost(f"force{i}", mb.CostModelContactForce(
+                    state, mb.FrameForce(fid, rng.uniform(-1, 1, 6)), nr, nu), 1e-3)
+        dam = mb.DifferentialActionModelContactFwdDynamics(state, act, cm, costs, damping,
+                                                           force_costs if enable_force is None else enable_force)
+    else:
+        dam = mb.DifferentialActionModelFreeFwdDynamics(state, act, costs)
+    if armature is not None:
+        dam.armature = armature
+    running = IntegratedActionModelEuler(dam, dt)
+    terminal = IntegratedActionModelEuler(dam, 0.0)
+    x0s = random_floating_state(model, rng, B, spread=spread)
+    return x0s, [running] * T, terminal

@@ -99,6 +99,16 @@ class Knot:
         else:
             raise ValueError(kind)
 
+    # StateVector (core/states/euclidean.hxx:28-61)
+    def state_diff(self, x0, x1):
+        return x1 - x0
+
+    def state_integrate(self, x, dx):
+        return x + dx
+
+    def state_zero(self):
+        return np.zeros(self.nx)
+
     # -- calc: returns (xnext, cost) -------------------------------------
     def calc(self, x, u=None):
         if u is None:
@@ -265,10 +275,12 @@ class FDDP:
         self.Quu_inv = [np.zeros((m.nu, m.nu)) for m in models[:-1]]
         self.T = len(models) - 1
         self.nx = models[0].nx
+        self.ndx = models[0].ndx
+        self.st = models[0]  # the problem's state: diff / integrate / zero (StateAbstract)
         self.nu_max = max(m.nu for m in models[:-1])
         self.p = params or default_params()
-        T, n = self.T, self.nx
-        self.xs = [np.zeros(n) for _ in range(T + 1)]
+        T, n = self.T, self.ndx
+        self.xs = [np.zeros(self.nx) for _ in range(T + 1)]
         self.us = [np.zeros(self.nu_max) for _ in range(T)]
         self.is_feasible = False
         self.was_feasible = False
@@ -278,7 +290,7 @@ class FDDP:
         self.steplength = 1.0
         self.iter = 0
         self.fs = [np.zeros(n) for _ in range(T + 1)]
-        self.xnext = [np.zeros(n) for _ in range(T)]
+        self.xnext = [np.zeros(self.nx) for _ in range(T)]
         self.trace = []
         self.status = 0
 
@@ -315,17 +327,17 @@ class FDDP:
         if self.iter == 0:
             self.problem_calc(self.xs, self.us)
         self.cost = self.problem_calc_diff(self.xs, self.us)
-        if not self.is_feasible:
-            self.fs[0] = self.x0 - self.xs[0]
+        if not self.is_feasible:  # fs[0] = diff(xs[0], x0), fs[t+1] = diff(xs[t+1], xnext[t])
+            self.fs[0] = self.st.state_diff(self.xs[0], self.x0)
             for t in range(self.T):
-                self.fs[t + 1] = self.xnext[t] - self.xs[t + 1]
+                self.fs[t + 1] = self.st.state_diff(self.xs[t + 1], self.xnext[t])
         elif not self.was_feasible:
-            self.fs = [np.zeros(self.nx) for _ in range(self.T + 1)]
+            self.fs = [np.zeros(self.ndx) for _ in range(self.T + 1)]
         return self.cost
 
     def backward_pass(self):
         """ddp.cpp:180-253; returns False on backward_error."""
-        T, n = self.T, self.nx
+        T, n = self.T, self.ndx
         dT = self.data[T]
         self.Vxx = [None] * (T + 1)
         self.Vx = [None] * (T + 1)
@@ -425,9 +437,9 @@ class FDDP:
             if self.is_feasible or alpha == 1:
                 xt = xnext.copy()
             else:
-                xt = xnext + self.fs[t] * (alpha - 1)
+                xt = self.st.state_integrate(xnext, self.fs[t] * (alpha - 1))
             self.xs_try[t] = xt
-            dx = xt - self.xs[t]
+            dx = self.st.state_diff(self.xs[t], xt)
             if m.nu != 0:
                 u = (self.us[t][:m.nu] - self.k[t] * alpha) - self.K[t] @ dx
                 if self.box and self.haslim[t]:  # box-fddp.cpp:100-102
@@ -444,7 +456,7 @@ class FDDP:
         if self.is_feasible or alpha == 1:
             xT = xnext.copy()
         else:
-            xT = xnext + self.fs[T] * (alpha - 1)
+            xT = self.st.state_integrate(xnext, self.fs[T] * (alpha - 1))
         self.xs_try[T] = xT
         _, cT = self.models[T].calc(xT)
         costs[T] = cT
@@ -480,11 +492,11 @@ class FDDP:
         """fddp.cpp:107-124."""
         dv = 0.0
         T = self.T
-        if not self.is_feasible:
-            dx = self.xs[T] - self.xs_try[T]
+        if not self.is_feasible:  # dx = diff(xs_try, xs)
+            dx = self.st.state_diff(self.xs_try[T], self.xs[T])
             dv -= self.fs[T] @ (self.Vxx[T] @ dx)
             for t in range(T):
-                dx = self.xs[t] - self.xs_try[t]
+                dx = self.st.state_diff(self.xs_try[t], self.xs[t])
                 dv -= self.fs[t] @ (self.Vxx[t] @ dx)
         self.d = np.array([self.dg + dv, self.dq - 2 * dv])
         return self.d
@@ -506,7 +518,7 @@ class FDDP:
 
     def set_candidate(self, xs=None, us=None, is_feasible=False):
         T = self.T
-        self.xs = [np.zeros(self.nx) for _ in range(T + 1)] if xs is None else [np.array(x, float) for x in xs]
+        self.xs = [self.st.state_zero() for _ in range(T + 1)] if xs is None else [np.array(x, float) for x in xs]
         self.us = [np.zeros(self.nu_max) for _ in range(T)] if us is None else [np.array(u, float) for u in us]
         self.is_feasible = is_feasible
 

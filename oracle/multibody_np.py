@@ -1,48 +1,66 @@
-"""ORACLE — TEST INFRASTRUCTURE ONLY (numpy restatement of the multibody knot).
+"""ORACLE — TEST INFRASTRUCTURE ONLY (numpy restatement of the multibody knots).
 
-CPU restatement of the knot the reference builds in
-benchmark/factory/arm.hpp:31-96 and the Talos-arm config (C3):
+CPU restatement of the knots the reference builds in
+benchmark/factory/arm.hpp:31-96 (C3), benchmark/bipedal-timings.cpp:52-140 (C5)
+and bindings/python/crocoddyl/utils/{quadruped,biped}.py (C4 / C5 gaits):
 
   IntegratedActionModelEuler          include/crocoddyl/core/integrator/euler.hxx:41-131
    ∘ DifferentialActionModelFreeFwdDynamics
                                       include/crocoddyl/multibody/actions/free-fwddyn.hxx:44-118
-     actuation ActuationModelFull     (tau = u)
+   ∘ DifferentialActionModelContactFwdDynamics
+                                      multibody/actions/contact-fwddyn.hxx:59-160
+  ActionModelImpulseFwdDynamics       multibody/actions/impulse-fwddyn.hxx:53-127
      costs CostModelSum               multibody/costs/cost-sum.hxx:89-160
        CostModelState                 multibody/costs/state.hxx:130-169
        CostModelControl               multibody/costs/control.hxx:56-87
        CostModelFramePlacement        multibody/costs/frame-placement.hxx:45-80
        CostModelFrameTranslation      multibody/costs/frame-translation.hxx:50-81
+       CostModelContactForce          multibody/costs/contact-force.hxx:33-74
      activations Quad / WeightedQuad  core/activations/{quadratic,weighted-quadratic}.hpp
-   on a fixed-base kinematic tree of revolute joints (StateMultibody over a
-   Pinocchio model whose q and v spaces coincide, so integrate / diff are
-   Euclidean and Jintegrate / Jdiff are identities).
+  StateMultibody                      multibody/states/multibody.hxx:54-240
+
+over a kinematic tree whose root joint is either fixed (a revolute joint on the
+universe) or a free-flyer (pinocchio JointModelFreeFlyer: q = (p, quat xyzw),
+v = body twist (linear, angular) in the base frame), with revolute joints below.
+
+The state is a manifold: x = (q, v) with nq = nv + 1 for a free-flyer root, and
+the reference's diff / integrate are pinocchio::difference / integrate
+(multibody.hxx:54-91): for the free-flyer, M0^-1 M1 -> log6 and M exp6(dq) with
+the quaternion re-extracted from the rotation (Eigen's algorithm), kept in the
+input's hemisphere and first-order normalised (pinocchio
+SpecialEuclideanOperationTpl<3>::integrate). Every derivative the oracle returns
+is in tangent coordinates, as the reference's: Fx = d diff(xnext, calc(x [+] dx)) / d dx.
 
 The rigid-body algorithms of Pinocchio (>= 2.4.7, third-party, absent here)
 are restated from their published form (Featherstone, "Rigid Body Dynamics
-Algorithms", 2008): ABA (Table 7.1) for the forward dynamics the reference
-gets from pinocchio::aba (free-fwddyn.hxx:64), RNEA (Table 5.1) and CRBA
-(Table 6.2) for the consistency checks, SE(3) log (Pinocchio's log6) for
-the frame-placement residual. The derivatives (Fx, Fu, the residual
-Jacobians Rx / Ru that the cost Hessians are built from) come from
-complex-step differentiation of those functions, exact to rounding and
-independent of the analytic linearisation the device uses.
+Algorithms", 2008): ABA (Table 7.1) with multi-dof joints for the forward
+dynamics the reference gets from pinocchio::aba (free-fwddyn.hxx:64), RNEA
+(Table 5.1) and CRBA (Table 6.2), SE(3) exp / log (Pinocchio's exp6 / log6).
+The derivatives (Fx, Fu, the residual Jacobians Rx / Ru that the cost Hessians
+are built from) come from complex-step differentiation of those functions in
+tangent coordinates (x [+] i h e_j), exact to rounding and independent of the
+analytic world-frame linearisation the device uses.
 
 Pinocchio itself is not available offline, so the multibody arithmetic is
 "parity unpinned" against the reference's own binary; it is pinned here by
 closed-form pendulum dynamics, ABA == CRBA^-1 (tau - RNEA(q, v, 0)),
-RNEA(q, v, ABA(q, v, tau)) == tau and finite differences at the reference's
-numdiff tolerance (tests/test_multibody_oracle.py).
+RNEA(q, v, ABA(q, v, tau)) == tau, free-body Newton-Euler in closed form, the
+exp / log identities and finite differences at the reference's numdiff
+tolerance (tests/test_multibody_oracle.py).
 
 Parameter-block layout: include/fddp_hip.h (FDDP_KNOT_EULER_FREEFWD).
 """
 import numpy as np
 
 HDR = 4
-JOINT_REC = 26
+JOINT_REC = 27
+REVOLUTE, FREEFLYER = 0, 1
 COST_HDR = 4
 STATE, CONTROL, FRAME_PLACEMENT, FRAME_TRANSLATION = 1, 2, 3, 4
 CONTACT_3D, CONTACT_6D = 5, 6  # contact records (FDDP_KNOT_EULER_CONTACTFWD)
 CONTACT_FORCE = 7  # CostModelContactForce: r = lambda[row0:row0+nr] - fref (contact-force.hxx:33-50)
+COM_POSITION = 8  # CostModelCoMPosition: r = com(q) - cref (com-position.hxx:49-75)
+FRICTION_CONE = 9  # CostModelContactFrictionCone: r = A lambda_lin (contact-friction-cone.hxx:64-90)
 H_CS = 1e-30  # complex-step size
 
 
@@ -143,49 +161,144 @@ def log6(R, p):
 
 
 def exp6(nu):
-    """SE(3) exp of (lin, ang) — tests only."""
-    v, w = np.asarray(nu[:3], float), np.asarray(nu[3:], float)
-    t = np.linalg.norm(w)
-    W = skew(w)
-    if t < 1e-12:
-        return np.eye(3) + W, v + 0.5 * W @ v
-    R = np.eye(3) + np.sin(t) / t * W + (1 - np.cos(t)) / t ** 2 * W @ W
-    V = np.eye(3) + (1 - np.cos(t)) / t ** 2 * W + (t - np.sin(t)) / t ** 3 * W @ W
-    return R, V @ v
+    """SE(3) exp of (lin, ang) (pinocchio exp6): R = cos t I + (1 - cos t)/t^2 w w^T
+    + sin t / t [w]x, p = V(w) v. Taylor branch for t^2 < 1e-8 (polynomial in t^2,
+    so complex steps through it are exact)."""
+    v, w = nu[:3], nu[3:]
+    t2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2]
+    if np.real(t2) < 1e-8:
+        ct = 1 - t2 / 2 + t2 * t2 / 24
+        st_t = 1 - t2 / 6 + t2 * t2 / 120
+        a_wxv = 0.5 - t2 / 24 + t2 * t2 / 720
+        a_w = 1.0 / 6 - t2 / 120 + t2 * t2 / 5040
+    else:
+        t = np.sqrt(t2)
+        ct = np.cos(t)
+        st_t = np.sin(t) / t
+        a_wxv = (1 - ct) / t2
+        a_w = (1 - st_t) / t2
+    R = ct * np.eye(3) + a_wxv * np.outer(w, w) + st_t * skew(w)
+    wv = w[0] * v[0] + w[1] * v[1] + w[2] * v[2]
+    p = st_t * v + a_w * wv * w + a_wxv * np.cross(w, v)
+    return R, p
+
+
+def quat_to_R(qv):
+    """Eigen QuaternionBase::toRotationMatrix, coefficients (x, y, z, w)."""
+    x, y, z, w = qv
+    tx, ty, tz = 2 * x, 2 * y, 2 * z
+    twx, twy, twz = tx * w, ty * w, tz * w
+    txx, txy, txz = tx * x, ty * x, tz * x
+    tyy, tyz, tzz = ty * y, tz * y, tz * z
+    return np.array([[1 - (tyy + tzz), txy - twz, txz + twy],
+                     [txy + twz, 1 - (txx + tzz), tyz - twx],
+                     [txz - twy, tyz + twx, 1 - (txx + tyy)]])
+
+
+def R_to_quat(R):
+    """Eigen's quaternion-from-rotation (quaternionbase_assign_impl), branches on
+    real parts. Returns (x, y, z, w)."""
+    t = R[0, 0] + R[1, 1] + R[2, 2]
+    q = [None] * 4
+    if np.real(t) > 0:
+        t = np.sqrt(t + 1.0)
+        q[3] = 0.5 * t
+        t = 0.5 / t
+        q[0] = (R[2, 1] - R[1, 2]) * t
+        q[1] = (R[0, 2] - R[2, 0]) * t
+        q[2] = (R[1, 0] - R[0, 1]) * t
+    else:
+        i = 0
+        if np.real(R[1, 1]) > np.real(R[0, 0]):
+            i = 1
+        if np.real(R[2, 2]) > np.real(R[i, i]):
+            i = 2
+        j, k = (i + 1) % 3, (i + 2) % 3
+        t = np.sqrt(R[i, i] - R[j, j] - R[k, k] + 1.0)
+        q[i] = 0.5 * t
+        t = 0.5 / t
+        q[3] = (R[k, j] - R[j, k]) * t
+        q[j] = (R[j, i] + R[i, j]) * t
+        q[k] = (R[k, i] + R[i, k]) * t
+    return np.array(q)
+
+
+def se3_integrate(q7, dq6):
+    """pinocchio SpecialEuclideanOperationTpl<3>::integrate: M1 = M0 exp6(dq);
+    quaternion from M1's rotation, flipped into q0's hemisphere, first-order
+    normalised."""
+    R0 = quat_to_R(q7[3:7])
+    Re, pe = exp6(dq6)
+    R1 = R0 @ Re
+    p1 = q7[:3] + R0 @ pe
+    qn = R_to_quat(R1)
+    if np.real(np.dot(qn, q7[3:7])) < 0:
+        qn = -qn
+    n2 = np.dot(qn, qn)
+    qn = qn * ((3 - n2) / 2)
+    return np.concatenate([p1, qn])
+
+
+def se3_difference(q0, q1):
+    """pinocchio SpecialEuclideanOperationTpl<3>::difference: log6(M0^-1 M1)."""
+    R0, R1 = quat_to_R(q0[3:7]), quat_to_R(q1[3:7])
+    return log6(R0.T @ R1, R0.T @ (q1[:3] - q0[:3]))
 
 
 # ---------------------------------------------------------------------------
 # model block
 # ---------------------------------------------------------------------------
 class Robot:
-    """Kinematic tree parsed from the block's robot section."""
+    """Kinematic tree parsed from the block's robot section: one record per
+    pinocchio joint (a free-flyer may only be the root)."""
 
-    def __init__(self, nj, gravity, armature, joints):
-        self.nj = nj
+    def __init__(self, nv, gravity, armature, joints):
         self.gravity = np.asarray(gravity, float)
         self.armature = np.asarray(armature, float)
-        self.parent = [int(j[0]) for j in joints]
-        self.axis = [np.asarray(j[1:4], float) for j in joints]
-        self.Rpl = [np.asarray(j[4:13], float).reshape(3, 3).T for j in joints]  # column-major
-        self.ppl = [np.asarray(j[13:16], float) for j in joints]
-        self.mass = [float(j[16]) for j in joints]
-        self.com = [np.asarray(j[17:20], float) for j in joints]
+        self.kind = [int(j[0]) for j in joints]
+        self.parent = [int(j[1]) for j in joints]
+        self.axis = [np.asarray(j[2:5], float) for j in joints]
+        self.Rpl = [np.asarray(j[5:14], float).reshape(3, 3).T for j in joints]  # column-major
+        self.ppl = [np.asarray(j[14:17], float) for j in joints]
+        self.mass = [float(j[17]) for j in joints]
+        self.com = [np.asarray(j[18:21], float) for j in joints]
         self.Ic = []
         for j in joints:
-            xx, yy, zz, xy, xz, yz = j[20:26]
+            xx, yy, zz, xy, xz, yz = j[21:27]
             self.Ic.append(np.array([[xx, xy, xz], [xy, yy, yz], [xz, yz, zz]], float))
-        self.I6 = [spatial_inertia(self.mass[i], self.com[i], self.Ic[i]) for i in range(nj)]
+        self.nb = len(joints)
+        self.I6 = [spatial_inertia(self.mass[i], self.com[i], self.Ic[i]) for i in range(self.nb)]
+        self.nvj = [6 if k == FREEFLYER else 1 for k in self.kind]
+        self.nqj = [7 if k == FREEFLYER else 1 for k in self.kind]
+        self.iv = np.concatenate([[0], np.cumsum(self.nvj)[:-1]]).astype(int)
+        self.iq = np.concatenate([[0], np.cumsum(self.nqj)[:-1]]).astype(int)
+        self.nv, self.nq = int(sum(self.nvj)), int(sum(self.nqj))
+        self.ff = self.kind[0] == FREEFLYER
+        assert self.nv == nv, "record count does not match nv"
+        assert all(k != FREEFLYER for k in self.kind[1:]), "a free-flyer may only be the root"
+        self.nj = self.nv  # legacy name: dofs
 
     def S(self, i):
-        return np.concatenate([np.zeros(3), self.axis[i]])
+        if self.kind[i] == FREEFLYER:
+            return np.eye(6)
+        return np.concatenate([np.zeros(3), self.axis[i]]).reshape(6, 1)
+
+    def vseg(self, v, i):
+        return v[self.iv[i]:self.iv[i] + self.nvj[i]]
 
     def liMi(self, q, i):
-        return self.Rpl[i] @ rot_axis(self.axis[i], q[i]), self.ppl[i] + 0 * q[i]
+        if self.kind[i] == FREEFLYER:
+            qq = q[self.iq[i]:self.iq[i] + 7]
+            Rj, pj = quat_to_R(qq[3:7]), qq[:3]
+        else:
+            qi = q[self.iq[i]]
+            Rj, pj = rot_axis(self.axis[i], qi), np.zeros(3) + 0 * qi
+        return self.Rpl[i] @ Rj, self.ppl[i] + self.Rpl[i] @ pj
 
     def placements(self, q):
         """oMi of every joint."""
         out = []
-        for i in range(self.nj):
+        for i in range(self.nb):
             R, p = self.liMi(q, i)
             lam = self.parent[i]
             if lam >= 0:
@@ -195,25 +308,29 @@ class Robot:
                 out.append((R, p))
         return out
 
-    # Featherstone Table 5.1 (Pinocchio rnea)
-    def rnea(self, q, v, a, gravity=None):
+    # Featherstone Table 5.1 (Pinocchio rnea); fext: forces in the joint frames
+    # (pinocchio's fext convention), may be None
+    def rnea(self, q, v, a, gravity=None, fext=None):
         dt = np.result_type(q, v, a)
-        nj = self.nj
-        X = [motion_X(*self.liMi(q, i)) for i in range(nj)]
-        vs, as_, fs = [None] * nj, [None] * nj, [None] * nj
+        nb = self.nb
+        X = [motion_X(*self.liMi(q, i)) for i in range(nb)]
+        vs, as_, fs = [None] * nb, [None] * nb, [None] * nb
         g = self.gravity if gravity is None else np.asarray(gravity, float)
         a0 = np.concatenate([-g, np.zeros(3)]).astype(dt)
-        for i in range(nj):
+        for i in range(nb):
             lam = self.parent[i]
             S = self.S(i)
             vp = vs[lam] if lam >= 0 else np.zeros(6, dt)
             ap = as_[lam] if lam >= 0 else a0
-            vs[i] = X[i] @ vp + S * v[i]
-            as_[i] = X[i] @ ap + S * a[i] + crm(vs[i]) @ (S * v[i])
+            vJ = S @ self.vseg(v, i)
+            vs[i] = X[i] @ vp + vJ
+            as_[i] = X[i] @ ap + S @ self.vseg(a, i) + crm(vs[i]) @ vJ
             fs[i] = self.I6[i] @ as_[i] + crf(vs[i]) @ (self.I6[i] @ vs[i])
-        tau = np.zeros(nj, dt)
-        for i in reversed(range(nj)):
-            tau[i] = self.S(i) @ fs[i]
+            if fext is not None:
+                fs[i] = fs[i] - fext[i]
+        tau = np.zeros(self.nv, dt)
+        for i in reversed(range(nb)):
+            tau[self.iv[i]:self.iv[i] + self.nvj[i]] = self.S(i).T @ fs[i]
             lam = self.parent[i]
             if lam >= 0:
                 fs[lam] = fs[lam] + X[i].T @ fs[i]
@@ -221,78 +338,123 @@ class Robot:
 
     # Featherstone Table 6.2 (Pinocchio crba)
     def crba(self, q):
-        nj = self.nj
-        X = [motion_X(*self.liMi(q, i)) for i in range(nj)]
-        Ic = [I.copy() for I in self.I6]
-        for i in reversed(range(nj)):
+        nb = self.nb
+        X = [motion_X(*self.liMi(q, i)) for i in range(nb)]
+        Ic = [I.astype(np.result_type(q, float)) for I in self.I6]
+        for i in reversed(range(nb)):
             lam = self.parent[i]
             if lam >= 0:
                 Ic[lam] = Ic[lam] + X[i].T @ Ic[i] @ X[i]
-        M = np.zeros((nj, nj), dtype=np.result_type(q, float))
-        for i in range(nj):
-            F = Ic[i] @ self.S(i)
-            M[i, i] = self.S(i) @ F
+        M = np.zeros((self.nv, self.nv), dtype=np.result_type(q, float))
+        for i in range(nb):
+            Si = self.S(i)
+            si = slice(self.iv[i], self.iv[i] + self.nvj[i])
+            F = Ic[i] @ Si
+            M[si, si] = Si.T @ F
             j = i
             while self.parent[j] >= 0:
                 F = X[j].T @ F
                 j = self.parent[j]
-                M[i, j] = M[j, i] = self.S(j) @ F
+                sj = slice(self.iv[j], self.iv[j] + self.nvj[j])
+                M[sj, si] = self.S(j).T @ F
+                M[si, sj] = M[sj, si].T
         return M
 
-    # Featherstone Table 7.1 (Pinocchio aba), armature added to D (rotor inertia)
+    # Featherstone Table 7.1 (Pinocchio aba) with multi-dof joints, armature added to D
     def aba(self, q, v, tau):
         dt = np.result_type(q, v, tau)
-        nj = self.nj
-        X = [motion_X(*self.liMi(q, i)) for i in range(nj)]
-        vs, cs, IA, pA = [None] * nj, [None] * nj, [None] * nj, [None] * nj
-        for i in range(nj):
+        nb = self.nb
+        X = [motion_X(*self.liMi(q, i)) for i in range(nb)]
+        vs, cs, IA, pA = [None] * nb, [None] * nb, [None] * nb, [None] * nb
+        for i in range(nb):
             lam = self.parent[i]
             S = self.S(i)
             vp = vs[lam] if lam >= 0 else np.zeros(6, dt)
-            vs[i] = X[i] @ vp + S * v[i]
-            cs[i] = crm(vs[i]) @ (S * v[i])
+            vJ = S @ self.vseg(v, i)
+            vs[i] = X[i] @ vp + vJ
+            cs[i] = crm(vs[i]) @ vJ
             IA[i] = self.I6[i].astype(dt)
             pA[i] = crf(vs[i]) @ (self.I6[i] @ vs[i])
-        U, D, u = [None] * nj, [None] * nj, [None] * nj
-        for i in reversed(range(nj)):
+        U, Dinv, u = [None] * nb, [None] * nb, [None] * nb
+        for i in reversed(range(nb)):
             S = self.S(i)
+            sl = slice(self.iv[i], self.iv[i] + self.nvj[i])
             U[i] = IA[i] @ S
-            D[i] = S @ U[i] + self.armature[i]
-            u[i] = tau[i] - S @ pA[i]
+            D = S.T @ U[i] + np.diag(self.armature[sl])
+            Dinv[i] = np.linalg.inv(D)
+            u[i] = tau[sl] - S.T @ pA[i]
             lam = self.parent[i]
             if lam >= 0:
-                Ia = IA[i] - np.outer(U[i], U[i]) / D[i]
-                pa = pA[i] + Ia @ cs[i] + U[i] * (u[i] / D[i])
+                Ia = IA[i] - U[i] @ Dinv[i] @ U[i].T
+                pa = pA[i] + Ia @ cs[i] + U[i] @ (Dinv[i] @ u[i])
                 IA[lam] = IA[lam] + X[i].T @ Ia @ X[i]
                 pA[lam] = pA[lam] + X[i].T @ pa
-        a = [None] * nj
-        qdd = np.zeros(nj, dt)
+        a = [None] * nb
+        qdd = np.zeros(self.nv, dt)
         a0 = np.concatenate([-self.gravity, np.zeros(3)]).astype(dt)
-        for i in range(nj):
+        for i in range(nb):
             lam = self.parent[i]
             ap = a[lam] if lam >= 0 else a0
             ai = X[i] @ ap + cs[i]
-            qdd[i] = (u[i] - U[i] @ ai) / D[i]
-            a[i] = ai + self.S(i) * qdd[i]
+            sl = slice(self.iv[i], self.iv[i] + self.nvj[i])
+            qdd[sl] = Dinv[i] @ (u[i] - U[i].T @ ai)
+            a[i] = ai + self.S(i) @ qdd[sl]
         return qdd
 
+    def center_of_mass(self, q):
+        """Centre of mass (pinocchio::centerOfMass)."""
+        oM = self.placements(q)
+        mt = sum(self.mass)
+        c = 0
+        for i in range(self.nb):
+            R, p = oM[i]
+            c = c + self.mass[i] * (p + R @ self.com[i])
+        return c / mt
 
-def parse_robot(body, nj):
+    # -- StateMultibody restated (multibody.hxx:54-91) -------------------------
+    def neutral(self):
+        q = np.zeros(self.nq)
+        if self.ff:
+            q[6] = 1.0
+        return q
+
+    def integrate_q(self, q, dq):
+        if self.ff:
+            return np.concatenate([se3_integrate(q[:7], dq[:6]), q[7:] + dq[6:]])
+        return q + dq
+
+    def difference_q(self, q0, q1):
+        if self.ff:
+            return np.concatenate([se3_difference(q0[:7], q1[:7]), q1[7:] - q0[7:]])
+        return q1 - q0
+
+    def state_integrate(self, x, dx):
+        nq, nv = self.nq, self.nv
+        return np.concatenate([self.integrate_q(x[:nq], dx[:nv]), x[nq:] + dx[nv:]])
+
+    def state_diff(self, x0, x1):
+        nq, nv = self.nq, self.nv
+        return np.concatenate([self.difference_q(x0[:nq], x1[:nq]), x1[nq:] - x0[nq:]])
+
+
+def parse_robot(body, nv):
     g = body[0:3]
-    arm = body[3:3 + nj]
-    o = 3 + nj
-    joints = [body[o + JOINT_REC * i:o + JOINT_REC * (i + 1)] for i in range(nj)]
-    return Robot(nj, g, arm, joints), o + JOINT_REC * nj
+    arm = body[3:3 + nv]
+    o = 3 + nv
+    nb = nv - 5 if int(body[o]) == FREEFLYER else nv
+    joints = [body[o + JOINT_REC * i:o + JOINT_REC * (i + 1)] for i in range(nb)]
+    return Robot(nv, g, arm, joints), o + JOINT_REC * nb
 
 
 class Cost:
-    def __init__(self, rec, nx, nu):
+    def __init__(self, rec, nx, ndx, nu):
         self.type = int(rec[0])
         self.weight = float(rec[1])
         weighted = rec[2] != 0
         d = rec[COST_HDR:]
+        self.size = int(rec[3])
         if self.type == STATE:
-            self.xref, w, nr = d[:nx], d[nx:2 * nx], nx
+            self.xref, w, nr = d[:nx], d[nx:nx + ndx], ndx
         elif self.type == CONTROL:
             self.uref, w, nr = d[:nu], d[nu:2 * nu], nu
         elif self.type in (FRAME_PLACEMENT, FRAME_TRANSLATION):
@@ -306,6 +468,9 @@ class Cost:
             else:
                 self.pref = d[13:16]
                 w, nr = d[16:19], 3
+        elif self.type == COM_POSITION:
+            self.cref = d[0:3]
+            w, nr = d[3:6], 3
         elif self.type == CONTACT_FORCE:
             self.row0, nr = int(d[0]), int(d[1])
             self.fref = d[2:2 + nr]
@@ -317,20 +482,32 @@ class Cost:
         self.w = np.asarray(w, float) if weighted else np.ones(nr)
 
     def residual(self, robot, x, u, oM=None):
-        nj = robot.nj
+        nq = robot.nq
         if self.type == STATE:
-            return x - self.xref  # diff(xref, x), state.hxx:136
+            return robot.state_diff(self.xref, x)  # diff(xref, x), state.hxx:136
         if self.type == CONTROL:
             return u - self.uref  # control.hxx:67
         if self.type == CONTACT_FORCE:
             return self.force_fn(x, u)[self.row0:self.row0 + len(self.fref)] - self.fref
+        if self.type == COM_POSITION:
+            return robot.center_of_mass(x[:nq]) - self.cref
         if oM is None:
-            oM = robot.placements(x[:nj])
+            oM = robot.placements(x[:nq])
         R0, p0 = oM[self.joint]
         Rf, pf = R0 @ self.Rf, p0 + R0 @ self.pf  # oMf = oMi[parent] * placement
         if self.type == FRAME_TRANSLATION:
             return pf - self.pref  # frame-translation.hxx:57
         return log6(self.Rri @ Rf, self.pri + self.Rri @ pf)  # log6(Mref^-1 oMf), frame-placement.hxx:48-50
+
+
+def _cs_jac(f, n_in, n_out):
+    """Complex-step Jacobian of f(dz) (dz complex, n_in) at dz = 0."""
+    J = np.zeros((n_out, n_in))
+    for j in range(n_in):
+        dz = np.zeros(n_in, complex)
+        dz[j] = 1j * H_CS
+        J[:, j] = np.imag(f(dz)) / H_CS
+    return J
 
 
 class FreeFwdKnot:
@@ -339,28 +516,41 @@ class FreeFwdKnot:
     def __init__(self, block, nx, nu, _contact=False):
         p = np.asarray(block, float)
         self.dt = float(p[0])
-        nj = int(p[1])
+        nv = int(p[1])
         ncost = int(p[2])
         self.size = int(p[3])
-        assert nx == 2 * nj and (_contact or nu == nj), "free-fwddyn knots: nx = 2 nv, nu = nv (full actuation)"
-        self.nx, self.nu, self.nj = nx, nu, nj
-        self.ndx = nx
-        self.kind = 4
         body = p[HDR:]
-        self.robot, o = parse_robot(body, nj)
+        self.robot, o = parse_robot(body, nv)
+        nq = self.robot.nq
+        assert nx == nq + nv, "multibody knots: nx = nq + nv"
+        assert _contact or nu == nv, "free-fwddyn knots: nu = nv (full actuation)"
+        self.nx, self.nu, self.nj, self.nv, self.nq = nx, nu, nv, nv, nq
+        self.ndx = 2 * nv
+        self.kind = 4
         self.costs = []
         for _ in range(ncost):
             rs = int(body[o + 3])
-            self.costs.append(Cost(body[o:o + rs], nx, nu))
+            self.costs.append(Cost(body[o:o + rs], nx, self.ndx, nu))
             o += rs
+        self._sec = o  # offset (in body) of the contact / impulse section
+
+    # StateMultibody (multibody.hxx:54-91)
+    def state_diff(self, x0, x1):
+        return self.robot.state_diff(x0, x1)
+
+    def state_integrate(self, x, dx):
+        return self.robot.state_integrate(x, dx)
+
+    def state_zero(self):
+        return np.concatenate([self.robot.neutral(), np.zeros(self.nv)])
 
     # DAM calc: a and the differential cost
     def accel(self, x, u):
-        nj = self.nj
-        return self.robot.aba(x[:nj], x[nj:], u)
+        nq = self.nq
+        return self.robot.aba(x[:nq], x[nq:], u)
 
     def cost_c(self, x, u):
-        oM = self.robot.placements(x[:self.nj])
+        oM = self.robot.placements(x[:self.nq])
         c = 0.0
         for k in self.costs:
             r = k.residual(self.robot, x, u, oM)
@@ -371,40 +561,36 @@ class FreeFwdKnot:
         """IntegratedActionModelEuler::calc (euler.hxx:41-80) -> (xnext, cost)."""
         if u is None:
             u = np.zeros(self.nu)
-        nj, dt = self.nj, self.dt
+        nq, dt = self.nq, self.dt
         a = self.accel(x, u)
         cc = self.cost_c(x, u)
         if dt != 0:
-            v = x[nj:]
-            xn = np.concatenate([x[:nj] + v * dt + a * dt * dt, x[nj:] + a * dt])
-            return xn, dt * cc
+            v = x[nq:]
+            dx = np.concatenate([v * dt + a * dt * dt, a * dt])
+            return self.state_integrate(x, dx), dt * cc
         return np.array(x, copy=True), cc
-
-    def _cs_jac(self, f, z, n_out):
-        J = np.zeros((n_out, z.size))
-        for j in range(z.size):
-            zc = z.astype(complex)
-            zc[j] += 1j * H_CS
-            J[:, j] = np.imag(f(zc)) / H_CS
-        return J
 
     def calc_diff(self, x, u=None):
         """IntegratedActionModelEuler::calcDiff (euler.hxx:83-131) with the
-        DAM's derivatives; Gauss-Newton cost Hessians (cost-sum.hxx:122-160)."""
+        DAM's derivatives; Gauss-Newton cost Hessians (cost-sum.hxx:122-160).
+        Tangent coordinates: Fx = d diff(xnext, calc(x [+] dx)) / d dx."""
         if u is None:
             u = np.zeros(self.nu)
-        n, m, nj, dt = self.nx, self.nu, self.nj, self.dt
-        z = np.concatenate([x, u])
+        n, m, dt = self.ndx, self.nu, self.dt
+        x = np.asarray(x, float)
+        u = np.asarray(u, float)
         if dt != 0:
-            Fz = self._cs_jac(lambda zz: self.calc(zz[:n], zz[n:])[0], z, n)
-            Fx, Fu = Fz[:, :n], Fz[:, n:]
+            xn0 = self.calc(x, u)[0]
+            Fx = _cs_jac(lambda dz: self.state_diff(xn0, self.calc(self.state_integrate(x, dz), u)[0]), n, n)
+            Fu = _cs_jac(lambda du: self.state_diff(xn0, self.calc(x, u + du)[0]), m, n)
         else:
             Fx, Fu = np.eye(n), np.zeros((n, m))
         Lz = np.zeros(n + m)
         Lzz = np.zeros((n + m, n + m))
         for k in self.costs:
             r = k.residual(self.robot, x, u)
-            Rz = self._cs_jac(lambda zz: k.residual(self.robot, zz[:n], zz[n:]), z, r.size)
+            Rz = _cs_jac(lambda dz: k.residual(self.robot, self.state_integrate(x, dz[:n]), u + dz[n:]), n + m,
+                         r.size)
             if getattr(k, "zero_jac", False):
                 Rz[:] = 0.0
             Lz += k.weight * Rz.T @ (k.w * r)
@@ -442,16 +628,39 @@ def local_motions(robot, q, v, qdd):
     computeAllTerms (qdd = 0) or forwardKinematics(q, v, qdd))."""
     dt = np.result_type(q, v, qdd)
     vs, as_ = [], []
-    for i in range(robot.nj):
+    for i in range(robot.nb):
         X = motion_X(*robot.liMi(q, i))
         lam = robot.parent[i]
         S = robot.S(i)
         vp = vs[lam] if lam >= 0 else np.zeros(6, dt)
         ap = as_[lam] if lam >= 0 else np.zeros(6, dt)
-        vi = X @ vp + S * v[i]
+        vJ = S @ robot.vseg(v, i)
+        vi = X @ vp + vJ
         vs.append(vi)
-        as_.append(X @ ap + S * qdd[i] + crm(vi) @ (S * v[i]))
+        as_.append(X @ ap + S @ robot.vseg(qdd, i) + crm(vi) @ vJ)
     return vs, as_
+
+
+def frame_jacobian(robot, q, joint, Rf, pf):
+    """LOCAL frame Jacobian (6 x nv): frame velocity per unit joint velocity."""
+    dt = np.result_type(q, float)
+    Xf = motion_X(Rf, pf)
+    J = np.zeros((6, robot.nv), dt)
+    for k in range(robot.nv):
+        e = np.zeros(robot.nv, dt)
+        e[k] = 1.0
+        J[:, k] = Xf @ local_motions(robot, q, e, np.zeros(robot.nv, dt))[0][joint]
+    return J
+
+
+def _section(body, nv, ncost):
+    """Offset (in body) of the contact / impulse section."""
+    o = 3 + nv
+    nb = nv - 5 if int(body[o]) == FREEFLYER else nv
+    o += JOINT_REC * nb
+    for _ in range(ncost):
+        o += int(body[o + 3])
+    return o
 
 
 class ContactFwdKnot(FreeFwdKnot):
@@ -467,18 +676,16 @@ class ContactFwdKnot(FreeFwdKnot):
     stacks the LOCAL frame Jacobians (3 linear rows for a 3D contact) and a0 the
     frame drift accelerations with the Baumgarte terms (contact-3d.hxx:27-43,
     contact-6d.hxx:27-45). Fx / Fu come from complex-step differentiation of
-    this calc: the reference's analytic KKT-inverse formula
+    this calc in tangent coordinates: the reference's analytic KKT-inverse formula
     (contact-fwddyn.hxx:127-140) is the implicit-function derivative of the
     same map, so the two agree to rounding."""
 
     def __init__(self, block, nx, nu):
         p = np.asarray(block, float)
-        nj = int(p[1])
+        nv = int(p[1])
         ncost = int(p[2])
         body = p[HDR:]
-        o = 3 + nj + JOINT_REC * nj
-        for _ in range(ncost):
-            o += int(body[o + 3])
+        o = _section(body, nv, ncost)
         self.nun = int(body[o])
         self.damping = float(body[o + 1])
         ncon = int(body[o + 2])
@@ -489,7 +696,7 @@ class ContactFwdKnot(FreeFwdKnot):
             rs = int(body[o + 3])
             self.contacts.append(Contact(body[o:o + rs]))
             o += rs
-        assert nu == nj - self.nun, "contact-fwddyn knots: nu = nv - (unactuated root dofs)"
+        assert nu == nv - self.nun, "contact-fwddyn knots: nu = nv - (unactuated root dofs)"
         super().__init__(block, nx, nu, _contact=True)
         self.kind = 5
         self.nc = sum(c.nc for c in self.contacts)
@@ -500,22 +707,17 @@ class ContactFwdKnot(FreeFwdKnot):
 
     def contact_terms(self, x):
         """(Jc (nc x nv), a0 (nc)) at ddq = 0 (ContactModelMultiple::calc)."""
-        nj = self.nj
-        q, v = x[:nj], x[nj:]
+        nq, nv = self.nq, self.nv
+        q, v = x[:nq], x[nq:]
         dt = np.result_type(x, float)
-        vs, as_ = local_motions(self.robot, q, v, np.zeros(nj, dt))
+        vs, as_ = local_motions(self.robot, q, v, np.zeros(nv, dt))
         oM = self.robot.placements(q)
         Js, a0s = [], []
         for c in self.contacts:
             Xf = motion_X(c.Rf, c.pf)  # joint -> frame (SE3::actInv by jMf)
             vf = Xf @ vs[c.joint]
             af = Xf @ as_[c.joint]
-            # LOCAL frame Jacobian: frame velocity per unit joint velocity
-            J = np.zeros((6, nj), dt)
-            for k in range(nj):
-                e = np.zeros(nj, dt)
-                e[k] = 1.0
-                J[:, k] = Xf @ local_motions(self.robot, q, e, np.zeros(nj, dt))[0][c.joint]
+            J = frame_jacobian(self.robot, q, c.joint, c.Rf, c.pf)
             R0, p0 = oM[c.joint]
             Rw, pw = R0 @ c.Rf, p0 + R0 @ c.pf  # oMf
             kp, kd = c.gains
@@ -535,23 +737,23 @@ class ContactFwdKnot(FreeFwdKnot):
                 Js.append(J)
             a0s.append(a0)
         if not Js:
-            return np.zeros((0, nj), dt), np.zeros(0, dt)
+            return np.zeros((0, nv), dt), np.zeros(0, dt)
         return np.vstack(Js), np.concatenate(a0s)
 
     def accel_force(self, x, u):
-        nj, nc = self.nj, self.nc
-        q, v = x[:nj], x[nj:]
+        nq, nv, nc = self.nq, self.nv, self.nc
+        q, v = x[:nq], x[nq:]
         M = self.robot.crba(q) + np.diag(self.robot.armature)
-        nle = self.robot.rnea(q, v, np.zeros(nj, np.result_type(x, float)))
+        nle = self.robot.rnea(q, v, np.zeros(nv, np.result_type(x, float)))
         tau = np.concatenate([np.zeros(self.nun, np.result_type(u, float)), u])
         Jc, a0 = self.contact_terms(x)
-        K = np.zeros((nj + nc, nj + nc), dtype=np.result_type(M, Jc))
-        K[:nj, :nj] = M
-        K[:nj, nj:] = Jc.T
-        K[nj:, :nj] = Jc
-        K[nj:, nj:] = -self.damping * np.eye(nc)
+        K = np.zeros((nv + nc, nv + nc), dtype=np.result_type(M, Jc))
+        K[:nv, :nv] = M
+        K[:nv, nv:] = Jc.T
+        K[nv:, :nv] = Jc
+        K[nv:, nv:] = -self.damping * np.eye(nc)
         sol = np.linalg.solve(K, np.concatenate([tau - nle, -a0]))
-        return sol[:nj], -sol[nj:]
+        return sol[:nv], -sol[nv:]
 
     def accel(self, x, u):
         return self.accel_force(x, u)[0]
@@ -567,17 +769,15 @@ class ImpulseFwdKnot(FreeFwdKnot):
     Fx = [[I, 0], [-G dtau_dq - H dv0_dq, G M]] with G, H the KKT-inverse blocks,
     dtau_dq = d/dq [RNEA(q, 0, v+ - v) - Jc^T Lambda] without gravity (fext fixed
     in their frames) and dv0_dq = d/dq (Jc v+), each by complex step of that
-    sub-function. For r = 0 this is the exact derivative of calc (tested); for
-    r > 0 the reference drops the restitution terms, and so does this."""
+    sub-function in tangent coordinates. For r = 0 this is the exact derivative of
+    calc (tested); for r > 0 the reference drops the restitution terms, and so does this."""
 
     def __init__(self, block, nx, nu):
         p = np.asarray(block, float)
-        nj = int(p[1])
+        nv = int(p[1])
         ncost = int(p[2])
         body = p[HDR:]
-        o = 3 + nj + JOINT_REC * nj
-        for _ in range(ncost):
-            o += int(body[o + 3])
+        o = _section(body, nv, ncost)
         self.r_coeff = float(body[o])
         self.damping = float(body[o + 1])
         nimp = int(body[o + 2])
@@ -591,51 +791,44 @@ class ImpulseFwdKnot(FreeFwdKnot):
         assert nu == 0, "impulse knots have no controls"
         super().__init__(block, nx, nu, _contact=True)
         self.kind = 6
-        self.nun = nj
+        self.nun = nv
         self.nc = sum(c.nc for c in self.contacts)
 
     def jac(self, q):
-        nj = self.nj
-        dt = np.result_type(q, float)
         Js = []
         for c in self.contacts:
-            Xf = motion_X(c.Rf, c.pf)
-            J = np.zeros((6, nj), dt)
-            for k in range(nj):
-                e = np.zeros(nj, dt)
-                e[k] = 1.0
-                J[:, k] = Xf @ local_motions(self.robot, q, e, np.zeros(nj, dt))[0][c.joint]
+            J = frame_jacobian(self.robot, q, c.joint, c.Rf, c.pf)
             Js.append(J[:3] if c.type == CONTACT_3D else J)
-        return np.vstack(Js) if Js else np.zeros((0, nj), dt)
+        return np.vstack(Js) if Js else np.zeros((0, self.nv), np.result_type(q, float))
 
     def kkt(self, q):
-        nj, nc = self.nj, self.nc
+        nv, nc = self.nv, self.nc
         M = self.robot.crba(q) + np.diag(self.robot.armature)
         J = self.jac(q)
-        K = np.zeros((nj + nc, nj + nc), dtype=np.result_type(M, J))
-        K[:nj, :nj] = M
-        K[:nj, nj:] = J.T
-        K[nj:, :nj] = J
-        K[nj:, nj:] = -self.damping * np.eye(nc)
+        K = np.zeros((nv + nc, nv + nc), dtype=np.result_type(M, J))
+        K[:nv, :nv] = M
+        K[:nv, nv:] = J.T
+        K[nv:, :nv] = J
+        K[nv:, nv:] = -self.damping * np.eye(nc)
         return M, J, K
 
     def impulse(self, x):
-        nj = self.nj
-        q, v = x[:nj], x[nj:]
+        nq, nv = self.nq, self.nv
+        q, v = x[:nq], x[nq:]
         M, J, K = self.kkt(q)
         sol = np.linalg.solve(K, np.concatenate([M @ v, -self.r_coeff * (J @ v)]))
-        return sol[:nj], -sol[nj:]
+        return sol[:nv], -sol[nv:]
 
     def calc(self, x, u=None):
-        nj = self.nj
+        nq = self.nq
         vp, _ = self.impulse(x)
-        xn = np.concatenate([x[:nj] + 0 * vp, vp])
+        xn = np.concatenate([x[:nq] + 0 * vp[0], vp])
         return xn, self.cost_c(x, np.zeros(0))
 
     def calc_diff(self, x, u=None):
-        n, nj = self.nx, self.nj
+        n, nq, nv = self.ndx, self.nq, self.nv
         x = np.asarray(x, float)
-        q, v = x[:nj], x[nj:]
+        q, v = x[:nq], x[nq:]
         vp, lam = self.impulse(x)
         M, J, _ = self.kkt(q)
         Minv = np.linalg.inv(M)
@@ -644,22 +837,24 @@ class ImpulseFwdKnot(FreeFwdKnot):
         H = Y @ np.linalg.inv(S)
         G = Minv - H @ Y.T
         dv = vp - v
+        rob = self.robot
 
-        def tau(qq):  # RNEA(q, 0, dv) - Jc^T lambda, no gravity, lambda fixed in the frames
-            return self.robot.rnea(qq, np.zeros(nj), dv, gravity=np.zeros(3)) - self.jac(qq).T @ lam
+        def tau(dq):  # RNEA(q, 0, dv) - Jc^T lambda, no gravity, lambda fixed in the frames
+            qq = rob.integrate_q(q, dq)
+            return rob.rnea(qq, np.zeros(nv), dv, gravity=np.zeros(3)) - self.jac(qq).T @ lam
 
-        dtau = self._cs_jac(tau, q, nj)
-        dv0 = self._cs_jac(lambda qq: self.jac(qq) @ vp, q, self.nc)
+        dtau = _cs_jac(tau, nv, nv)
+        dv0 = _cs_jac(lambda dq: self.jac(rob.integrate_q(q, dq)) @ vp, nv, self.nc)
         Fx = np.zeros((n, n))
-        Fx[:nj, :nj] = np.eye(nj)
-        Fx[nj:, :nj] = -G @ dtau - H @ dv0
-        Fx[nj:, nj:] = G @ M
+        Fx[:nv, :nv] = np.eye(nv)
+        Fx[nv:, :nv] = -G @ dtau - H @ dv0
+        Fx[nv:, nv:] = G @ M
         Lx = np.zeros(n)
         Lxx = np.zeros((n, n))
         u0 = np.zeros(0)
         for k in self.costs:
-            r = k.residual(self.robot, x, u0)
-            Rx = self._cs_jac(lambda xx: k.residual(self.robot, xx, u0), x, r.size)
+            r = k.residual(rob, x, u0)
+            Rx = _cs_jac(lambda dz: k.residual(rob, self.state_integrate(x, dz), u0), n, r.size)
             Lx += k.weight * Rx.T @ (k.w * r)
             Lxx += k.weight * Rx.T @ (k.w[:, None] * Rx)
         return dict(Fx=Fx, Fu=np.zeros((n, 0)), Lx=Lx, Lu=np.zeros(0), Lxx=Lxx, Lxu=np.zeros((n, 0)),

@@ -24,7 +24,7 @@
 namespace mbo {
 
 constexpr int kMaxJ = 32;
-constexpr int kJRec = 26;
+constexpr int kJRec = 27;  // [type, parent, axis(3), R(9), p(3), mass, CoM(3), I(6)]
 enum { C_STATE = 1, C_CONTROL = 2, C_FRAME_PLACEMENT = 3, C_FRAME_TRANSLATION = 4 };
 
 // 3x3 column-major helpers
@@ -122,19 +122,19 @@ struct Robot {
     const double* J = arm + nj;
     for (int i = 0; i < nj; ++i) {
       rec[i] = J + (size_t)kJRec * i;
-      parent[i] = (int)rec[i][0];
-      inertia6(rec[i][16], rec[i] + 17, rec[i] + 20, I6[i]);
+      parent[i] = (int)rec[i][1];
+      inertia6(rec[i][17], rec[i] + 18, rec[i] + 21, I6[i]);
     }
   }
-  const double* axis(int i) const { return rec[i] + 1; }
+  const double* axis(int i) const { return rec[i] + 2; }
   void liMi(const double* q, int i, double* R, double* p) const {
     const double* ax = axis(i);
     const double s = std::sin(q[i]), c = std::cos(q[i]), oc = 1. - c;
     const double Rj[9] = {c + oc * ax[0] * ax[0],         oc * ax[1] * ax[0] + s * ax[2], oc * ax[2] * ax[0] - s * ax[1],
                           oc * ax[0] * ax[1] - s * ax[2], c + oc * ax[1] * ax[1],         oc * ax[2] * ax[1] + s * ax[0],
                           oc * ax[0] * ax[2] + s * ax[1], oc * ax[1] * ax[2] - s * ax[0], c + oc * ax[2] * ax[2]};
-    mm(rec[i] + 4, Rj, R);
-    for (int e = 0; e < 3; ++e) p[e] = rec[i][13 + e];
+    mm(rec[i] + 5, Rj, R);
+    for (int e = 0; e < 3; ++e) p[e] = rec[i][14 + e];
   }
 };
 

@@ -387,7 +387,7 @@ def test_impulse_identities_and_derivatives(kw):
         np.testing.assert_array_equal(xn[:7], x[:7])
         if k.r_coeff == 0.0:
             d = k.calc_diff(x)
-            F = k._cs_jac(lambda xx: k.calc(xx)[0], x, 14)
+            F = onp._cs_jac(lambda dz: k.state_diff(xn, k.calc(k.state_integrate(x, dz))[0]), 14, 14)
             np.testing.assert_allclose(d["Fx"], F, atol=1e-8 * max(1.0, np.abs(F).max()))
 
 
