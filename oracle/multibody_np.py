@@ -487,7 +487,9 @@ class Cost:
             return robot.state_diff(self.xref, x)  # diff(xref, x), state.hxx:136
         if self.type == CONTROL:
             return u - self.uref  # control.hxx:67
-        if self.type == CONTACT_FORCE:
+        if self.type == CONTACT_FORCE:  # an inactive contact has lambda = 0 (row0 = -2)
+            if self.row0 < 0:
+                return -self.fref + 0 * x[0]
             return self.force_fn(x, u)[self.row0:self.row0 + len(self.fref)] - self.fref
         if self.type == COM_POSITION:
             return robot.center_of_mass(x[:nq]) - self.cref
@@ -570,31 +572,59 @@ class FreeFwdKnot:
             return self.state_integrate(x, dx), dt * cc
         return np.array(x, copy=True), cc
 
+    def _calc_res(self, x, u):
+        """(xnext, residuals of every cost) from one evaluation of the dynamics."""
+        nq, dt = self.nq, self.dt
+        a, lam = self.accel_force(x, u)
+        oM = self.robot.placements(x[:nq])
+        res = []
+        for k in self.costs:
+            if k.type == CONTACT_FORCE:
+                res.append(lam[k.row0:k.row0 + len(k.fref)] - k.fref if k.row0 >= 0 else 0 * lam[:0].sum() - k.fref)
+            else:
+                res.append(k.residual(self.robot, x, u, oM))
+        if dt != 0:
+            v = x[nq:]
+            xn = self.state_integrate(x, np.concatenate([v * dt + a * dt * dt, a * dt]))
+        else:
+            xn = x
+        return xn, res
+
+    def accel_force(self, x, u):
+        return self.accel(x, u), np.zeros(0)
+
     def calc_diff(self, x, u=None):
         """IntegratedActionModelEuler::calcDiff (euler.hxx:83-131) with the
         DAM's derivatives; Gauss-Newton cost Hessians (cost-sum.hxx:122-160).
-        Tangent coordinates: Fx = d diff(xnext, calc(x [+] dx)) / d dx."""
+        Tangent coordinates: Fx = d diff(xnext, calc(x [+] dx)) / d dx; one complex
+        step per direction drives the dynamics and every residual."""
         if u is None:
             u = np.zeros(self.nu)
         n, m, dt = self.ndx, self.nu, self.dt
         x = np.asarray(x, float)
         u = np.asarray(u, float)
+        xn0, r0 = self._calc_res(x, u)
+        Fz = np.zeros((n, n + m))
+        Rz = [np.zeros((np.size(r), n + m)) for r in r0]
+        for j in range(n + m):
+            dz = np.zeros(n + m, complex)
+            dz[j] = 1j * H_CS
+            xn, res = self._calc_res(self.state_integrate(x, dz[:n]), u + dz[n:])
+            if dt != 0:
+                Fz[:, j] = np.imag(self.state_diff(xn0, xn)) / H_CS
+            for R, r in zip(Rz, res):
+                R[:, j] = np.imag(r) / H_CS
         if dt != 0:
-            xn0 = self.calc(x, u)[0]
-            Fx = _cs_jac(lambda dz: self.state_diff(xn0, self.calc(self.state_integrate(x, dz), u)[0]), n, n)
-            Fu = _cs_jac(lambda du: self.state_diff(xn0, self.calc(x, u + du)[0]), m, n)
+            Fx, Fu = Fz[:, :n], Fz[:, n:]
         else:
             Fx, Fu = np.eye(n), np.zeros((n, m))
         Lz = np.zeros(n + m)
         Lzz = np.zeros((n + m, n + m))
-        for k in self.costs:
-            r = k.residual(self.robot, x, u)
-            Rz = _cs_jac(lambda dz: k.residual(self.robot, self.state_integrate(x, dz[:n]), u + dz[n:]), n + m,
-                         r.size)
+        for k, r, R in zip(self.costs, r0, Rz):
             if getattr(k, "zero_jac", False):
-                Rz[:] = 0.0
-            Lz += k.weight * Rz.T @ (k.w * r)
-            Lzz += k.weight * Rz.T @ (k.w[:, None] * Rz)
+                R = np.zeros_like(R)
+            Lz += k.weight * R.T @ (k.w * r)
+            Lzz += k.weight * R.T @ (k.w[:, None] * R)
         s = dt if dt != 0 else 1.0
         return dict(Fx=Fx, Fu=Fu, Lx=s * Lz[:n], Lu=s * Lz[n:], Lxx=s * Lzz[:n, :n], Lxu=s * Lzz[:n, n:],
                     Luu=s * Lzz[n:, n:])
@@ -641,16 +671,24 @@ def local_motions(robot, q, v, qdd):
     return vs, as_
 
 
-def frame_jacobian(robot, q, joint, Rf, pf):
-    """LOCAL frame Jacobian (6 x nv): frame velocity per unit joint velocity."""
+def joint_jacobians(robot, q):
+    """LOCAL joint Jacobians J_i (6 x nv): joint i's spatial velocity (joint frame)
+    per unit generalised velocity, by the forward recursion J_i = X_i J_parent + S_i."""
     dt = np.result_type(q, float)
-    Xf = motion_X(Rf, pf)
-    J = np.zeros((6, robot.nv), dt)
-    for k in range(robot.nv):
-        e = np.zeros(robot.nv, dt)
-        e[k] = 1.0
-        J[:, k] = Xf @ local_motions(robot, q, e, np.zeros(robot.nv, dt))[0][joint]
-    return J
+    out = []
+    for i in range(robot.nb):
+        X = motion_X(*robot.liMi(q, i))
+        lam = robot.parent[i]
+        J = X @ out[lam] if lam >= 0 else np.zeros((6, robot.nv), dt)
+        J[:, robot.iv[i]:robot.iv[i] + robot.nvj[i]] += robot.S(i)
+        out.append(J)
+    return out
+
+
+def frame_jacobian(robot, q, joint, Rf, pf, Js=None):
+    """LOCAL frame Jacobian (6 x nv): frame velocity per unit joint velocity."""
+    Js = joint_jacobians(robot, q) if Js is None else Js
+    return motion_X(Rf, pf) @ Js[joint]
 
 
 def _section(body, nv, ncost):
@@ -712,12 +750,13 @@ class ContactFwdKnot(FreeFwdKnot):
         dt = np.result_type(x, float)
         vs, as_ = local_motions(self.robot, q, v, np.zeros(nv, dt))
         oM = self.robot.placements(q)
+        JJ = joint_jacobians(self.robot, q)
         Js, a0s = [], []
         for c in self.contacts:
             Xf = motion_X(c.Rf, c.pf)  # joint -> frame (SE3::actInv by jMf)
             vf = Xf @ vs[c.joint]
             af = Xf @ as_[c.joint]
-            J = frame_jacobian(self.robot, q, c.joint, c.Rf, c.pf)
+            J = frame_jacobian(self.robot, q, c.joint, c.Rf, c.pf, JJ)
             R0, p0 = oM[c.joint]
             Rw, pw = R0 @ c.Rf, p0 + R0 @ c.pf  # oMf
             kp, kd = c.gains
@@ -796,8 +835,9 @@ class ImpulseFwdKnot(FreeFwdKnot):
 
     def jac(self, q):
         Js = []
+        JJ = joint_jacobians(self.robot, q)
         for c in self.contacts:
-            J = frame_jacobian(self.robot, q, c.joint, c.Rf, c.pf)
+            J = frame_jacobian(self.robot, q, c.joint, c.Rf, c.pf, JJ)
             Js.append(J[:3] if c.type == CONTACT_3D else J)
         return np.vstack(Js) if Js else np.zeros((0, self.nv), np.result_type(q, float))
 
