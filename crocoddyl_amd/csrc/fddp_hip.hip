@@ -74,7 +74,7 @@ int64_t block_doubles(int kind, int nx, int nu) {
 // pool. Returns its size in doubles, or -1 with `why` set. nj / njac / nc:
 // dofs, jac costs and contact rows (LDS sizing).
 int64_t mb_block_check(const double* P, int64_t avail, int kind, int nx, int nu, std::string& why, int* nj_out,
-                       int* njac_out, int* nc_out) {
+                       int* njac_out, int* nc_out, bool* vcols_out = nullptr) {
   using namespace fddp::mb;
   if (avail < FDDP_PARAM_HEADER) return why = "block out of range", -1;
   const double dt = P[0];
@@ -110,38 +110,59 @@ int64_t mb_block_check(const double* P, int64_t avail, int kind, int nx, int nu,
   }
   o += (int64_t)kJRec * nb;
   int njac = 0;
+  bool vcols = false;
   for (int k = 0; k < ncost; ++k) {
     if (o + kCHdr > size) return why = "cost records out of range", -1;
     const double* C = P + o;
     const int type = (int)C[0];
     const int64_t rs = (int64_t)C[3];
+    const int act = (int)C[2];
+    if ((double)act != C[2] || act < A_QUAD || act > A_WEIGHTED_QUAD_BARRIER)
+      return why = "unknown activation kind", -1;
+    const int ap = act <= A_WEIGHTED_QUAD ? 1 : (act == A_QUAD_BARRIER ? 2 : 3);  // parameter rows per residual
     int64_t want = -1;
-    if (type == C_STATE) want = kCHdr + nx + 2 * nj;
-    if (type == C_CONTROL) want = kCHdr + 2 * (int64_t)nu;
-    if (type == C_FRAME_PLACEMENT) want = kCHdr + 31;
-    if (type == C_FRAME_TRANSLATION) want = kCHdr + 19;
-    if (type == C_COM_POSITION) want = kCHdr + 6;
-    if (type == C_CONTACT_FORCE) {  // [row0, nr, fref(6)] + w(nr); rows checked against the contacts below
-      const int nrf = o + kCHdr + 1 < size ? (int)C[kCHdr + 1] : 0;
-      if (kind != FDDP_KNOT_EULER_CONTACTFWD || (nrf != 3 && nrf != 6))
-        return why = "contact-force costs need contact knots and a 3- or 6-row force", -1;
-      want = kCHdr + 8 + nrf;
+    if (type == C_STATE) want = kCHdr + nx + ap * 2 * nj;
+    if (type == C_CONTROL) want = kCHdr + nu + ap * (int64_t)nu;
+    if (type == C_FRAME_PLACEMENT) want = kCHdr + 25 + ap * 6;
+    if (type == C_FRAME_TRANSLATION) want = kCHdr + 16 + ap * 3;
+    if (type == C_FRAME_VELOCITY) {
+      if (impulse) return why = "frame-velocity costs are covered on Euler knots only", -1;
+      want = kCHdr + 19 + ap * 6;
+    }
+    if (type == C_COM_POSITION) want = kCHdr + 3 + ap * 3;
+    if (type == C_CONTACT_FORCE || type == C_FRICTION_CONE) {
+      // [row0, nr, fref(6)] | [row0, nc, nr, A(3 nr)]; rows checked against the contacts below
+      if (kind != FDDP_KNOT_EULER_CONTACTFWD) return why = "force costs need contact knots", -1;
+      if (o + kCHdr + 3 > size) return why = "cost records out of range", -1;
       const int row0 = (int)C[kCHdr];
       if ((double)row0 != C[kCHdr] || (row0 < 0 && row0 != kInactiveForceRow))
         return why = "contact-force cost row out of range", -1;
-      if (row0 >= 0) force_rows = std::max(force_rows, row0 + nrf);
+      if (type == C_CONTACT_FORCE) {
+        const int nrf = (int)C[kCHdr + 1];
+        if (nrf != 3 && nrf != 6) return why = "contact-force costs need a 3- or 6-row force", -1;
+        want = kCHdr + 8 + ap * nrf;
+        if (row0 >= 0) force_rows = std::max(force_rows, row0 + nrf);
+      } else {
+        const int ncc = (int)C[kCHdr + 1], nrc = (int)C[kCHdr + 2];
+        if ((double)nrc != C[kCHdr + 2] || nrc < 1 || nrc > 6) return why = "friction cone rows out of [1, 6]", -1;
+        if (row0 >= 0 && ncc != 3 && ncc != 6) return why = "friction cone on a contact of 3 or 6 rows", -1;
+        want = kCHdr + 3 + 3 * nrc + ap * nrc;
+        if (row0 >= 0) force_rows = std::max(force_rows, row0 + ncc);
+      }
     }
     if (want < 0) return why = "unknown cost type " + std::to_string(type), -1;
     if (rs != want || o + rs > size) return why = "cost record of the wrong size", -1;
-    if (type == C_FRAME_PLACEMENT || type == C_FRAME_TRANSLATION) {
+    if (type == C_FRAME_PLACEMENT || type == C_FRAME_TRANSLATION || type == C_FRAME_VELOCITY) {
       const int fj = (int)C[kCHdr];
       if ((double)fj != C[kCHdr] || fj < 0 || fj >= nb) return why = "frame attached to an unknown joint", -1;
     }
     if (type == C_STATE && ff)  // the reference state's free-flyer pose must be finite
       for (int e = 0; e < 7; ++e)
         if (!std::isfinite(C[kCHdr + e])) return why = "non-finite reference state", -1;
-    if (type == C_FRAME_PLACEMENT || type == C_FRAME_TRANSLATION || type == C_COM_POSITION || (type == C_STATE && ff))
+    if (type == C_FRAME_PLACEMENT || type == C_FRAME_TRANSLATION || type == C_COM_POSITION ||
+        type == C_FRAME_VELOCITY || (type == C_STATE && ff))
       ++njac;
+    if (type == C_FRAME_VELOCITY) vcols = true;
     o += rs;
   }
   int nc = 0;
@@ -187,21 +208,22 @@ int64_t mb_block_check(const double* P, int64_t avail, int kind, int nx, int nu,
     int64_t oc = FDDP_PARAM_HEADER + 3 + nj + (int64_t)kJRec * nb;
     for (int k = 0; k < ncost; ++k) {
       const double* C = P + oc;
-      if ((int)C[0] == C_CONTACT_FORCE && (int)C[kCHdr] >= 0) {
+      if (((int)C[0] == C_CONTACT_FORCE || (int)C[0] == C_FRICTION_CONE) && (int)C[kCHdr] >= 0) {
         bool hit = false;
         for (const auto& r : crow) hit = hit || (r.first == (int)C[kCHdr] && r.second == (int)C[kCHdr + 1]);
-        if (!hit) return why = "a contact-force cost must read one whole contact of its size", -1;
+        if (!hit) return why = "a force cost must read one whole contact of its size", -1;
       }
       oc += (int64_t)C[3];
     }
   }
   if (o != size) return why = "block size does not match its records", -1;
-  if (njac > kMaxJacCosts) return why = "more than 8 frame / CoM / free-flyer state costs in one knot", -1;
-  if ((pad2(diff_layout(nj, njac, nc).total) + pad2(size)) * 8 > 160 * 1024)
+  if (njac > kMaxJacCosts) return why = "more than 8 frame / CoM / frame-velocity / free-flyer state costs in one knot", -1;
+  if ((pad2(diff_layout(nj, njac, nc, vcols).total) + pad2(size)) * 8 > 160 * 1024)
     return why = "too many dofs for the calcDiff LDS plan", -1;
   if (nj_out) *nj_out = std::max(*nj_out, nj);
   if (njac_out) *njac_out = std::max(*njac_out, njac);
   if (nc_out) *nc_out = std::max(*nc_out, nc);
+  if (vcols_out) *vcols_out = *vcols_out || vcols;
   return size;
 }
 
@@ -611,6 +633,7 @@ int apply_knots(fddp_handle* h, const fddp_knot_desc* knots, const double* param
   {
     int64_t pmax = 0;
     int mb_nj = 0, mb_njac = 0, mb_nc = 0;
+    bool mb_vcols = false;
     h->has_mb = false;
     for (int t = 0; t <= d.T; ++t) {
       int64_t sz;
@@ -622,7 +645,7 @@ int apply_knots(fddp_handle* h, const fddp_knot_desc* knots, const double* param
           const int64_t off = knots[t].param_offset + (int64_t)b * knots[t].param_stride;
           std::string why;
           sz = std::max(sz, mb_block_check(params + off, n_params - off, knots[t].kind, d.nx, knots[t].nu, why, &mb_nj,
-                                           &mb_njac, &mb_nc));
+                                           &mb_njac, &mb_nc, &mb_vcols));
         }
       } else {
         sz = block_doubles(knots[t].kind, d.nx, knots[t].nu);
@@ -639,7 +662,7 @@ int apply_knots(fddp_handle* h, const fddp_knot_desc* knots, const double* param
         for (int b = 0; b < nb; ++b)
           mb_pmax = std::max<int64_t>(mb_pmax, (int64_t)params[knots[t].param_offset + (int64_t)b * knots[t].param_stride + 3]);
       }
-    D.mbd = h->has_mb ? pad2(fddp::mb::diff_layout(mb_nj, mb_njac, mb_nc).total) : 0;
+    D.mbd = h->has_mb ? pad2(fddp::mb::diff_layout(mb_nj, mb_njac, mb_nc, mb_vcols).total) : 0;
     h->mb_diff_smem = h->has_mb ? sizeof(double) * (D.mbd + pad2(mb_pmax)) : 0;
     const int64_t budget = (150 * 1024) / 8 - (2 * D.sX + D.sM + 2 * D.sN + 5 * (kNT / kWave) + 16) - D.mbw;
     h->pcap = pmax <= budget ? pad2(pmax) : 0;

@@ -58,8 +58,13 @@ enum {
   C_CONTACT_3D = 5,
   C_CONTACT_6D = 6,
   C_CONTACT_FORCE = 7,  // cost on a contact's force: payload [row0, nr, fref(6)] (contact-force.hxx)
-  C_COM_POSITION = 8    // r = com(q) - cref: payload [cref(3)] (com-position.hxx:49-75)
+  C_COM_POSITION = 8,   // r = com(q) - cref: payload [cref(3)] (com-position.hxx:49-75)
+  C_FRICTION_CONE = 9,  // r = A lambda_lin: payload [row0, nc, nr, A (nr x 3 row-major)]
+                        // (contact-friction-cone.hxx:51-91)
+  C_FRAME_VELOCITY = 10  // r = LOCAL frame velocity - vref: frame payload + vref(6) (frame-velocity.hxx:53-84)
 };
+// Activation of a cost record: header slot 2 (core/activations/*.hpp)
+enum { A_QUAD = 0, A_WEIGHTED_QUAD = 1, A_QUAD_BARRIER = 2, A_WEIGHTED_QUAD_BARRIER = 3 };
 constexpr int kInactiveForceRow = -2;  // contact-force cost on an inactive contact: lambda = 0, no Jacobians
 
 struct Blk {
@@ -1003,50 +1008,101 @@ MB_HD inline int frame_residual(const Blk& b, const WVals& V, const CRec& C, con
   return 6;
 }
 
-// Residual size of a cost record, and its activation weights (the last nr
-// doubles of the record).
+// Residual size of a cost record.
 MB_HD inline int cost_nr(const Blk& b, const CRec& C, int nu) {
   const int t = C.type();
   if (t == C_CONTACT_FORCE) return (int)C.d()[1];
+  if (t == C_FRICTION_CONE) return (int)C.d()[2];
   if (t == C_STATE) return 2 * b.nj;
   if (t == C_CONTROL) return nu;
-  return t == C_FRAME_PLACEMENT ? 6 : 3;
+  return (t == C_FRAME_PLACEMENT || t == C_FRAME_VELOCITY) ? 6 : 3;
 }
-MB_HD inline const double* cost_weights(const Blk& b, const CRec& C, int nu) {
-  return C.r + C.size() - cost_nr(b, C, nu);
+// The activation of a cost record (its parameters end the record):
+//   Quad / WeightedQuad (quadratic.hpp, weighted-quadratic.hpp:42-71): w (ones if
+//     unweighted); a = 0.5 w r^2, Ar = w r, Arr = w
+//   QuadraticBarrier (quadratic-barrier.hpp:88-117): lb, ub; with rl = min(r - lb, 0),
+//     ru = max(r - ub, 0): a = 0.5 (rl^2 + ru^2), Ar = rl + ru, Arr = [r <= lb or r >= ub]
+//   WeightedQuadraticBarrier (weighted-quadratic-barrier.hpp:35-70): lb, ub, w;
+//     a = 0.5 w^2 (rl^2 + ru^2), Ar = w^2 (rl + ru), Arr = w [r <= lb or r >= ub]
+// Per residual row i: value2 (twice its share of a: callers sum the rows, then
+// halve), sgrad (X * Ar_i, as (X w) r for the quadratic kinds), hess (Arr_ii).
+struct Act {
+  int kind, nr;
+  const double* p;
+  MB_HD __forceinline__ double value2(int i, double r) const {
+    if (kind <= A_WEIGHTED_QUAD) return p[i] * r * r;
+    const double rl = fmin(r - p[i], 0.), ru = fmax(r - p[nr + i], 0.);
+    const double v = rl * rl + ru * ru;
+    return kind == A_WEIGHTED_QUAD_BARRIER ? p[2 * nr + i] * p[2 * nr + i] * v : v;
+  }
+  MB_HD __forceinline__ double sgrad(int i, double r, double X) const {
+    if (kind <= A_WEIGHTED_QUAD) return X * p[i] * r;
+    const double g = fmin(r - p[i], 0.) + fmax(r - p[nr + i], 0.);
+    return X * (kind == A_WEIGHTED_QUAD_BARRIER ? p[2 * nr + i] * p[2 * nr + i] * g : g);
+  }
+  MB_HD __forceinline__ double hess(int i, double r) const {
+    if (kind <= A_WEIGHTED_QUAD) return p[i];
+    const double h = (r - p[i] <= 0.) ? 1. : ((r - p[nr + i] >= 0.) ? 1. : 0.);
+    return kind == A_WEIGHTED_QUAD_BARRIER ? p[2 * nr + i] * h : h;
+  }
+};
+MB_HD inline Act cost_act(const Blk& b, const CRec& C, int nu) {
+  const int nr = cost_nr(b, C, nu), kind = (int)C.r[2];
+  const int np = kind <= A_WEIGHTED_QUAD ? nr : (kind == A_QUAD_BARRIER ? 2 * nr : 3 * nr);
+  return Act{kind, nr, C.r + C.size() - np};
 }
 // costs whose residual Jacobian is dense over the configuration tangent (stored
-// per cost: rows x nj): frame costs, CoM, and the free-flyer block of a state cost
+// per cost: rows x jw, jw = nj, or 2 nj when a frame-velocity cost needs the
+// velocity columns too): frame costs, CoM, frame velocity, and the free-flyer
+// block of a state cost
 MB_HD __forceinline__ bool jac_cost(const Blk& b, int type) {
   return type == C_FRAME_PLACEMENT || type == C_FRAME_TRANSLATION || type == C_COM_POSITION ||
-         (type == C_STATE && b.ff);
+         type == C_FRAME_VELOCITY || (type == C_STATE && b.ff);
 }
 MB_HD __forceinline__ int jac_rows(int type) {
   return (type == C_FRAME_TRANSLATION || type == C_COM_POSITION) ? 3 : 6;
 }
-MB_HD inline int count_jac_costs(const Blk& b) {
+MB_HD inline int count_jac_costs(const Blk& b, bool* vel_cols = nullptr) {
   int n = 0;
+  bool fv = false;
   const double* cr = b.C;
   for (int k = 0; k < b.ncost; ++k) {
     const CRec C{cr};
     if (jac_cost(b, C.type())) ++n;
+    if (C.type() == C_FRAME_VELOCITY) fv = true;
     cr += C.size();
   }
+  if (vel_cols) *vel_cols = fv;
   return n;
 }
-
-// 0.5 r^T W r of a contact-force cost, r = lambda[row0 .. row0 + nr) - fref
-// (contact-force.hxx:33-50: jMf.actInv(f) is the multiplier itself); an
-// inactive contact has lambda = 0.
-MB_HD inline double force_cost_activation(const Blk& b, const CRec& C, const double* lam, int nu) {
+// costs on the contact multipliers: CostModelContactForce, CostModelContactFrictionCone
+MB_HD __forceinline__ bool force_cost(int type) { return type == C_CONTACT_FORCE || type == C_FRICTION_CONE; }
+// row i of a force cost's residual from the multipliers lam of the contact rows
+// [row0, row0 + nc) (lam unread for an inactive contact: lambda = 0):
+//   contact force: lambda_i - fref_i (contact-force.hxx:33-50: jMf.actInv(f) is the multiplier);
+//   friction cone: A_i . lambda_lin (contact-friction-cone.hxx:58)
+MB_HD __forceinline__ double force_res(const CRec& C, const double* lam, int i) {
   const double* d = C.d();
-  const int row0 = (int)d[0], nr = (int)d[1];
-  const double* w = cost_weights(b, C, nu);
+  const int row0 = (int)d[0];
+  if (C.type() == C_CONTACT_FORCE) return (row0 >= 0 ? lam[row0 + i] : 0.) - d[2 + i];
+  if (row0 < 0) return 0.;
+  const double* A = d + 3 + 3 * i;
+  return A[0] * lam[row0] + A[1] * lam[row0 + 1] + A[2] * lam[row0 + 2];
+}
+// row i of a force cost's Jacobian column from the multiplier Jacobian column
+// dl[row * ld] (the same linear map as force_res, without the offset)
+MB_HD __forceinline__ double force_jac(const CRec& C, const double* dl, int64_t ld, int i) {
+  const double* d = C.d();
+  const int row0 = (int)d[0];
+  if (C.type() == C_CONTACT_FORCE) return dl[(int64_t)(row0 + i) * ld];
+  const double* A = d + 3 + 3 * i;
+  return A[0] * dl[(int64_t)row0 * ld] + A[1] * dl[(int64_t)(row0 + 1) * ld] + A[2] * dl[(int64_t)(row0 + 2) * ld];
+}
+// activation value of a force cost (inactive contact: lambda = 0)
+MB_HD inline double force_cost_activation(const Blk& b, const CRec& C, const double* lam, int nu) {
+  const Act act = cost_act(b, C, nu);
   double a = 0.;
-  for (int e = 0; e < nr; ++e) {
-    const double r = (row0 >= 0 ? lam[row0 + e] : 0.) - d[2 + e];
-    a += w[e] * r * r;
-  }
+  for (int e = 0; e < act.nr; ++e) a += act.value2(e, force_res(C, lam, e));
   return 0.5 * a;
 }
 
@@ -1095,10 +1151,23 @@ MB_HD __forceinline__ double state_res(const Blk& b, const double* xref, const d
   return x[b.nq + i - b.nj] - xref[b.nq + i - b.nj];
 }
 
-// 0.5 r^T W r of one cost record (kinematics in V).
+// LOCAL velocity of a frame payload d minus vref (pinocchio::getFrameVelocity,
+// frame-velocity.hxx:57-59), from the world body velocities in V.
+MB_HD inline void frame_velocity_res(const Blk& b, const WVals& V, const double* d, double* r) {
+  const int j = frame_dof(b, d);
+  double Rf[9], pf[3], m6[6];
+  frame_placement(b, V, d, Rf, pf);
+  for (int e = 0; e < 6; ++e) m6[e] = V.v(j)[e];
+  motion_act_inv(Rf, pf, m6, r);
+  for (int e = 0; e < 6; ++e) r[e] -= d[13 + e];
+}
+
+// Activation value of one cost record (kinematics in V; velocities in V only with
+// vel: frame-velocity costs are skipped without). Force costs return 0: they need
+// the multipliers and are added after the contact solve.
 MB_HD __forceinline__ double cost_activation(const Blk& b, const WVals& V, const CRec& C, const double* x,
-                                             const double* u, int nu) {
-  const double* w = cost_weights(b, C, nu);
+                                             const double* u, int nu, bool vel = true) {
+  const Act act = cost_act(b, C, nu);
   double a = 0.;
   if (C.type() == C_STATE) {
     const int ndx = 2 * b.nj;
@@ -1107,39 +1176,35 @@ MB_HD __forceinline__ double cost_activation(const Blk& b, const WVals& V, const
       double Rr[9], pr[3], r[6];
       ff_rel(C.d(), x, Rr, pr);
       log6_t<double>(Rr, pr, r);
-      for (int e = 0; e < 6; ++e) a += w[e] * r[e] * r[e];
+      for (int e = 0; e < 6; ++e) a += act.value2(e, r[e]);
       i0 = 6;
     }
-    for (int i = i0; i < ndx; ++i) {
-      const double r = state_res(b, C.d(), x, i);
-      a += w[i] * r * r;
-    }
+    for (int i = i0; i < ndx; ++i) a += act.value2(i, state_res(b, C.d(), x, i));
   } else if (C.type() == C_CONTROL) {
-    for (int i = 0; i < nu; ++i) {
-      const double r = u[i] - C.d()[i];
-      a += w[i] * r * r;
-    }
-  } else if (C.type() == C_CONTACT_FORCE) {
-    return 0.;  // needs the multipliers: added after the contact solve
+    for (int i = 0; i < nu; ++i) a += act.value2(i, u[i] - C.d()[i]);
+  } else if (force_cost(C.type())) {
+    return 0.;
   } else if (C.type() == C_COM_POSITION) {
     double c[3];
     com_value(b, V, c);
-    for (int i = 0; i < 3; ++i) {
-      const double r = c[i] - C.d()[i];
-      a += w[i] * r * r;
-    }
+    for (int i = 0; i < 3; ++i) a += act.value2(i, c[i] - C.d()[i]);
+  } else if (C.type() == C_FRAME_VELOCITY) {
+    if (!vel) return 0.;
+    double r[6];
+    frame_velocity_res(b, V, C.d(), r);
+    for (int i = 0; i < 6; ++i) a += act.value2(i, r[i]);
   } else {
     double r[6] = {0., 0., 0., 0., 0., 0.};
     const int nr = frame_residual_value(b, V, C, r);
 #pragma unroll
     for (int i = 0; i < 6; ++i)  // fixed trip count: r stays in registers
-      if (i < nr) a += w[i] * r[i] * r[i];
+      if (i < nr) a += act.value2(i, r[i]);
   }
   return 0.5 * a;
 }
 
-// Cost value of the DAM (one thread; kinematics in V): sum of weight * 0.5 r^T W r
-// in record (name) order (cost-sum.hxx:89-117).
+// Cost value of the DAM (one thread; kinematics and velocities in V): sum of
+// weight * activation in record (name) order (cost-sum.hxx:89-117).
 MB_HD inline double cost_value(const Blk& b, const WVals& V, const double* x, const double* u, int nu) {
   double total = 0.;
   const double* cr = b.C;
@@ -1361,7 +1426,7 @@ MB_HD inline double knot_calc_x(const X& ex, const double* P, int nx, const doub
     const double* cr = b.C;
     for (int k = 0; k < b.ncost; ++k) {
       const CRec C{cr};
-      if (wave == 2 + (k & 1) && l == (k >> 1)) cv[k] = C.weight() * cost_activation(b, W, C, x, ub, nu);
+      if (wave == 2 + (k & 1) && l == (k >> 1)) cv[k] = C.weight() * cost_activation(b, W, C, x, ub, nu, false);
       cr += C.size();
     }
     const int kc = l - 32;  // contact position terms on the upper half of wave 2
@@ -1389,8 +1454,10 @@ MB_HD inline double knot_calc_x(const X& ex, const double* P, int nx, const doub
       for (int k = 0; k < b.ncost; ++k) {
         const CRec C{cr};
         total += cv[k];
-        // contact-force costs without active contact rows (lambda = 0)
-        if (C.type() == C_CONTACT_FORCE && nc == 0) total += C.weight() * force_cost_activation(b, C, nullptr, nu);
+        // force costs without active contact rows (lambda = 0)
+        if (force_cost(C.type()) && nc == 0) total += C.weight() * force_cost_activation(b, C, nullptr, nu);
+        // frame velocities, now that the body velocities exist (impulse knots: rejected by the host)
+        if (C.type() == C_FRAME_VELOCITY && !imp) total += C.weight() * cost_activation(b, W, C, x, ub, nu);
         cr += C.size();
       }
       red[0] = total;
@@ -1419,7 +1486,7 @@ MB_HD inline double knot_calc_x(const X& ex, const double* P, int nx, const doub
         const double* cr = b.C;
         for (int k = 0; k < b.ncost; ++k) {
           const CRec C{cr};
-          if (C.type() == C_CONTACT_FORCE) add += C.weight() * force_cost_activation(b, C, lamv, nu);
+          if (force_cost(C.type())) add += C.weight() * force_cost_activation(b, C, lamv, nu);
           cr += C.size();
         }
         red[0] += add;
@@ -1492,7 +1559,7 @@ struct DiffLayout {
 };
 // vec area: x (nq + nj <= 2 nj + 1), u (nj), nle / z / a / tau (3 nj), jac-cost
 // residuals (6 per cost), Jexp6 / Ad(exp6^-1) (72)
-__host__ __device__ inline DiffLayout diff_layout(int nj, int njac, int nc = 0) {
+__host__ __device__ inline DiffLayout diff_layout(int nj, int njac, int nc = 0, bool vel_cols = false) {
   const int L = 2 * nj;
   DiffLayout l;
   l.wv = 0;
@@ -1502,7 +1569,7 @@ __host__ __device__ inline DiffLayout diff_layout(int nj, int njac, int nc = 0) 
   l.qp = l.da + (int64_t)nj * L;        // da = -Kinv (dtau; da0) [r][L]
   l.vec = l.qp + (int64_t)12 * nj;      // Q_k, P_k
   l.J = l.vec + pad2(6 * nj + 1 + 6 * kMaxJacCosts + 72);
-  l.red = l.J + (int64_t)6 * nj * (njac > 0 ? njac : 1);  // jac-cost Jacobians [cost][6][nj]
+  l.red = l.J + (int64_t)6 * (vel_cols ? L : nj) * (njac > 0 ? njac : 1);  // jac-cost Jacobians [cost][6][jw]
   l.total = l.red + 8;
   l.Jc = l.total;
   l.a0 = l.Jc + (int64_t)nc * nj;
@@ -1727,10 +1794,11 @@ MB_HD inline void impulse_direction(const Blk& b, const WVals& W, int j, int L, 
   }
 }
 
-// lane j < nj: column j of every jac-cost Jacobian (Jf[(f*6 + e)*nj + j]) and, on
-// lane 0, their residuals (rf[6 f + e]); lanes j < 6 of a free-flyer knot also the
-// Euler step's Jexp6(dq) column j (Je, col-major 6x6) and, on lane 0, Ad(exp6(dq)^-1) (Ai).
-MB_HD inline void jac_lane(const Blk& b, const WVals& W, const double* x, int j, double* Jf, double* rf,
+// lane j < nj: column j of every jac-cost Jacobian (Jf[(f*6 + e)*jw + j]; a
+// frame-velocity cost also its velocity column nj + j) and, on lane 0, their
+// residuals (rf[6 f + e]); lanes j < 6 of a free-flyer knot also the Euler step's
+// Jexp6(dq) column j (Je, col-major 6x6) and, on lane 0, Ad(exp6(dq)^-1) (Ai).
+MB_HD inline void jac_lane(const Blk& b, const WVals& W, const double* x, int j, double* Jf, int jw, double* rf,
                            const double* dqff, double* Je, double* Ai) {
   const int nj = b.nj;
   double S[6];
@@ -1745,6 +1813,22 @@ MB_HD inline void jac_lane(const Blk& b, const WVals& W, const double* x, int j,
       if (t == C_FRAME_PLACEMENT || t == C_FRAME_TRANSLATION) {
         const bool sup = (*W.anc(frame_dof(b, C.d())) >> j) & 1ull;
         frame_residual(b, W, C, sup ? S : nullptr, r, Jc);
+      } else if (t == C_FRAME_VELOCITY) {  // getFrameVelocityDerivatives (LOCAL)
+        // dv_f/dq_j = -Ad(oMf)^-1 (S_j x V_P) (the transport of the subtree cancels),
+        // dv_f/dv_j = Ad(oMf)^-1 S_j, for the dofs that move the frame's body
+        const double* d = C.d();
+        double Jv[6] = {0., 0., 0., 0., 0., 0.};
+        if ((*W.anc(frame_dof(b, d)) >> j) & 1ull) {
+          double Rf[9], pf[3], VP[6], AP[6], u6[6];
+          frame_placement(b, W, d, Rf, pf);
+          parent_motion(b, W, j, VP, AP);
+          cross_m(S, VP, u6);
+          for (int e = 0; e < 6; ++e) u6[e] = -u6[e];
+          motion_act_inv(Rf, pf, u6, Jc);
+          motion_act_inv(Rf, pf, S, Jv);
+        }
+        for (int e = 0; e < 6; ++e) Jf[((int64_t)f * 6 + e) * jw + nj + j] = Jv[e];
+        if (j == 0) frame_velocity_res(b, W, d, r);
       } else if (t == C_COM_POSITION) {  // Jcom col j = (m_sub S_lin + S_ang x h_sub) / m_total
         double mt = 0.;
         for (int bb = 0; bb < nj; ++bb)
@@ -1768,7 +1852,7 @@ MB_HD inline void jac_lane(const Blk& b, const WVals& W, const double* x, int j,
 #pragma unroll
       for (int e = 0; e < 6; ++e)
         if (e < nr) {
-          Jf[((int64_t)f * 6 + e) * nj + j] = Jc[e];
+          Jf[((int64_t)f * 6 + e) * jw + j] = Jc[e];
           if (j == 0) rf[6 * f + e] = r[e];
         }
       ++f;
@@ -1814,8 +1898,10 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
   const Blk b = parse(P);
   const bool imp = b.impulse;  // ActionModelImpulseFwdDynamics (impulse-fwddyn.hxx:53-127)
   const int nj = b.nj, nq = b.nq, n = 2 * nj, L = 2 * nj, nc = b.nc, nu = nj - b.nun;
-  const int njac = count_jac_costs(b);
-  const DiffLayout l = diff_layout(nj, njac, nc);
+  bool vcols;
+  const int njac = count_jac_costs(b, &vcols);
+  const int jw = vcols ? L : nj;  // columns of the stored jac-cost Jacobians
+  const DiffLayout l = diff_layout(nj, njac, nc, vcols);
   const WVals W{w + l.wv, nj};
   double* A = w + l.A;
   double* dtau = w + l.dtau;
@@ -1959,7 +2045,7 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
         const double* cr = b.C;
         for (int k = 0; k < b.ncost; ++k) {
           const CRec C{cr};
-          if (C.type() == C_CONTACT_FORCE) cc += C.weight() * force_cost_activation(b, C, lam, nu);
+          if (force_cost(C.type())) cc += C.weight() * force_cost_activation(b, C, lam, nu);
           cr += C.size();
         }
         *cost_out = dt != 0. ? dt * cc : cc;
@@ -1978,7 +2064,7 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
     double dq[6];
     if (ffe)
       for (int e = 0; e < 6; ++e) dq[e] = x[nq + e] * dt + av[e] * dt2;
-    jac_lane(b, W, x, lane, Jf, rf, ffe ? dq : nullptr, Je, Ai);
+    jac_lane(b, W, x, lane, Jf, jw, rf, ffe ? dq : nullptr, Je, Ai);
   });
   if (imp) {  // V = 0 in the impulse RNEA: P_k = 0, Q_k = Ycrb_k S_k
     ex.run([&](int lane) {
@@ -2083,17 +2169,16 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
         }
       }
       Fu[e] = f;
-      double lxu = 0.;  // only contact-force costs couple x and u
+      double lxu = 0.;  // only the force costs couple x and u
       if (fd && c < nu) {
         const double* cr = b.C;
         for (int k = 0; k < b.ncost; ++k) {
           const CRec C{cr};
-          if (C.type() == C_CONTACT_FORCE && (int)C.d()[0] >= 0) {
-            const int row0 = (int)C.d()[0], nr = (int)C.d()[1];
-            const double* wv = cost_weights(b, C, nu);
+          if (force_cost(C.type()) && (int)C.d()[0] >= 0) {
+            const Act act = cost_act(b, C, nu);
             double s2 = 0.;
-            for (int r = 0; r < nr; ++r)
-              s2 += dfx[(int64_t)(row0 + r) * L + i] * wv[r] * dfu[(int64_t)(row0 + r) * nj + c];
+            for (int r = 0; r < act.nr; ++r)
+              s2 += force_jac(C, dfx + i, L, r) * act.hess(r, force_res(C, lam, r)) * force_jac(C, dfu + c, nj, r);
             lxu += C.weight() * s2;
           }
           cr += C.size();
@@ -2111,23 +2196,25 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
         const CRec C{cr};
         const int t = C.type();
         const double wt = C.weight();
-        const double* wv = cost_weights(b, C, nu);
         if (jac_cost(b, t)) {
-          if (i < nj && j < nj) {
+          const int cols = t == C_FRAME_VELOCITY ? L : nj;
+          if (i < cols && j < cols) {
+            const Act act = cost_act(b, C, nu);
             const int nr = jac_rows(t);
-            const double* Jk = Jf + (int64_t)f * 6 * nj;
+            const double* Jk = Jf + (int64_t)f * 6 * jw;
             double s2 = 0.;
-            for (int r = 0; r < nr; ++r) s2 += Jk[(int64_t)r * nj + i] * wv[r] * Jk[(int64_t)r * nj + j];
+            for (int r = 0; r < nr; ++r) s2 += Jk[(int64_t)r * jw + i] * act.hess(r, rf[6 * f + r]) * Jk[(int64_t)r * jw + j];
             lv += wt * s2;
           }
           ++f;
         }
-        if (t == C_STATE && i == j && !(b.ff && i < 6)) lv += wt * wv[j];
-        if (t == C_CONTACT_FORCE && fd && (int)C.d()[0] >= 0) {
-          const int row0 = (int)C.d()[0], nr = (int)C.d()[1];
+        if (t == C_STATE && i == j && !(b.ff && i < 6))
+          lv += wt * cost_act(b, C, nu).hess(j, state_res(b, C.d(), x, j));
+        if (force_cost(t) && fd && (int)C.d()[0] >= 0) {
+          const Act act = cost_act(b, C, nu);
           double s2 = 0.;
-          for (int r = 0; r < nr; ++r)
-            s2 += dfx[(int64_t)(row0 + r) * L + i] * wv[r] * dfx[(int64_t)(row0 + r) * L + j];
+          for (int r = 0; r < act.nr; ++r)
+            s2 += force_jac(C, dfx + i, L, r) * act.hess(r, force_res(C, lam, r)) * force_jac(C, dfx + j, L, r);
           lv += wt * s2;
         }
         cr += C.size();
@@ -2142,13 +2229,12 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
         const double* cr = b.C;
         for (int k = 0; k < b.ncost; ++k) {
           const CRec C{cr};
-          if (C.type() == C_CONTROL && i == j) lv += C.weight() * cost_weights(b, C, nu)[j];
-          if (C.type() == C_CONTACT_FORCE && fd && (int)C.d()[0] >= 0) {
-            const int row0 = (int)C.d()[0], nr = (int)C.d()[1];
-            const double* wv = cost_weights(b, C, nu);
+          if (C.type() == C_CONTROL && i == j) lv += C.weight() * cost_act(b, C, nu).hess(j, u[j] - C.d()[j]);
+          if (force_cost(C.type()) && fd && (int)C.d()[0] >= 0) {
+            const Act act = cost_act(b, C, nu);
             double s2 = 0.;
-            for (int r = 0; r < nr; ++r)
-              s2 += dfu[(int64_t)(row0 + r) * nj + i] * wv[r] * dfu[(int64_t)(row0 + r) * nj + j];
+            for (int r = 0; r < act.nr; ++r)
+              s2 += force_jac(C, dfu + i, nj, r) * act.hess(r, force_res(C, lam, r)) * force_jac(C, dfu + j, nj, r);
             lv += C.weight() * s2;
           }
           cr += C.size();
@@ -2163,12 +2249,11 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
         const double* cr = b.C;
         for (int k = 0; k < b.ncost; ++k) {
           const CRec C{cr};
-          if (C.type() == C_CONTROL) lu += C.weight() * cost_weights(b, C, nu)[j] * (u[j] - C.d()[j]);
-          if (C.type() == C_CONTACT_FORCE && fd && (int)C.d()[0] >= 0) {
-            const int row0 = (int)C.d()[0], nr = (int)C.d()[1];
-            const double* wv = cost_weights(b, C, nu);
-            for (int r = 0; r < nr; ++r)
-              lu += C.weight() * dfu[(int64_t)(row0 + r) * nj + j] * wv[r] * (lam[row0 + r] - C.d()[2 + r]);
+          if (C.type() == C_CONTROL) lu += cost_act(b, C, nu).sgrad(j, u[j] - C.d()[j], C.weight());
+          if (force_cost(C.type()) && fd && (int)C.d()[0] >= 0) {
+            const Act act = cost_act(b, C, nu);
+            for (int r = 0; r < act.nr; ++r)
+              lu += act.sgrad(r, force_res(C, lam, r), C.weight() * force_jac(C, dfu + j, nj, r));
           }
           cr += C.size();
         }
@@ -2183,20 +2268,19 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
         const CRec C{cr};
         const int t = C.type();
         const double wt = C.weight();
-        const double* wv = cost_weights(b, C, nu);
         if (jac_cost(b, t)) {
-          if (j < nj) {
+          if (j < (t == C_FRAME_VELOCITY ? L : nj)) {
+            const Act act = cost_act(b, C, nu);
             const int nr = jac_rows(t);
-            const double* Jk = Jf + (int64_t)f * 6 * nj;
-            for (int r = 0; r < nr; ++r) lx += wt * Jk[(int64_t)r * nj + j] * wv[r] * rf[6 * f + r];
+            const double* Jk = Jf + (int64_t)f * 6 * jw;
+            for (int r = 0; r < nr; ++r) lx += act.sgrad(r, rf[6 * f + r], wt * Jk[(int64_t)r * jw + j]);
           }
           ++f;
         }
-        if (t == C_STATE && !(b.ff && j < 6)) lx += wt * wv[j] * state_res(b, C.d(), x, j);
-        if (t == C_CONTACT_FORCE && fd && (int)C.d()[0] >= 0) {
-          const int row0 = (int)C.d()[0], nr = (int)C.d()[1];
-          for (int r = 0; r < nr; ++r)
-            lx += wt * dfx[(int64_t)(row0 + r) * L + j] * wv[r] * (lam[row0 + r] - C.d()[2 + r]);
+        if (t == C_STATE && !(b.ff && j < 6)) lx += cost_act(b, C, nu).sgrad(j, state_res(b, C.d(), x, j), wt);
+        if (force_cost(t) && fd && (int)C.d()[0] >= 0) {
+          const Act act = cost_act(b, C, nu);
+          for (int r = 0; r < act.nr; ++r) lx += act.sgrad(r, force_res(C, lam, r), wt * force_jac(C, dfx + j, L, r));
         }
         cr += C.size();
       }
@@ -2210,21 +2294,18 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
       for (int k = 0; k < b.ncost; ++k) {
         const CRec C{cr};
         const int t = C.type();
-        const double* wv = cost_weights(b, C, nu);
+        const Act act = cost_act(b, C, nu);
         double a = 0.;
         if (jac_cost(b, t)) {
           const int nr = jac_rows(t);
-          for (int i = 0; i < nr; ++i) a += wv[i] * rf[6 * f + i] * rf[6 * f + i];
+          for (int i = 0; i < nr; ++i) a += act.value2(i, rf[6 * f + i]);
           ++f;
         }
         if (t == C_STATE) {
-          for (int i = b.ff ? 6 : 0; i < n; ++i) {
-            const double r = state_res(b, C.d(), x, i);
-            a += wv[i] * r * r;
-          }
+          for (int i = b.ff ? 6 : 0; i < n; ++i) a += act.value2(i, state_res(b, C.d(), x, i));
         } else if (t == C_CONTROL) {
-          for (int i = 0; i < nu; ++i) a += wv[i] * (u[i] - C.d()[i]) * (u[i] - C.d()[i]);
-        } else if (t == C_CONTACT_FORCE) {
+          for (int i = 0; i < nu; ++i) a += act.value2(i, u[i] - C.d()[i]);
+        } else if (force_cost(t)) {
           a = 2. * force_cost_activation(b, C, lam, nu);
         }
         total += C.weight() * (0.5 * a);

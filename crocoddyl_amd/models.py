@@ -332,6 +332,13 @@ class IntegratedActionModelEuler(ActionModelAbstract):
         self._dt = float(v)
         self._touch()
 
+    def quasiStatic(self, data, x, maxiter=100, tol=1e-9):
+        """IntegratedActionModelEuler::quasiStatic (euler.hxx:185-201): the
+        differential model's quasi-static controls (multibody DAMs only)."""
+        if not self._mb:
+            raise NotImplementedError("crocoddyl_amd: quasiStatic is covered for the multibody models")
+        return self.differential.quasiStatic(x, maxiter, tol)
+
     def pack(self):
         d = self.differential
         if self._mb:

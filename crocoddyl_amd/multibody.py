@@ -36,6 +36,7 @@ CONTACT_3D, CONTACT_6D = 5, 6
 COST_CONTACT_FORCE = 7
 COST_COM_POSITION = 8
 COST_FRICTION_CONE = 9
+COST_FRAME_VELOCITY = 10
 MAX_CONTACT_ROWS = 24
 MAX_DOFS = 64  # nv of the device path (one lane per tangent direction of a wave pair)
 
@@ -138,6 +139,7 @@ class RobotModel:
         self.frames = [("universe", 0, SE3())]
         self.gravity = np.array([0.0, 0.0, -9.81])  # pinocchio Model::gravity981
         self.referenceConfigurations = {}
+        self._limits = {}  # joint id -> (lower, upper, velocity) (pinocchio Model limits; +-inf by default)
         self._version = 0
         if root_joint is not None:  # pinocchio::buildModel(urdf, JointModelFreeFlyer(), model)
             self.addJoint(0, root_joint, SE3(), "root_joint")
@@ -192,6 +194,34 @@ class RobotModel:
         self.inertias.append(Inertia.Zero())
         self._version += 1
         return self.njoints - 1
+
+    def setJointLimits(self, joint_id, lower, upper, velocity):
+        """Position / velocity limits of a revolute joint (the URDF <limit> that
+        pinocchio stores in lower/upperPositionLimit, velocityLimit)."""
+        self._limits[int(joint_id)] = (float(lower), float(upper), float(velocity))
+
+    @property
+    def lowerPositionLimit(self):
+        return self._qlim(0, -np.inf)
+
+    @property
+    def upperPositionLimit(self):
+        return self._qlim(1, np.inf)
+
+    @property
+    def velocityLimit(self):
+        out = np.full(self.nv, np.inf)
+        for j in range(1, self.njoints):
+            if self.kinds[j] != JOINT_FREEFLYER and j in self._limits:
+                out[self.idx_v(j)] = self._limits[j][2]
+        return out
+
+    def _qlim(self, k, default):
+        out = np.full(self.nq, default)
+        for j in range(1, self.njoints):
+            if self.kinds[j] != JOINT_FREEFLYER and j in self._limits:
+                out[self.idx_q(j)] = self._limits[j][k]
+        return out
 
     def getJointId(self, name):
         if name in self.names:
@@ -248,6 +278,63 @@ class RobotModel:
         mt = sum(I.mass for I in self.inertias)
         c = sum(I.mass * (oM[j].translation + oM[j].rotation @ I.lever) for j, I in enumerate(self.inertias))
         return c / mt
+
+    def _world_motions(self, q, oM):
+        """(nv, 6) world motion subspace of every dof at the world origin (linear,
+        angular) and the joint owning it; free-flyer dofs are the base twist axes in
+        the base frame (pinocchio's local free-flyer velocity)."""
+        S, owner = [], []
+        for j in range(1, self.njoints):
+            R, p = oM[j].rotation, oM[j].translation
+            if self.kinds[j] == JOINT_FREEFLYER:
+                for k in range(6):
+                    ax = R[:, k % 3]
+                    S.append(np.concatenate([ax, np.zeros(3)]) if k < 3 else np.concatenate([np.cross(p, ax), ax]))
+                    owner.append(j)
+            else:
+                w = R @ self.axes[j]
+                S.append(np.concatenate([np.cross(p, w), w]))
+                owner.append(j)
+        return np.array(S), owner
+
+    def _ancestors(self, j):
+        out = set()
+        while j > 0:
+            out.add(j)
+            j = self.parents[j]
+        return out
+
+    def getFrameJacobian(self, q, frame_id):
+        """pinocchio::getFrameJacobian(LOCAL) after computeJointJacobians (6 x nv)."""
+        oM = self.placements(q)
+        S, owner = self._world_motions(q, oM)
+        name, pj, pl = self.frames[frame_id]
+        oMf = oM[pj] * pl
+        anc = self._ancestors(pj)
+        Rt, pf = oMf.rotation.T, oMf.translation
+        J = np.zeros((6, self.nv))
+        for d in range(self.nv):
+            if owner[d] in anc:
+                J[:3, d] = Rt @ (S[d, :3] - np.cross(pf, S[d, 3:]))
+                J[3:, d] = Rt @ S[d, 3:]
+        return J
+
+    def computeGeneralizedGravity(self, q):
+        """pinocchio::computeGeneralizedGravity = rnea(q, 0, 0): tau_d = S_d . F_d with F
+        the gravity wrenches (-m g at the CoM, about the world origin) of d's subtree."""
+        oM = self.placements(q)
+        S, owner = self._world_motions(q, oM)
+        wrench = np.zeros((self.njoints, 6))
+        for j in range(1, self.njoints):
+            I = self.inertias[j]
+            f = -I.mass * self.gravity
+            c = oM[j].translation + oM[j].rotation @ I.lever
+            wrench[j] = np.concatenate([f, np.cross(c, f)])
+        tau = np.zeros(self.nv)
+        for d in range(self.nv):
+            F = sum(wrench[b] for b in range(1, self.njoints) if owner[d] in self._ancestors(b))
+            tau[d] = S[d] @ F
+        return tau
 
     def pack_robot(self, armature):
         """gravity(3) armature(nv) then one 27-double record per joint:
@@ -402,6 +489,12 @@ class StateMultibody:
         self.nv = model.nv
         self.nx = self.nq + self.nv
         self.ndx = 2 * self.nv
+        # limits (multibody.hxx:23-34): the first joint unbounded, then the model's
+        nq0 = 7 if model.has_freeflyer else 1
+        lb = np.concatenate([model.lowerPositionLimit, -model.velocityLimit])
+        ub = np.concatenate([model.upperPositionLimit, model.velocityLimit])
+        lb[:nq0], ub[:nq0] = -np.inf, np.inf
+        self.lb, self.ub = lb, ub
 
     def zero(self):
         return np.concatenate([self.pinocchio.neutral(), np.zeros(self.nv)])
@@ -461,26 +554,210 @@ class ActuationModelFloatingBase:
         self.nu = state.nv - self.nun
 
 
+ACT_QUAD, ACT_WEIGHTED_QUAD, ACT_QUAD_BARRIER, ACT_WEIGHTED_QUAD_BARRIER = 0, 1, 2, 3
+DBL_MAX = np.finfo(np.float64).max
+
+
 class ActivationModelQuad:
     """a = 0.5 ||r||^2, Ar = r, Arr = I (core/activations/quadratic.hpp)."""
+
+    kind = ACT_QUAD
 
     def __init__(self, nr):
         self.nr = int(nr)
         self.weights = None
 
+    def params(self):
+        return np.ones((1, self.nr))
+
 
 class ActivationModelWeightedQuad:
     """a = 0.5 r^T diag(w) r, Ar = w r, Arr = diag(w) (weighted-quadratic.hpp:42-71)."""
 
+    kind = ACT_WEIGHTED_QUAD
+
     def __init__(self, weights):
         self.weights = np.array(weights, np.float64).reshape(-1)
         self.nr = self.weights.size
+
+    def params(self):
+        return self.weights.reshape(1, -1)
+
+
+class ActivationBounds:
+    """ActivationBounds(lb, ub, beta=1) (quadratic-barrier.hpp:24-68): the bounds
+    are stored shrunk around their midpoint, m -+ beta d with m = (lb + ub) / 2,
+    d = (ub - lb) / 2 (so infinite bounds give NaN, as in the reference)."""
+
+    def __init__(self, lb, ub, beta=1.0):
+        lb = np.array(lb, np.float64).reshape(-1)
+        ub = np.array(ub, np.float64).reshape(-1)
+        if lb.size != ub.size:
+            raise ValueError("Invalid argument: The lower and upper bounds don't have the same dimension "
+                             f"(lb,ub dimensions equal to {lb.size},{ub.size}, respectively)")
+        if beta < 0.0 or beta > 1.0:
+            raise ValueError("Invalid argument: The range of beta is between 0 and 1")
+        fin = np.isfinite(lb) & np.isfinite(ub)
+        if np.any(lb[fin] - ub[fin] > 0):
+            raise ValueError("Invalid argument: The lower and upper bounds are badly defined; ub has to be "
+                             "bigger / equals to lb")
+        with np.errstate(invalid="ignore", over="ignore"):
+            m = 0.5 * (lb + ub)
+            d = 0.5 * (ub - lb)
+            self.lb = m - beta * d
+            self.ub = m + beta * d
+        self.beta = float(beta)
+
+
+class ActivationModelQuadraticBarrier:
+    """a = 0.5 ||min(r - lb, 0)||^2 + 0.5 ||max(r - ub, 0)||^2, Ar = min(r - lb, 0) +
+    max(r - ub, 0), Arr = diag(r <= lb or r >= ub) (quadratic-barrier.hpp:88-117)."""
+
+    kind = ACT_QUAD_BARRIER
+
+    def __init__(self, bounds):
+        if not isinstance(bounds, ActivationBounds):
+            raise TypeError("ActivationModelQuadraticBarrier needs an ActivationBounds")
+        self.bounds = bounds
+        self.nr = bounds.lb.size
+        self.weights = None
+
+    def params(self):
+        return np.concatenate([self.bounds.lb, self.bounds.ub]).reshape(1, -1)
+
+
+class ActivationModelWeightedQuadraticBarrier:
+    """ActivationModelWeightedQuadraticBarrier(bounds, weights)
+    (weighted-quadratic-barrier.hpp:35-70): the barrier residuals scaled by w before
+    squaring, a = 0.5 sum w^2 (rl^2 + ru^2), Ar = w^2 (rl + ru), and — as the
+    reference has it — Arr = w (r <= lb or r >= ub)."""
+
+    kind = ACT_WEIGHTED_QUAD_BARRIER
+
+    def __init__(self, bounds, weights):
+        if not isinstance(bounds, ActivationBounds):
+            raise TypeError("ActivationModelWeightedQuadraticBarrier needs an ActivationBounds")
+        self.bounds = bounds
+        self.weights = np.array(weights, np.float64).reshape(-1)
+        self.nr = bounds.lb.size
+        if self.weights.size != self.nr:
+            raise ValueError(f"Invalid argument: weight vector has wrong dimension (it should be {self.nr})")
+
+    def params(self):
+        return np.concatenate([self.bounds.lb, self.bounds.ub, self.weights]).reshape(1, -1)
+
+
+_ACTIVATIONS = (ActivationModelQuad, ActivationModelWeightedQuad, ActivationModelQuadraticBarrier,
+                ActivationModelWeightedQuadraticBarrier)
+
+
+def _quat_from_two_vectors(a, b):
+    """Eigen Quaternion::setFromTwoVectors(a, b) as a rotation matrix (the rotation
+    taking a onto b)."""
+    v0 = np.asarray(a, float) / np.linalg.norm(a)
+    v1 = np.asarray(b, float) / np.linalg.norm(b)
+    c = float(v1 @ v0)
+    if c < -1.0 + np.finfo(float).eps:  # antiparallel: the axis from the null space of [v0; v1]
+        c = max(c, -1.0)
+        _, _, vt = np.linalg.svd(np.vstack([v0, v1]))
+        axis = vt[2]
+        w2 = (1.0 + c) * 0.5
+        q = np.concatenate([axis * np.sqrt(1.0 - w2), [np.sqrt(w2)]])
+    else:
+        axis = np.cross(v0, v1)
+        s = np.sqrt((1.0 + c) * 2.0)
+        q = np.concatenate([axis / s, [0.5 * s]])
+    return _quat_to_R(q)
+
+
+class FrictionCone:
+    """FrictionCone(normal, mu, nf=4, inner_appr=True, min_nforce=0, max_nforce=DBL_MAX)
+    (multibody/friction-cone.hxx:24-96): lb <= A f <= ub with nf facets
+    A_{2i} = (-mu z + t_i)^T cRo, A_{2i+1} = (-mu z - t_i)^T cRo (t_i at angle 2 pi i / nf,
+    mu scaled by cos(pi / nf) for the inner approximation) and the normal row
+    nsurf^T in [min_nforce, max_nforce]."""
+
+    def __init__(self, normal=(0.0, 0.0, 1.0), mu=0.7, nf=4, inner_appr=True, min_nforce=0.0, max_nforce=DBL_MAX):
+        nf = int(nf)
+        if nf % 2 != 0:
+            nf = 4  # the reference warns and uses 4
+        self.nf = nf
+        self.update(normal, mu, inner_appr, min_nforce, max_nforce)
+
+    def update(self, normal, mu, inner_appr=True, min_nforce=0.0, max_nforce=DBL_MAX):
+        n = np.array(normal, np.float64).reshape(3)
+        if abs(np.linalg.norm(n) - 1.0) > 1e-12:
+            n = n / np.linalg.norm(n)
+        self.nsurf = n
+        self.mu = float(mu)
+        self.inner_appr = bool(inner_appr)
+        self.min_nforce = float(min_nforce) if min_nforce >= 0 else 0.0
+        self.max_nforce = float(max_nforce) if max_nforce >= 0 else DBL_MAX
+        theta = 2.0 * np.pi / self.nf
+        if self.inner_appr:
+            self.mu *= np.cos(theta / 2.0)
+        cRo = _quat_from_two_vectors(n, (0.0, 0.0, 1.0))
+        A = np.zeros((self.nf + 1, 3))
+        lb = np.zeros(self.nf + 1)
+        ub = np.zeros(self.nf + 1)
+        z = np.array([0.0, 0.0, 1.0])
+        for i in range(self.nf // 2):
+            ti = np.array([np.cos(theta * i), np.sin(theta * i), 0.0])
+            A[2 * i] = (-self.mu * z + ti) @ cRo
+            A[2 * i + 1] = (-self.mu * z - ti) @ cRo
+            lb[2 * i] = lb[2 * i + 1] = -DBL_MAX
+        A[self.nf] = n
+        lb[self.nf] = self.min_nforce
+        ub[self.nf] = self.max_nforce
+        self.A, self.lb, self.ub = A, lb, ub
+
+
+class FrameFrictionCone:
+    """FrameFrictionCone(id, cone) (multibody/frames.hpp:139-152)."""
+
+    def __init__(self, id, cone):
+        self.id = int(id)
+        self.cone = cone
+
+
+class Motion:
+    """pinocchio.Motion subset: linear, angular."""
+
+    def __init__(self, linear=None, angular=None):
+        self.linear = np.zeros(3) if linear is None else np.array(linear, np.float64).reshape(3)
+        self.angular = np.zeros(3) if angular is None else np.array(angular, np.float64).reshape(3)
+
+    @staticmethod
+    def Zero():
+        return Motion()
+
+    @property
+    def vector(self):
+        return np.concatenate([self.linear, self.angular])
+
+
+LOCAL = 0  # pinocchio::ReferenceFrame (the device covers LOCAL frame velocities)
+
+
+class FrameMotion:
+    """FrameMotion(id, motion, reference=LOCAL) (multibody/frames.hpp:86-116)."""
+
+    def __init__(self, id, motion, reference=LOCAL):
+        if reference != LOCAL:
+            raise NotImplementedError("crocoddyl_amd: frame velocities are covered in the LOCAL frame only")
+        self.id = int(id)
+        self.motion = motion if isinstance(motion, Motion) else Motion(np.asarray(motion)[:3], np.asarray(motion)[3:])
+        self.reference = reference
 
 
 class FramePlacement:
     def __init__(self, id, placement):
         self.id = int(id)
         self.placement = placement
+
+    # deprecated aliases the reference's bindings keep (bindings/python/crocoddyl/multibody/frames.cpp:77-86)
+    frame = property(lambda s: s.id)
+    oMf = property(lambda s: s.placement)
 
 
 class FrameTranslation:
@@ -505,13 +782,13 @@ class _Cost:
         raise NotImplementedError
 
     def pack(self):
-        """(Bm, size) record: [type, weight=0 (set by the sum), weighted, size] + payload."""
+        """(Bm, size) record: [type, weight=0 (set by the sum), activation kind, size]
+        + payload + activation parameters (w | lb, ub | lb, ub, w)."""
         parts = self._payload()
-        w = self.activation.weights
-        parts.append(np.ones((1, self.activation.nr)) if w is None else w.reshape(1, -1))
+        parts.append(self.activation.params())
         Bm = max(p.shape[0] for p in parts)
         size = COST_HDR + sum(p.shape[1] for p in parts)
-        hdr = np.array([[self.type, 0.0, 0.0 if w is None else 1.0, size]])
+        hdr = np.array([[self.type, 0.0, float(self.activation.kind), size]])
         return np.concatenate([np.broadcast_to(p, (Bm, p.shape[1])) for p in [hdr] + parts], axis=1)
 
 
@@ -524,7 +801,7 @@ def _cost_args(args, kw):
     """Sort the reference's overloads: (activation?, reference?, nu?)."""
     act = ref = nu = None
     for a in args:
-        if isinstance(a, (ActivationModelQuad, ActivationModelWeightedQuad)):
+        if isinstance(a, _ACTIVATIONS):
             act = a
         elif isinstance(a, (int, np.integer)) and not isinstance(a, bool):
             nu = int(a)
@@ -659,7 +936,7 @@ class CostModelContactForce(_Cost):
         fref = None
         ints = []
         for a in args:
-            if isinstance(a, (ActivationModelQuad, ActivationModelWeightedQuad)):
+            if isinstance(a, _ACTIVATIONS):
                 act = a
             elif isinstance(a, FrameForce):
                 fref = a
@@ -688,9 +965,86 @@ class CostModelContactForce(_Cost):
         return [np.concatenate([[-1.0, self.activation.nr], self.fref.force]).reshape(1, -1)]
 
 
+class CostModelContactFrictionCone(_Cost):
+    """r = A lambda_lin (contact-friction-cone.hxx:51-91): the cone matrix times the
+    linear part of the force of the contact on frame fref.id, in the contact frame.
+    Overloads (state, activation, fref[, nu]) and (state, fref[, nu]) with
+    ActivationModelQuad(nf + 1) by default; the activation must have nf + 1 rows.
+    Its derivatives are A d lambda_lin / dx (du), which the DAM computes only with
+    enable_force=True (zero otherwise, as in the reference)."""
+
+    type = COST_FRICTION_CONE
+
+    def __init__(self, state, *args, **kw):
+        act = fref = nu = None
+        for a in args:
+            if isinstance(a, _ACTIVATIONS):
+                act = a
+            elif isinstance(a, FrameFrictionCone):
+                fref = a
+            elif isinstance(a, (int, np.integer)) and not isinstance(a, bool):
+                nu = int(a)
+        act = kw.get("activation", act)
+        fref = kw.get("fref", fref)
+        nu = kw.get("nu", nu)
+        if not isinstance(fref, FrameFrictionCone):
+            raise TypeError("CostModelContactFrictionCone needs a FrameFrictionCone reference")
+        nr = fref.cone.nf + 1
+        if act is not None and act.nr != nr:
+            raise ValueError(f"Invalid argument: nr is equals to {nr}")
+        super().__init__(state, act, nr, nu)
+        self.fref = fref
+
+    @property
+    def frame_id(self):
+        return self.fref.id
+
+    def _payload(self):  # [row0 (resolved by the DAM), contact rows, nr, A (nr x 3, row-major)]
+        A = self.fref.cone.A
+        return [np.concatenate([[-1.0, 0.0, A.shape[0]], A.reshape(-1)]).reshape(1, -1)]
+
+
+class CostModelFrameVelocity(_Cost):
+    """r = v_f - vref (frame-velocity.hxx:53-84): the LOCAL spatial velocity of frame
+    vref.id (pinocchio::getFrameVelocity) minus the reference motion; Rx =
+    getFrameVelocityDerivatives (dv/dq, dv/dv), Ru = 0."""
+
+    type = COST_FRAME_VELOCITY
+
+    def __init__(self, state, *args, **kw):
+        act, ref, nu = _cost_args(args, kw)
+        ref = kw.get("vref", ref)
+        if not isinstance(ref, FrameMotion):
+            raise TypeError("CostModelFrameVelocity needs a FrameMotion reference")
+        super().__init__(state, act, 6, nu)
+        self.vref = ref
+
+    def _payload(self):
+        model = self.state.pinocchio
+        name, pj, pl = model.frames[self.vref.id]
+        if pj == 0:
+            raise ValueError("Invalid argument: frames attached to the universe are not supported")
+        frame = np.concatenate([[pj - 1], pl.rotation.T.reshape(-1), pl.translation]).reshape(1, -1)
+        return [frame, self.vref.motion.vector.reshape(1, -1)]
+
+
 class CostItem:
-    def __init__(self, name, cost, weight, active=True):
-        self.name, self.cost, self.weight, self.active = name, cost, float(weight), bool(active)
+    """CostItem (cost-sum.hpp): name, cost, weight, active; changing the weight
+    marks the owning CostModelSum as modified (its blocks are re-packed)."""
+
+    def __init__(self, name, cost, weight, active=True, owner=None):
+        self.name, self.cost, self._weight, self.active = name, cost, float(weight), bool(active)
+        self._owner = owner
+
+    @property
+    def weight(self):
+        return self._weight
+
+    @weight.setter
+    def weight(self, w):
+        self._weight = float(w)
+        if self._owner is not None:
+            self._owner._version += 1
 
 
 class CostModelSum:
@@ -709,7 +1063,7 @@ class CostModelSum:
                              f"(it should be {self.nu})")
         if name in self.costs:
             raise ValueError(f"Invalid argument: {name} cost item already existed")
-        self.costs[name] = CostItem(name, cost, weight, active)
+        self.costs[name] = CostItem(name, cost, weight, active, self)
         self._version += 1
 
     def removeCost(self, name):
@@ -789,6 +1143,13 @@ class DifferentialActionModelFreeFwdDynamics:
     def version(self):
         return (self.state.pinocchio._version, self.costs._version, self._arm_version,
                 tuple(getattr(c.cost, "_version", 0) for c in self.costs.costs.values()))
+
+    def quasiStatic(self, x, maxiter=100, tol=1e-9):
+        """u holding x = (q, 0) still (free-fwddyn.hxx:137-160): pinv(dtau/du) g(q),
+        i.e. g(q) on the actuated dofs. Host-side setup (warm starts), not the device path."""
+        x = np.asarray(x, float)
+        g = self.state.pinocchio.computeGeneralizedGravity(x[:self.state.nq])
+        return g[self.state.nv - self.nu:].copy()
 
     def pack_body(self, dt):
         """(Bm, size) rows of the FDDP_KNOT_EULER_FREEFWD block for step dt (with a
@@ -968,6 +1329,20 @@ class DifferentialActionModelContactFwdDynamics(DifferentialActionModelFreeFwdDy
                                     tuple(c.contact.gains.tobytes() for c in self.contacts.contacts.values()))
 
     knot_kind = _abi.KNOT_EULER_CONTACTFWD
+
+    def quasiStatic(self, x, maxiter=100, tol=1e-9):
+        """u = (pinv([dtau/du | Jc^T]) g(q))[:nu] (contact-fwddyn.hxx:169-207): the
+        controls (with the contact forces) that hold x = (q, 0) still. Host-side setup."""
+        x = np.asarray(x, float)
+        model, nv, nu = self.state.pinocchio, self.state.nv, self.nu
+        q = x[:self.state.nq]
+        g = model.computeGeneralizedGravity(q)
+        cols = [np.vstack([np.zeros((nv - nu, nu)), np.eye(nu)])]
+        for n in self.contacts.active:
+            c = self.contacts.contacts[n].contact
+            J = model.getFrameJacobian(q, c._ref.id)
+            cols.append((J[:3] if c.nc == 3 else J).T)
+        return (np.linalg.pinv(np.hstack(cols)) @ g)[:nu]
 
     def pack_body(self, dt):
         """(Bm, size) rows of the FDDP_KNOT_EULER_CONTACTFWD block: the
@@ -1161,6 +1536,9 @@ class ActionModelImpulseFwdDynamics(_impulse_model_base()):
 
     def pack(self):
         recs = self.impulses.pack()
+        if any(it.active and it.cost.type in (COST_FRAME_VELOCITY, COST_CONTACT_FORCE, COST_FRICTION_CONE)
+               for it in self.costs.costs.values()):
+            raise NotImplementedError("crocoddyl_amd: frame-velocity / force costs on impulse knots are not covered")
         if self.impulses.ni > MAX_CONTACT_ROWS:
             raise ValueError(f"Invalid argument: the device path holds at most {MAX_CONTACT_ROWS} impulse rows")
         sec = np.concatenate([[self.r_coeff, self.JMinvJt_damping, len(recs), 1.0]] + recs)

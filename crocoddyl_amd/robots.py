@@ -101,6 +101,8 @@ def sample_solo12():
             ("_KFE", _Y, (0.0, 0.03745 * sy, -0.16), 0.033, (0.0, 0.007 * sy, -0.078), (0.0001, 0.0001, 0.000003)),
         ], leg)
         m.addFrame(f"{leg}_FOOT", ids[-1], SE3(np.eye(3), (0.0, 0.008 * sy, -0.16)))
+        for j, (lo, hi) in zip(ids, ((-0.9, 0.9), (-1.9, 1.9), (-3.0, 3.0))):  # URDF-style limits, 20 rad/s
+            m.setJointLimits(j, lo, hi, 20.0)
     front, hind = [0.0, 0.8, -1.6], [0.0, -0.8, 1.6]
     q = np.concatenate([[0.0, 0.0, 0.235, 0.0, 0.0, 0.0, 1.0], front, front, hind, hind])
     assert q.size == m.nq == 19 and m.nv == 18

@@ -1,12 +1,17 @@
 """Seeded synthetic problems for the BASELINE.json configs.
 
-There is no robot data here (no URDFs, no Pinocchio), so C3-C5 use
-Euler(dt) ∘ DifferentialActionModelLQR knots with the exact (n, m, T, B) of
-the named robots: the solver core sees the same shapes and arithmetic
-intensity; multibody model cost is not represented (SURVEY §8d caveat).
+The robot configs run on real multibody knots over code-built robots
+(crocoddyl_amd.robots: URDFs and Pinocchio are absent offline):
+  C3_arm_multibody / C3_arm_contact   the 7-DoF Talos-class arm (free / contact dynamics)
+  C4_solo12_trot                      Solo12 trotting gait (utils/quadruped.py), T = 60
+  C5_talos_walk                       Talos walking gait (utils/biped.py), T = 100
+The gait configs give every batch element its own x0 (the reference posture
+perturbed on the manifold) over one shared knot sequence.
 
-Every batch element gets its own seeded perturbation of the model matrices
-(shared over t), so every (b, t) derivative block is distinct data.
+C3_talos_arm / C4_solo12 / C5_talos_full are the Euler(dt) ∘
+DifferentialActionModelLQR stand-ins with the robots' (n, m, T, B): the solver core
+alone at those shapes; every batch element gets its own seeded perturbation of the
+model matrices (shared over t), so every (b, t) derivative block is distinct data.
 """
 import numpy as np
 
@@ -25,7 +30,58 @@ CONFIGS = {
     # the same arm on contact dynamics: Euler ∘ ContactFwdDynamics, gripper 6D
     # contact, floating-base actuation (nu = 6), build_arm_contact
     "C3_arm_contact": ("multibody_contact", 7, 6, 250, 512, 1e-3),
+    # legged robots on their gaits (contact dynamics, free-flyer root): nq, nu
+    "C4_solo12_trot": ("gait_quadruped", 19, 12, 60, 1024, 1e-2),
+    "C5_talos_walk": ("gait_biped", 39, 32, 100, 1024, 0.0375),
 }
+
+
+def gait_models(name, T=None):
+    """(gait builder, running models, terminal model) of a gait config. The knot
+    counts are the reference benchmark's gait parameters stretched to the config's
+    T: Talos walking (benchmark/bipedal_walk_optctrl.py:82-90: step 0.6 m / 0.1 m,
+    dt 0.0375, 1 support knot) with 48 step knots -> T = 100; Solo12 trotting
+    (benchmark/quadrupedal_gaits_optctrl.py:134-142: step 0.15 m / 0.1 m, dt 1e-2,
+    2 support knots) with 27 step knots -> T = 60. A smaller T shortens the steps
+    (for parity tests)."""
+    from . import gaits, robots
+    kind, _, _, T0, _, dt = CONFIGS[name]
+    T = T0 if T is None else T
+    if kind == "gait_biped":
+        g = gaits.SimpleBipedGaitProblem(robots.sample_talos(), "right_sole_link", "left_sole_link")
+        sk = max(1, T // 2 - 2)
+        models = g.createWalkingModels(g.rmodel.defaultState, 0.6, 0.1, dt, sk, 1)
+    else:
+        g = gaits.SimpleQuadrupedalGaitProblem(robots.sample_solo12(), "FL_FOOT", "FR_FOOT", "HL_FOOT", "HR_FOOT")
+        sk = max(1, T // 2 - 3)
+        models = g.createTrottingModels(g.rmodel.defaultState, 0.15, 0.1, dt, sk, 2)
+    models = models[:T]
+    return g, models, models[-1]
+
+
+def build_gait(name, T=None, B=None, seed=None, spread=0.02, v_spread=0.1):
+    """(x0s, running, terminal) of a gait config: x0_b = the reference posture
+    integrated along a seeded tangent perturbation (q +- spread, v +- v_spread)."""
+    _, _, _, T0, B0, _ = CONFIGS[name]
+    B = B0 if B is None else B
+    g, running, terminal = gait_models(name, T)
+    rng = np.random.default_rng(seed_of(name) + 1 if seed is None else seed)
+    x0 = g.rmodel.defaultState
+    nv = g.state.nv
+    x0s = np.stack([g.state.integrate(x0, np.concatenate([rng.uniform(-spread, spread, nv),
+                                                          rng.uniform(-v_spread, v_spread, nv)]))
+                    for _ in range(B)])
+    if B:
+        x0s[0] = x0
+    return x0s, running, terminal
+
+
+def gait_warm_start(name, running, x0):
+    """The reference benchmark's warm start (bipedal_walk_optctrl.py:29-32): xs =
+    the default state at every knot, us = each knot's quasiStatic controls."""
+    xs = [x0] * (len(running) + 1)
+    us = [m.quasiStatic(None, x0) if m.nu else np.zeros(0) for m in running]
+    return xs, us
 
 
 def seed_of(name):
@@ -80,6 +136,8 @@ def build(name, T=None, B=None, seed=None, drift_free=True):
     B = B0 if B is None else B
     if kind == "multibody":
         return build_arm(T=T, B=B, seed=seed)
+    if kind in ("gait_biped", "gait_quadruped"):
+        return build_gait(name, T=T, B=B, seed=seed)
     if kind == "multibody_contact":
         return build_arm_contact(T=T, B=B, seed=seed_of(name) + 1 if seed is None else seed, dt=dt, contact="6d",
                                  q_nominal=ARM_BENT, spread=0.3)
@@ -301,7 +359,8 @@ def random_floating_state(model, rng, B, spread=0.3, v_spread=0.5):
 
 
 def build_floating(T=4, B=2, seed=0, robot=None, dt=1e-2, contacts=(), gains=(2.0, 1.5), damping=0.0,
-                   weighted=False, com=False, force_costs=False, enable_force=None, armature=None, spread=0.3):
+                   weighted=False, com=False, force_costs=False, enable_force=None, armature=None, spread=0.3,
+                   friction=False, fvel=False, barrier=False):
     """Floating-base knots (the reference's legged-robot models, on a tree below a
     free-flyer root): Euler(dt) ∘ DifferentialAction{Free,Contact}FwdDynamics with
     ActuationModelFloatingBase (nu = nv - 6). ``contacts``: ("6d" | "3d", frame
@@ -309,7 +368,11 @@ def build_floating(T=4, B=2, seed=0, robot=None, dt=1e-2, contacts=(), gains=(2.
     non-neutral reference state, weighted with ``weighted``), uReg, a tip
     FramePlacement (+ a FrameTranslation when ``weighted``), CoMPosition with
     ``com``, a CostModelContactForce per contact with ``force_costs``. The
-    terminal model is the same DAM with dt = 0."""
+    terminal model is the same DAM with dt = 0. ``friction``: a
+    CostModelContactFrictionCone per contact (QuadraticBarrier on the cone bounds, a
+    tilted surface normal); ``fvel``: a CostModelFrameVelocity on the tip;
+    ``barrier``: a WeightedQuadraticBarrier state-bounds cost and a QuadraticBarrier
+    control-bounds cost (finite bounds the random states cross)."""
     from . import multibody as mb
     rng = np.random.default_rng(seed)
     model = mb.sample_tree(5, seed=3, freeflyer=True) if robot is None else robot
@@ -333,6 +396,16 @@ def build_floating(T=4, B=2, seed=0, robot=None, dt=1e-2, contacts=(), gains=(2.
         tip, mb.SE3(mb._rot_axis(np.array([0.0, 0.6, 0.8]), 0.4), (0.2, -0.1, 0.3))), nu), 0.5)
     if com:
         costs.addCost("comTrack", mb.CostModelCoMPosition(state, (0.05, -0.02, 0.1), nu), 2.0)
+    if fvel:
+        costs.addCost("tipVel", mb.CostModelFrameVelocity(state, mb.FrameMotion(
+            tip, mb.Motion((0.1, -0.2, 0.05), (0.3, 0.0, -0.1))), nu), 0.2)
+    if barrier:
+        nd = state.ndx
+        bounds = mb.ActivationBounds(np.full(nd, -0.2), np.full(nd, 0.25), 0.9)
+        costs.addCost("xBounds", mb.CostModelState(state, mb.ActivationModelWeightedQuadraticBarrier(
+            bounds, np.linspace(1.0, 3.0, nd)), state.zero(), nu), 5.0)
+        costs.addCost("uBounds", mb.CostModelControl(state, mb.ActivationModelQuadraticBarrier(
+            mb.ActivationBounds(np.full(nu, -0.5), np.full(nu, 0.5))), nu), 3.0)
     if contacts:
         cm = mb.ContactModelMultiple(state, nu)
         for i, (kind, fname) in enumerate(contacts):
@@ -346,8 +419,13 @@ def build_floating(T=4, B=2, seed=0, robot=None, dt=1e-2, contacts=(), gains=(2.
                 nr = 6 if kind == "6d" else 3
                 costs.addCost(f"force{i}", mb.CostModelContactForce(
                     state, mb.FrameForce(fid, rng.uniform(-1, 1, 6)), nr, nu), 1e-3)
-        dam = mb.DifferentialActionModelContactFwdDynamics(state, act, cm, costs, damping,
-                                                           force_costs if enable_force is None else enable_force)
+            if friction:
+                cone = mb.FrictionCone(np.array([0.1, -0.2, 1.0]), 0.7, 4, False, 0.5)
+                costs.addCost(f"cone{i}", mb.CostModelContactFrictionCone(
+                    state, mb.ActivationModelQuadraticBarrier(mb.ActivationBounds(cone.lb, cone.ub)),
+                    mb.FrameFrictionCone(fid, cone), nu), 0.1)
+        ef = (force_costs or friction) if enable_force is None else enable_force
+        dam = mb.DifferentialActionModelContactFwdDynamics(state, act, cm, costs, damping, ef)
     else:
         dam = mb.DifferentialActionModelFreeFwdDynamics(state, act, costs)
     if armature is not None:

@@ -16,7 +16,12 @@ and bindings/python/crocoddyl/utils/{quadruped,biped}.py (C4 / C5 gaits):
        CostModelFramePlacement        multibody/costs/frame-placement.hxx:45-80
        CostModelFrameTranslation      multibody/costs/frame-translation.hxx:50-81
        CostModelContactForce          multibody/costs/contact-force.hxx:33-74
-     activations Quad / WeightedQuad  core/activations/{quadratic,weighted-quadratic}.hpp
+       CostModelContactFrictionCone   multibody/costs/contact-friction-cone.hxx:51-91
+       CostModelCoMPosition           multibody/costs/com-position.hxx:49-75
+       CostModelFrameVelocity         multibody/costs/frame-velocity.hxx:53-84
+     activations Quad / WeightedQuad / QuadraticBarrier / WeightedQuadraticBarrier
+                                      core/activations/{quadratic,weighted-quadratic,
+                                      quadratic-barrier,weighted-quadratic-barrier}.hpp
   StateMultibody                      multibody/states/multibody.hxx:54-240
 
 over a kinematic tree whose root joint is either fixed (a revolute joint on the
@@ -60,7 +65,8 @@ STATE, CONTROL, FRAME_PLACEMENT, FRAME_TRANSLATION = 1, 2, 3, 4
 CONTACT_3D, CONTACT_6D = 5, 6  # contact records (FDDP_KNOT_EULER_CONTACTFWD)
 CONTACT_FORCE = 7  # CostModelContactForce: r = lambda[row0:row0+nr] - fref (contact-force.hxx:33-50)
 COM_POSITION = 8  # CostModelCoMPosition: r = com(q) - cref (com-position.hxx:49-75)
-FRICTION_CONE = 9  # CostModelContactFrictionCone: r = A lambda_lin (contact-friction-cone.hxx:64-90)
+FRICTION_CONE = 9  # CostModelContactFrictionCone: r = A lambda_lin (contact-friction-cone.hxx:51-91)
+FRAME_VELOCITY = 10  # CostModelFrameVelocity: r = v_frame (LOCAL) - vref (frame-velocity.hxx:53-84)
 H_CS = 1e-30  # complex-step size
 
 
@@ -450,36 +456,74 @@ class Cost:
     def __init__(self, rec, nx, ndx, nu):
         self.type = int(rec[0])
         self.weight = float(rec[1])
-        weighted = rec[2] != 0
+        self.act = int(rec[2])  # 0 Quad, 1 WeightedQuad, 2 QuadraticBarrier, 3 WeightedQuadraticBarrier
         d = rec[COST_HDR:]
         self.size = int(rec[3])
         if self.type == STATE:
-            self.xref, w, nr = d[:nx], d[nx:nx + ndx], ndx
+            self.xref, o, nr = d[:nx], nx, ndx
         elif self.type == CONTROL:
-            self.uref, w, nr = d[:nu], d[nu:2 * nu], nu
-        elif self.type in (FRAME_PLACEMENT, FRAME_TRANSLATION):
+            self.uref, o, nr = d[:nu], nu, nu
+        elif self.type in (FRAME_PLACEMENT, FRAME_TRANSLATION, FRAME_VELOCITY):
             self.joint = int(d[0])
             self.Rf = d[1:10].reshape(3, 3).T
             self.pf = d[10:13]
             if self.type == FRAME_PLACEMENT:
                 self.Rri = d[13:22].reshape(3, 3).T  # Mref^-1
                 self.pri = d[22:25]
-                w, nr = d[25:31], 6
+                o, nr = 25, 6
+            elif self.type == FRAME_VELOCITY:
+                self.vref = d[13:19]
+                o, nr = 19, 6
             else:
                 self.pref = d[13:16]
-                w, nr = d[16:19], 3
+                o, nr = 16, 3
         elif self.type == COM_POSITION:
             self.cref = d[0:3]
-            w, nr = d[3:6], 3
+            o, nr = 3, 3
         elif self.type == CONTACT_FORCE:
             self.row0, nr = int(d[0]), int(d[1])
             self.fref = d[2:2 + nr]
-            w = d[8:8 + nr]
+            o = 8
             self.force_fn = None  # set by ContactFwdKnot: (x, u) -> lambda
             self.zero_jac = False  # reference: Rx = Ru = 0 unless enable_force
+        elif self.type == FRICTION_CONE:
+            self.row0, nr = int(d[0]), int(d[2])
+            self.A = d[3:3 + 3 * nr].reshape(nr, 3)
+            o = 3 + 3 * nr
+            self.force_fn = None
+            self.zero_jac = False
         else:
             raise ValueError(f"unknown cost type {self.type}")
-        self.w = np.asarray(w, float) if weighted else np.ones(nr)
+        self.nr = nr
+        prm = np.asarray(d[o:], float)
+        if self.act in (0, 1):
+            self.w = prm[:nr] if self.act == 1 else np.ones(nr)
+        elif self.act in (2, 3):
+            self.lb, self.ub = prm[:nr], prm[nr:2 * nr]
+            self.w = prm[2 * nr:3 * nr] if self.act == 3 else None
+        else:
+            raise ValueError(f"unknown activation kind {self.act}")
+
+    # activations (core/activations/*.hpp): value, Ar, diag(Arr) of a real residual
+    def a_value(self, r):
+        if self.act in (0, 1):
+            return 0.5 * np.sum(self.w * r * r)
+        rl, ru = np.minimum(r - self.lb, 0.0), np.maximum(r - self.ub, 0.0)
+        if self.act == 3:  # weighted-quadratic-barrier.hpp:42-46: w scales before squaring
+            rl, ru = self.w * rl, self.w * ru
+        return 0.5 * np.sum(rl * rl) + 0.5 * np.sum(ru * ru)
+
+    def a_grad(self, r):
+        if self.act in (0, 1):
+            return self.w * r
+        g = np.minimum(r - self.lb, 0.0) + np.maximum(r - self.ub, 0.0)
+        return self.w * self.w * g if self.act == 3 else g
+
+    def a_hess(self, r):
+        if self.act in (0, 1):
+            return self.w
+        h = np.where(r - self.lb <= 0.0, 1.0, np.where(r - self.ub >= 0.0, 1.0, 0.0))
+        return self.w * h if self.act == 3 else h
 
     def residual(self, robot, x, u, oM=None):
         nq = robot.nq
@@ -491,8 +535,15 @@ class Cost:
             if self.row0 < 0:
                 return -self.fref + 0 * x[0]
             return self.force_fn(x, u)[self.row0:self.row0 + len(self.fref)] - self.fref
+        if self.type == FRICTION_CONE:  # r = A lambda_lin (contact-friction-cone.hxx:58)
+            if self.row0 < 0:
+                return np.zeros(self.nr) + 0 * x[0]
+            return self.A @ self.force_fn(x, u)[self.row0:self.row0 + 3]
         if self.type == COM_POSITION:
             return robot.center_of_mass(x[:nq]) - self.cref
+        if self.type == FRAME_VELOCITY:  # LOCAL frame velocity - vref (frame-velocity.hxx:57-59)
+            vs, _ = local_motions(robot, x[:nq], x[nq:], np.zeros(robot.nv))
+            return motion_X(self.Rf, self.pf) @ vs[self.joint] - self.vref
         if oM is None:
             oM = robot.placements(x[:nq])
         R0, p0 = oM[self.joint]
@@ -556,7 +607,7 @@ class FreeFwdKnot:
         c = 0.0
         for k in self.costs:
             r = k.residual(self.robot, x, u, oM)
-            c = c + k.weight * (0.5 * np.sum(k.w * r * r))
+            c = c + k.weight * k.a_value(r)
         return c
 
     def calc(self, x, u=None):
@@ -581,6 +632,8 @@ class FreeFwdKnot:
         for k in self.costs:
             if k.type == CONTACT_FORCE:
                 res.append(lam[k.row0:k.row0 + len(k.fref)] - k.fref if k.row0 >= 0 else 0 * lam[:0].sum() - k.fref)
+            elif k.type == FRICTION_CONE:
+                res.append(k.A @ lam[k.row0:k.row0 + 3] if k.row0 >= 0 else np.zeros(k.nr) + 0 * lam[:0].sum())
             else:
                 res.append(k.residual(self.robot, x, u, oM))
         if dt != 0:
@@ -623,8 +676,8 @@ class FreeFwdKnot:
         for k, r, R in zip(self.costs, r0, Rz):
             if getattr(k, "zero_jac", False):
                 R = np.zeros_like(R)
-            Lz += k.weight * R.T @ (k.w * r)
-            Lzz += k.weight * R.T @ (k.w[:, None] * R)
+            Lz += k.weight * R.T @ k.a_grad(r)
+            Lzz += k.weight * R.T @ (k.a_hess(r)[:, None] * R)
         s = dt if dt != 0 else 1.0
         return dict(Fx=Fx, Fu=Fu, Lx=s * Lz[:n], Lu=s * Lz[n:], Lxx=s * Lzz[:n, :n], Lxu=s * Lzz[:n, n:],
                     Luu=s * Lzz[n:, n:])
@@ -739,7 +792,7 @@ class ContactFwdKnot(FreeFwdKnot):
         self.kind = 5
         self.nc = sum(c.nc for c in self.contacts)
         for c in self.costs:
-            if c.type == CONTACT_FORCE:
+            if c.type in (CONTACT_FORCE, FRICTION_CONE):
                 c.force_fn = lambda xx, uu: self.accel_force(xx, uu)[1]
                 c.zero_jac = not self.enable_force
 
@@ -895,8 +948,8 @@ class ImpulseFwdKnot(FreeFwdKnot):
         for k in self.costs:
             r = k.residual(rob, x, u0)
             Rx = _cs_jac(lambda dz: k.residual(rob, self.state_integrate(x, dz), u0), n, r.size)
-            Lx += k.weight * Rx.T @ (k.w * r)
-            Lxx += k.weight * Rx.T @ (k.w[:, None] * Rx)
+            Lx += k.weight * Rx.T @ k.a_grad(r)
+            Lxx += k.weight * Rx.T @ (k.a_hess(r)[:, None] * Rx)
         return dict(Fx=Fx, Fu=np.zeros((n, 0)), Lx=Lx, Lu=np.zeros(0), Lxx=Lxx, Lxu=np.zeros((n, 0)),
                     Luu=np.zeros((0, 0)))
 

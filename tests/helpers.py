@@ -14,8 +14,9 @@ def setup(name, T=None, B=None, seed=None, drift_free=True):
     B = x0s.shape[0]
     knots, pool = pack_problem(running, terminal, B)
     nx = running[0].state.nx
+    ndx = getattr(running[0].state, "ndx", nx)
     nu_max = max(m.nu for m in running)
-    dims = _abi.Dims(nx, nx, nu_max, len(running), B)
+    dims = _abi.Dims(nx, ndx, nu_max, len(running), B)
     return dict(dims=dims, knots=knots, pool=pool, x0s=x0s, running=running, terminal=terminal)
 
 

@@ -101,7 +101,12 @@ FF_CASES = [dict(), dict(weighted=True, com=True),
             dict(contacts=[("6d", "tip")], force_costs=True), dict(contacts=[("3d", "mid_site")], force_costs=True,
                                                                      weighted=True),
             dict(robot=mb.sample_tree(8, seed=9, freeflyer=True), contacts=[("6d", "tip")], com=True,
-                 armature=np.concatenate([np.zeros(6), np.full(8, 0.02)]))]
+                 armature=np.concatenate([np.zeros(6), np.full(8, 0.02)])),
+            # friction cones (QuadraticBarrier on the cone), frame velocity, barrier activations
+            dict(contacts=[("6d", "tip"), ("3d", "mid_site")], friction=True),
+            dict(contacts=[("3d", "mid_site")], friction=True, fvel=True, barrier=True, com=True),
+            dict(fvel=True, barrier=True),
+            dict(contacts=[("6d", "tip")], friction=True, enable_force=False, fvel=True)]
 
 
 def _fd_check(k, x, u, ref, nu):
