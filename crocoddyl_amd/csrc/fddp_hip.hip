@@ -74,7 +74,8 @@ int64_t block_doubles(int kind, int nx, int nu) {
 // pool. Returns its size in doubles, or -1 with `why` set. nj / njac / nc:
 // dofs, jac costs and contact rows (LDS sizing).
 int64_t mb_block_check(const double* P, int64_t avail, int kind, int nx, int nu, std::string& why, int* nj_out,
-                       int* njac_out, int* nc_out, bool* vcols_out = nullptr) {
+                       int* njac_out, int* nc_out, bool* vcols_out = nullptr, int* nu_out = nullptr,
+                       int* nrows_out = nullptr) {
   using namespace fddp::mb;
   if (avail < FDDP_PARAM_HEADER) return why = "block out of range", -1;
   const double dt = P[0];
@@ -218,12 +219,16 @@ int64_t mb_block_check(const double* P, int64_t avail, int kind, int nx, int nu,
   }
   if (o != size) return why = "block size does not match its records", -1;
   if (njac > kMaxJacCosts) return why = "more than 8 frame / CoM / frame-velocity / free-flyer state costs in one knot", -1;
-  if ((pad2(diff_layout(nj, njac, nc, vcols).total) + pad2(size)) * 8 > 160 * 1024)
+  const int nrows = count_cost_rows(parse(P), nu);
+  if (nrows > kMaxCostRows) return why = "more than 64 cost residual rows with dense Jacobians in one knot", -1;
+  if ((pad2(diff_layout(nj, njac, nc, vcols, nu, nrows).total) + pad2(size)) * 8 > 160 * 1024)
     return why = "too many dofs for the calcDiff LDS plan", -1;
   if (nj_out) *nj_out = std::max(*nj_out, nj);
   if (njac_out) *njac_out = std::max(*njac_out, njac);
   if (nc_out) *nc_out = std::max(*nc_out, nc);
   if (vcols_out) *vcols_out = *vcols_out || vcols;
+  if (nu_out) *nu_out = std::max(*nu_out, nu);
+  if (nrows_out) *nrows_out = std::max(*nrows_out, nrows);
   return size;
 }
 
@@ -634,6 +639,7 @@ int apply_knots(fddp_handle* h, const fddp_knot_desc* knots, const double* param
     int64_t pmax = 0;
     int mb_nj = 0, mb_njac = 0, mb_nc = 0;
     bool mb_vcols = false;
+    int mb_nu = 0, mb_nrows = 0;
     h->has_mb = false;
     for (int t = 0; t <= d.T; ++t) {
       int64_t sz;
@@ -645,7 +651,7 @@ int apply_knots(fddp_handle* h, const fddp_knot_desc* knots, const double* param
           const int64_t off = knots[t].param_offset + (int64_t)b * knots[t].param_stride;
           std::string why;
           sz = std::max(sz, mb_block_check(params + off, n_params - off, knots[t].kind, d.nx, knots[t].nu, why, &mb_nj,
-                                           &mb_njac, &mb_nc, &mb_vcols));
+                                           &mb_njac, &mb_nc, &mb_vcols, &mb_nu, &mb_nrows));
         }
       } else {
         sz = block_doubles(knots[t].kind, d.nx, knots[t].nu);
@@ -662,10 +668,13 @@ int apply_knots(fddp_handle* h, const fddp_knot_desc* knots, const double* param
         for (int b = 0; b < nb; ++b)
           mb_pmax = std::max<int64_t>(mb_pmax, (int64_t)params[knots[t].param_offset + (int64_t)b * knots[t].param_stride + 3]);
       }
-    D.mbd = h->has_mb ? pad2(fddp::mb::diff_layout(mb_nj, mb_njac, mb_nc, mb_vcols).total) : 0;
+    D.mbd = h->has_mb ? pad2(fddp::mb::diff_layout(mb_nj, mb_njac, mb_nc, mb_vcols, mb_nu, mb_nrows).total) : 0;
     h->mb_diff_smem = h->has_mb ? sizeof(double) * (D.mbd + pad2(mb_pmax)) : 0;
     const int64_t budget = (150 * 1024) / 8 - (2 * D.sX + D.sM + 2 * D.sN + 5 * (kNT / kWave) + 16) - D.mbw;
     h->pcap = pmax <= budget ? pad2(pmax) : 0;
+    // the multibody calc reads its parameter block from LDS only (knots.hpp)
+    if (h->has_mb && h->pcap < pad2(mb_pmax))
+      return fail(FDDP_ERR_INVALID_ARG, "multibody parameter blocks exceed the LDS budget of the calc / rollout kernels");
   }
   h->fwd_smem = sizeof(double) * (h->pcap + fwd_lds_doubles<kNT, false>(D.sX, D.sN, D.sM) + D.mbw);
   h->calc_smem = sizeof(double) * (h->pcap + 2 * D.sX + D.sM + 5 * (kNT / kWave) + 16 + D.mbw);

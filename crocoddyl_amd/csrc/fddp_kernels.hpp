@@ -789,24 +789,26 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2))) void fo
       return fwd_trial<NT>(D, b, s, alpha, xv, uv, xn, red, flag, ct, dv, pl, pcap, cached, (double*)flag + 2 + 2 * D.sN,
                            (double*)flag + 2);
   };
-  if (mode == 1) {
-    double ct, dv;
-    const bool ok = trial(alpha1, ct, dv);
-    if (threadIdx.x == 0) {
-      st->fwd_fail = ok ? 0 : 1;
-      st->cost_try = ct;
-      st->dV = s.cost - ct;
-      st->dv = ok ? dv : 0.;
-    }
-    return;
-  }
-  // line search (fddp.cpp:53-81)
+  // line search (fddp.cpp:53-81); mode 1 (tryStep): one trial at alpha1. One call
+  // site of the trial, so it is inlined (its LDS pointers keep their address space).
   bool accepted = false;
-  for (int a = 0; a < prm.n_alphas; ++a) {
-    const double alpha = prm.alphas[a];
-    s.steplength = alpha;
+  const int na = mode == 1 ? 1 : prm.n_alphas;
+  for (int a = 0; a < na; ++a) {
+    const double alpha = mode == 1 ? alpha1 : prm.alphas[a];
     double ct, dv;
-    if (!trial(alpha, ct, dv)) continue;
+    bool ok;
+    [[clang::always_inline]] ok = trial(alpha, ct, dv);
+    if (mode == 1) {
+      if (threadIdx.x == 0) {
+        st->fwd_fail = ok ? 0 : 1;
+        st->cost_try = ct;
+        st->dV = s.cost - ct;
+        st->dv = ok ? dv : 0.;
+      }
+      return;
+    }
+    s.steplength = alpha;
+    if (!ok) continue;
     s.cost_try = ct;
     s.dV = s.cost - ct;
     s.dv = dv;

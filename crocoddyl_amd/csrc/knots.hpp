@@ -98,7 +98,10 @@ __device__ __forceinline__ double knot_calc(const fddp_knot_desc& kd, const doub
                             bool use_u, double* xnext, double* red, double* mbw) {
   const int nu = kd.nu;
   use_u = use_u && nu > 0;
-  if (is_mb_kind(kd.kind)) return mb::knot_calc<NT>(P, nx, x, u, use_u, xnext, mbw);
+  // multibody blocks are always staged in LDS (fddp_create checks the budget), as are
+  // the trial state / control / next state and the scratch of every caller
+  if (is_mb_kind(kd.kind))
+    return mb::knot_calc<NT>(lds_ptr(P), nx, lds_ptr(x), lds_ptr(u), use_u, lds_ptr(xnext), lds_ptr(mbw));
   double t[5] = {0., 0., 0., 0., 0.};
   if (kd.kind == FDDP_KNOT_LQR) {
     LQRBlk Pm(P, nx, nu);

@@ -371,17 +371,21 @@ MB_HD inline void R_to_quat(const double* R, double* q) {
 // wave 0 works in, closed by a wave-level fence instead of a workgroup barrier
 // (the other waves skip ahead to the next sync()); sync(): the barrier that
 // hands wave-0 results back to the whole workgroup.
+// Everything the device executor runs is inlined into the kernel: LDS pointers
+// keep their address space only through inlining (an outlined phase or helper
+// takes them as generic pointers and reaches LDS with flat instructions, at
+// global-memory latency).
 struct DevExec {
   int nt;
   template <class F>
-  __device__ void run(F f) const {
-    f((int)threadIdx.x);
+  __device__ __forceinline__ void run(F f) const {
+    [[clang::always_inline]] f((int)threadIdx.x);
     __syncthreads();
   }
   template <class F>
-  __device__ void run_w0(F f) const {
+  __device__ __forceinline__ void run_w0(F f) const {
     if (threadIdx.x < 64) {
-      f((int)threadIdx.x);
+      [[clang::always_inline]] f((int)threadIdx.x);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -409,15 +413,65 @@ struct HostExec {
 // lanes in a second pass of each pivot step.
 // Runs on wave 0 between wave-level fences; the caller's preceding phase must
 // have ended in a workgroup barrier.
+// Leading dimension of the nj-row matrices in LDS that are walked column per lane
+// (mass matrix / KKT blocks): odd, so a wave's 64 column reads hit distinct banks.
+MB_HD __forceinline__ int lda_of(int nj) { return nj | 1; }
+
+// Device version: every thread of the workgroup takes columns tid, tid + nt, ...
+// (one pass for nc <= nt), one workgroup barrier per pivot; plain arguments and no
+// lambdas, so nothing of it lives in scratch. The column update runs in chunks of 8
+// rows, loads first, so the LDS round trips overlap.
+__device__ __forceinline__ bool gauss_jordan_dev(double* A, int nr, int ld, int nc, int* flag) {
+  const int tid = (int)threadIdx.x, nt = (int)blockDim.x;
+  __syncthreads();
+  bool bad = false;
+#pragma unroll 1
+  for (int k = 0; k < nr; ++k) {
+    const double piv = A[(int64_t)k * ld + k];
+    bad = bad || !(piv > 0.);
+    const double* pc = A + (int64_t)k * ld;
+#pragma unroll 1
+    for (int cc = tid; cc < nc; cc += nt) {
+      if (cc <= k || bad) continue;
+      double* col = A + (int64_t)cc * ld;
+      const double akc = col[k] / piv;
+      int r0 = 0;
+#pragma unroll 1
+      for (; r0 + 8 <= nr; r0 += 8) {
+        double pv[8], cv[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          pv[r] = pc[r0 + r];
+          cv[r] = col[r0 + r];
+        }
+#pragma unroll
+        for (int r = 0; r < 8; ++r) col[r0 + r] = (r0 + r == k) ? akc : cv[r] - pv[r] * akc;
+      }
+#pragma unroll 1
+      for (; r0 < nr; ++r0) col[r0] = (r0 == k) ? akc : col[r0] - pc[r0] * akc;
+    }
+    __syncthreads();
+  }
+  if (tid == 0) *flag = bad ? 1 : 0;
+  __syncthreads();
+  return !bad;
+}
+
+// the device executor takes the all-thread version (overload resolution prefers it
+// to the template below, which serves the host emulation)
+__device__ __forceinline__ bool gauss_jordan(const DevExec&, double* A, int nr, int ld, int nc, int* flag) {
+  return gauss_jordan_dev(A, nr, ld, nc, flag);
+}
+
 template <class X>
-MB_HD __attribute__((noinline)) bool gauss_jordan(const X& ex, double* A, int nr, int nc, int* flag) {
+MB_HD __attribute__((noinline)) bool gauss_jordan(const X& ex, double* A, int nr, int ld, int nc, int* flag) {
   ex.run_w0([&](int lane) {
     if (lane == 0) *flag = 0;
   });
 #pragma unroll 1
   for (int k = 0; k < nr; ++k) {
     ex.run_w0([&](int lane) {
-      const double piv = A[(int64_t)k * nr + k];
+      const double piv = A[(int64_t)k * ld + k];
       if (!(piv > 0.)) {
         if (lane == 0) *flag = 1;
         return;
@@ -427,8 +481,8 @@ MB_HD __attribute__((noinline)) bool gauss_jordan(const X& ex, double* A, int nr
         if (cc <= k) continue;
         // pivot column and own column in chunks of 8 rows through registers
         // (independent loads, then the updates): no LDS round trip per row
-        double* col = A + (int64_t)cc * nr;
-        const double* pc = A + (int64_t)k * nr;
+        double* col = A + (int64_t)cc * ld;
+        const double* pc = A + (int64_t)k * ld;
         const double akc = col[k] / piv;
 #pragma unroll 1
         for (int r0 = 0; r0 < nr; r0 += 8) {
@@ -1077,6 +1131,20 @@ MB_HD inline int count_jac_costs(const Blk& b, bool* vel_cols = nullptr) {
 }
 // costs on the contact multipliers: CostModelContactForce, CostModelContactFrictionCone
 MB_HD __forceinline__ bool force_cost(int type) { return type == C_CONTACT_FORCE || type == C_FRICTION_CONE; }
+// Residual rows with a dense Jacobian (jac costs; force costs on an active contact
+// when the force Jacobians are computed): the rows of the stacked R of calcDiff.
+MB_HD inline int count_cost_rows(const Blk& b, int nu) {
+  int n = 0;
+  const bool fd = b.enable_force && b.nc > 0 && !b.impulse;
+  const double* cr = b.C;
+  for (int k = 0; k < b.ncost; ++k) {
+    const CRec C{cr};
+    if (jac_cost(b, C.type())) n += jac_rows(C.type());
+    if (fd && force_cost(C.type()) && (int)C.d()[0] >= 0) n += cost_nr(b, C, nu);
+    cr += C.size();
+  }
+  return n;
+}
 // row i of a force cost's residual from the multipliers lam of the contact rows
 // [row0, row0 + nc) (lam unread for an inactive contact: lambda = 0):
 //   contact force: lambda_i - fref_i (contact-force.hxx:33-50: jMf.actInv(f) is the multiplier);
@@ -1234,14 +1302,14 @@ MB_HD inline const double* contact_rec(const Blk& b, int k, int* row0) {
 // Baumgarte position term kp * (p - p_ref) | kp * log6(Mref^-1 oMf) (needs only
 // the placements), then the frame drift acceleration (classical for 3D, gravity
 // removed) + kd * v from the world velocity / acceleration of the body.
-MB_HD __attribute__((noinline)) void contact_a0_position(const Blk& b, const WVals& W, const CRec& C, double* a0) {
+MB_HD __attribute__((always_inline)) inline void contact_a0_position(const Blk& b, const WVals& W, const CRec& C, double* a0) {
   const double kp = C.r[1];
   double r[6] = {0., 0., 0., 0., 0., 0.};
   if (kp != 0.) frame_residual_value(b, W, C, r);
   const int n = C.type() == C_CONTACT_3D ? 3 : 6;
   for (int e = 0; e < n; ++e) a0[e] = kp * r[e];
 }
-MB_HD __attribute__((noinline)) void contact_a0_drift(const Blk& b, const WVals& W, const CRec& C, double* a0) {
+MB_HD __attribute__((always_inline)) inline void contact_a0_drift(const Blk& b, const WVals& W, const CRec& C, double* a0) {
   const double* d = C.d();
   const int j = frame_dof(b, d);
   double Rf[9], pf[3], m6[6], vf[6], af[6];
@@ -1292,8 +1360,9 @@ MB_HD inline void contact_joint_forces(const Blk& b, const WVals& W, const doubl
 // Jc[row * nj + c]) — the LOCAL frame Jacobian (pinocchio getFrameJacobian LOCAL,
 // contact-3d.hxx:29 / contact-6d.hxx:29): the world motion S_c moved to the frame
 // (SE3::actInv of oMf), zero unless c moves the frame's body; with At != null also
-// into the columns [nj + row] of A (ld nj).
-MB_HD __attribute__((noinline)) void contact_jac_lane(const Blk& b, const WVals& W, int c, double* Jc, double* At) {
+// into the columns [nj + row] of A (ld lda).
+MB_HD __attribute__((always_inline)) inline void contact_jac_lane(const Blk& b, const WVals& W, int c, double* Jc, double* At,
+                                                      int lda = 0) {
   double Sc[6];
   for (int e = 0; e < 6; ++e) Sc[e] = W.S(c)[e];
   const double* r = b.K;
@@ -1310,7 +1379,7 @@ MB_HD __attribute__((noinline)) void contact_jac_lane(const Blk& b, const WVals&
     const int n = C.type() == C_CONTACT_3D ? 3 : 6;
     for (int e = 0; e < n; ++e) {
       Jc[(int64_t)(row + e) * b.nj + c] = o[e];
-      if (At) At[(int64_t)(b.nj + row + e) * b.nj + c] = o[e];
+      if (At) At[(int64_t)(b.nj + row + e) * lda + c] = o[e];
     }
     row += n;
     r += C.size();
@@ -1321,7 +1390,7 @@ MB_HD __attribute__((noinline)) void contact_jac_lane(const Blk& b, const WVals&
 // the caller) for configuration q; `costs(wave, l)` runs on waves >= 2 in
 // the phase after the kinematics (nullptr-like no-op allowed).
 template <class X, class CostF>
-MB_HD inline void world_kinematics(const X& ex, const Blk& b, const WVals& W, const double* q, double* A,
+MB_HD inline void world_kinematics(const X& ex, const Blk& b, const WVals& W, const double* q, double* A, int lda,
                                    CostF costs) {
   const int nj = b.nj, R = jump_rounds(nj);
   ex.run([&](int lane) {
@@ -1340,7 +1409,7 @@ MB_HD inline void world_kinematics(const X& ex, const Blk& b, const WVals& W, co
     if (wave >= 2) costs(wave, l);
   });
   ex.run([&](int lane) {
-    if (lane < nj) w_crba_column(b, W, lane, A, nj);
+    if (lane < nj) w_crba_column(b, W, lane, A, lda);
   });
 }
 
@@ -1386,7 +1455,7 @@ MB_HD inline void euler_step(const Blk& b, const double* x, const double* a, dou
 
 // LDS (doubles) of the calc scratch for nj dofs and nc contact rows.
 MB_HD inline int64_t calc_work_doubles(int nj, int nc = 0) {
-  return pad2(WVals::doubles(nj)) + (int64_t)nj * (nj + nc + 1) + 2 * nj + kMaxCosts + 8 + (int64_t)nc * nj + nc +
+  return pad2(WVals::doubles(nj)) + (int64_t)lda_of(nj) * (nj + nc + 1) + 2 * nj + kMaxCosts + 8 + (int64_t)nc * nj + nc +
          (int64_t)nc * (nc + 1);
 }
 
@@ -1407,9 +1476,10 @@ MB_HD inline double knot_calc_x(const X& ex, const double* P, int nx, const doub
   const Blk b = parse(P);
   const bool imp = b.impulse;  // impulse: [M | Jc^T] only, z = v
   const int nj = b.nj, nq = b.nq, nc = b.nc, nu = nj - b.nun, ncol = imp ? nj + nc : nj + nc + 1;
+  const int lda = lda_of(nj);
   const WVals W{w, nj};
-  double* A = w + pad2(WVals::doubles(nj));  // nj x (nj + nc + 1), ld nj: [M | Jc^T | tau - nle]
-  double* tau = A + (int64_t)nj * ncol;
+  double* A = w + pad2(WVals::doubles(nj));  // nj x (nj + nc + 1), ld lda: [M | Jc^T | tau - nle]
+  double* tau = A + (int64_t)lda * ncol;
   double* ub = tau + nj;  // u (zero if !use_u)
   double* cv = ub + nj;   // per-cost activations
   double* red = cv + kMaxCosts;
@@ -1419,10 +1489,10 @@ MB_HD inline double knot_calc_x(const X& ex, const double* P, int nx, const doub
   double* S = a0 + nc;                   // nc x (nc + 1), ld nc: [S | Jc z + a0]
   ex.run([&](int lane) {
     if (lane < nu) ub[lane] = use_u ? u[lane] : 0.;
-    for (int e = lane; e < nj * ncol; e += ex.nt) A[e] = 0.;
+    for (int e = lane; e < lda * ncol; e += ex.nt) A[e] = 0.;
   });
   // cost records k on wave 2 + (k & 1), lane k >> 1, once the placements exist
-  world_kinematics(ex, b, W, x, A, [&](int wave, int l) {
+  world_kinematics(ex, b, W, x, A, lda, [&](int wave, int l) {
     const double* cr = b.C;
     for (int k = 0; k < b.ncost; ++k) {
       const CRec C{cr};
@@ -1440,8 +1510,8 @@ MB_HD inline double knot_calc_x(const X& ex, const double* P, int nx, const doub
   ex.run([&](int lane) {
     if (lane < nj) {
       const double ti = lane < b.nun ? 0. : ub[lane - b.nun];  // ActuationModelFloatingBase: tau = [0; u]
-      if (!imp) A[(int64_t)nj * (nj + nc) + lane] = ti - tau[lane];
-      if (nc) contact_jac_lane(b, W, lane, Jc, A);
+      if (!imp) A[(int64_t)lda * (nj + nc) + lane] = ti - tau[lane];
+      if (nc) contact_jac_lane(b, W, lane, Jc, A, lda);
     }
     if (!imp && lane >= 64 && lane < 64 + b.ncon) {
       int row0;
@@ -1463,21 +1533,21 @@ MB_HD inline double knot_calc_x(const X& ex, const double* P, int nx, const doub
       red[0] = total;
     }
   });
-  bool ok = gauss_jordan(ex, A, nj, ncol, flag);
+  bool ok = gauss_jordan(ex, A, nj, lda, ncol, flag);
   // z, then a (impulse: v+, in tau's slot; z = M^-1 M v = v)
-  double* a = imp ? tau : A + (int64_t)nj * (nj + nc);
+  double* a = imp ? tau : A + (int64_t)lda * (nj + nc);
   if (nc > 0) {
     ex.run([&](int lane) {
       for (int e = lane; e < nc * (nc + 1); e += ex.nt) {
         const int col = e / nc, row = e % nc;
         // column col of Y, or z (impulse: v, and the restitution term r Jc v)
-        const double* yc = (imp && col == nc) ? x + nq : A + (int64_t)nj * (nj + col);
+        const double* yc = (imp && col == nc) ? x + nq : A + (int64_t)lda * (nj + col);
         double s = 0.;
         for (int i = 0; i < nj; ++i) s += Jc[(int64_t)row * nj + i] * yc[i];
         S[e] = col < nc ? s + (row == col ? b.damping : 0.) : (imp ? (1. + b.r_coeff) * s : s + a0[row]);
       }
     });
-    ok = gauss_jordan(ex, S, nc, nc + 1, flag) && ok;
+    ok = gauss_jordan(ex, S, nc, nc, nc + 1, flag) && ok;
     ex.run([&](int lane) {
       if (lane == 64 && !imp) {  // contact-force costs (lambda = -S^-1 r, in S's last column, negated)
         double lamv[kMaxNc];
@@ -1493,7 +1563,7 @@ MB_HD inline double knot_calc_x(const X& ex, const double* P, int nx, const doub
       }
       if (lane >= nj) return;
       double s = imp ? x[nq + lane] : a[lane];
-      for (int k = 0; k < nc; ++k) s -= A[(int64_t)nj * (nj + k) + lane] * S[(int64_t)nc * nc + k];
+      for (int k = 0; k < nc; ++k) s -= A[(int64_t)lda * (nj + k) + lane] * S[(int64_t)nc * nc + k];
       a[lane] = s;
     });
   }
@@ -1525,7 +1595,7 @@ MB_HD inline double knot_calc_x(const X& ex, const double* P, int nx, const doub
 }
 
 template <int NT>
-__device__ inline double knot_calc(const double* P, int nx, const double* x, const double* u, bool use_u, double* xnext,
+__device__ __forceinline__ double knot_calc(const double* P, int nx, const double* x, const double* u, bool use_u, double* xnext,
                                    double* w) {
   static_assert(NT >= 256, "the multibody calc splits its phases over 4 waves");
   return knot_calc_x(DevExec{NT}, P, nx, x, u, use_u, xnext, w);
@@ -1553,18 +1623,29 @@ __device__ inline double knot_calc(const double* P, int nx, const double* x, con
 // ---------------------------------------------------------------------------
 struct DiffLayout {
   int64_t wv, A, dtau, da, qp, vec, J, red, total;
+  // cost-derivative area (after the dynamics, over the dead world values when it
+  // fits): group table, per-row Arr / Ar factors, the stacked residual Jacobians
+  int64_t R;
   // contact area (nc > 0): Jc nc x nj, a0 nc, lambda nc, Y = Minv Jc^T and
   // H = Y S^-1 (nj x nc each), [S | I | r] nc x (2nc + 1), da0/dx nc x L, fx 6 nj
   int64_t Jc, a0, lam, Y, H, Sx, da0, fx, zv, dfx, dfu;
 };
 // vec area: x (nq + nj <= 2 nj + 1), u (nj), nle / z / a / tau (3 nj), jac-cost
 // residuals (6 per cost), Jexp6 / Ad(exp6^-1) (72)
-__host__ __device__ inline DiffLayout diff_layout(int nj, int njac, int nc = 0, bool vel_cols = false) {
+// Cost-derivative area (doubles) for nrows stacked residual rows over L + nu columns.
+constexpr int kMaxCostRows = 64;
+// (4 columns of slack: the GEMM reads rows four columns at a time)
+MB_HD __forceinline__ int cost_rows_ld(int nj, int nu) { return (int)pad2(2 * nj + nu) + 4; }
+MB_HD __forceinline__ int64_t cost_area_doubles(int nj, int nu, int nrows) {
+  return 4 * kMaxCosts + 5 * kMaxCostRows + (int64_t)nrows * cost_rows_ld(nj, nu);
+}
+__host__ __device__ inline DiffLayout diff_layout(int nj, int njac, int nc = 0, bool vel_cols = false, int nu = 0,
+                                                  int nrows = 0) {
   const int L = 2 * nj;
   DiffLayout l;
   l.wv = 0;
   l.A = l.wv + pad2(WVals::doubles(nj));
-  l.dtau = l.A + (int64_t)nj * 2 * nj;  // [M | I] -> [. | Minv]
+  l.dtau = l.A + (int64_t)lda_of(nj) * 2 * nj;  // [M | I] -> [. | Minv], ld lda_of(nj)
   l.da = l.dtau + (int64_t)nj * L;      // dtau [k][L]
   l.qp = l.da + (int64_t)nj * L;        // da = -Kinv (dtau; da0) [r][L]
   l.vec = l.qp + (int64_t)12 * nj;      // Q_k, P_k
@@ -1583,6 +1664,13 @@ __host__ __device__ inline DiffLayout diff_layout(int nj, int njac, int nc = 0, 
   l.dfx = l.zv + nj;     // d lambda / dx (nc x L), d lambda / du (nc x nj): CostModelContactForce
   l.dfu = l.dfx + (int64_t)nc * L;
   l.total = nc > 0 ? l.dfu + (int64_t)nc * nj : l.total;
+  const int64_t ca = cost_area_doubles(nj, nu, nrows);
+  if (ca <= pad2(WVals::doubles(nj))) {
+    l.R = l.wv;
+  } else {
+    l.R = pad2(l.total);
+    l.total = l.R + ca;
+  }
   return l;
 }
 
@@ -1898,10 +1986,12 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
   const Blk b = parse(P);
   const bool imp = b.impulse;  // ActionModelImpulseFwdDynamics (impulse-fwddyn.hxx:53-127)
   const int nj = b.nj, nq = b.nq, n = 2 * nj, L = 2 * nj, nc = b.nc, nu = nj - b.nun;
+  const int lda = lda_of(nj);
   bool vcols;
   const int njac = count_jac_costs(b, &vcols);
   const int jw = vcols ? L : nj;  // columns of the stored jac-cost Jacobians
-  const DiffLayout l = diff_layout(nj, njac, nc, vcols);
+  const int nrows = count_cost_rows(b, nu);
+  const DiffLayout l = diff_layout(nj, njac, nc, vcols, nu, nrows);
   const WVals W{w + l.wv, nj};
   double* A = w + l.A;
   double* dtau = w + l.dtau;
@@ -1929,13 +2019,13 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
   ex.run([&](int lane) {
     for (int e = lane; e < nq + nj; e += ex.nt) x[e] = xg[e];
     if (lane < nj) u[lane] = (use_u && lane < nu) ? ug[lane] : 0.;  // (impulse: a zero velocity)
-    for (int e = lane; e < 2 * nj * nj; e += ex.nt) {
-      const int c = e / nj, r = e % nj;
-      A[e] = (c == nj + r) ? 1. : 0.;
+    for (int e = lane; e < 2 * nj * lda; e += ex.nt) {
+      const int c = e / lda, r = e % lda;
+      A[e] = (r < nj && c == nj + r) ? 1. : 0.;
     }
   });
   // world-frame kinematics, M into the left half of [M | I], nle
-  world_kinematics(ex, b, W, x, A, [](int, int) {});
+  world_kinematics(ex, b, W, x, A, lda, [](int, int) {});
   if (!imp) world_rnea(ex, b, W, x + nq, nullptr, nle);
   if (nc > 0)  // contact rows at the drift (ddq = 0; ContactModelMultiple::calc)
     ex.run([&](int lane) {
@@ -1947,8 +2037,8 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
         contact_a0_drift(b, W, C, a0 + row0);
       }
     });
-  bool ok = gauss_jordan(ex, A, nj, 2 * nj, flag);
-  double* Minv = A + (int64_t)nj * nj;  // column-major nj x nj; with contacts: d a / d tau after the Schur step
+  bool ok = gauss_jordan(ex, A, nj, lda, 2 * nj, flag);
+  double* Minv = A + (int64_t)lda * nj;  // column-major nj x nj; with contacts: d a / d tau after the Schur step
   // z = (M + A)^-1 (tau - nle) (the acceleration without contacts); Y = Minv Jc^T
   ex.run([&](int lane) {
     if (lane < nj && imp) {
@@ -1958,13 +2048,13 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
         for (int e = 0; e < 6; ++e) W.root_a()[e] = 0.;  // the impulse RNEA has no gravity
     } else if (lane < nj) {
       double s = 0.;
-      for (int k = 0; k < nj; ++k) s += Minv[(int64_t)k * nj + lane] * ((k < b.nun ? 0. : u[k - b.nun]) - nle[k]);
+      for (int k = 0; k < nj; ++k) s += Minv[(int64_t)k * lda + lane] * ((k < b.nun ? 0. : u[k - b.nun]) - nle[k]);
       av[lane] = ok ? s : NAN;
     }
     for (int e = lane; e < nj * nc; e += ex.nt) {
       const int k = e / nj, i = e % nj;
       double s = 0.;
-      for (int r = 0; r < nj; ++r) s += Minv[(int64_t)r * nj + i] * Jc[(int64_t)k * nj + r];
+      for (int r = 0; r < nj; ++r) s += Minv[(int64_t)r * lda + i] * Jc[(int64_t)k * nj + r];
       Y[e] = s;
     }
   });
@@ -1988,7 +2078,7 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
         Sx[e] = v;
       }
     });
-    ok = gauss_jordan(ex, Sx, nc, 2 * nc + 1, flag) && ok;
+    ok = gauss_jordan(ex, Sx, nc, nc, 2 * nc + 1, flag) && ok;
     // lambda = -S^-1 r, a = z + Y lambda, H = Y S^-1 (= Kinv top-right)
     ex.run([&](int lane) {
       const double* Sinv = Sx + (int64_t)nc * nc;
@@ -2010,9 +2100,9 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
     ex.run([&](int lane) {
       for (int e = lane; e < nj * nj; e += ex.nt) {
         const int c = e / nj, i = e % nj;
-        double s = Minv[e];
+        double s = Minv[(int64_t)c * lda + i];
         for (int k = 0; k < nc; ++k) s -= H[(int64_t)k * nj + i] * Y[(int64_t)k * nj + c];
-        Minv[e] = s;
+        Minv[(int64_t)c * lda + i] = s;
       }
       if (lane < nj) {
         contact_joint_forces(b, W, lam, fx, lane);
@@ -2099,7 +2189,7 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
       const int r = e / L, c = e % L;
       double s = 0.;
       if (!imp || c < nj) {
-        for (int k = 0; k < nj; ++k) s += Minv[(int64_t)k * nj + r] * dtau[(int64_t)k * L + c];
+        for (int k = 0; k < nj; ++k) s += Minv[(int64_t)k * lda + r] * dtau[(int64_t)k * L + c];
         for (int k = 0; k < nc; ++k) s += H[(int64_t)k * nj + r] * da0[(int64_t)k * L + c];
       }
       da[e] = ok ? -s : NAN;
@@ -2120,6 +2210,16 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
     }
   });
   const double sc = integ ? dt : 1.;
+  // cost-derivative area (layout: group table 4 kMaxCosts | Arr, Ar mul, Ar val,
+  // source per row | R rows)
+  double* cg = w + l.R;
+  double* ch = cg + 4 * kMaxCosts;
+  double* cam = ch + kMaxCostRows;
+  double* cav = cam + kMaxCostRows;
+  double* csrc = cav + kMaxCostRows;
+  double* cgi = csrc + kMaxCostRows;  // group of each row
+  double* Rm = csrc + 2 * kMaxCostRows;
+  const int ldR = cost_rows_ld(nj, nu);
   // Output blocks, entry by entry over all lanes (consecutive lanes write
   // consecutive addresses of the column-major blocks).
   ex.run([&](int lane) {
@@ -2161,130 +2261,175 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
       if (integ && c < nu && !imp) {
         if (i < nj && ffe && i < 6) {
           double s = 0.;
-          for (int r = 0; r < 6; ++r) s += Je[r * 6 + i] * Minv[(int64_t)(b.nun + c) * nj + r];
+          for (int r = 0; r < 6; ++r) s += Je[r * 6 + i] * Minv[(int64_t)(b.nun + c) * lda + r];
           f = ok ? s * dt2 : NAN;
         } else {
-          const double mi = ok ? Minv[(int64_t)(b.nun + c) * nj + (i < nj ? i : i - nj)] : NAN;
+          const double mi = ok ? Minv[(int64_t)(b.nun + c) * lda + (i < nj ? i : i - nj)] : NAN;
           f = i < nj ? mi * dt2 : mi * dt;
         }
       }
       Fu[e] = f;
-      double lxu = 0.;  // only the force costs couple x and u
-      if (fd && c < nu) {
-        const double* cr = b.C;
-        for (int k = 0; k < b.ncost; ++k) {
-          const CRec C{cr};
-          if (force_cost(C.type()) && (int)C.d()[0] >= 0) {
-            const Act act = cost_act(b, C, nu);
-            double s2 = 0.;
-            for (int r = 0; r < act.nr; ++r)
-              s2 += force_jac(C, dfx + i, L, r) * act.hess(r, force_res(C, lam, r)) * force_jac(C, dfu + c, nj, r);
-            lxu += C.weight() * s2;
-          }
-          cr += C.size();
-        }
-      }
-      Lxu[e] = sc * lxu;
     }
-    // Lxx(i, j): Gauss-Newton, cost-sum.hxx:122-160
-    for (int e = lane; e < n * n; e += ex.nt) {
-      const int j = e / n, i = e % n;
-      double lv = 0.;
+    // the cost-derivative table (last thread): groups in cost (name) order, each the
+    // rows of one cost with a dense residual Jacobian, or the diagonal of a state /
+    // control cost; per row Arr (hess), and Ar as amul * aval (the quadratic kinds'
+    // (w, r), so the gradient keeps the order (X w) r of the reference's R^T (w r))
+    if (lane == ex.nt - 1) {
+      int g = 0, row = 0, f = 0;
       const double* cr = b.C;
-      int f = 0;
       for (int k = 0; k < b.ncost; ++k) {
         const CRec C{cr};
         const int t = C.type();
-        const double wt = C.weight();
+        const Act act = cost_act(b, C, nu);
+        const double co = (double)(cr - P);
         if (jac_cost(b, t)) {
-          const int cols = t == C_FRAME_VELOCITY ? L : nj;
-          if (i < cols && j < cols) {
-            const Act act = cost_act(b, C, nu);
-            const int nr = jac_rows(t);
-            const double* Jk = Jf + (int64_t)f * 6 * jw;
-            double s2 = 0.;
-            for (int r = 0; r < nr; ++r) s2 += Jk[(int64_t)r * jw + i] * act.hess(r, rf[6 * f + r]) * Jk[(int64_t)r * jw + j];
-            lv += wt * s2;
+          const int r0 = row;
+          for (int e = 0; e < jac_rows(t); ++e, ++row) {
+            const double rv = rf[6 * f + e];
+            ch[row] = act.hess(e, rv);
+            cam[row] = act.kind <= A_WEIGHTED_QUAD ? act.p[e] : 1.;
+            cav[row] = act.kind <= A_WEIGHTED_QUAD ? rv : act.sgrad(e, rv, 1.);
+            csrc[row] = (double)(f * 8 + e);
+            cgi[row] = g;
           }
+          cg[4 * g] = r0;
+          cg[4 * g + 1] = row;
+          cg[4 * g + 2] = co;
+          cg[4 * g + 3] = t == C_FRAME_VELOCITY ? 1. : 0.;  // 0: q columns only, 1: x columns
+          ++g;
           ++f;
         }
-        if (t == C_STATE && i == j && !(b.ff && i < 6))
-          lv += wt * cost_act(b, C, nu).hess(j, state_res(b, C.d(), x, j));
-        if (force_cost(t) && fd && (int)C.d()[0] >= 0) {
-          const Act act = cost_act(b, C, nu);
-          double s2 = 0.;
-          for (int r = 0; r < act.nr; ++r)
-            s2 += force_jac(C, dfx + i, L, r) * act.hess(r, force_res(C, lam, r)) * force_jac(C, dfx + j, L, r);
-          lv += wt * s2;
+        if (t == C_STATE || t == C_CONTROL) {  // diagonal part (state: beyond the free-flyer block)
+          cg[4 * g] = -1.;
+          cg[4 * g + 1] = t == C_STATE ? 0. : 1.;
+          cg[4 * g + 2] = co;
+          cg[4 * g + 3] = 0.;
+          ++g;
+        }
+        if (fd && force_cost(t) && (int)C.d()[0] >= 0) {
+          const int r0 = row;
+          for (int e = 0; e < act.nr; ++e, ++row) {
+            const double rv = force_res(C, lam, e);
+            ch[row] = act.hess(e, rv);
+            cam[row] = act.kind <= A_WEIGHTED_QUAD ? act.p[e] : 1.;
+            cav[row] = act.kind <= A_WEIGHTED_QUAD ? rv : act.sgrad(e, rv, 1.);
+            csrc[row] = -1. - e;
+            cgi[row] = g;
+          }
+          cg[4 * g] = r0;
+          cg[4 * g + 1] = row;
+          cg[4 * g + 2] = co;
+          cg[4 * g + 3] = 2.;  // x and u columns
+          ++g;
         }
         cr += C.size();
       }
-      Lxx[e] = integ ? sc * lv : lv;
+      cg[4 * kMaxCosts - 1] = g;
     }
-    // Luu, Lu, Lx
-    for (int e = lane; e < m * m; e += ex.nt) {
-      const int j = e / m, i = e % m;
-      double lv = 0.;
-      if (i < nu && j < nu) {
-        const double* cr = b.C;
-        for (int k = 0; k < b.ncost; ++k) {
-          const CRec C{cr};
-          if (C.type() == C_CONTROL && i == j) lv += C.weight() * cost_act(b, C, nu).hess(j, u[j] - C.d()[j]);
-          if (force_cost(C.type()) && fd && (int)C.d()[0] >= 0) {
-            const Act act = cost_act(b, C, nu);
-            double s2 = 0.;
-            for (int r = 0; r < act.nr; ++r)
-              s2 += force_jac(C, dfu + i, nj, r) * act.hess(r, force_res(C, lam, r)) * force_jac(C, dfu + j, nj, r);
-            lv += C.weight() * s2;
-          }
-          cr += C.size();
-        }
+  });
+  // the stacked residual Jacobians R (nrows x (L + nu), ld ldR): jac-cost rows from
+  // their q (or x) columns, force-cost rows from d lambda / dx, du
+  const int ngr = (int)cg[4 * kMaxCosts - 1];
+  ex.run([&](int lane) {
+    for (int e = lane; e < nrows * ldR; e += ex.nt) {
+      const int row = e / ldR, c = e % ldR;
+      const int src = (int)csrc[row];
+      double v = 0.;
+      if (src >= 0) {  // jac cost f, row e2
+        const int f = src >> 3, e2 = src & 7;
+        const bool xc = c < nj || (c < L && jw == L);
+        v = xc ? Jf[((int64_t)f * 6 + e2) * jw + c] : 0.;
+        // a q-only cost stored with jw = L carries zeros in its velocity columns
+        if (c >= nj && c < L && jw == L && cg[4 * (int)cgi[row] + 3] == 0.) v = 0.;
+      } else {  // force cost row -1 - src of its group
+        const CRec C{P + (int64_t)cg[4 * (int)cgi[row] + 2]};
+        const int e2 = -1 - src;
+        if (c < L)
+          v = force_jac(C, dfx + c, L, e2);
+        else if (c - L < nu)
+          v = force_jac(C, dfu + (c - L), nj, e2);
       }
-      Luu[e] = integ ? sc * lv : lv;
+      Rm[e] = c < L + nu ? v : 0.;
     }
-    if (lane < m) {
-      const int j = lane;
-      double lu = 0.;
-      if (j < nu) {
-        const double* cr = b.C;
-        for (int k = 0; k < b.ncost; ++k) {
-          const CRec C{cr};
-          if (C.type() == C_CONTROL) lu += cost_act(b, C, nu).sgrad(j, u[j] - C.d()[j], C.weight());
-          if (force_cost(C.type()) && fd && (int)C.d()[0] >= 0) {
-            const Act act = cost_act(b, C, nu);
-            for (int r = 0; r < act.nr; ++r)
-              lu += act.sgrad(r, force_res(C, lam, r), C.weight() * force_jac(C, dfu + j, nj, r));
-          }
-          cr += C.size();
-        }
+  });
+  // Gauss-Newton blocks (cost-sum.hxx:122-160) as a small GEMM over the rows, in
+  // cost order: Lxx / Lxu / Luu entries four rows i at a time, then Lx / Lu.
+  ex.run([&](int lane) {
+    const int n4 = (n + 3) / 4, m4 = (m + 3) / 4;
+    const int tx = n4 * n, txu = n4 * m, tuu = m4 * m;
+    for (int task = lane; task < tx + txu + tuu; task += ex.nt) {
+      int blk, i0, j;
+      if (task < tx) {
+        blk = 0, i0 = 4 * (task % n4), j = task / n4;
+      } else if (task < tx + txu) {
+        blk = 1, i0 = 4 * ((task - tx) % n4), j = (task - tx) / n4;
+      } else {
+        blk = 2, i0 = 4 * ((task - tx - txu) % m4), j = (task - tx - txu) / m4;
       }
-      Lu[j] = integ ? sc * lu : lu;
-    }
-    for (int j = lane; j < n; j += ex.nt) {
-      double lx = 0.;
-      const double* cr = b.C;
-      int f = 0;
-      for (int k = 0; k < b.ncost; ++k) {
-        const CRec C{cr};
-        const int t = C.type();
-        const double wt = C.weight();
-        if (jac_cost(b, t)) {
-          if (j < (t == C_FRAME_VELOCITY ? L : nj)) {
-            const Act act = cost_act(b, C, nu);
-            const int nr = jac_rows(t);
-            const double* Jk = Jf + (int64_t)f * 6 * jw;
-            for (int r = 0; r < nr; ++r) lx += act.sgrad(r, rf[6 * f + r], wt * Jk[(int64_t)r * jw + j]);
+      // R columns of the rows (i) and of the column (j): x tangent or u (L + c)
+      const int ci = blk == 2 ? L + i0 : i0;
+      const int cj = blk == 0 ? j : L + j;
+      const bool jin = blk == 0 || j < nu;
+      double lv[4] = {0., 0., 0., 0.};
+      for (int g = 0; g < ngr; ++g) {
+        const int r0 = (int)cg[4 * g];
+        const CRec C{P + (int64_t)cg[4 * g + 2]};
+        if (r0 >= 0) {
+          const int r1 = (int)cg[4 * g + 1];
+          double s2[4] = {0., 0., 0., 0.};
+          for (int r = r0; r < r1; ++r) {
+            const double* Rr = Rm + (int64_t)r * ldR;
+            const double rj = jin ? Rr[cj] : 0.;
+            const double hr = ch[r];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) s2[q] += Rr[ci + q] * hr * rj;
           }
-          ++f;
-        }
-        if (t == C_STATE && !(b.ff && j < 6)) lx += cost_act(b, C, nu).sgrad(j, state_res(b, C.d(), x, j), wt);
-        if (force_cost(t) && fd && (int)C.d()[0] >= 0) {
+          const double wt = C.weight();
+#pragma unroll
+          for (int q = 0; q < 4; ++q) lv[q] += wt * s2[q];
+        } else if ((cg[4 * g + 1] == 0.) == (blk == 0) && blk != 1) {  // state (Lxx) / control (Luu) diagonal
           const Act act = cost_act(b, C, nu);
-          for (int r = 0; r < act.nr; ++r) lx += act.sgrad(r, force_res(C, lam, r), wt * force_jac(C, dfx + j, L, r));
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int i = i0 + q;
+            if (i != j) continue;
+            if (blk == 0 && !(b.ff && j < 6)) lv[q] += C.weight() * act.hess(j, state_res(b, C.d(), x, j));
+            if (blk == 2 && j < nu) lv[q] += C.weight() * act.hess(j, u[j] - C.d()[j]);
+          }
         }
-        cr += C.size();
       }
-      Lx[j] = integ ? sc * lx : lx;
+      const int rows = blk == 2 ? m : n;
+      double* out = blk == 0 ? Lxx : (blk == 1 ? Lxu : Luu);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int i = i0 + q;
+        if (i >= rows) continue;
+        const bool zero = (blk == 1 && j >= nu) || (blk == 2 && (i >= nu || j >= nu));
+        out[(int64_t)j * rows + i] = zero ? 0. : (blk == 1 || integ ? sc * lv[q] : lv[q]);
+      }
+    }
+    // Lx (x columns) and Lu (u columns): R^T Ar in cost order
+    for (int c = lane; c < n + m; c += ex.nt) {
+      const bool isu = c >= n;
+      const int j = isu ? c - n : c;
+      double acc = 0.;
+      if (!isu || j < nu) {
+        const int cc = isu ? L + j : j;
+        for (int g = 0; g < ngr; ++g) {
+          const int r0 = (int)cg[4 * g];
+          const CRec C{P + (int64_t)cg[4 * g + 2]};
+          const double wt = C.weight();
+          if (r0 >= 0) {
+            for (int r = r0; r < (int)cg[4 * g + 1]; ++r)
+              acc += wt * Rm[(int64_t)r * ldR + cc] * cam[r] * cav[r];
+          } else if (!isu && cg[4 * g + 1] == 0. && !(b.ff && j < 6)) {
+            acc += cost_act(b, C, nu).sgrad(j, state_res(b, C.d(), x, j), wt);
+          } else if (isu && cg[4 * g + 1] == 1.) {
+            acc += cost_act(b, C, nu).sgrad(j, u[j] - C.d()[j], wt);
+          }
+        }
+      }
+      (isu ? Lu : Lx)[j] = integ ? sc * acc : acc;
     }
     // the fused calc's cost: jac-cost residuals from the Jacobian phase (cost-sum.hxx:89-117)
     if (cost_out && lane == 0) {
@@ -2317,7 +2462,7 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
   (void)nx;
 }
 
-__device__ inline void knot_calc_diff(const double* P, int nx, int m, const double* xg, const double* ug, bool use_u,
+__device__ __forceinline__ void knot_calc_diff(const double* P, int nx, int m, const double* xg, const double* ug, bool use_u,
                                       double* w, double* Fx, double* Fu, double* Lxx, double* Lxu, double* Luu,
                                       double* Lx, double* Lu, double* xnext_out, double* cost_out) {
   knot_calc_diff_x(DevExec{kMbDiffNT}, P, nx, m, xg, ug, use_u, w, Fx, Fu, Lxx, Lxu, Luu, Lx, Lu, xnext_out, cost_out);

@@ -20,7 +20,7 @@ void mb_host_calc_diff(const double* P, int nx, int m, const double* x, const do
                        double* Fu, double* Lxx, double* Lxu, double* Luu, double* Lx, double* Lu, double* xnext,
                        double* cost) {
   const Blk b = parse(P);
-  std::vector<double> w(diff_layout(b.nj, kMaxJacCosts, b.nc, true).total, 0.);
+  std::vector<double> w(diff_layout(b.nj, kMaxJacCosts, b.nc, true, b.nj - b.nun, count_cost_rows(b, b.nj - b.nun)).total, 0.);
   knot_calc_diff_x(HostExec{kMbDiffNT}, P, nx, m, x, u, use_u != 0, w.data(), Fx, Fu, Lxx, Lxu, Luu, Lx, Lu, xnext, cost);
 }
 }

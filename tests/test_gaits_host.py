@@ -125,3 +125,22 @@ def test_quasi_static_holds_still(talos_walk, solo_trot):
             k = onp.ContactFwdKnot(m.pack()[2][0], g.state.nx, m.nu)
             a, _ = k.accel_force(x0, u)
             assert np.max(np.abs(a)) < 1e-8
+
+
+@pytest.mark.parametrize("t", [0, 1, 49])
+def test_talos_active_friction_cones(lib, talos_walk, t):  # noqa: F811
+    """Large tangential forces put the friction-cone barriers on (Arr = 1 rows) at the
+    reference posture (v = 0): knots whose first cost-derivative group is a control
+    diagonal (double support: ctrlReg before the cones in name order) included."""
+    g, models = talos_walk
+    x = g.rmodel.defaultState.copy()
+    rng = np.random.default_rng(20 + t)
+    m = models[t]
+    hit = 0
+    for _ in range(6):
+        u = m.quasiStatic(None, x) + rng.uniform(-300, 300, m.nu)
+        k = onp.ContactFwdKnot(m.pack()[2][0], x.size, m.nu)
+        _, res = k._calc_res(x, u)
+        hit += sum(int(np.any(c.a_hess(np.real(r)) > 0)) for c, r in zip(k.costs, res) if c.type == onp.FRICTION_CONE)
+        _check_knot(lib, m, x, u, tol=1e-8)
+    assert hit > 0

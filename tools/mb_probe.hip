@@ -1,0 +1,192 @@
+// Diagnostic (not product): per-phase cycle breakdown of the multibody knot
+// calcDiff / calc (crocoddyl_amd/csrc/multibody.hpp) on one packed block.
+// Usage: mb_probe <input.bin> <nwg>  (input from tools/mb_probe.py).
+// Every executor phase (run / run_w0 / sync) is stamped with s_memtime by
+// thread 0 of workgroup 0; nwg workgroups run concurrently (load as in the
+// knot-parallel kernel).
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <vector>
+#include "../crocoddyl_amd/csrc/multibody.hpp"
+
+using namespace fddp::mb;
+using fddp::pad2;
+
+struct StampExec {
+  int nt;
+  unsigned long long* st;  // LDS: [0] = count, then stamps
+  template <class F>
+  __device__ __forceinline__ void run(F f) const {
+    [[clang::always_inline]] f((int)threadIdx.x);
+    __syncthreads();
+    mark();
+  }
+  template <class F>
+  __device__ __forceinline__ void run_w0(F f) const {
+    if (threadIdx.x < 64) {
+      [[clang::always_inline]] f((int)threadIdx.x);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    if (threadIdx.x == 0) {
+      unsigned long long i = st[0]++;
+      if (i < 254) st[2 + i] = __builtin_amdgcn_s_memtime() | (1ull << 63);
+    }
+  }
+  __device__ __forceinline__ void sync() const {
+    __syncthreads();
+    mark();
+  }
+  __device__ __forceinline__ void mark() const {
+    if (threadIdx.x == 0) {
+      unsigned long long i = st[0]++;
+      if (i < 254) st[2 + i] = __builtin_amdgcn_s_memtime();
+    }
+  }
+};
+
+// found by argument-dependent lookup (StampExec is in the global namespace)
+__device__ inline bool gauss_jordan(const StampExec& ex, double* A, int nr, int ld, int nc, int* flag) {
+  const bool ok = gauss_jordan_dev(A, nr, ld, nc, flag);
+  ex.mark();
+  return ok;
+}
+
+__global__ __launch_bounds__(kMbDiffNT) void probe_diff(const double* Pg, int nx, int m, const double* xg,
+                                                        const double* ug, int use_u, double* out, int64_t so,
+                                                        unsigned long long* stamps, int mode) {
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  const int psz = (int)Pg[3];
+  const Blk bk = parse(Pg);
+  bool vc;
+  const int njac = count_jac_costs(bk, &vc);
+  const DiffLayout l = diff_layout(bk.nj, njac, bk.nc, vc, bk.nj - bk.nun, count_cost_rows(bk, bk.nj - bk.nun));
+  double* P = sm + pad2(l.total);
+  unsigned long long* st = (unsigned long long*)(P + pad2(psz));
+  for (int e = threadIdx.x; e < psz; e += kMbDiffNT) P[e] = Pg[e];
+  if (threadIdx.x == 0) {
+    st[0] = 0;
+    st[1] = __builtin_amdgcn_s_memtime();
+  }
+  __syncthreads();
+  StampExec ex{kMbDiffNT, st};
+  double* o = out + so * blockIdx.x;
+  const int n = 2 * (int)Pg[1];
+  double xn[1];
+  (void)xn;
+  if (mode == 0)
+    knot_calc_diff_x(ex, P, nx, m, xg, ug, use_u != 0, sm, o, o + n * n, o + n * n + n * m, o + 2 * n * n + n * m,
+                     o + 2 * n * n + 2 * n * m, o + 2 * n * n + 2 * n * m + m * m, o + 2 * n * n + 2 * n * m + m * m + n,
+                     o + 2 * n * n + 2 * n * m + m * m + n + m, o + 2 * n * n + 2 * n * m + m * m + n + m + nx);
+  __syncthreads();
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    const unsigned long long c = st[0] < 254 ? st[0] : 254;
+    stamps[0] = c;
+    stamps[1] = st[1];
+    for (unsigned long long i = 0; i < c; ++i) stamps[2 + i] = st[2 + i];
+  }
+}
+
+__global__ __launch_bounds__(256) void probe_calc(const double* Pg, int nx, const double* xg, const double* ug,
+                                                  int use_u, double* out, unsigned long long* stamps) {
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  const int psz = (int)Pg[3];
+  const int64_t w = pad2(calc_work_doubles((int)Pg[1], parse(Pg).nc));
+  double* P = sm + w;
+  unsigned long long* st = (unsigned long long*)(P + pad2(psz));
+  for (int e = threadIdx.x; e < psz; e += 256) P[e] = Pg[e];
+  if (threadIdx.x == 0) {
+    st[0] = 0;
+    st[1] = __builtin_amdgcn_s_memtime();
+  }
+  __syncthreads();
+  StampExec ex{256, st};
+  const double c = knot_calc_x(ex, P, nx, xg, ug, use_u != 0, out + (int64_t)blockIdx.x * (nx + 1), sm);
+  if (threadIdx.x == 0) out[(int64_t)blockIdx.x * (nx + 1) + nx] = c;
+  __syncthreads();
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    const unsigned long long cc = st[0] < 254 ? st[0] : 254;
+    stamps[0] = cc;
+    stamps[1] = st[1];
+    for (unsigned long long i = 0; i < cc; ++i) stamps[2 + i] = st[2 + i];
+  }
+}
+
+#define CK(x)                                                                   \
+  do {                                                                          \
+    hipError_t e_ = (x);                                                        \
+    if (e_ != hipSuccess) {                                                     \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      return 1;                                                                 \
+    }                                                                           \
+  } while (0)
+
+int main(int argc, char** argv) {
+  if (argc < 3) return 2;
+  FILE* f = fopen(argv[1], "rb");
+  if (!f) return 2;
+  int hdr[4];  // nx, nu, m, psz
+  if (fread(hdr, 4, 4, f) != 4) return 2;
+  const int nx = hdr[0], nu = hdr[1], m = hdr[2], psz = hdr[3];
+  std::vector<double> P(psz), x(nx), u(m > 0 ? m : 1);
+  if (fread(P.data(), 8, psz, f) != (size_t)psz || fread(x.data(), 8, nx, f) != (size_t)nx ||
+      fread(u.data(), 8, u.size(), f) != u.size())
+    return 2;
+  fclose(f);
+  const int nwg = atoi(argv[2]);
+  const int nj = (int)P[1], n = 2 * nj;
+  double *dP, *dx, *du, *dout;
+  unsigned long long* dst;
+  CK(hipMalloc(&dP, 8 * psz));
+  CK(hipMalloc(&dx, 8 * nx));
+  CK(hipMalloc(&du, 8 * u.size()));
+  const int64_t so = 2 * n * n + 2 * n * m + m * m + n + m + nx + 2;
+  CK(hipMalloc(&dout, 8 * so * nwg + 8 * (nx + 1) * nwg));
+  CK(hipMalloc(&dst, 8 * 256));
+  CK(hipMemcpy(dP, P.data(), 8 * psz, hipMemcpyHostToDevice));
+  CK(hipMemcpy(dx, x.data(), 8 * nx, hipMemcpyHostToDevice));
+  CK(hipMemcpy(du, u.data(), 8 * u.size(), hipMemcpyHostToDevice));
+  const Blk bk = parse(P.data());
+  bool vc;
+  const int njac = count_jac_costs(bk, &vc);
+  const DiffLayout l = diff_layout(nj, njac, bk.nc, vc, bk.nj - bk.nun, count_cost_rows(bk, bk.nj - bk.nun));
+  const size_t smd = 8 * (pad2(l.total) + pad2(psz) + 256);
+  const size_t smc = 8 * (pad2(calc_work_doubles(nj, bk.nc)) + pad2(psz) + 256);
+  printf("nj %d nx %d nu %d m %d psz %d lds diff %zu calc %zu\n", nj, nx, nu, m, psz, smd, smc);
+  CK(hipFuncSetAttribute((const void*)probe_diff, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smd));
+  CK(hipFuncSetAttribute((const void*)probe_calc, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smc));
+  std::vector<unsigned long long> st(256);
+  for (int which = 0; which < 2; ++which) {
+    for (int rep = 0; rep < 3; ++rep) {
+      hipEvent_t e0, e1;
+      CK(hipEventCreate(&e0));
+      CK(hipEventCreate(&e1));
+      CK(hipEventRecord(e0));
+      if (which == 0)
+        hipLaunchKernelGGL(probe_diff, dim3(nwg), dim3(kMbDiffNT), smd, 0, dP, nx, m, dx, du, nu > 0 ? 1 : 0, dout, so,
+                           dst, 0);
+      else
+        hipLaunchKernelGGL(probe_calc, dim3(nwg), dim3(256), smc, 0, dP, nx, dx, du, nu > 0 ? 1 : 0, dout, dst);
+      CK(hipEventRecord(e1));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      CK(hipMemcpy(st.data(), dst, 8 * 256, hipMemcpyDeviceToHost));
+      printf("%s nwg %d: %.3f ms (%.2f us per WG-knot at 256 CUs)\n", which == 0 ? "calcDiff" : "calc", nwg, ms,
+             1e3 * ms / (nwg / 256.0 > 1 ? nwg / 256.0 : 1));
+      if (rep == 2) {
+        unsigned long long prev = st[1];
+        printf("  phases (s_memtime ticks; * = wave-0 phase):");
+        for (unsigned long long i = 0; i < st[0]; ++i) {
+          const bool w0 = st[2 + i] >> 63;
+          const unsigned long long t = st[2 + i] & ~(1ull << 63);
+          printf(" %llu%s", t - prev, w0 ? "*" : "");
+          prev = t;
+        }
+        printf("\n  total %llu\n", prev - st[1]);
+      }
+    }
+  }
+  return 0;
+}
