@@ -46,7 +46,7 @@ constexpr int kJRec = 27;         // doubles per joint record
 constexpr int kCHdr = 4;          // doubles of a cost record's header
 constexpr int kMaxJacCosts = 8;   // costs with a dense residual Jacobian (frame, CoM, free-flyer state)
 constexpr int kMaxNc = 24;        // stacked contact rows (FDDP_KNOT_EULER_CONTACTFWD)
-constexpr int kMbDiffNT = 128;    // threads of the knot-parallel calcDiff workgroup
+constexpr int kMbDiffNT = 256;    // threads of the knot-parallel calcDiff workgroup
 enum { J_REVOLUTE = 0, J_FREEFLYER = 1 };
 // Cost record types; contact records (after the costs) use 5 / 6 and the same
 // frame payload as the frame costs, so frame_residual serves both.
@@ -457,14 +457,93 @@ __device__ __forceinline__ bool gauss_jordan_dev(double* A, int nr, int ld, int 
   return !bad;
 }
 
-// the device executor takes the all-thread version (overload resolution prefers it
-// to the template below, which serves the host emulation)
-__device__ __forceinline__ bool gauss_jordan(const DevExec&, double* A, int nr, int ld, int nc, int* flag) {
+// v from lane l (uniform l) of the wave, as a scalar
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  const long long bits = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)bits, l);
+  const int hi = __builtin_amdgcn_readlane((int)(bits >> 32), l);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// Gauss-Jordan with the rows in registers: lane r of every wave holds row r
+// (nr <= 64) of the column slabs of CPW columns the wave owns (slab s of wave w:
+// columns (w + s nw) CPW ..); per pivot k the wave owning column k publishes it
+// through LDS (pb: 2 x 64 doubles, double-buffered, so one barrier per pivot), the
+// pivot row comes from lane k by readlane. The pivot loop runs in chunks of CPW
+// unrolled steps, so the owner's register of column k is static. No LDS traffic
+// beyond the one published column per pivot. Returns false if a pivot is not
+// positive (the LLT failure the reference reports).
+template <int CPW, int SPW>
+__device__ __forceinline__ bool gauss_jordan_rows(double* A, int nr, int ld, int nc, double* pb, int* flag) {
+  const int tid = (int)threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = (int)(blockDim.x >> 6);
+  const int nslab = (nc + CPW - 1) / CPW;
+  double v[SPW][CPW];
+  __syncthreads();
+#pragma unroll
+  for (int s = 0; s < SPW; ++s) {
+    const int slab = wave + s * nw;
+#pragma unroll
+    for (int j = 0; j < CPW; ++j) {
+      const int c = slab * CPW + j;
+      v[s][j] = (lane < nr && slab < nslab && c < nc) ? A[(int64_t)c * ld + lane] : 0.;
+    }
+  }
+  bool bad = false;
+#pragma unroll 1
+  for (int kk = 0; kk < nr; kk += CPW) {
+    const int kslab = kk / CPW, owner = kslab % nw, os = kslab / nw;
+#pragma unroll
+    for (int j = 0; j < CPW; ++j) {
+      const int k = kk + j;
+      if (k >= nr) continue;  // (uniform)
+      double* pcol = pb + (k & 1) * 64;
+      if (wave == owner) {
+        double val = 0.;
+#pragma unroll
+        for (int s = 0; s < SPW; ++s)
+          if (s == os) val = v[s][j];
+        pcol[lane] = val;
+      }
+      __syncthreads();
+      const double piv = pcol[k];
+      const double ark = pcol[lane];  // A[r][k] of this lane's row
+      bad = bad || !(piv > 0.);
+      const double ipiv = 1. / piv;
+#pragma unroll
+      for (int s = 0; s < SPW; ++s) {
+#pragma unroll
+        for (int jj = 0; jj < CPW; ++jj) {
+          const double akc = readlane_d(v[s][jj], k) * ipiv;  // pivot row, scaled
+          v[s][jj] = lane == k ? akc : v[s][jj] - ark * akc;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < SPW; ++s) {
+    const int slab = wave + s * nw;
+#pragma unroll
+    for (int j = 0; j < CPW; ++j) {
+      const int c = slab * CPW + j;
+      if (lane < nr && slab < nslab && c < nc) A[(int64_t)c * ld + lane] = v[s][j];
+    }
+  }
+  if (tid == 0) *flag = bad ? 1 : 0;
+  __syncthreads();
+  return !bad;
+}
+
+// the device executor takes the register version when the slabs fit (overload
+// resolution prefers these to the template below, which serves the host emulation)
+__device__ __forceinline__ bool gauss_jordan(const DevExec&, double* A, int nr, int ld, int nc, int* flag,
+                                             double* pb) {
+  if (nr <= 64 && nc <= 3 * 8 * (int)(blockDim.x >> 6)) return gauss_jordan_rows<8, 3>(A, nr, ld, nc, pb, flag);
   return gauss_jordan_dev(A, nr, ld, nc, flag);
 }
 
 template <class X>
-MB_HD __attribute__((noinline)) bool gauss_jordan(const X& ex, double* A, int nr, int ld, int nc, int* flag) {
+MB_HD __attribute__((noinline)) bool gauss_jordan(const X& ex, double* A, int nr, int ld, int nc, int* flag,
+                                                 double* = nullptr) {
   ex.run_w0([&](int lane) {
     if (lane == 0) *flag = 0;
   });
@@ -1456,7 +1535,7 @@ MB_HD inline void euler_step(const Blk& b, const double* x, const double* a, dou
 // LDS (doubles) of the calc scratch for nj dofs and nc contact rows.
 MB_HD inline int64_t calc_work_doubles(int nj, int nc = 0) {
   return pad2(WVals::doubles(nj)) + (int64_t)lda_of(nj) * (nj + nc + 1) + 2 * nj + kMaxCosts + 8 + (int64_t)nc * nj + nc +
-         (int64_t)nc * (nc + 1);
+         (int64_t)nc * (nc + 1) + 128;
 }
 
 // model->calc(data, x, u) for the Euler∘FreeFwdDynamics knot (euler.hxx:41-80,
@@ -1487,6 +1566,7 @@ MB_HD inline double knot_calc_x(const X& ex, const double* P, int nx, const doub
   double* Jc = red + 8;                  // nc x nj
   double* a0 = Jc + (int64_t)nc * nj;    // nc
   double* S = a0 + nc;                   // nc x (nc + 1), ld nc: [S | Jc z + a0]
+  double* pb = S + (int64_t)nc * (nc + 1);  // Gauss-Jordan pivot-column buffer (128)
   ex.run([&](int lane) {
     if (lane < nu) ub[lane] = use_u ? u[lane] : 0.;
     for (int e = lane; e < lda * ncol; e += ex.nt) A[e] = 0.;
@@ -1533,7 +1613,7 @@ MB_HD inline double knot_calc_x(const X& ex, const double* P, int nx, const doub
       red[0] = total;
     }
   });
-  bool ok = gauss_jordan(ex, A, nj, lda, ncol, flag);
+  bool ok = gauss_jordan(ex, A, nj, lda, ncol, flag, pb);
   // z, then a (impulse: v+, in tau's slot; z = M^-1 M v = v)
   double* a = imp ? tau : A + (int64_t)lda * (nj + nc);
   if (nc > 0) {
@@ -1547,7 +1627,7 @@ MB_HD inline double knot_calc_x(const X& ex, const double* P, int nx, const doub
         S[e] = col < nc ? s + (row == col ? b.damping : 0.) : (imp ? (1. + b.r_coeff) * s : s + a0[row]);
       }
     });
-    ok = gauss_jordan(ex, S, nc, nc, nc + 1, flag) && ok;
+    ok = gauss_jordan(ex, S, nc, nc, nc + 1, flag, pb) && ok;
     ex.run([&](int lane) {
       if (lane == 64 && !imp) {  // contact-force costs (lambda = -S^-1 r, in S's last column, negated)
         double lamv[kMaxNc];
@@ -1651,7 +1731,7 @@ __host__ __device__ inline DiffLayout diff_layout(int nj, int njac, int nc = 0, 
   l.vec = l.qp + (int64_t)12 * nj;      // Q_k, P_k
   l.J = l.vec + pad2(6 * nj + 1 + 6 * kMaxJacCosts + 72);
   l.red = l.J + (int64_t)6 * (vel_cols ? L : nj) * (njac > 0 ? njac : 1);  // jac-cost Jacobians [cost][6][jw]
-  l.total = l.red + 8;
+  l.total = l.red + 8 + 128;  // reductions, Gauss-Jordan pivot-column buffer
   l.Jc = l.total;
   l.a0 = l.Jc + (int64_t)nc * nj;
   l.lam = l.a0 + nc;
@@ -2037,7 +2117,8 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
         contact_a0_drift(b, W, C, a0 + row0);
       }
     });
-  bool ok = gauss_jordan(ex, A, nj, lda, 2 * nj, flag);
+  double* pb = red + 8;
+  bool ok = gauss_jordan(ex, A, nj, lda, 2 * nj, flag, pb);
   double* Minv = A + (int64_t)lda * nj;  // column-major nj x nj; with contacts: d a / d tau after the Schur step
   // z = (M + A)^-1 (tau - nle) (the acceleration without contacts); Y = Minv Jc^T
   ex.run([&](int lane) {
@@ -2078,7 +2159,7 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
         Sx[e] = v;
       }
     });
-    ok = gauss_jordan(ex, Sx, nc, nc, 2 * nc + 1, flag) && ok;
+    ok = gauss_jordan(ex, Sx, nc, nc, 2 * nc + 1, flag, pb) && ok;
     // lambda = -S^-1 r, a = z + Y lambda, H = Y S^-1 (= Kinv top-right)
     ex.run([&](int lane) {
       const double* Sinv = Sx + (int64_t)nc * nc;

@@ -47,8 +47,9 @@ struct StampExec {
 };
 
 // found by argument-dependent lookup (StampExec is in the global namespace)
-__device__ inline bool gauss_jordan(const StampExec& ex, double* A, int nr, int ld, int nc, int* flag) {
-  const bool ok = gauss_jordan_dev(A, nr, ld, nc, flag);
+__device__ inline bool gauss_jordan(const StampExec& ex, double* A, int nr, int ld, int nc, int* flag, double* pb) {
+  const bool ok = (nr <= 64 && nc <= 3 * 8 * (int)(blockDim.x >> 6)) ? gauss_jordan_rows<8, 3>(A, nr, ld, nc, pb, flag)
+                                                                      : gauss_jordan_dev(A, nr, ld, nc, flag);
   ex.mark();
   return ok;
 }
