@@ -216,6 +216,9 @@ def main():
     elapsed = time.perf_counter() - t0
     solver.set_timing(False)
     timing = solver.get_timing()
+    # line-search trials of the last step, per element: alpha = 2^-k accepted after k + 1 trials
+    sl = np.atleast_1d(np.asarray(solver.stepLength, float))
+    trials = np.round(-np.log2(np.clip(sl, 2.0 ** -12, 1.0))) + 1
     elapsed, total_iters = cdist.job_time_and_work(elapsed, iters, f"cuda:{dev}")
     assert xs_all.shape[0] == ws * B
 
@@ -267,6 +270,8 @@ def main():
                        "solver": "SolverBoxFDDP" if box else "SolverFDDP"},
             "mpc_solves_per_s": round(B * ws * args.steps / elapsed, 2),
             "kernel_ms_per_step": {k: round(v[0] / max(args.steps, 1), 3) for k, v in timing.items()},
+            "line_search_trials_last_step": {"mean": round(float(trials.mean()), 2), "max": int(trials.max()),
+                                             "hist": np.bincount(trials.astype(int), minlength=11)[1:].tolist()},
             "roofline": roof,
             "cpu_baseline": cpu,
         }

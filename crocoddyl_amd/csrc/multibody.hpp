@@ -1726,8 +1726,11 @@ __host__ __device__ inline DiffLayout diff_layout(int nj, int njac, int nc = 0, 
   l.wv = 0;
   l.A = l.wv + pad2(WVals::doubles(nj));
   l.dtau = l.A + (int64_t)lda_of(nj) * 2 * nj;  // [M | I] -> [. | Minv], ld lda_of(nj)
-  l.da = l.dtau + (int64_t)nj * L;      // dtau [k][L]
-  l.qp = l.da + (int64_t)nj * L;        // da = -Kinv (dtau; da0) [r][L]
+  // dtau [k][L] (first the per-body N_b, h_b: 42 per dof); da = -Kinv (dtau; da0) [r][L]
+  // (first the subtree sums Nsub, Hsub)
+  const int64_t dsz = (int64_t)nj * L > 42 * (int64_t)nj ? (int64_t)nj * L : 42 * (int64_t)nj;
+  l.da = l.dtau + dsz;
+  l.qp = l.da + dsz;
   l.vec = l.qp + (int64_t)12 * nj;      // Q_k, P_k
   l.J = l.vec + pad2(6 * nj + 1 + 6 * kMaxJacCosts + 72);
   l.red = l.J + (int64_t)6 * (vel_cols ? L : nj) * (njac > 0 ? njac : 1);  // jac-cost Jacobians [cost][6][jw]
@@ -1752,6 +1755,72 @@ __host__ __device__ inline DiffLayout diff_layout(int nj, int njac, int nc = 0, 
     l.total = l.R + ca;
   }
   return l;
+}
+
+// The velocity-product terms of the derivatives are linear maps of the subtree
+// bodies: with N_b x = V_b x* (Y_b x) - Y_b (V_b x x) and h_b = Y_b V_b,
+//   P_k = Nsub_k S_k - S_k x* Hsub_k,   B_j x = Nsub_j x + x x* Hsub_j,
+// Nsub / Hsub the subtree sums. lane d < nj: N_d (column-major 6x6) and h_d of d's
+// body (zero on the massless free-flyer dofs) into nb[42 d ..].
+MB_HD inline void body_nh_lane(const Blk& b, const WVals& W, int d, double* nb) {
+  double* o = nb + 42 * d;
+  if (!carries_body(b, d)) {
+    for (int e = 0; e < 42; ++e) o[e] = 0.;
+    return;
+  }
+  const double m = *W.m(d);
+  double c[3], I6[6], V[6];
+  for (int e = 0; e < 3; ++e) c[e] = W.c(d)[e];
+  for (int e = 0; e < 6; ++e) {
+    I6[e] = W.Ic(d)[e];
+    V[e] = W.v(d)[e];
+  }
+  for (int col = 0; col < 6; ++col) {
+    double x[6] = {0., 0., 0., 0., 0., 0.}, Yx[6], t1[6], VxX[6], t2[6];
+    x[col] = 1.;
+    inertia_mul(m, c, I6, x, Yx);
+    cross_f(V, Yx, t1);
+    cross_m(V, x, VxX);
+    inertia_mul(m, c, I6, VxX, t2);
+    for (int e = 0; e < 6; ++e) o[6 * col + e] = t1[e] - t2[e];
+  }
+  inertia_mul(m, c, I6, V, o + 36);
+}
+// lane j < nj: Nsub_j, Hsub_j (sums over the bodies below dof j) into ns[42 j ..]
+MB_HD inline void subtree_nh_lane(const Blk& b, const WVals& W, int j, const double* nb, double* ns) {
+  double acc[42];
+  for (int e = 0; e < 42; ++e) acc[e] = 0.;
+  for (int bb = 0; bb < b.nj; ++bb) {
+    if (!((*W.anc(bb) >> j) & 1ull) || !carries_body(b, bb)) continue;
+    const double* o = nb + 42 * bb;
+    for (int e = 0; e < 42; ++e) acc[e] += o[e];
+  }
+  for (int e = 0; e < 42; ++e) ns[42 * j + e] = acc[e];
+}
+// B_j x = Nsub_j x + x x* Hsub_j
+MB_HD __forceinline__ void bsub_mul_ns(const double* ns, int j, const double* x, double* o) {
+  const double* N = ns + 42 * j;
+  double t[6];
+  cross_f(x, N + 36, t);
+  for (int e = 0; e < 6; ++e) {
+    double v = t[e];
+    for (int col = 0; col < 6; ++col) v += N[6 * col + e] * x[col];
+    o[e] = v;
+  }
+}
+// lane k < nj: Q_k = Ycrb_k S_k, P_k = Nsub_k S_k - S_k x* Hsub_k. qp[12 k ..].
+MB_HD inline void qp_lane_ns(const WVals& W, int k, const double* ns, double* qp) {
+  double S[6], Q[6], t6[6];
+  for (int e = 0; e < 6; ++e) S[e] = W.S(k)[e];
+  comp_mul(W, k, S, Q);
+  const double* N = ns + 42 * k;
+  cross_f(S, N + 36, t6);
+  for (int e = 0; e < 6; ++e) {
+    double v = -t6[e];
+    for (int col = 0; col < 6; ++col) v += N[6 * col + e] * S[col];
+    qp[12 * k + e] = Q[e];
+    qp[12 * k + 6 + e] = v;
+  }
 }
 
 // lane k < nj: Q_k = Ycrb_k S_k, P_k (header comment). qp[12 k ..].
@@ -1819,7 +1888,8 @@ MB_HD inline void parent_motion(const Blk& b, const WVals& W, int j, double* VP,
   }
 }
 
-MB_HD inline void dtau_direction(const Blk& b, const WVals& W, const double* qp, int dd, int L, double* dtau) {
+MB_HD inline void dtau_direction(const Blk& b, const WVals& W, const double* qp, int dd, int L, double* dtau,
+                                  const double* ns = nullptr) {
   const int nj = b.nj, j = dd < nj ? dd : dd - nj;
   const bool isq = dd < nj;
   double S[6], VP[6], AP[6], u[6], cj[6], G[6], t6[6], t7[6];
@@ -1835,7 +1905,10 @@ MB_HD inline void dtau_direction(const Blk& b, const WVals& W, const double* qp,
     for (int e = 0; e < 6; ++e) F[e] = W.F(j)[e];
     cross_f(S, F, G);
     comp_mul(W, j, cj, t6);
-    bsub_mul(b, W, j, u, Bu);
+    if (ns)
+      bsub_mul_ns(ns, j, u, Bu);
+    else
+      bsub_mul(b, W, j, u, Bu);
     for (int e = 0; e < 6; ++e) G[e] += t6[e] - Bu[e];
   } else {
     // w_j = (V_b(j) + V_P) x S_j ; G_j = Ycrb_j w_j + B_j S_j
@@ -1843,7 +1916,10 @@ MB_HD inline void dtau_direction(const Blk& b, const WVals& W, const double* qp,
     for (int e = 0; e < 6; ++e) Vs[e] = W.v(j)[e] + VP[e];
     cross_m(Vs, S, cj);  // (w_j in cj)
     comp_mul(W, j, cj, G);
-    bsub_mul(b, W, j, S, BS);
+    if (ns)
+      bsub_mul_ns(ns, j, S, BS);
+    else
+      bsub_mul(b, W, j, S, BS);
     for (int e = 0; e < 6; ++e) G[e] += BS[e];
     for (int e = 0; e < 6; ++e) u[e] = S[e];  // P_k . S_j
   }
@@ -2229,9 +2305,20 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
   const bool ffe = b.ff && integ && !imp;  // Euler on the free-flyer: Jexp6 / Ad(exp6^-1)
   // per-dof Q_k, P_k (lanes < nj) and the jac-cost Jacobians / residuals; the
   // free-flyer Euler step's Jexp6 and Ad(exp6(dq)^-1) (dq = v dt + a dt^2)
+  // per-body velocity-product maps (in the dtau area, free until the dtau phase), then
+  // their subtree sums (in the da area, free until the da phase)
+  double* nsub = imp ? nullptr : da;
+  if (!imp) {
+    ex.run([&](int lane) {
+      if (lane < nj) body_nh_lane(b, W, lane, dtau);
+    });
+    ex.run([&](int lane) {
+      if (lane < nj) subtree_nh_lane(b, W, lane, dtau, nsub);
+    });
+  }
   ex.run([&](int lane) {
     if (lane >= nj) return;
-    if (!imp) qp_lane(b, W, lane, qp);
+    if (!imp) qp_lane_ns(W, lane, nsub, qp);
     double dq[6];
     if (ffe)
       for (int e = 0; e < 6; ++e) dq[e] = x[nq + e] * dt + av[e] * dt2;
@@ -2247,7 +2334,7 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
   // tangent directions: dtau/dx (impulse: q only) and da0/dx
   ex.run([&](int lane) {
     for (int dd = lane; dd < (imp ? nj : L); dd += ex.nt) {
-      dtau_direction(b, W, qp, dd, L, dtau);
+      dtau_direction(b, W, qp, dd, L, dtau, nsub);
       if (nc > 0 && !imp) contact_direction(b, W, dd, L, da0);
     }
   });
@@ -2458,12 +2545,18 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
         if (r0 >= 0) {
           const int r1 = (int)cg[4 * g + 1];
           double s2[4] = {0., 0., 0., 0.};
+#pragma unroll 4
           for (int r = r0; r < r1; ++r) {
             const double* Rr = Rm + (int64_t)r * ldR;
             const double rj = jin ? Rr[cj] : 0.;
             const double hr = ch[r];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) s2[q] += Rr[ci + q] * hr * rj;
+            // rows are 16-B aligned (ldR even) and ci is a multiple of 4 (blk 2: L even)
+            const double2 a01 = *reinterpret_cast<const double2*>(Rr + ci);
+            const double2 a23 = *reinterpret_cast<const double2*>(Rr + ci + 2);
+            s2[0] += a01.x * hr * rj;
+            s2[1] += a01.y * hr * rj;
+            s2[2] += a23.x * hr * rj;
+            s2[3] += a23.y * hr * rj;
           }
           const double wt = C.weight();
 #pragma unroll
