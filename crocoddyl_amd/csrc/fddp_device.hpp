@@ -42,13 +42,14 @@ static_assert(sizeof(ElemState) % 8 == 0, "ElemState alignment");
 
 __host__ __device__ inline int64_t pad2(int64_t v) { return (v + 1) & ~int64_t(1); }
 
-// A pointer known to address LDS, re-typed through the LDS address space: accesses
-// through it compile to ds_* instructions even where the compiler cannot trace it
-// back to the kernel's __shared__ array (a pointer that is LDS on one path and
-// global on another is otherwise accessed with flat instructions).
+// A pointer known to address LDS: the assumption lets the address-space inference
+// compile accesses through it to ds_* instructions even where the compiler cannot
+// trace it back to the kernel's __shared__ array (a pointer that is LDS on one path
+// and global on another is otherwise accessed with flat instructions).
 template <class T>
 __device__ __forceinline__ T* lds_ptr(T* p) {
-  return (T*)((__attribute__((address_space(3))) T*)p);
+  __builtin_assume(__builtin_amdgcn_is_shared((const __attribute__((address_space(0))) void*)(p)));
+  return p;
 }
 
 // fddp_boxqp_params on the device (BoxQP, box-qp.hpp:92-93)

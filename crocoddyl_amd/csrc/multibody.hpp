@@ -392,6 +392,11 @@ struct DevExec {
     }
   }
   __device__ void sync() const { __syncthreads(); }
+  // an LDS pointer re-typed through the LDS address space (fddp_device.hpp lds_ptr)
+  template <class T>
+  __device__ __forceinline__ T* lds(T* p) const {
+    return lds_ptr(p);
+  }
 };
 struct HostExec {
   int nt;
@@ -404,6 +409,10 @@ struct HostExec {
     for (int l = 0; l < 64 && l < nt; ++l) f(l);
   }
   void sync() const {}
+  template <class T>
+  T* lds(T* p) const {
+    return p;
+  }
 };
 
 // Gauss-Jordan on the column-major nr x nc matrix A (ld nr) without pivoting
@@ -1552,6 +1561,8 @@ MB_HD inline int64_t calc_work_doubles(int nj, int nc = 0) {
 template <class X>
 MB_HD inline double knot_calc_x(const X& ex, const double* P, int nx, const double* x, const double* u, bool use_u,
                                 double* xnext, double* w) {
+  w = ex.lds(w);  // the work area and the parameter block live in LDS
+  P = ex.lds(P);
   const Blk b = parse(P);
   const bool imp = b.impulse;  // impulse: [M | Jc^T] only, z = v
   const int nj = b.nj, nq = b.nq, nc = b.nc, nu = nj - b.nun, ncol = imp ? nj + nc : nj + nc + 1;
@@ -2139,6 +2150,8 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
                                    bool use_u, double* w, double* Fx, double* Fu, double* Lxx, double* Lxu,
                                    double* Luu, double* Lx, double* Lu, double* xnext_out = nullptr,
                                    double* cost_out = nullptr) {
+  w = ex.lds(w);  // the work area and the parameter block live in LDS
+  P = ex.lds(P);
   const Blk b = parse(P);
   const bool imp = b.impulse;  // ActionModelImpulseFwdDynamics (impulse-fwddyn.hxx:53-127)
   const int nj = b.nj, nq = b.nq, n = 2 * nj, L = 2 * nj, nc = b.nc, nu = nj - b.nun;
@@ -2307,7 +2320,7 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
   // free-flyer Euler step's Jexp6 and Ad(exp6(dq)^-1) (dq = v dt + a dt^2)
   // per-body velocity-product maps (in the dtau area, free until the dtau phase), then
   // their subtree sums (in the da area, free until the da phase)
-  double* nsub = imp ? nullptr : da;
+  double* nsub = da;  // (unused by impulse knots)
   if (!imp) {
     ex.run([&](int lane) {
       if (lane < nj) body_nh_lane(b, W, lane, dtau);
@@ -2334,7 +2347,7 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
   // tangent directions: dtau/dx (impulse: q only) and da0/dx
   ex.run([&](int lane) {
     for (int dd = lane; dd < (imp ? nj : L); dd += ex.nt) {
-      dtau_direction(b, W, qp, dd, L, dtau, nsub);
+      dtau_direction(b, W, qp, dd, L, dtau, imp ? nullptr : nsub);
       if (nc > 0 && !imp) contact_direction(b, W, dd, L, da0);
     }
   });

@@ -38,6 +38,10 @@ struct StampExec {
     __syncthreads();
     mark();
   }
+  template <class T>
+  __device__ __forceinline__ T* lds(T* p) const {
+    return fddp::lds_ptr(p);
+  }
   __device__ __forceinline__ void mark() const {
     if (threadIdx.x == 0) {
       unsigned long long i = st[0]++;
