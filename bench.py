@@ -54,8 +54,6 @@ def cpu_baseline(cfg, T, seed, target_s=12.0, box=False):
     native build of the multibody oracle crashes on some host CPUs under gcc
     11) the in-tree -march=x86-64-v3 build; the sample string says which."""
     import subprocess
-    if synthetic_kind(cfg).startswith("gait"):
-        return {"error": "the C++ port (oracle/) does not restate free-flyer roots yet: no CPU baseline for " + cfg}
     errs = []
     for arch in ("native", "x86-64-v3"):
         cmd = [sys.executable, os.path.abspath(__file__), "--cpu-baseline-child", cfg, str(T), str(seed),
@@ -108,6 +106,12 @@ def _cpu_baseline_child(cfg, T, seed, target_s, box, arch):
             o.set_params(p)
         if synthetic.CONFIGS[cfg][0] == "multibody_contact":  # as the GPU run: warm start at x0
             o.set_candidate(np.repeat(S["x0s"][:, None, :], T + 1, axis=1), None, False)
+        elif synthetic.CONFIGS[cfg][0].startswith("gait"):  # as the GPU run: default state, quasi-static us
+            xs_w, us_w = synthetic.gait_warm_start(cfg, S["running"], S["x0s"][0])
+            us = np.zeros((d.B, d.T, d.nu_max))
+            for t, u in enumerate(us_w):
+                us[:, t, :u.size] = u
+            o.set_candidate(np.repeat(np.asarray(xs_w)[None], d.B, axis=0), us, False)
         else:
             o.set_candidate(None, None, False)
         o.solve(maxiter=2)
@@ -119,6 +123,12 @@ def _cpu_baseline_child(cfg, T, seed, target_s, box, arch):
             it += sum(x.n_iter_run for x in r)
         return it, time.perf_counter() - t0
 
+    cpu_model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            cpu_model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), "")
+    except OSError:
+        pass
     it, dt = run(threads, 1)
     steps = 4
     Bs = int(max(threads, min(1024, target_s * (it / max(dt, 1e-9)) / steps)))
@@ -127,7 +137,8 @@ def _cpu_baseline_child(cfg, T, seed, target_s, box, arch):
     print(json.dumps({"value": it / dt, "unit": "FDDP iterations/s", "cores": threads, "kind": "port",
                       "sample": f"{cfg} T={T}: {Bs} elements x {steps} warm-started solve(maxiter={2 if box else 1}) "
                                 f"({it} element-iterations in {dt:.1f} s); oracle/fddp_oracle.cpp {flags} -fopenmp, "
-                                f"OpenMP over elements{', SolverBoxFDDP |u| <= 1' if box else ''}"}), flush=True)
+                                f"OpenMP over elements ({threads} threads of {os.cpu_count()} host CPUs, {cpu_model})"
+                                f"{', SolverBoxFDDP |u| <= 1' if box else ''}"}), flush=True)
 
 
 def load_pmc(cfg):

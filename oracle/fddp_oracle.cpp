@@ -34,6 +34,7 @@
 #endif
 
 #include "../include/fddp_hip.h"
+#include "floating_oracle.hpp"
 #include "multibody_oracle.hpp"
 
 namespace oracle {
@@ -260,7 +261,14 @@ static void calc(const Model& m, Data& d, const double* x, const double* u_in) {
       break;
     }
     case FDDP_KNOT_EULER_FREEFWD:     // euler.hxx:41-80 around free-fwddyn.hxx:44-79 (multibody_oracle.hpp)
-    case FDDP_KNOT_EULER_CONTACTFWD: {  // ... or contact-fwddyn.hxx:59-104
+    case FDDP_KNOT_EULER_CONTACTFWD:  // ... or contact-fwddyn.hxx:59-104
+    case FDDP_KNOT_IMPULSEFWD: {      // impulse-fwddyn.hxx:53-86
+      if (m.nx != m.ndx || m.kind == FDDP_KNOT_IMPULSEFWD) {  // free-flyer root / impulses (floating_oracle.hpp)
+        fbo::Knot k;
+        k.parse(m.p);
+        k.calc(x, u, d.xnext.data(), &d.cost);
+        break;
+      }
       mbo::Knot k;
       k.parse(m.p);
       k.calc(x, u, d.xnext.data(), &d.cost);
@@ -344,7 +352,15 @@ static void calcDiff(const Model& m, Data& d, const double* x, const double* u_i
       break;
     }
     case FDDP_KNOT_EULER_FREEFWD:     // euler.hxx:83-131 around free-fwddyn.hxx:82-118 (multibody_oracle.hpp)
-    case FDDP_KNOT_EULER_CONTACTFWD: {  // ... or contact-fwddyn.hxx:107-160
+    case FDDP_KNOT_EULER_CONTACTFWD:  // ... or contact-fwddyn.hxx:107-160
+    case FDDP_KNOT_IMPULSEFWD: {      // impulse-fwddyn.hxx:89-127
+      if (m.nx != m.ndx || m.kind == FDDP_KNOT_IMPULSEFWD) {
+        fbo::Knot k;
+        k.parse(m.p);
+        k.calc_diff(x, u, m.nu, d.Fx.a.data(), d.Fu.a.data(), d.Lxx.a.data(), d.Lxu.a.data(), d.Luu.a.data(),
+                    d.Lx.data(), d.Lu.data());
+        break;
+      }
       mbo::Knot k;
       k.parse(m.p);
       k.calc_diff(x, u, m.nu, d.Fx.a.data(), d.Fu.a.data(), d.Lxx.a.data(), d.Lxu.a.data(), d.Luu.a.data(),
@@ -364,6 +380,17 @@ struct Problem {
   std::vector<Data> datas;
   double cost = 0.;
   int omp_knots = 0;  // reference WITH_MULTITHREADING
+  // StateMultibody on SE(3) x R^n when nx != ndx (multibody.hxx:54-91), else StateVector
+  fbo::State st{0, 0, false};
+  bool manifold() const { return nx != ndx; }
+  void diff(const double* x0, const double* x1, double* out) const {  // state->diff(x0, x1)
+    if (manifold()) return st.diff(x0, x1, out);
+    for (int i = 0; i < ndx; ++i) out[i] = x1[i] - x0[i];
+  }
+  void integrate(const double* x, const double* dx, double* out) const {  // state->integrate(x, dx)
+    if (manifold()) return st.integrate(x, dx, out);
+    for (int i = 0; i < nx; ++i) out[i] = x[i] + dx[i];
+  }
 
   // shooting.hxx:133-161
   double calc(const std::vector<Vec>& xs, const std::vector<Vec>& us) {
@@ -396,6 +423,8 @@ struct Problem {
     return cost;
   }
 };
+
+constexpr int kMaxN = 256;  // largest ndx the backward's column accumulators hold
 
 struct TraceRec {
   double cost, stop, d0, d1, xreg, ureg, steplength, is_feasible;
@@ -670,6 +699,8 @@ struct Solver {
     const int T = P->T, nx = P->nx, nu = P->nu_max;
     for (int t = 0; t <= T; ++t)
       for (int i = 0; i < nx; ++i) xs[t][i] = xs_warm ? xs_warm[(size_t)t * nx + i] : 0.;
+    if (!xs_warm && P->manifold())  // state->zero(): the neutral configuration
+      for (int t = 0; t <= T; ++t) xs[t][6] = 1.;
     for (int t = 0; t < T; ++t)
       for (int i = 0; i < nu; ++i) us[t][i] = us_warm ? us_warm[(size_t)t * nu + i] : 0.;
     is_feasible = feasible;
@@ -686,9 +717,9 @@ struct Solver {
     cost = P->calcDiff(xs, us);
     const int T = P->T, ndx = P->ndx;
     if (!is_feasible) {
-      for (int i = 0; i < ndx; ++i) fs[0][i] = P->x0[i] - xs[0][i];  // diff(xs[0], x0)
-      for (int t = 0; t < T; ++t)
-        for (int i = 0; i < ndx; ++i) fs[t + 1][i] = P->datas[t].xnext[i] - xs[t + 1][i];
+      P->diff(xs[0].data(), P->x0.data(), fs[0].data());  // diff(xs[0], x0)
+      for (int t = 0; t < T; ++t) P->diff(xs[t + 1].data(), P->datas[t].xnext.data(), fs[t + 1].data());
+      (void)ndx;
     } else if (!was_feasible) {
       for (auto& f : fs) std::fill(f.begin(), f.end(), 0.);
     }
@@ -798,13 +829,18 @@ struct Solver {
       // FxTVxx = Fx^T Vxx'
       for (int j = 0; j < n; ++j)
         for (int i = 0; i < n; ++i) FxTVxx(i, j) = dot(&d.Fx.a[(size_t)i * n], &Vxx_p.a[(size_t)j * n], n);
-      // Qxx += FxTVxx Fx
-      for (int j = 0; j < n; ++j)
-        for (int i = 0; i < n; ++i) {
-          double s = 0.;
-          for (int kk = 0; kk < n; ++kk) s += FxTVxx(i, kk) * d.Fx(kk, j);
-          Qxx[t](i, j) += s;
+      // Qxx += FxTVxx Fx (column axpys: the same summation order per entry)
+      for (int j = 0; j < n; ++j) {
+        double* q = &Qxx[t].a[(size_t)j * n];
+        double acc[kMaxN];
+        for (int i = 0; i < n; ++i) acc[i] = 0.;
+        for (int kk = 0; kk < n; ++kk) {
+          const double f = d.Fx(kk, j);
+          const double* c = &FxTVxx.a[(size_t)kk * n];
+          for (int i = 0; i < n; ++i) acc[i] += c[i] * f;
         }
+        for (int i = 0; i < n; ++i) q[i] += acc[i];
+      }
       // Qx += Fx^T Vx'
       {
         Vec tmp(n);
@@ -817,18 +853,26 @@ struct Solver {
         Qu[t] = d.Lu;
         for (int j = 0; j < n; ++j)
           for (int i = 0; i < nu; ++i) FuTVxx[t](i, j) = dot(&d.Fu.a[(size_t)i * n], &Vxx_p.a[(size_t)j * n], n);
-        for (int j = 0; j < nu; ++j)
-          for (int i = 0; i < n; ++i) {
-            double s = 0.;
-            for (int kk = 0; kk < n; ++kk) s += FxTVxx(i, kk) * d.Fu(kk, j);
-            Qxu[t](i, j) += s;
+        for (int j = 0; j < nu; ++j) {
+          double acc[kMaxN];
+          for (int i = 0; i < n; ++i) acc[i] = 0.;
+          for (int kk = 0; kk < n; ++kk) {
+            const double f = d.Fu(kk, j);
+            const double* c = &FxTVxx.a[(size_t)kk * n];
+            for (int i = 0; i < n; ++i) acc[i] += c[i] * f;
           }
-        for (int j = 0; j < nu; ++j)
-          for (int i = 0; i < nu; ++i) {
-            double s = 0.;
-            for (int kk = 0; kk < n; ++kk) s += FuTVxx[t](i, kk) * d.Fu(kk, j);
-            Quu[t](i, j) += s;
+          for (int i = 0; i < n; ++i) Qxu[t](i, j) += acc[i];
+        }
+        for (int j = 0; j < nu; ++j) {
+          double acc[kMaxN];
+          for (int i = 0; i < nu; ++i) acc[i] = 0.;
+          for (int kk = 0; kk < n; ++kk) {
+            const double f = d.Fu(kk, j);
+            const double* c = &FuTVxx[t].a[(size_t)kk * nu];
+            for (int i = 0; i < nu; ++i) acc[i] += c[i] * f;
           }
+          for (int i = 0; i < nu; ++i) Quu[t](i, j) += acc[i];
+        }
         Vec tmp(nu);
         gemvT(d.Fu.a.data(), n, nu, Vx_p.data(), tmp.data());
         for (int i = 0; i < nu; ++i) Qu[t][i] += tmp[i];
@@ -846,12 +890,16 @@ struct Solver {
           for (int i = 0; i < n; ++i) Vx[t][i] += dot(&K[t].a[(size_t)i * nu], Quuk[t].data(), nu);
           for (int i = 0; i < n; ++i) Vx[t][i] -= 2 * dot(&K[t].a[(size_t)i * nu], Qu[t].data(), nu);
         }
-        for (int j = 0; j < n; ++j)
-          for (int i = 0; i < n; ++i) {
-            double s = 0.;
-            for (int kk = 0; kk < nu; ++kk) s += Qxu[t](i, kk) * K[t](kk, j);
-            Vxx[t](i, j) -= s;
+        for (int j = 0; j < n; ++j) {
+          double acc[kMaxN];
+          for (int i = 0; i < n; ++i) acc[i] = 0.;
+          for (int kk = 0; kk < nu; ++kk) {
+            const double f = K[t](kk, j);
+            const double* c = &Qxu[t].a[(size_t)kk * n];
+            for (int i = 0; i < n; ++i) acc[i] += c[i] * f;
           }
+          for (int i = 0; i < n; ++i) Vxx[t](i, j) -= acc[i];
+        }
       }
       // Vxx = 0.5 (Vxx + Vxx^T)
       {
@@ -882,7 +930,7 @@ struct Solver {
 
   // fddp.cpp:149-225 ; false on forward_error
   bool forwardPass(double alpha) {
-    const int T = P->T, n = P->ndx, nx = P->nx;
+    const int T = P->T, n = P->ndx;
     cost_try = 0.;
     xnext = P->x0;
     for (int t = 0; t < T; ++t) {
@@ -891,9 +939,10 @@ struct Solver {
       if (is_feasible || alpha == 1) {
         xs_try[t] = xnext;
       } else {
-        for (int i = 0; i < nx; ++i) xs_try[t][i] = xnext[i] + fs[t][i] * (alpha - 1);
+        for (int i = 0; i < n; ++i) dx[t][i] = fs[t][i] * (alpha - 1);  // integrate(xnext, fs (alpha - 1))
+        P->integrate(xnext.data(), dx[t].data(), xs_try[t].data());
       }
-      for (int i = 0; i < n; ++i) dx[t][i] = xs_try[t][i] - xs[t][i];  // diff(xs, xs_try)
+      P->diff(xs[t].data(), xs_try[t].data(), dx[t].data());  // diff(xs, xs_try)
       if (m.nu != 0) {
         for (int i = 0; i < m.nu; ++i) {
           double v = us[t][i] - k[t][i] * alpha;
@@ -918,7 +967,8 @@ struct Solver {
     if (is_feasible || alpha == 1) {
       xs_try[T] = xnext;
     } else {
-      for (int i = 0; i < nx; ++i) xs_try[T][i] = xnext[i] + fs[T][i] * (alpha - 1);
+      for (int i = 0; i < n; ++i) dx[T][i] = fs[T][i] * (alpha - 1);
+      P->integrate(xnext.data(), dx[T].data(), xs_try[T].data());
     }
     oracle::calc(m, d, xs_try[T].data(), nullptr);
     cost_try += d.cost;
@@ -936,11 +986,11 @@ struct Solver {
     dv = 0.;
     const int T = P->T, n = P->ndx;
     if (!is_feasible) {
-      for (int i = 0; i < n; ++i) dx[T][i] = xs[T][i] - xs_try[T][i];  // diff(xs_try, xs)
+      P->diff(xs_try[T].data(), xs[T].data(), dx[T].data());  // diff(xs_try, xs)
       gemv(Vxx[T].a.data(), n, n, dx[T].data(), fTVxx.data());
       dv -= dot(fs[T].data(), fTVxx.data(), n);
       for (int t = 0; t < T; ++t) {
-        for (int i = 0; i < n; ++i) dx[t][i] = xs[t][i] - xs_try[t][i];
+        P->diff(xs_try[t].data(), xs[t].data(), dx[t].data());
         gemv(Vxx[t].a.data(), n, n, dx[t].data(), fTVxx.data());
         dv -= dot(fs[t].data(), fTVxx.data(), n);
       }
@@ -1104,10 +1154,17 @@ static void bind_models(oracle_handle* h) {
 
 int oracle_create(const fddp_dims* dims, const fddp_knot_desc* knots, const double* params, int64_t n_params,
                   oracle_handle** out) {
-  if (!dims || !knots || !params || !out || dims->T < 1 || dims->B < 1 || dims->nx < 1 || dims->nx != dims->ndx) {
+  if (!dims || !knots || !params || !out || dims->T < 1 || dims->B < 1 || dims->nx < 1 || dims->ndx > kMaxN || dims->nu_max > kMaxN ||
+      (dims->nx != dims->ndx && (dims->nx != dims->ndx + 1 || dims->ndx % 2 || dims->ndx < 12))) {
     g_err = "oracle_create: invalid argument";
     return FDDP_ERR_INVALID_ARG;
   }
+  if (dims->nx != dims->ndx)
+    for (int t = 0; t <= dims->T; ++t)
+      if (knots[t].kind < FDDP_KNOT_EULER_FREEFWD || knots[t].kind > FDDP_KNOT_IMPULSEFWD) {
+        g_err = "oracle_create: free-flyer states are restated for the multibody knots only";
+        return FDDP_ERR_INVALID_ARG;
+      }
   auto* h = new oracle_handle();
   h->dims = *dims;
   h->knots.assign(knots, knots + dims->T + 1);
@@ -1122,6 +1179,7 @@ int oracle_create(const fddp_dims* dims, const fddp_knot_desc* knots, const doub
     P.ndx = dims->ndx;
     P.nu_max = dims->nu_max;
     P.x0.assign(dims->nx, 0.);
+    P.st = fbo::State{dims->nx - dims->ndx / 2, dims->ndx / 2, dims->nx != dims->ndx};
     P.models.resize(dims->T + 1);
     P.datas.resize(dims->T + 1);
     for (int t = 0; t <= dims->T; ++t) {

@@ -39,7 +39,7 @@ def lib(path=None):
         _bind(L)
         return L
     if _lib is None:
-        srcs = [os.path.join(ORACLE_DIR, f) for f in ("fddp_oracle.cpp", "multibody_oracle.hpp")]
+        srcs = [os.path.join(ORACLE_DIR, f) for f in ("fddp_oracle.cpp", "multibody_oracle.hpp", "floating_oracle.hpp", "Makefile")]
         if not os.path.exists(ORACLE_SO) or os.path.getmtime(ORACLE_SO) < max(os.path.getmtime(f) for f in srcs):
             build()
         _lib = C.CDLL(ORACLE_SO)
