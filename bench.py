@@ -34,6 +34,30 @@ def backward_flops_per_knot(n, m):
     return 4 * n ** 3 + 6 * n * n * m + 4 * n * m * m + m ** 3 / 3 + 6 * n * n + 6 * n * m + 4 * m * m
 
 
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E, MI355X_MICROARCH.md
+
+
+def rollout_bytes_per_knot_trial(nx, n, m, psz):
+    """One knot of one line-search trial (fddp.cpp:149-225): reads xs, us, fs, Vxx fs,
+    K (m x n), k and the knot's parameter block (psz doubles); writes xs_try, us_try,
+    xnext and the knot cost."""
+    return 8 * ((nx + m + 2 * n + m * n + m + psz) + (2 * nx + m + 1))
+
+
+def calc_diff_bytes_per_knot(nx, n, m, psz):
+    """One knot of calcDiff (euler.hxx:83-131 + the DAM): reads x, u and the parameter
+    block; writes Fx, Fu, Lxx, Lxu, Luu, Lx, Lu, xnext and the knot cost."""
+    return 8 * ((nx + m + psz) + (2 * n * n + 2 * n * m + m * m + n + m + nx + 1))
+
+
+def mean_param_doubles(problem):
+    """Mean parameter-block size over the knots (multibody blocks carry it in their
+    header; 0 for the fixed-size kinds, whose blocks are the derivatives themselves)."""
+    knots, pool = problem._packed()
+    sizes = [int(pool[off + 3]) if kind in (4, 5, 6) else 0 for kind, _, off, _ in knots]
+    return float(np.mean(sizes))
+
+
 def backward_bytes_per_knot(n, m):
     """reads Fx, Lxx, Fu, Lxu, Luu, Lx, fs, Lu; writes K, k, Qu, Quuk, Vx, Vxx·fs."""
     return 8 * ((2 * n * n + 2 * n * m + m * m + 2 * n + m) + (m * n + 2 * m + 2 * n + m))
@@ -94,10 +118,10 @@ def _cpu_baseline_child(cfg, T, seed, target_s, box, arch):
 
     from crocoddyl_amd import _abi, synthetic
 
-    def run(Bs, steps):
+    def run(Bs, steps, mode=2):
         S = helpers.setup(cfg, T=T, B=Bs, seed=seed)
         d = S["dims"]
-        o = oracle_lib.Oracle(S["dims"], S["knots"], S["pool"], S["x0s"], threads=threads, mode=2)
+        o = oracle_lib.Oracle(S["dims"], S["knots"], S["pool"], S["x0s"], threads=threads, mode=mode)
         if box:
             o.set_solver_kind(_abi.SOLVER_BOXFDDP)
             o.set_control_limits(np.full((d.B, d.T, d.nu_max), -BOX_LIMIT), np.full((d.B, d.T, d.nu_max), BOX_LIMIT))
@@ -129,15 +153,26 @@ def _cpu_baseline_child(cfg, T, seed, target_s, box, arch):
             cpu_model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), "")
     except OSError:
         pass
+    # batch-parallel (OpenMP over elements): the main figure
     it, dt = run(threads, 1)
     steps = 4
     Bs = int(max(threads, min(1024, target_s * (it / max(dt, 1e-9)) / steps)))
     Bs = max(threads, (Bs // threads) * threads)
     it, dt = run(Bs, steps)
-    print(json.dumps({"value": it / dt, "unit": "FDDP iterations/s", "cores": threads, "kind": "port",
-                      "sample": f"{cfg} T={T}: {Bs} elements x {steps} warm-started solve(maxiter={2 if box else 1}) "
-                                f"({it} element-iterations in {dt:.1f} s); oracle/fddp_oracle.cpp {flags} -fopenmp, "
-                                f"OpenMP over elements ({threads} threads of {os.cpu_count()} host CPUs, {cpu_model})"
+    # reference-faithful (WITH_MULTITHREADING: OpenMP over knots inside calc / calcDiff,
+    # shooting.hxx:143-145,176-178; elements one after another) on a third of the budget
+    it1, dt1 = run(1, 1, mode=1)
+    B1 = int(max(1, min(256, target_s / 3 * (it1 / max(dt1, 1e-9)) / steps)))
+    it1, dt1 = run(B1, steps, mode=1)
+    v2, v1 = it / dt, it1 / dt1
+    print(json.dumps({"value": max(v1, v2), "unit": "FDDP iterations/s", "cores": threads, "kind": "port",
+                      "host_cpus": os.cpu_count(), "cpu_model": cpu_model,
+                      "modes": {"batch_parallel": round(v2, 2), "knot_parallel": round(v1, 2)},
+                      "sample": f"{cfg} T={T}, warm-started solve(maxiter={2 if box else 1}) per element: "
+                                f"batch-parallel {Bs} elements x {steps} steps ({it} element-iterations in {dt:.1f} s), "
+                                f"knot-parallel {B1} elements x {steps} steps ({it1} in {dt1:.1f} s); value = the faster "
+                                f"mode. oracle/fddp_oracle.cpp {flags} -fopenmp, {threads} threads (the box's CPU share) "
+                                f"of {os.cpu_count()} host CPUs ({cpu_model})"
                                 f"{', SolverBoxFDDP |u| <= 1' if box else ''}"}), flush=True)
 
 
@@ -146,6 +181,42 @@ def load_pmc(cfg):
         return json.load(open(os.path.join(ROOT, "profiles", "pmc_backward.json"))).get(cfg)
     except Exception:
         return None
+
+
+def make_shard_solver(config, B, rank, dev, box=False, T=None):
+    """Rank `rank`'s shard of the job: B problems of `config` (seeded per rank, so
+    every rank owns distinct problems) on GPU `dev`, warm-started and solved once
+    (solve(maxiter=5)) as the timed loop expects."""
+    from crocoddyl_amd import ShootingProblem, SolverBoxFDDP, SolverFDDP, synthetic
+    kind = synthetic.CONFIGS[config][0]
+    T = synthetic.CONFIGS[config][3] if T is None else T
+    seed = synthetic.seed_of(config) + 1000 * rank
+    x0s, running, terminal = synthetic.build(config, T=T, B=B, seed=seed)
+    if box:
+        for md in set(running):
+            md.u_lb = np.full(md.nu, -BOX_LIMIT)
+            md.u_ub = np.full(md.nu, BOX_LIMIT)
+    problem = ShootingProblem(x0s, running, terminal, device=dev)
+    solver = SolverBoxFDDP(problem) if box else SolverFDDP(problem)
+    if kind in ("gait_biped", "gait_quadruped"):
+        # the reference benchmark's warm start (bipedal_walk_optctrl.py:29-32): the
+        # default state at every knot, quasi-static controls
+        xs_w, us_w = synthetic.gait_warm_start(config, running, x0s[0])
+        solver.solve(xs_w, us_w, maxiter=5)
+    elif kind == "multibody_contact":
+        # warm start at x0: the default (state.zero(), the stretched arm) is a
+        # singular configuration of the gripper contact (rank-deficient Jc)
+        solver.solve(np.repeat(x0s[:, None, :], T + 1, axis=1), [], maxiter=5)
+    else:
+        solver.solve(maxiter=5)  # converge once from a cold start
+    return solver
+
+
+def mpc_step(solver, mpc_iters):
+    """One receding-horizon MPC solve of every element: device shift, then a
+    warm-started solve(maxiter=mpc_iters, regInit=0.1)."""
+    solver.mpcShift()
+    solver.solve_from_candidate(maxiter=mpc_iters, isFeasible=False, regInit=0.1)
 
 
 def main():
@@ -168,7 +239,7 @@ def main():
 
     import torch
 
-    from crocoddyl_amd import ShootingProblem, SolverBoxFDDP, SolverFDDP, synthetic
+    from crocoddyl_amd import synthetic
     from crocoddyl_amd import dist as cdist
 
     ws, rank, local_rank = cdist.world()
@@ -177,36 +248,16 @@ def main():
 
     kind, d1, nu, T, B0, dt = synthetic.CONFIGS[args.config]
     B = args.batch or B0
-    seed = synthetic.seed_of(args.config) + 1000 * rank  # each rank owns distinct problems
-    x0s, running, terminal = synthetic.build(args.config, B=B, seed=seed)
-    if box:
-        for md in set(running):
-            md.u_lb = np.full(md.nu, -BOX_LIMIT)
-            md.u_ub = np.full(md.nu, BOX_LIMIT)
-    problem = ShootingProblem(x0s, running, terminal, device=dev)
-    solver = SolverBoxFDDP(problem) if box else SolverFDDP(problem)
+    solver = make_shard_solver(args.config, B, rank, dev, box)
+    problem = solver.problem
     n, m, nx = problem.ndx, problem.nu_max, problem.nx
     mpc_iters = 2 if box else 1
 
-    if kind in ("gait_biped", "gait_quadruped"):
-        # the reference benchmark's warm start (bipedal_walk_optctrl.py:29-32): the
-        # default state at every knot, quasi-static controls
-        xs_w, us_w = synthetic.gait_warm_start(args.config, running, x0s[0])
-        solver.solve(xs_w, us_w, maxiter=5)
-    elif kind == "multibody_contact":
-        # warm start at x0: the default (state.zero(), the stretched arm) is a
-        # singular configuration of the gripper contact (rank-deficient Jc)
-        solver.solve(np.repeat(x0s[:, None, :], T + 1, axis=1), [], maxiter=5)
-    else:
-        solver.solve(maxiter=5)  # converge once from a cold start
-
     def step():  # one receding-horizon MPC solve, all elements
-        solver.mpcShift()
-        solver.solve_from_candidate(maxiter=mpc_iters, isFeasible=False, regInit=0.1)
+        mpc_step(solver, mpc_iters)
 
     for _ in range(args.warmup):
         step()
-    xs_local = torch.empty((B, T + 1, nx), dtype=torch.float64, device=f"cuda:{dev}")
     if ws > 1:
         torch.distributed.barrier()
     solver.synchronize()
@@ -218,9 +269,9 @@ def main():
     for _ in range(args.steps):
         step()
         iters += int(np.sum(solver.n_iter_run))
-    solver.xs_device(xs_local.data_ptr())  # the solved trajectories, on device
-    solver.synchronize()
-    xs_all = cdist.gather_rows(xs_local)  # the single collective (RCCL all-gather)
+    # the solved trajectories and per-element results, device to device, then the
+    # all-gathers (RCCL over xGMI): the only collectives of the batched solve
+    xs_all, us_all, res_all = cdist.gather_solution(solver, f"cuda:{dev}")
     torch.cuda.synchronize(dev)
     if ws > 1:
         torch.distributed.barrier()
@@ -231,7 +282,7 @@ def main():
     sl = np.atleast_1d(np.asarray(solver.stepLength, float))
     trials = np.round(-np.log2(np.clip(sl, 2.0 ** -12, 1.0))) + 1
     elapsed, total_iters = cdist.job_time_and_work(elapsed, iters, f"cuda:{dev}")
-    assert xs_all.shape[0] == ws * B
+    assert xs_all.shape[0] == us_all.shape[0] == res_all.shape[0] == ws * B
 
     if rank == 0:
         value = total_iters / elapsed
@@ -241,12 +292,38 @@ def main():
         Y = backward_bytes_per_knot(n, m) * B * T
         achieved = F / avg_bwd_s / 1e12
         pmc = load_pmc(args.config)
-        roof = {"kernel": "backward Riccati sweep (bwd_mfma.hpp)", "bound": "mfma", "achieved": round(achieved, 3),
-                "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / FP64_PEAK_TFLOPS, 4),
-                "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
-                "algorithmic_flops_per_launch": F, "algorithmic_bytes_per_launch": Y,
-                "achieved_algorithmic_GBps": round(Y / avg_bwd_s / 1e9, 1),
-                "avg_launch_ms": round(avg_bwd_s * 1e3, 3), "timer": "HIP events on the solver stream"}
+        roof_bwd = {"kernel": "backward Riccati sweep (bwd_mfma.hpp)", "bound": "mfma", "achieved": round(achieved, 3),
+                    "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / FP64_PEAK_TFLOPS, 4),
+                    "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
+                    "algorithmic_flops_per_launch": F, "algorithmic_bytes_per_launch": Y,
+                    "achieved_algorithmic_GBps": round(Y / avg_bwd_s / 1e9, 1),
+                    "avg_launch_ms": round(avg_bwd_s * 1e3, 3), "timer": "HIP events on the solver stream"}
+        # the knot kernels: algorithmic HBM bytes (they are latency-bound recursions, far
+        # from either roof; the fraction says how far)
+        psz = mean_param_doubles(problem)
+        rooflines = {"backward": (bwd_ms, roof_bwd)}
+        fw_ms, fw_n = timing["forward"]
+        if fw_n:
+            kt = float(np.sum(trials)) * (T + 1)  # knot-trials of one line search (last step's trials)
+            Yf = rollout_bytes_per_knot_trial(nx, n, m, psz) * kt
+            a = Yf / (fw_ms / fw_n / 1e3) / 1e9
+            rooflines["forward"] = (fw_ms, {
+                "kernel": "line-search rollout (forward_kernel + ls_select_kernel, knot calc per trial)",
+                "bound": "hbm", "achieved": round(a, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                "frac": round(a / HBM_PEAK_GBPS, 5), "traffic": None, "algorithmic_bytes_per_launch": int(Yf),
+                "knot_trials_per_launch": int(kt), "avg_launch_ms": round(fw_ms / fw_n, 3),
+                "timer": "HIP events on the solver stream"})
+        cd_ms, cd_n = timing["calcDiff"]
+        if cd_n:
+            Yc = calc_diff_bytes_per_knot(nx, n, m, psz) * B * (T + 1)
+            a = Yc / (cd_ms / cd_n / 1e3) / 1e9
+            rooflines["calcDiff"] = (cd_ms, {
+                "kernel": "knot-parallel calcDiff (mb_knot_kernel / calc_diff_kernel)", "bound": "hbm",
+                "achieved": round(a, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(a / HBM_PEAK_GBPS, 5),
+                "traffic": None, "algorithmic_bytes_per_launch": int(Yc), "avg_launch_ms": round(cd_ms / cd_n, 3),
+                "timer": "HIP events on the solver stream"})
+        dominant = max(rooflines, key=lambda k: rooflines[k][0])
+        roof = dict(rooflines[dominant][1], dominant_of=sorted(rooflines))
         cpu = None
         if ws == 1 and not args.no_cpu_baseline:
             try:
@@ -284,6 +361,7 @@ def main():
             "line_search_trials_last_step": {"mean": round(float(trials.mean()), 2), "max": int(trials.max()),
                                              "hist": np.bincount(trials.astype(int), minlength=11)[1:].tolist()},
             "roofline": roof,
+            "rooflines": {k: v[1] for k, v in rooflines.items()},
             "cpu_baseline": cpu,
         }
         if cpu and "value" in cpu:

@@ -12,7 +12,7 @@ problem written for ``crocoddyl`` drops in:
     solver.solve()
 """
 from ._lib import FDDPError, LIB_PATH  # noqa: F401
-from .models import (ActionData, ActionModelAbstract, ActionModelLQR, ActionModelUnicycle,  # noqa: F401
+from .models import (ActionData, ActionDataAbstract, ActionModelAbstract, ActionModelLQR, ActionModelUnicycle,  # noqa: F401
                      DifferentialActionModelLQR, IntegratedActionModelEuler, StateVector)
 from .problem import ShootingProblem, SolverBoxFDDP, SolverFDDP, pack_problem  # noqa: F401
 from .boxqp import BoxQP, BoxQPSolution  # noqa: F401

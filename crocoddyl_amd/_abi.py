@@ -18,6 +18,7 @@ KNOT_LQR, KNOT_UNICYCLE, KNOT_EULER_DIFFLQR, KNOT_EULER_FREEFWD, KNOT_EULER_CONT
 PARAM_HEADER = 4
 
 Q_FX, Q_FU, Q_LXX, Q_LXU, Q_LUU, Q_LX, Q_LU, Q_XNEXT, Q_FS, Q_K, Q_KV = range(11)
+Q_COST = 19
 Q_VXX, Q_VX, Q_QXX, Q_QXU, Q_QUU, Q_QX, Q_QU = range(11, 18)
 Q_QUU_INV = 18
 

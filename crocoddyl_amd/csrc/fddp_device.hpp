@@ -94,6 +94,13 @@ struct Dev {
   BoxQPCfg boxcfg;                 // qp_(nu, 100, 0.1, 1e-5, 0.) (box-fddp.cpp:16)
   int64_t mbw;                     // LDS doubles of the multibody calc scratch (0: no multibody knots)
   int64_t mbd;                     // LDS doubles of the multibody calcDiff work area (its parameter block follows)
+  // parallel line search (generic trials): npar trials of one element run in
+  // npar workgroups; trial slot 0 writes the other trajectory buffer, slots
+  // 1..npar-1 their own copies (same [b][t] layout), accepted ones are copied back
+  int npar;                        // trials per element evaluated together (1: serial line search)
+  double *pxs, *pus, *pxnext, *pkcost, *pdvp;  // slots 1..npar-1: [slot][B][T+1|T][...]
+  double* ptrial;                  // [B][npar][4]: ok, cost_try, dv, -
+  int* ls_done;                    // [B] line search decided in an earlier group of this iteration
   __device__ bool box_knot(int b, int t) const { return box && haslim && haslim[(int64_t)b * T + t]; }
 
   __device__ __host__ int64_t knot(int b, int t) const { return (int64_t)b * (T + 1) + t; }

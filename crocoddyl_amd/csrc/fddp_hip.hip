@@ -286,6 +286,8 @@ int check_knots(const fddp_dims& d, const fddp_knot_desc* knots, const double* p
 struct fddp_handle_s {
   fddp_dims dims;
   int device = 0;
+  int npar_env = 0;    // CROCODDYL_AMD_LS_PAR (0: chosen per problem)
+  int npar_alloc = 1;  // trial slots allocated for the parallel line search
   hipStream_t stream = nullptr;
   std::vector<fddp_knot_desc> knots;
   int64_t n_params = 0;
@@ -525,9 +527,42 @@ template <int NTL, int MTL>
 int setup_bwd_mfma_nw(fddp_handle* h, int nw) {
   return nw == 4 ? setup_bwd_mfma<NTL, MTL, 4>(h) : setup_bwd_mfma<NTL, MTL, 8>(h);
 }
+// slot buffers of the parallel line search (generic trials), allocated on first use
+static int ensure_par_slots(fddp_handle* h) {
+  Dev& D = h->D;
+  if (D.npar <= h->npar_alloc) return FDDP_OK;  // (buffers of a smaller npar stay until fddp_destroy)
+  const int64_t B = D.B, K1 = D.T + 1, K0 = D.T, q = D.npar - 1;
+  int rc;
+  double* done = nullptr;
+  if ((rc = dalloc(h, &D.pxs, q * B * K1 * D.sX)) || (rc = dalloc(h, &D.pus, q * B * K0 * D.sM)) ||
+      (rc = dalloc(h, &D.pxnext, q * B * K0 * D.sX)) || (rc = dalloc(h, &D.pkcost, q * B * K1)) ||
+      (rc = dalloc(h, &D.pdvp, q * B * K1)) || (rc = dalloc(h, &D.ptrial, B * D.npar * 4)) ||
+      (rc = dalloc(h, &done, (B + 1) / 2)))
+    return rc;
+  D.ls_done = (int*)done;
+  h->npar_alloc = D.npar;
+  return FDDP_OK;
+}
+
 int launch_forward(fddp_handle* h, int mode, double alpha, int* count) {
   Timed tm(h, 3);
   const Dev& D = h->D;
+  if (!h->fast && mode == 0 && D.npar > 1) {
+    // the line search in groups of npar trials evaluated together; every group
+    // is launched (decided elements exit at once), so there is no host round trip
+    int rc;
+    if ((rc = ensure_par_slots(h))) return rc;
+    const int na = h->prm.n_alphas, G = (na + D.npar - 1) / D.npar;
+    for (int g = 0; g < G; ++g) {
+      hipLaunchKernelGGL((forward_kernel<kNT, false>), dim3(D.B, D.npar), dim3(kNT), h->fwd_smem, h->stream, D,
+                         to_prm(h->prm), 2, 1., nullptr, h->pcap, g);
+      LAUNCH_CHECK();
+      hipLaunchKernelGGL((ls_select_kernel<kNT>), dim3(D.B), dim3(kNT), 0, h->stream, D, to_prm(h->prm), g,
+                         g == G - 1 ? 1 : 0, count);
+      LAUNCH_CHECK();
+    }
+    return FDDP_OK;
+  }
   if (h->fast)
     hipLaunchKernelGGL((forward_kernel<kNT, true>), dim3(D.B), dim3(kNT), h->fwd_fast_smem, h->stream, D,
                        to_prm(h->prm), mode, alpha, count, h->pcap);
@@ -661,6 +696,10 @@ int apply_knots(fddp_handle* h, const fddp_knot_desc* knots, const double* param
     h->all_mb = true;
     for (int t = 0; t <= d.T; ++t) h->all_mb = h->all_mb && is_mb_kind(knots[t].kind);
     D.mbw = h->has_mb ? pad2(fddp::mb::calc_work_doubles(mb_nj, mb_nc)) : 0;
+    // parallel line-search trials: they pay on the large trees (C5 Talos, nv = 38:
+    // forward -12 %), where one rollout keeps a CU busy longest; on small ones (C4
+    // Solo12, nv = 18) the extra trials cost more than the shorter chains save
+    D.npar = h->npar_env ? h->npar_env : (h->has_mb && mb_nj >= 24 ? 4 : 1);
     int64_t mb_pmax = 0;  // largest multibody parameter block (staged in LDS by mb_knot_kernel)
     for (int t = 0; t <= d.T; ++t)
       if (is_mb_kind(knots[t].kind)) {
@@ -819,6 +858,11 @@ int fddp_create(const fddp_dims* dims, const fddp_knot_desc* knots, const double
   D.sNN = pad2((int64_t)d.ndx * d.ndx);
   D.sNM = pad2((int64_t)d.ndx * (d.nu_max > 0 ? d.nu_max : 1));
   D.sMM = pad2((int64_t)d.nu_max * d.nu_max > 0 ? (int64_t)d.nu_max * d.nu_max : 1);
+  // line-search trials evaluated together per element on the generic (multibody)
+  // path: the same trials and the same choice as the serial search, fewer serial
+  // rollouts for the elements that backtrack (CROCODDYL_AMD_LS_PAR = 1 is serial)
+  D.npar = 1;
+  if (const char* e = std::getenv("CROCODDYL_AMD_LS_PAR")) D.npar = h->npar_env = std::max(1, std::min(16, std::atoi(e)));
   const int64_t B = d.B, K1 = (int64_t)d.T + 1, K0 = d.T;
   {  // SolverBoxFDDP's qp_(nu, 100, 0.1, 1e-5, 0.) (box-fddp.cpp:16); unused until BOXFDDP
     fddp_boxqp_params bp;
@@ -1229,6 +1273,7 @@ int fddp_get_quantity(fddp_handle* h, int which, double* out) {
     case FDDP_Q_LX: src = D.Lx; per = n; stride = D.sN; nk = D.T + 1; break;
     case FDDP_Q_LU: src = D.Lu; per = m; stride = D.sM; nk = D.T + 1; break;
     case FDDP_Q_XNEXT: cur = 1; per = D.nx; stride = D.sX; nk = D.T; break;
+    case FDDP_Q_COST: cur = 2; per = 1; stride = 1; nk = D.T + 1; break;
     case FDDP_Q_FS: src = D.fs; per = n; stride = D.sN; nk = D.T + 1; break;
     case FDDP_Q_K: src = D.K; per = m * n; stride = D.sNM; nk = D.T; break;
     case FDDP_Q_KV: src = D.k; per = m; stride = D.sM; nk = D.T; break;
@@ -1244,12 +1289,12 @@ int fddp_get_quantity(fddp_handle* h, int which, double* out) {
   }
   if (per == 0) return FDDP_OK;
   if (cur >= 0) {
-    // xnext lives in the current trajectory buffer of each element
+    // xnext / knot costs live in the current trajectory buffer of each element
     std::vector<ElemState> st;
     int rc;
     if ((rc = download_states(h, st))) return rc;
     for (int b = 0; b < D.B; ++b) {
-      const double* s = D.xnext[st[b].cur] + (int64_t)b * nk * stride;
+      const double* s = (cur == 2 ? D.kcost[st[b].cur] : D.xnext[st[b].cur]) + (int64_t)b * nk * stride;
       HIP_TRY(hipMemcpy2DAsync(out + (int64_t)b * nk * per, sizeof(double) * per, s, sizeof(double) * stride,
                                sizeof(double) * per, nk, hipMemcpyDeviceToHost, h->stream));
     }

@@ -637,25 +637,41 @@ __global__ __launch_bounds__(NT) void backward_kernel(Dev D, Prm prm, int mode) 
 // mode 0: full line search + regularisation/convergence update (solve).
 // mode 1: a single trial at `alpha` (tryStep), storing cost_try, dV and dv.
 // ---------------------------------------------------------------------------
+// Where a trial writes xs_try / us_try / xnext / knot costs / dv terms: slot 0 is the
+// other trajectory buffer (accepted by flipping cur), slots > 0 the parallel copies.
+struct TrialOut {
+  double *xs, *us, *xnext, *kcost, *dvp;
+  __device__ TrialOut(const Dev& D, int o, int slot) {
+    if (slot == 0) {
+      xs = D.xs[o], us = D.us[o], xnext = D.xnext[o], kcost = D.kcost[o], dvp = D.dvp;
+    } else {
+      const int64_t B = D.B, K1 = D.T + 1, K0 = D.T, q = slot - 1;
+      xs = D.pxs + q * B * K1 * D.sX, us = D.pus + q * B * K0 * D.sM, xnext = D.pxnext + q * B * K0 * D.sX;
+      kcost = D.pkcost + q * B * K1, dvp = D.pdvp + q * B * K1;
+    }
+  }
+};
+
 template <int NT>
 __device__ __forceinline__ bool fwd_trial(const Dev& D, int b, const ElemState& s, double alpha, double* xv, double* uv, double* xn,
                           double* red, int* flag, double& cost_try, double& dv, double* pl, int64_t pcap,
-                          const double*& cached, double* mbw, double* dxv) {
+                          const double*& cached, double* mbw, double* dxv, int slot = 0) {
   const int n = D.n, nx = D.nx, m = D.m, T = D.T, tid = threadIdx.x;
   const int c = s.cur, o = 1 - c;
+  const TrialOut out(D, o, slot);
   const bool feas = s.is_feasible != 0;
   const bool full = feas || alpha == 1.;
   const bool ff = nx != n;  // free-flyer state (dxv: 2 sN doubles of LDS)
   const double* x0 = D.x0 + (int64_t)b * D.sX;
   for (int i = tid; i < nx; i += NT) xn[i] = x0[i];
   cost_try = 0.;
-  double* dvp = D.dvp + D.knot(b, 0);
+  double* dvp = out.dvp + D.knot(b, 0);
   __syncthreads();
   for (int t = 0; t <= T; ++t) {
     const int64_t kk = D.knot(b, t);
     const double* fs = D.fs + kk * D.sN;
     const double* xs = D.xs[c] + kk * D.sX;
-    double* xt = D.xs[o] + kk * D.sX;
+    double* xt = out.xs + kk * D.sX;
     // xs_try[t] = xnext  or  integrate(xnext, fs[t] * (alpha - 1))
     double pd = 0.;
     if (!ff) {
@@ -687,7 +703,7 @@ __device__ __forceinline__ bool fwd_trial(const Dev& D, int b, const ElemState& 
       const double* us = D.us[c] + D.run(b, t) * D.sM;
       const double* K = D.K + D.run(b, t) * D.sNM;
       const double* kv = D.k + D.run(b, t) * D.sM;
-      double* ut = D.us[o] + D.run(b, t) * D.sM;
+      double* ut = out.us + D.run(b, t) * D.sM;
       // us_try = us - k * alpha - K * dx ,  dx = diff(xs, xs_try)
       for (int i = tid; i < m; i += NT) {
         double v = 0.;
@@ -709,7 +725,7 @@ __device__ __forceinline__ bool fwd_trial(const Dev& D, int b, const ElemState& 
     const double ct = knot_calc<NT>(kd, P, nx, xv, uv, running, xn, red, mbw);
     bool bad = false;
     if (running) {
-      double* xo = D.xnext[o] + D.run(b, t) * D.sX;
+      double* xo = out.xnext + D.run(b, t) * D.sX;
       for (int i = tid; i < nx; i += NT) {
         xo[i] = xn[i];
         bad |= bad_entry(xn[i]);
@@ -717,7 +733,7 @@ __device__ __forceinline__ bool fwd_trial(const Dev& D, int b, const ElemState& 
     }
     if (!feas) pd = wg_sum<NT>(pd, red);
     if (tid == 0) {
-      D.kcost[o][kk] = ct;
+      out.kcost[kk] = ct;
       dvp[t] = pd;
     }
     cost_try += ct;
@@ -754,12 +770,69 @@ __host__ __device__ inline int64_t fwd_lds_doubles(int64_t sX, int64_t sN, int64
   return FAST ? (sX + sM) + sN + sX + 2 * NT + 24 + 2 : 2 * sX + sM + 5 * (NT / 64) + 8 + 2 + 2 * sN;
 }
 
+// The line search's test of one finished trial (fddp.cpp:57-78): fills the
+// trial's bookkeeping into s; true if alpha is accepted (then s holds the new state).
+__device__ __forceinline__ bool ls_accept(const Prm& prm, ElemState& s, double alpha, double ct, double dv) {
+  s.cost_try = ct;
+  s.dV = s.cost - ct;
+  s.dv = dv;
+  s.d0 = s.dg + dv;
+  s.d1 = s.dq - 2 * dv;
+  s.dVexp = alpha * (s.d0 + 0.5 * alpha * s.d1);
+  bool acc;
+  if (s.dVexp >= 0)
+    acc = s.d0 < prm.th_grad || s.dV > prm.th_acceptstep * s.dVexp;
+  else
+    acc = s.dV > prm.th_acceptnegstep * s.dVexp;
+  if (acc) {
+    s.was_feasible = s.is_feasible;
+    s.is_feasible = (s.was_feasible || alpha == 1.) ? 1 : 0;
+    s.cur = 1 - s.cur;
+    s.cost = ct;
+  }
+  return acc;
+}
+
+// After the line search: regularisation schedule (fddp.cpp:83-91) and the loop's
+// convergence / abort test (fddp.cpp:92-103).
+__device__ __forceinline__ void ls_finish(const Prm& prm, ElemState& s, bool accepted) {
+  s.recalc = accepted ? 1 : 0;
+  bool abort = false;
+  if (s.steplength > prm.th_stepdec) {
+    s.xreg /= prm.regfactor;
+    if (s.xreg < prm.regmin) s.xreg = prm.regmin;
+    s.ureg = s.xreg;
+  }
+  if (s.steplength <= prm.th_stepinc) {
+    s.xreg *= prm.regfactor;
+    if (s.xreg > prm.regmax) s.xreg = prm.regmax;
+    s.ureg = s.xreg;
+    if (s.xreg == prm.regmax) abort = true;
+  }
+  s.n_iter_run += 1;
+  if (abort) {
+    s.status = FDDP_STATUS_REGMAX;
+    s.active = 0;
+  } else if (s.was_feasible && s.stop < prm.th_stop) {  // fddp.cpp:100-102
+    s.status = FDDP_STATUS_CONVERGED;
+    s.active = 0;
+  } else {
+    s.iter += 1;
+  }
+}
+
+// mode 0: the serial line search + update; mode 1 (tryStep): one trial at alpha1;
+// mode 2: trial alphas[group * npar + blockIdx.y] of a parallel group into slot
+// blockIdx.y, its outcome into ptrial (ls_select_kernel decides).
 template <int NT, bool FAST>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2))) void forward_kernel(Dev D, Prm prm, int mode, double alpha1, int* active_count,
-                                                     int64_t pcap) {
+                                                     int64_t pcap, int group = 0) {
   const int b = blockIdx.x;
   ElemState* st = D.st + b;
-  if (mode == 0 && !st->active) return;
+  if (mode != 1 && !st->active) return;
+  const int slot = mode == 2 ? (int)blockIdx.y : 0;
+  const int a2 = group * D.npar + slot;
+  if (mode == 2 && (D.ls_done[b] || a2 >= prm.n_alphas)) return;
   extern __shared__ __attribute__((aligned(16))) double sm[];
   double* pl = sm;
   const double* cached = nullptr;
@@ -787,14 +860,14 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2))) void fo
       return fwd_trial_fast<NT, true>(D, b, s, alpha, xv, dxv, xn, pa, pdyn, red, flag, ct, dv, pl, pcap, cached);
     else
       return fwd_trial<NT>(D, b, s, alpha, xv, uv, xn, red, flag, ct, dv, pl, pcap, cached, (double*)flag + 2 + 2 * D.sN,
-                           (double*)flag + 2);
+                           (double*)flag + 2, slot);
   };
-  // line search (fddp.cpp:53-81); mode 1 (tryStep): one trial at alpha1. One call
-  // site of the trial, so it is inlined (its LDS pointers keep their address space).
+  // line search (fddp.cpp:53-81). One call site of the trial, so it is inlined (its
+  // LDS pointers keep their address space).
   bool accepted = false;
-  const int na = mode == 1 ? 1 : prm.n_alphas;
+  const int na = mode == 0 ? prm.n_alphas : 1;
   for (int a = 0; a < na; ++a) {
-    const double alpha = mode == 1 ? alpha1 : prm.alphas[a];
+    const double alpha = mode == 1 ? alpha1 : prm.alphas[mode == 2 ? a2 : a];
     double ct, dv;
     bool ok;
     [[clang::always_inline]] ok = trial(alpha, ct, dv);
@@ -807,54 +880,77 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2))) void fo
       }
       return;
     }
+    if (mode == 2) {
+      if (threadIdx.x == 0) {
+        double* r = D.ptrial + ((int64_t)b * D.npar + slot) * 4;
+        r[0] = ok ? 1. : 0.;
+        r[1] = ct;
+        r[2] = dv;
+      }
+      return;
+    }
     s.steplength = alpha;
     if (!ok) continue;
-    s.cost_try = ct;
-    s.dV = s.cost - ct;
-    s.dv = dv;
-    s.d0 = s.dg + dv;
-    s.d1 = s.dq - 2 * dv;
-    s.dVexp = alpha * (s.d0 + 0.5 * alpha * s.d1);
-    bool acc;
-    if (s.dVexp >= 0)
-      acc = s.d0 < prm.th_grad || s.dV > prm.th_acceptstep * s.dVexp;
-    else
-      acc = s.dV > prm.th_acceptnegstep * s.dVexp;
-    if (acc) {
-      s.was_feasible = s.is_feasible;
-      s.is_feasible = (s.was_feasible || alpha == 1.) ? 1 : 0;
-      s.cur = 1 - s.cur;
-      s.cost = ct;
+    if (ls_accept(prm, s, alpha, ct, dv)) {
       accepted = true;
       break;
     }
   }
-  s.recalc = accepted ? 1 : 0;
-  // regularisation schedule (fddp.cpp:83-91)
-  bool abort = false;
-  if (s.steplength > prm.th_stepdec) {
-    s.xreg /= prm.regfactor;
-    if (s.xreg < prm.regmin) s.xreg = prm.regmin;
-    s.ureg = s.xreg;
-  }
-  if (s.steplength <= prm.th_stepinc) {
-    s.xreg *= prm.regfactor;
-    if (s.xreg > prm.regmax) s.xreg = prm.regmax;
-    s.ureg = s.xreg;
-    if (s.xreg == prm.regmax) abort = true;
-  }
-  s.n_iter_run += 1;
-  if (abort) {
-    s.status = FDDP_STATUS_REGMAX;
-    s.active = 0;
-  } else if (s.was_feasible && s.stop < prm.th_stop) {  // fddp.cpp:100-102
-    s.status = FDDP_STATUS_CONVERGED;
-    s.active = 0;
-  } else {
-    s.iter += 1;
-  }
+  ls_finish(prm, s, accepted);
   if (threadIdx.x == 0) {
     *st = s;
+    if (s.active && active_count) atomicAdd(active_count, 1);
+  }
+}
+
+// Decision after parallel group `group`: the first accepted trial in alpha order
+// (the serial line search's choice); its slot is copied into the other trajectory
+// buffer when it is not slot 0. Undecided elements wait for the next group; the
+// last group resets ls_done for the next iteration.
+template <int NT>
+__global__ __launch_bounds__(NT) void ls_select_kernel(Dev D, Prm prm, int group, int last, int* active_count) {
+  const int b = blockIdx.x, tid = threadIdx.x;
+  ElemState* st = D.st + b;
+  if (!st->active || D.ls_done[b]) {
+    if (last && tid == 0) D.ls_done[b] = 0;
+    return;
+  }
+  ElemState s = *st;
+  int acc_slot = -1;
+  bool exhausted = false;
+  for (int p = 0; p < D.npar; ++p) {
+    const int a = group * D.npar + p;
+    if (a >= prm.n_alphas) {
+      exhausted = true;
+      break;
+    }
+    const double alpha = prm.alphas[a];
+    s.steplength = alpha;
+    const double* r = D.ptrial + ((int64_t)b * D.npar + p) * 4;
+    if (r[0] == 0.) continue;
+    if (ls_accept(prm, s, alpha, r[1], r[2])) {
+      acc_slot = p;
+      break;
+    }
+  }
+  if (group * D.npar + D.npar >= prm.n_alphas) exhausted = true;
+  if (acc_slot < 0 && !exhausted) {  // next group
+    if (tid == 0) *st = s;
+    return;
+  }
+  if (acc_slot > 0) {  // the accepted slot's trajectories into the (new) current buffer
+    const TrialOut src(D, 0, acc_slot), dst(D, s.cur, 0);
+    const int64_t K1 = D.T + 1;
+    for (int64_t i = tid; i < K1 * D.sX; i += NT) dst.xs[D.knot(b, 0) * D.sX + i] = src.xs[D.knot(b, 0) * D.sX + i];
+    for (int64_t i = tid; i < D.T * D.sM; i += NT) dst.us[D.run(b, 0) * D.sM + i] = src.us[D.run(b, 0) * D.sM + i];
+    for (int64_t i = tid; i < D.T * D.sX; i += NT)
+      dst.xnext[D.run(b, 0) * D.sX + i] = src.xnext[D.run(b, 0) * D.sX + i];
+    for (int64_t i = tid; i < K1; i += NT) dst.kcost[D.knot(b, 0) + i] = src.kcost[D.knot(b, 0) + i];
+  }
+  ls_finish(prm, s, acc_slot >= 0);
+  if (tid == 0) {
+    *st = s;
+    D.ls_done[b] = last ? 0 : 1;
     if (s.active && active_count) atomicAdd(active_count, 1);
   }
 }

@@ -50,6 +50,29 @@ def gather_rows(local):
     return out
 
 
+# per-element solve results gathered with the trajectories, one row each
+RESULT_FIELDS = ("status", "iter", "is_feasible", "n_iter_run", "cost", "stop", "steplength")
+
+
+def gather_solution(solver, device):
+    """All-gather every rank's solved shard: (xs (B_all, T+1, nx), us (B_all, T, nu_max),
+    results (B_all, len(RESULT_FIELDS))), rows in rank order. The trajectories are
+    copied device to device from the solver (no host round trip); with the gloo
+    backend (CPU tests) the collective runs on host copies."""
+    p = solver.problem
+    dev = torch.device(device) if not isinstance(device, torch.device) else device
+    xs = torch.empty((p.B, p.T + 1, p.nx), dtype=torch.float64, device=dev)
+    us = torch.empty((p.B, p.T, p.nu_max), dtype=torch.float64, device=dev)
+    solver.xs_device(xs.data_ptr())
+    solver.us_device(us.data_ptr())
+    res = torch.tensor([[float(getattr(r, f)) for f in RESULT_FIELDS] for r in solver._res()], dtype=torch.float64,
+                       device=dev)
+    solver.synchronize()
+    if dist.is_initialized() and dist.get_backend() == "gloo":
+        xs, us, res = xs.cpu(), us.cpu(), res.cpu()
+    return gather_rows(xs), gather_rows(us), gather_rows(res)
+
+
 def job_time_and_work(elapsed_s, work, device):
     """Whole-job numbers: the slowest rank's time, the sum of the work."""
     if not dist.is_initialized() or dist.get_world_size() == 1:

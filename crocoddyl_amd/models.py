@@ -121,6 +121,7 @@ class ActionModelAbstract(_ControlLimits):
         self.state = state
         self.nu = int(nu)
         self.nr = int(nr)
+        self.unone = np.zeros(self.nu)  # action-base.hpp: the default control of calc(data, x)
         self._version = 0
         self._init_limits()
 
@@ -128,8 +129,17 @@ class ActionModelAbstract(_ControlLimits):
         self._version += 1
 
     def pack(self):
-        """(kind, nu, blocks (Bm, size)) for the parameter pool."""
+        """(kind, nu, blocks (Bm, size)) for the parameter pool. A Python subclass
+        without a device kind overrides calc(data, x, u=None) / calcDiff(data, x,
+        u=None) instead (action-base.hpp:18-55); its problems run on the host
+        (crocoddyl_amd.host)."""
         raise NotImplementedError
+
+    def calc(self, data, x, u=None):
+        raise NotImplementedError("crocoddyl_amd: calc of a Python-defined action model must be overridden")
+
+    def calcDiff(self, data, x, u=None):
+        raise NotImplementedError("crocoddyl_amd: calcDiff of a Python-defined action model must be overridden")
 
     def createData(self):
         return ActionData(self)
@@ -142,6 +152,7 @@ class ActionData:
     def __init__(self, model):
         n, m = model.state.ndx, model.nu
         self.cost = 0.0
+        self.r = np.zeros(getattr(model, "nr", 0))
         self.xnext = np.zeros(model.state.nx)
         self.Fx = np.zeros((n, n))
         self.Fu = np.zeros((n, m))
@@ -150,6 +161,9 @@ class ActionData:
         self.Lxx = np.zeros((n, n))
         self.Lxu = np.zeros((n, m))
         self.Luu = np.zeros((m, m))
+
+
+ActionDataAbstract = ActionData  # the reference's base name for derived data classes
 
 
 class ActionModelLQR(ActionModelAbstract):

@@ -1308,8 +1308,9 @@ class DifferentialActionModelContactFwdDynamics(DifferentialActionModelFreeFwdDy
     """contact-fwddyn.hxx:24-160: the KKT dynamics
         [M  Jc^T ; Jc  0] [a ; -lambda] = [tau(u) - nle ; -a0]
     (Schur complement with JMinvJt + inv_damping I), costs.calc(x, u).
-    ``enable_force`` only selects the force Jacobians, which no device-covered
-    cost reads."""
+    ``enable_force`` selects the force Jacobians d lambda / d(x, u)
+    (contact-fwddyn.hxx:141-156) that CostModelContactForce / ContactFrictionCone
+    read; without it their residual Jacobians are zero, as in the reference."""
 
     def __init__(self, state, actuation, contacts, costs, inv_damping=0.0, enable_force=False):
         if not isinstance(actuation, ActuationModelFloatingBase):

@@ -23,6 +23,7 @@ import numpy as np
 
 from . import _abi
 from ._lib import FDDPError, check, default_params, lib
+from .host import HostProblem, HostSolverFDDP, is_host_model
 from .models import ActionData, ActionModelAbstract
 
 
@@ -144,8 +145,17 @@ class ShootingProblem:
             raise ValueError("Invalid argument: nx in terminal node is not consistent with the other nodes")
         if x0.shape[-1] != self.nx or x0.ndim not in (1, 2):
             raise ValueError(f"Invalid argument: x0 has wrong dimension (it should be {self.nx})")
-        self.batched = x0.ndim == 2 or any(m.pack()[2].shape[0] > 1 for m in set(runningModels + [terminalModel]))
-        self.B = batch_size_of(x0, set(runningModels + [terminalModel]))
+        # a Python-defined model anywhere: the whole problem runs on the host (host.py)
+        self.host_mode = any(is_host_model(m) for m in runningModels + [terminalModel])
+        if self.host_mode:
+            if x0.ndim != 1 or any(m.pack()[2].shape[0] > 1 for m in set(runningModels + [terminalModel])
+                                   if not is_host_model(m)):
+                raise ValueError("Invalid argument: problems with Python-defined action models are single problems "
+                                 "(one x0, unbatched model parameters)")
+            self.batched, self.B = False, 1
+        else:
+            self.batched = x0.ndim == 2 or any(m.pack()[2].shape[0] > 1 for m in set(runningModels + [terminalModel]))
+            self.B = batch_size_of(x0, set(runningModels + [terminalModel]))
         self._x0b = np.broadcast_to(x0, (self.B, self.nx)).copy() if x0.ndim == 1 else x0.copy()
         self.device = device
         self._calc_h = None
@@ -201,7 +211,10 @@ class ShootingProblem:
             raise ValueError("Invalid argument: nu node is not bigger than the maximun nu")
         if data is not None and (not isinstance(data, ActionData) or data.Fu.shape[1] != model.nu):
             raise ValueError("Invalid argument: action data is not consistent with the action model")
-        if model.pack()[2].shape[0] not in (1, self.B):
+        if is_host_model(model) and not self.host_mode:
+            raise ValueError("Invalid argument: a Python-defined model cannot join a device problem; build a new "
+                             "ShootingProblem")
+        if not is_host_model(model) and model.pack()[2].shape[0] not in (1, self.B):
             raise ValueError(f"Invalid argument: model parameters are batched over {model.pack()[2].shape[0]} "
                              f"elements but the problem has B={self.B}")
 
@@ -345,8 +358,16 @@ class ShootingProblem:
                 d.Lu = Lu[:, t][sel][..., :mdl.nu].copy()
 
     # -- ShootingProblem::calc / calcDiff / rollout ----------------------------
+    def _host(self):
+        if getattr(self, "_hostp", None) is None:
+            self._hostp = HostProblem(self)
+        return self._hostp
+
     def calc(self, xs, us):
         """shooting.hxx:133-161; returns the total cost (per element if batched)."""
+        if self.host_mode:
+            self.cost = self._host().calc(list(xs), list(us))
+            return self.cost
         h = self._calc_handle()
         xa, ua = self._xs_array(xs), self._us_array(us)
         if xa is None or (ua is None and self.nu_max > 0):
@@ -361,6 +382,9 @@ class ShootingProblem:
     def calcDiff(self, xs, us):
         """shooting.hxx:164-195 (calc first, as the reference's datas carry the costs)."""
         self.calc(xs, us)
+        if self.host_mode:
+            self.cost = self._host().calc(list(xs), list(us), diff=True)
+            return self.cost
         h = self._calc_handle()
         cost = np.zeros(self.B)
         check(lib().fddp_problem_calc_diff(h, _abi.dptr(cost)))
@@ -373,6 +397,8 @@ class ShootingProblem:
 
         Runs as the device forward pass with zero feedback gains (this
         handle never computes a backward pass, so K = k = 0), alpha = 1."""
+        if self.host_mode:
+            return self._host().rollout(list(us))
         h = self._calc_handle()
         ua = self._us_array(us)
         check(lib().fddp_set_candidate(h, None, _abi.dptr(ua), 1))
@@ -392,7 +418,16 @@ def _cm(flat, r, c):
 
 
 class SolverFDDP:
-    """SolverFDDP (src/core/solvers/fddp.cpp) on the device, batched."""
+    """SolverFDDP (src/core/solvers/fddp.cpp) on the device, batched. A problem with
+    Python-defined action models gets the host solver (host.HostSolverFDDP)."""
+
+    def __new__(cls, problem):
+        if getattr(problem, "host_mode", False):
+            if cls is not SolverFDDP:
+                raise NotImplementedError(f"crocoddyl_amd: {cls.__name__} needs device models (Python-defined "
+                                          "action models run with SolverFDDP)")
+            return HostSolverFDDP(problem)
+        return super().__new__(cls)
 
     def __init__(self, problem):
         self.problem = problem

@@ -59,35 +59,52 @@ extern "C" {
 #define FDDP_KNOT_EULER_DIFFLQR 3
 /* IntegratedActionModelEuler (euler.hxx:41-131) around
  * DifferentialActionModelFreeFwdDynamics (multibody/actions/free-fwddyn.hxx:44-118)
- * with ActuationModelFull (tau = u) and a CostModelSum (cost-sum.hxx:89-160),
- * over a fixed-base kinematic tree of nv revolute joints (StateMultibody with
- * nq = nv: nx = ndx = 2 nv, nu = nv). Variable-size block:
+ * with ActuationModelFull (tau = u) and a CostModelSum (cost-sum.hxx:89-160) over
+ * a kinematic tree (StateMultibody, multibody/states/multibody.hxx:54-240): revolute
+ * joints, optionally below a free-flyer root (JointModelFreeFlyer: q = (p, quat
+ * x y z w), v = body twist (linear, angular); nq = nv + 1). nx = nq + nv,
+ * ndx = 2 nv; nu = nv (no free-flyer). Variable-size block:
  *   header [dt, nv, ncost, size (doubles, header included)]
  *   gravity(3)  armature(nv)
- *   nv joint records of 26 doubles, parents before children (Pinocchio order):
- *     parent (-1 = universe), axis(3, unit, joint frame), placement in the
- *     parent joint frame R(9, column-major) p(3), body mass, CoM(3, joint
- *     frame), rotational inertia about the CoM (Ixx Iyy Izz Ixy Ixz Iyz)
+ *   one 27-double record per joint (a free-flyer root is ONE record for its 6
+ *   dofs), parents before children (Pinocchio order):
+ *     [type (0 revolute, 1 free-flyer), parent record (-1 = universe), axis(3,
+ *     unit, joint frame; unused for the free-flyer), placement in the parent
+ *     joint frame R(9, column-major) p(3), body mass, CoM(3, joint frame),
+ *     rotational inertia about the CoM (Ixx Iyy Izz Ixy Ixz Iyz)]
  *   ncost cost records in name order (CostModelSum's std::map), each
- *     [type, weight, weighted (0: ActivationModelQuad, 1: WeightedQuad), size]
- *     then the payload and the activation weights (ones when unweighted):
- *     1 CostModelState (state.hxx:130-169):       xref(nx) w(nx)
- *     2 CostModelControl (control.hxx:56-87):     uref(nu) w(nu)
+ *     [type, weight, activation kind, size (doubles, record header included)]
+ *     then the payload, then the activation parameters:
+ *       kind 0 ActivationModelQuad: ones(nr); 1 WeightedQuad: w(nr);
+ *       2 QuadraticBarrier: lb(nr) ub(nr); 3 WeightedQuadraticBarrier: lb ub w
+ *       (core/activations/*.hpp; the bounds already shrunk by beta)
+ *     payloads by type:
+ *     1 CostModelState (state.hxx:130-169): xref(nx); r = diff(xref, x), nr = ndx
+ *     2 CostModelControl (control.hxx:56-87): uref(nu)
  *     3 CostModelFramePlacement (frame-placement.hxx:45-80): frame joint,
- *       frame placement in that joint R(9) p(3), Mref^-1 R(9) p(3), w(6)
+ *       frame placement in that joint R(9) p(3), Mref^-1 R(9) p(3); nr = 6
  *     4 CostModelFrameTranslation (frame-translation.hxx:50-81): frame joint,
- *       frame placement R(9) p(3), reference translation(3), w(3)
- * At most 32 joints (fewer when the calcDiff LDS plan does not fit) and 8
- * frame costs per knot. */
+ *       frame placement R(9) p(3), reference translation(3); nr = 3
+ *     7 CostModelContactForce (contact-force.hxx:33-74, contact knots only):
+ *       [row0, nr, fref(6)]: r = lambda[row0 .. row0+nr) - fref, row0 the
+ *       contact's first row (-2: the contact exists but is inactive, lambda = 0)
+ *     8 CostModelCoMPosition (com-position.hxx:49-75): cref(3)
+ *     9 CostModelContactFrictionCone (contact-friction-cone.hxx:51-91, contact
+ *       knots only): [row0, contact rows, nr, A(nr x 3, row-major)]: r = A lambda_lin
+ *    10 CostModelFrameVelocity (frame-velocity.hxx:53-84, Euler knots): frame
+ *       joint, frame placement R(9) p(3), vref(6) (LOCAL); nr = 6
+ * At most 64 dofs, 64 cost records and 64 stacked residual rows with dense
+ * Jacobians per knot (the calcDiff LDS plan must fit; fddp_create says why not). */
 #define FDDP_KNOT_EULER_FREEFWD 4
 /* IntegratedActionModelEuler around DifferentialActionModelContactFwdDynamics
  * (multibody/actions/contact-fwddyn.hxx:59-160) with ActuationModelFloatingBase
- * (actuations/floating-base.hpp:29-40: tau = [0_nun; u], nu = nv - nun) and a
- * ContactModelMultiple (contacts/multiple-contacts.hxx) of ContactModel3D /
- * ContactModel6D (contacts/contact-{3d,6d}.hxx, LOCAL frame, Baumgarte gains),
- * over the same fixed-base revolute trees. Block: the FDDP_KNOT_EULER_FREEFWD
- * layout (header size covers everything), then
- *   [nun, JMinvJt_damping, ncontact, 0]
+ * (actuations/floating-base.hpp:29-40: tau = [0_nun; u], nu = nv - nun; nun = 6
+ * on a free-flyer root) and a ContactModelMultiple (contacts/multiple-contacts.hxx)
+ * of ContactModel3D / ContactModel6D (contacts/contact-{3d,6d}.hxx, LOCAL frame,
+ * Baumgarte gains). Block: the FDDP_KNOT_EULER_FREEFWD layout (header size covers
+ * everything; dt = 0 is the biped's pseudo-impulse knot), then
+ *   [nun, JMinvJt_damping, ncontact, flag (0; 2 = enable_force: the force
+ *    Jacobians the contact-force / friction-cone costs read)]
  *   ncontact active contact records in name order, each
  *     [type (5: 3D, 6: 6D), gains[0], gains[1], size], frame joint, frame
  *     placement in that joint R(9) p(3), then 3D: reference translation(3);
@@ -99,7 +116,8 @@ extern "C" {
  * action model (no integrator), nu = 0, xnext = (q, v+) with the impulse
  * dynamics [M Jc^T; Jc 0][v+; -Lambda] = [M v; -r_coeff Jc v], cost = costs(x);
  * ImpulseModelMultiple of ImpulseModel3D / 6D (impulses/impulse-{3d,6d}.hxx).
- * Block: the FDDP_KNOT_EULER_FREEFWD layout with dt = 0, then
+ * Block: the FDDP_KNOT_EULER_FREEFWD layout with dt = 0 (no frame-velocity or
+ * force costs), then
  *   [r_coeff, JMinvJt_damping, nimpulse, 1]
  *   nimpulse active impulse records in name order, each
  *     [type (5: 3D, 6: 6D), 0, 0, size = 17], frame joint, frame placement R(9) p(3)
@@ -111,7 +129,7 @@ extern "C" {
 
 typedef struct {
   int32_t nx;      /* state dimension (ShootingProblem::get_nx, shooting.hxx:25) */
-  int32_t ndx;     /* tangent dimension (== nx for the Euclidean states covered) */
+  int32_t ndx;     /* tangent dimension (nx, or nx - 1 on a free-flyer multibody state) */
   int32_t nu_max;  /* max controls over the running knots (shooting.hxx:27-34) */
   int32_t T;       /* number of running knots */
   int32_t B;       /* number of independent problems in the batch */
@@ -267,6 +285,8 @@ int fddp_get_us_try(fddp_handle* h, double* out);
 #define FDDP_Q_QUU_INV 18 /* T x nu_max*nu_max: SolverBoxFDDP::get_Quu_inv (box-fddp.cpp:162);
                              like the reference, a knot keeps its last value
                              (zero initially) while the box QP does not run on it */
+#define FDDP_Q_COST 19 /* (T+1) x 1: data[t].cost of the current candidate (after
+                          fddp_problem_calc / calc_diff or a solve) */
 int fddp_get_quantity(fddp_handle* h, int which, double* out);
 /* Store Vxx/Vx/Q* per knot during backward passes (costs HBM traffic). */
 int fddp_set_debug(fddp_handle* h, int on);

@@ -263,13 +263,7 @@ static void calc(const Model& m, Data& d, const double* x, const double* u_in) {
     case FDDP_KNOT_EULER_FREEFWD:     // euler.hxx:41-80 around free-fwddyn.hxx:44-79 (multibody_oracle.hpp)
     case FDDP_KNOT_EULER_CONTACTFWD:  // ... or contact-fwddyn.hxx:59-104
     case FDDP_KNOT_IMPULSEFWD: {      // impulse-fwddyn.hxx:53-86
-      if (m.nx != m.ndx || m.kind == FDDP_KNOT_IMPULSEFWD) {  // free-flyer root / impulses (floating_oracle.hpp)
-        fbo::Knot k;
-        k.parse(m.p);
-        k.calc(x, u, d.xnext.data(), &d.cost);
-        break;
-      }
-      mbo::Knot k;
+      fbo::Knot k;  // (floating_oracle.hpp: any root, every cost type)
       k.parse(m.p);
       k.calc(x, u, d.xnext.data(), &d.cost);
       break;
@@ -354,14 +348,7 @@ static void calcDiff(const Model& m, Data& d, const double* x, const double* u_i
     case FDDP_KNOT_EULER_FREEFWD:     // euler.hxx:83-131 around free-fwddyn.hxx:82-118 (multibody_oracle.hpp)
     case FDDP_KNOT_EULER_CONTACTFWD:  // ... or contact-fwddyn.hxx:107-160
     case FDDP_KNOT_IMPULSEFWD: {      // impulse-fwddyn.hxx:89-127
-      if (m.nx != m.ndx || m.kind == FDDP_KNOT_IMPULSEFWD) {
-        fbo::Knot k;
-        k.parse(m.p);
-        k.calc_diff(x, u, m.nu, d.Fx.a.data(), d.Fu.a.data(), d.Lxx.a.data(), d.Lxu.a.data(), d.Luu.a.data(),
-                    d.Lx.data(), d.Lu.data());
-        break;
-      }
-      mbo::Knot k;
+      fbo::Knot k;
       k.parse(m.p);
       k.calc_diff(x, u, m.nu, d.Fx.a.data(), d.Fu.a.data(), d.Lxx.a.data(), d.Lxu.a.data(), d.Luu.a.data(),
                   d.Lx.data(), d.Lu.data());
