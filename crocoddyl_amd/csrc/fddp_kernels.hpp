@@ -246,7 +246,7 @@ __global__ __launch_bounds__(NT) void calc_diff_kernel(Dev D, int sel, int gaps,
 // (derivative blocks) for those selected by sel_diff (-1: none), fused: the
 // calcDiff evaluates the dynamics the calc needs anyway. The gaps of these
 // knots are written by calc_diff_kernel as for any knot.
-__global__ __launch_bounds__(mb::kMbDiffNT) void mb_knot_kernel(Dev D, int sel_calc, int sel_diff) {
+__global__ __launch_bounds__(mb::kMbDiffNT) __attribute__((amdgpu_waves_per_eu(2))) void mb_knot_kernel(Dev D, int sel_calc, int sel_diff) {
   const int t = blockIdx.x, b = blockIdx.y;
   const fddp_knot_desc kd = D.knots[t];
   if (!is_mb_kind(kd.kind)) return;
