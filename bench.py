@@ -310,7 +310,9 @@ def main():
             rooflines["forward"] = (fw_ms, {
                 "kernel": "line-search rollout (forward_kernel + ls_select_kernel, knot calc per trial)",
                 "bound": "hbm", "achieved": round(a, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                "frac": round(a / HBM_PEAK_GBPS, 5), "traffic": None, "algorithmic_bytes_per_launch": int(Yf),
+                "frac": round(a / HBM_PEAK_GBPS, 5),
+                "traffic": None,  # per group dispatch in profiles/pmc_backward.json ("forward"); a call is 3
+                "algorithmic_bytes_per_launch": int(Yf),
                 "knot_trials_per_launch": int(kt), "avg_launch_ms": round(fw_ms / fw_n, 3),
                 "timer": "HIP events on the solver stream"})
         cd_ms, cd_n = timing["calcDiff"]
@@ -320,7 +322,7 @@ def main():
             rooflines["calcDiff"] = (cd_ms, {
                 "kernel": "knot-parallel calcDiff (mb_knot_kernel / calc_diff_kernel)", "bound": "hbm",
                 "achieved": round(a, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(a / HBM_PEAK_GBPS, 5),
-                "traffic": None, "algorithmic_bytes_per_launch": int(Yc), "avg_launch_ms": round(cd_ms / cd_n, 3),
+                "traffic": ((pmc or {}).get("kernels", {}).get("mb_calc_diff") or {}).get("hbm_bytes_per_launch"), "algorithmic_bytes_per_launch": int(Yc), "avg_launch_ms": round(cd_ms / cd_n, 3),
                 "timer": "HIP events on the solver stream"})
         dominant = max(rooflines, key=lambda k: rooflines[k][0])
         roof = dict(rooflines[dominant][1], dominant_of=sorted(rooflines))

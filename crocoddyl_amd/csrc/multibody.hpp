@@ -2618,34 +2618,42 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
       }
       (isu ? Lu : Lx)[j] = integ ? sc * acc : acc;
     }
-    // the fused calc's cost: jac-cost residuals from the Jacobian phase (cost-sum.hxx:89-117)
-    if (cost_out && lane == 0) {
-      double total = 0.;
+    // the fused calc's cost (cost-sum.hxx:89-117): record k's weighted activation on
+    // lane nt-1-k (the lanes with the fewest GEMM tasks), into the dead pivot buffer;
+    // jac-cost residuals from the Jacobian phase
+    if (cost_out && ex.nt - 1 - lane < b.ncost) {
+      const int k = ex.nt - 1 - lane;
       const double* cr = b.C;
       int f = 0;
-      for (int k = 0; k < b.ncost; ++k) {
-        const CRec C{cr};
-        const int t = C.type();
-        const Act act = cost_act(b, C, nu);
-        double a = 0.;
-        if (jac_cost(b, t)) {
-          const int nr = jac_rows(t);
-          for (int i = 0; i < nr; ++i) a += act.value2(i, rf[6 * f + i]);
-          ++f;
-        }
-        if (t == C_STATE) {
-          for (int i = b.ff ? 6 : 0; i < n; ++i) a += act.value2(i, state_res(b, C.d(), x, i));
-        } else if (t == C_CONTROL) {
-          for (int i = 0; i < nu; ++i) a += act.value2(i, u[i] - C.d()[i]);
-        } else if (force_cost(t)) {
-          a = 2. * force_cost_activation(b, C, lam, nu);
-        }
-        total += C.weight() * (0.5 * a);
-        cr += C.size();
+      for (int q = 0; q < k; ++q) {
+        f += jac_cost(b, CRec{cr}.type()) ? 1 : 0;
+        cr += CRec{cr}.size();
       }
-      *cost_out = integ ? dt * total : total;
+      const CRec C{cr};
+      const int t = C.type();
+      const Act act = cost_act(b, C, nu);
+      double a = 0.;
+      if (jac_cost(b, t)) {
+        const int nr = jac_rows(t);
+        for (int i = 0; i < nr; ++i) a += act.value2(i, rf[6 * f + i]);
+      }
+      if (t == C_STATE) {
+        for (int i = b.ff ? 6 : 0; i < n; ++i) a += act.value2(i, state_res(b, C.d(), x, i));
+      } else if (t == C_CONTROL) {
+        for (int i = 0; i < nu; ++i) a += act.value2(i, u[i] - C.d()[i]);
+      } else if (force_cost(t)) {
+        a = 2. * force_cost_activation(b, C, lam, nu);
+      }
+      pb[k] = C.weight() * (0.5 * a);
     }
   });
+  if (cost_out)  // summed in cost order
+    ex.run([&](int lane) {
+      if (lane != 0) return;
+      double total = 0.;
+      for (int k = 0; k < b.ncost; ++k) total += pb[k];
+      *cost_out = integ ? dt * total : total;
+    });
   (void)nx;
 }
 

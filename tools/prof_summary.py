@@ -35,12 +35,13 @@ def main():
     tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
     cfg = sys.argv[2] if len(sys.argv) > 2 else "C5_talos_full"
     src = os.path.join(ROOT, "gpurun_out", "prof")
+    kt = sys.argv[3] if len(sys.argv) > 3 else os.path.join(src, "kt")
     prof = os.path.join(ROOT, "profiles")
     os.makedirs(prof, exist_ok=True)
-    shutil.copy(os.path.join(src, "kt", "run_kernel_stats.csv"), os.path.join(prof, f"{tag}_kernel_stats.csv"))
+    shutil.copy(os.path.join(kt, "run_kernel_stats.csv"), os.path.join(prof, f"{tag}_kernel_stats.csv"))
     out = {}
     for kname, key in (("backward_mfma_kernel", "backward"), ("calc_fused_kernel", "calc_fused"),
-                       ("forward_kernel", "forward")):
+                       ("forward_kernel", "forward"), ("mb_knot_kernel", "mb_calc_diff")):
         f = counter(os.path.join(src, "pmc_fetch", "run_counter_collection.csv"), kname, "FETCH_SIZE")
         w = counter(os.path.join(src, "pmc_write", "run_counter_collection.csv"), kname, "WRITE_SIZE")
         if not f or not w:
@@ -52,6 +53,15 @@ def main():
         write = statistics.mean(w) * 1024.0
         out[key] = {"hbm_bytes_per_launch": fetch + write, "fetch_bytes": fetch, "write_bytes": write,
                     "dispatches": [len(f), len(w)]}
+        mf = os.path.join(src, "pmc_mfma", "run_counter_collection.csv")
+        if os.path.exists(mf):  # MFMA / busy counters (SQ_* summed over the SIMDs, GRBM over the 8 XCDs)
+            c = {n: statistics.mean(counter(mf, kname, n) or [0.]) for n in
+                 ("SQ_VALU_MFMA_BUSY_CYCLES", "SQ_INSTS_VALU_MFMA_F64", "SQ_INSTS_VALU_MFMA_MOPS_F64",
+                  "SQ_INSTS_VALU", "SQ_BUSY_CYCLES", "SQ_WAVE_CYCLES", "GRBM_GUI_ACTIVE")}
+            clk = c["GRBM_GUI_ACTIVE"] / 8.0  # per-XCD GPU cycles of the dispatch
+            c["mfma_busy_frac"] = c["SQ_VALU_MFMA_BUSY_CYCLES"] / max(clk * 256 * 4, 1.0)  # per SIMD
+            c["mfma_f64_flops"] = c["SQ_INSTS_VALU_MFMA_F64"] * 16 * 16 * 4 * 2  # v_mfma_f64_16x16x4
+            out[key]["counters"] = c
     path = os.path.join(prof, "pmc_backward.json")
     data = json.load(open(path)) if os.path.exists(path) else {}
     data[cfg] = dict(out.get("backward", {}), kernels=out, tag=tag,
