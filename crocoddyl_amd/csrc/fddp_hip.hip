@@ -544,6 +544,16 @@ static int ensure_par_slots(fddp_handle* h) {
   return FDDP_OK;
 }
 
+// every knot multibody: the rollout variant with only the multibody calc compiled in
+// (FDDP_FWD_MB=0 selects the generic one, for A/B runs)
+static bool mb_rollout(const fddp_handle* h) {
+  static const bool off = [] {
+    const char* e = std::getenv("FDDP_FWD_MB");
+    return e && e[0] == '0';
+  }();
+  return h->all_mb && !off;
+}
+
 int launch_forward(fddp_handle* h, int mode, double alpha, int* count) {
   Timed tm(h, 3);
   const Dev& D = h->D;
@@ -554,8 +564,12 @@ int launch_forward(fddp_handle* h, int mode, double alpha, int* count) {
     if ((rc = ensure_par_slots(h))) return rc;
     const int na = h->prm.n_alphas, G = (na + D.npar - 1) / D.npar;
     for (int g = 0; g < G; ++g) {
-      hipLaunchKernelGGL((forward_kernel<kNT, false>), dim3(D.B, D.npar), dim3(kNT), h->fwd_smem, h->stream, D,
-                         to_prm(h->prm), 2, 1., nullptr, h->pcap, g);
+      if (mb_rollout(h))
+        hipLaunchKernelGGL((forward_kernel<kNT, false, true>), dim3(D.B, D.npar), dim3(kNT), h->fwd_smem, h->stream,
+                           D, to_prm(h->prm), 2, 1., nullptr, h->pcap, g);
+      else
+        hipLaunchKernelGGL((forward_kernel<kNT, false>), dim3(D.B, D.npar), dim3(kNT), h->fwd_smem, h->stream, D,
+                           to_prm(h->prm), 2, 1., nullptr, h->pcap, g);
       LAUNCH_CHECK();
       hipLaunchKernelGGL((ls_select_kernel<kNT>), dim3(D.B), dim3(kNT), 0, h->stream, D, to_prm(h->prm), g,
                          g == G - 1 ? 1 : 0, count);
@@ -565,6 +579,9 @@ int launch_forward(fddp_handle* h, int mode, double alpha, int* count) {
   }
   if (h->fast)
     hipLaunchKernelGGL((forward_kernel<kNT, true>), dim3(D.B), dim3(kNT), h->fwd_fast_smem, h->stream, D,
+                       to_prm(h->prm), mode, alpha, count, h->pcap);
+  else if (mb_rollout(h))
+    hipLaunchKernelGGL((forward_kernel<kNT, false, true>), dim3(D.B), dim3(kNT), h->fwd_smem, h->stream, D,
                        to_prm(h->prm), mode, alpha, count, h->pcap);
   else
     hipLaunchKernelGGL((forward_kernel<kNT, false>), dim3(D.B), dim3(kNT), h->fwd_smem, h->stream, D,
@@ -765,6 +782,8 @@ int apply_knots(fddp_handle* h, const fddp_knot_desc* knots, const double* param
                           (int)h->fwd_smem) != hipSuccess ||
       hipFuncSetAttribute((const void*)forward_kernel<kNT, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)h->fwd_fast_smem) != hipSuccess ||
+      (h->has_mb && hipFuncSetAttribute((const void*)forward_kernel<kNT, false, true>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->fwd_smem) != hipSuccess) ||
       hipFuncSetAttribute((const void*)calc_tiled_kernel<kNTF>, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)h->fused_smem) != hipSuccess ||
       hipFuncSetAttribute((const void*)calc_kernel<kNT>, hipFuncAttributeMaxDynamicSharedMemorySize,

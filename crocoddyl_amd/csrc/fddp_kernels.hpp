@@ -652,7 +652,7 @@ struct TrialOut {
   }
 };
 
-template <int NT>
+template <int NT, bool MB = false>
 __device__ __forceinline__ bool fwd_trial(const Dev& D, int b, const ElemState& s, double alpha, double* xv, double* uv, double* xn,
                           double* red, int* flag, double& cost_try, double& dv, double* pl, int64_t pcap,
                           const double*& cached, double* mbw, double* dxv, int slot = 0) {
@@ -722,7 +722,7 @@ __device__ __forceinline__ bool fwd_trial(const Dev& D, int b, const ElemState& 
       }
       __syncthreads();
     }
-    const double ct = knot_calc<NT>(kd, P, nx, xv, uv, running, xn, red, mbw);
+    const double ct = knot_calc<NT, MB>(kd, P, nx, xv, uv, running, xn, red, mbw);
     bool bad = false;
     if (running) {
       double* xo = out.xnext + D.run(b, t) * D.sX;
@@ -824,8 +824,14 @@ __device__ __forceinline__ void ls_finish(const Prm& prm, ElemState& s, bool acc
 // mode 0: the serial line search + update; mode 1 (tryStep): one trial at alpha1;
 // mode 2: trial alphas[group * npar + blockIdx.y] of a parallel group into slot
 // blockIdx.y, its outcome into ptrial (ls_select_kernel decides).
-template <int NT, bool FAST>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2))) void forward_kernel(Dev D, Prm prm, int mode, double alpha1, int* active_count,
+// MB: every knot is a multibody kind (h->all_mb), only that calc is compiled in.
+#ifndef FDDP_FWD_WPE
+#define FDDP_FWD_WPE 2
+#endif
+// (the generic variant, for horizons that mix multibody and dense knots, gets the
+// whole register file: under the 2-waves cap its spills trip a backend error)
+template <int NT, bool FAST, bool MB = false>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((FAST || MB) ? FDDP_FWD_WPE : 1))) void forward_kernel(Dev D, Prm prm, int mode, double alpha1, int* active_count,
                                                      int64_t pcap, int group = 0) {
   const int b = blockIdx.x;
   ElemState* st = D.st + b;
@@ -859,7 +865,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2))) void fo
     if constexpr (FAST)
       return fwd_trial_fast<NT, true>(D, b, s, alpha, xv, dxv, xn, pa, pdyn, red, flag, ct, dv, pl, pcap, cached);
     else
-      return fwd_trial<NT>(D, b, s, alpha, xv, uv, xn, red, flag, ct, dv, pl, pcap, cached, (double*)flag + 2 + 2 * D.sN,
+      return fwd_trial<NT, MB>(D, b, s, alpha, xv, uv, xn, red, flag, ct, dv, pl, pcap, cached, (double*)flag + 2 + 2 * D.sN,
                            (double*)flag + 2, slot);
   };
   // line search (fddp.cpp:53-81). One call site of the trial, so it is inlined (its

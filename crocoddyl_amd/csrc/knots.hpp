@@ -93,14 +93,16 @@ __device__ inline double lq_cost_total(const double (&t)[5]) {
 // Writes xnext[0..nx) and returns the knot cost in every thread.
 // `red`: LDS scratch of >= 5*NT/64 doubles; `mbw`: LDS scratch of
 // mb::calc_work_doubles(nj) for multibody knots. Contains barriers: call uniformly.
-template <int NT>
+// MB: the caller guarantees every knot is a multibody kind (the dense kinds are not
+// compiled in, which keeps the rollout's register budget for the multibody calc).
+template <int NT, bool MB = false>
 __device__ __forceinline__ double knot_calc(const fddp_knot_desc& kd, const double* P, int nx, const double* x, const double* u,
                             bool use_u, double* xnext, double* red, double* mbw) {
   const int nu = kd.nu;
   use_u = use_u && nu > 0;
   // multibody blocks are always staged in LDS (fddp_create checks the budget), as are
   // the trial state / control / next state and the scratch of every caller
-  if (is_mb_kind(kd.kind))
+  if (MB || is_mb_kind(kd.kind))
     return mb::knot_calc<NT>(lds_ptr(P), nx, lds_ptr(x), lds_ptr(u), use_u, lds_ptr(xnext), lds_ptr(mbw));
   double t[5] = {0., 0., 0., 0., 0.};
   if (kd.kind == FDDP_KNOT_LQR) {

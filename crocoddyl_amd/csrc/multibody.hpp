@@ -482,8 +482,11 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
 // unrolled steps, so the owner's register of column k is static. No LDS traffic
 // beyond the one published column per pivot. Returns false if a pivot is not
 // positive (the LLT failure the reference reports).
+// id0: A's columns from id0 on start as an identity block ([M | I]); their slabs
+// are skipped until the pivot reaches them (the update is the identity there too).
 template <int CPW, int SPW>
-__device__ __forceinline__ bool gauss_jordan_rows(double* A, int nr, int ld, int nc, double* pb, int* flag) {
+__device__ __forceinline__ bool gauss_jordan_rows(double* A, int nr, int ld, int nc, double* pb, int* flag,
+                                                  int id0 = 1 << 30) {
   const int tid = (int)threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = (int)(blockDim.x >> 6);
   const int nslab = (nc + CPW - 1) / CPW;
   double v[SPW][CPW];
@@ -520,6 +523,10 @@ __device__ __forceinline__ bool gauss_jordan_rows(double* A, int nr, int ld, int
       const double ipiv = 1. / piv;
 #pragma unroll
       for (int s = 0; s < SPW; ++s) {
+        // a slab left of the pivot holds unit columns (row k zero): the update is the
+        // identity there, so it is skipped (wave-uniform)
+        const int slab = wave + s * nw;
+        if (slab >= nslab || slab * CPW + CPW <= k || slab * CPW - id0 > k) continue;
 #pragma unroll
         for (int jj = 0; jj < CPW; ++jj) {
           const double akc = readlane_d(v[s][jj], k) * ipiv;  // pivot row, scaled
@@ -544,15 +551,28 @@ __device__ __forceinline__ bool gauss_jordan_rows(double* A, int nr, int ld, int
 
 // the device executor takes the register version when the slabs fit (overload
 // resolution prefers these to the template below, which serves the host emulation)
-__device__ __forceinline__ bool gauss_jordan(const DevExec&, double* A, int nr, int ld, int nc, int* flag,
-                                             double* pb) {
-  if (nr <= 64 && nc <= 3 * 8 * (int)(blockDim.x >> 6)) return gauss_jordan_rows<8, 3>(A, nr, ld, nc, pb, flag);
+// The slab count per wave follows nc (the block is uniform): every unrolled register
+// column costs a readlane pair and an FMA per pivot, so the [M | Jc^T | r] block of
+// the calc (nc = nj + nc + 1) and the small Schur block do not pay for the 3 slabs
+// per wave that the calcDiff's [M | I] needs.
+// SPW: the call site's bound on the slabs per wave (one instantiation per call site
+// keeps the register budget of the kernels it is inlined into); blocks wider than
+// SPW slabs per wave take the LDS version.
+template <int SPW>
+__device__ __forceinline__ bool gauss_jordan_regs(double* A, int nr, int ld, int nc, int* flag, double* pb,
+                                                  int id0 = 1 << 30) {
+  if (nr <= 64 && nc <= SPW * 8 * (int)(blockDim.x >> 6)) return gauss_jordan_rows<8, SPW>(A, nr, ld, nc, pb, flag, id0);
   return gauss_jordan_dev(A, nr, ld, nc, flag);
 }
+template <int SPW>
+__device__ __forceinline__ bool gauss_jordan(const DevExec&, double* A, int nr, int ld, int nc, int* flag,
+                                             double* pb, int id0 = 1 << 30) {
+  return gauss_jordan_regs<SPW>(A, nr, ld, nc, flag, pb, id0);
+}
 
-template <class X>
+template <int SPW, class X>
 MB_HD __attribute__((noinline)) bool gauss_jordan(const X& ex, double* A, int nr, int ld, int nc, int* flag,
-                                                 double* = nullptr) {
+                                                 double* = nullptr, int = 0) {
   ex.run_w0([&](int lane) {
     if (lane == 0) *flag = 0;
   });
@@ -970,21 +990,24 @@ MB_HD inline void w_joint_world(const Blk& b, const WVals& W, int i, bool from_b
 // (m, h = m c, I_O = Ic + m (|c|^2 I - c c^T)): additive over the subtree.
 MB_HD inline void w_composite(const Blk& b, const WVals& W, int i) {
   double m = 0., h[3] = {0., 0., 0.}, I[6] = {0., 0., 0., 0., 0., 0.};
-  for (int k = 0; k < b.nj; ++k) {
-    if (!((*W.anc(k) >> i) & 1ull) || !carries_body(b, k)) continue;
+  // every body read, the ones outside the subtree weighted 0 (adds of +0: the sums are
+  // unchanged), so the unrolled iterations' LDS loads overlap instead of branching
+#pragma unroll 2
+  for (int k = b.ff ? 5 : 0; k < b.nj; ++k) {
+    const double sel = ((*W.anc(k) >> i) & 1ull) ? 1. : 0.;
     const double mk = *W.m(k);
     double c[3], Ic[6];
     for (int e = 0; e < 3; ++e) c[e] = W.c(k)[e];
     for (int e = 0; e < 6; ++e) Ic[e] = W.Ic(k)[e];
     const double cc = c[0] * c[0] + c[1] * c[1] + c[2] * c[2];
-    m += mk;
-    for (int e = 0; e < 3; ++e) h[e] += mk * c[e];
-    I[0] += Ic[0] + mk * (cc - c[0] * c[0]);
-    I[1] += Ic[1] + mk * (cc - c[1] * c[1]);
-    I[2] += Ic[2] + mk * (cc - c[2] * c[2]);
-    I[3] += Ic[3] - mk * c[0] * c[1];
-    I[4] += Ic[4] - mk * c[0] * c[2];
-    I[5] += Ic[5] - mk * c[1] * c[2];
+    m += sel * mk;
+    for (int e = 0; e < 3; ++e) h[e] += sel * (mk * c[e]);
+    I[0] += sel * (Ic[0] + mk * (cc - c[0] * c[0]));
+    I[1] += sel * (Ic[1] + mk * (cc - c[1] * c[1]));
+    I[2] += sel * (Ic[2] + mk * (cc - c[2] * c[2]));
+    I[3] += sel * (Ic[3] - mk * c[0] * c[1]);
+    I[4] += sel * (Ic[4] - mk * c[0] * c[2]);
+    I[5] += sel * (Ic[5] - mk * c[1] * c[2]);
   }
   *W.cm(i) = m;
   for (int e = 0; e < 3; ++e) W.ch(i)[e] = h[e];
@@ -1359,6 +1382,33 @@ MB_HD __forceinline__ double cost_activation(const Blk& b, const WVals& V, const
   return 0.5 * a;
 }
 
+// The long vector residuals (state, control) are summed lane-parallel in the calc:
+// wide_cost says which records (the first kMaxWide such records) take that path.
+constexpr int kMaxWide = 2;
+MB_HD __forceinline__ bool wide_cost(const CRec& C, int nwide) {
+  return (C.type() == C_STATE || C.type() == C_CONTROL) && nwide < kMaxWide;
+}
+// Lane l's share of twice the activation of a wide record: the rows i = l (mod L)
+// (lane 0 also the free-flyer block of a state residual, log6 of the base).
+MB_HD __forceinline__ double cost_activation_part(const Blk& b, const CRec& C, const double* x, const double* u,
+                                                  int nu, int l, int L) {
+  const Act act = cost_act(b, C, nu);
+  double a = 0.;
+  if (C.type() == C_STATE) {
+    const int ndx = 2 * b.nj, i0 = b.ff ? 6 : 0;
+    if (b.ff && l == 0) {
+      double Rr[9], pr[3], r[6];
+      ff_rel(C.d(), x, Rr, pr);
+      log6_t<double>(Rr, pr, r);
+      for (int e = 0; e < 6; ++e) a += act.value2(e, r[e]);
+    }
+    for (int i = i0 + l; i < ndx; i += L) a += act.value2(i, state_res(b, C.d(), x, i));
+  } else {
+    for (int i = l; i < nu; i += L) a += act.value2(i, u[i] - C.d()[i]);
+  }
+  return a;
+}
+
 // Cost value of the DAM (one thread; kinematics and velocities in V): sum of
 // weight * activation in record (name) order (cost-sum.hxx:89-117).
 MB_HD inline double cost_value(const Blk& b, const WVals& V, const double* x, const double* u, int nu) {
@@ -1475,7 +1525,7 @@ MB_HD __attribute__((always_inline)) inline void contact_jac_lane(const Blk& b, 
 }
 
 // Placements, world quantities, composite inertias and M (into A, zeroed by
-// the caller) for configuration q; `costs(wave, l)` runs on waves >= 2 in
+// the caller) for configuration q; `costs(wave, l)` runs on waves >= 1 in
 // the phase after the kinematics (nullptr-like no-op allowed).
 template <class X, class CostF>
 MB_HD inline void world_kinematics(const X& ex, const Blk& b, const WVals& W, const double* q, double* A, int lda,
@@ -1494,7 +1544,7 @@ MB_HD inline void world_kinematics(const X& ex, const Blk& b, const WVals& W, co
   ex.run([&](int lane) {
     const int wave = lane >> 6, l = lane & 63;
     if (wave == 0 && l < nj) w_composite(b, W, l);
-    if (wave >= 2) costs(wave, l);
+    if (wave >= 1) costs(wave, l);
   });
   ex.run([&](int lane) {
     if (lane < nj) w_crba_column(b, W, lane, A, lda);
@@ -1555,7 +1605,7 @@ MB_HD inline int64_t calc_work_doubles(int nj, int nc = 0) {
 //   lambda = -S^-1 (Jc z + a0),  a = z + Y lambda.
 // Needs >= 256 threads (4 waves): independent work of one phase runs on
 // different waves (divergent lanes of one wave would serialise) — wave 0 the
-// recursions, wave 1 composite inertias and CRBA, waves 2-3 the cost records.
+// recursions and composite inertias, waves 1-3 the cost records (state / control residuals row-parallel).
 // Every thread must call (phases end in barriers). x, u readable by all lanes;
 // writes xnext[0..nx) and returns the knot cost. `w`: calc_work_doubles(nj, nc).
 template <class X>
@@ -1582,12 +1632,21 @@ MB_HD inline double knot_calc_x(const X& ex, const double* P, int nx, const doub
     if (lane < nu) ub[lane] = use_u ? u[lane] : 0.;
     for (int e = lane; e < lda * ncol; e += ex.nt) A[e] = 0.;
   });
-  // cost records k on wave 2 + (k & 1), lane k >> 1, once the placements exist
+  // once the placements exist: the wide records (state / control residuals) row-parallel
+  // on waves 3 and 1, their lane partials into pb (free until the Gauss-Jordan); the
+  // other records one per lane of wave 2
   world_kinematics(ex, b, W, x, A, lda, [&](int wave, int l) {
     const double* cr = b.C;
+    int nn = 0, nw = 0;
     for (int k = 0; k < b.ncost; ++k) {
       const CRec C{cr};
-      if (wave == 2 + (k & 1) && l == (k >> 1)) cv[k] = C.weight() * cost_activation(b, W, C, x, ub, nu, false);
+      if (wide_cost(C, nw)) {
+        if (wave == (nw == 0 ? 3 : 1)) pb[64 * nw + l] = cost_activation_part(b, C, x, ub, nu, l, 64);
+        ++nw;
+      } else {
+        if (wave == 2 && l == nn) cv[k] = C.weight() * cost_activation(b, W, C, x, ub, nu, false);
+        ++nn;
+      }
       cr += C.size();
     }
     const int kc = l - 32;  // contact position terms on the upper half of wave 2
@@ -1612,9 +1671,17 @@ MB_HD inline double knot_calc_x(const X& ex, const double* P, int nx, const doub
     if (lane == 128) {
       double total = 0.;
       const double* cr = b.C;
+      int nw = 0;
       for (int k = 0; k < b.ncost; ++k) {
         const CRec C{cr};
-        total += cv[k];
+        if (wide_cost(C, nw)) {
+          double a = 0.;
+          for (int l = 0; l < 64; ++l) a += pb[64 * nw + l];
+          total += C.weight() * (0.5 * a);
+          ++nw;
+        } else {
+          total += cv[k];
+        }
         // force costs without active contact rows (lambda = 0)
         if (force_cost(C.type()) && nc == 0) total += C.weight() * force_cost_activation(b, C, nullptr, nu);
         // frame velocities, now that the body velocities exist (impulse knots: rejected by the host)
@@ -1624,7 +1691,7 @@ MB_HD inline double knot_calc_x(const X& ex, const double* P, int nx, const doub
       red[0] = total;
     }
   });
-  bool ok = gauss_jordan(ex, A, nj, lda, ncol, flag, pb);
+  bool ok = gauss_jordan<2>(ex, A, nj, lda, ncol, flag, pb);
   // z, then a (impulse: v+, in tau's slot; z = M^-1 M v = v)
   double* a = imp ? tau : A + (int64_t)lda * (nj + nc);
   if (nc > 0) {
@@ -1638,7 +1705,7 @@ MB_HD inline double knot_calc_x(const X& ex, const double* P, int nx, const doub
         S[e] = col < nc ? s + (row == col ? b.damping : 0.) : (imp ? (1. + b.r_coeff) * s : s + a0[row]);
       }
     });
-    ok = gauss_jordan(ex, S, nc, nc, nc + 1, flag, pb) && ok;
+    ok = gauss_jordan<1>(ex, S, nc, nc, nc + 1, flag, pb) && ok;
     ex.run([&](int lane) {
       if (lane == 64 && !imp) {  // contact-force costs (lambda = -S^-1 r, in S's last column, negated)
         double lamv[kMaxNc];
@@ -2207,7 +2274,7 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
       }
     });
   double* pb = red + 8;
-  bool ok = gauss_jordan(ex, A, nj, lda, 2 * nj, flag, pb);
+  bool ok = gauss_jordan<3>(ex, A, nj, lda, 2 * nj, flag, pb, nj);
   double* Minv = A + (int64_t)lda * nj;  // column-major nj x nj; with contacts: d a / d tau after the Schur step
   // z = (M + A)^-1 (tau - nle) (the acceleration without contacts); Y = Minv Jc^T
   ex.run([&](int lane) {
@@ -2248,7 +2315,7 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
         Sx[e] = v;
       }
     });
-    ok = gauss_jordan(ex, Sx, nc, nc, 2 * nc + 1, flag, pb) && ok;
+    ok = gauss_jordan<1>(ex, Sx, nc, nc, 2 * nc + 1, flag, pb) && ok;
     // lambda = -S^-1 r, a = z + Y lambda, H = Y S^-1 (= Kinv top-right)
     ex.run([&](int lane) {
       const double* Sinv = Sx + (int64_t)nc * nc;

@@ -77,7 +77,7 @@ extern "C" {
  *     then the payload, then the activation parameters:
  *       kind 0 ActivationModelQuad: ones(nr); 1 WeightedQuad: w(nr);
  *       2 QuadraticBarrier: lb(nr) ub(nr); 3 WeightedQuadraticBarrier: lb ub w
- *       (core/activations/*.hpp; the bounds already shrunk by beta)
+ *       (core/activations/<kind>.hpp; the bounds already shrunk by beta)
  *     payloads by type:
  *     1 CostModelState (state.hxx:130-169): xref(nx); r = diff(xref, x), nr = ndx
  *     2 CostModelControl (control.hxx:56-87): uref(nu)

@@ -1,12 +1,11 @@
-# round 2 (session 3): Gauss-Jordan slab skipping / per-site slab bound: probe phases, multibody GPU parity, C5 + C4 benches
+# round 2 (session 3): row-parallel state / control cost values and unrolled composite sums in the knot calc: probe, full GPU suite, C5 + C4 benches
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-O=gpurun_out/r02_9
+O=gpurun_out/r02_10
 mkdir -p $O
 export TMPDIR=/tmp
 (timeout -k 10 60 python tools/mb_probe.py C5_talos_walk 20 1 && timeout -k 10 60 python tools/mb_probe.py C5_talos_walk 20 2048 && timeout -k 10 60 python tools/mb_probe.py C4_solo12_trot 10 4096) > $O/probe.log 2>&1 || exit 1
-for c in "" comTrack right_sole_link_footTrack stateReg ctrlReg; do PROBE_COSTS=$c timeout -k 10 60 python tools/mb_probe.py C5_talos_walk 20 1 > "$O/probe_costs_$c.log" 2>&1 || exit 1; done
-timeout -k 10 400 python -u -m pytest -x -q -m gpu --timeout 240 --timeout-method thread tests/test_contact_gpu.py tests/test_gaits_gpu.py tests/test_freeflyer_gpu.py tests/test_multibody_gpu.py > $O/gpu_tests.log 2>&1
+timeout -k 10 400 python -u -m pytest -x -q -m gpu --timeout 240 --timeout-method thread tests > $O/gpu_tests.log 2>&1
 rc=$?; tail -n 2 $O/gpu_tests.log; [ $rc -ne 0 ] && exit $rc
 B="python bench.py --steps 5 --warmup 1 --no-cpu-baseline"
 timeout -k 10 300 $B > $O/c5.json 2> $O/c5.err || exit 1

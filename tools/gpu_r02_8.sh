@@ -1,11 +1,13 @@
-# LDS pivot-row Gauss-Jordan in calcDiff: phase probe, parity tests, C5 / C4 benches
+# round 2 (session 3): GPU suite, then the C5 rollout A/B (generic vs multibody-only kernel, 2 vs 1 waves/EU)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-mkdir -p gpurun_out/r02_8
-bash tools/gpu_probe.sh > gpurun_out/r02_8/probe.log 2>&1 || exit 1
-timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gaits_gpu.py tests/test_freeflyer_gpu.py tests/test_contact_gpu.py tests/test_multibody_gpu.py > gpurun_out/r02_8/tests.log 2>&1
-rc=$?; tail -2 gpurun_out/r02_8/tests.log; [ $rc -ne 0 ] && exit $rc
-for cfg in C5_talos_walk C4_solo12_trot; do
-  timeout -k 10 300 python bench.py --config $cfg --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/r02_8/bench_$cfg.json 2> gpurun_out/r02_8/bench_$cfg.err || exit 1
-  python -c "import json;d=json.load(open('gpurun_out/r02_8/bench_$cfg.json'));print('$cfg', d['value'], d['kernel_ms_per_step'])"
-done
+O=gpurun_out/r02_8
+mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 400 python -u -m pytest -x -q -m gpu --timeout 240 --timeout-method thread tests > $O/gpu_tests.log 2>&1
+rc=$?; tail -n 2 $O/gpu_tests.log; [ $rc -ne 0 ] && exit $rc
+B="python bench.py --steps 5 --warmup 1 --no-cpu-baseline"
+FDDP_FWD_MB=0 timeout -k 10 300 $B > $O/c5_generic.json 2> $O/c5_generic.err || exit 1
+timeout -k 10 300 $B > $O/c5_mb.json 2> $O/c5_mb.err || exit 1
+CROCODDYL_AMD_LIB=$PWD/crocoddyl_amd/lib/libfddp_hip_wpe1.so timeout -k 10 300 $B > $O/c5_mb_wpe1.json 2> $O/c5_mb_wpe1.err || exit 1
+for f in generic mb mb_wpe1; do python -c "import json,sys;d=json.load(open('$O/c5_$f.json'));print('$f',d['value'],d['kernel_ms_per_step'])"; done

@@ -6,6 +6,7 @@
 // knot-parallel kernel).
 #include <hip/hip_runtime.h>
 #include <cstdio>
+#include <cstdlib>
 #include <vector>
 #include "../crocoddyl_amd/csrc/multibody.hpp"
 
@@ -51,9 +52,10 @@ struct StampExec {
 };
 
 // found by argument-dependent lookup (StampExec is in the global namespace)
-__device__ inline bool gauss_jordan(const StampExec& ex, double* A, int nr, int ld, int nc, int* flag, double* pb) {
-  const bool ok = (nr <= 64 && nc <= 3 * 8 * (int)(blockDim.x >> 6)) ? gauss_jordan_rows<8, 3>(A, nr, ld, nc, pb, flag)
-                                                                      : gauss_jordan_dev(A, nr, ld, nc, flag);
+template <int SPW>
+__device__ inline bool gauss_jordan(const StampExec& ex, double* A, int nr, int ld, int nc, int* flag, double* pb,
+                                    int id0 = 1 << 30) {
+  const bool ok = gauss_jordan_regs<SPW>(A, nr, ld, nc, flag, pb, id0);
   ex.mark();
   return ok;
 }
@@ -84,6 +86,10 @@ __global__ __launch_bounds__(kMbDiffNT) void probe_diff(const double* Pg, int nx
     knot_calc_diff_x(ex, P, nx, m, xg, ug, use_u != 0, sm, o, o + n * n, o + n * n + n * m, o + 2 * n * n + n * m,
                      o + 2 * n * n + 2 * n * m, o + 2 * n * n + 2 * n * m + m * m, o + 2 * n * n + 2 * n * m + m * m + n,
                      o + 2 * n * n + 2 * n * m + m * m + n + m, o + 2 * n * n + 2 * n * m + m * m + n + m + nx);
+  else  // without the fused calc's outputs (next state, cost)
+    knot_calc_diff_x(ex, P, nx, m, xg, ug, use_u != 0, sm, o, o + n * n, o + n * n + n * m, o + 2 * n * n + n * m,
+                     o + 2 * n * n + 2 * n * m, o + 2 * n * n + 2 * n * m + m * m, o + 2 * n * n + 2 * n * m + m * m + n,
+                     nullptr, nullptr);
   __syncthreads();
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     const unsigned long long c = st[0] < 254 ? st[0] : 254;
@@ -170,7 +176,7 @@ int main(int argc, char** argv) {
       CK(hipEventRecord(e0));
       if (which == 0)
         hipLaunchKernelGGL(probe_diff, dim3(nwg), dim3(kMbDiffNT), smd, 0, dP, nx, m, dx, du, nu > 0 ? 1 : 0, dout, so,
-                           dst, 0);
+                           dst, getenv("PROBE_DIFF_NOCOST") ? 1 : 0);
       else
         hipLaunchKernelGGL(probe_calc, dim3(nwg), dim3(256), smc, 0, dP, nx, dx, du, nu > 0 ? 1 : 0, dout, dst);
       CK(hipEventRecord(e1));

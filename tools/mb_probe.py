@@ -1,5 +1,7 @@
 """Diagnostic (not a test): writes one knot of a config (block, x, u) for
-tools/mb_probe and runs it. Usage: python tools/mb_probe.py <config> <knot> <nwg>"""
+tools/mb_probe and runs it. Usage: python tools/mb_probe.py <config> <knot> <nwg>
+(PROBE_COSTS=a,b keeps only those cost records active; PROBE_COSTS= none).
+"""
 import os
 import subprocess
 import sys
@@ -13,6 +15,12 @@ from crocoddyl_amd import synthetic  # noqa: E402
 cfg, t, nwg = sys.argv[1], int(sys.argv[2]), sys.argv[3]
 x0s, running, terminal = synthetic.build(cfg, B=1)
 m = running[t] if t < len(running) else terminal
+keep = os.environ.get("PROBE_COSTS")  # comma-separated cost names to keep active ("" = none)
+if keep is not None:
+    dam = getattr(m, "differential", m)
+    for name, it in dam.costs.costs.items():
+        it.active = name in keep.split(",")
+    print("costs kept:", [n for n, it in dam.costs.costs.items() if it.active])
 kind, nu, blk = m.pack()
 blk = np.ascontiguousarray(blk[0], np.float64)
 mm = max(r.nu for r in running)
