@@ -652,6 +652,38 @@ struct TrialOut {
   }
 };
 
+// sum_j K(i, j) dx_j (K row-major m x n rows of the gains, read from HBM), summed in
+// j order as the reference's GEMV; the loads of 8 consecutive j are issued before
+// their FMAs, so a lane waits for one round trip per 8 entries instead of per entry.
+template <class F>
+__device__ __forceinline__ double gains_dot(const double* K, int m, int i, int n, F dx) {
+  double s = 0.;
+  int j = 0;
+#pragma unroll 1
+  for (; j + 8 <= n; j += 8) {
+    double k[8], d[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      k[q] = K[(int64_t)(j + q) * m + i];
+      d[q] = dx(j + q);
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) s += k[q] * d[q];
+  }
+  if (j < n) {  // the tail as one guarded batch
+    double k[8], d[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      k[q] = j + q < n ? K[(int64_t)(j + q) * m + i] : 0.;
+      d[q] = j + q < n ? dx(j + q) : 0.;
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      if (j + q < n) s += k[q] * d[q];
+  }
+  return s;
+}
+
 template <int NT, bool MB = false>
 __device__ __forceinline__ bool fwd_trial(const Dev& D, int b, const ElemState& s, double alpha, double* xv, double* uv, double* xn,
                           double* red, int* flag, double& cost_try, double& dv, double* pl, int64_t pcap,
@@ -708,11 +740,8 @@ __device__ __forceinline__ bool fwd_trial(const Dev& D, int b, const ElemState& 
       for (int i = tid; i < m; i += NT) {
         double v = 0.;
         if (i < nu) {
-          double kd2 = 0.;
-          if (ff)
-            for (int j = 0; j < n; ++j) kd2 += K[(int64_t)j * m + i] * dxv[j];
-          else
-            for (int j = 0; j < n; ++j) kd2 += K[(int64_t)j * m + i] * (xv[j] - xs[j]);
+          const double kd2 = ff ? gains_dot(K, m, i, n, [&](int j) { return dxv[j]; })
+                                : gains_dot(K, m, i, n, [&](int j) { return xv[j] - xs[j]; });
           v = (us[i] - kv[i] * alpha) - kd2;
           // SolverBoxFDDP::forwardPass: cwiseMax(u_lb).cwiseMin(u_ub) (box-fddp.cpp:100-102)
           if (D.box_knot(b, t)) v = std_min(std_max(v, D.ulb[D.run(b, t) * D.sM + i]), D.uub[D.run(b, t) * D.sM + i]);

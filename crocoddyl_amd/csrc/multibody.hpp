@@ -37,6 +37,20 @@
 // on the CPU against the oracle (tests/test_multibody_host.py).
 #define MB_HD __host__ __device__
 
+// On the device every multibody record (parameter block) and the work area live in
+// LDS; the record / work-area accessors re-assert it where the pointer is formed, so
+// the accesses compile to ds_* even where the address-space inference loses the
+// entry's assumption (flat accesses to LDS pay a full round trip each). The host
+// emulation (tests/cpp/mb_host.cpp) reads ordinary memory.
+template <class T>
+MB_HD __forceinline__ T* mb_lds(T* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return ::fddp::lds_ptr(p);
+#else
+  return p;
+#endif
+}
+
 namespace fddp {
 namespace mb {
 
@@ -235,7 +249,7 @@ MB_HD __forceinline__ double dot6(const double* a, const double* b) {
 // R(9) p(3), mass, CoM(3), I(6)]
 struct JRec {
   const double* r;
-  MB_HD JRec(const Blk& b, int i) : r(b.J + (int64_t)kJRec * i) {}
+  MB_HD JRec(const Blk& b, int i) : r(mb_lds(b.J + (int64_t)kJRec * i)) {}
   MB_HD int type() const { return (int)r[0]; }
   MB_HD int parent() const { return (int)r[1]; }
   MB_HD const double* axis() const { return r + 2; }
@@ -432,6 +446,8 @@ MB_HD __forceinline__ int lda_of(int nj) { return nj | 1; }
 // rows, loads first, so the LDS round trips overlap.
 __device__ __forceinline__ bool gauss_jordan_dev(double* A, int nr, int ld, int nc, int* flag) {
   const int tid = (int)threadIdx.x, nt = (int)blockDim.x;
+  A = lds_ptr(A);
+  flag = lds_ptr(flag);
   __syncthreads();
   bool bad = false;
 #pragma unroll 1
@@ -489,6 +505,9 @@ __device__ __forceinline__ bool gauss_jordan_rows(double* A, int nr, int ld, int
                                                   int id0 = 1 << 30) {
   const int tid = (int)threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = (int)(blockDim.x >> 6);
   const int nslab = (nc + CPW - 1) / CPW;
+  A = lds_ptr(A);
+  pb = lds_ptr(pb);
+  flag = lds_ptr(flag);
   double v[SPW][CPW];
   __syncthreads();
 #pragma unroll
@@ -834,7 +853,7 @@ constexpr int kMaxCosts = 64;
 struct WVals {
   double* base;
   int nj;
-  MB_HD double* R(int i) const { return base + kWPerJoint * i; }  // liMi rotation
+  MB_HD double* R(int i) const { return mb_lds(base + kWPerJoint * i); }  // liMi rotation
   MB_HD double* p(int i) const { return R(i) + 9; }
   MB_HD double* oR(int i) const { return R(i) + 12; }  // oMi (also pointer-jumping buffer A)
   MB_HD double* op(int i) const { return R(i) + 21; }
@@ -855,7 +874,7 @@ struct WVals {
   MB_HD double* jB(int i) const { return R(i) + 87; }
   MB_HD double* fb(int i) const { return R(i) + 90; }  // body force I a + v x* I v
   MB_HD Mask* anc(int i) const { return (Mask*)(base + kWPerJoint * nj) + i; }  // ancestors-or-self dofs
-  MB_HD double* root_a() const { return base + kWPerJoint * nj + nj; }
+  MB_HD double* root_a() const { return mb_lds(base + kWPerJoint * nj + nj); }
   MB_HD static int64_t doubles(int nj) { return (int64_t)kWPerJoint * nj + nj + 6; }
 };
 
@@ -1106,10 +1125,10 @@ MB_HD inline void w_crba_column(const Blk& b, const WVals& W, int j, double* A, 
 // Cost records
 struct CRec {
   const double* r;
-  MB_HD int type() const { return (int)r[0]; }
-  MB_HD double weight() const { return r[1]; }
-  MB_HD int size() const { return (int)r[3]; }
-  MB_HD const double* d() const { return r + kCHdr; }
+  MB_HD int type() const { return (int)mb_lds(r)[0]; }
+  MB_HD double weight() const { return mb_lds(r)[1]; }
+  MB_HD int size() const { return (int)mb_lds(r)[3]; }
+  MB_HD const double* d() const { return mb_lds(r + kCHdr); }
 };
 
 // dof carrying the frame of a frame / contact payload d = [joint record, R 9, p 3, ...]
@@ -1195,17 +1214,20 @@ struct Act {
   int kind, nr;
   const double* p;
   MB_HD __forceinline__ double value2(int i, double r) const {
+    const double* p = mb_lds(this->p);
     if (kind <= A_WEIGHTED_QUAD) return p[i] * r * r;
     const double rl = fmin(r - p[i], 0.), ru = fmax(r - p[nr + i], 0.);
     const double v = rl * rl + ru * ru;
     return kind == A_WEIGHTED_QUAD_BARRIER ? p[2 * nr + i] * p[2 * nr + i] * v : v;
   }
   MB_HD __forceinline__ double sgrad(int i, double r, double X) const {
+    const double* p = mb_lds(this->p);
     if (kind <= A_WEIGHTED_QUAD) return X * p[i] * r;
     const double g = fmin(r - p[i], 0.) + fmax(r - p[nr + i], 0.);
     return X * (kind == A_WEIGHTED_QUAD_BARRIER ? p[2 * nr + i] * p[2 * nr + i] * g : g);
   }
   MB_HD __forceinline__ double hess(int i, double r) const {
+    const double* p = mb_lds(this->p);
     if (kind <= A_WEIGHTED_QUAD) return p[i];
     const double h = (r - p[i] <= 0.) ? 1. : ((r - p[nr + i] >= 0.) ? 1. : 0.);
     return kind == A_WEIGHTED_QUAD_BARRIER ? p[2 * nr + i] * h : h;
@@ -2433,14 +2455,25 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
   double* dfu = w + l.dfu;
   // da = -Kinv_tl dtau - H da0 (impulse: -G dtau_dq - H dv0_dq on the q columns)
   ex.run([&](int lane) {
-    for (int e = lane; e < nj * L; e += ex.nt) {
-      const int r = e / L, c = e % L;
-      double s = 0.;
-      if (!imp || c < nj) {
-        for (int k = 0; k < nj; ++k) s += Minv[(int64_t)k * lda + r] * dtau[(int64_t)k * L + c];
-        for (int k = 0; k < nc; ++k) s += H[(int64_t)k * nj + r] * da0[(int64_t)k * L + c];
+    // two entries per lane at a time: two independent dot-product chains, so the LDS
+    // loads of one overlap the other's FMAs (each entry's summation order unchanged)
+    const int ne = nj * L;
+    for (int e0 = lane; e0 < ne; e0 += 2 * ex.nt) {
+      const int e1 = e0 + ex.nt < ne ? e0 + ex.nt : e0;
+      const int r0 = e0 / L, c0 = e0 % L, r1 = e1 / L, c1 = e1 % L;
+      double s0 = 0., s1 = 0.;
+      for (int k = 0; k < nj; ++k) {
+        s0 += Minv[(int64_t)k * lda + r0] * dtau[(int64_t)k * L + c0];
+        s1 += Minv[(int64_t)k * lda + r1] * dtau[(int64_t)k * L + c1];
       }
-      da[e] = ok ? -s : NAN;
+      for (int k = 0; k < nc; ++k) {
+        s0 += H[(int64_t)k * nj + r0] * da0[(int64_t)k * L + c0];
+        s1 += H[(int64_t)k * nj + r1] * da0[(int64_t)k * L + c1];
+      }
+      if (imp && c0 >= nj) s0 = 0.;
+      if (imp && c1 >= nj) s1 = 0.;
+      da[e0] = ok ? -s0 : NAN;
+      if (e1 != e0) da[e1] = ok ? -s1 : NAN;
     }
     if (fd) {
       const double* Sinv = Sx + (int64_t)nc * nc;
@@ -2600,9 +2633,21 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
       Rm[e] = c < L + nu ? v : 0.;
     }
   });
+  const double *const Rm_ = Rm, *const ch_ = ch, *const cg_ = cg, *const cam_ = cam, *const cav_ = cav, *const P_ = P,
+                      *const x_ = x, *const u_ = u;
   // Gauss-Newton blocks (cost-sum.hxx:122-160) as a small GEMM over the rows, in
   // cost order: Lxx / Lxu / Luu entries four rows i at a time, then Lx / Lu.
   ex.run([&](int lane) {
+    // the operands re-asserted as LDS where they are used (the inference does not carry
+    // the entry's assumption this far: the loads were flat, each one a full round trip)
+    const double* const Rm = ex.lds(Rm_);
+    const double* const ch = ex.lds(ch_);
+    const double* const cg = ex.lds(cg_);
+    const double* const cam = ex.lds(cam_);
+    const double* const cav = ex.lds(cav_);
+    const double* const P = ex.lds(P_);
+    const double* const x = ex.lds(x_);
+    const double* const u = ex.lds(u_);
     const int n4 = (n + 3) / 4, m4 = (m + 3) / 4;
     const int tx = n4 * n, txu = n4 * m, tuu = m4 * m;
     for (int task = lane; task < tx + txu + tuu; task += ex.nt) {
@@ -2686,39 +2731,62 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
       (isu ? Lu : Lx)[j] = integ ? sc * acc : acc;
     }
     // the fused calc's cost (cost-sum.hxx:89-117): record k's weighted activation on
-    // lane nt-1-k (the lanes with the fewest GEMM tasks), into the dead pivot buffer;
-    // jac-cost residuals from the Jacobian phase
-    if (cost_out && ex.nt - 1 - lane < b.ncost) {
-      const int k = ex.nt - 1 - lane;
+    // lane nt-1-k (the lanes with the fewest GEMM tasks), into the dead pivot buffer
+    // (pb[0, 64)); jac-cost residuals from the Jacobian phase.
+    // The wide records (state / control, wide_cost) row-parallel instead: 32 lanes each
+    // from lane 128 on, their partials into pb[64 + 32 w + l], summed below.
+    if (cost_out) {
       const double* cr = b.C;
-      int f = 0;
-      for (int q = 0; q < k; ++q) {
-        f += jac_cost(b, CRec{cr}.type()) ? 1 : 0;
-        cr += CRec{cr}.size();
+      int f = 0, nw = 0;
+      for (int k = 0; k < b.ncost; ++k) {
+        const CRec C{cr};
+        const int t = C.type();
+        const bool wide = wide_cost(C, nw);
+        const int wl = lane - 128 - 32 * nw;  // this lane's share of wide record nw
+        if (wide ? (wl >= 0 && wl < 32) : lane == ex.nt - 1 - k) {
+          const Act act = cost_act(b, C, nu);
+          double a = 0.;
+          if (jac_cost(b, t) && (!wide || wl == 0)) {
+            const int nr = jac_rows(t);
+            for (int i = 0; i < nr; ++i) a += act.value2(i, rf[6 * f + i]);
+          }
+          if (t == C_STATE) {
+            for (int i = (b.ff ? 6 : 0) + (wide ? wl : 0); i < n; i += wide ? 32 : 1)
+              a += act.value2(i, state_res(b, C.d(), x, i));
+          } else if (t == C_CONTROL) {
+            for (int i = wide ? wl : 0; i < nu; i += wide ? 32 : 1) a += act.value2(i, u[i] - C.d()[i]);
+          } else if (force_cost(t)) {
+            a = 2. * force_cost_activation(b, C, lam, nu);
+          }
+          if (wide)
+            pb[64 + 32 * nw + wl] = a;
+          else
+            pb[k] = C.weight() * (0.5 * a);
+        }
+        f += jac_cost(b, t) ? 1 : 0;
+        nw += wide ? 1 : 0;
+        cr += C.size();
       }
-      const CRec C{cr};
-      const int t = C.type();
-      const Act act = cost_act(b, C, nu);
-      double a = 0.;
-      if (jac_cost(b, t)) {
-        const int nr = jac_rows(t);
-        for (int i = 0; i < nr; ++i) a += act.value2(i, rf[6 * f + i]);
-      }
-      if (t == C_STATE) {
-        for (int i = b.ff ? 6 : 0; i < n; ++i) a += act.value2(i, state_res(b, C.d(), x, i));
-      } else if (t == C_CONTROL) {
-        for (int i = 0; i < nu; ++i) a += act.value2(i, u[i] - C.d()[i]);
-      } else if (force_cost(t)) {
-        a = 2. * force_cost_activation(b, C, lam, nu);
-      }
-      pb[k] = C.weight() * (0.5 * a);
     }
   });
   if (cost_out)  // summed in cost order
     ex.run([&](int lane) {
       if (lane != 0) return;
       double total = 0.;
-      for (int k = 0; k < b.ncost; ++k) total += pb[k];
+      const double* cr = b.C;
+      int nw = 0;
+      for (int k = 0; k < b.ncost; ++k) {
+        const CRec C{cr};
+        if (wide_cost(C, nw)) {
+          double a = 0.;
+          for (int l = 0; l < 32; ++l) a += pb[64 + 32 * nw + l];
+          total += C.weight() * (0.5 * a);
+          ++nw;
+        } else {
+          total += pb[k];
+        }
+        cr += C.size();
+      }
       *cost_out = integ ? dt * total : total;
     });
   (void)nx;
