@@ -303,6 +303,10 @@ def main():
         psz = mean_param_doubles(problem)
         rooflines = {"backward": (bwd_ms, roof_bwd)}
         fw_ms, fw_n = timing["forward"]
+        fwd_pmc = ((pmc or {}).get("kernels", {}).get("forward") or None)
+        n_alphas = 10  # the reference's default alphas (solver-base.cpp: 2^-k, k < 10)
+        nv = n // 2
+        ls_par = int(os.environ.get("CROCODDYL_AMD_LS_PAR", "0")) or (4 if nv >= 24 else 1)
         if fw_n:
             kt = float(np.sum(trials)) * (T + 1)  # knot-trials of one line search (last step's trials)
             Yf = rollout_bytes_per_knot_trial(nx, n, m, psz) * kt
@@ -311,7 +315,9 @@ def main():
                 "kernel": "line-search rollout (forward_kernel + ls_select_kernel, knot calc per trial)",
                 "bound": "hbm", "achieved": round(a, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                 "frac": round(a / HBM_PEAK_GBPS, 5),
-                "traffic": None,  # per group dispatch in profiles/pmc_backward.json ("forward"); a call is 3
+                # HBM bytes per call: the PMC mean per group dispatch x the group dispatches of
+                # one line search (npar trials per group, as fddp_hip.hip chooses it)
+                "traffic": (fwd_pmc["hbm_bytes_per_launch"] * -(-n_alphas // ls_par) if fwd_pmc else None),
                 "algorithmic_bytes_per_launch": int(Yf),
                 "knot_trials_per_launch": int(kt), "avg_launch_ms": round(fw_ms / fw_n, 3),
                 "timer": "HIP events on the solver stream"})

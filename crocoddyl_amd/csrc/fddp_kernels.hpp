@@ -23,17 +23,19 @@ __device__ inline int64_t block_doubles_dev(int kind, int nx, int nu, const doub
 // StateMultibody with a free-flyer root (nx = ndx + 1: x = (p, quat xyzw, q_rest, v)),
 // otherwise a Euclidean state (StateVector, or StateMultibody over revolute joints).
 // diff(x0, x1) / integrate(x, dx) (multibody.hxx:54-91, euclidean.hxx:28-61) over the
-// threads of a workgroup; thread 0 does the free-flyer's SE(3) part. out may not
-// alias the inputs. No barrier inside.
+// threads of a workgroup; thread `first` (0 by default) does the free-flyer's SE(3)
+// part, so two differences of one phase can run their logs on different waves. out
+// may not alias the inputs. No barrier inside.
 template <int NT>
-__device__ __forceinline__ void state_diff_wg(const Dev& D, const double* x0, const double* x1, double* out) {
+__device__ __forceinline__ void state_diff_wg(const Dev& D, const double* x0, const double* x1, double* out,
+                                              int first = 0) {
   const int n = D.n;
   if (D.nx == n) {
     for (int i = threadIdx.x; i < n; i += NT) out[i] = x1[i] - x0[i];
     return;
   }
   const int nv = n / 2, nq = D.nx - nv;
-  for (int i = threadIdx.x; i < n; i += NT) {
+  for (int i = ((int)threadIdx.x + NT - first) % NT; i < n; i += NT) {
     if (i < 6) {
       if (i == 0) mb::ff_difference(x0, x1, out);
     } else if (i < nv) {
@@ -652,6 +654,10 @@ struct TrialOut {
   }
 };
 
+// A store of the rollout's trial trajectories / per-knot terms (HBM) through a global
+// pointer: a flat store would make the wave's next LDS access wait for it.
+__device__ __forceinline__ void gstore(double* p, double v) { *(__attribute__((address_space(1))) double*)p = v; }
+
 // sum_j K(i, j) dx_j (K row-major m x n rows of the gains, read from HBM), summed in
 // j order as the reference's GEMV; the loads of 8 consecutive j are issued before
 // their FMAs, so a lane waits for one round trip per 8 entries instead of per entry.
@@ -710,7 +716,7 @@ __device__ __forceinline__ bool fwd_trial(const Dev& D, int b, const ElemState& 
       for (int i = tid; i < nx; i += NT) {
         const double v = full ? xn[i] : xn[i] + fs[i] * (alpha - 1);
         xv[i] = v;
-        xt[i] = v;
+        gstore(xt + i, v);
         if (!feas) pd += (v - xs[i]) * D.Vxxfs[kk * D.sN + i];  // -fs^T Vxx diff(xs_try, xs)
       }
       __syncthreads();
@@ -720,9 +726,9 @@ __device__ __forceinline__ bool fwd_trial(const Dev& D, int b, const ElemState& 
       else
         state_integrate_wg<NT>(D, xn, fs, alpha - 1, xv);
       __syncthreads();
-      for (int i = tid; i < nx; i += NT) xt[i] = xv[i];
+      for (int i = tid; i < nx; i += NT) gstore(xt + i, xv[i]);
       state_diff_wg<NT>(D, xs, xv, dxv);
-      if (!feas) state_diff_wg<NT>(D, xv, xs, dxv + D.sN);
+      if (!feas) state_diff_wg<NT>(D, xv, xs, dxv + D.sN, kWave);
       __syncthreads();
       if (!feas)
         for (int i = tid; i < n; i += NT) pd -= dxv[D.sN + i] * D.Vxxfs[kk * D.sN + i];
@@ -747,7 +753,7 @@ __device__ __forceinline__ bool fwd_trial(const Dev& D, int b, const ElemState& 
           if (D.box_knot(b, t)) v = std_min(std_max(v, D.ulb[D.run(b, t) * D.sM + i]), D.uub[D.run(b, t) * D.sM + i]);
         }
         uv[i] = v;
-        ut[i] = v;
+        gstore(ut + i, v);
       }
       __syncthreads();
     }
@@ -756,14 +762,14 @@ __device__ __forceinline__ bool fwd_trial(const Dev& D, int b, const ElemState& 
     if (running) {
       double* xo = out.xnext + D.run(b, t) * D.sX;
       for (int i = tid; i < nx; i += NT) {
-        xo[i] = xn[i];
+        gstore(xo + i, xn[i]);
         bad |= bad_entry(xn[i]);
       }
     }
     if (!feas) pd = wg_sum<NT>(pd, red);
     if (tid == 0) {
-      out.kcost[kk] = ct;
-      dvp[t] = pd;
+      gstore(out.kcost + kk, ct);
+      gstore(dvp + t, pd);
     }
     cost_try += ct;
     bad |= raise_if_nan(cost_try);

@@ -42,6 +42,16 @@
 // the accesses compile to ds_* even where the address-space inference loses the
 // entry's assumption (flat accesses to LDS pay a full round trip each). The host
 // emulation (tests/cpp/mb_host.cpp) reads ordinary memory.
+// A store to the caller's output blocks, which are in HBM: through a global pointer,
+// so the compiler emits global_store instead of a flat store that every later LDS
+// access of the wave must wait behind (flat may alias LDS).
+MB_HD __forceinline__ void mb_gstore(double* p, double v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  *(__attribute__((address_space(1))) double*)p = v;
+#else
+  *p = v;
+#endif
+}
 template <class T>
 MB_HD __forceinline__ T* mb_lds(T* p) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -1051,10 +1061,16 @@ MB_HD __forceinline__ void comp_mul(const WVals& W, int i, const double* x, doub
 MB_HD inline void w_velocity(const WVals& W, const double* qd, int i) {
   double v[6] = {0., 0., 0., 0., 0., 0.};
   const Mask am = *W.anc(i);
+  // every dof's terms loaded, the others' selected away (not branched around), so the
+  // unrolled iterations' LDS loads overlap; the sums keep their order
+#pragma unroll 2
   for (int k = 0; k < W.nj; ++k) {
-    if (!((am >> k) & 1ull)) continue;
+    const bool in = (am >> k) & 1ull;
     const double w = qd[k];
-    for (int e = 0; e < 6; ++e) v[e] += W.S(k)[e] * w;
+    for (int e = 0; e < 6; ++e) {
+      const double t = W.S(k)[e] * w;
+      v[e] += in ? t : 0.;
+    }
   }
   for (int e = 0; e < 6; ++e) W.v(i)[e] = v[e];
 }
@@ -1078,9 +1094,13 @@ MB_HD inline void w_accel_force(const WVals& W, int i, const double* fx = nullpt
   double a[6];
   for (int e = 0; e < 6; ++e) a[e] = W.root_a()[e];
   const Mask am = *W.anc(i);
-  for (int k = 0; k < W.nj; ++k) {
-    if (!((am >> k) & 1ull)) continue;
-    for (int e = 0; e < 6; ++e) a[e] += W.cq(k)[e];
+#pragma unroll 2
+  for (int k = 0; k < W.nj; ++k) {  // (selected, not branched: as w_velocity)
+    const bool in = (am >> k) & 1ull;
+    for (int e = 0; e < 6; ++e) {
+      const double t = W.cq(k)[e];
+      a[e] += in ? t : 0.;
+    }
   }
   double v[6], f[6], Iv[6], t6[6], c[3], I6[6];
   for (int e = 0; e < 6; ++e) {
@@ -1099,9 +1119,13 @@ MB_HD inline void w_accel_force(const WVals& W, int i, const double* fx = nullpt
 // lane i < nj: F_i = sum over the subtree of the body forces, tau_i = S_i . F_i
 MB_HD inline void w_joint_force(const Blk& b, const WVals& W, double* tau, int i) {
   double F[6] = {0., 0., 0., 0., 0., 0.};
-  for (int k = 0; k < b.nj; ++k) {
-    if (!((*W.anc(k) >> i) & 1ull)) continue;
-    for (int e = 0; e < 6; ++e) F[e] += W.fb(k)[e];
+#pragma unroll 2
+  for (int k = 0; k < b.nj; ++k) {  // (selected, not branched: as w_velocity)
+    const bool in = (*W.anc(k) >> i) & 1ull;
+    for (int e = 0; e < 6; ++e) {
+      const double t = W.fb(k)[e];
+      F[e] += in ? t : 0.;
+    }
   }
   for (int e = 0; e < 6; ++e) W.F(i)[e] = F[e];
   tau[i] = dot6(W.S(i), F);
@@ -2418,13 +2442,19 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
       if (lane < nj) subtree_nh_lane(b, W, lane, dtau, nsub);
     });
   }
+  // the velocity-product maps on the lower half of the workgroup, the cost / Euler
+  // Jacobians on the upper half (independent: they run side by side)
   ex.run([&](int lane) {
-    if (lane >= nj) return;
-    if (!imp) qp_lane_ns(W, lane, nsub, qp);
+    const int h = ex.nt / 2;
+    if (lane < h) {
+      if (!imp)
+        for (int j = lane; j < nj; j += h) qp_lane_ns(W, j, nsub, qp);
+      return;
+    }
     double dq[6];
     if (ffe)
       for (int e = 0; e < 6; ++e) dq[e] = x[nq + e] * dt + av[e] * dt2;
-    jac_lane(b, W, x, lane, Jf, jw, rf, ffe ? dq : nullptr, Je, Ai);
+    for (int j = lane - h; j < nj; j += h) jac_lane(b, W, x, j, Jf, jw, rf, ffe ? dq : nullptr, Je, Ai);
   });
   if (imp) {  // V = 0 in the impulse RNEA: P_k = 0, Q_k = Ycrb_k S_k
     ex.run([&](int lane) {
@@ -2434,10 +2464,13 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
     });
   }
   // tangent directions: dtau/dx (impulse: q only) and da0/dx
+  // (dtau on the lower half of the workgroup, da0 on the upper half, side by side)
   ex.run([&](int lane) {
-    for (int dd = lane; dd < (imp ? nj : L); dd += ex.nt) {
-      dtau_direction(b, W, qp, dd, L, dtau, imp ? nullptr : nsub);
-      if (nc > 0 && !imp) contact_direction(b, W, dd, L, da0);
+    const int h = ex.nt / 2;
+    if (lane < h) {
+      for (int dd = lane; dd < (imp ? nj : L); dd += h) dtau_direction(b, W, qp, dd, L, dtau, imp ? nullptr : nsub);
+    } else if (nc > 0 && !imp) {
+      for (int dd = lane - h; dd < L; dd += h) contact_direction(b, W, dd, L, da0);
     }
   });
   if (imp && nc > 0) {  // velocities at v+, then d(Jc v+)/dq
@@ -2532,7 +2565,7 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
       } else {
         f = c == i ? 1. : 0.;
       }
-      Fx[e] = f;
+      mb_gstore(Fx + e, f);
     }
     // Fu(i, c) = Kinv_tl(i mod nj, nun + c) dt^2 | dt (dtau/du = [0; I]), Jexp6 on
     // the free-flyer rows; Lxu from the contact-force costs
@@ -2549,7 +2582,7 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
           f = i < nj ? mi * dt2 : mi * dt;
         }
       }
-      Fu[e] = f;
+      mb_gstore(Fu + e, f);
     }
     // the cost-derivative table (last thread): groups in cost (name) order, each the
     // rows of one cost with a dense residual Jacobian, or the diagonal of a state /
@@ -2670,18 +2703,30 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
         if (r0 >= 0) {
           const int r1 = (int)cg[4 * g + 1];
           double s2[4] = {0., 0., 0., 0.};
-#pragma unroll 4
-          for (int r = r0; r < r1; ++r) {
-            const double* Rr = Rm + (int64_t)r * ldR;
-            const double rj = jin ? Rr[cj] : 0.;
-            const double hr = ch[r];
-            // rows are 16-B aligned (ldR even) and ci is a multiple of 4 (blk 2: L even)
-            const double2 a01 = *reinterpret_cast<const double2*>(Rr + ci);
-            const double2 a23 = *reinterpret_cast<const double2*>(Rr + ci + 2);
-            s2[0] += a01.x * hr * rj;
-            s2[1] += a01.y * hr * rj;
-            s2[2] += a23.x * hr * rj;
-            s2[3] += a23.y * hr * rj;
+          // rows in guarded batches of 4, loads first: a group (3-6 rows here) costs one
+          // or two LDS round trips instead of one per row (the sums keep row order)
+#pragma unroll 1
+          for (int rb = r0; rb < r1; rb += 4) {
+            double2 a01[4], a23[4];
+            double hr[4], rj[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const int r = rb + q < r1 ? rb + q : r0;
+              const double* Rr = Rm + (int64_t)r * ldR;
+              // rows are 16-B aligned (ldR even) and ci is a multiple of 4 (blk 2: L even)
+              a01[q] = *reinterpret_cast<const double2*>(Rr + ci);
+              a23[q] = *reinterpret_cast<const double2*>(Rr + ci + 2);
+              hr[q] = ch[r];
+              rj[q] = jin ? Rr[cj] : 0.;
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              if (rb + q >= r1) break;
+              s2[0] += a01[q].x * hr[q] * rj[q];
+              s2[1] += a01[q].y * hr[q] * rj[q];
+              s2[2] += a23[q].x * hr[q] * rj[q];
+              s2[3] += a23[q].y * hr[q] * rj[q];
+            }
           }
           const double wt = C.weight();
 #pragma unroll
@@ -2704,7 +2749,7 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
         const int i = i0 + q;
         if (i >= rows) continue;
         const bool zero = (blk == 1 && j >= nu) || (blk == 2 && (i >= nu || j >= nu));
-        out[(int64_t)j * rows + i] = zero ? 0. : (blk == 1 || integ ? sc * lv[q] : lv[q]);
+        mb_gstore(out + (int64_t)j * rows + i, zero ? 0. : (blk == 1 || integ ? sc * lv[q] : lv[q]));
       }
     }
     // Lx (x columns) and Lu (u columns): R^T Ar in cost order
@@ -2719,8 +2764,23 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
           const CRec C{P + (int64_t)cg[4 * g + 2]};
           const double wt = C.weight();
           if (r0 >= 0) {
-            for (int r = r0; r < (int)cg[4 * g + 1]; ++r)
-              acc += wt * Rm[(int64_t)r * ldR + cc] * cam[r] * cav[r];
+            const int r1 = (int)cg[4 * g + 1];
+#pragma unroll 1
+            for (int rb = r0; rb < r1; rb += 4) {  // guarded batches of 4 (as above)
+              double rv[4], am[4], av[4];
+#pragma unroll
+              for (int q = 0; q < 4; ++q) {
+                const int r = rb + q < r1 ? rb + q : r0;
+                rv[q] = Rm[(int64_t)r * ldR + cc];
+                am[q] = cam[r];
+                av[q] = cav[r];
+              }
+#pragma unroll
+              for (int q = 0; q < 4; ++q) {
+                if (rb + q >= r1) break;
+                acc += wt * rv[q] * am[q] * av[q];
+              }
+            }
           } else if (!isu && cg[4 * g + 1] == 0. && !(b.ff && j < 6)) {
             acc += cost_act(b, C, nu).sgrad(j, state_res(b, C.d(), x, j), wt);
           } else if (isu && cg[4 * g + 1] == 1.) {
@@ -2728,7 +2788,7 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
           }
         }
       }
-      (isu ? Lu : Lx)[j] = integ ? sc * acc : acc;
+      mb_gstore((isu ? Lu : Lx) + j, integ ? sc * acc : acc);
     }
     // the fused calc's cost (cost-sum.hxx:89-117): record k's weighted activation on
     // lane nt-1-k (the lanes with the fewest GEMM tasks), into the dead pivot buffer
