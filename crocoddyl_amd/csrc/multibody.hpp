@@ -2486,13 +2486,26 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
   const bool fd = b.enable_force && nc > 0 && !imp;
   double* dfx = w + l.dfx;
   double* dfu = w + l.dfu;
-  // da = -Kinv_tl dtau - H da0 (impulse: -G dtau_dq - H dv0_dq on the q columns)
+  const double sc = integ ? dt : 1.;
+  // cost-derivative area (layout: group table 4 kMaxCosts | Arr, Ar mul, Ar val,
+  // source per row | R rows)
+  double* cg = w + l.R;
+  double* ch = cg + 4 * kMaxCosts;
+  double* cam = ch + kMaxCostRows;
+  double* cav = cam + kMaxCostRows;
+  double* csrc = cav + kMaxCostRows;
+  double* cgi = csrc + kMaxCostRows;  // group of each row
+  double* Rm = csrc + 2 * kMaxCostRows;
+  const int ldR = cost_rows_ld(nj, nu);
+  // da = -Kinv_tl dtau - H da0 (impulse: -G dtau_dq - H dv0_dq on the q columns) on all
+  // lanes but the last, which builds the cost-derivative table meanwhile (its area may be
+  // the world-value area, dead since the tangent-direction phase)
   ex.run([&](int lane) {
     // two entries per lane at a time: two independent dot-product chains, so the LDS
     // loads of one overlap the other's FMAs (each entry's summation order unchanged)
-    const int ne = nj * L;
-    for (int e0 = lane; e0 < ne; e0 += 2 * ex.nt) {
-      const int e1 = e0 + ex.nt < ne ? e0 + ex.nt : e0;
+    const int ne = nj * L, nl = ex.nt - 1;
+    for (int e0 = lane; e0 < ne && lane < nl; e0 += 2 * nl) {
+      const int e1 = e0 + nl < ne ? e0 + nl : e0;
       const int r0 = e0 / L, c0 = e0 % L, r1 = e1 / L, c1 = e1 % L;
       double s0 = 0., s1 = 0.;
       for (int k = 0; k < nj; ++k) {
@@ -2521,68 +2534,6 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
         const int k = e / nj, c = e % nj;
         dfu[e] = c < nu ? -H[(int64_t)k * nj + b.nun + c] : 0.;
       }
-    }
-  });
-  const double sc = integ ? dt : 1.;
-  // cost-derivative area (layout: group table 4 kMaxCosts | Arr, Ar mul, Ar val,
-  // source per row | R rows)
-  double* cg = w + l.R;
-  double* ch = cg + 4 * kMaxCosts;
-  double* cam = ch + kMaxCostRows;
-  double* cav = cam + kMaxCostRows;
-  double* csrc = cav + kMaxCostRows;
-  double* cgi = csrc + kMaxCostRows;  // group of each row
-  double* Rm = csrc + 2 * kMaxCostRows;
-  const int ldR = cost_rows_ld(nj, nu);
-  // Output blocks, entry by entry over all lanes (consecutive lanes write
-  // consecutive addresses of the column-major blocks).
-  ex.run([&](int lane) {
-    // Fx(i, c): Euler assembly (euler.hxx:100-112) with JintegrateTransport / Jintegrate
-    for (int e = lane; e < n * n; e += ex.nt) {
-      const int c = e / n, i = e % n;
-      double f;
-      if (imp) {  // [[I, 0], [-G dtau_dq - H dv0_dq, G M = I - H Jc]] (impulse-fwddyn.hxx:111-115)
-        if (i < nj) {
-          f = c == i ? 1. : 0.;
-        } else if (c < nj) {
-          f = da[(int64_t)(i - nj) * L + c];
-        } else {
-          double s = 0.;
-          for (int k = 0; k < nc; ++k) s += H[(int64_t)k * nj + (i - nj)] * Jc[(int64_t)k * nj + (c - nj)];
-          f = ok ? (c - nj == i - nj ? 1. : 0.) - s : NAN;
-        }
-      } else if (integ) {
-        if (i < nj && ffe && i < 6) {  // Jexp6(dq) (da dt^2 + [0 dt I]) + Ad(exp6(dq)^-1)
-          double s = c < 6 ? Ai[c * 6 + i] : 0.;
-          for (int r = 0; r < 6; ++r)
-            s += Je[r * 6 + i] * (da[(int64_t)r * L + c] * dt2 + (c == nj + r ? dt : 0.));
-          f = s;
-        } else if (i < nj) {
-          f = da[(int64_t)i * L + c] * dt2 + (c == nj + i ? dt : 0.) + (c == i ? 1. : 0.);
-        } else {
-          f = da[(int64_t)(i - nj) * L + c] * dt + (c == i ? 1. : 0.);
-        }
-      } else {
-        f = c == i ? 1. : 0.;
-      }
-      mb_gstore(Fx + e, f);
-    }
-    // Fu(i, c) = Kinv_tl(i mod nj, nun + c) dt^2 | dt (dtau/du = [0; I]), Jexp6 on
-    // the free-flyer rows; Lxu from the contact-force costs
-    for (int e = lane; e < n * m; e += ex.nt) {
-      const int c = e / n, i = e % n;
-      double f = 0.;
-      if (integ && c < nu && !imp) {
-        if (i < nj && ffe && i < 6) {
-          double s = 0.;
-          for (int r = 0; r < 6; ++r) s += Je[r * 6 + i] * Minv[(int64_t)(b.nun + c) * lda + r];
-          f = ok ? s * dt2 : NAN;
-        } else {
-          const double mi = ok ? Minv[(int64_t)(b.nun + c) * lda + (i < nj ? i : i - nj)] : NAN;
-          f = i < nj ? mi * dt2 : mi * dt;
-        }
-      }
-      mb_gstore(Fu + e, f);
     }
     // the cost-derivative table (last thread): groups in cost (name) order, each the
     // rows of one cost with a dense residual Jacobian, or the diagonal of a state /
@@ -2641,6 +2592,57 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
       cg[4 * kMaxCosts - 1] = g;
     }
   });
+  // Output blocks, entry by entry over all lanes (consecutive lanes write
+  // consecutive addresses of the column-major blocks).
+  ex.run([&](int lane) {
+    // Fx(i, c): Euler assembly (euler.hxx:100-112) with JintegrateTransport / Jintegrate
+    for (int e = lane; e < n * n; e += ex.nt) {
+      const int c = e / n, i = e % n;
+      double f;
+      if (imp) {  // [[I, 0], [-G dtau_dq - H dv0_dq, G M = I - H Jc]] (impulse-fwddyn.hxx:111-115)
+        if (i < nj) {
+          f = c == i ? 1. : 0.;
+        } else if (c < nj) {
+          f = da[(int64_t)(i - nj) * L + c];
+        } else {
+          double s = 0.;
+          for (int k = 0; k < nc; ++k) s += H[(int64_t)k * nj + (i - nj)] * Jc[(int64_t)k * nj + (c - nj)];
+          f = ok ? (c - nj == i - nj ? 1. : 0.) - s : NAN;
+        }
+      } else if (integ) {
+        if (i < nj && ffe && i < 6) {  // Jexp6(dq) (da dt^2 + [0 dt I]) + Ad(exp6(dq)^-1)
+          double s = c < 6 ? Ai[c * 6 + i] : 0.;
+          for (int r = 0; r < 6; ++r)
+            s += Je[r * 6 + i] * (da[(int64_t)r * L + c] * dt2 + (c == nj + r ? dt : 0.));
+          f = s;
+        } else if (i < nj) {
+          f = da[(int64_t)i * L + c] * dt2 + (c == nj + i ? dt : 0.) + (c == i ? 1. : 0.);
+        } else {
+          f = da[(int64_t)(i - nj) * L + c] * dt + (c == i ? 1. : 0.);
+        }
+      } else {
+        f = c == i ? 1. : 0.;
+      }
+      mb_gstore(Fx + e, f);
+    }
+    // Fu(i, c) = Kinv_tl(i mod nj, nun + c) dt^2 | dt (dtau/du = [0; I]), Jexp6 on
+    // the free-flyer rows; Lxu from the contact-force costs
+    for (int e = lane; e < n * m; e += ex.nt) {
+      const int c = e / n, i = e % n;
+      double f = 0.;
+      if (integ && c < nu && !imp) {
+        if (i < nj && ffe && i < 6) {
+          double s = 0.;
+          for (int r = 0; r < 6; ++r) s += Je[r * 6 + i] * Minv[(int64_t)(b.nun + c) * lda + r];
+          f = ok ? s * dt2 : NAN;
+        } else {
+          const double mi = ok ? Minv[(int64_t)(b.nun + c) * lda + (i < nj ? i : i - nj)] : NAN;
+          f = i < nj ? mi * dt2 : mi * dt;
+        }
+      }
+      mb_gstore(Fu + e, f);
+    }
+  });
   // the stacked residual Jacobians R (nrows x (L + nu), ld ldR): jac-cost rows from
   // their q (or x) columns, force-cost rows from d lambda / dx, du
   const int ngr = (int)cg[4 * kMaxCosts - 1];
@@ -2682,11 +2684,20 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
     const double* const x = ex.lds(x_);
     const double* const u = ex.lds(u_);
     const int n4 = (n + 3) / 4, m4 = (m + 3) / 4;
-    const int tx = n4 * n, txu = n4 * m, tuu = m4 * m;
+    // Lxx is symmetric: only its row blocks i0 <= j are tasks (column j has j / 4 + 1 of
+    // them; columns 4a .. 4a+3 follow 2a(a+1) tasks), each entry above the diagonal also
+    // stored mirrored
+    int tx = 0;
+    for (int jj = 0; jj < n; ++jj) tx += jj / 4 + 1;
+    const int txu = n4 * m, tuu = m4 * m;
     for (int task = lane; task < tx + txu + tuu; task += ex.nt) {
       int blk, i0, j;
       if (task < tx) {
-        blk = 0, i0 = 4 * (task % n4), j = task / n4;
+        int a = (int)((sqrt(1. + 2. * task) - 1.) * 0.5);
+        while (2 * (a + 1) * (a + 2) <= task) ++a;
+        while (a > 0 && 2 * a * (a + 1) > task) --a;
+        const int rem = task - 2 * a * (a + 1);
+        blk = 0, j = 4 * a + rem / (a + 1), i0 = 4 * (rem % (a + 1));
       } else if (task < tx + txu) {
         blk = 1, i0 = 4 * ((task - tx) % n4), j = (task - tx) / n4;
       } else {
@@ -2747,9 +2758,11 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int i = i0 + q;
-        if (i >= rows) continue;
+        if (i >= rows || (blk == 0 && i > j)) continue;
         const bool zero = (blk == 1 && j >= nu) || (blk == 2 && (i >= nu || j >= nu));
-        mb_gstore(out + (int64_t)j * rows + i, zero ? 0. : (blk == 1 || integ ? sc * lv[q] : lv[q]));
+        const double v = zero ? 0. : (blk == 1 || integ ? sc * lv[q] : lv[q]);
+        mb_gstore(out + (int64_t)j * rows + i, v);
+        if (blk == 0 && i < j) mb_gstore(out + (int64_t)i * rows + j, v);
       }
     }
     // Lx (x columns) and Lu (u columns): R^T Ar in cost order
