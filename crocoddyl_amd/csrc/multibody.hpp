@@ -1138,9 +1138,12 @@ MB_HD inline void w_crba_column(const Blk& b, const WVals& W, int j, double* A, 
   comp_mul(W, j, W.S(j), F);
   A[(int64_t)j * lda + j] = dot6(W.S(j), F) + b.arm[j];
   const Mask am = *W.anc(j);
+  // every i < j visited, the non-ancestors storing their zero (only lane j writes the
+  // pair {i, j}), so the loop has no branch and the unrolled loads overlap
+#pragma unroll 2
   for (int i = 0; i < j; ++i) {
-    if (!((am >> i) & 1ull)) continue;
-    const double Mij = dot6(W.S(i), F);
+    const double d = dot6(W.S(i), F);
+    const double Mij = ((am >> i) & 1ull) ? d : 0.;
     A[(int64_t)j * lda + i] = Mij;
     A[(int64_t)i * lda + j] = Mij;
   }
@@ -1852,7 +1855,8 @@ __host__ __device__ inline DiffLayout diff_layout(int nj, int njac, int nc = 0, 
   l.dtau = l.A + (int64_t)lda_of(nj) * 2 * nj;  // [M | I] -> [. | Minv], ld lda_of(nj)
   // dtau [k][L] (first the per-body N_b, h_b: 42 per dof); da = -Kinv (dtau; da0) [r][L]
   // (first the subtree sums Nsub, Hsub)
-  const int64_t dsz = (int64_t)nj * L > 42 * (int64_t)nj ? (int64_t)nj * L : 42 * (int64_t)nj;
+  // (da rows at the odd stride L + 1: the Fx assembly reads a column of it per wave)
+  const int64_t dsz = (int64_t)nj * (L + 1) > 42 * (int64_t)nj ? (int64_t)nj * (L + 1) : 42 * (int64_t)nj;
   l.da = l.dtau + dsz;
   l.qp = l.da + dsz;
   l.vec = l.qp + (int64_t)12 * nj;      // Q_k, P_k
@@ -2278,6 +2282,7 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
   double* A = w + l.A;
   double* dtau = w + l.dtau;
   double* da = w + l.da;
+  const int Ld = L + 1;  // row stride of da (odd: conflict-free column reads)
   double* qp = w + l.qp;
   double* x = w + l.vec;
   double* u = x + nq + nj;
@@ -2498,12 +2503,12 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
   double* Rm = csrc + 2 * kMaxCostRows;
   const int ldR = cost_rows_ld(nj, nu);
   // da = -Kinv_tl dtau - H da0 (impulse: -G dtau_dq - H dv0_dq on the q columns) on all
-  // lanes but the last, which builds the cost-derivative table meanwhile (its area may be
+  // lanes but the last ncost, which build the cost-derivative table meanwhile (its area may be
   // the world-value area, dead since the tangent-direction phase)
   ex.run([&](int lane) {
     // two entries per lane at a time: two independent dot-product chains, so the LDS
     // loads of one overlap the other's FMAs (each entry's summation order unchanged)
-    const int ne = nj * L, nl = ex.nt - 1;
+    const int ne = nj * L, nl = ex.nt - (b.ncost > 0 ? b.ncost : 1);
     for (int e0 = lane; e0 < ne && lane < nl; e0 += 2 * nl) {
       const int e1 = e0 + nl < ne ? e0 + nl : e0;
       const int r0 = e0 / L, c0 = e0 % L, r1 = e1 / L, c1 = e1 % L;
@@ -2518,8 +2523,8 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
       }
       if (imp && c0 >= nj) s0 = 0.;
       if (imp && c1 >= nj) s1 = 0.;
-      da[e0] = ok ? -s0 : NAN;
-      if (e1 != e0) da[e1] = ok ? -s1 : NAN;
+      da[(int64_t)r0 * Ld + c0] = ok ? -s0 : NAN;
+      if (e1 != e0) da[(int64_t)r1 * Ld + c1] = ok ? -s1 : NAN;
     }
     if (fd) {
       const double* Sinv = Sx + (int64_t)nc * nc;
@@ -2535,14 +2540,31 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
         dfu[e] = c < nu ? -H[(int64_t)k * nj + b.nun + c] : 0.;
       }
     }
-    // the cost-derivative table (last thread): groups in cost (name) order, each the
-    // rows of one cost with a dense residual Jacobian, or the diagonal of a state /
-    // control cost; per row Arr (hess), and Ar as amul * aval (the quadratic kinds'
-    // (w, r), so the gradient keeps the order (X w) r of the reference's R^T (w r))
-    if (lane == ex.nt - 1) {
+    // the cost-derivative table: groups in cost (name) order, each the rows of one cost
+    // with a dense residual Jacobian, or the diagonal of a state / control cost; per row
+    // Arr (hess), and Ar as amul * aval (the quadratic kinds' (w, r), so the gradient
+    // keeps the order (X w) r of the reference's R^T (w r)). Cost k on lane nt-1-k
+    // (no da entries there), from its group / row / jac-cost offsets, prefix-counted.
+    if (lane >= nl) {
+      const int kk = ex.nt - 1 - lane;
       int g = 0, row = 0, f = 0;
       const double* cr = b.C;
-      for (int k = 0; k < b.ncost; ++k) {
+      for (int k = 0; k < kk; ++k) {  // offsets of record kk
+        const CRec C{cr};
+        const int t = C.type();
+        if (jac_cost(b, t)) {
+          row += jac_rows(t);
+          ++g;
+          ++f;
+        }
+        if (t == C_STATE || t == C_CONTROL) ++g;
+        if (fd && force_cost(t) && (int)C.d()[0] >= 0) {
+          row += cost_act(b, C, nu).nr;
+          ++g;
+        }
+        cr += C.size();
+      }
+      if (kk < b.ncost) {
         const CRec C{cr};
         const int t = C.type();
         const Act act = cost_act(b, C, nu);
@@ -2587,9 +2609,8 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
           cg[4 * g + 3] = 2.;  // x and u columns
           ++g;
         }
-        cr += C.size();
       }
-      cg[4 * kMaxCosts - 1] = g;
+      if (kk == (b.ncost > 0 ? b.ncost - 1 : 0)) cg[4 * kMaxCosts - 1] = g;  // the group count
     }
   });
   // Output blocks, entry by entry over all lanes (consecutive lanes write
@@ -2603,7 +2624,7 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
         if (i < nj) {
           f = c == i ? 1. : 0.;
         } else if (c < nj) {
-          f = da[(int64_t)(i - nj) * L + c];
+          f = da[(int64_t)(i - nj) * Ld + c];
         } else {
           double s = 0.;
           for (int k = 0; k < nc; ++k) s += H[(int64_t)k * nj + (i - nj)] * Jc[(int64_t)k * nj + (c - nj)];
@@ -2613,12 +2634,12 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
         if (i < nj && ffe && i < 6) {  // Jexp6(dq) (da dt^2 + [0 dt I]) + Ad(exp6(dq)^-1)
           double s = c < 6 ? Ai[c * 6 + i] : 0.;
           for (int r = 0; r < 6; ++r)
-            s += Je[r * 6 + i] * (da[(int64_t)r * L + c] * dt2 + (c == nj + r ? dt : 0.));
+            s += Je[r * 6 + i] * (da[(int64_t)r * Ld + c] * dt2 + (c == nj + r ? dt : 0.));
           f = s;
         } else if (i < nj) {
-          f = da[(int64_t)i * L + c] * dt2 + (c == nj + i ? dt : 0.) + (c == i ? 1. : 0.);
+          f = da[(int64_t)i * Ld + c] * dt2 + (c == nj + i ? dt : 0.) + (c == i ? 1. : 0.);
         } else {
-          f = da[(int64_t)(i - nj) * L + c] * dt + (c == i ? 1. : 0.);
+          f = da[(int64_t)(i - nj) * Ld + c] * dt + (c == i ? 1. : 0.);
         }
       } else {
         f = c == i ? 1. : 0.;
