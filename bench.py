@@ -1,11 +1,15 @@
 """Benchmark: FDDP iterations/s + MPC solves/s, Talos walking (contact dynamics) T=100, B=1024 per GPU.
 
-One step = one warm-started MPC solve of every batch element on this GPU
-(SolverFDDP::solve(xs, us, maxiter=1, isFeasible=false, regInit=0.1) after a
-receding-horizon shift x0 <- xs[1], xs/us shifted — the reference's
-benchmark unit, benchmark/quadrupedal-gaits-optctrl.cpp:63). Each step runs
-exactly one FDDP iteration per element (calc, calcDiff + gaps, backward
-Riccati sweep, line search), so FDDP iterations/s == MPC solves/s.
+One step = one warm-started solve of every batch element on this GPU,
+SolverFDDP::solve(xs, us, maxiter=1, isFeasible=false, regInit=0.1) — the
+reference's benchmark unit. Two protocols:
+  fixed (default): the same warm start every step (default state, quasi-static
+      controls), exactly the loop of benchmark/bipedal_walk_optctrl.py:36-43 and
+      quadrupedal-gaits-optctrl.cpp:60-64; the warm start is kept in HBM.
+  shift: a receding horizon — the gait knots rotate one knot (circularAppend,
+      shooting.hxx:235-281), x0 <- xs[1] and xs/us shift on device, then the solve.
+Each step runs exactly one FDDP iteration per element (calc, calcDiff + gaps,
+backward Riccati sweep, line search), so FDDP iterations/s == MPC solves/s.
 
 Multi-GPU: one process per GPU (torchrun), the batch axis is sharded (each
 rank owns B independent problems: weak scaling, no collective inside the
@@ -71,52 +75,63 @@ def synthetic_kind(cfg):
     return synthetic.CONFIGS[cfg][0]
 
 
-def cpu_baseline(cfg, T, seed, target_s=12.0, box=False):
-    """Time the CPU oracle (C++ port of the reference solver, OpenMP over batch
-    elements) on this host, on a bounded sample of the same workload. Runs in a
-    child process: first the -march=native build, and if that fails (the
-    native build of the multibody oracle crashes on some host CPUs under gcc
-    11) the in-tree -march=x86-64-v3 build; the sample string says which."""
-    import subprocess
-    errs = []
-    for arch in ("native", "x86-64-v3"):
-        cmd = [sys.executable, os.path.abspath(__file__), "--cpu-baseline-child", cfg, str(T), str(seed),
-               str(target_s), "1" if box else "0", arch]
+def cpu_share():
+    """The CPUs this process may use: the affinity mask and the cgroup CPU quota
+    (cgroup v2 cpu.max, or v1 cfs_quota_us / cfs_period_us). threads = the smaller."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except Exception:
+        aff = os.cpu_count() or 1
+    quota = None
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(p)
+    except Exception:
         try:
-            p = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
-        except subprocess.TimeoutExpired:
-            errs.append(f"{arch}: timeout")
-            continue
-        lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
-        if p.returncode == 0 and lines:
-            out = json.loads(lines[-1])
-            if errs:
-                out["sample"] += f" (native build failed: {'; '.join(errs)})"
-            return out
-        errs.append(f"{arch}: exit {p.returncode}")
-    return {"error": "; ".join(errs)}
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            p = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = q / p
+        except Exception:
+            pass
+    threads = aff if quota is None else max(1, min(aff, int(quota)))
+    return threads, aff, quota
 
 
-def _cpu_baseline_child(cfg, T, seed, target_s, box, arch):
+def cpu_baseline(cfg, T, seed, protocol, target_s=12.0, box=False):
+    """Time the CPU oracle (C++ port of the reference solver, OpenMP) on this host, on
+    a bounded sample of the same workload and protocol. Runs in a child process
+    (the oracle is test infrastructure: never loaded into the benchmarking process)."""
+    import subprocess
+    cmd = [sys.executable, os.path.abspath(__file__), "--cpu-baseline-child", cfg, str(T), str(seed),
+           str(target_s), "1" if box else "0", protocol]
+    try:
+        p = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
+    except subprocess.TimeoutExpired:
+        return {"error": "timeout"}
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    if p.returncode == 0 and lines:
+        return json.loads(lines[-1])
+    return {"error": f"exit {p.returncode}: {p.stderr[-400:]}"}
+
+
+def _cpu_baseline_child(cfg, T, seed, target_s, box, protocol):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import helpers
     import oracle_lib
 
-    if arch == "native":
-        out = os.path.join("/tmp", f"oracle_native_{os.getpid()}")
-        oracle_lib.build(out_dir=out, arch="-march=native")
-        oracle_lib._lib = oracle_lib.lib(os.path.join(out, "liboracle.so"))
-        flags = "-O3 -march=native"
-    else:
-        oracle_lib._lib = None  # the in-tree x86-64-v3 build
-        flags = "-O3 -march=x86-64-v3"
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except Exception:
-        cores = os.cpu_count() or 1
-    threads = max(1, min(16, cores))
+    # -march=native build of the oracle for this host (built here, in /tmp)
+    out = os.path.join("/tmp", f"oracle_native_{os.getpid()}")
+    oracle_lib.build(out_dir=out, arch="-march=native")
+    oracle_lib._lib = oracle_lib.lib(os.path.join(out, "liboracle.so"))
+    flags = "-O3 -march=native"
+    threads, aff, quota = cpu_share()
 
     from crocoddyl_amd import _abi, synthetic
+    import ctypes as C
+
+    kind = synthetic.CONFIGS[cfg][0]
 
     def run(Bs, steps, mode=2):
         S = helpers.setup(cfg, T=T, B=Bs, seed=seed)
@@ -128,22 +143,23 @@ def _cpu_baseline_child(cfg, T, seed, target_s, box, arch):
             p = oracle_lib.default_params()
             p.th_stop = 5e-5
             o.set_params(p)
-        if synthetic.CONFIGS[cfg][0] == "multibody_contact":  # as the GPU run: warm start at x0
-            o.set_candidate(np.repeat(S["x0s"][:, None, :], T + 1, axis=1), None, False)
-        elif synthetic.CONFIGS[cfg][0].startswith("gait"):  # as the GPU run: default state, quasi-static us
-            xs_w, us_w = synthetic.gait_warm_start(cfg, S["running"], S["x0s"][0])
-            us = np.zeros((d.B, d.T, d.nu_max))
-            for t, u in enumerate(us_w):
-                us[:, t, :u.size] = u
-            o.set_candidate(np.repeat(np.asarray(xs_w)[None], d.B, axis=0), us, False)
-        else:
-            o.set_candidate(None, None, False)
-        o.solve(maxiter=2)
+        xs_w, us_w = warm_start_arrays(cfg, S["running"], S["x0s"], d)
+        o.set_candidate(xs_w, us_w, False)
+        knots = list(S["knots"])
+        iters = 2 if box else 1
+        if protocol == "shift":
+            o.solve(maxiter=5)
         t0 = time.perf_counter()
         it = 0
         for _ in range(steps):
-            o.mpc_shift()
-            r = o.solve(maxiter=2 if box else 1, reg_init=0.1)
+            if protocol == "shift":
+                knots = knots[1:T] + knots[:1] + knots[T:]
+                kd = (_abi.KnotDesc * len(knots))(*[_abi.KnotDesc(*k) for k in knots])
+                o.L.oracle_set_knots(o.h, kd, _abi.dptr(o.pool), o.pool.size)
+                o.mpc_shift()
+            else:
+                o.set_candidate(xs_w, us_w, False)
+            r = o.solve(maxiter=iters, reg_init=0.1)
             it += sum(x.n_iter_run for x in r)
         return it, time.perf_counter() - t0
 
@@ -165,14 +181,17 @@ def _cpu_baseline_child(cfg, T, seed, target_s, box, arch):
     B1 = int(max(1, min(256, target_s / 3 * (it1 / max(dt1, 1e-9)) / steps)))
     it1, dt1 = run(B1, steps, mode=1)
     v2, v1 = it / dt, it1 / dt1
+    share = f"affinity {aff} CPUs, cgroup quota {'none' if quota is None else round(quota, 2)}"
     print(json.dumps({"value": max(v1, v2), "unit": "FDDP iterations/s", "cores": threads, "kind": "port",
-                      "host_cpus": os.cpu_count(), "cpu_model": cpu_model,
+                      "host_cpus": os.cpu_count(), "affinity_cpus": aff, "cgroup_cpu_quota": quota,
+                      "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS"), "cpu_model": cpu_model,
+                      "build": f"{flags} -fopenmp",
                       "modes": {"batch_parallel": round(v2, 2), "knot_parallel": round(v1, 2)},
-                      "sample": f"{cfg} T={T}, warm-started solve(maxiter={2 if box else 1}) per element: "
-                                f"batch-parallel {Bs} elements x {steps} steps ({it} element-iterations in {dt:.1f} s), "
-                                f"knot-parallel {B1} elements x {steps} steps ({it1} in {dt1:.1f} s); value = the faster "
-                                f"mode. oracle/fddp_oracle.cpp {flags} -fopenmp, {threads} threads (the box's CPU share) "
-                                f"of {os.cpu_count()} host CPUs ({cpu_model})"
+                      "sample": f"{cfg} T={T}, protocol {protocol}, solve(maxiter={2 if box else 1}, reg_init=0.1) "
+                                f"per element per step: batch-parallel {Bs} elements x {steps} steps ({it} "
+                                f"element-iterations in {dt:.1f} s), knot-parallel {B1} elements x {steps} steps "
+                                f"({it1} in {dt1:.1f} s); value = the faster mode. oracle/fddp_oracle.cpp {flags} "
+                                f"-fopenmp, {threads} threads ({share}) of {os.cpu_count()} host CPUs ({cpu_model})"
                                 f"{', SolverBoxFDDP |u| <= 1' if box else ''}"}), flush=True)
 
 
@@ -183,12 +202,34 @@ def load_pmc(cfg):
         return None
 
 
-def make_shard_solver(config, B, rank, dev, box=False, T=None):
-    """Rank `rank`'s shard of the job: B problems of `config` (seeded per rank, so
-    every rank owns distinct problems) on GPU `dev`, warm-started and solved once
-    (solve(maxiter=5)) as the timed loop expects."""
-    from crocoddyl_amd import ShootingProblem, SolverBoxFDDP, SolverFDDP, synthetic
+def warm_start_arrays(config, running, x0s, dims):
+    """The warm start of every element as dense (B, T+1, nx) / (B, T, nu_max) arrays.
+    Gaits: the reference benchmark's (bipedal_walk_optctrl.py:29-32,
+    quadrupedal-gaits-optctrl.cpp:51-57): the default state at every knot, each knot's
+    quasi-static controls. The arm on contact dynamics: x0 at every knot (state.zero(),
+    the stretched arm, is a singular configuration of the gripper contact). Otherwise
+    None (state.zero() / zeros, setCandidate's defaults)."""
+    from crocoddyl_amd import synthetic
     kind = synthetic.CONFIGS[config][0]
+    B, T, nx, m = dims.B, dims.T, dims.nx, dims.nu_max
+    if kind in ("gait_biped", "gait_quadruped"):
+        xs_w, us_w = synthetic.gait_warm_start(config, running, x0s[0])
+        xs = np.ascontiguousarray(np.broadcast_to(np.asarray(xs_w)[None], (B, T + 1, nx)))
+        us = np.zeros((B, T, m))
+        for t, u in enumerate(us_w):
+            us[:, t, :u.size] = u
+        return xs, us
+    if kind == "multibody_contact":
+        return np.ascontiguousarray(np.repeat(x0s[:, None, :], T + 1, axis=1)), None
+    return None, None
+
+
+def make_shard_solver(config, B, rank, dev, box=False, T=None, presolve=True):
+    """Rank `rank`'s shard of the job: B problems of `config` (seeded per rank, so
+    every rank owns distinct problems) on GPU `dev`, with the config's warm start set
+    as the candidate (solver.warm = (xs, us) host arrays). presolve: then
+    solve(maxiter=5) once, the starting point of the receding-horizon protocol."""
+    from crocoddyl_amd import ShootingProblem, SolverBoxFDDP, SolverFDDP, synthetic
     T = synthetic.CONFIGS[config][3] if T is None else T
     seed = synthetic.seed_of(config) + 1000 * rank
     x0s, running, terminal = synthetic.build(config, T=T, B=B, seed=seed)
@@ -198,25 +239,55 @@ def make_shard_solver(config, B, rank, dev, box=False, T=None):
             md.u_ub = np.full(md.nu, BOX_LIMIT)
     problem = ShootingProblem(x0s, running, terminal, device=dev)
     solver = SolverBoxFDDP(problem) if box else SolverFDDP(problem)
-    if kind in ("gait_biped", "gait_quadruped"):
-        # the reference benchmark's warm start (bipedal_walk_optctrl.py:29-32): the
-        # default state at every knot, quasi-static controls
-        xs_w, us_w = synthetic.gait_warm_start(config, running, x0s[0])
-        solver.solve(xs_w, us_w, maxiter=5)
-    elif kind == "multibody_contact":
-        # warm start at x0: the default (state.zero(), the stretched arm) is a
-        # singular configuration of the gripper contact (rank-deficient Jc)
-        solver.solve(np.repeat(x0s[:, None, :], T + 1, axis=1), [], maxiter=5)
-    else:
-        solver.solve(maxiter=5)  # converge once from a cold start
+    solver.warm = warm_start_arrays(config, running, x0s, problem._dims())
+    solver.setCandidate(solver.warm[0] if solver.warm[0] is not None else [],
+                        solver.warm[1] if solver.warm[1] is not None else [], False)
+    if presolve:
+        solver.solve_from_candidate(maxiter=5)
     return solver
 
 
-def mpc_step(solver, mpc_iters):
-    """One receding-horizon MPC solve of every element: device shift, then a
-    warm-started solve(maxiter=mpc_iters, regInit=0.1)."""
+def mpc_step(solver, mpc_iters, rotate=False):
+    """One receding-horizon MPC solve of every element: the gait knots rotated one
+    knot (ShootingProblem::circularAppend of the first running model, shooting.hxx:
+    235-281) when `rotate`, the device shift of x0 / xs / us, then a warm-started
+    solve(maxiter=mpc_iters, regInit=0.1)."""
+    if rotate:
+        p = solver.problem
+        p.circularAppend(p.runningModels[0])
     solver.mpcShift()
     solver.solve_from_candidate(maxiter=mpc_iters, isFeasible=False, regInit=0.1)
+
+
+class FixedWarmStart:
+    """The reference benchmark's step (bipedal_walk_optctrl.py:36-43,
+    quadrupedal-gaits-optctrl.cpp:60-64): solve(xs, us, MAXITER, false, 0.1) from the
+    same warm start every time. The warm start lives in HBM (device tensors) and is
+    re-applied on the solver's stream before each solve."""
+
+    def __init__(self, solver, dev):
+        import torch
+        self.solver = solver
+        xs, us = solver.warm
+        self.xs = None if xs is None else torch.from_numpy(xs).to(f"cuda:{dev}")
+        self.us = None if us is None else torch.from_numpy(us).to(f"cuda:{dev}")
+        torch.cuda.synchronize(dev)
+
+    def __call__(self, mpc_iters):
+        self.solver.setCandidate_device(None if self.xs is None else self.xs.data_ptr(),
+                                        None if self.us is None else self.us.data_ptr(), False)
+        self.solver.solve_from_candidate(maxiter=mpc_iters, isFeasible=False, regInit=0.1)
+
+
+def line_search_trials(solver):
+    """Trials per element of the last line search: alpha = 2^-k accepted after k + 1."""
+    sl = np.atleast_1d(np.asarray(solver.stepLength, float))
+    return np.round(-np.log2(np.clip(sl, 2.0 ** -12, 1.0))) + 1
+
+
+def trials_summary(trials):
+    return {"mean": round(float(trials.mean()), 2), "max": int(trials.max()),
+            "hist": np.bincount(trials.astype(int), minlength=11)[1:].tolist()}
 
 
 def main():
@@ -234,6 +305,12 @@ def main():
     ap.add_argument("--solver", choices=["fddp", "boxfddp"], default="fddp",
                     help="boxfddp: SolverBoxFDDP with |u| <= 1 limits, solve(maxiter=2) per MPC step so the "
                          "box QP runs (iteration 1 is feasible)")
+    ap.add_argument("--protocol", choices=["fixed", "shift"], default="fixed",
+                    help="fixed: the reference benchmark's loop, solve(xs, us, 1, false, 0.1) from the same warm "
+                         "start every step (bipedal_walk_optctrl.py:36-43); shift: receding horizon, gait knots "
+                         "rotated (circularAppend) + device shift of x0/xs/us, then the warm-started solve")
+    ap.add_argument("--secondary-steps", type=int, default=5,
+                    help="steps of the other protocol, reported beside the headline (1 GPU only; 0: off)")
     args = ap.parse_args()
     box = args.solver == "boxfddp"
 
@@ -248,13 +325,19 @@ def main():
 
     kind, d1, nu, T, B0, dt = synthetic.CONFIGS[args.config]
     B = args.batch or B0
-    solver = make_shard_solver(args.config, B, rank, dev, box)
-    problem = solver.problem
-    n, m, nx = problem.ndx, problem.nu_max, problem.nx
     mpc_iters = 2 if box else 1
 
-    def step():  # one receding-horizon MPC solve, all elements
-        mpc_step(solver, mpc_iters)
+    def make_stepper(protocol):
+        s = make_shard_solver(args.config, B, rank, dev, box, presolve=(protocol == "shift"))
+        if protocol == "fixed":
+            fw = FixedWarmStart(s, dev)
+            return s, (lambda: fw(mpc_iters))
+        rotate = kind in ("gait_biped", "gait_quadruped")
+        return s, (lambda: mpc_step(s, mpc_iters, rotate=rotate))
+
+    solver, step = make_stepper(args.protocol)
+    problem = solver.problem
+    n, m, nx = problem.ndx, problem.nu_max, problem.nx
 
     for _ in range(args.warmup):
         step()
@@ -278,11 +361,28 @@ def main():
     elapsed = time.perf_counter() - t0
     solver.set_timing(False)
     timing = solver.get_timing()
-    # line-search trials of the last step, per element: alpha = 2^-k accepted after k + 1 trials
-    sl = np.atleast_1d(np.asarray(solver.stepLength, float))
-    trials = np.round(-np.log2(np.clip(sl, 2.0 ** -12, 1.0))) + 1
+    trials = line_search_trials(solver)  # of the last step
     elapsed, total_iters = cdist.job_time_and_work(elapsed, iters, f"cuda:{dev}")
     assert xs_all.shape[0] == us_all.shape[0] == res_all.shape[0] == ws * B
+
+    secondary = None
+    if ws == 1 and args.secondary_steps > 0:
+        other = "shift" if args.protocol == "fixed" else "fixed"
+        del xs_all, us_all, res_all
+        s2, step2 = make_stepper(other)
+        step2()
+        s2.synchronize()
+        t1 = time.perf_counter()
+        it2 = 0
+        for _ in range(args.secondary_steps):
+            step2()
+            it2 += int(np.sum(s2.n_iter_run))
+        s2.synchronize()
+        el2 = time.perf_counter() - t1
+        secondary = {"protocol": other, "steps": args.secondary_steps, "value": round(it2 / el2, 2),
+                     "ms_per_step": round(el2 / args.secondary_steps * 1e3, 3),
+                     "line_search_trials_last_step": trials_summary(line_search_trials(s2))}
+        del s2, step2
 
     if rank == 0:
         value = total_iters / elapsed
@@ -335,7 +435,7 @@ def main():
         cpu = None
         if ws == 1 and not args.no_cpu_baseline:
             try:
-                cpu = cpu_baseline(args.config, T, synthetic.seed_of(args.config), box=box)
+                cpu = cpu_baseline(args.config, T, synthetic.seed_of(args.config), args.protocol, box=box)
             except Exception as e:  # reported, never fatal for the GPU number
                 cpu = {"error": repr(e)}
         out = {
@@ -359,15 +459,21 @@ def main():
                      "per-element x0 = bent posture + U[-0.3, 0.3]" if kind == "multibody_contact" else
                      "synthetic: seeded Euler(dt)∘DifferentialActionModelLQR knots at the config's (n, m, T); "
                      "per-element matrices (SURVEY §8d); no robot model (Pinocchio/URDF absent)"),
-            "config": {"workload": f"{args.config}: n={n}, m={m}, T={T}, B={B} per GPU, warm-started "
-                                   f"solve(maxiter={mpc_iters}, reg_init=0.1) after a device receding-horizon shift"
+            "config": {"workload": f"{args.config}: n={n}, m={m}, T={T}, B={B} per GPU, "
+                                   + (f"protocol fixed: solve(xs_w, us_w, maxiter={mpc_iters}, isFeasible=false, "
+                                      f"reg_init=0.1) from the same HBM-resident warm start every step, as the "
+                                      f"reference benchmark (bipedal_walk_optctrl.py:36-43)"
+                                      if args.protocol == "fixed" else
+                                      f"protocol shift: gait knots rotated (circularAppend), device shift of x0/xs/us, "
+                                      f"then solve(maxiter={mpc_iters}, isFeasible=false, reg_init=0.1)")
                                    + (", SolverBoxFDDP with |u| <= 1" if box else ""),
+                       "protocol": args.protocol,
                        "global_batch": B * ws, "T": T, "parallelism": f"batch-sharded x{ws}",
                        "solver": "SolverBoxFDDP" if box else "SolverFDDP"},
             "mpc_solves_per_s": round(B * ws * args.steps / elapsed, 2),
             "kernel_ms_per_step": {k: round(v[0] / max(args.steps, 1), 3) for k, v in timing.items()},
-            "line_search_trials_last_step": {"mean": round(float(trials.mean()), 2), "max": int(trials.max()),
-                                             "hist": np.bincount(trials.astype(int), minlength=11)[1:].tolist()},
+            "line_search_trials_last_step": trials_summary(trials),
+            "secondary_protocol": secondary,
             "roofline": roof,
             "rooflines": {k: v[1] for k, v in rooflines.items()},
             "cpu_baseline": cpu,

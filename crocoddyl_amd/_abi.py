@@ -86,6 +86,7 @@ PROTOS = {
 PROTOS_GPU = {
     "create": (C.c_int, [C.POINTER(Dims), C.POINTER(KnotDesc), D, C.c_int64, C.c_int, C.POINTER(P)]),
     "set_model_params": (C.c_int, [P, D, C.c_int64]),
+    "set_candidate_device": (C.c_int, [P, D, D, C.c_int]),
     "get_x0": (C.c_int, [P, D]),
     "get_params": (C.c_int, [P, C.POINTER(Params)]),
     "get_xs": (C.c_int, [P, D, C.c_int]),

@@ -464,19 +464,16 @@ int launch_calc_then_diff(fddp_handle* h, int sel_calc, int sel_calc_sum, int se
     return launch_cost_sum(h, sel_calc_sum, nullptr);
   }
   if (h->has_mb) {  // multibody knots: their calc fused into the knot-parallel calcDiff
-    {
-      Timed tm(h, 1);
-      if ((rc = launch_mb(h, sel_calc, sel_diff))) return rc;
-    }
+    // one timer record per calcDiff call (class 1): the knot-parallel kernel, the
+    // dense knots' calc (mixed horizons only), the cost sum and the gaps pass
+    Timed tm(h, 1);
+    const Dev& D = h->D;
+    if ((rc = launch_mb(h, sel_calc, sel_diff))) return rc;
     if (!h->all_mb) {
-      Timed tm(h, 0);
-      const Dev& D = h->D;
       hipLaunchKernelGGL(calc_kernel<kNT>, dim3(D.B), dim3(kNT), h->calc_smem, h->stream, D, sel_calc, h->pcap, 1);
       LAUNCH_CHECK();
     }
     if ((rc = launch_cost_sum(h, sel_calc_sum, nullptr))) return rc;
-    Timed tm(h, 1);
-    const Dev& D = h->D;
     hipLaunchKernelGGL(calc_diff_kernel<kNT>, dim3(D.B), dim3(kNT), h->cdiff_smem, h->stream, D, sel_diff, gaps,
                        h->pcap);
     LAUNCH_CHECK();
@@ -727,8 +724,10 @@ int apply_knots(fddp_handle* h, const fddp_knot_desc* knots, const double* param
     D.mbd = h->has_mb ? pad2(fddp::mb::diff_layout(mb_nj, mb_njac, mb_nc, mb_vcols, mb_nu, mb_nrows).total) : 0;
     h->mb_diff_smem = h->has_mb ? sizeof(double) * (D.mbd + pad2(mb_pmax)) : 0;
     const int64_t budget = (150 * 1024) / 8 - (2 * D.sX + D.sM + 2 * D.sN + 5 * (kNT / kWave) + 16) - D.mbw;
-    h->pcap = pmax <= budget ? pad2(pmax) : 0;
-    // the multibody calc reads its parameter block from LDS only (knots.hpp)
+    // LDS-staged parameter blocks up to pcap doubles; larger (dense) blocks are read from
+    // global memory. The multibody calc reads its block from LDS only (knots.hpp), so
+    // pcap covers at least the largest multibody block.
+    h->pcap = pmax <= budget ? pad2(pmax) : (pad2(mb_pmax) <= budget ? pad2(mb_pmax) : 0);
     if (h->has_mb && h->pcap < pad2(mb_pmax))
       return fail(FDDP_ERR_INVALID_ARG, "multibody parameter blocks exceed the LDS budget of the calc / rollout kernels");
   }
@@ -1074,6 +1073,21 @@ int fddp_set_candidate(fddp_handle* h, const double* xs, const double* us, int i
   hipLaunchKernelGGL(set_feasible_kernel, dim3((D.B + 255) / 256), dim3(256), 0, h->stream, D, is_feasible ? 1 : 0);
   LAUNCH_CHECK();
   HIP_TRY(hipStreamSynchronize(h->stream));
+  return FDDP_OK;
+}
+
+int fddp_set_candidate_device(fddp_handle* h, const double* xs, const double* us, int is_feasible) {
+  if (!h) return fail(FDDP_ERR_INVALID_ARG, "fddp_set_candidate_device: null handle");
+  DeviceGuard g(h->device);
+  const Dev& D = h->D;
+  hipLaunchKernelGGL(scatter_traj_kernel, dim3(8, D.B), dim3(256), 0, h->stream, D, 0, xs, xs ? 0 : 1);
+  LAUNCH_CHECK();
+  if (D.m > 0) {
+    hipLaunchKernelGGL(scatter_traj_kernel, dim3(8, D.B), dim3(256), 0, h->stream, D, 1, us, us ? 0 : 1);
+    LAUNCH_CHECK();
+  }
+  hipLaunchKernelGGL(set_feasible_kernel, dim3((D.B + 255) / 256), dim3(256), 0, h->stream, D, is_feasible ? 1 : 0);
+  LAUNCH_CHECK();
   return FDDP_OK;
 }
 

@@ -979,8 +979,13 @@ __global__ __launch_bounds__(NT) void ls_select_kernel(Dev D, Prm prm, int group
     if (tid == 0) *st = s;
     return;
   }
-  if (acc_slot > 0) {  // the accepted slot's trajectories into the (new) current buffer
-    const TrialOut src(D, 0, acc_slot), dst(D, s.cur, 0);
+  // the accepted slot's trajectories into the (new) current buffer; on an exhausted
+  // search the last trial's into the trial buffer, where the serial search (and the
+  // reference's xs_try_ / us_try_) leaves them
+  const int last_slot = prm.n_alphas - 1 - group * D.npar;
+  const int copy_slot = acc_slot >= 0 ? acc_slot : last_slot;
+  if (copy_slot > 0) {
+    const TrialOut src(D, 0, copy_slot), dst(D, acc_slot >= 0 ? s.cur : 1 - s.cur, 0);
     const int64_t K1 = D.T + 1;
     for (int64_t i = tid; i < K1 * D.sX; i += NT) dst.xs[D.knot(b, 0) * D.sX + i] = src.xs[D.knot(b, 0) * D.sX + i];
     for (int64_t i = tid; i < D.T * D.sM; i += NT) dst.us[D.run(b, 0) * D.sM + i] = src.us[D.run(b, 0) * D.sM + i];
@@ -1037,6 +1042,9 @@ __global__ void init_state_kernel(Dev D, int is_feasible, double xreg) {
   s.n_iter_run = 0;
   s.bwd_fail = 0;
   s.fwd_fail = 0;
+  // the parallel line search's per-element "decided" flag: a solve never starts with a
+  // stale one (a failed launch between groups would otherwise skip a line search)
+  if (D.ls_done) D.ls_done[b] = 0;
 }
 
 // Copy xs/us of the current buffer of every element into a dense output.

@@ -27,11 +27,13 @@ from .host import HostProblem, HostSolverFDDP, is_host_model
 from .models import ActionData, ActionModelAbstract
 
 
-def pack_problem(running, terminal, B):
+def pack_problem(running, terminal, B, cache=None):
     """Knot descriptors + parameter pool for T running knots and the terminal.
 
     Models shared by several knots get one block (or one block per batch
-    element if their parameters are batched)."""
+    element if their parameters are batched). `cache` (dict, optional) keeps each
+    model's packed block by (id, version), so a re-pack after circularAppend /
+    updateNode only packs the models that changed."""
     models = list(running) + [terminal]
     for m in models:
         if not isinstance(m, ActionModelAbstract) or m.kind is None:
@@ -43,7 +45,15 @@ def pack_problem(running, terminal, B):
     for m in models:
         key = id(m)
         if key not in offsets:
-            kind, nu, blocks = m.pack()
+            if cache is not None:
+                ver = m._version
+                hit = cache.get(key)
+                if hit is None or hit[0] != ver or hit[1] is not m:
+                    hit = (ver, m, m.pack())
+                    cache[key] = hit
+                kind, nu, blocks = hit[2]
+            else:
+                kind, nu, blocks = m.pack()
             if blocks.shape[0] not in (1, B):
                 raise ValueError(f"Invalid argument: model parameters are batched over {blocks.shape[0]} "
                                  f"elements but the problem has B={B}")
@@ -77,7 +87,7 @@ class _Handle:
         self.problem = problem
         self.device = device
         self.ptr = C.c_void_p()
-        knots, pool = problem._packed()
+        knots, pool = problem._packed(fresh=True)
         self.n_params = pool.size
         self._knots = knots
         self._sig = problem._signature()
@@ -195,8 +205,14 @@ class ShootingProblem:
     def _dims(self):
         return _abi.Dims(self.nx, self.ndx, self.nu_max, self.T, self.B)
 
-    def _packed(self):
-        return pack_problem(self._models, self._terminal, self.B)
+    def _packed(self, fresh=False):
+        cache = self.__dict__.setdefault("_pack_cache", {})
+        if fresh:  # a new handle packs every model again (in-place array edits included)
+            cache.clear()
+        live = {id(m) for m in self._models + [self._terminal]}
+        for k in [k for k in cache if k not in live]:  # models no longer in the horizon
+            del cache[k]
+        return pack_problem(self._models, self._terminal, self.B, cache)
 
     def _signature(self):
         return tuple((id(m), m._version) for m in self._models + [self._terminal])
@@ -465,6 +481,14 @@ class SolverFDDP:
         p = self.problem
         xa, ua = p._xs_array(xs), p._us_array(us)
         check(lib().fddp_set_candidate(self._ptr, _abi.dptr(xa), _abi.dptr(ua), 1 if isFeasible else 0))
+        self._results = None
+
+    def setCandidate_device(self, xs_ptr, us_ptr, isFeasible=False):
+        """setCandidate from device-resident (B, T+1, nx) / (B, T, nu_max) fp64 arrays
+        (integer device addresses on the solver's GPU, or None); enqueued on the
+        handle's stream without a host synchronisation."""
+        cast = (lambda p: None if p is None else C.cast(C.c_void_p(int(p)), _abi.D))
+        check(lib().fddp_set_candidate_device(self._ptr, cast(xs_ptr), cast(us_ptr), 1 if isFeasible else 0))
         self._results = None
 
     def solve(self, init_xs=[], init_us=[], maxiter=100, isFeasible=False, regInit=1e-9):

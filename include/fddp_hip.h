@@ -218,6 +218,13 @@ int fddp_get_params(fddp_handle* h, fddp_params* p);
 /* Warm start. xs: B*(T+1)*nx or NULL (= state.zero()), us: B*T*nu_max or NULL
  * (= zeros). Replaces SolverAbstract::setCandidate (solver-base.cpp:42-67). */
 int fddp_set_candidate(fddp_handle* h, const double* xs, const double* us, int is_feasible);
+/* The same from device-resident arrays (same dense layout, device pointers on the
+ * handle's device; NULL = state.zero() / zeros). Enqueued on the handle's stream,
+ * no host synchronisation: a warm start kept in HBM and re-applied before every
+ * solve, as the reference's benchmarks call solve(xs, us, ...) with the same
+ * arrays each time (benchmark/bipedal_walk_optctrl.py:39-43,
+ * quadrupedal-gaits-optctrl.cpp:60-64). */
+int fddp_set_candidate_device(fddp_handle* h, const double* xs, const double* us, int is_feasible);
 
 /* SolverFDDP::solve (fddp.cpp:19-105) from the current candidate, for every
  * element at once, each element with its own state machine. reg_init may be

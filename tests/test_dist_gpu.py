@@ -3,8 +3,10 @@ size 2) each drive libfddp_hip on device 0 through bench.py's own shard / solve 
 gather code (make_shard_solver, mpc_step, dist.gather_solution), and the gathered
 xs / us / per-element results must equal solving every shard in one process.
 
-The box has one GPU, so both ranks share device 0 and the collective runs on gloo
-over host copies; the RCCL-over-xGMI all-gather of the 8-GPU job is the same
+Shapes: the C4 trot (T = 60) and the headline C5 Talos walk (T = 100, nx = 77,
+nu = 32: the gather moves the xs / us rows at the bench's widths), a few elements
+per rank. The box has one GPU, so both ranks share device 0 and the collective runs
+on gloo over host copies; the RCCL-over-xGMI all-gather of the 8-GPU job is the same
 dist.gather_rows call on device tensors and is unmeasured on hardware here."""
 import os
 import socket
@@ -15,7 +17,8 @@ import pytest
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-CONFIG, B, STEPS = "C4_solo12_trot", 3, 2
+STEPS = 2
+CASES = [("C4_solo12_trot", 3), ("C5_talos_walk", 2)]
 
 pytestmark = pytest.mark.gpu
 
@@ -28,7 +31,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, ws, port, q):
+def _worker(rank, ws, port, q, CONFIG, B):
     sys.path.insert(0, ROOT)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(ws), RANK=str(rank),
                       LOCAL_RANK=str(rank))
@@ -49,7 +52,8 @@ def _worker(rank, ws, port, q):
     torch.distributed.destroy_process_group()
 
 
-def test_world2_product_shards_gather_matches_single_process():
+@pytest.mark.parametrize("CONFIG,B", CASES)
+def test_world2_product_shards_gather_matches_single_process(CONFIG, B):
     import torch.multiprocessing as mp
 
     sys.path.insert(0, ROOT)
@@ -59,7 +63,7 @@ def test_world2_product_shards_gather_matches_single_process():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, CONFIG, B)) for r in range(2)]
     for p in procs:
         p.start()
     xs, us, res, t, w = q.get(timeout=300)

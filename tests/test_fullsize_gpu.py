@@ -1,0 +1,139 @@
+"""The headline workloads at full size, solve-checked against the C++ oracle.
+
+C5 (Talos walk, T = 100, B = 1024) and C4 (Solo12 trot, T = 60, B = 1024) are built
+with bench.py's own code (make_shard_solver, FixedWarmStart, mpc_step) and run the
+bench's steps on the GPU:
+  * protocol fixed: solve(xs_w, us_w, maxiter=1, isFeasible=False, regInit=0.1) from
+    the reference benchmark's warm start (bipedal_walk_optctrl.py:36-43);
+  * protocol shift: solve(maxiter=5) from the warm start, then two receding-horizon
+    steps (gait knots rotated, x0 / xs / us shifted, solve(maxiter=1, regInit=0.1)).
+Spot elements {0, B/2, B-1} are replayed on the C++ oracle (oracle/floating_oracle.hpp)
+from the same x0 and warm start with the same knot rotation: identical status,
+iteration count and step length (every branch decision of the line search), xs / us /
+cost within 1e-6 relative (north_star's bar).
+
+The parallel line search (groups of 4 trials, the default on Talos) is also compared
+with the serial one on the same problems: identical to the last bit, including
+elements that accept in a later group, accept in a slot above 0, or reject every trial.
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+import helpers
+import oracle_lib
+from crocoddyl_amd import _abi
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+FULL = {"C5_talos_walk": (100, 1024), "C4_solo12_trot": (60, 1024)}
+
+
+def _oracle_spots(solver, spots, threads=3):
+    p = solver.problem
+    knots, pool = p._packed()
+    d = _abi.Dims(p.nx, p.ndx, p.nu_max, p.T, len(spots))
+    o = oracle_lib.Oracle(d, knots, pool, p.x0[spots], threads=threads)
+    xs, us = solver.warm
+    o.set_candidate(None if xs is None else xs[spots], None if us is None else us[spots], False)
+    return o, knots
+
+
+def _compare(solver, o, spots, what):
+    r = helpers.results_dict(solver._res())
+    ro = helpers.results_dict(o.results())
+    xs, us = np.asarray(solver.xs), np.asarray(solver.us)
+    xo, uo = o.xs(), o.us()
+    for i, b in enumerate(spots):
+        for f in ("status", "iter", "n_iter_run", "steplength", "is_feasible"):
+            assert r[f][b] == ro[f][i], (what, b, f, r[f][b], ro[f][i])
+        assert abs(r["cost"][b] - ro["cost"][i]) <= 1e-6 * abs(ro["cost"][i]), (what, b, r["cost"][b], ro["cost"][i])
+        assert helpers.rel_err(xs[b], xo[i]) < 1e-6, (what, b, helpers.rel_err(xs[b], xo[i]))
+        assert helpers.rel_err(us[b], uo[i]) < 1e-6, (what, b, helpers.rel_err(us[b], uo[i]))
+    assert np.all(np.isfinite(xs)) and np.all(np.isfinite(r["cost"])), what
+
+
+@pytest.mark.parametrize("cfg", list(FULL))
+def test_fullsize_fixed_protocol_vs_oracle(cfg):
+    T, B = FULL[cfg]
+    solver = bench.make_shard_solver(cfg, B, 0, 0, presolve=False)
+    step = bench.FixedWarmStart(solver, 0)
+    spots = np.array([0, B // 2, B - 1])
+    o, _ = _oracle_spots(solver, spots)
+    for k in range(2):  # every step starts from the same warm start: same result twice
+        step(1)
+        o.set_candidate(*[None if a is None else a[spots] for a in solver.warm], False)
+        o.solve(maxiter=1, is_feasible=False, reg_init=0.1)
+        _compare(solver, o, spots, f"{cfg} fixed step {k}")
+    trials = bench.line_search_trials(solver)
+    assert trials.min() >= 1 and trials.max() <= 10
+
+
+@pytest.mark.parametrize("cfg", list(FULL))
+def test_fullsize_shift_protocol_vs_oracle(cfg):
+    T, B = FULL[cfg]
+    solver = bench.make_shard_solver(cfg, B, 0, 0, presolve=True)
+    spots = np.array([0, B // 2, B - 1])
+    o, knots = _oracle_spots(solver, spots)
+    o.solve(maxiter=5)
+    _compare(solver, o, spots, f"{cfg} presolve")
+    for k in range(2):
+        bench.mpc_step(solver, 1, rotate=True)
+        knots = knots[1:T] + knots[:1] + knots[T:]
+        kd = (_abi.KnotDesc * len(knots))(*[_abi.KnotDesc(*x) for x in knots])
+        assert o.L.oracle_set_knots(o.h, kd, _abi.dptr(o.pool), o.pool.size) == 0
+        o.mpc_shift()
+        o.solve(maxiter=1, is_feasible=False, reg_init=0.1)
+        _compare(solver, o, spots, f"{cfg} shift step {k}")
+    q = np.linalg.norm(np.asarray(solver.xs)[..., 3:7], axis=-1)
+    np.testing.assert_allclose(q, 1.0, atol=1e-9)
+
+
+def _solver_with_npar(cfg, B, npar, monkeypatch):
+    monkeypatch.setenv("CROCODDYL_AMD_LS_PAR", str(npar))  # read per handle at fddp_create
+    return bench.make_shard_solver(cfg, B, 0, 0, presolve=False)
+
+
+def test_parallel_line_search_equals_serial(monkeypatch):
+    """the 4-trial groups of the parallel line search give the serial
+    search's result bit for bit, on a batch that covers acceptance at alpha index 0..9
+    (slots above 0, later groups) and fully rejected searches."""
+    cfg, B = "C5_talos_walk", 256
+    out = {}
+    for npar in (4, 1):
+        s = _solver_with_npar(cfg, B, npar, monkeypatch)
+        step = bench.FixedWarmStart(s, 0)
+        hist = np.zeros(11, int)
+        snaps = []
+        for _ in range(3):  # fixed protocol, then two shift steps from its result
+            step(1) if not snaps else bench.mpc_step(s, 1, rotate=True)
+            r = helpers.results_dict(s._res())
+            L = s._h.refresh()
+            xt = np.zeros((B, s.problem.T + 1, s.problem.nx))
+            ut = np.zeros((B, s.problem.T, s.problem.nu_max))
+            from crocoddyl_amd._lib import lib
+            assert lib().fddp_get_xs_try(L, _abi.dptr(xt)) == 0 and lib().fddp_get_us_try(L, _abi.dptr(ut)) == 0
+            snaps.append((r, np.asarray(s.xs).copy(), np.asarray(s.us).copy(), xt, ut))
+            hist += np.bincount(bench.line_search_trials(s).astype(int), minlength=11)
+        out[npar] = (snaps, hist)
+    (par, hist), (ser, _) = out[4], out[1]
+    for k, (a, b) in enumerate(zip(par, ser)):
+        ra, rb = a[0], b[0]
+        for f in ("status", "iter", "n_iter_run", "is_feasible"):
+            np.testing.assert_array_equal(ra[f], rb[f], err_msg=f"step {k} {f}")
+        for f in ("steplength", "cost", "dV", "dVexp", "xreg", "stop"):
+            np.testing.assert_array_equal(ra[f], rb[f], err_msg=f"step {k} {f}")
+        np.testing.assert_array_equal(a[1], b[1], err_msg=f"step {k} xs")
+        np.testing.assert_array_equal(a[2], b[2], err_msg=f"step {k} us")
+        # the trial buffer: the accepted trial, or the last rejected one (alpha_9)
+        np.testing.assert_array_equal(a[3], b[3], err_msg=f"step {k} xs_try")
+        np.testing.assert_array_equal(a[4], b[4], err_msg=f"step {k} us_try")
+    # coverage of the parallel search's cases: accepted in group 0 slot > 0, in a
+    # later group, and the 10-trial searches (accepted at alpha_9 or all rejected)
+    assert hist[2:5].sum() > 0 and hist[5:10].sum() > 0 and hist[10] > 0, hist.tolist()
