@@ -1,5 +1,12 @@
 """Legged-locomotion problem builders with the reference's Python API.
 
+Attribution: the phase sequences, cost sets, weights and reference trajectories
+below restate Crocoddyl's gait builders (bindings/python/crocoddyl/utils/biped.py
+and quadruped.py), Copyright (C) 2018-2020, LAAS-CNRS, University of Edinburgh,
+BSD-3-Clause license. They are the workload definition of the C4 / C5 benchmarks
+and must reproduce the reference's knot sequences exactly, so the structure and
+identifiers follow the original.
+
 Mirrors bindings/python/crocoddyl/utils/biped.py (SimpleBipedGaitProblem, the
 Talos walking / jumping problems of benchmark/bipedal_walk_optctrl.py and
 bipedal-timings.cpp) and bindings/python/crocoddyl/utils/quadruped.py
@@ -428,7 +435,7 @@ class SimpleQuadrupedalGaitProblem:
         stateWeights = np.array([0.] * 3 + [500.] * 3 + [0.01] * (nv - 6) + [10.] * 6 + [1.] * (nv - 6))
         costModel.addCost("stateReg", self._stateReg(stateWeights, self.actuation.nu), 1e1)
         costModel.addCost("ctrlReg", mb.CostModelControl(self.state, self.actuation.nu), 1e-1)
-        if np.all(np.isfinite(self.state.lb[7:])):  # finite joint limits (module note)
+        if np.all(np.isfinite(self.state.lb[7:self.state.nq])):  # finite joint position limits (module note)
             lb = np.concatenate([self.state.lb[1:nv + 1], self.state.lb[-nv:]])
             ub = np.concatenate([self.state.ub[1:nv + 1], self.state.ub[-nv:]])
             lb, ub = np.nan_to_num(lb, neginf=-mb.DBL_MAX), np.nan_to_num(ub, posinf=mb.DBL_MAX)

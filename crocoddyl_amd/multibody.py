@@ -598,7 +598,7 @@ class ActivationBounds:
         if beta < 0.0 or beta > 1.0:
             raise ValueError("Invalid argument: The range of beta is between 0 and 1")
         fin = np.isfinite(lb) & np.isfinite(ub)
-        if np.any(lb[fin] - ub[fin] > 0):
+        if np.any(lb[fin] > ub[fin]):
             raise ValueError("Invalid argument: The lower and upper bounds are badly defined; ub has to be "
                              "bigger / equals to lb")
         with np.errstate(invalid="ignore", over="ignore"):

@@ -77,8 +77,22 @@ struct ActionModelBase : ControlLimits {
   virtual ~ActionModelBase() {}
   virtual int kind() const = 0;
   virtual int nx() const = 0;
+  virtual int ndx() const { return nx(); }  // StateAbstract::get_ndx (nx - 1 on a free-flyer state)
   virtual int nu() const = 0;
   virtual void pack(VectorXd& pool) const = 0;
+  int limits_nu() const { return nu(); }
+};
+
+// A differential (continuous-time) action model the device integrates with
+// IntegratedActionModelEuler (core/diff-action-base.hpp:41-72): its knot kind
+// under Euler and the block packer for a step dt.
+struct DifferentialActionModelBase : ControlLimits {
+  virtual ~DifferentialActionModelBase() {}
+  virtual int euler_kind() const = 0;
+  virtual int nx() const = 0;
+  virtual int ndx() const { return nx(); }
+  virtual int nu() const = 0;
+  virtual void pack_euler(double dt, VectorXd& pool) const = 0;
   int limits_nu() const { return nu(); }
 };
 
@@ -116,35 +130,37 @@ struct ActionModelUnicycle : ActionModelBase {  // unicycle.hxx:13-16
   }
 };
 
-struct DifferentialActionModelLQR : ControlLimits {  // diff-lqr.hxx:14-28
-  int nq, nu;
-  int limits_nu() const { return nu; }
+struct DifferentialActionModelLQR : DifferentialActionModelBase {  // diff-lqr.hxx:14-28
+  int nq, nu_;
   bool drift_free;
   VectorXd Fq, Fv, Fu, f0, Lxx, Lxu, Luu, lx, lu;
-  DifferentialActionModelLQR(int nq_, int nu_, bool drift_free_ = true)
-      : nq(nq_), nu(nu_), drift_free(drift_free_), Fq(eye(nq_, nq_)), Fv(eye(nq_, nq_)), Fu(eye(nq_, nu_)),
-        f0(nq_, 1.), Lxx(eye(2 * nq_, 2 * nq_)), Lxu(eye(2 * nq_, nu_)), Luu(eye(nu_, nu_)), lx(2 * nq_, 1.),
-        lu(nu_, 1.) {}
+  DifferentialActionModelLQR(int nq_, int nu__, bool drift_free_ = true)
+      : nq(nq_), nu_(nu__), drift_free(drift_free_), Fq(eye(nq_, nq_)), Fv(eye(nq_, nq_)), Fu(eye(nq_, nu__)),
+        f0(nq_, 1.), Lxx(eye(2 * nq_, 2 * nq_)), Lxu(eye(2 * nq_, nu__)), Luu(eye(nu__, nu__)), lx(2 * nq_, 1.),
+        lu(nu__, 1.) {}
+  int euler_kind() const { return FDDP_KNOT_EULER_DIFFLQR; }
+  int nx() const { return 2 * nq; }
+  int nu() const { return nu_; }
+  void pack_euler(double dt, VectorXd& p) const {
+    const double hdr[FDDP_PARAM_HEADER] = {dt, drift_free ? 1. : 0., 0., 0.};
+    p.insert(p.end(), hdr, hdr + FDDP_PARAM_HEADER);
+    for (const VectorXd* v : {&Fq, &Fv, &Fu, &f0, &Lxx, &Lxu, &Luu, &lx, &lu}) p.insert(p.end(), v->begin(), v->end());
+  }
 };
 
 struct IntegratedActionModelEuler : ActionModelBase {  // euler.hxx:16-35
-  std::shared_ptr<DifferentialActionModelLQR> differential;
+  std::shared_ptr<DifferentialActionModelBase> differential;
   double dt;
-  IntegratedActionModelEuler(std::shared_ptr<DifferentialActionModelLQR> d, double time_step = 1e-3)
+  IntegratedActionModelEuler(std::shared_ptr<DifferentialActionModelBase> d, double time_step = 1e-3)
       : differential(d), dt(time_step < 0. ? 1e-3 : time_step) {
     set_u_lb(d->get_u_lb());  // euler.hxx:25-26
     set_u_ub(d->get_u_ub());
   }
-  int kind() const { return FDDP_KNOT_EULER_DIFFLQR; }
-  int nx() const { return 2 * differential->nq; }
-  int nu() const { return differential->nu; }
-  void pack(VectorXd& p) const {
-    const DifferentialActionModelLQR& d = *differential;
-    const double hdr[FDDP_PARAM_HEADER] = {dt, d.drift_free ? 1. : 0., 0., 0.};
-    p.insert(p.end(), hdr, hdr + FDDP_PARAM_HEADER);
-    for (const VectorXd* v : {&d.Fq, &d.Fv, &d.Fu, &d.f0, &d.Lxx, &d.Lxu, &d.Luu, &d.lx, &d.lu})
-      p.insert(p.end(), v->begin(), v->end());
-  }
+  int kind() const { return differential->euler_kind(); }
+  int nx() const { return differential->nx(); }
+  int ndx() const { return differential->ndx(); }
+  int nu() const { return differential->nu(); }
+  void pack(VectorXd& p) const { differential->pack_euler(dt, p); }
 };
 
 // ShootingProblem over one problem (B = 1) or B problems sharing the models
@@ -157,9 +173,12 @@ class ShootingProblem {
       : x0_(to_vec(x0)), running_(running), terminal_(terminal), B_(batch) {
     if (running.empty()) throw Exception("Invalid argument: no running models");
     nx_ = running[0]->nx();
+    ndx_ = running[0]->ndx();
     nu_max_ = 0;
     for (size_t i = 0; i < running.size(); ++i) {  // shooting.hxx:28-49
       if (running[i]->nx() != nx_) throw Exception("Invalid argument: nx in " + std::to_string(i) + " node is not consistent");
+      if (running[i]->ndx() != ndx_)
+        throw Exception("Invalid argument: ndx in " + std::to_string(i) + " node is not consistent");
       if (running[i]->nu() > nu_max_) nu_max_ = running[i]->nu();
     }
     if (terminal->nx() != nx_) throw Exception("Invalid argument: nx in terminal node is not consistent");
@@ -167,7 +186,7 @@ class ShootingProblem {
   }
   int get_T() const { return (int)running_.size(); }
   int get_nx() const { return nx_; }
-  int get_ndx() const { return nx_; }
+  int get_ndx() const { return ndx_; }
   int get_nu_max() const { return nu_max_; }
   int get_B() const { return B_; }
   const VectorXd& get_x0() const { return x0_; }
@@ -226,7 +245,7 @@ class ShootingProblem {
   VectorXd x0_;
   std::vector<std::shared_ptr<ActionModelBase> > running_;
   std::shared_ptr<ActionModelBase> terminal_;
-  int nx_, nu_max_, B_;
+  int nx_, ndx_, nu_max_, B_;
 };
 
 // SolverFDDP (fddp.hpp:50-101) on the GPU.
