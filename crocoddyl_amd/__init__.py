@@ -13,7 +13,9 @@ problem written for ``crocoddyl`` drops in:
 """
 from ._lib import FDDPError, LIB_PATH  # noqa: F401
 from .models import (ActionData, ActionDataAbstract, ActionModelAbstract, ActionModelLQR, ActionModelUnicycle,  # noqa: F401
-                     DifferentialActionModelLQR, IntegratedActionModelEuler, StateVector)
+                     DifferentialActionData, DifferentialActionDataAbstract, DifferentialActionModelAbstract,
+                     DifferentialActionModelLQR, DifferentialActionModelNumDiff, IntegratedActionModelEuler,
+                     StateVector)
 from .problem import ShootingProblem, SolverBoxFDDP, SolverFDDP, pack_problem  # noqa: F401
 from .boxqp import BoxQP, BoxQPSolution  # noqa: F401
 

@@ -302,24 +302,92 @@ class IntegratedActionModelEuler(ActionModelAbstract):
     def __init__(self, diffModel, stepTime=1e-3, withCostResidual=True):
         from .multibody import DifferentialActionModelFreeFwdDynamics
         self._mb = isinstance(diffModel, DifferentialActionModelFreeFwdDynamics)
-        if not (self._mb or isinstance(diffModel, DifferentialActionModelLQR)):
-            raise NotImplementedError("crocoddyl_amd: the device path covers Euler(DifferentialActionModelLQR) "
-                                      "and Euler(DifferentialActionModelFreeFwdDynamics) knots only; got "
+        self._host = isinstance(diffModel, DifferentialActionModelAbstract)
+        if not (self._mb or self._host or isinstance(diffModel, DifferentialActionModelLQR)):
+            raise NotImplementedError("crocoddyl_amd: IntegratedActionModelEuler covers DifferentialActionModelLQR, "
+                                      "the multibody DAMs and Python-subclassed DifferentialActionModelAbstract; got "
                                       f"{type(diffModel).__name__}")
         if self._mb:
             self.kind = diffModel.knot_kind
+        if self._host:
+            # a Python-defined DAM: no device kind, so the knot (and its problem) runs on
+            # the host path (crocoddyl_amd.host), the integrator below in numpy
+            if diffModel.state.nx != diffModel.state.ndx:
+                raise NotImplementedError("crocoddyl_amd: Python-defined differential models are integrated on "
+                                          "Euclidean states (nx == ndx)")
+            self.kind = None
         super().__init__(diffModel.state, diffModel.nu, diffModel.nr)
         # the integrated model copies the differential model's limits (euler.hxx:25-26)
         self.u_lb = diffModel.u_lb
         self.u_ub = diffModel.u_ub
         self.differential = diffModel
-        if not self._mb:
+        if not (self._mb or self._host):
             diffModel._owners.append(self)
         self.withCostResidual = bool(withCostResidual)
         dt = float(stepTime)
         if dt < 0.0:  # euler.hxx:27-31
             dt = 1e-3
         self._dt = dt
+
+    # -- host path of a Python-defined DAM: euler.hxx:41-131 on numpy ----------------
+    def createData(self):
+        if not self.__dict__.get("_host"):
+            return ActionData(self)
+        return IntegratedActionDataEuler(self)
+
+    def calc(self, data, x, u=None):
+        """euler.hxx:41-80 (calc(data, x) evaluates at unone, action-base.hxx:28-37)."""
+        if not self.__dict__.get("_host"):
+            return super().calc(data, x, u)
+        x = np.asarray(x, float)
+        u = self.unone if u is None else np.asarray(u, float)
+        st, nv = self.differential.state, self.differential.state.nv
+        dd = data.differential
+        self.differential.calc(dd, x, u)
+        v, a = x[st.nx - nv:], np.asarray(dd.xout, float)
+        if self._dt != 0.0:  # enable_integration_
+            dt = self._dt
+            data.dx = np.concatenate([v * dt + a * (dt * dt), a * dt])
+            data.xnext = st.integrate(x, data.dx)
+            data.cost = dt * dd.cost
+        else:
+            data.dx = np.zeros(st.ndx)
+            data.xnext = x.copy()
+            data.cost = dd.cost
+        if self.withCostResidual:
+            data.r = np.array(dd.r, float, copy=True)
+
+    def calcDiff(self, data, x, u=None):
+        """euler.hxx:83-131 on a Euclidean state (Jintegrate = I, JintegrateTransport = id)."""
+        if not self.__dict__.get("_host"):
+            return super().calcDiff(data, x, u)
+        x = np.asarray(x, float)
+        u = self.unone if u is None else np.asarray(u, float)
+        st, nv, nu = self.differential.state, self.differential.state.nv, self.nu
+        dd = data.differential
+        self.differential.calcDiff(dd, x, u)
+        ndx = st.ndx
+        if self._dt != 0.0:
+            dt, dt2 = self._dt, self._dt * self._dt
+            da_dx, da_du = np.asarray(dd.Fx, float), np.asarray(dd.Fu, float).reshape(nv, nu)
+            Fx = np.zeros((ndx, ndx))
+            Fx[:nv] = da_dx * dt2
+            Fx[nv:] = da_dx * dt
+            Fx[np.arange(nv), ndx - nv + np.arange(nv)] += dt
+            Fx += np.eye(ndx)  # Jintegrate(first, addto) of a Euclidean state
+            data.Fx = Fx
+            Fu = np.zeros((ndx, nu))
+            Fu[:nv] = da_du * dt2
+            Fu[nv:] = da_du * dt
+            data.Fu = Fu
+            data.Lx, data.Lu = dt * np.asarray(dd.Lx, float), dt * np.asarray(dd.Lu, float)
+            data.Lxx, data.Lxu = dt * np.asarray(dd.Lxx, float), dt * np.asarray(dd.Lxu, float)
+            data.Luu = dt * np.asarray(dd.Luu, float)
+        else:
+            data.Fx = np.eye(ndx)
+            data.Fu = np.zeros((ndx, nu))
+            data.Lx, data.Lu = np.array(dd.Lx, float), np.array(dd.Lu, float)
+            data.Lxx, data.Lxu, data.Luu = np.array(dd.Lxx, float), np.array(dd.Lxu, float), np.array(dd.Luu, float)
 
     # the multibody DAM's parameters (robot, costs, armature) are part of the
     # version the problem compares before re-uploading parameter blocks
@@ -363,3 +431,119 @@ class IntegratedActionModelEuler(ActionModelAbstract):
                  _vec(d._f0, nq, "f0"), _colmajor(d._Lxx, nx, nx, "Lxx"), _colmajor(d._Lxu, nx, nu, "Lxu"),
                  _colmajor(d._Luu, nu, nu, "Luu"), _vec(d._lx, nx, "lx"), _vec(d._lu, nu, "lu")]
         return self.kind, nu, _stack(parts, [self._dt, 1.0 if d.driftFree else 0.0, 0, 0])
+
+
+class IntegratedActionDataEuler(ActionData):
+    """IntegratedActionDataEuler (euler.hpp): the differential model's data + dx."""
+
+    def __init__(self, model):
+        super().__init__(model)
+        self.differential = model.differential.createData()
+        self.dx = np.zeros(model.state.ndx)
+
+
+class DifferentialActionModelAbstract(_ControlLimits):
+    """Base of Python-defined differential (continuous-time) action models
+    (core/diff-action-base.hpp:41-72; Python overrides as
+    bindings/python/crocoddyl/core/diff-action-base.hpp:19-35): override
+    calc(data, x, u=None) to fill data.xout (the acceleration, nv), data.cost
+    (and data.r), and calcDiff(data, x, u=None) to fill data.Fx (nv x ndx),
+    data.Fu (nv x nu), data.Lx, data.Lu, data.Lxx, data.Lxu, data.Luu. Integrated
+    with IntegratedActionModelEuler, such a knot runs on the host path."""
+
+    def __init__(self, state, nu, nr=0):
+        self.state = state
+        self.nu = int(nu)
+        self.nr = int(nr)
+        self.unone = np.zeros(self.nu)
+        self._init_limits()
+
+    def calc(self, data, x, u=None):
+        raise NotImplementedError("crocoddyl_amd: calc of a Python-defined differential model must be overridden")
+
+    def calcDiff(self, data, x, u=None):
+        raise NotImplementedError("crocoddyl_amd: calcDiff of a Python-defined differential model must be overridden")
+
+    def createData(self):
+        return DifferentialActionData(self)
+
+
+class DifferentialActionData:
+    """DifferentialActionDataAbstract (core/diff-action-base.hpp:118-150)."""
+
+    def __init__(self, model):
+        nv, ndx, nu = model.state.nv, model.state.ndx, model.nu
+        self.cost = 0.0
+        self.xout = np.zeros(nv)
+        self.r = np.zeros(model.nr)
+        self.Fx = np.zeros((nv, ndx))
+        self.Fu = np.zeros((nv, nu))
+        self.Lx = np.zeros(ndx)
+        self.Lu = np.zeros(nu)
+        self.Lxx = np.zeros((ndx, ndx))
+        self.Lxu = np.zeros((ndx, nu))
+        self.Luu = np.zeros((nu, nu))
+
+
+DifferentialActionDataAbstract = DifferentialActionData
+
+
+class DifferentialActionModelNumDiff(DifferentialActionModelAbstract):
+    """DifferentialActionModelNumDiff(model, gaussApprox=False)
+    (core/numdiff/diff-action.hxx:13-93): forward differences of the model's calc
+    with disturbance sqrt(2 eps) along state.integrate(x, dx) and u + du; with
+    gaussApprox the cost Hessians from the residual Jacobians (Rx^T Rx, Rx^T Ru,
+    Ru^T Ru). calcDiff uses the data of the preceding calc at (x, u), as the reference."""
+
+    def __init__(self, model, gaussApprox=False):
+        super().__init__(model.state, model.nu, model.nr)
+        self.model = model
+        self.withGaussApprox = bool(gaussApprox)
+        self.disturbance = np.sqrt(2.0 * np.finfo(float).eps)
+        if self.withGaussApprox and self.nr == 1:
+            raise ValueError("No Gauss approximation possible with nr = 1")
+
+    def createData(self):
+        d = DifferentialActionData(self)
+        d.data_0 = self.model.createData()
+        d.data_x = [self.model.createData() for _ in range(self.state.ndx)]
+        d.data_u = [self.model.createData() for _ in range(self.nu)]
+        d.Rx = np.zeros((self.nr, self.state.ndx))
+        d.Ru = np.zeros((self.nr, self.nu))
+        return d
+
+    def calc(self, data, x, u=None):
+        u = self.unone if u is None else u
+        self.model.calc(data.data_0, x, u)
+        data.cost = data.data_0.cost
+        data.xout = np.array(data.data_0.xout, float, copy=True)
+
+    def calcDiff(self, data, x, u=None):
+        u = self.unone if u is None else np.asarray(u, float)
+        x = np.asarray(x, float)
+        d0 = data.data_0
+        xn0, c0, r0 = np.asarray(d0.xout, float), d0.cost, np.asarray(d0.r, float)
+        data.xout, data.cost = xn0.copy(), c0
+        h = self.disturbance
+        dx = np.zeros(self.state.ndx)
+        for ix in range(self.state.ndx):
+            dx[ix] = h
+            dxi = data.data_x[ix]
+            self.model.calc(dxi, self.state.integrate(x, dx), u)
+            data.Fx[:, ix] = (np.asarray(dxi.xout, float) - xn0) / h
+            data.Lx[ix] = (dxi.cost - c0) / h
+            data.Rx[:, ix] = (np.asarray(dxi.r, float) - r0) / h
+            dx[ix] = 0.0
+        du = np.zeros(self.nu)
+        for iu in range(self.nu):
+            du[iu] = h
+            dui = data.data_u[iu]
+            self.model.calc(dui, x, u + du)
+            data.Fu[:, iu] = (np.asarray(dui.xout, float) - xn0) / h
+            data.Lu[iu] = (dui.cost - c0) / h
+            data.Ru[:, iu] = (np.asarray(dui.r, float) - r0) / h
+            du[iu] = 0.0
+        if self.withGaussApprox:
+            data.Lxx = data.Rx.T @ data.Rx
+            data.Lxu = data.Rx.T @ data.Ru
+            data.Luu = data.Ru.T @ data.Ru
