@@ -121,11 +121,13 @@ def _cpu_baseline_child(cfg, T, seed, target_s, box, protocol):
     import helpers
     import oracle_lib
 
-    # -march=native build of the oracle for this host (built here, in /tmp)
+    # -march=native build of the oracle for this host (built here, in /tmp) with ROCm's
+    # clang++ and libomp (gcc 11's native build crashes on AVX-512 hosts: oracle/Makefile)
     out = os.path.join("/tmp", f"oracle_native_{os.getpid()}")
-    oracle_lib.build(out_dir=out, arch="-march=native")
+    cxx = "/opt/rocm/llvm/bin/clang++"
+    oracle_lib.build(out_dir=out, arch="-march=native", cxx=cxx, ldflags="-Wl,-rpath,/opt/rocm/llvm/lib")
     oracle_lib._lib = oracle_lib.lib(os.path.join(out, "liboracle.so"))
-    flags = "-O3 -march=native"
+    flags = f"{cxx} -O3 -march=native"
     threads, aff, quota = cpu_share()
 
     from crocoddyl_amd import _abi, synthetic

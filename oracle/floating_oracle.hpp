@@ -347,15 +347,19 @@ inline void crba(const Robot& rb, const Kin& K, double* M) {
   for (int i = rb.nb - 1; i >= 0; --i) {
     const int l = rb.parent[i];
     if (l < 0) continue;
-    double X[36], IX[36];
+    double X[36], IX[36], XtIX[36];
     mbo::xmotion(K.R[i], K.p[i], X);
     for (int c = 0; c < 6; ++c) m6v(Ic[i], X + 6 * c, IX + 6 * c);
     for (int c = 0; c < 6; ++c)
       for (int r = 0; r < 6; ++r) {
         double s = 0.;
         for (int k = 0; k < 6; ++k) s += X[r * 6 + k] * IX[c * 6 + k];
-        Ic[l][c * 6 + r] += s;
+        XtIX[c * 6 + r] = s;
       }
+    // accumulated into the parent in one contiguous pass: gcc 11 at -march=native on
+    // AVX-512 hosts (Zen 5: znver3 + avx512*) vectorised the strided += above with an
+    // aligned 32-byte store at a 16-byte-aligned address (the baseline's SIGSEGV)
+    for (int e = 0; e < 36; ++e) Ic[l][e] += XtIX[e];
   }
   std::memset(M, 0, sizeof(double) * nv * nv);
   for (int i = 0; i < rb.nb; ++i)
@@ -1042,10 +1046,12 @@ struct Knot {
     }
     // costs: stacked residual rows over (x, u) and diagonal terms (cost-sum.hxx:122-160)
     std::memset(Lxx, 0, sizeof(double) * n * n);
-    std::memset(Lxu, 0, sizeof(double) * n * m);
-    std::memset(Luu, 0, sizeof(double) * m * m);
+    if (m > 0) {  // impulse knots have no control blocks (null pointers)
+      std::memset(Lxu, 0, sizeof(double) * n * m);
+      std::memset(Luu, 0, sizeof(double) * m * m);
+      std::memset(Lu, 0, sizeof(double) * m);
+    }
     std::memset(Lx, 0, sizeof(double) * n);
-    std::memset(Lu, 0, sizeof(double) * m);
     static thread_local double R[kMaxRows * 3 * kMaxV];
     const int ld = L + nuk;
     for (int k = 0; k < ncost; ++k) {

@@ -22,13 +22,17 @@ ORACLE_SO = os.path.join(ORACLE_DIR, "_build", "liboracle.so")
 _lib = None
 
 
-def build(out_dir=None, arch=None):
+def build(out_dir=None, arch=None, cxx=None, ldflags=None):
     env = dict(os.environ)
     args = ["make", "-s", "-C", ORACLE_DIR]
     if out_dir:
         args.append(f"OUT={out_dir}")
     if arch:
         args.append(f"ARCH={arch}")
+    if cxx:
+        args.append(f"CXX={cxx}")
+    if ldflags:
+        args.append(f"LDFLAGS={ldflags}")
     subprocess.run(args, check=True, env=env)
 
 
