@@ -288,6 +288,8 @@ struct fddp_handle_s {
   int device = 0;
   int npar_env = 0;    // CROCODDYL_AMD_LS_PAR (0: chosen per problem)
   int npar_alloc = 1;  // trial slots allocated for the parallel line search
+  bool npar_adapt = false;  // trial-group size re-chosen after every solve (choose_npar)
+  double ls_slots = 0.;     // rollout workgroups resident on the device at once
   hipStream_t stream = nullptr;
   std::vector<fddp_knot_desc> knots;
   int64_t n_params = 0;
@@ -415,10 +417,24 @@ int launch_fused(fddp_handle* h, int sel_calc, int sel_diff, int gaps) {
   LAUNCH_CHECK();
   return FDDP_OK;
 }
+// The knot-parallel kernel's LDS plan leaves room for one workgroup per CU: take the
+// 1-wave/EU build (no spills; FDDP_MB_W1=0 forces the 2-wave one, for A/B runs).
+static bool mb_one_per_cu(const fddp_handle* h) {
+  static const int env = [] {
+    const char* e = std::getenv("FDDP_MB_W1");
+    return e ? (e[0] == '0' ? 0 : 1) : -1;
+  }();
+  return env >= 0 ? env == 1 : h->mb_diff_smem > 80 * 1024;
+}
 // Multibody knots (knot-parallel): calc for sel_calc, calcDiff for sel_diff (-1: none).
 int launch_mb(fddp_handle* h, int sel_calc, int sel_diff) {
   const Dev& D = h->D;
-  hipLaunchKernelGGL(mb_knot_kernel, dim3(D.T + 1, D.B), dim3(mb::kMbDiffNT), h->mb_diff_smem, h->stream, D, sel_calc, sel_diff);
+  if (mb_one_per_cu(h))
+    hipLaunchKernelGGL(mb_knot_kernel_w1, dim3(D.T + 1, D.B), dim3(mb::kMbDiffNT), h->mb_diff_smem, h->stream, D, sel_calc,
+                       sel_diff);
+  else
+    hipLaunchKernelGGL(mb_knot_kernel, dim3(D.T + 1, D.B), dim3(mb::kMbDiffNT), h->mb_diff_smem, h->stream, D, sel_calc,
+                       sel_diff);
   LAUNCH_CHECK();
   return FDDP_OK;
 }
@@ -549,6 +565,57 @@ static bool mb_rollout(const fddp_handle* h) {
     return e && e[0] == '0';
   }();
   return h->all_mb && !off;
+}
+
+// Trial-group size of the next line searches from the trial counts of the last one
+// (the results are bit-identical for every size; only the work and the number of
+// sequential launches change). With S rollout workgroups resident at once and t_b the
+// trials element b needed: serial (1) takes ~max(sum t_b / S, max t_b) trial-times, one
+// group launch per g trials ~sum_k max(U_k / S, 1) with U_k the trial slots of group k.
+static void choose_npar(fddp_handle* h, const std::vector<ElemState>& st) {
+  if (!h->npar_adapt || h->fast) return;
+  const int na = h->prm.n_alphas;
+  if (h->ls_slots <= 0.) {
+    int dev_cus = 0, per_cu = 0;
+    (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, h->device);
+    const void* k = mb_rollout(h) ? (const void*)forward_kernel<kNT, false, true> : (const void*)forward_kernel<kNT, false>;
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, kNT, h->fwd_smem);
+    h->ls_slots = (double)std::max(1, dev_cus) * std::max(1, per_cu);
+  }
+  std::vector<int> t;
+  t.reserve(st.size());
+  for (const ElemState& s : st) {
+    if (s.n_iter_run <= 0) continue;
+    int k = na;  // exhausted: every alpha tried
+    for (int a = 0; a < na; ++a)
+      if (s.steplength == h->prm.alphas[a]) {
+        k = a + 1;
+        break;
+      }
+    t.push_back(k);
+  }
+  if (t.empty()) return;
+  const double S = h->ls_slots;
+  double best = 0.;
+  int best_g = 1;
+  for (int g : {1, 2, 4}) {
+    double time = 0.;
+    if (g == 1) {
+      double w = 0.;
+      int tmax = 0;
+      for (int v : t) w += v, tmax = std::max(tmax, v);
+      time = std::max(w / S, (double)tmax);
+    } else {
+      for (int k0 = 0; k0 < na; k0 += g) {
+        const int slots = std::min(g, na - k0);
+        double u = 0.;
+        for (int v : t) u += v > k0 ? slots : 0;
+        if (u > 0.) time += std::max(u / S, 1.);
+      }
+    }
+    if (g == 1 || time < best) best = time, best_g = g;
+  }
+  h->D.npar = best_g;
 }
 
 int launch_forward(fddp_handle* h, int mode, double alpha, int* count) {
@@ -714,6 +781,7 @@ int apply_knots(fddp_handle* h, const fddp_knot_desc* knots, const double* param
     // forward -12 %), where one rollout keeps a CU busy longest; on small ones (C4
     // Solo12, nv = 18) the extra trials cost more than the shorter chains save
     D.npar = h->npar_env ? h->npar_env : (h->has_mb && mb_nj >= 24 ? 4 : 1);
+    h->npar_adapt = !h->npar_env && h->has_mb;
     int64_t mb_pmax = 0;  // largest multibody parameter block (staged in LDS by mb_knot_kernel)
     for (int t = 0; t <= d.T; ++t)
       if (is_mb_kind(knots[t].kind)) {
@@ -790,6 +858,8 @@ int apply_knots(fddp_handle* h, const fddp_knot_desc* knots, const double* param
       hipFuncSetAttribute((const void*)calc_diff_kernel<kNT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)h->cdiff_smem) != hipSuccess ||
       (h->has_mb && hipFuncSetAttribute((const void*)mb_knot_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        (int)h->mb_diff_smem) != hipSuccess) ||
+      (h->has_mb && hipFuncSetAttribute((const void*)mb_knot_kernel_w1, hipFuncAttributeMaxDynamicSharedMemorySize,
                                         (int)h->mb_diff_smem) != hipSuccess))
     return fail(FDDP_ERR_RUNTIME, "hipFuncSetAttribute(dynamic LDS)");
   {  // backward sweep variant: MFMA tiles when every running knot has nu == nu_max
@@ -1120,6 +1190,7 @@ int fddp_solve(fddp_handle* h, int maxiter, int is_feasible, double reg_init, fd
     std::vector<ElemState> st;
     if ((rc = download_states(h, st))) return rc;
     for (int b = 0; b < D.B; ++b) fill_result(st[b], &out[b]);
+    choose_npar(h, st);
   } else {
     HIP_TRY(hipStreamSynchronize(h->stream));
   }

@@ -248,7 +248,7 @@ __global__ __launch_bounds__(NT) void calc_diff_kernel(Dev D, int sel, int gaps,
 // (derivative blocks) for those selected by sel_diff (-1: none), fused: the
 // calcDiff evaluates the dynamics the calc needs anyway. The gaps of these
 // knots are written by calc_diff_kernel as for any knot.
-__global__ __launch_bounds__(mb::kMbDiffNT) __attribute__((amdgpu_waves_per_eu(2))) void mb_knot_kernel(Dev D, int sel_calc, int sel_diff) {
+__device__ __forceinline__ void mb_knot_body(const Dev& D, int sel_calc, int sel_diff) {
   const int t = blockIdx.x, b = blockIdx.y;
   const fddp_knot_desc kd = D.knots[t];
   if (!is_mb_kind(kd.kind)) return;
@@ -277,6 +277,17 @@ __global__ __launch_bounds__(mb::kMbDiffNT) __attribute__((amdgpu_waves_per_eu(2
   else
     mb::knot_calc_diff(P, D.nx, D.m, xg, ug, running && kd.nu > 0, sm, nullptr, nullptr, nullptr, nullptr, nullptr,
                        nullptr, nullptr, xn, cost);
+}
+// Two register budgets of the same kernel: 2 waves/EU (256 VGPRs, a few spills) lets two
+// workgroups share a CU where the LDS plan allows it (<= 80 KB: the trot, the arm); when
+// the plan leaves room for one workgroup per CU anyway (Talos: ~140 KB) the 1-wave/EU
+// build gets the whole register file (VGPRs + AGPRs) and nothing spills.
+__global__ __launch_bounds__(mb::kMbDiffNT) __attribute__((amdgpu_waves_per_eu(2))) void mb_knot_kernel(Dev D, int sel_calc, int sel_diff) {
+  mb_knot_body(D, sel_calc, sel_diff);
+}
+__global__ __launch_bounds__(mb::kMbDiffNT) __attribute__((amdgpu_waves_per_eu(1, 1))) void mb_knot_kernel_w1(Dev D, int sel_calc,
+                                                                                                   int sel_diff) {
+  mb_knot_body(D, sel_calc, sel_diff);
 }
 
 // ---------------------------------------------------------------------------

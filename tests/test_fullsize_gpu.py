@@ -101,22 +101,21 @@ def test_fullsize_shift_protocol_vs_oracle(cfg):
 
 def _solver_with_npar(cfg, B, npar, monkeypatch):
     monkeypatch.setenv("CROCODDYL_AMD_LS_PAR", str(npar))  # read per handle at fddp_create
-    return bench.make_shard_solver(cfg, B, 0, 0, presolve=False)
+    return bench.make_shard_solver(cfg, B, 0, 0, presolve=True)
 
 
 def test_parallel_line_search_equals_serial(monkeypatch):
     """the 4-trial groups of the parallel line search give the serial
-    search's result bit for bit, on a batch that covers acceptance at alpha index 0..9
-    (slots above 0, later groups) and fully rejected searches."""
-    cfg, B = "C5_talos_walk", 256
+    search's result bit for bit, on receding-horizon steps whose line searches accept
+    at every alpha index 0..9 (slots above 0, later groups) or reject every trial."""
+    cfg, B = "C5_talos_walk", 512
     out = {}
     for npar in (4, 1):
         s = _solver_with_npar(cfg, B, npar, monkeypatch)
-        step = bench.FixedWarmStart(s, 0)
         hist = np.zeros(11, int)
         snaps = []
-        for _ in range(3):  # fixed protocol, then two shift steps from its result
-            step(1) if not snaps else bench.mpc_step(s, 1, rotate=True)
+        for _ in range(3):
+            bench.mpc_step(s, 1, rotate=True)
             r = helpers.results_dict(s._res())
             L = s._h.refresh()
             xt = np.zeros((B, s.problem.T + 1, s.problem.nx))
@@ -141,3 +140,27 @@ def test_parallel_line_search_equals_serial(monkeypatch):
     # coverage of the parallel search's cases: accepted in group 0 slot > 0, in a
     # later group, and the 10-trial searches (accepted at alpha_9 or all rejected)
     assert hist[2:5].sum() > 0 and hist[5:10].sum() > 0 and hist[10] > 0, hist.tolist()
+
+
+def test_adaptive_trial_groups_give_the_same_solves():
+    """The trial-group size chosen per solve from the last line search's trial counts
+    (fddp_hip.hip choose_npar) changes the work, not the result: the default handle's
+    receding-horizon steps equal the serial handle's bit for bit."""
+    cfg, B = "C5_talos_walk", 256
+    res = []
+    for env in (None, "1"):
+        if env:
+            os.environ["CROCODDYL_AMD_LS_PAR"] = env
+        try:
+            s = bench.make_shard_solver(cfg, B, 0, 0, presolve=True)
+        finally:
+            os.environ.pop("CROCODDYL_AMD_LS_PAR", None)
+        snaps = []
+        for _ in range(3):
+            bench.mpc_step(s, 1, rotate=True)
+            snaps.append((np.asarray(s.xs).copy(), np.asarray(s.cost).copy(), np.asarray(s.stepLength).copy()))
+        res.append(snaps)
+    for (xa, ca, sa), (xb, cb, sb) in zip(*res):
+        np.testing.assert_array_equal(sa, sb)
+        np.testing.assert_array_equal(ca, cb)
+        np.testing.assert_array_equal(xa, xb)
