@@ -704,7 +704,7 @@ __device__ __forceinline__ double gains_dot(const double* K, int m, int i, int n
 template <int NT, bool MB = false>
 __device__ __forceinline__ bool fwd_trial(const Dev& D, int b, const ElemState& s, double alpha, double* xv, double* uv, double* xn,
                           double* red, int* flag, double& cost_try, double& dv, double* pl, int64_t pcap,
-                          const double*& cached, double* mbw, double* dxv, int slot = 0) {
+                          const double*& cached, double* mbw, double* dxv, int slot = 0, int* nwritten = nullptr) {
   const int n = D.n, nx = D.nx, m = D.m, T = D.T, tid = threadIdx.x;
   const int c = s.cur, o = 1 - c;
   const TrialOut out(D, o, slot);
@@ -784,8 +784,12 @@ __device__ __forceinline__ bool fwd_trial(const Dev& D, int b, const ElemState& 
     }
     cost_try += ct;
     bad |= raise_if_nan(cost_try);
-    if (wg_any(bad, flag)) return false;
+    if (wg_any(bad, flag)) {
+      if (nwritten) *nwritten = t + 1;  // the knots of the trial buffers this trial wrote
+      return false;
+    }
   }
+  if (nwritten) *nwritten = T + 1;
   // dv: terminal first, then t = 0..T-1 (fddp.cpp:110-119). Summed by the
   // thread that stored the terms (program order), broadcast through LDS.
   if (tid == 0) {
@@ -907,12 +911,13 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((FAST || MB)
     flag = (int*)(red + 5 * (NT / kWave) + 8);
   }
   ElemState s = *st;
+  int nwr = D.T + 1;
   auto trial = [&](double alpha, double& ct, double& dv) {
     if constexpr (FAST)
       return fwd_trial_fast<NT, true>(D, b, s, alpha, xv, dxv, xn, pa, pdyn, red, flag, ct, dv, pl, pcap, cached);
     else
       return fwd_trial<NT, MB>(D, b, s, alpha, xv, uv, xn, red, flag, ct, dv, pl, pcap, cached, (double*)flag + 2 + 2 * D.sN,
-                           (double*)flag + 2, slot);
+                           (double*)flag + 2, slot, &nwr);
   };
   // line search (fddp.cpp:53-81). One call site of the trial, so it is inlined (its
   // LDS pointers keep their address space).
@@ -938,6 +943,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((FAST || MB)
         r[0] = ok ? 1. : 0.;
         r[1] = ct;
         r[2] = dv;
+        r[3] = (double)nwr;  // knots written (a failed trial stops early)
       }
       return;
     }
@@ -996,11 +1002,14 @@ __global__ __launch_bounds__(NT) void ls_select_kernel(Dev D, Prm prm, int group
   const int last_slot = prm.n_alphas - 1 - group * D.npar;
   const int copy_slot = acc_slot >= 0 ? acc_slot : last_slot;
   if (copy_slot > 0) {
+    // only the knots the trial wrote: a trial stopped by a forward_error leaves the
+    // rest of the buffer as it was, as in the serial search
     const TrialOut src(D, 0, copy_slot), dst(D, acc_slot >= 0 ? s.cur : 1 - s.cur, 0);
-    const int64_t K1 = D.T + 1;
+    const int64_t K1 = (int64_t)D.ptrial[((int64_t)b * D.npar + copy_slot) * 4 + 3];
+    const int64_t K0 = K1 < D.T ? K1 : D.T;
     for (int64_t i = tid; i < K1 * D.sX; i += NT) dst.xs[D.knot(b, 0) * D.sX + i] = src.xs[D.knot(b, 0) * D.sX + i];
-    for (int64_t i = tid; i < D.T * D.sM; i += NT) dst.us[D.run(b, 0) * D.sM + i] = src.us[D.run(b, 0) * D.sM + i];
-    for (int64_t i = tid; i < D.T * D.sX; i += NT)
+    for (int64_t i = tid; i < K0 * D.sM; i += NT) dst.us[D.run(b, 0) * D.sM + i] = src.us[D.run(b, 0) * D.sM + i];
+    for (int64_t i = tid; i < K0 * D.sX; i += NT)
       dst.xnext[D.run(b, 0) * D.sX + i] = src.xnext[D.run(b, 0) * D.sX + i];
     for (int64_t i = tid; i < K1; i += NT) dst.kcost[D.knot(b, 0) + i] = src.kcost[D.knot(b, 0) + i];
   }

@@ -1843,8 +1843,9 @@ struct DiffLayout {
 constexpr int kMaxCostRows = 64;
 // (4 columns of slack: the GEMM reads rows four columns at a time)
 MB_HD __forceinline__ int cost_rows_ld(int nj, int nu) { return (int)pad2(2 * nj + nu) + 4; }
+constexpr int kMaxCostCols = 3 * kMaxJ;  // diagonal terms per column of [x tangent | u]
 MB_HD __forceinline__ int64_t cost_area_doubles(int nj, int nu, int nrows) {
-  return 4 * kMaxCosts + 5 * kMaxCostRows + (int64_t)nrows * cost_rows_ld(nj, nu);
+  return 4 * kMaxCosts + 5 * kMaxCostRows + kMaxCostCols + (int64_t)nrows * cost_rows_ld(nj, nu);
 }
 __host__ __device__ inline DiffLayout diff_layout(int nj, int njac, int nc = 0, bool vel_cols = false, int nu = 0,
                                                   int nrows = 0) {
@@ -2262,6 +2263,113 @@ MB_HD inline void jac_lane(const Blk& b, const WVals& W, const double* x, int j,
 // pass reports as backward_error. `w`: diff_layout(nj, njac, nc).total doubles of LDS.
 // xnext_out / cost_out (may be null): the knot's calc (xnext, cost) as well;
 // Fx == nullptr: calc only (no derivative block is written).
+#if defined(__HIP_DEVICE_COMPILE__)
+// ---- fp64 matrix-core products of the calcDiff (v_mfma_f64_16x16x4_f64) -------
+// Fragment maps (MI355X guide, f64 16x16x4): A[i = lane & 15][k = lane >> 4],
+// B[k = lane >> 4][j = lane & 15], C/D col = lane & 15, row = (lane >> 4) + 4 reg.
+// Every wave of the workgroup takes 16 x 16 output tiles round-robin; loads outside
+// the operands read as exact zeros, so padded rows / columns stay zero.
+typedef double mb_f64x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ mb_f64x4 mb_mfma(double a, double b, mb_f64x4 c) {
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+typedef __attribute__((address_space(3))) double mb_lds_d;
+__device__ __attribute__((noinline)) void da_mfma_lds(const mb_lds_d* Minv, int lda, const mb_lds_d* H,
+                                                      const mb_lds_d* dtau, const mb_lds_d* da0, int nj, int nc, int L,
+                                                      int Ld, double mul_v, int vcols, mb_lds_d* da) {
+  const int lane = (int)threadIdx.x & 63, wave = (int)threadIdx.x >> 6, nw = (int)blockDim.x >> 6;
+  const int li = lane & 15, lk = lane >> 4;
+  const int tr = (nj + 15) >> 4, tc = (L + 15) >> 4, K = nj + nc;
+#pragma unroll 1
+  for (int tile = wave; tile < tr * tc; tile += nw) {
+    const int ti = tile / tc, tj = tile - ti * tc;
+    const int r = 16 * ti + li, c = 16 * tj + li;
+    const bool rv = r < nj, cvld = c < L;
+    mb_f64x4 acc = {0., 0., 0., 0.};
+#pragma unroll 1
+    for (int kb = 0; kb < K; kb += 4) {
+      const int k = kb + lk;
+      const bool km = k < nj, kh = !km && k < K;
+      const double a = (rv && km) ? Minv[k * lda + r] : ((rv && kh) ? H[(k - nj) * nj + r] : 0.);
+      const double bv = (cvld && km) ? dtau[k * L + c] : ((cvld && kh) ? da0[(k - nj) * L + c] : 0.);
+      acc = mb_mfma(a, bv, acc);
+    }
+    // (impulse knots: the v columns (>= vcols) are zero; a failed factorisation: NaN)
+    const int jc = 16 * tj + li;
+    const double mul = jc >= vcols ? 0. * mul_v : mul_v;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int i = 16 * ti + lk + 4 * q;
+      if (i < nj && jc < L) da[i * Ld + jc] = acc[q] * mul;
+    }
+  }
+}
+// da = -(Kinv_tl dtau + H da0) (contact-fwddyn.hxx:127-140 as computeABADerivatives /
+// the KKT inverse): [Kinv_tl | H] (nj x (nj + nc)) times [dtau; da0] ((nj + nc) x L),
+// rows of da at stride Ld; impulse knots keep only the q columns.
+__device__ __forceinline__ void da_mfma(const double* Minv, int lda, const double* H, const double* dtau,
+                                        const double* da0, int nj, int nc, int L, int Ld, bool imp, bool ok,
+                                        double* da) {
+  da_mfma_lds((const mb_lds_d*)lds_ptr(Minv), lda, (const mb_lds_d*)lds_ptr(H), (const mb_lds_d*)lds_ptr(dtau),
+              (const mb_lds_d*)lds_ptr(da0), nj, nc, L, Ld, ok ? -1. : (double)NAN, imp ? nj : L,
+              (mb_lds_d*)lds_ptr(da));
+}
+
+// The Gauss-Newton blocks sc * (R^T diag(w h) R + the diagonal state / control terms)
+// (cost-sum.hxx:122-160) over the combined column space [x tangent (L) | u (m)]: the
+// upper-triangle 16 x 16 tiles (bi <= bj) of the (L + m)^2 product; Lxx and Luu are
+// written from the upper triangle and mirrored, Lxu from the x-row / u-column tiles.
+// wrow[r]: the row's weight times its activation Hessian (w h).
+__device__ __forceinline__ void gn_blocks_mfma(const double* Rm, int ldR, const double* wrow, int nrows, int L,
+                                               int nu, int m, double sc, double* Lxx, double* Lxu, double* Luu,
+                                               const double* diag) {
+  const int lane = (int)threadIdx.x & 63, wave = (int)threadIdx.x >> 6, nw = (int)blockDim.x >> 6;
+  const int li = lane & 15, lk = lane >> 4;
+  const int NC = L + m, cv = L + nu, NT = (NC + 15) >> 4, ntiles = NT * (NT + 1) / 2, n = L;
+  Rm = lds_ptr(Rm);
+  wrow = lds_ptr(wrow);
+  diag = lds_ptr(diag);
+#pragma unroll 1
+  for (int tile = wave; tile < ntiles; tile += nw) {
+    int bi = 0, rem = tile;
+    while (rem >= NT - bi) {
+      rem -= NT - bi;
+      ++bi;
+    }
+    const int bj = bi + rem;
+    const int ca = 16 * bi + li, cb = 16 * bj + li;
+    mb_f64x4 acc = {0., 0., 0., 0.};
+#pragma unroll 2
+    for (int kb = 0; kb < nrows; kb += 4) {
+      const int r = kb + lk;
+      double a = 0., bv = 0.;
+      if (r < nrows) {
+        const double* Rr = Rm + (int64_t)r * ldR;
+        a = ca < cv ? Rr[ca] * wrow[r] : 0.;
+        bv = cb < cv ? Rr[cb] : 0.;
+      }
+      acc = mb_mfma(a, bv, acc);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int i = 16 * bi + lk + 4 * q, j = 16 * bj + li;
+      if (i > j || j >= NC) continue;
+      const double v = sc * (i == j ? acc[q] + diag[i] : acc[q]);
+      if (j < L) {  // Lxx (symmetric)
+        mb_gstore(Lxx + (int64_t)j * n + i, v);
+        if (i < j) mb_gstore(Lxx + (int64_t)i * n + j, v);
+      } else if (i < L) {  // Lxu
+        mb_gstore(Lxu + (int64_t)(j - L) * n + i, v);
+      } else {  // Luu (symmetric)
+        mb_gstore(Luu + (int64_t)(j - L) * m + (i - L), v);
+        if (i < j) mb_gstore(Luu + (int64_t)(i - L) * m + (j - L), v);
+      }
+    }
+  }
+}
+#endif
+
 template <class X>
 MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, const double* xg, const double* ug,
                                    bool use_u, double* w, double* Fx, double* Fu, double* Lxx, double* Lxu,
@@ -2500,15 +2608,21 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
   double* cav = cam + kMaxCostRows;
   double* csrc = cav + kMaxCostRows;
   double* cgi = csrc + kMaxCostRows;  // group of each row
-  double* Rm = csrc + 2 * kMaxCostRows;
+  double* cdg = cgi + kMaxCostRows;   // device: the state / control diagonal terms per column
+  double* Rm = cdg + kMaxCostCols;
   const int ldR = cost_rows_ld(nj, nu);
   // da = -Kinv_tl dtau - H da0 (impulse: -G dtau_dq - H dv0_dq on the q columns) on all
   // lanes but the last ncost, which build the cost-derivative table meanwhile (its area may be
   // the world-value area, dead since the tangent-direction phase)
   ex.run([&](int lane) {
+    const int nl = ex.nt - (b.ncost > 0 ? b.ncost : 1);
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(MB_NO_MFMA_DA)
+    // on the matrix cores, every wave (the whole workgroup is converged here)
+    da_mfma(Minv, lda, H, dtau, da0, nj, nc, L, Ld, imp, ok, da);
+#else
     // two entries per lane at a time: two independent dot-product chains, so the LDS
     // loads of one overlap the other's FMAs (each entry's summation order unchanged)
-    const int ne = nj * L, nl = ex.nt - (b.ncost > 0 ? b.ncost : 1);
+    const int ne = nj * L;
     for (int e0 = lane; e0 < ne && lane < nl; e0 += 2 * nl) {
       const int e1 = e0 + nl < ne ? e0 + nl : e0;
       const int r0 = e0 / L, c0 = e0 % L, r1 = e1 / L, c1 = e1 % L;
@@ -2526,6 +2640,7 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
       da[(int64_t)r0 * Ld + c0] = ok ? -s0 : NAN;
       if (e1 != e0) da[(int64_t)r1 * Ld + c1] = ok ? -s1 : NAN;
     }
+#endif
     if (fd) {
       const double* Sinv = Sx + (int64_t)nc * nc;
       for (int e = lane; e < nc * L; e += ex.nt) {
@@ -2687,10 +2802,33 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
           v = force_jac(C, dfu + (c - L), nj, e2);
       }
       Rm[e] = c < L + nu ? v : 0.;
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(MB_NO_MFMA_GN)
+      // the matrix-core GEMM takes each row's weight times its activation Hessian (w h)
+      if (c == 0) {
+        const CRec C{P + (int64_t)cg[4 * (int)cgi[row] + 2]};
+        ch[row] *= C.weight();
+      }
+#endif
     }
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(MB_NO_MFMA_GN)
+    // the diagonal terms of the state / control costs (beyond the free-flyer block), per
+    // column of [x tangent | u], in cost order
+    for (int i = lane; i < L + m; i += ex.nt) {
+      double d = 0.;
+      for (int g = 0; g < ngr; ++g) {
+        if ((int)cg[4 * g] >= 0) continue;
+        const CRec C{P + (int64_t)cg[4 * g + 2]};
+        if (cg[4 * g + 1] == 0. && i < L && !(b.ff && i < 6))
+          d += C.weight() * cost_act(b, C, nu).hess(i, state_res(b, C.d(), x, i));
+        else if (cg[4 * g + 1] == 1. && i >= L && i - L < nu)
+          d += C.weight() * cost_act(b, C, nu).hess(i - L, u[i - L] - C.d()[i - L]);
+      }
+      cdg[i] = d;
+    }
+#endif
   });
   const double *const Rm_ = Rm, *const ch_ = ch, *const cg_ = cg, *const cam_ = cam, *const cav_ = cav, *const P_ = P,
-                      *const x_ = x, *const u_ = u;
+                      *const x_ = x, *const u_ = u, *const cdg_ = cdg;
   // Gauss-Newton blocks (cost-sum.hxx:122-160) as a small GEMM over the rows, in
   // cost order: Lxx / Lxu / Luu entries four rows i at a time, then Lx / Lu.
   ex.run([&](int lane) {
@@ -2704,6 +2842,9 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
     const double* const P = ex.lds(P_);
     const double* const x = ex.lds(x_);
     const double* const u = ex.lds(u_);
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(MB_NO_MFMA_GN)
+    gn_blocks_mfma(Rm, ldR, ch, nrows, L, nu, m, sc, Lxx, Lxu, Luu, cdg_);
+#else
     const int n4 = (n + 3) / 4, m4 = (m + 3) / 4;
     // Lxx is symmetric: only its row blocks i0 <= j are tasks (column j has j / 4 + 1 of
     // them; columns 4a .. 4a+3 follow 2a(a+1) tasks), each entry above the diagonal also
@@ -2786,6 +2927,7 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
         if (blk == 0 && i < j) mb_gstore(out + (int64_t)i * rows + j, v);
       }
     }
+#endif
     // Lx (x columns) and Lu (u columns): R^T Ar in cost order
     for (int c = lane; c < n + m; c += ex.nt) {
       const bool isu = c >= n;
