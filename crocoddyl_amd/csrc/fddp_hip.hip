@@ -843,25 +843,31 @@ int apply_knots(fddp_handle* h, const fddp_knot_desc* knots, const double* param
     HIP_TRY(hipMemcpyAsync((void*)D.segend, se.data(), sizeof(int) * se.size(), hipMemcpyHostToDevice, h->stream));
     HIP_TRY(hipStreamSynchronize(h->stream));  // the host staging vectors go out of scope
   }
-  if (hipFuncSetAttribute((const void*)backward_kernel<kNT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)h->bwd_smem) != hipSuccess ||
-      hipFuncSetAttribute((const void*)forward_kernel<kNT, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)h->fwd_smem) != hipSuccess ||
-      hipFuncSetAttribute((const void*)forward_kernel<kNT, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)h->fwd_fast_smem) != hipSuccess ||
-      (h->has_mb && hipFuncSetAttribute((const void*)forward_kernel<kNT, false, true>,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->fwd_smem) != hipSuccess) ||
-      hipFuncSetAttribute((const void*)calc_tiled_kernel<kNTF>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)h->fused_smem) != hipSuccess ||
-      hipFuncSetAttribute((const void*)calc_kernel<kNT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)h->calc_smem) != hipSuccess ||
-      hipFuncSetAttribute((const void*)calc_diff_kernel<kNT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)h->cdiff_smem) != hipSuccess ||
-      (h->has_mb && hipFuncSetAttribute((const void*)mb_knot_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                        (int)h->mb_diff_smem) != hipSuccess) ||
-      (h->has_mb && hipFuncSetAttribute((const void*)mb_knot_kernel_w1, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                        (int)h->mb_diff_smem) != hipSuccess))
-    return fail(FDDP_ERR_RUNTIME, "hipFuncSetAttribute(dynamic LDS)");
+  {  // dynamic LDS of every kernel the handle may launch (a refusal names the kernel and size)
+    struct Req {
+      const void* f;
+      size_t bytes;
+      bool use;
+      const char* name;
+    } reqs[] = {
+        {(const void*)backward_kernel<kNT>, h->bwd_smem, true, "backward_kernel"},
+        {(const void*)forward_kernel<kNT, false>, h->fwd_smem, true, "forward_kernel"},
+        {(const void*)forward_kernel<kNT, true>, h->fwd_fast_smem, true, "forward_kernel<fast>"},
+        {(const void*)forward_kernel<kNT, false, true>, h->fwd_smem, h->has_mb, "forward_kernel<multibody>"},
+        {(const void*)calc_tiled_kernel<kNTF>, h->fused_smem, true, "calc_tiled_kernel"},
+        {(const void*)calc_kernel<kNT>, h->calc_smem, true, "calc_kernel"},
+        {(const void*)calc_diff_kernel<kNT>, h->cdiff_smem, true, "calc_diff_kernel"},
+        {(const void*)mb_knot_kernel, h->mb_diff_smem, h->has_mb, "mb_knot_kernel"},
+        {(const void*)mb_knot_kernel_w1, h->mb_diff_smem, h->has_mb, "mb_knot_kernel_w1"},
+    };
+    for (const Req& r : reqs) {
+      if (!r.use) continue;
+      const hipError_t e = hipFuncSetAttribute(r.f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)r.bytes);
+      if (e != hipSuccess)
+        return fail(FDDP_ERR_RUNTIME, std::string("hipFuncSetAttribute(dynamic LDS) of ") + r.name + ": " +
+                                          std::to_string(r.bytes) + " bytes: " + hipGetErrorString(e));
+    }
+  }
   {  // backward sweep variant: MFMA tiles when every running knot has nu == nu_max
     bool uniform_nu = d.nu_max > 0;
     for (int t = 0; t < d.T; ++t) uniform_nu = uniform_nu && knots[t].nu == d.nu_max;

@@ -863,6 +863,7 @@ constexpr int kMaxCosts = 64;
 struct WVals {
   double* base;
   int nj;
+  double* parts;  // per-wave partial sums of the recursions: 4 x 6 per dof (kPartDoubles)
   MB_HD double* R(int i) const { return mb_lds(base + kWPerJoint * i); }  // liMi rotation
   MB_HD double* p(int i) const { return R(i) + 9; }
   MB_HD double* oR(int i) const { return R(i) + 12; }  // oMi (also pointer-jumping buffer A)
@@ -883,10 +884,14 @@ struct WVals {
   MB_HD double* jA(int i) const { return R(i) + 86; }  // jump targets of buffers A / B
   MB_HD double* jB(int i) const { return R(i) + 87; }
   MB_HD double* fb(int i) const { return R(i) + 90; }  // body force I a + v x* I v
+  // per-wave partial sums of the ancestor / subtree recursions (wave w's share of the dofs)
+  MB_HD double* part(int w, int i) const { return mb_lds(parts + 6 * ((int64_t)w * nj + i)); }
   MB_HD Mask* anc(int i) const { return (Mask*)(base + kWPerJoint * nj) + i; }  // ancestors-or-self dofs
   MB_HD double* root_a() const { return mb_lds(base + kWPerJoint * nj + nj); }
   MB_HD static int64_t doubles(int nj) { return (int64_t)kWPerJoint * nj + nj + 6; }
 };
+
+MB_HD __forceinline__ int64_t part_doubles(int nj) { return (int64_t)4 * 6 * nj; }
 
 MB_HD inline int jump_rounds(int nj) {
   int r = 0;
@@ -1131,22 +1136,127 @@ MB_HD inline void w_joint_force(const Blk& b, const WVals& W, double* tau, int i
   tau[i] = dot6(W.S(i), F);
 }
 
-// lane j < nj: CRBA column j in world frame: F = Ic_j S_j, M_ij = S_i . F for
-// the ancestors-or-self i < j of j (+ armature on the diagonal). A: ld lda, zeroed.
-MB_HD inline void w_crba_column(const Blk& b, const WVals& W, int j, double* A, int lda) {
+// lane j < nj of wave w (of nw): CRBA column j in world frame, F = Ic_j S_j, M_ij = S_i . F
+// for the ancestors-or-self i < j of j (+ armature on the diagonal), the rows i < j split
+// in nw contiguous ranges, one per wave (the waves run side by side: the per-lane chain
+// of LDS loads is a quarter as long). A: ld lda, zeroed.
+MB_HD inline void w_crba_column(const Blk& b, const WVals& W, int j, double* A, int lda, int w = 0, int nw = 1) {
   double F[6];
   comp_mul(W, j, W.S(j), F);
-  A[(int64_t)j * lda + j] = dot6(W.S(j), F) + b.arm[j];
+  if (w == 0) A[(int64_t)j * lda + j] = dot6(W.S(j), F) + b.arm[j];
   const Mask am = *W.anc(j);
+  const int ch = (j + nw - 1) / nw, i0 = w * ch, i1 = i0 + ch < j ? i0 + ch : j;
   // every i < j visited, the non-ancestors storing their zero (only lane j writes the
   // pair {i, j}), so the loop has no branch and the unrolled loads overlap
 #pragma unroll 2
-  for (int i = 0; i < j; ++i) {
+  for (int i = i0; i < i1; ++i) {
     const double d = dot6(W.S(i), F);
     const double Mij = ((am >> i) & 1ull) ? d : 0.;
     A[(int64_t)j * lda + i] = Mij;
     A[(int64_t)i * lda + j] = Mij;
   }
+}
+
+// ---- the RNEA recursions split over the waves ---------------------------------
+// Each ancestor (or subtree) sum of lane i runs over the dofs k in wave w's contiguous
+// range [w c, (w + 1) c), c = ceil(nj / nw), into part(w, i); the next phase combines
+// the nw partials in wave order. (The sums' association changes, not their terms.)
+MB_HD __forceinline__ void k_range(int nj, int w, int nw, int& k0, int& k1) {
+  const int c = (nj + nw - 1) / nw;
+  k0 = w * c;
+  k1 = k0 + c < nj ? k0 + c : nj;
+}
+MB_HD __forceinline__ void combine6(const WVals& W, int i, int nw, double* o) {
+  for (int e = 0; e < 6; ++e) o[e] = W.part(0, i)[e];
+  for (int w = 1; w < nw; ++w)
+    for (int e = 0; e < 6; ++e) o[e] += W.part(w, i)[e];
+}
+// lane i, wave w: sum over ancestors-or-self k in w's range of S_k qd_k
+MB_HD inline void w_velocity_part(const WVals& W, const double* qd, int i, int w, int nw) {
+  double v[6] = {0., 0., 0., 0., 0., 0.};
+  const Mask am = *W.anc(i);
+  int k0, k1;
+  k_range(W.nj, w, nw, k0, k1);
+#pragma unroll 2
+  for (int k = k0; k < k1; ++k) {
+    const bool in = (am >> k) & 1ull;
+    const double qk = qd[k];
+    for (int e = 0; e < 6; ++e) {
+      const double t = W.S(k)[e] * qk;
+      v[e] += in ? t : 0.;
+    }
+  }
+  for (int e = 0; e < 6; ++e) W.part(w, i)[e] = v[e];
+}
+// lane i, wave w: sum over ancestors-or-self k in w's range of cq_k
+MB_HD inline void w_accel_part(const WVals& W, int i, int w, int nw) {
+  double a[6] = {0., 0., 0., 0., 0., 0.};
+  const Mask am = *W.anc(i);
+  int k0, k1;
+  k_range(W.nj, w, nw, k0, k1);
+#pragma unroll 2
+  for (int k = k0; k < k1; ++k) {
+    const bool in = (am >> k) & 1ull;
+    for (int e = 0; e < 6; ++e) {
+      const double t = W.cq(k)[e];
+      a[e] += in ? t : 0.;
+    }
+  }
+  for (int e = 0; e < 6; ++e) W.part(w, i)[e] = a[e];
+}
+// lane i, wave w: sum over the subtree bodies k in w's range of the body forces
+MB_HD inline void w_force_part(const WVals& W, int i, int w, int nw) {
+  double F[6] = {0., 0., 0., 0., 0., 0.};
+  int k0, k1;
+  k_range(W.nj, w, nw, k0, k1);
+#pragma unroll 2
+  for (int k = k0; k < k1; ++k) {
+    const bool in = (*W.anc(k) >> i) & 1ull;
+    for (int e = 0; e < 6; ++e) {
+      const double t = W.fb(k)[e];
+      F[e] += in ? t : 0.;
+    }
+  }
+  for (int e = 0; e < 6; ++e) W.part(w, i)[e] = F[e];
+}
+// lane i: v_i from the partials, then cq_i = S_i qdd_i + v_i x (S_i qd_i)
+MB_HD inline void w_velocity_accel_term(const WVals& W, const double* qd, const double* qdd, int i, int nw) {
+  double v[6];
+  combine6(W, i, nw, v);
+  for (int e = 0; e < 6; ++e) W.v(i)[e] = v[e];
+  double S[6], Sw[6], t6[6];
+  const double wq = qd[i], qa = qdd ? qdd[i] : 0.;
+  for (int e = 0; e < 6; ++e) {
+    S[e] = W.S(i)[e];
+    Sw[e] = S[e] * wq;
+  }
+  cross_m(v, Sw, t6);
+  for (int e = 0; e < 6; ++e) W.cq(i)[e] = S[e] * qa + t6[e];
+}
+// lane i: a_i = -g + the partials, then the body force f_i = I_i a_i + v_i x* (I_i v_i) - fext_i
+MB_HD inline void w_accel_body_force(const WVals& W, int i, int nw, const double* fx) {
+  double a[6], p[6];
+  combine6(W, i, nw, p);
+  for (int e = 0; e < 6; ++e) a[e] = W.root_a()[e] + p[e];
+  double v[6], f[6], Iv[6], t6[6], c[3], I6[6];
+  for (int e = 0; e < 6; ++e) {
+    W.a(i)[e] = a[e];
+    v[e] = W.v(i)[e];
+    I6[e] = W.Ic(i)[e];
+  }
+  for (int e = 0; e < 3; ++e) c[e] = W.c(i)[e];
+  const double m = *W.m(i);
+  inertia_mul(m, c, I6, a, f);
+  inertia_mul(m, c, I6, v, Iv);
+  cross_f(v, Iv, t6);
+  for (int e = 0; e < 6; ++e) W.fb(i)[e] = f[e] + t6[e] - (fx ? fx[6 * i + e] : 0.);
+}
+// lane i: F_i from the partials, tau_i = S_i . F_i
+MB_HD inline void w_joint_force_comb(const WVals& W, double* tau, int i, int nw) {
+  double F[6];
+  combine6(W, i, nw, F);
+  for (int e = 0; e < 6; ++e) W.F(i)[e] = F[e];
+  tau[i] = dot6(W.S(i), F);
 }
 
 // Cost records
@@ -1596,7 +1706,8 @@ MB_HD inline void world_kinematics(const X& ex, const Blk& b, const WVals& W, co
     if (wave >= 1) costs(wave, l);
   });
   ex.run([&](int lane) {
-    if (lane < nj) w_crba_column(b, W, lane, A, lda);
+    const int w = lane >> 6, j = lane & 63;
+    if (j < nj) w_crba_column(b, W, j, A, lda, w, ex.nt >> 6);
   });
 }
 
@@ -1606,18 +1717,28 @@ MB_HD inline void world_kinematics(const X& ex, const Blk& b, const WVals& W, co
 template <class X>
 MB_HD inline void world_rnea(const X& ex, const Blk& b, const WVals& W, const double* qd, const double* qdd,
                              double* tau, const double* fx = nullptr) {
-  const int nj = b.nj;
+  const int nj = b.nj, nw = ex.nt >> 6;
+  // every ancestor / subtree sum split over the waves (w_*_part), combined by lane i
   ex.run([&](int lane) {
-    if (lane < nj) w_velocity(W, qd, lane);
+    const int w = lane >> 6, i = lane & 63;
+    if (i < nj) w_velocity_part(W, qd, i, w, nw);
   });
   ex.run([&](int lane) {
-    if (lane < nj) w_accel_term(W, qd, qdd, lane);
+    if (lane < nj) w_velocity_accel_term(W, qd, qdd, lane, nw);
   });
   ex.run([&](int lane) {
-    if (lane < nj) w_accel_force(W, lane, fx);
+    const int w = lane >> 6, i = lane & 63;
+    if (i < nj) w_accel_part(W, i, w, nw);
   });
   ex.run([&](int lane) {
-    if (lane < nj) w_joint_force(b, W, tau, lane);
+    if (lane < nj) w_accel_body_force(W, lane, nw, fx);
+  });
+  ex.run([&](int lane) {
+    const int w = lane >> 6, i = lane & 63;
+    if (i < nj) w_force_part(W, i, w, nw);
+  });
+  ex.run([&](int lane) {
+    if (lane < nj) w_joint_force_comb(W, tau, lane, nw);
   });
 }
 
@@ -1643,7 +1764,7 @@ MB_HD inline void euler_step(const Blk& b, const double* x, const double* a, dou
 // LDS (doubles) of the calc scratch for nj dofs and nc contact rows.
 MB_HD inline int64_t calc_work_doubles(int nj, int nc = 0) {
   return pad2(WVals::doubles(nj)) + (int64_t)lda_of(nj) * (nj + nc + 1) + 2 * nj + kMaxCosts + 8 + (int64_t)nc * nj + nc +
-         (int64_t)nc * (nc + 1) + 128;
+         (int64_t)nc * (nc + 1) + 128 + part_doubles(nj);
 }
 
 // model->calc(data, x, u) for the Euler∘FreeFwdDynamics knot (euler.hxx:41-80,
@@ -1666,7 +1787,6 @@ MB_HD inline double knot_calc_x(const X& ex, const double* P, int nx, const doub
   const bool imp = b.impulse;  // impulse: [M | Jc^T] only, z = v
   const int nj = b.nj, nq = b.nq, nc = b.nc, nu = nj - b.nun, ncol = imp ? nj + nc : nj + nc + 1;
   const int lda = lda_of(nj);
-  const WVals W{w, nj};
   double* A = w + pad2(WVals::doubles(nj));  // nj x (nj + nc + 1), ld lda: [M | Jc^T | tau - nle]
   double* tau = A + (int64_t)lda * ncol;
   double* ub = tau + nj;  // u (zero if !use_u)
@@ -1677,6 +1797,7 @@ MB_HD inline double knot_calc_x(const X& ex, const double* P, int nx, const doub
   double* a0 = Jc + (int64_t)nc * nj;    // nc
   double* S = a0 + nc;                   // nc x (nc + 1), ld nc: [S | Jc z + a0]
   double* pb = S + (int64_t)nc * (nc + 1);  // Gauss-Jordan pivot-column buffer (128)
+  const WVals W{w, nj, pb + 128};            // the recursions' per-wave partials after it
   ex.run([&](int lane) {
     if (lane < nu) ub[lane] = use_u ? u[lane] : 0.;
     for (int e = lane; e < lda * ncol; e += ex.nt) A[e] = 0.;
@@ -2386,7 +2507,8 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
   const int jw = vcols ? L : nj;  // columns of the stored jac-cost Jacobians
   const int nrows = count_cost_rows(b, nu);
   const DiffLayout l = diff_layout(nj, njac, nc, vcols, nu, nrows);
-  const WVals W{w + l.wv, nj};
+  // the recursions' per-wave partials in the dtau area (free until the tangent directions)
+  const WVals W{w + l.wv, nj, w + l.dtau};
   double* A = w + l.A;
   double* dtau = w + l.dtau;
   double* da = w + l.da;
