@@ -1022,12 +1022,22 @@ MB_HD inline void w_joint_world(const Blk& b, const WVals& W, int i, bool from_b
 
 // lane i < nj: composite inertia of the subtree of i in origin form
 // (m, h = m c, I_O = Ic + m (|c|^2 I - c c^T)): additive over the subtree.
-MB_HD inline void w_composite(const Blk& b, const WVals& W, int i) {
+// wave w's contiguous share [w c, (w + 1) c), c = ceil(nj / nw), of nj dofs
+MB_HD __forceinline__ void k_range(int nj, int w, int nw, int& k0, int& k1) {
+  const int c = (nj + nw - 1) / nw;
+  k0 = w * c;
+  k1 = k0 + c < nj ? k0 + c : nj;
+}
+MB_HD inline void w_composite(const Blk& b, const WVals& W, int i, int w = 0, int nw = 1) {
   double m = 0., h[3] = {0., 0., 0.}, I[6] = {0., 0., 0., 0., 0., 0.};
   // every body read, the ones outside the subtree weighted 0 (adds of +0: the sums are
-  // unchanged), so the unrolled iterations' LDS loads overlap instead of branching
+  // unchanged), so the unrolled iterations' LDS loads overlap instead of branching;
+  // nw > 1: wave w's share of the bodies into its partial (W.parts, 10 per dof)
+  int k0 = b.ff ? 5 : 0, k1 = b.nj;
+  if (nw > 1) k_range(b.nj, w, nw, k0, k1);
+  if (b.ff && k0 < 5) k0 = 5;
 #pragma unroll 2
-  for (int k = b.ff ? 5 : 0; k < b.nj; ++k) {
+  for (int k = k0; k < k1; ++k) {
     const double sel = ((*W.anc(k) >> i) & 1ull) ? 1. : 0.;
     const double mk = *W.m(k);
     double c[3], Ic[6];
@@ -1043,9 +1053,31 @@ MB_HD inline void w_composite(const Blk& b, const WVals& W, int i) {
     I[4] += sel * (Ic[4] - mk * c[0] * c[2]);
     I[5] += sel * (Ic[5] - mk * c[1] * c[2]);
   }
+  if (nw > 1) {
+    double* o = mb_lds(W.parts + 10 * ((int64_t)w * b.nj + i));
+    o[0] = m;
+    for (int e = 0; e < 3; ++e) o[1 + e] = h[e];
+    for (int e = 0; e < 6; ++e) o[4 + e] = I[e];
+    return;
+  }
   *W.cm(i) = m;
   for (int e = 0; e < 3; ++e) W.ch(i)[e] = h[e];
   for (int e = 0; e < 6; ++e) W.cI(i)[e] = I[e];
+}
+// lane i: the composite of dof i from the nw wave partials (wave order); `store`: into W
+MB_HD inline void w_composite_combine(const WVals& W, int i, int nw, bool store) {
+  double v[10];
+  const double* p0 = mb_lds(W.parts + 10 * (int64_t)i);
+  for (int e = 0; e < 10; ++e) v[e] = p0[e];
+  for (int w = 1; w < nw; ++w) {
+    const double* p = mb_lds(W.parts + 10 * ((int64_t)w * W.nj + i));
+    for (int e = 0; e < 10; ++e) v[e] += p[e];
+  }
+  if (store) {
+    *W.cm(i) = v[0];
+    for (int e = 0; e < 3; ++e) W.ch(i)[e] = v[1 + e];
+    for (int e = 0; e < 6; ++e) W.cI(i)[e] = v[4 + e];
+  }
 }
 
 // composite inertia of dof i's subtree times a motion x: (m v - h x w, I_O w + h x v)
@@ -1161,11 +1193,6 @@ MB_HD inline void w_crba_column(const Blk& b, const WVals& W, int j, double* A, 
 // Each ancestor (or subtree) sum of lane i runs over the dofs k in wave w's contiguous
 // range [w c, (w + 1) c), c = ceil(nj / nw), into part(w, i); the next phase combines
 // the nw partials in wave order. (The sums' association changes, not their terms.)
-MB_HD __forceinline__ void k_range(int nj, int w, int nw, int& k0, int& k1) {
-  const int c = (nj + nw - 1) / nw;
-  k0 = w * c;
-  k1 = k0 + c < nj ? k0 + c : nj;
-}
 MB_HD __forceinline__ void combine6(const WVals& W, int i, int nw, double* o) {
   for (int e = 0; e < 6; ++e) o[e] = W.part(0, i)[e];
   for (int w = 1; w < nw; ++w)
@@ -1688,7 +1715,7 @@ MB_HD __attribute__((always_inline)) inline void contact_jac_lane(const Blk& b, 
 // the phase after the kinematics (nullptr-like no-op allowed).
 template <class X, class CostF>
 MB_HD inline void world_kinematics(const X& ex, const Blk& b, const WVals& W, const double* q, double* A, int lda,
-                                   CostF costs) {
+                                   CostF costs, bool split_composite = false) {
   const int nj = b.nj, R = jump_rounds(nj);
   ex.run([&](int lane) {
     if (lane < nj) w_joint_local(b, W, q, lane);
@@ -1700,11 +1727,21 @@ MB_HD inline void world_kinematics(const X& ex, const Blk& b, const WVals& W, co
   ex.run([&](int lane) {
     if (lane < nj) w_joint_world(b, W, lane, (R & 1) != 0);
   });
-  ex.run([&](int lane) {
-    const int wave = lane >> 6, l = lane & 63;
-    if (wave == 0 && l < nj) w_composite(b, W, l);
-    if (wave >= 1) costs(wave, l);
-  });
+  if (split_composite) {  // (no cost work alongside) the composites over all waves
+    ex.run([&](int lane) {
+      const int w = lane >> 6, l = lane & 63;
+      if (l < nj) w_composite(b, W, l, w, ex.nt >> 6);
+    });
+    ex.run([&](int lane) {
+      if (lane < nj) w_composite_combine(W, lane, ex.nt >> 6, true);
+    });
+  } else {
+    ex.run([&](int lane) {
+      const int wave = lane >> 6, l = lane & 63;
+      if (wave == 0 && l < nj) w_composite(b, W, l);
+      if (wave >= 1) costs(wave, l);
+    });
+  }
   ex.run([&](int lane) {
     const int w = lane >> 6, j = lane & 63;
     if (j < nj) w_crba_column(b, W, j, A, lda, w, ex.nt >> 6);
@@ -2036,16 +2073,32 @@ MB_HD inline void body_nh_lane(const Blk& b, const WVals& W, int d, double* nb) 
   }
   inertia_mul(m, c, I6, V, o + 36);
 }
-// lane j < nj: Nsub_j, Hsub_j (sums over the bodies below dof j) into ns[42 j ..]
-MB_HD inline void subtree_nh_lane(const Blk& b, const WVals& W, int j, const double* nb, double* ns) {
-  double acc[42];
-  for (int e = 0; e < 42; ++e) acc[e] = 0.;
-  for (int bb = 0; bb < b.nj; ++bb) {
-    if (!((*W.anc(bb) >> j) & 1ull) || !carries_body(b, bb)) continue;
-    const double* o = nb + 42 * bb;
-    for (int e = 0; e < 42; ++e) acc[e] += o[e];
+// lane j < nj of wave w (of nw): components [11 w, 11 w + 11) of Nsub_j, Hsub_j (sums over
+// the bodies below dof j) into ns[42 j ..]; every body read, the others weighted 0 (no
+// branch: the unrolled loads overlap), the 42 components split over the waves
+MB_HD inline void subtree_nh_lane(const Blk& b, const WVals& W, int j, const double* nb, double* ns, int w = 0,
+                                  int nw = 1) {
+  constexpr int kC = 11;  // components per wave (4 x 11 >= 42)
+  const int e0 = nw == 1 ? 0 : w * kC, e1 = nw == 1 ? 42 : (e0 + kC < 42 ? e0 + kC : 42);
+  double acc[kC];
+  for (int e = 0; e < kC; ++e) acc[e] = 0.;
+  for (int c0 = e0; c0 < e1; c0 += kC) {
+#pragma unroll 2
+    for (int bb = 0; bb < b.nj; ++bb) {
+      const bool in = ((*W.anc(bb) >> j) & 1ull) && carries_body(b, bb);
+      const double* o = nb + 42 * bb + c0;
+#pragma unroll
+      for (int e = 0; e < kC; ++e) {
+        const double v = c0 + e < e1 ? o[e] : 0.;
+        acc[e] += in ? v : 0.;
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < kC; ++e) {
+      if (c0 + e < e1) ns[42 * j + c0 + e] = acc[e];
+      acc[e] = 0.;
+    }
   }
-  for (int e = 0; e < 42; ++e) ns[42 * j + e] = acc[e];
 }
 // B_j x = Nsub_j x + x x* Hsub_j
 MB_HD __forceinline__ void bsub_mul_ns(const double* ns, int j, const double* x, double* o) {
@@ -2542,7 +2595,7 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
     }
   });
   // world-frame kinematics, M into the left half of [M | I], nle
-  world_kinematics(ex, b, W, x, A, lda, [](int, int) {});
+  world_kinematics(ex, b, W, x, A, lda, [](int, int) {}, true);
   if (!imp) world_rnea(ex, b, W, x + nq, nullptr, nle);
   if (nc > 0)  // contact rows at the drift (ddq = 0; ContactModelMultiple::calc)
     ex.run([&](int lane) {
@@ -2674,7 +2727,8 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
       if (lane < nj) body_nh_lane(b, W, lane, dtau);
     });
     ex.run([&](int lane) {
-      if (lane < nj) subtree_nh_lane(b, W, lane, dtau, nsub);
+      const int w = lane >> 6, j = lane & 63;
+      if (j < nj) subtree_nh_lane(b, W, j, dtau, nsub, w, ex.nt >> 6);
     });
   }
   // the velocity-product maps on the lower half of the workgroup, the cost / Euler
