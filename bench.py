@@ -67,7 +67,32 @@ def backward_bytes_per_knot(n, m):
     return 8 * ((2 * n * n + 2 * n * m + m * m + 2 * n + m) + (m * n + 2 * m + 2 * n + m))
 
 
-BOX_LIMIT = 1.0  # --solver boxfddp: |u_i| <= 1 on every running knot (~30% of the C5 controls saturate)
+BOX_LIMIT = 1.0  # --solver boxfddp on configs without an effort table: |u_i| <= 1
+
+
+BOX_PRESOLVE = 20  # --solver boxfddp: solve(maxiter=20, regInit=0.1) once from the warm start (untimed), then
+# every step restarts from that feasible iterate with solve(xs_f, us_f, 1, isFeasible=true, 0.1):
+# the box QP (box-fddp.cpp:48-79, only taken when feasible) runs on every knot of every step
+
+
+def box_limits(config, nu):
+    """--solver boxfddp control bounds (lb, ub) of a running knot with nu controls: on
+    Talos (C5) the robot's effortLimit on the actuated joints (ActuationModelFloatingBase:
+    u = tau[6:]), as examples/bipedal_walk_ubound.py:16-18 bounds the controls. (That
+    example halves the limits of Talos' legs alone; on the full body the halved ankle-roll
+    limit is below the single-support torque and no step is ever accepted.) Elsewhere
+    |u_i| <= BOX_LIMIT."""
+    if config.startswith("C5"):
+        from crocoddyl_amd import robots
+        lim = robots.sample_talos().effortLimit[6:]
+        if lim.size == nu:
+            return -lim, lim.copy()
+    return np.full(nu, -BOX_LIMIT), np.full(nu, BOX_LIMIT)
+
+
+def box_text(config):
+    return ("u within the Talos effortLimit (bipedal_walk_ubound.py)" if config.startswith("C5")
+            else f"|u| <= {BOX_LIMIT}")
 
 
 def synthetic_kind(cfg):
@@ -141,16 +166,21 @@ def _cpu_baseline_child(cfg, T, seed, target_s, box, protocol):
         o = oracle_lib.Oracle(S["dims"], S["knots"], S["pool"], S["x0s"], threads=threads, mode=mode)
         if box:
             o.set_solver_kind(_abi.SOLVER_BOXFDDP)
-            o.set_control_limits(np.full((d.B, d.T, d.nu_max), -BOX_LIMIT), np.full((d.B, d.T, d.nu_max), BOX_LIMIT))
+            lo, hi = box_limits(cfg, d.nu_max)
+            o.set_control_limits(np.ascontiguousarray(np.broadcast_to(lo, (d.B, d.T, d.nu_max))),
+                                 np.ascontiguousarray(np.broadcast_to(hi, (d.B, d.T, d.nu_max))))
             p = oracle_lib.default_params()
             p.th_stop = 5e-5
             o.set_params(p)
         xs_w, us_w = warm_start_arrays(cfg, S["running"], S["x0s"], d)
         o.set_candidate(xs_w, us_w, False)
         knots = list(S["knots"])
-        iters = 2 if box else 1
+        iters = 1
         if protocol == "shift":
             o.solve(maxiter=5)
+        if protocol == "feasible":
+            o.solve(maxiter=BOX_PRESOLVE, reg_init=0.1)
+            xs_w, us_w = o.xs(), o.us()
         t0 = time.perf_counter()
         it = 0
         for _ in range(steps):
@@ -160,8 +190,8 @@ def _cpu_baseline_child(cfg, T, seed, target_s, box, protocol):
                 o.L.oracle_set_knots(o.h, kd, _abi.dptr(o.pool), o.pool.size)
                 o.mpc_shift()
             else:
-                o.set_candidate(xs_w, us_w, False)
-            r = o.solve(maxiter=iters, reg_init=0.1)
+                o.set_candidate(xs_w, us_w, protocol == "feasible")
+            r = o.solve(maxiter=iters, is_feasible=protocol == "feasible", reg_init=0.1)
             it += sum(x.n_iter_run for x in r)
         return it, time.perf_counter() - t0
 
@@ -189,12 +219,12 @@ def _cpu_baseline_child(cfg, T, seed, target_s, box, protocol):
                       "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS"), "cpu_model": cpu_model,
                       "build": f"{flags} -fopenmp",
                       "modes": {"batch_parallel": round(v2, 2), "knot_parallel": round(v1, 2)},
-                      "sample": f"{cfg} T={T}, protocol {protocol}, solve(maxiter={2 if box else 1}, reg_init=0.1) "
+                      "sample": f"{cfg} T={T}, protocol {protocol}, solve(maxiter=1, reg_init=0.1) "
                                 f"per element per step: batch-parallel {Bs} elements x {steps} steps ({it} "
                                 f"element-iterations in {dt:.1f} s), knot-parallel {B1} elements x {steps} steps "
                                 f"({it1} in {dt1:.1f} s); value = the faster mode. oracle/fddp_oracle.cpp {flags} "
                                 f"-fopenmp, {threads} threads ({share}) of {os.cpu_count()} host CPUs ({cpu_model})"
-                                f"{', SolverBoxFDDP |u| <= 1' if box else ''}"}), flush=True)
+                                f"{', SolverBoxFDDP ' + box_text(cfg) if box else ''}"}), flush=True)
 
 
 def load_pmc(cfg):
@@ -237,8 +267,7 @@ def make_shard_solver(config, B, rank, dev, box=False, T=None, presolve=True):
     x0s, running, terminal = synthetic.build(config, T=T, B=B, seed=seed)
     if box:
         for md in set(running):
-            md.u_lb = np.full(md.nu, -BOX_LIMIT)
-            md.u_ub = np.full(md.nu, BOX_LIMIT)
+            md.u_lb, md.u_ub = box_limits(config, md.nu)
     problem = ShootingProblem(x0s, running, terminal, device=dev)
     solver = SolverBoxFDDP(problem) if box else SolverFDDP(problem)
     solver.warm = warm_start_arrays(config, running, x0s, problem._dims())
@@ -281,6 +310,28 @@ class FixedWarmStart:
         self.solver.solve_from_candidate(maxiter=mpc_iters, isFeasible=False, regInit=0.1)
 
 
+class FeasibleRestart:
+    """--solver boxfddp's step: solve(xs_f, us_f, 1, isFeasible=true, 0.1) from the iterate
+    of an untimed solve(maxiter=BOX_PRESOLVE) from the warm start (the box QP only runs on
+    feasible iterates, box-fddp.cpp:48-51). `start`: (xs, us) device tensors to restart
+    from (default: this solver's presolved iterate)."""
+
+    def __init__(self, solver, dev, start=None):
+        import torch
+        self.solver = solver
+        if start is None:
+            solver.solve_from_candidate(maxiter=BOX_PRESOLVE, regInit=0.1)
+            self.feasible = float(np.mean(np.asarray(solver.isFeasible, float)))
+            start = (torch.from_numpy(np.ascontiguousarray(solver.xs)).to(f"cuda:{dev}"),
+                     torch.from_numpy(np.ascontiguousarray(solver.us)).to(f"cuda:{dev}"))
+        self.xs, self.us = start
+        torch.cuda.synchronize(dev)
+
+    def __call__(self, mpc_iters):
+        self.solver.setCandidate_device(self.xs.data_ptr(), self.us.data_ptr(), True)
+        self.solver.solve_from_candidate(maxiter=mpc_iters, isFeasible=True, regInit=0.1)
+
+
 def line_search_trials(solver):
     """Trials per element of the last line search: alpha = 2^-k accepted after k + 1."""
     sl = np.atleast_1d(np.asarray(solver.stepLength, float))
@@ -305,9 +356,9 @@ def main():
     ap.add_argument("--batch", type=int, default=None, help="elements per GPU (default: the config's)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--solver", choices=["fddp", "boxfddp"], default="fddp",
-                    help="boxfddp: SolverBoxFDDP with |u| <= 1 limits, solve(maxiter=2) per MPC step so the "
+                    help="boxfddp: SolverBoxFDDP with control limits (C5: half the Talos effort limits), solve(maxiter=2) per MPC step so the "
                          "box QP runs (iteration 1 is feasible)")
-    ap.add_argument("--protocol", choices=["fixed", "shift"], default="fixed",
+    ap.add_argument("--protocol", choices=["fixed", "shift", "feasible"], default=None,
                     help="fixed: the reference benchmark's loop, solve(xs, us, 1, false, 0.1) from the same warm "
                          "start every step (bipedal_walk_optctrl.py:36-43); shift: receding horizon, gait knots "
                          "rotated (circularAppend) + device shift of x0/xs/us, then the warm-started solve")
@@ -315,6 +366,8 @@ def main():
                     help="steps of the other protocol, reported beside the headline (1 GPU only; 0: off)")
     args = ap.parse_args()
     box = args.solver == "boxfddp"
+    if args.protocol is None:
+        args.protocol = "feasible" if box else "fixed"
 
     import torch
 
@@ -327,13 +380,17 @@ def main():
 
     kind, d1, nu, T, B0, dt = synthetic.CONFIGS[args.config]
     B = args.batch or B0
-    mpc_iters = 2 if box else 1
+    mpc_iters = 1
 
     def make_stepper(protocol):
         s = make_shard_solver(args.config, B, rank, dev, box, presolve=(protocol == "shift"))
         if protocol == "fixed":
             fw = FixedWarmStart(s, dev)
             return s, (lambda: fw(mpc_iters))
+        if protocol == "feasible":
+            fr = FeasibleRestart(s, dev)
+            s.restart = fr
+            return s, (lambda: fr(mpc_iters))
         rotate = kind in ("gait_biped", "gait_quadruped")
         return s, (lambda: mpc_step(s, mpc_iters, rotate=rotate))
 
@@ -367,8 +424,32 @@ def main():
     elapsed, total_iters = cdist.job_time_and_work(elapsed, iters, f"cuda:{dev}")
     assert xs_all.shape[0] == us_all.shape[0] == res_all.shape[0] == ws * B
 
+    box_bwd = None
+    if box and ws == 1 and args.protocol == "feasible":
+        # the FDDP backward on the same step: SolverFDDP on the same problems, restarted
+        # from the same feasible iterate (FDDP gains: no box QP)
+        sf = make_shard_solver(args.config, B, rank, dev, False, presolve=False)
+        fr = FeasibleRestart(sf, dev, start=(solver.restart.xs, solver.restart.us))
+        fr(mpc_iters)
+        sf.synchronize()
+        sf.get_timing()
+        sf.set_timing(True)
+        for _ in range(args.steps):
+            fr(mpc_iters)
+        sf.synchronize()
+        sf.set_timing(False)
+        f_ms = sf.get_timing()["backward"][0] / args.steps
+        b_ms = timing["backward"][0] / args.steps
+        box_bwd = {"backward_ms_boxfddp": round(b_ms, 3), "backward_ms_fddp": round(f_ms, 3),
+                   "ratio": round(b_ms / f_ms, 3),
+                   "feasible_fraction_after_presolve": solver.restart.feasible,
+                   "method": "per-step backward (HIP events) of SolverBoxFDDP and of SolverFDDP on the same "
+                             "problems, both restarted from the same feasible iterate with "
+                             "solve(xs_f, us_f, 1, isFeasible=true, 0.1)"}
+        del sf, fr
+
     secondary = None
-    if ws == 1 and args.secondary_steps > 0:
+    if ws == 1 and args.secondary_steps > 0 and args.protocol != "feasible":
         other = "shift" if args.protocol == "fixed" else "fixed"
         del xs_all, us_all, res_all
         s2, step2 = make_stepper(other)
@@ -467,8 +548,12 @@ def main():
                                       f"reference benchmark (bipedal_walk_optctrl.py:36-43)"
                                       if args.protocol == "fixed" else
                                       f"protocol shift: gait knots rotated (circularAppend), device shift of x0/xs/us, "
-                                      f"then solve(maxiter={mpc_iters}, isFeasible=false, reg_init=0.1)")
-                                   + (", SolverBoxFDDP with |u| <= 1" if box else ""),
+                                      f"then solve(maxiter={mpc_iters}, isFeasible=false, reg_init=0.1)"
+                                      if args.protocol == "shift" else
+                                      f"protocol feasible: solve(xs_f, us_f, {mpc_iters}, isFeasible=true, reg_init=0.1) "
+                                      f"from the HBM-resident iterate of an untimed solve(maxiter={BOX_PRESOLVE}, reg_init=0.1) "
+                                      f"from the warm start")
+                                   + (", SolverBoxFDDP, " + box_text(args.config) if box else ""),
                        "protocol": args.protocol,
                        "global_batch": B * ws, "T": T, "parallelism": f"batch-sharded x{ws}",
                        "solver": "SolverBoxFDDP" if box else "SolverFDDP"},
@@ -476,6 +561,7 @@ def main():
             "kernel_ms_per_step": {k: round(v[0] / max(args.steps, 1), 3) for k, v in timing.items()},
             "line_search_trials_last_step": trials_summary(trials),
             "secondary_protocol": secondary,
+            **({"box_backward": box_bwd} if box_bwd else {}),
             "roofline": roof,
             "rooflines": {k: v[1] for k, v in rooflines.items()},
             "cpu_baseline": cpu,

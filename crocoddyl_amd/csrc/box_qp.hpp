@@ -11,11 +11,13 @@
 // trial). Every branch is taken on a ballot or on lane 0's sum, so the wave
 // stays uniform.
 //
-// Same results as the reference, with two exact shortcuts:
+// Same results as the reference, with three exact shortcuts:
 //  - an iteration whose line search accepts no alpha leaves x unchanged, so
 //    every later iteration repeats it bit for bit until maxiter: the loop
 //    stops there with the state the reference returns after maxiter;
-//  - Hff_inv is kept embedded in an nx x nx matrix (zero off the free set).
+//  - Hff_inv is kept embedded in an nx x nx matrix (zero off the free set), and
+//    an iteration on the free set of the previous one reuses it (and the
+//    accepted trial's H x) instead of recomputing the same values.
 // When the QP converges at k > 0 the reference returns the previous
 // iteration's Hff_inv with the new free_idx, and SolverBoxFDDP scatters it
 // by position (box-fddp.cpp:64-69); `remap` reproduces that scatter by
@@ -180,8 +182,14 @@ __device__ __forceinline__ bool box_qp_wave(const double* H, int ldh, double* Qi
   free_sol = 0;
   iters = 0;
   uint64_t fr = 0;
+  // Qi holds the plain inverse of free_inv from the last Newton step (an iteration on the
+  // same free set reuses it: the reference refactorises the same matrix to the same bits);
+  // H x of an accepted trial is the next iteration's H x
+  bool qi_plain = false, have_hx = false;
+  double Hx = 0.;
   for (int k = 0; k < c.maxiter; ++k) {
-    const double Hx = matvec(H, ldh, x);
+    if (!have_hx) Hx = matvec(H, ldh, x);
+    have_hx = false;
     const double g = q + Hx;
     const bool clamped = valid && ((x == lb && g > 0.) || (x == ub && g < 0.));
     fr = __ballot(valid && !clamped);
@@ -201,8 +209,9 @@ __device__ __forceinline__ bool box_qp_wave(const double* H, int ldh, double* Qi
     }
     ++iters;
     // Newton step on the free subspace (:138-175)
-    if (inv(InvMap::plain(fr, m, c.reg))) return false;
+    if (!(qi_plain && fr == free_inv) && inv(InvMap::plain(fr, m, c.reg))) return false;
     free_inv = fr;
+    qi_plain = true;
     const bool isfree = valid && ((fr >> lane) & 1);
     const double Hxc = matvec(H, ldh, clamped ? x : 0.);
     const double rf = isfree ? (-q - Hxc) : 0.;
@@ -219,6 +228,8 @@ __device__ __forceinline__ bool box_qp_wave(const double* H, int ldh, double* Qi
       const double gd = wave_sum(valid ? g * (x - xn) : 0.);
       if (uniform(fold - fnew > c.th_acceptstep * gd)) {
         x = xn;
+        Hx = Hxn;
+        have_hx = true;
         accepted = true;
         break;
       }

@@ -274,27 +274,6 @@ __device__ __forceinline__ bool sym_sweep_inverse(const double* Quu, double* Qi,
   return bad;
 }
 
-// The masked / relabelled inverse an InvMap describes (the box QP's free
-// Hessian, box_qp.hpp) with the register sweep: the masked matrix is staged
-// into Qi, swept in place (the sweep reads all of it before writing), and
-// the result is cut to the `out` set.
-template <int MP, int LDQ>
-__device__ __forceinline__ bool sym_sweep_inverse_masked(const double* H, double* Qi, double* rb, int m, int lane,
-                                                         const InvMap& mp) {
-  for (int e = lane; e < m * m; e += 64) {
-    const int i = e % m, j = e / m;
-    Qi[j * LDQ + i] = mp.load(H, LDQ, i, j);
-  }
-  const bool bad = sym_sweep_inverse<MP, LDQ>(Qi, Qi, rb, m, lane);
-  asm volatile("" ::: "memory");
-  for (int e = lane; e < m * m; e += 64) {
-    const int i = e % m, j = e / m;
-    if (!(mp.out(i) && mp.out(j))) Qi[j * LDQ + i] = 0.;
-  }
-  asm volatile("" ::: "memory");
-  return bad;
-}
-
 // Same sweep with each lane owning a BS x BS block of the matrix (BS = MP/8,
 // an 8 x 8 grid of blocks over the 64 lanes): per step one FMA per element
 // as before, but the column-k / row-k fix-ups touch BS elements of 8 lanes
@@ -366,6 +345,27 @@ __device__ __forceinline__ bool sym_sweep_inverse_blk(const double* Quu, double*
       const int i = BS * bi + a, j = BS * bj + b;
       Qi[j * LDQ + i] = (i < m && j < m) ? -A[a][b] : 0.;
     }
+  return bad;
+}
+
+// The masked / relabelled inverse an InvMap describes (the box QP's free
+// Hessian, box_qp.hpp) with the register sweep: the masked matrix is staged
+// into Qi, swept in place (the sweep reads all of it before writing), and
+// the result is cut to the `out` set.
+template <int MP, int LDQ>
+__device__ __forceinline__ bool sym_sweep_inverse_masked(const double* H, double* Qi, double* rb, int m, int lane,
+                                                         const InvMap& mp) {
+  for (int e = lane; e < m * m; e += 64) {
+    const int i = e % m, j = e / m;
+    Qi[j * LDQ + i] = mp.load(H, LDQ, i, j);
+  }
+  const bool bad = sym_sweep_inverse<MP, LDQ>(Qi, Qi, rb, m, lane);
+  asm volatile("" ::: "memory");
+  for (int e = lane; e < m * m; e += 64) {
+    const int i = e % m, j = e / m;
+    if (!(mp.out(i) && mp.out(j))) Qi[j * LDQ + i] = 0.;
+  }
+  asm volatile("" ::: "memory");
   return bad;
 }
 
@@ -544,9 +544,19 @@ __device__ __forceinline__ bool box_gains_wave(const Dev& D, const BwdLds& L, in
   }
   uint64_t fsol, finv;
   int iters;
-  auto inv = [&](const InvMap& mp) { return sym_sweep_inverse_masked<MP, LDQ>(L.Quu, L.Qi, L.rowbuf, nu, lane, mp); };
-  if (!box_qp_wave(L.Quu, LDQ, L.Qi, LDQ, L.rowbuf, nu, lane, q, lb, ub, x, D.boxcfg, inv, true, fsol, finv, iters))
-    return false;
+  int ninv = 0;
+  auto inv = [&](const InvMap& mp) {
+    ++ninv;
+    return sym_sweep_inverse_masked<MP, LDQ>(L.Quu, L.Qi, L.rowbuf, nu, lane, mp);
+  };
+  const bool qp_ok = box_qp_wave(L.Quu, LDQ, L.Qi, LDQ, L.rowbuf, nu, lane, q, lb, ub, x, D.boxcfg, inv, true, fsol,
+                                 finv, iters);
+  if (D.box_stats && lane == 0) {
+    atomicAdd(D.box_stats, 1ull);
+    atomicAdd(D.box_stats + 1, (unsigned long long)iters);
+    atomicAdd(D.box_stats + 2, (unsigned long long)ninv);
+  }
+  if (!qp_ok) return false;
   asm volatile("" ::: "memory");
   if (lane < MP) L.kv[lane] = valid ? -x : 0.;
   if (valid) {

@@ -91,6 +91,7 @@ struct Dev {
   const double *ulb, *uub;         // [B][T][sM] control limits (null = none set)
   const unsigned char* haslim;     // [B][T] has_control_limits (null = none)
   double* dQuuInv;                 // debug [B][T][sMM] Quu_inv_ (null unless debug + box)
+  unsigned long long* box_stats;   // diagnostics (FDDP_BOX_STATS=1): box QPs, Newton iterations, inverses
   BoxQPCfg boxcfg;                 // qp_(nu, 100, 0.1, 1e-5, 0.) (box-fddp.cpp:16)
   int64_t mbw;                     // LDS doubles of the multibody calc scratch (0: no multibody knots)
   int64_t mbd;                     // LDS doubles of the multibody calcDiff work area (its parameter block follows)

@@ -1171,6 +1171,12 @@ int fddp_solve(fddp_handle* h, int maxiter, int is_feasible, double reg_init, fd
   if (!h) return fail(FDDP_ERR_INVALID_ARG, "fddp_solve: null handle");
   if (maxiter < 0) return fail(FDDP_ERR_INVALID_ARG, "fddp_solve: maxiter < 0");
   DeviceGuard g(h->device);
+  static const bool box_stats = getenv("FDDP_BOX_STATS") && atoi(getenv("FDDP_BOX_STATS")) == 1;
+  if (box_stats && h->D.box && !h->D.box_stats) {
+    int rc0;
+    if ((rc0 = dalloc(h, (double**)&h->D.box_stats, 4))) return rc0;
+  }
+  if (h->D.box_stats) HIP_TRY(hipMemsetAsync(h->D.box_stats, 0, 4 * sizeof(unsigned long long), h->stream));
   const Dev& D = h->D;
   const double xreg0 = std::isnan(reg_init) ? h->prm.regmin : reg_init;
   hipLaunchKernelGGL(init_state_kernel, dim3((D.B + 255) / 256), dim3(256), 0, h->stream, D, is_feasible ? 1 : 0,
@@ -1199,6 +1205,12 @@ int fddp_solve(fddp_handle* h, int maxiter, int is_feasible, double reg_init, fd
     choose_npar(h, st);
   } else {
     HIP_TRY(hipStreamSynchronize(h->stream));
+  }
+  if (D.box_stats) {  // diagnostics: mean Newton iterations / inverses per box QP of this solve
+    unsigned long long bs[4];
+    HIP_TRY(hipMemcpy(bs, D.box_stats, sizeof(bs), hipMemcpyDeviceToHost));
+    fprintf(stderr, "fddp box stats: %llu QPs, %.3f Newton iterations and %.3f inverses per QP\n", bs[0],
+            bs[0] ? (double)bs[1] / bs[0] : 0., bs[0] ? (double)bs[2] / bs[0] : 0.);
   }
   return FDDP_OK;
 }

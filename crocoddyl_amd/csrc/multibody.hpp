@@ -2002,21 +2002,24 @@ constexpr int kMaxCostRows = 64;
 // (4 columns of slack: the GEMM reads rows four columns at a time)
 MB_HD __forceinline__ int cost_rows_ld(int nj, int nu) { return (int)pad2(2 * nj + nu) + 4; }
 constexpr int kMaxCostCols = 3 * kMaxJ;  // diagonal terms per column of [x tangent | u]
+MB_HD __forceinline__ int64_t cost_table_doubles() { return 4 * kMaxCosts + 5 * kMaxCostRows; }
 MB_HD __forceinline__ int64_t cost_area_doubles(int nj, int nu, int nrows) {
-  return 4 * kMaxCosts + 5 * kMaxCostRows + kMaxCostCols + (int64_t)nrows * cost_rows_ld(nj, nu);
+  return cost_table_doubles() + kMaxCostCols + (int64_t)nrows * cost_rows_ld(nj, nu);
 }
 __host__ __device__ inline DiffLayout diff_layout(int nj, int njac, int nc = 0, bool vel_cols = false, int nu = 0,
                                                   int nrows = 0) {
   const int L = 2 * nj;
   DiffLayout l;
-  l.wv = 0;
-  l.A = l.wv + pad2(WVals::doubles(nj));
-  l.dtau = l.A + (int64_t)lda_of(nj) * 2 * nj;  // [M | I] -> [. | Minv], ld lda_of(nj)
   // dtau [k][L] (first the per-body N_b, h_b: 42 per dof); da = -Kinv (dtau; da0) [r][L]
   // (first the subtree sums Nsub, Hsub)
   // (da rows at the odd stride L + 1: the Fx assembly reads a column of it per wave)
-  const int64_t dsz = (int64_t)nj * (L + 1) > 42 * (int64_t)nj ? (int64_t)nj * (L + 1) : 42 * (int64_t)nj;
-  l.da = l.dtau + dsz;
+  const int64_t dsz = pad2((int64_t)nj * (L + 1) > 42 * (int64_t)nj ? (int64_t)nj * (L + 1) : 42 * (int64_t)nj);
+  // the world values, then dtau: both dead after the da phase, so the cost-derivative
+  // area can run over both
+  l.wv = 0;
+  l.dtau = l.wv + pad2(WVals::doubles(nj));
+  l.A = l.dtau + dsz;  // [M | I] -> [. | Minv], ld lda_of(nj)
+  l.da = l.A + pad2((int64_t)lda_of(nj) * 2 * nj);
   l.qp = l.da + dsz;
   l.vec = l.qp + (int64_t)12 * nj;      // Q_k, P_k
   l.J = l.vec + pad2(6 * nj + 1 + 6 * kMaxJacCosts + 72);
@@ -2034,8 +2037,10 @@ __host__ __device__ inline DiffLayout diff_layout(int nj, int njac, int nc = 0, 
   l.dfx = l.zv + nj;     // d lambda / dx (nc x L), d lambda / du (nc x nj): CostModelContactForce
   l.dfu = l.dfx + (int64_t)nc * L;
   l.total = nc > 0 ? l.dfu + (int64_t)nc * nj : l.total;
+  // the table (written on spare lanes during the da phase, beside the dtau reads) within
+  // the world values; the diagonal terms and R rows (written after it) also over dtau
   const int64_t ca = cost_area_doubles(nj, nu, nrows);
-  if (ca <= pad2(WVals::doubles(nj))) {
+  if (cost_table_doubles() <= pad2(WVals::doubles(nj)) && ca <= pad2(WVals::doubles(nj)) + dsz) {
     l.R = l.wv;
   } else {
     l.R = pad2(l.total);

@@ -140,6 +140,7 @@ class RobotModel:
         self.gravity = np.array([0.0, 0.0, -9.81])  # pinocchio Model::gravity981
         self.referenceConfigurations = {}
         self._limits = {}  # joint id -> (lower, upper, velocity) (pinocchio Model limits; +-inf by default)
+        self._effort = {}  # joint id -> effort limit (pinocchio Model::effortLimit; +inf by default)
         self._version = 0
         if root_joint is not None:  # pinocchio::buildModel(urdf, JointModelFreeFlyer(), model)
             self.addJoint(0, root_joint, SE3(), "root_joint")
@@ -214,6 +215,20 @@ class RobotModel:
         for j in range(1, self.njoints):
             if self.kinds[j] != JOINT_FREEFLYER and j in self._limits:
                 out[self.idx_v(j)] = self._limits[j][2]
+        return out
+
+    def setEffortLimit(self, joint_id, effort):
+        """Torque limit of a revolute joint (the URDF <limit effort> that pinocchio
+        stores in Model::effortLimit)."""
+        self._effort[int(joint_id)] = float(effort)
+
+    @property
+    def effortLimit(self):
+        """Model::effortLimit (nv; +inf where unset, as on the free-flyer's dofs)."""
+        out = np.full(self.nv, np.inf)
+        for j, e in self._effort.items():
+            if self.kinds[j] != JOINT_FREEFLYER:
+                out[self.idx_v(j)] = e
         return out
 
     def _qlim(self, k, default):

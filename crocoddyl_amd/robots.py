@@ -77,6 +77,18 @@ def sample_talos():
         ("_1_joint", _Y, (0.0, 0.0, 0.4), 0.66, (0.0, 0.0, 0.02), (0.001, 0.001, 0.001)),
         ("_2_joint", _Z, (0.0, 0.0, 0.0), 1.16, (0.02, 0.0, 0.09), (0.006, 0.006, 0.005)),
     ], "head")
+    # effort limits (N m) of the Talos actuator classes, as the talos URDF's <limit effort>
+    # gives them (approximate: the URDF is not in this image); hips / knee / ankles,
+    # torso, shoulder / elbow / wrist, gripper, neck
+    effort = {"leg_%s_1_joint": 100.0, "leg_%s_2_joint": 160.0, "leg_%s_3_joint": 160.0, "leg_%s_4_joint": 300.0,
+              "leg_%s_5_joint": 160.0, "leg_%s_6_joint": 100.0, "arm_%s_1_joint": 44.64, "arm_%s_2_joint": 22.32,
+              "arm_%s_3_joint": 22.32, "arm_%s_4_joint": 22.32, "arm_%s_5_joint": 3.0, "arm_%s_6_joint": 3.0,
+              "arm_%s_7_joint": 3.0, "gripper_%s_joint": 1.0}
+    for side in ("left", "right"):
+        for name, e in effort.items():
+            m.setEffortLimit(m.getJointId(name % side), e)
+    for name, e in (("torso_1_joint", 200.0), ("torso_2_joint", 200.0), ("head_1_joint", 6.0), ("head_2_joint", 6.0)):
+        m.setEffortLimit(m.getJointId(name), e)
     leg = [0.0, 0.0, -0.411354, 0.859395, -0.448041, -0.001708]
     q = np.concatenate([[0.0, 0.0, 1.0192720229567027, 0.0, 0.0, 0.0, 1.0], leg, leg, [0.0, 0.006761],
                         [0.25847, 0.173046, -0.0002, -0.525366, 0.0, 0.0, 0.1, -0.005],

@@ -147,6 +147,18 @@ int main(int argc, char** argv) {
   fclose(f);
   const int nwg = atoi(argv[2]);
   const int nj = (int)P[1], n = 2 * nj;
+  const Blk bk = parse(P.data());
+  bool vc;
+  const int njac = count_jac_costs(bk, &vc);
+  const DiffLayout l = diff_layout(nj, njac, bk.nc, vc, bk.nj - bk.nun, count_cost_rows(bk, bk.nj - bk.nun));
+  const size_t smd = 8 * (pad2(l.total) + pad2(psz) + 256);
+  const size_t smc = 8 * (pad2(calc_work_doubles(nj, bk.nc)) + pad2(psz) + 256);
+  printf("nj %d nx %d nu %d m %d psz %d lds diff %zu calc %zu\n", nj, nx, nu, m, psz, smd, smc);
+  printf("  layout: wv %ld A %ld dtau %ld da %ld qp %ld vec %ld J %ld red %ld Jc %ld R %ld total %ld (njac %d vcols %d nc %d nrows %d)\n",
+         (long)l.wv, (long)l.A, (long)l.dtau, (long)l.da, (long)l.qp, (long)l.vec, (long)l.J, (long)l.red, (long)l.Jc,
+         (long)l.R, (long)l.total, njac, (int)vc, bk.nc, count_cost_rows(bk, bk.nj - bk.nun));
+  fflush(stdout);
+  if (argc > 3) return 0;  // layout only
   double *dP, *dx, *du, *dout;
   unsigned long long* dst;
   CK(hipMalloc(&dP, 8 * psz));
@@ -158,13 +170,6 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(dP, P.data(), 8 * psz, hipMemcpyHostToDevice));
   CK(hipMemcpy(dx, x.data(), 8 * nx, hipMemcpyHostToDevice));
   CK(hipMemcpy(du, u.data(), 8 * u.size(), hipMemcpyHostToDevice));
-  const Blk bk = parse(P.data());
-  bool vc;
-  const int njac = count_jac_costs(bk, &vc);
-  const DiffLayout l = diff_layout(nj, njac, bk.nc, vc, bk.nj - bk.nun, count_cost_rows(bk, bk.nj - bk.nun));
-  const size_t smd = 8 * (pad2(l.total) + pad2(psz) + 256);
-  const size_t smc = 8 * (pad2(calc_work_doubles(nj, bk.nc)) + pad2(psz) + 256);
-  printf("nj %d nx %d nu %d m %d psz %d lds diff %zu calc %zu\n", nj, nx, nu, m, psz, smd, smc);
   CK(hipFuncSetAttribute((const void*)probe_diff, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smd));
   CK(hipFuncSetAttribute((const void*)probe_calc, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smc));
   std::vector<unsigned long long> st(256);
