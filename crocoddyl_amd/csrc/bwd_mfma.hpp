@@ -582,13 +582,18 @@ __device__ __forceinline__ bool bwd_knot(const Dev& D, const BwdLds& L, int b, i
   // The lane id and the dimensions are laundered through empty asm on every
   // knot: otherwise LICM hoists every per-lane address of the unrolled code
   // out of the knot loop and keeps them all live (hundreds of registers).
-  int lane = threadIdx.x & 63, n = D.n, m = D.m;
+  // m: the padded control dimension of the blocks (nu_max); mu: this knot's nu (an
+  // impulse knot has none: Quu_inv, K and k vanish, Vx = Qx, Vxx = Qxx as the reference's
+  // backwardPass does for nu = 0, ddp.cpp:229-253); the blocks' columns beyond mu are
+  // not read
+  int lane = threadIdx.x & 63, n = D.n, m = D.m, mu = D.knots[t].nu;
   asm volatile("" : "+v"(lane));
   asm volatile("" : "+s"(n), "+s"(m));
+  mu = __builtin_amdgcn_readfirstlane(mu);
   const int q = lane >> 4, c = lane & 15;
   const bool xr = !isnan(xreg), ur = !isnan(ureg);
   const int64_t kk = D.knot(b, t), rr = D.run(b, t);
-  const bool boxk = feas && D.box_knot(b, t);  // SolverBoxFDDP gains on this knot
+  const bool boxk = feas && mu > 0 && D.box_knot(b, t);  // SolverBoxFDDP gains on this knot (box-fddp.cpp:47)
   if constexpr (W != 0 && P.owns_u(W)) __builtin_amdgcn_s_setprio(2);  // Quu first: the inversion waits on it
   // the next knot's operands (LDS-DMA; lands during P2 / P3)
   auto issue_dma = [&]() {
@@ -651,10 +656,10 @@ __device__ __forceinline__ bool bwd_knot(const Dev& D, const BwdLds& L, int b, i
           double v = 0.;
           if (i < NTL) {
             const int R = 16 * i + q + 4 * r;
-            if (R < n && Cu < m) v = Lxu[(int64_t)Cu * n + R];
+            if (R < n && Cu < mu) v = Lxu[(int64_t)Cu * n + R];
           } else {
             const int Ru = 16 * (i - NTL) + q + 4 * r;
-            if (Ru < m && Cu < m) v = Luu[(int64_t)Cu * m + Ru];
+            if (Ru < mu && Cu < mu) v = Luu[(int64_t)Cu * m + Ru];
           }
           Lq[o][ju][r] = v;
         }
@@ -715,7 +720,7 @@ __device__ __forceinline__ bool bwd_knot(const Dev& D, const BwdLds& L, int b, i
         L.qx[R] = R < n ? L.lxv[R] + v : 0.;
       } else {
         const int Ru = 16 * (i - NTL) + c;
-        L.qu[Ru] = Ru < m ? L.luv[Ru] + v : 0.;
+        L.qu[Ru] = Ru < mu ? L.luv[Ru] + v : 0.;
       }
     }
   }
@@ -777,7 +782,7 @@ __device__ __forceinline__ bool bwd_knot(const Dev& D, const BwdLds& L, int b, i
           v = 0.;  // + sym(Lxx) in P2
         } else {
           v = Lq[o][isx ? 0 : ju][r];
-          if (ur && i >= NTL && 16 * (i - NTL) + q + 4 * r == 16 * ju + c && 16 * ju + c < m) v += ureg;
+          if (ur && i >= NTL && 16 * (i - NTL) + q + 4 * r == 16 * ju + c && 16 * ju + c < mu) v += ureg;
         }
         acc[o][r] = v;
       }
@@ -828,9 +833,9 @@ __device__ __forceinline__ bool bwd_knot(const Dev& D, const BwdLds& L, int b, i
       if (!box_gains_wave<MP, LDQ>(D, L, b, t, cur, lane) && lane == 0) *L.flag = 1;
     } else {
 #ifdef FDDP_INV_BLK
-      const bool bad = sym_sweep_inverse_blk<MP, LDQ>(Quu, Qi, L.rowbuf, m, lane);
+      const bool bad = sym_sweep_inverse_blk<MP, LDQ>(Quu, Qi, L.rowbuf, mu, lane);
 #else
-      const bool bad = sym_sweep_inverse<MP, LDQ>(Quu, Qi, L.rowbuf, m, lane);
+      const bool bad = sym_sweep_inverse<MP, LDQ>(Quu, Qi, L.rowbuf, mu, lane);
 #endif
       if (bad && lane == 0) *L.flag = 1;
     }
@@ -916,15 +921,15 @@ __device__ __forceinline__ bool bwd_knot(const Dev& D, const BwdLds& L, int b, i
       const int row = lane % MP, part = lane / MP;
       double a0 = 0., a1 = 0.;
       if (!boxk) {
-        for (int k2 = part; k2 < m; k2 += 2 * LPR) {
+        for (int k2 = part; k2 < mu; k2 += 2 * LPR) {
           a0 = fma(Qi[k2 * LDQ + row], L.qu[k2], a0);
-          if (k2 + LPR < m) a1 = fma(Qi[(k2 + LPR) * LDQ + row], L.qu[k2 + LPR], a1);
+          if (k2 + LPR < mu) a1 = fma(Qi[(k2 + LPR) * LDQ + row], L.qu[k2 + LPR], a1);
         }
         double a = a0 + a1;
 #pragma unroll
         for (int o2 = MP; o2 < 64; o2 <<= 1) a += __shfl_xor(a, o2, 64);
         if (part == 0) {
-          if (row >= m) a = 0.;
+          if (row >= mu) a = 0.;
           L.kv[row] = a;
           if (row < m) D.k[rr * D.sM + row] = a;
         }
@@ -933,14 +938,14 @@ __device__ __forceinline__ bool bwd_knot(const Dev& D, const BwdLds& L, int b, i
       double a;
       a0 = 0.;
       a1 = 0.;
-      for (int k2 = part; k2 < m; k2 += 2 * LPR) {
+      for (int k2 = part; k2 < mu; k2 += 2 * LPR) {
         a0 = fma(Quu[k2 * LDQ + row], L.kv[k2], a0);
-        if (k2 + LPR < m) a1 = fma(Quu[(k2 + LPR) * LDQ + row], L.kv[k2 + LPR], a1);
+        if (k2 + LPR < mu) a1 = fma(Quu[(k2 + LPR) * LDQ + row], L.kv[k2 + LPR], a1);
       }
       a = a0 + a1;
 #pragma unroll
       for (int o2 = MP; o2 < 64; o2 <<= 1) a += __shfl_xor(a, o2, 64);
-      if (part == 0) L.quuk[row] = row < m ? a : 0.;
+      if (part == 0) L.quuk[row] = row < mu ? a : 0.;
     }
     if (bad) *L.flag = 1;
   }

@@ -426,10 +426,22 @@ static bool mb_one_per_cu(const fddp_handle* h) {
   }();
   return env >= 0 ? env == 1 : h->mb_diff_smem > 80 * 1024;
 }
+// 512-thread (8-wave) workgroups for the one-per-CU plans: two waves per SIMD where the
+// 256-thread plan has one (C5 calcDiff 66 -> 59 ms); FDDP_MB_NT=256 / 512 forces
+static bool mb_x8(const fddp_handle* h) {
+  static const int env = [] {
+    const char* e = std::getenv("FDDP_MB_NT");
+    return e ? std::atoi(e) : 0;
+  }();
+  return env ? env == 512 : mb_one_per_cu(h);
+}
 // Multibody knots (knot-parallel): calc for sel_calc, calcDiff for sel_diff (-1: none).
 int launch_mb(fddp_handle* h, int sel_calc, int sel_diff) {
   const Dev& D = h->D;
-  if (mb_one_per_cu(h))
+  if (mb_x8(h))
+    hipLaunchKernelGGL(mb_knot_kernel_x8, dim3(D.T + 1, D.B), dim3(2 * mb::kMbDiffNT), h->mb_diff_smem, h->stream, D,
+                       sel_calc, sel_diff);
+  else if (mb_one_per_cu(h))
     hipLaunchKernelGGL(mb_knot_kernel_w1, dim3(D.T + 1, D.B), dim3(mb::kMbDiffNT), h->mb_diff_smem, h->stream, D, sel_calc,
                        sel_diff);
   else
@@ -859,6 +871,7 @@ int apply_knots(fddp_handle* h, const fddp_knot_desc* knots, const double* param
         {(const void*)calc_diff_kernel<kNT>, h->cdiff_smem, true, "calc_diff_kernel"},
         {(const void*)mb_knot_kernel, h->mb_diff_smem, h->has_mb, "mb_knot_kernel"},
         {(const void*)mb_knot_kernel_w1, h->mb_diff_smem, h->has_mb, "mb_knot_kernel_w1"},
+        {(const void*)mb_knot_kernel_x8, h->mb_diff_smem, h->has_mb, "mb_knot_kernel_x8"},
     };
     for (const Req& r : reqs) {
       if (!r.use) continue;
@@ -868,9 +881,12 @@ int apply_knots(fddp_handle* h, const fddp_knot_desc* knots, const double* param
                                           std::to_string(r.bytes) + " bytes: " + hipGetErrorString(e));
     }
   }
-  {  // backward sweep variant: MFMA tiles when every running knot has nu == nu_max
+  {  // backward sweep variant: MFMA tiles when every running knot has nu == nu_max, or on
+    // multibody horizons (their calcDiff zero-fills the Fu columns beyond a knot's nu, so
+    // the sweep runs a knot on its own nu: the impulse knots of the gaits)
     bool uniform_nu = d.nu_max > 0;
     for (int t = 0; t < d.T; ++t) uniform_nu = uniform_nu && knots[t].nu == d.nu_max;
+    uniform_nu = uniform_nu || (h->all_mb && d.nu_max > 0);
     const char* env = std::getenv("FDDP_BACKWARD");
     const bool force_generic = env && std::strcmp(env, "generic") == 0;
     const int ntl = (d.ndx + 15) / 16, mtl = (d.nu_max + 15) / 16;

@@ -248,6 +248,7 @@ __global__ __launch_bounds__(NT) void calc_diff_kernel(Dev D, int sel, int gaps,
 // (derivative blocks) for those selected by sel_diff (-1: none), fused: the
 // calcDiff evaluates the dynamics the calc needs anyway. The gaps of these
 // knots are written by calc_diff_kernel as for any knot.
+template <int NT>
 __device__ __forceinline__ void mb_knot_body(const Dev& D, int sel_calc, int sel_diff) {
   const int t = blockIdx.x, b = blockIdx.y;
   const fddp_knot_desc kd = D.knots[t];
@@ -268,14 +269,14 @@ __device__ __forceinline__ void mb_knot_body(const Dev& D, int sel_calc, int sel
   const double* Pg = D.pblock(b, t);
   double* P = sm + D.mbd;
   const int psz = (int)Pg[3];
-  for (int e = threadIdx.x; e < psz; e += mb::kMbDiffNT) P[e] = Pg[e];
+  for (int e = threadIdx.x; e < psz; e += NT) P[e] = Pg[e];
   __syncthreads();
   if (do_diff)
-    mb::knot_calc_diff(P, D.nx, D.m, xg, ug, running && kd.nu > 0, sm, D.Fx + kk * D.sNN, D.Fu + kk * D.sNM,
+    mb::knot_calc_diff<NT>(P, D.nx, D.m, xg, ug, running && kd.nu > 0, sm, D.Fx + kk * D.sNN, D.Fu + kk * D.sNM,
                        D.Lxx + kk * D.sNN, D.Lxu + kk * D.sNM, D.Luu + kk * D.sMM, D.Lx + kk * D.sN,
                        D.Lu + kk * D.sM, xn, cost);
   else
-    mb::knot_calc_diff(P, D.nx, D.m, xg, ug, running && kd.nu > 0, sm, nullptr, nullptr, nullptr, nullptr, nullptr,
+    mb::knot_calc_diff<NT>(P, D.nx, D.m, xg, ug, running && kd.nu > 0, sm, nullptr, nullptr, nullptr, nullptr, nullptr,
                        nullptr, nullptr, xn, cost);
 }
 // Two register budgets of the same kernel: 2 waves/EU (256 VGPRs, a few spills) lets two
@@ -283,11 +284,17 @@ __device__ __forceinline__ void mb_knot_body(const Dev& D, int sel_calc, int sel
 // the plan leaves room for one workgroup per CU anyway (Talos: ~140 KB) the 1-wave/EU
 // build gets the whole register file (VGPRs + AGPRs) and nothing spills.
 __global__ __launch_bounds__(mb::kMbDiffNT) __attribute__((amdgpu_waves_per_eu(2))) void mb_knot_kernel(Dev D, int sel_calc, int sel_diff) {
-  mb_knot_body(D, sel_calc, sel_diff);
+  mb_knot_body<mb::kMbDiffNT>(D, sel_calc, sel_diff);
 }
 __global__ __launch_bounds__(mb::kMbDiffNT) __attribute__((amdgpu_waves_per_eu(1, 1))) void mb_knot_kernel_w1(Dev D, int sel_calc,
                                                                                                    int sel_diff) {
-  mb_knot_body(D, sel_calc, sel_diff);
+  mb_knot_body<mb::kMbDiffNT>(D, sel_calc, sel_diff);
+}
+// Eight waves per (knot, element) workgroup: one workgroup per CU on the large LDS plans
+// still puts two waves on every SIMD, and the phases' independent work (Gauss-Jordan
+// slabs, MFMA tiles, the output blocks) spreads over twice the waves.
+__global__ __launch_bounds__(2 * mb::kMbDiffNT) void mb_knot_kernel_x8(Dev D, int sel_calc, int sel_diff) {
+  mb_knot_body<2 * mb::kMbDiffNT>(D, sel_calc, sel_diff);
 }
 
 // ---------------------------------------------------------------------------

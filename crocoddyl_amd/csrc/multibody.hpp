@@ -891,7 +891,12 @@ struct WVals {
   MB_HD static int64_t doubles(int nj) { return (int64_t)kWPerJoint * nj + nj + 6; }
 };
 
-MB_HD __forceinline__ int64_t part_doubles(int nj) { return (int64_t)4 * 6 * nj; }
+// The per-wave partial sums (RNEA recursions: 6 per dof, composites: 10 per dof) come
+// from at most kPartWaves waves (their LDS areas are sized for that); larger workgroups
+// leave the other waves idle in those phases.
+constexpr int kPartWaves = 4;
+MB_HD __forceinline__ int part_waves(int nt) { return (nt >> 6) < kPartWaves ? (nt >> 6) : kPartWaves; }
+MB_HD __forceinline__ int64_t part_doubles(int nj) { return (int64_t)kPartWaves * 6 * nj; }
 
 MB_HD inline int jump_rounds(int nj) {
   int r = 0;
@@ -1727,13 +1732,14 @@ MB_HD inline void world_kinematics(const X& ex, const Blk& b, const WVals& W, co
   ex.run([&](int lane) {
     if (lane < nj) w_joint_world(b, W, lane, (R & 1) != 0);
   });
-  if (split_composite) {  // (no cost work alongside) the composites over all waves
+  if (split_composite) {  // (no cost work alongside) the composites over the waves
+    const int nw = part_waves(ex.nt);
     ex.run([&](int lane) {
       const int w = lane >> 6, l = lane & 63;
-      if (l < nj) w_composite(b, W, l, w, ex.nt >> 6);
+      if (l < nj && w < nw) w_composite(b, W, l, w, nw);
     });
     ex.run([&](int lane) {
-      if (lane < nj) w_composite_combine(W, lane, ex.nt >> 6, true);
+      if (lane < nj) w_composite_combine(W, lane, nw, true);
     });
   } else {
     ex.run([&](int lane) {
@@ -1754,25 +1760,25 @@ MB_HD inline void world_kinematics(const X& ex, const Blk& b, const WVals& W, co
 template <class X>
 MB_HD inline void world_rnea(const X& ex, const Blk& b, const WVals& W, const double* qd, const double* qdd,
                              double* tau, const double* fx = nullptr) {
-  const int nj = b.nj, nw = ex.nt >> 6;
+  const int nj = b.nj, nw = part_waves(ex.nt);
   // every ancestor / subtree sum split over the waves (w_*_part), combined by lane i
   ex.run([&](int lane) {
     const int w = lane >> 6, i = lane & 63;
-    if (i < nj) w_velocity_part(W, qd, i, w, nw);
+    if (i < nj && w < nw) w_velocity_part(W, qd, i, w, nw);
   });
   ex.run([&](int lane) {
     if (lane < nj) w_velocity_accel_term(W, qd, qdd, lane, nw);
   });
   ex.run([&](int lane) {
     const int w = lane >> 6, i = lane & 63;
-    if (i < nj) w_accel_part(W, i, w, nw);
+    if (i < nj && w < nw) w_accel_part(W, i, w, nw);
   });
   ex.run([&](int lane) {
     if (lane < nj) w_accel_body_force(W, lane, nw, fx);
   });
   ex.run([&](int lane) {
     const int w = lane >> 6, i = lane & 63;
-    if (i < nj) w_force_part(W, i, w, nw);
+    if (i < nj && w < nw) w_force_part(W, i, w, nw);
   });
   ex.run([&](int lane) {
     if (lane < nj) w_joint_force_comb(W, tau, lane, nw);
@@ -2081,9 +2087,9 @@ MB_HD inline void body_nh_lane(const Blk& b, const WVals& W, int d, double* nb) 
 // lane j < nj of wave w (of nw): components [11 w, 11 w + 11) of Nsub_j, Hsub_j (sums over
 // the bodies below dof j) into ns[42 j ..]; every body read, the others weighted 0 (no
 // branch: the unrolled loads overlap), the 42 components split over the waves
+template <int kC = 11>  // components per wave: nw * kC >= 42 (11 for 4 waves, 6 for 8)
 MB_HD inline void subtree_nh_lane(const Blk& b, const WVals& W, int j, const double* nb, double* ns, int w = 0,
                                   int nw = 1) {
-  constexpr int kC = 11;  // components per wave (4 x 11 >= 42)
   const int e0 = nw == 1 ? 0 : w * kC, e1 = nw == 1 ? 42 : (e0 + kC < 42 ? e0 + kC : 42);
   double acc[kC];
   for (int e = 0; e < kC; ++e) acc[e] = 0.;
@@ -2196,8 +2202,9 @@ MB_HD inline void parent_motion(const Blk& b, const WVals& W, int j, double* VP,
   }
 }
 
+// part / np: this lane's share of the rows k (the direction's setup is repeated per part)
 MB_HD inline void dtau_direction(const Blk& b, const WVals& W, const double* qp, int dd, int L, double* dtau,
-                                  const double* ns = nullptr) {
+                                  const double* ns = nullptr, int part = 0, int np = 1) {
   const int nj = b.nj, j = dd < nj ? dd : dd - nj;
   const bool isq = dd < nj;
   double S[6], VP[6], AP[6], u[6], cj[6], G[6], t6[6], t7[6];
@@ -2232,7 +2239,9 @@ MB_HD inline void dtau_direction(const Blk& b, const WVals& W, const double* qp,
     for (int e = 0; e < 6; ++e) u[e] = S[e];  // P_k . S_j
   }
   const Mask aj = *W.anc(j);
-  for (int k = 0; k < nj; ++k) {
+  int k0 = 0, k1 = nj;
+  if (np > 1) k_range(nj, part, np, k0, k1);
+  for (int k = k0; k < k1; ++k) {
     double val = 0.;
     if ((*W.anc(k) >> j) & 1ull) {  // k's body below j's (or the same body)
       const double* Q = qp + 12 * k;
@@ -2733,7 +2742,12 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
     });
     ex.run([&](int lane) {
       const int w = lane >> 6, j = lane & 63;
-      if (j < nj) subtree_nh_lane(b, W, j, dtau, nsub, w, ex.nt >> 6);
+      if (j < nj) {
+        if (ex.nt >= 512)
+          subtree_nh_lane<6>(b, W, j, dtau, nsub, w, ex.nt >> 6);
+        else
+          subtree_nh_lane<11>(b, W, j, dtau, nsub, w, ex.nt >> 6);
+      }
     });
   }
   // the velocity-product maps on the lower half of the workgroup, the cost / Euler
@@ -2762,7 +2776,12 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
   ex.run([&](int lane) {
     const int h = ex.nt / 2;
     if (lane < h) {
-      for (int dd = lane; dd < (imp ? nj : L); dd += h) dtau_direction(b, W, qp, dd, L, dtau, imp ? nullptr : nsub);
+      // (direction, row part) per lane: a direction's rows split over up to 3 lanes when
+      // the half-workgroup has the lanes for it
+      const int nd = imp ? nj : L;
+      const int np = h >= 3 * nd ? 3 : (h >= 2 * nd ? 2 : 1);
+      for (int id = lane; id < nd * np; id += h)
+        dtau_direction(b, W, qp, id % nd, L, dtau, imp ? nullptr : nsub, id / nd, np);
     } else if (nc > 0 && !imp) {
       for (int dd = lane - h; dd < L; dd += h) contact_direction(b, W, dd, L, da0);
     }
@@ -3209,10 +3228,12 @@ MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, 
   (void)nx;
 }
 
+template <int NT>
 __device__ __forceinline__ void knot_calc_diff(const double* P, int nx, int m, const double* xg, const double* ug, bool use_u,
                                       double* w, double* Fx, double* Fu, double* Lxx, double* Lxu, double* Luu,
                                       double* Lx, double* Lu, double* xnext_out, double* cost_out) {
-  knot_calc_diff_x(DevExec{kMbDiffNT}, P, nx, m, xg, ug, use_u, w, Fx, Fu, Lxx, Lxu, Luu, Lx, Lu, xnext_out, cost_out);
+  static_assert(NT >= 256 && NT % 64 == 0, "the knot phases split over >= 4 waves");
+  knot_calc_diff_x(DevExec{NT}, P, nx, m, xg, ug, use_u, w, Fx, Fu, Lxx, Lxu, Luu, Lx, Lu, xnext_out, cost_out);
 }
 
 }  // namespace mb

@@ -60,7 +60,8 @@ __device__ inline bool gauss_jordan(const StampExec& ex, double* A, int nr, int 
   return ok;
 }
 
-__global__ __launch_bounds__(kMbDiffNT) void probe_diff(const double* Pg, int nx, int m, const double* xg,
+template <int NT>
+__global__ __launch_bounds__(NT) void probe_diff(const double* Pg, int nx, int m, const double* xg,
                                                         const double* ug, int use_u, double* out, int64_t so,
                                                         unsigned long long* stamps, int mode) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
@@ -71,13 +72,13 @@ __global__ __launch_bounds__(kMbDiffNT) void probe_diff(const double* Pg, int nx
   const DiffLayout l = diff_layout(bk.nj, njac, bk.nc, vc, bk.nj - bk.nun, count_cost_rows(bk, bk.nj - bk.nun));
   double* P = sm + pad2(l.total);
   unsigned long long* st = (unsigned long long*)(P + pad2(psz));
-  for (int e = threadIdx.x; e < psz; e += kMbDiffNT) P[e] = Pg[e];
+  for (int e = threadIdx.x; e < psz; e += NT) P[e] = Pg[e];
   if (threadIdx.x == 0) {
     st[0] = 0;
     st[1] = __builtin_amdgcn_s_memtime();
   }
   __syncthreads();
-  StampExec ex{kMbDiffNT, st};
+  StampExec ex{NT, st};
   double* o = out + so * blockIdx.x;
   const int n = 2 * (int)Pg[1];
   double xn[1];
@@ -170,7 +171,10 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(dP, P.data(), 8 * psz, hipMemcpyHostToDevice));
   CK(hipMemcpy(dx, x.data(), 8 * nx, hipMemcpyHostToDevice));
   CK(hipMemcpy(du, u.data(), 8 * u.size(), hipMemcpyHostToDevice));
-  CK(hipFuncSetAttribute((const void*)probe_diff, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smd));
+  const int pnt = getenv("PROBE_NT") ? atoi(getenv("PROBE_NT")) : kMbDiffNT;  // calcDiff workgroup size
+  printf("calcDiff workgroup: %d threads\n", pnt == 512 ? 512 : 256);
+  CK(hipFuncSetAttribute((const void*)probe_diff<256>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smd));
+  CK(hipFuncSetAttribute((const void*)probe_diff<512>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smd));
   CK(hipFuncSetAttribute((const void*)probe_calc, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smc));
   std::vector<unsigned long long> st(256);
   for (int which = 0; which < 2; ++which) {
@@ -179,11 +183,16 @@ int main(int argc, char** argv) {
       CK(hipEventCreate(&e0));
       CK(hipEventCreate(&e1));
       CK(hipEventRecord(e0));
-      if (which == 0)
-        hipLaunchKernelGGL(probe_diff, dim3(nwg), dim3(kMbDiffNT), smd, 0, dP, nx, m, dx, du, nu > 0 ? 1 : 0, dout, so,
-                           dst, getenv("PROBE_DIFF_NOCOST") ? 1 : 0);
-      else
+      if (which == 0) {
+        if (pnt == 512)
+          hipLaunchKernelGGL(probe_diff<512>, dim3(nwg), dim3(512), smd, 0, dP, nx, m, dx, du, nu > 0 ? 1 : 0, dout, so,
+                             dst, getenv("PROBE_DIFF_NOCOST") ? 1 : 0);
+        else
+          hipLaunchKernelGGL(probe_diff<256>, dim3(nwg), dim3(256), smd, 0, dP, nx, m, dx, du, nu > 0 ? 1 : 0, dout, so,
+                             dst, getenv("PROBE_DIFF_NOCOST") ? 1 : 0);
+      } else {
         hipLaunchKernelGGL(probe_calc, dim3(nwg), dim3(256), smc, 0, dP, nx, dx, du, nu > 0 ? 1 : 0, dout, dst);
+      }
       CK(hipEventRecord(e1));
       CK(hipEventSynchronize(e1));
       float ms;
