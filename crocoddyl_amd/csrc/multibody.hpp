@@ -1822,7 +1822,7 @@ MB_HD inline int64_t calc_work_doubles(int nj, int nc = 0) {
 // Every thread must call (phases end in barriers). x, u readable by all lanes;
 // writes xnext[0..nx) and returns the knot cost. `w`: calc_work_doubles(nj, nc).
 template <class X>
-MB_HD inline double knot_calc_x(const X& ex, const double* P, int nx, const double* x, const double* u, bool use_u,
+MB_HD __forceinline__ double knot_calc_x(const X& ex, const double* P, int nx, const double* x, const double* u, bool use_u,
                                 double* xnext, double* w) {
   w = ex.lds(w);  // the work area and the parameter block live in LDS
   P = ex.lds(P);
@@ -2559,7 +2559,7 @@ __device__ __forceinline__ void gn_blocks_mfma(const double* Rm, int ldR, const 
 #endif
 
 template <class X>
-MB_HD inline void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, const double* xg, const double* ug,
+MB_HD __forceinline__ void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, const double* xg, const double* ug,
                                    bool use_u, double* w, double* Fx, double* Fu, double* Lxx, double* Lxu,
                                    double* Luu, double* Lx, double* Lu, double* xnext_out = nullptr,
                                    double* cost_out = nullptr) {
