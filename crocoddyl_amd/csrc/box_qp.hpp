@@ -161,6 +161,21 @@ __device__ __forceinline__ bool box_qp_wave(const double* H, int ldh, double* Qi
     double s0 = 0., s1 = 0.;
     if (valid) {
       int j = 0;
+      // eight columns' loads issued before their FMAs (one LDS round trip per eight);
+      // the even / odd chains as below, so the sums are the same
+      for (; j + 8 <= m; j += 8) {
+        double a[8], x[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          a[q] = A[(j + q) * lda + lane];
+          x[q] = vb[j + q];
+        }
+#pragma unroll
+        for (int q = 0; q < 8; q += 2) {
+          s0 = fma(a[q], x[q], s0);
+          s1 = fma(a[q + 1], x[q + 1], s1);
+        }
+      }
       for (; j + 1 < m; j += 2) {
         s0 = fma(A[j * lda + lane], vb[j], s0);
         s1 = fma(A[(j + 1) * lda + lane], vb[j + 1], s1);

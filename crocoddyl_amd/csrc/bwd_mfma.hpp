@@ -355,7 +355,16 @@ __device__ __forceinline__ bool sym_sweep_inverse_blk(const double* Quu, double*
 template <int MP, int LDQ>
 __device__ __forceinline__ bool sym_sweep_inverse_masked(const double* H, double* Qi, double* rb, int m, int lane,
                                                          const InvMap& mp) {
-  for (int e = lane; e < m * m; e += 64) {
+  // staged four entries per lane at a time, loads before stores (one LDS round trip per four)
+  int e = lane;
+  for (; e + 3 * 64 < m * m; e += 4 * 64) {
+    double v[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = mp.load(H, LDQ, (e + 64 * q) % m, (e + 64 * q) / m);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) Qi[((e + 64 * q) / m) * LDQ + (e + 64 * q) % m] = v[q];
+  }
+  for (; e < m * m; e += 64) {
     const int i = e % m, j = e / m;
     Qi[j * LDQ + i] = mp.load(H, LDQ, i, j);
   }

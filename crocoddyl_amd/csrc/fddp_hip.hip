@@ -317,6 +317,7 @@ struct fddp_handle_s {
   bool has_mb = false;     // multibody knots present (mb_knot_kernel)
   bool all_mb = false;     // every knot is a multibody knot
   size_t mb_diff_smem = 0; // its dynamic LDS
+  int mb_nj = 0;            // largest multibody tree (dofs)
   int bwd_variant = 0;  // 0 generic, else (NTL*10+MTL)*10+waves of the MFMA sweep
   // timing
   bool timing = false;
@@ -435,10 +436,21 @@ static bool mb_x8(const fddp_handle* h) {
   }();
   return env ? env == 512 : mb_one_per_cu(h);
 }
+// 128-thread (2-wave) workgroups for the small trees whose LDS plan fits four per CU
+static bool mb_x2(const fddp_handle* h) {
+  static const int env = [] {
+    const char* e = std::getenv("FDDP_MB_NT");
+    return e ? std::atoi(e) : 0;
+  }();
+  return env ? env == 128 : (h->mb_nj <= 16 && h->mb_diff_smem <= 40 * 1024);
+}
 // Multibody knots (knot-parallel): calc for sel_calc, calcDiff for sel_diff (-1: none).
 int launch_mb(fddp_handle* h, int sel_calc, int sel_diff) {
   const Dev& D = h->D;
-  if (mb_x8(h))
+  if (mb_x2(h))
+    hipLaunchKernelGGL(mb_knot_kernel_x2, dim3(D.T + 1, D.B), dim3(mb::kMbDiffNT / 2), h->mb_diff_smem, h->stream, D,
+                       sel_calc, sel_diff);
+  else if (mb_x8(h))
     hipLaunchKernelGGL(mb_knot_kernel_x8, dim3(D.T + 1, D.B), dim3(2 * mb::kMbDiffNT), h->mb_diff_smem, h->stream, D,
                        sel_calc, sel_diff);
   else if (mb_one_per_cu(h))
@@ -789,6 +801,7 @@ int apply_knots(fddp_handle* h, const fddp_knot_desc* knots, const double* param
     h->all_mb = true;
     for (int t = 0; t <= d.T; ++t) h->all_mb = h->all_mb && is_mb_kind(knots[t].kind);
     D.mbw = h->has_mb ? pad2(fddp::mb::calc_work_doubles(mb_nj, mb_nc)) : 0;
+    h->mb_nj = mb_nj;
     // parallel line-search trials: they pay on the large trees (C5 Talos, nv = 38:
     // forward -12 %), where one rollout keeps a CU busy longest; on small ones (C4
     // Solo12, nv = 18) the extra trials cost more than the shorter chains save
@@ -872,6 +885,7 @@ int apply_knots(fddp_handle* h, const fddp_knot_desc* knots, const double* param
         {(const void*)mb_knot_kernel, h->mb_diff_smem, h->has_mb, "mb_knot_kernel"},
         {(const void*)mb_knot_kernel_w1, h->mb_diff_smem, h->has_mb, "mb_knot_kernel_w1"},
         {(const void*)mb_knot_kernel_x8, h->mb_diff_smem, h->has_mb, "mb_knot_kernel_x8"},
+        {(const void*)mb_knot_kernel_x2, h->mb_diff_smem, h->has_mb, "mb_knot_kernel_x2"},
     };
     for (const Req& r : reqs) {
       if (!r.use) continue;

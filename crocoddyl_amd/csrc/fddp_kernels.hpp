@@ -290,6 +290,12 @@ __global__ __launch_bounds__(mb::kMbDiffNT) __attribute__((amdgpu_waves_per_eu(1
                                                                                                    int sel_diff) {
   mb_knot_body<mb::kMbDiffNT>(D, sel_calc, sel_diff);
 }
+// Two waves per (knot, element) workgroup, for the small trees (the arm: nv = 7), whose
+// phases leave most lanes of four waves idle: four workgroups per CU under the same
+// register budget.
+__global__ __launch_bounds__(mb::kMbDiffNT / 2) __attribute__((amdgpu_waves_per_eu(2))) void mb_knot_kernel_x2(Dev D, int sel_calc, int sel_diff) {
+  mb_knot_body<mb::kMbDiffNT / 2>(D, sel_calc, sel_diff);
+}
 // Eight waves per (knot, element) workgroup: one workgroup per CU on the large LDS plans
 // still puts two waves on every SIMD, and the phases' independent work (Gauss-Jordan
 // slabs, MFMA tiles, the output blocks) spreads over twice the waves.

@@ -2087,10 +2087,11 @@ MB_HD inline void body_nh_lane(const Blk& b, const WVals& W, int d, double* nb) 
 // lane j < nj of wave w (of nw): components [11 w, 11 w + 11) of Nsub_j, Hsub_j (sums over
 // the bodies below dof j) into ns[42 j ..]; every body read, the others weighted 0 (no
 // branch: the unrolled loads overlap), the 42 components split over the waves
-template <int kC = 11>  // components per wave: nw * kC >= 42 (11 for 4 waves, 6 for 8)
+template <int kC = 11>  // components per pass (11 for 4 waves, 6 for 8: one pass per wave)
 MB_HD inline void subtree_nh_lane(const Blk& b, const WVals& W, int j, const double* nb, double* ns, int w = 0,
                                   int nw = 1) {
-  const int e0 = nw == 1 ? 0 : w * kC, e1 = nw == 1 ? 42 : (e0 + kC < 42 ? e0 + kC : 42);
+  // wave w's components [w per, (w + 1) per), per = ceil(42 / nw), in chunks of kC
+  const int per = (42 + nw - 1) / nw, e0 = w * per, e1 = e0 + per < 42 ? e0 + per : 42;
   double acc[kC];
   for (int e = 0; e < kC; ++e) acc[e] = 0.;
   for (int c0 = e0; c0 < e1; c0 += kC) {
@@ -3170,15 +3171,17 @@ MB_HD __forceinline__ void knot_calc_diff_x(const X& ex, const double* P, int nx
     // lane nt-1-k (the lanes with the fewest GEMM tasks), into the dead pivot buffer
     // (pb[0, 64)); jac-cost residuals from the Jacobian phase.
     // The wide records (state / control, wide_cost) row-parallel instead: 32 lanes each
-    // from lane 128 on, their partials into pb[64 + 32 w + l], summed below.
+    // from lane 128 on (from lane 0 in a 128-thread workgroup), their partials into
+    // pb[64 + 32 w + l], summed below.
     if (cost_out) {
       const double* cr = b.C;
+      const int wbase = ex.nt >= 256 ? 128 : 0;
       int f = 0, nw = 0;
       for (int k = 0; k < b.ncost; ++k) {
         const CRec C{cr};
         const int t = C.type();
         const bool wide = wide_cost(C, nw);
-        const int wl = lane - 128 - 32 * nw;  // this lane's share of wide record nw
+        const int wl = lane - wbase - 32 * nw;  // this lane's share of wide record nw
         if (wide ? (wl >= 0 && wl < 32) : lane == ex.nt - 1 - k) {
           const Act act = cost_act(b, C, nu);
           double a = 0.;
@@ -3232,7 +3235,7 @@ template <int NT>
 __device__ __forceinline__ void knot_calc_diff(const double* P, int nx, int m, const double* xg, const double* ug, bool use_u,
                                       double* w, double* Fx, double* Fu, double* Lxx, double* Lxu, double* Luu,
                                       double* Lx, double* Lu, double* xnext_out, double* cost_out) {
-  static_assert(NT >= 256 && NT % 64 == 0, "the knot phases split over >= 4 waves");
+  static_assert(NT >= 128 && NT % 64 == 0, "the calcDiff phases take >= 2 waves");
   knot_calc_diff_x(DevExec{NT}, P, nx, m, xg, ug, use_u, w, Fx, Fu, Lxx, Lxu, Luu, Lx, Lu, xnext_out, cost_out);
 }
 

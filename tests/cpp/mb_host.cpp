@@ -2,6 +2,7 @@
 // crocoddyl_amd/csrc/multibody.hpp compiled for the host and run with the
 // sequential-lane executor, so tests/test_multibody_host.py can check the
 // exact device arithmetic against the numpy oracle without a GPU.
+#include <cstdlib>
 #include <vector>
 
 #include "../../crocoddyl_amd/csrc/multibody.hpp"
@@ -21,6 +22,9 @@ void mb_host_calc_diff(const double* P, int nx, int m, const double* x, const do
                        double* cost) {
   const Blk b = parse(P);
   std::vector<double> w(diff_layout(b.nj, kMaxJacCosts, b.nc, true, b.nj - b.nun, count_cost_rows(b, b.nj - b.nun)).total, 0.);
-  knot_calc_diff_x(HostExec{kMbDiffNT}, P, nx, m, x, u, use_u != 0, w.data(), Fx, Fu, Lxx, Lxu, Luu, Lx, Lu, xnext, cost);
+  // MB_HOST_NT: the workgroup size the lanes emulate (128 / 256 / 512: the device's
+  // small-tree, default and 8-wave calcDiff kernels)
+  const char* e = std::getenv("MB_HOST_NT");
+  knot_calc_diff_x(HostExec{e ? std::atoi(e) : kMbDiffNT}, P, nx, m, x, u, use_u != 0, w.data(), Fx, Fu, Lxx, Lxu, Luu, Lx, Lu, xnext, cost);
 }
 }

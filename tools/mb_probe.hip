@@ -172,7 +172,8 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(dx, x.data(), 8 * nx, hipMemcpyHostToDevice));
   CK(hipMemcpy(du, u.data(), 8 * u.size(), hipMemcpyHostToDevice));
   const int pnt = getenv("PROBE_NT") ? atoi(getenv("PROBE_NT")) : kMbDiffNT;  // calcDiff workgroup size
-  printf("calcDiff workgroup: %d threads\n", pnt == 512 ? 512 : 256);
+  printf("calcDiff workgroup: %d threads\n", pnt == 512 || pnt == 128 ? pnt : 256);
+  CK(hipFuncSetAttribute((const void*)probe_diff<128>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smd));
   CK(hipFuncSetAttribute((const void*)probe_diff<256>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smd));
   CK(hipFuncSetAttribute((const void*)probe_diff<512>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smd));
   CK(hipFuncSetAttribute((const void*)probe_calc, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smc));
@@ -184,7 +185,10 @@ int main(int argc, char** argv) {
       CK(hipEventCreate(&e1));
       CK(hipEventRecord(e0));
       if (which == 0) {
-        if (pnt == 512)
+        if (pnt == 128)
+          hipLaunchKernelGGL(probe_diff<128>, dim3(nwg), dim3(128), smd, 0, dP, nx, m, dx, du, nu > 0 ? 1 : 0, dout, so,
+                             dst, getenv("PROBE_DIFF_NOCOST") ? 1 : 0);
+        else if (pnt == 512)
           hipLaunchKernelGGL(probe_diff<512>, dim3(nwg), dim3(512), smd, 0, dP, nx, m, dx, du, nu > 0 ? 1 : 0, dout, so,
                              dst, getenv("PROBE_DIFF_NOCOST") ? 1 : 0);
         else
