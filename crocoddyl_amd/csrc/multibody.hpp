@@ -52,6 +52,15 @@ MB_HD __forceinline__ void mb_gstore(double* p, double v) {
   *p = v;
 #endif
 }
+// two consecutive doubles (16-B aligned) in one store
+MB_HD __forceinline__ void mb_gstore2(double* p, double v0, double v1) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  *(__attribute__((address_space(1))) double2*)p = make_double2(v0, v1);
+#else
+  p[0] = v0;
+  p[1] = v1;
+#endif
+}
 template <class T>
 MB_HD __forceinline__ T* mb_lds(T* p) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -599,6 +608,204 @@ __device__ __forceinline__ bool gauss_jordan(const DevExec&, double* A, int nr, 
   return gauss_jordan_regs<SPW>(A, nr, ld, nc, flag, pb, id0);
 }
 
+// no side work for the idle waves of gj_mfma
+struct GjNoSide {
+  __device__ void operator()(int, int, int) const {}
+};
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(MB_GJ_ROWS)
+// Blocked Gauss-Jordan on the fp64 matrix cores. A: nr x nc column-major in LDS (ld),
+// its left nr x nr block SPD. Pivot blocks of 16 rows; per block k:
+//  A  every wave inverts the diagonal block D itself, in registers (the symmetric sweep:
+//     a_pp <- -1/a_pp, a_ip <- a_ip/a_pp, a_pj <- a_pj/a_pp, a_ij <- a_ij - a_ip a_pj/a_pp;
+//     after all 16 pivots N = -D^-1), so no barrier separates it from B;
+//  B  the wave owning column tile j (j mod nw) forms R_j = N A_kj = -D^-1 A_kj and updates
+//     its whole column: A_ij += A_ik R_j (i != k), A_kj <- -R_j (v_mfma_f64_16x16x4_f64);
+//  C  (inverse) the diagonal column block, A_ik <- A_ik N, A_kk <- -N, deferred to its
+//     owner's next pass (nobody else reads it before then): one workgroup barrier per
+//     pivot block instead of one per pivot.
+// N's registers serve as both MFMA operands: lane (i = lane & 15, g = lane >> 4) holds
+// N[i][g + 4q], q = 0..3, which is the A fragment of k-chunk q (k = g + 4q) and, N being
+// symmetric, the B fragment too; R_j's accumulators are the B fragments of the update
+// with the same k order. Columns: the right-hand sides start at the 16-aligned virtual
+// column nrp (their tiles never share a tile with the matrix). The pivots are the LDL^T
+// pivots in order, so a non-positive one is the LLT failure the unblocked sweep reports.
+// inverse: the left block becomes M^-1 in place; the right-hand sides M^-1 B either way.
+#ifndef MB_GJ_MARK
+#define MB_GJ_MARK(id)  // (tools/mb_probe: phase stamps)
+#endif
+// side(slot, lane, nlanes): independent work of the caller for the waves that own no
+// column tile (wave >= nct), one slot per barrier interval (nbr + 1 of them), so the
+// latency-bound pivot chain of the owners hides it.
+template <class Side = GjNoSide>
+__device__ __forceinline__ bool gj_mfma(double* A_, int nr, int ld, int nc, bool inverse, int* flag,
+                                        Side side = Side{}) {
+  typedef __attribute__((address_space(3))) double lds_d;
+  typedef double f64x4 __attribute__((ext_vector_type(4)));
+  lds_d* A = (lds_d*)lds_ptr(A_);
+  const int tid = (int)threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = (int)(blockDim.x >> 6);
+  const int li = lane & 15, lk = lane >> 4;
+  const int nrp = (nr + 15) & ~15, nbr = nrp >> 4, nct = (nrp + nc - nr + 15) >> 4;
+  auto phys = [&](int v) { return v < nr ? v : (v < nrp ? -1 : v - nrp + nr); };
+  // branch-free guarded load: an in-range address always, the value selected
+  auto at = [&](int r, int c) -> double {
+    const bool v = r < nr && c >= 0 && c < nc;
+    const double x = A[(v ? r : 0) + ld * (v ? c : 0)];
+    return v ? x : 0.;
+  };
+  __syncthreads();
+  MB_GJ_MARK(0);
+  bool bad = false;
+  double Np[4] = {0., 0., 0., 0.};
+  // C: column block kc <- A_ik N (i != kc), the diagonal block <- -N
+  auto col_update = [&](int kc, const double* N) {
+    const int c = 16 * kc + li;
+#pragma unroll 1
+    for (int i = 0; i < nbr; ++i) {
+      if (i == kc) continue;
+      f64x4 acc = {0., 0., 0., 0.};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int kk = 16 * kc + lk + 4 * q;
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(at(16 * i + li, kk < nr ? kk : -1), N[q], acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int r = 16 * i + lk + 4 * q;
+        if (r < nr && c < nr) A[r + ld * c] = acc[q];
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = 16 * kc + li, cc = 16 * kc + lk + 4 * q;
+      if (r < nr && cc < nr) A[r + ld * cc] = -N[q];
+    }
+  };
+#pragma unroll 1
+  for (int k = 0; k < nbr; ++k) {
+    const int r0 = 16 * k;
+    double d[4] = {0., 0., 0., 0.};
+    // A: only the waves that own a column tile need N (one sweep per SIMD, not two);
+    // the padding pivots beyond nr are skipped (their identity rows stay +1, which only
+    // ever multiplies the zero-loaded padding)
+    if (wave < nct) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int c = lk + 4 * q;
+        const double x = at(r0 + li, r0 + c < nr ? r0 + c : -1);
+        d[q] = (r0 + li < nr && r0 + c < nr) ? x : (li == c ? 1. : 0.);
+      }
+#pragma unroll
+      for (int p = 0; p < 16; ++p) {
+        if (r0 + p < nr) {  // (uniform; the loop stays fully unrolled, d[] static)
+          const int pq = p >> 2, pg = p & 3;
+          const double app = readlane_d(d[pq], p + 16 * pg);
+          const double aip = __shfl(d[pq], li + 16 * pg);
+          double apc[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) apc[q] = __shfl(d[q], p + 16 * lk);
+          bad = bad || !(app > 0.);
+          // 1 / app: v_rcp_f64 and one Newton step (the pivot chain is latency-bound:
+          // 35 cycles per dependent f64 op; without the IEEE division's special-case
+          // scaling, app > 0 is all that is used)
+          double ip = __builtin_amdgcn_rcp(app);
+          ip = __builtin_fma(ip, __builtin_fma(-app, ip, 1.), ip);
+          const double t = aip * ip;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {  // selects, no branches
+            const int c = lk + 4 * q;
+            const double upd = d[q] - t * apc[q];
+            const double rowp = c == p ? -ip : apc[q] * ip;
+            d[q] = li == p ? rowp : (c == p ? t : upd);
+          }
+        }
+      }
+    }
+    MB_GJ_MARK(1 + 3 * k);
+#pragma unroll 1
+    for (int j = wave; j < nct; j += nw) {
+      if (inverse && j == k - 1) col_update(j, Np);
+      if (j == k || (!inverse && j < k)) continue;
+      const int pc = phys(16 * j + li);
+      f64x4 R = {0., 0., 0., 0.};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) R = __builtin_amdgcn_mfma_f64_16x16x4f64(d[q], at(r0 + lk + 4 * q, pc), R, 0, 0, 0);
+#pragma unroll 1
+      for (int i = 0; i < nbr; ++i) {
+        if (i == k) continue;
+        f64x4 acc;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[q] = at(16 * i + lk + 4 * q, pc);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int kk = r0 + lk + 4 * q;
+          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(at(16 * i + li, kk < nr ? kk : -1), R[q], acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int r = 16 * i + lk + 4 * q;
+          if (r < nr && pc >= 0 && pc < nc) A[r + ld * pc] = acc[q];
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int r = r0 + lk + 4 * q;
+        if (r < nr && pc >= 0 && pc < nc) A[r + ld * pc] = -R[q];
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) Np[q] = d[q];
+    if (wave >= nct) side(k, tid - 64 * nct, (nw - nct) * 64);
+    MB_GJ_MARK(2 + 3 * k);
+    __syncthreads();
+    MB_GJ_MARK(3 + 3 * k);
+  }
+  if (inverse)
+    for (int j = wave; j < nct; j += nw)
+      if (j == nbr - 1) col_update(j, Np);
+  if (wave >= nct) side(nbr, tid - 64 * nct, (nw - nct) * 64);
+  if (tid == 0) *lds_ptr(flag) = bad ? 1 : 0;
+  __syncthreads();
+  MB_GJ_MARK(20);
+  return !bad;
+}
+#endif
+
+// whether mb_invert works in place (then [M | I] needs no identity half)
+__device__ __forceinline__ constexpr bool mb_inv_inplace(const DevExec&) {
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(MB_GJ_ROWS)
+  return true;
+#else
+  return false;
+#endif
+}
+// [M | B] (nr x nc, M SPD) -> M^-1 B in the columns beyond M (the left block is consumed)
+__device__ __forceinline__ bool mb_solve(const DevExec&, double* A, int nr, int ld, int nc, int* flag, double* pb) {
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(MB_GJ_ROWS)
+  (void)pb;
+  return gj_mfma(A, nr, ld, nc, false, flag);
+#else
+  return gauss_jordan_regs<2>(A, nr, ld, nc, flag, pb);
+#endif
+}
+// [M | I] (nr x 2 nr, M SPD) -> M^-1, at *Minv (device: in place of M). side: work the
+// idle waves run meanwhile (gj_mfma); *nslots: the slots it ran (0: none)
+template <class Side = GjNoSide>
+__device__ __forceinline__ bool mb_invert(const DevExec&, double* A, int nr, int ld, int* flag, double* pb,
+                                          double** Minv, Side side = Side{}, int* nslots = nullptr) {
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(MB_GJ_ROWS)
+  (void)pb;
+  *Minv = A;
+  const int nbr = (nr + 15) >> 4, nw = (int)(blockDim.x >> 6);
+  if (nslots) *nslots = nw > nbr ? nbr + 1 : 0;
+  return gj_mfma(A, nr, ld, nr, true, flag, side);
+#else
+  (void)side;
+  if (nslots) *nslots = 0;
+  *Minv = A + (int64_t)ld * nr;
+  return gauss_jordan_regs<3>(A, nr, ld, 2 * nr, flag, pb, nr);
+#endif
+}
+
 template <int SPW, class X>
 MB_HD __attribute__((noinline)) bool gauss_jordan(const X& ex, double* A, int nr, int ld, int nc, int* flag,
                                                  double* = nullptr, int = 0) {
@@ -639,6 +846,22 @@ MB_HD __attribute__((noinline)) bool gauss_jordan(const X& ex, double* A, int nr
   }
   ex.sync();
   return *flag == 0;
+}
+// the host emulation (and any other executor): the unblocked sweep on [M | B], [M | I]
+template <class X>
+MB_HD __forceinline__ constexpr bool mb_inv_inplace(const X&) {
+  return false;
+}
+template <class X>
+MB_HD __forceinline__ bool mb_solve(const X& ex, double* A, int nr, int ld, int nc, int* flag, double* pb) {
+  return gauss_jordan<2>(ex, A, nr, ld, nc, flag, pb);
+}
+template <class X, class Side = int>
+MB_HD __forceinline__ bool mb_invert(const X& ex, double* A, int nr, int ld, int* flag, double* pb, double** Minv,
+                                     Side = Side{}, int* nslots = nullptr) {
+  if (nslots) *nslots = 0;
+  *Minv = A + (int64_t)ld * nr;
+  return gauss_jordan<3>(ex, A, nr, ld, 2 * nr, flag, pb, nr);
 }
 
 // ---- dual numbers for the exp6 / log6 Jacobians ----------------------------
@@ -1904,7 +2127,7 @@ MB_HD __forceinline__ double knot_calc_x(const X& ex, const double* P, int nx, c
       red[0] = total;
     }
   });
-  bool ok = gauss_jordan<2>(ex, A, nj, lda, ncol, flag, pb);
+  bool ok = mb_solve(ex, A, nj, lda, ncol, flag, pb);
   // z, then a (impulse: v+, in tau's slot; z = M^-1 M v = v)
   double* a = imp ? tau : A + (int64_t)lda * (nj + nc);
   if (nc > 0) {
@@ -2360,17 +2583,21 @@ MB_HD inline void impulse_direction(const Blk& b, const WVals& W, int j, int L, 
 // frame-velocity cost also its velocity column nj + j) and, on lane 0, their
 // residuals (rf[6 f + e]); lanes j < 6 of a free-flyer knot also the Euler step's
 // Jexp6(dq) column j (Je, col-major 6x6) and, on lane 0, Ad(exp6(dq)^-1) (Ai).
+// only: -1 every jac cost, -2 none (the free-flyer Euler terms alone), f >= 0 jac cost f
+// alone (one (dof, cost) item per lane)
 MB_HD inline void jac_lane(const Blk& b, const WVals& W, const double* x, int j, double* Jf, int jw, double* rf,
-                           const double* dqff, double* Je, double* Ai) {
+                           const double* dqff, double* Je, double* Ai, int only = -1) {
   const int nj = b.nj;
   double S[6];
   for (int e = 0; e < 6; ++e) S[e] = W.S(j)[e];
   const double* cr = b.C;
   int f = 0;
-  for (int k = 0; k < b.ncost; ++k) {
+  for (int k = 0; k < b.ncost && only != -2; ++k) {
     const CRec C{cr};
     const int t = C.type();
-    if (jac_cost(b, t)) {
+    if (jac_cost(b, t) && only >= 0 && f != only) {
+      ++f;
+    } else if (jac_cost(b, t)) {
       double r[6] = {0., 0., 0., 0., 0., 0.}, Jc[6] = {0., 0., 0., 0., 0., 0.};
       if (t == C_FRAME_PLACEMENT || t == C_FRAME_TRANSLATION) {
         const bool sup = (*W.anc(frame_dof(b, C.d())) >> j) & 1ull;
@@ -2466,21 +2693,27 @@ __device__ __forceinline__ mb_f64x4 mb_mfma(double a, double b, mb_f64x4 c) {
 typedef __attribute__((address_space(3))) double mb_lds_d;
 __device__ __attribute__((noinline)) void da_mfma_lds(const mb_lds_d* Minv, int lda, const mb_lds_d* H,
                                                       const mb_lds_d* dtau, const mb_lds_d* da0, int nj, int nc, int L,
-                                                      int Ld, double mul_v, int vcols, mb_lds_d* da) {
+                                                      int Ld, double mul_v, int vcols, mb_lds_d* da,
+                                                      const mb_lds_d* Sinv, int nfd, mb_lds_d* dfx) {
   const int lane = (int)threadIdx.x & 63, wave = (int)threadIdx.x >> 6, nw = (int)blockDim.x >> 6;
   const int li = lane & 15, lk = lane >> 4;
-  const int tr = (nj + 15) >> 4, tc = (L + 15) >> 4, K = nj + nc;
+  const int NR = nj + nfd, tr = (NR + 15) >> 4, tc = (L + 15) >> 4, K = nj + nc;
 #pragma unroll 1
   for (int tile = wave; tile < tr * tc; tile += nw) {
     const int ti = tile / tc, tj = tile - ti * tc;
     const int r = 16 * ti + li, c = 16 * tj + li;
-    const bool rv = r < nj, cvld = c < L;
+    const bool rv = r < nj, rf = !rv && r < NR, cvld = c < L;
     mb_f64x4 acc = {0., 0., 0., 0.};
 #pragma unroll 1
     for (int kb = 0; kb < K; kb += 4) {
       const int k = kb + lk;
       const bool km = k < nj, kh = !km && k < K;
-      const double a = (rv && km) ? Minv[k * lda + r] : ((rv && kh) ? H[(k - nj) * nj + r] : 0.);
+      // rows < nj: [Kinv_tl | H]; the force rows nj + k': [H^T | -S^-1] (S symmetric)
+      double a = 0.;
+      if (rv)
+        a = km ? Minv[k * lda + r] : (kh ? H[(k - nj) * nj + r] : 0.);
+      else if (rf)
+        a = km ? H[(r - nj) * nj + k] : (kh ? -Sinv[(k - nj) * nc + (r - nj)] : 0.);
       const double bv = (cvld && km) ? dtau[k * L + c] : ((cvld && kh) ? da0[(k - nj) * L + c] : 0.);
       acc = mb_mfma(a, bv, acc);
     }
@@ -2491,18 +2724,21 @@ __device__ __attribute__((noinline)) void da_mfma_lds(const mb_lds_d* Minv, int 
     for (int q = 0; q < 4; ++q) {
       const int i = 16 * ti + lk + 4 * q;
       if (i < nj && jc < L) da[i * Ld + jc] = acc[q] * mul;
+      if (i >= nj && i < NR && jc < L) dfx[(i - nj) * L + jc] = acc[q];
     }
   }
 }
 // da = -(Kinv_tl dtau + H da0) (contact-fwddyn.hxx:127-140 as computeABADerivatives /
 // the KKT inverse): [Kinv_tl | H] (nj x (nj + nc)) times [dtau; da0] ((nj + nc) x L),
-// rows of da at stride Ld; impulse knots keep only the q columns.
+// rows of da at stride Ld; impulse knots keep only the q columns. With the contact-force
+// costs (nfd = nc) the same product's extra rows [H^T | -S^-1] give d lambda / dx
+// (contact-fwddyn.hxx:131-137), row-major nc x L into dfx.
 __device__ __forceinline__ void da_mfma(const double* Minv, int lda, const double* H, const double* dtau,
                                         const double* da0, int nj, int nc, int L, int Ld, bool imp, bool ok,
-                                        double* da) {
+                                        double* da, const double* Sinv, int nfd, double* dfx) {
   da_mfma_lds((const mb_lds_d*)lds_ptr(Minv), lda, (const mb_lds_d*)lds_ptr(H), (const mb_lds_d*)lds_ptr(dtau),
               (const mb_lds_d*)lds_ptr(da0), nj, nc, L, Ld, ok ? -1. : (double)NAN, imp ? nj : L,
-              (mb_lds_d*)lds_ptr(da));
+              (mb_lds_d*)lds_ptr(da), (const mb_lds_d*)lds_ptr(Sinv), nfd, (mb_lds_d*)lds_ptr(dfx));
 }
 
 // The Gauss-Newton blocks sc * (R^T diag(w h) R + the diagonal state / control terms)
@@ -2535,14 +2771,17 @@ __device__ __forceinline__ void gn_blocks_mfma(const double* Rm, int ldR, const 
       double a = 0., bv = 0.;
       if (r < nrows) {
         const double* Rr = Rm + (int64_t)r * ldR;
-        a = ca < cv ? Rr[ca] * wrow[r] : 0.;
-        bv = cb < cv ? Rr[cb] : 0.;
+        // (the tile's transpose: the accumulator rows run over bj, its columns over bi,
+        // so lane li holds row 16 bi + li and the 16 lanes of a column store 128
+        // contiguous bytes of the column-major blocks)
+        a = cb < cv ? Rr[cb] : 0.;
+        bv = ca < cv ? Rr[ca] * wrow[r] : 0.;
       }
       acc = mb_mfma(a, bv, acc);
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int i = 16 * bi + lk + 4 * q, j = 16 * bj + li;
+      const int i = 16 * bi + li, j = 16 * bj + lk + 4 * q;
       if (i > j || j >= NC) continue;
       const double v = sc * (i == j ? acc[q] + diag[i] : acc[q]);
       if (j < L) {  // Lxx (symmetric)
@@ -2554,6 +2793,38 @@ __device__ __forceinline__ void gn_blocks_mfma(const double* Rm, int ldR, const 
         mb_gstore(Luu + (int64_t)(j - L) * m + (i - L), v);
         if (i < j) mb_gstore(Luu + (int64_t)(i - L) * m + (j - L), v);
       }
+    }
+  }
+}
+
+// The subtree sums of the velocity-product maps (subtree_nh_lane) on the matrix cores:
+// Nsub (nj x 42) = T nb with the subtree indicator T[j][b] = 1 when dof j is an ancestor-
+// or-self of b and b carries a body; waves w of nw (the caller's numbering) take the
+// 16 x 16 output tiles round-robin. (The sums' association changes, not their terms.)
+__device__ __forceinline__ void subtree_nh_mfma(const Blk& b, const WVals& W, const double* nb_, double* ns_, int w,
+                                                int nw) {
+  const mb_lds_d* nb = (const mb_lds_d*)lds_ptr(nb_);
+  mb_lds_d* ns = (mb_lds_d*)lds_ptr(ns_);
+  const int lane = (int)threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
+  const int nj = b.nj, tr = (nj + 15) >> 4, tc = 3;  // 42 components in 3 tiles
+#pragma unroll 1
+  for (int tile = w; tile < tr * tc; tile += nw) {
+    const int ti = tile / tc, tj = tile - ti * tc;
+    const int j = 16 * ti + li, c = 16 * tj + li;
+    mb_f64x4 acc = {0., 0., 0., 0.};
+#pragma unroll 2
+    for (int kb = 0; kb < nj; kb += 4) {
+      const int bb = kb + lk;
+      const bool bv_ok = bb < nj && c < 42;
+      const int bs = bb < nj ? bb : 0;
+      const double nv = nb[42 * bs + (c < 42 ? c : 0)];
+      const bool in = bb < nj && j < nj && carries_body(b, bs) && ((*W.anc(bs) >> j) & 1ull);
+      acc = mb_mfma(in ? 1. : 0., bv_ok ? nv : 0., acc);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int row = 16 * ti + lk + 4 * q;
+      if (row < nj && c < 42) ns[42 * row + c] = acc[q];
     }
   }
 }
@@ -2604,10 +2875,10 @@ MB_HD __forceinline__ void knot_calc_diff_x(const X& ex, const double* P, int nx
   ex.run([&](int lane) {
     for (int e = lane; e < nq + nj; e += ex.nt) x[e] = xg[e];
     if (lane < nj) u[lane] = (use_u && lane < nu) ? ug[lane] : 0.;  // (impulse: a zero velocity)
-    for (int e = lane; e < 2 * nj * lda; e += ex.nt) {
-      const int c = e / lda, r = e % lda;
-      A[e] = (r < nj && c == nj + r) ? 1. : 0.;
-    }
+    // the identity half of [M | I] (the CRBA writes every entry of M); the device
+    // inverts M in place and needs none
+    if (!mb_inv_inplace(ex))
+      for (int e = lane; e < nj * lda; e += ex.nt) A[(int64_t)nj * lda + e] = e % lda == e / lda ? 1. : 0.;
   });
   // world-frame kinematics, M into the left half of [M | I], nle
   world_kinematics(ex, b, W, x, A, lda, [](int, int) {}, true);
@@ -2623,8 +2894,36 @@ MB_HD __forceinline__ void knot_calc_diff_x(const X& ex, const double* P, int nx
       }
     });
   double* pb = red + 8;
-  bool ok = gauss_jordan<3>(ex, A, nj, lda, 2 * nj, flag, pb, nj);
-  double* Minv = A + (int64_t)lda * nj;  // column-major nj x nj; with contacts: d a / d tau after the Schur step
+  double* Minv;  // column-major nj x nj (ld lda); with contacts: d a / d tau after the Schur step
+  // The velocity-product maps of the derivatives (per-body N_b, h_b into the dtau area;
+  // their subtree sums into the da area; P_k, Q_k) need the velocities and composite
+  // inertias only: the waves the blocked Gauss-Jordan leaves idle build them meanwhile,
+  // one map per barrier interval (vp: how many are done when it returns)
+  double* nsub = da;  // (unused by impulse knots)
+  // The cost-Jacobian columns (one (dof, jac cost) item per lane, jac_lane) need the
+  // kinematics only as well: beside the body maps in the first slot, when the idle
+  // waves are at least two (jac_side).
+  bool jac_side = false;
+  auto vp_side = [&](int slot, int sl, int snt) {
+    if (slot == 0) {
+      if (!imp)
+        for (int d = sl; d < nj; d += 64) body_nh_lane(b, W, d, dtau);
+      if (snt >= 128)
+        for (int id = sl - 64; id >= 0 && id < nj * njac; id += snt - 64)
+          jac_lane(b, W, x, id % nj, Jf, jw, rf, nullptr, nullptr, nullptr, id / nj);
+    } else if (slot == 1 && !imp) {
+#if defined(__HIP_DEVICE_COMPILE__)
+      subtree_nh_mfma(b, W, dtau, nsub, sl >> 6, snt >> 6);
+#endif
+    } else if (slot == 2 && !imp) {
+      for (int j = sl; j < nj; j += snt) qp_lane_ns(W, j, nsub, qp);
+    }
+  };
+  int vp = 0;
+  bool ok = mb_invert(ex, A, nj, lda, flag, pb, &Minv, vp_side, &vp);
+  jac_side = vp > 0 && (ex.nt >> 6) - ((nj + 15) >> 4) >= 2;
+  vp = imp ? 0 : (vp < 3 ? vp : 3);
+  Minv = ex.lds(Minv);
   // z = (M + A)^-1 (tau - nle) (the acceleration without contacts); Y = Minv Jc^T
   ex.run([&](int lane) {
     if (lane < nj && imp) {
@@ -2736,34 +3035,42 @@ MB_HD __forceinline__ void knot_calc_diff_x(const X& ex, const double* P, int nx
   // free-flyer Euler step's Jexp6 and Ad(exp6(dq)^-1) (dq = v dt + a dt^2)
   // per-body velocity-product maps (in the dtau area, free until the dtau phase), then
   // their subtree sums (in the da area, free until the da phase)
-  double* nsub = da;  // (unused by impulse knots)
-  if (!imp) {
+  // (the maps the Gauss-Jordan's idle waves did not build)
+  if (!imp && vp < 1)
     ex.run([&](int lane) {
       if (lane < nj) body_nh_lane(b, W, lane, dtau);
     });
+  if (!imp && vp < 2)
     ex.run([&](int lane) {
       const int w = lane >> 6, j = lane & 63;
+#if defined(__HIP_DEVICE_COMPILE__)
+      (void)j;
+      subtree_nh_mfma(b, W, dtau, nsub, w, ex.nt >> 6);
+#else
       if (j < nj) {
         if (ex.nt >= 512)
           subtree_nh_lane<6>(b, W, j, dtau, nsub, w, ex.nt >> 6);
         else
           subtree_nh_lane<11>(b, W, j, dtau, nsub, w, ex.nt >> 6);
       }
+#endif
     });
-  }
-  // the velocity-product maps on the lower half of the workgroup, the cost / Euler
-  // Jacobians on the upper half (independent: they run side by side)
+  // the velocity-product maps (if still to do) on the lower half of the workgroup, the
+  // cost / Euler Jacobians on the rest (independent: they run side by side)
   ex.run([&](int lane) {
-    const int h = ex.nt / 2;
+    const int h = !imp && vp < 3 ? ex.nt / 2 : 0;
     if (lane < h) {
-      if (!imp)
-        for (int j = lane; j < nj; j += h) qp_lane_ns(W, j, nsub, qp);
+      for (int j = lane; j < nj; j += h) qp_lane_ns(W, j, nsub, qp);
       return;
     }
     double dq[6];
     if (ffe)
       for (int e = 0; e < 6; ++e) dq[e] = x[nq + e] * dt + av[e] * dt2;
-    for (int j = lane - h; j < nj; j += h) jac_lane(b, W, x, j, Jf, jw, rf, ffe ? dq : nullptr, Je, Ai);
+    if (jac_side) {  // the Jacobian columns are done: the free-flyer Euler terms only
+      if (ffe && lane - h < 6) jac_lane(b, W, x, lane - h, Jf, jw, rf, dq, Je, Ai, -2);
+      return;
+    }
+    for (int j = lane - h; j < nj; j += ex.nt - h) jac_lane(b, W, x, j, Jf, jw, rf, ffe ? dq : nullptr, Je, Ai);
   });
   if (imp) {  // V = 0 in the impulse RNEA: P_k = 0, Q_k = Ycrb_k S_k
     ex.run([&](int lane) {
@@ -2819,8 +3126,10 @@ MB_HD __forceinline__ void knot_calc_diff_x(const X& ex, const double* P, int nx
     const int nl = ex.nt - (b.ncost > 0 ? b.ncost : 1);
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(MB_NO_MFMA_DA)
     // on the matrix cores, every wave (the whole workgroup is converged here)
-    da_mfma(Minv, lda, H, dtau, da0, nj, nc, L, Ld, imp, ok, da);
+    da_mfma(Minv, lda, H, dtau, da0, nj, nc, L, Ld, imp, ok, da, Sx + (int64_t)nc * nc, fd ? nc : 0, dfx);
+    constexpr bool dfx_done = true;
 #else
+    constexpr bool dfx_done = false;
     // two entries per lane at a time: two independent dot-product chains, so the LDS
     // loads of one overlap the other's FMAs (each entry's summation order unchanged)
     const int ne = nj * L;
@@ -2844,7 +3153,7 @@ MB_HD __forceinline__ void knot_calc_diff_x(const X& ex, const double* P, int nx
 #endif
     if (fd) {
       const double* Sinv = Sx + (int64_t)nc * nc;
-      for (int e = lane; e < nc * L; e += ex.nt) {
+      for (int e = lane; e < (dfx_done ? 0 : nc * L); e += ex.nt) {
         const int k = e / L, c = e % L;
         double s = 0.;
         for (int i = 0; i < nj; ++i) s += H[(int64_t)k * nj + i] * dtau[(int64_t)i * L + c];
@@ -2929,55 +3238,60 @@ MB_HD __forceinline__ void knot_calc_diff_x(const X& ex, const double* P, int nx
       if (kk == (b.ncost > 0 ? b.ncost - 1 : 0)) cg[4 * kMaxCosts - 1] = g;  // the group count
     }
   });
-  // Output blocks, entry by entry over all lanes (consecutive lanes write
-  // consecutive addresses of the column-major blocks).
+  // Output blocks in row pairs over all lanes: consecutive lanes write consecutive
+  // 16-B pairs of the column-major blocks (n even, blocks 16-B aligned); the lane's
+  // (column, row pair) advances by nt pairs without a division.
   ex.run([&](int lane) {
     // Fx(i, c): Euler assembly (euler.hxx:100-112) with JintegrateTransport / Jintegrate
-    for (int e = lane; e < n * n; e += ex.nt) {
-      const int c = e / n, i = e % n;
-      double f;
+    auto fx_at = [&](int i, int c) -> double {
       if (imp) {  // [[I, 0], [-G dtau_dq - H dv0_dq, G M = I - H Jc]] (impulse-fwddyn.hxx:111-115)
-        if (i < nj) {
-          f = c == i ? 1. : 0.;
-        } else if (c < nj) {
-          f = da[(int64_t)(i - nj) * Ld + c];
-        } else {
-          double s = 0.;
-          for (int k = 0; k < nc; ++k) s += H[(int64_t)k * nj + (i - nj)] * Jc[(int64_t)k * nj + (c - nj)];
-          f = ok ? (c - nj == i - nj ? 1. : 0.) - s : NAN;
-        }
-      } else if (integ) {
-        if (i < nj && ffe && i < 6) {  // Jexp6(dq) (da dt^2 + [0 dt I]) + Ad(exp6(dq)^-1)
-          double s = c < 6 ? Ai[c * 6 + i] : 0.;
-          for (int r = 0; r < 6; ++r)
-            s += Je[r * 6 + i] * (da[(int64_t)r * Ld + c] * dt2 + (c == nj + r ? dt : 0.));
-          f = s;
-        } else if (i < nj) {
-          f = da[(int64_t)i * Ld + c] * dt2 + (c == nj + i ? dt : 0.) + (c == i ? 1. : 0.);
-        } else {
-          f = da[(int64_t)(i - nj) * Ld + c] * dt + (c == i ? 1. : 0.);
-        }
-      } else {
-        f = c == i ? 1. : 0.;
+        if (i < nj) return c == i ? 1. : 0.;
+        if (c < nj) return da[(int64_t)(i - nj) * Ld + c];
+        double s = 0.;
+        for (int k = 0; k < nc; ++k) s += H[(int64_t)k * nj + (i - nj)] * Jc[(int64_t)k * nj + (c - nj)];
+        return ok ? (c - nj == i - nj ? 1. : 0.) - s : NAN;
       }
-      mb_gstore(Fx + e, f);
-    }
+      if (!integ) return c == i ? 1. : 0.;
+      if (i < nj && ffe && i < 6) {  // Jexp6(dq) (da dt^2 + [0 dt I]) + Ad(exp6(dq)^-1)
+        double s = c < 6 ? Ai[c * 6 + i] : 0.;
+        for (int r = 0; r < 6; ++r) s += Je[r * 6 + i] * (da[(int64_t)r * Ld + c] * dt2 + (c == nj + r ? dt : 0.));
+        return s;
+      }
+      if (i < nj) return da[(int64_t)i * Ld + c] * dt2 + (c == nj + i ? dt : 0.) + (c == i ? 1. : 0.);
+      return da[(int64_t)(i - nj) * Ld + c] * dt + (c == i ? 1. : 0.);
+    };
     // Fu(i, c) = Kinv_tl(i mod nj, nun + c) dt^2 | dt (dtau/du = [0; I]), Jexp6 on
-    // the free-flyer rows; Lxu from the contact-force costs
-    for (int e = lane; e < n * m; e += ex.nt) {
-      const int c = e / n, i = e % n;
-      double f = 0.;
-      if (integ && c < nu && !imp) {
-        if (i < nj && ffe && i < 6) {
-          double s = 0.;
-          for (int r = 0; r < 6; ++r) s += Je[r * 6 + i] * Minv[(int64_t)(b.nun + c) * lda + r];
-          f = ok ? s * dt2 : NAN;
-        } else {
-          const double mi = ok ? Minv[(int64_t)(b.nun + c) * lda + (i < nj ? i : i - nj)] : NAN;
-          f = i < nj ? mi * dt2 : mi * dt;
-        }
+    // the free-flyer rows
+    auto fu_at = [&](int i, int c) -> double {
+      if (!(integ && c < nu && !imp)) return 0.;
+      if (i < nj && ffe && i < 6) {
+        double s = 0.;
+        for (int r = 0; r < 6; ++r) s += Je[r * 6 + i] * Minv[(int64_t)(b.nun + c) * lda + r];
+        return ok ? s * dt2 : NAN;
       }
-      mb_gstore(Fu + e, f);
+      const double mi = ok ? Minv[(int64_t)(b.nun + c) * lda + (i < nj ? i : i - nj)] : NAN;
+      return i < nj ? mi * dt2 : mi * dt;
+    };
+    // the free-flyer Euler rows (Jexp6 products, 6 terms each) on lanes of their own,
+    // so the row pairs below all take the short path (a wave pays for its slowest lane)
+    const int r6 = ffe ? 6 : 0;
+    for (int e = lane; e < r6 * (n + m); e += ex.nt) {
+      const int c = e / 6, i = e - 6 * c;
+      if (c < n)
+        mb_gstore(Fx + (int64_t)c * n + i, fx_at(i, c));
+      else
+        mb_gstore(Fu + (int64_t)(c - n) * n + i, fu_at(i, c - n));
+    }
+    const int p0 = r6 >> 1, hp = (n >> 1) - p0, dq = ex.nt / hp, dr = ex.nt % hp;
+    for (int c = lane / hp, ip = lane % hp; c < n + m;) {
+      const int i = 2 * (p0 + ip);
+      if (c < n)
+        mb_gstore2(Fx + (int64_t)c * n + i, fx_at(i, c), fx_at(i + 1, c));
+      else
+        mb_gstore2(Fu + (int64_t)(c - n) * n + i, fu_at(i, c - n), fu_at(i + 1, c - n));
+      c += dq;
+      ip += dr;
+      if (ip >= hp) ip -= hp, ++c;
     }
   });
   // the stacked residual Jacobians R (nrows x (L + nu), ld ldR): jac-cost rows from

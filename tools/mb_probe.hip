@@ -8,6 +8,12 @@
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
+// stamps inside the blocked Gauss-Jordan (multibody.hpp gj_mfma), thread 0 of workgroup 0
+__device__ unsigned long long g_gjst[32];
+#define MB_GJ_MARK(id)                                                            \
+  do {                                                                            \
+    if (threadIdx.x == 0 && blockIdx.x == 0) g_gjst[id] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
 #include "../crocoddyl_amd/csrc/multibody.hpp"
 
 using namespace fddp::mb;
@@ -56,6 +62,19 @@ template <int SPW>
 __device__ inline bool gauss_jordan(const StampExec& ex, double* A, int nr, int ld, int nc, int* flag, double* pb,
                                     int id0 = 1 << 30) {
   const bool ok = gauss_jordan_regs<SPW>(A, nr, ld, nc, flag, pb, id0);
+  ex.mark();
+  return ok;
+}
+__device__ constexpr bool mb_inv_inplace(const StampExec& ex) { return mb_inv_inplace(DevExec{ex.nt}); }
+__device__ inline bool mb_solve(const StampExec& ex, double* A, int nr, int ld, int nc, int* flag, double* pb) {
+  const bool ok = mb_solve(DevExec{ex.nt}, A, nr, ld, nc, flag, pb);
+  ex.mark();
+  return ok;
+}
+template <class Side>
+__device__ inline bool mb_invert(const StampExec& ex, double* A, int nr, int ld, int* flag, double* pb,
+                                 double** Minv, Side side, int* nslots) {
+  const bool ok = mb_invert(DevExec{ex.nt}, A, nr, ld, flag, pb, Minv, side, nslots);
   ex.mark();
   return ok;
 }
@@ -214,6 +233,14 @@ int main(int argc, char** argv) {
           prev = t;
         }
         printf("\n  total %llu\n", prev - st[1]);
+        unsigned long long gj[32];
+        CK(hipMemcpyFromSymbol(gj, HIP_SYMBOL(g_gjst), sizeof(gj)));
+        printf("  gauss-jordan marks (ticks from its start; per block: sweep, update, barrier):");
+        for (int i = 1; i < 32; ++i)
+          if (gj[i] >= gj[0] && gj[i] - gj[0] < 10000000ull) printf(" %d:%llu", i, gj[i] - gj[0]);
+        printf("\n");
+        std::vector<unsigned long long> z(32, 0ull);
+        CK(hipMemcpyToSymbol(HIP_SYMBOL(g_gjst), z.data(), sizeof(gj)));
       }
     }
   }

@@ -13,6 +13,7 @@ half the bytes of a wide coalesced streaming read (MI355X_MICROARCH.md, HBM
 section): it is doubled here; WRITE_SIZE is taken as is.
 """
 import csv
+import glob
 import json
 import os
 import shutil
@@ -31,6 +32,12 @@ def counter(path, name_sub, counter_name):
     return vals
 
 
+def find(d, name):
+    """rocprofv3 writes under <dir>/<host>/<pid>/ or straight into <dir>."""
+    hits = sorted(glob.glob(os.path.join(d, "**", name), recursive=True))
+    return hits[0] if hits else os.path.join(d, name)
+
+
 def main():
     tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
     cfg = sys.argv[2] if len(sys.argv) > 2 else "C5_talos_full"
@@ -38,12 +45,12 @@ def main():
     kt = sys.argv[3] if len(sys.argv) > 3 else os.path.join(src, "kt")
     prof = os.path.join(ROOT, "profiles")
     os.makedirs(prof, exist_ok=True)
-    shutil.copy(os.path.join(kt, "run_kernel_stats.csv"), os.path.join(prof, f"{tag}_kernel_stats.csv"))
+    shutil.copy(find(kt, "run_kernel_stats.csv"), os.path.join(prof, f"{tag}_kernel_stats.csv"))
     out = {}
     for kname, key in (("backward_mfma_kernel", "backward"), ("calc_fused_kernel", "calc_fused"),
                        ("forward_kernel", "forward"), ("mb_knot_kernel", "mb_calc_diff")):
-        f = counter(os.path.join(src, "pmc_fetch", "run_counter_collection.csv"), kname, "FETCH_SIZE")
-        w = counter(os.path.join(src, "pmc_write", "run_counter_collection.csv"), kname, "WRITE_SIZE")
+        f = counter(find(os.path.join(src, "pmc_fetch"), "run_counter_collection.csv"), kname, "FETCH_SIZE")
+        w = counter(find(os.path.join(src, "pmc_write"), "run_counter_collection.csv"), kname, "WRITE_SIZE")
         if not f or not w:
             continue
         # steady state: drop the first (cold) dispatch when there are several
@@ -53,7 +60,7 @@ def main():
         write = statistics.mean(w) * 1024.0
         out[key] = {"hbm_bytes_per_launch": fetch + write, "fetch_bytes": fetch, "write_bytes": write,
                     "dispatches": [len(f), len(w)]}
-        mf = os.path.join(src, "pmc_mfma", "run_counter_collection.csv")
+        mf = find(os.path.join(src, "pmc_mfma"), "run_counter_collection.csv")
         if os.path.exists(mf):  # MFMA / busy counters (SQ_* summed over the SIMDs, GRBM over the 8 XCDs)
             c = {n: statistics.mean(counter(mf, kname, n) or [0.]) for n in
                  ("SQ_VALU_MFMA_BUSY_CYCLES", "SQ_INSTS_VALU_MFMA_F64", "SQ_INSTS_VALU_MFMA_MOPS_F64",
