@@ -710,12 +710,14 @@ __device__ __forceinline__ bool gj_mfma(double* A_, int nr, int ld, int nc, bool
           double ip = __builtin_amdgcn_rcp(app);
           ip = __builtin_fma(ip, __builtin_fma(-app, ip, 1.), ip);
           const double t = aip * ip;
+          // row p: a_pc ip; the others: a_ic - t a_pc (one fma with per-lane factors);
+          // column p (register pq of the lanes with lk == pg): t, the pivot itself -ip
+          const bool rp = li == p;
+          const double sf = rp ? ip : -t;
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {  // selects, no branches
-            const int c = lk + 4 * q;
-            const double upd = d[q] - t * apc[q];
-            const double rowp = c == p ? -ip : apc[q] * ip;
-            d[q] = li == p ? rowp : (c == p ? t : upd);
+          for (int q = 0; q < 4; ++q) {
+            const double v = __builtin_fma(sf, apc[q], rp ? 0. : d[q]);
+            d[q] = (q == pq && lk == pg) ? (rp ? -ip : t) : v;
           }
         }
       }
@@ -1121,12 +1123,6 @@ constexpr int kPartWaves = 4;
 MB_HD __forceinline__ int part_waves(int nt) { return (nt >> 6) < kPartWaves ? (nt >> 6) : kPartWaves; }
 MB_HD __forceinline__ int64_t part_doubles(int nj) { return (int64_t)kPartWaves * 6 * nj; }
 
-MB_HD inline int jump_rounds(int nj) {
-  int r = 0;
-  while ((1 << r) < nj) ++r;
-  return r;
-}
-
 // lane i < nj: local placement (buffer A starts as liMi), ancestor bits.
 MB_HD inline void w_joint_local(const Blk& b, const WVals& W, const double* q, int i) {
   double R[9], p[3];
@@ -1165,34 +1161,30 @@ MB_HD inline void w_joint_local(const Blk& b, const WVals& W, const double* q, i
   *W.anc(i) = anc_mask(b, i);
 }
 
-// lane i < nj, round r: T_i <- T_j(i) o T_i, j(i) <- j(j(i)) (A -> B on even
-// rounds, B -> A on odd ones).
-MB_HD inline void w_jump(const WVals& W, int i, int r) {
-  const bool ab = (r & 1) == 0;
-  double* sR = ab ? W.oR(i) : W.Rb(i);
-  double* sp = ab ? W.op(i) : W.pb(i);
-  double* dR = ab ? W.Rb(i) : W.oR(i);
-  double* dp = ab ? W.pb(i) : W.op(i);
-  const int j = (int)*(ab ? W.jA(i) : W.jB(i));
+// lane i < nj: oMi = L_root ... L_i, the local placements of i's ancestors composed
+// by walking its ancestor mask from i towards the root (parents precede children):
+// one phase, no barrier per level, and the loads do not wait on the products (the
+// pointer-jumping rounds this replaced took ceil(log2 nj) barrier phases). The free-flyer's
+// dofs 1..5 carry identity placements and are skipped (exact).
+MB_HD inline void w_walk(const Blk& b, const WVals& W, int i) {
   double R[9], p[3];
-  for (int e = 0; e < 9; ++e) R[e] = sR[e];
-  for (int e = 0; e < 3; ++e) p[e] = sp[e];
-  if (j >= 0) {
-    double Rj[9], pj[3], Ro[9], t[3];
-    const double* jR = ab ? W.oR(j) : W.Rb(j);
-    const double* jp = ab ? W.op(j) : W.pb(j);
-    for (int e = 0; e < 9; ++e) Rj[e] = jR[e];
-    for (int e = 0; e < 3; ++e) pj[e] = jp[e];
-    matmul3(Rj, R, Ro);
-    matvec3(Rj, p, t);
-    for (int e = 0; e < 9; ++e) dR[e] = Ro[e];
-    for (int e = 0; e < 3; ++e) dp[e] = pj[e] + t[e];
-    *(ab ? W.jB(i) : W.jA(i)) = *(ab ? W.jA(j) : W.jB(j));
-  } else {
-    for (int e = 0; e < 9; ++e) dR[e] = R[e];
-    for (int e = 0; e < 3; ++e) dp[e] = p[e];
-    *(ab ? W.jB(i) : W.jA(i)) = -1.;
+  for (int e = 0; e < 9; ++e) R[e] = W.R(i)[e];
+  for (int e = 0; e < 3; ++e) p[e] = W.p(i)[e];
+  Mask m = *W.anc(i) & ~(1ull << i);
+  if (b.ff) m &= ~0x3Eull;
+  while (m) {
+    const int k = 63 - __builtin_clzll(m);
+    m &= ~(1ull << k);
+    double Rk[9], pk[3], Rn[9], t[3];
+    for (int e = 0; e < 9; ++e) Rk[e] = W.R(k)[e];
+    for (int e = 0; e < 3; ++e) pk[e] = W.p(k)[e];
+    matmul3(Rk, R, Rn);
+    matvec3(Rk, p, t);
+    for (int e = 0; e < 9; ++e) R[e] = Rn[e];
+    for (int e = 0; e < 3; ++e) p[e] = pk[e] + t[e];
   }
+  for (int e = 0; e < 9; ++e) W.oR(i)[e] = R[e];
+  for (int e = 0; e < 3; ++e) W.op(i)[e] = p[e];
 }
 
 // lane i < nj: oMi into oR/op (from buffer B after an odd number of rounds),
@@ -1944,16 +1936,15 @@ MB_HD __attribute__((always_inline)) inline void contact_jac_lane(const Blk& b, 
 template <class X, class CostF>
 MB_HD inline void world_kinematics(const X& ex, const Blk& b, const WVals& W, const double* q, double* A, int lda,
                                    CostF costs, bool split_composite = false) {
-  const int nj = b.nj, R = jump_rounds(nj);
+  const int nj = b.nj;
   ex.run([&](int lane) {
     if (lane < nj) w_joint_local(b, W, q, lane);
   });
-  for (int r = 0; r < R; ++r)
-    ex.run([&](int lane) {
-      if (lane < nj) w_jump(W, lane, r);
-    });
   ex.run([&](int lane) {
-    if (lane < nj) w_joint_world(b, W, lane, (R & 1) != 0);
+    if (lane < nj) {
+      w_walk(b, W, lane);
+      w_joint_world(b, W, lane, false);
+    }
   });
   if (split_composite) {  // (no cost work alongside) the composites over the waves
     const int nw = part_waves(ex.nt);
