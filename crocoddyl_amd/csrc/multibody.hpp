@@ -2134,17 +2134,21 @@ MB_HD __forceinline__ double knot_calc_x(const X& ex, const double* P, int nx, c
     });
     ok = gauss_jordan<1>(ex, S, nc, nc, nc + 1, flag, pb) && ok;
     ex.run([&](int lane) {
-      if (lane == 64 && !imp) {  // contact-force costs (lambda = -S^-1 r, in S's last column, negated)
-        double lamv[kMaxNc];
-        for (int k = 0; k < nc; ++k) lamv[k] = -S[(int64_t)nc * nc + k];
-        double add = 0.;
+      // contact-force costs (lambda = -S^-1 r, in S's last column, negated): record k's
+      // term on lane 64 + k into cv[k] (dead since the cost total), summed in record
+      // order with the next phase
+      const int kf = lane - 64;
+      if (kf >= 0 && kf < b.ncost && !imp) {
         const double* cr = b.C;
-        for (int k = 0; k < b.ncost; ++k) {
-          const CRec C{cr};
-          if (force_cost(C.type())) add += C.weight() * force_cost_activation(b, C, lamv, nu);
-          cr += C.size();
+        for (int k = 0; k < kf; ++k) cr += CRec{cr}.size();
+        const CRec C{cr};
+        double term = 0.;
+        if (force_cost(C.type())) {
+          double lamv[kMaxNc];
+          for (int k = 0; k < nc; ++k) lamv[k] = -S[(int64_t)nc * nc + k];
+          term = C.weight() * force_cost_activation(b, C, lamv, nu);
         }
-        red[0] += add;
+        cv[kf] = term;
       }
       if (lane >= nj) return;
       double s = imp ? x[nq + lane] : a[lane];
@@ -2152,13 +2156,22 @@ MB_HD __forceinline__ double knot_calc_x(const X& ex, const double* P, int nx, c
       a[lane] = s;
     });
   }
-  const double cc = red[0];
   const double dt = b.dt;
   if (!ok)  // a singular mass matrix / Schur complement surfaces as forward_error
     ex.run([&](int i) {
       if (i < nj) a[i] = NAN;
     });
   ex.run([&](int i) {
+    if (i == 64 && nc > 0 && !imp) {  // the contact-force terms, in record order
+      double add = 0.;
+      const double* cr = b.C;
+      for (int k = 0; k < b.ncost; ++k) {
+        const CRec C{cr};
+        if (force_cost(C.type())) add += cv[k];
+        cr += C.size();
+      }
+      red[0] += add;
+    }
     if (i >= nj) return;
     if (imp) {  // impulse-fwddyn.hxx:80-81: xnext = (q, v+)
       xnext[nq + i] = nc > 0 ? a[i] : x[nq + i];
@@ -2175,6 +2188,7 @@ MB_HD __forceinline__ double knot_calc_x(const X& ex, const double* P, int nx, c
       if (i == nj - 1 && b.ff) xnext[nq - 1] = x[nq - 1];
     }
   });
+  const double cc = red[0];
   (void)nx;
   return dt != 0. ? dt * cc : cc;
 }
