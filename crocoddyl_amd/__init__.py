@@ -18,5 +18,6 @@ from .models import (ActionData, ActionDataAbstract, ActionModelAbstract, Action
                      StateVector)
 from .problem import ShootingProblem, SolverBoxFDDP, SolverFDDP, pack_problem  # noqa: F401
 from .boxqp import BoxQP, BoxQPSolution  # noqa: F401
+from .callbacks import CallbackAbstract, CallbackLogger, CallbackVerbose, VerboseLevel  # noqa: F401
 
 __version__ = "0.1.0"

@@ -57,6 +57,9 @@ D = C.POINTER(C.c_double)
 I32 = C.POINTER(C.c_int32)
 U64 = C.POINTER(C.c_uint64)
 
+# fddp_iteration_callback(void* user, int iter, const fddp_result* results, const int32_t* reported, int B)
+IterationCallback = C.CFUNCTYPE(None, C.c_void_p, C.c_int, C.POINTER(Result), I32, C.c_int)
+
 # name -> (restype, argtypes); `h` is an opaque handle pointer
 PROTOS = {
     "default_params": (None, [C.POINTER(Params)]),
@@ -100,6 +103,7 @@ PROTOS_GPU = {
     "set_timing": (C.c_int, [P, C.c_int]),
     "device_bytes": (C.c_int64, [P]),
     "get_solver_kind": (C.c_int, [P, I32]),
+    "set_callback": (C.c_int, [P, IterationCallback, C.c_void_p]),
     "boxqp_default_params": (None, [C.POINTER(BoxQPParams)]),
     "boxqp_solve": (C.c_int, [C.c_int, C.c_int, C.c_int, D, D, D, D, D, C.POINTER(BoxQPParams), D, U64, U64, D, I32]),
 }

@@ -319,6 +319,9 @@ struct fddp_handle_s {
   size_t mb_diff_smem = 0; // its dynamic LDS
   int mb_nj = 0;            // largest multibody tree (dofs)
   int bwd_variant = 0;  // 0 generic, else (NTL*10+MTL)*10+waves of the MFMA sweep
+  fddp_iteration_callback cb = nullptr;  // per-iteration callback (fddp_set_callback)
+  void* cb_user = nullptr;
+  bool in_solve = false;
   // timing
   bool timing = false;
   std::vector<hipEvent_t> ev_pool;
@@ -1199,6 +1202,7 @@ int fddp_set_candidate_device(fddp_handle* h, const double* xs, const double* us
 
 int fddp_solve(fddp_handle* h, int maxiter, int is_feasible, double reg_init, fddp_result* out) {
   if (!h) return fail(FDDP_ERR_INVALID_ARG, "fddp_solve: null handle");
+  if (h->in_solve) return fail(FDDP_ERR_INVALID_ARG, "fddp_solve: called from its own iteration callback");
   if (maxiter < 0) return fail(FDDP_ERR_INVALID_ARG, "fddp_solve: maxiter < 0");
   DeviceGuard g(h->device);
   static const bool box_stats = getenv("FDDP_BOX_STATS") && atoi(getenv("FDDP_BOX_STATS")) == 1;
@@ -1213,6 +1217,15 @@ int fddp_solve(fddp_handle* h, int maxiter, int is_feasible, double reg_init, fd
                      xreg0);
   LAUNCH_CHECK();
   int rc;
+  // per-iteration callbacks (fddp.cpp:92-98): the states read back after every body
+  std::vector<ElemState> cbst;
+  std::vector<fddp_result> cbres;
+  std::vector<int32_t> cbrep, cbrun(h->cb ? D.B : 0, 0);
+  struct InSolve {
+    bool& f;
+    explicit InSolve(bool& f_) : f(f_) { f = true; }
+    ~InSolve() { f = false; }
+  } in_solve(h->in_solve);
   for (int it = 0; it < maxiter; ++it) {
     if (it == 0) {
       if ((rc = launch_calc_then_diff(h, SEL_ACTIVE, SEL_ACTIVE, SEL_RECALC, 1))) return rc;
@@ -1222,6 +1235,22 @@ int fddp_solve(fddp_handle* h, int maxiter, int is_feasible, double reg_init, fd
     if ((rc = launch_backward(h, 0))) return rc;
     HIP_TRY(hipMemsetAsync(h->d_count, 0, sizeof(int), h->stream));
     if ((rc = launch_forward(h, 0, 1., h->d_count))) return rc;
+    if (h->cb) {
+      // reported: ran this body (n_iter_run advanced) and did not abort at regmax in it
+      if ((rc = download_states(h, cbst))) return rc;
+      cbres.resize(D.B);
+      cbrep.assign(D.B, 0);
+      int any = 0;
+      for (int b = 0; b < D.B; ++b) {
+        fill_result(cbst[b], &cbres[b]);
+        cbres[b].iter = it;
+        cbrep[b] = (cbst[b].n_iter_run > cbrun[b] && cbst[b].status != FDDP_STATUS_REGMAX) ? 1 : 0;
+        cbrun[b] = cbst[b].n_iter_run;
+        any |= cbrep[b];
+      }
+      if (any) h->cb(h->cb_user, it, cbres.data(), cbrep.data(), D.B);
+      (void)hipSetDevice(h->device);  // (the callback may have switched devices)
+    }
     if (it + 1 < maxiter) {
       HIP_TRY(hipMemcpyAsync(h->h_count, h->d_count, sizeof(int), hipMemcpyDeviceToHost, h->stream));
       HIP_TRY(hipStreamSynchronize(h->stream));
@@ -1242,6 +1271,14 @@ int fddp_solve(fddp_handle* h, int maxiter, int is_feasible, double reg_init, fd
     fprintf(stderr, "fddp box stats: %llu QPs, %.3f Newton iterations and %.3f inverses per QP\n", bs[0],
             bs[0] ? (double)bs[1] / bs[0] : 0., bs[0] ? (double)bs[2] / bs[0] : 0.);
   }
+  return FDDP_OK;
+}
+
+int fddp_set_callback(fddp_handle* h, fddp_iteration_callback cb, void* user) {
+  if (!h) return fail(FDDP_ERR_INVALID_ARG, "fddp_set_callback: null handle");
+  if (h->in_solve) return fail(FDDP_ERR_INVALID_ARG, "fddp_set_callback: not from inside a callback");
+  h->cb = cb;
+  h->cb_user = cb ? user : nullptr;
   return FDDP_OK;
 }
 

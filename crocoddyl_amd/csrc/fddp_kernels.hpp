@@ -860,6 +860,10 @@ __device__ __forceinline__ bool ls_accept(const Prm& prm, ElemState& s, double a
 // convergence / abort test (fddp.cpp:92-103).
 __device__ __forceinline__ void ls_finish(const Prm& prm, ElemState& s, bool accepted) {
   s.recalc = accepted ? 1 : 0;
+  // an accepted trial became xs_ (setCandidate(xs_try_, ...)), so a later
+  // expectedImprovement() (e.g. CallbackLogger's) sees diff(xs_try, xs) = 0; d_ keeps
+  // the accepted trial's value (fddp.cpp:107-124)
+  if (accepted) s.dv = 0.;
   bool abort = false;
   if (s.steplength > prm.th_stepdec) {
     s.xreg /= prm.regfactor;

@@ -704,11 +704,21 @@ __device__ __forceinline__ bool gj_mfma(double* A_, int nr, int ld, int nc, bool
 #pragma unroll
           for (int q = 0; q < 4; ++q) apc[q] = __shfl(d[q], p + 16 * lk);
           bad = bad || !(app > 0.);
-          // 1 / app: v_rcp_f64 and one Newton step (the pivot chain is latency-bound:
-          // 35 cycles per dependent f64 op; without the IEEE division's special-case
-          // scaling, app > 0 is all that is used)
+          // 1 / app from v_rcp_f64 (relative error up to ~2^-23) corrected to working
+          // precision in three dependent fmas: with e = 1 - app x0, x0 (1 + e + e^2) has
+          // relative error e^3 (one Newton step leaves e^2 ~ 1e-14, which the contact
+          // KKT's conditioning, ~1e7, turned into 1e-7 trajectory errors). The pivot chain
+          // is latency-bound (35 cycles per dependent f64 op), so not the IEEE division's
+          // special-case scaling: app > 0 is all that is used.
           double ip = __builtin_amdgcn_rcp(app);
+#ifdef MB_GJ_RCP_FAST
           ip = __builtin_fma(ip, __builtin_fma(-app, ip, 1.), ip);
+#else
+          {
+            const double e = __builtin_fma(-app, ip, 1.);
+            ip = __builtin_fma(ip, __builtin_fma(e, e, e), ip);
+          }
+#endif
           const double t = aip * ip;
           // row p: a_pc ip; the others: a_ic - t a_pc (one fma with per-lane factors);
           // column p (register pq of the lanes with lk == pg): t, the pivot itself -ip

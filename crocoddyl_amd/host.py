@@ -181,6 +181,13 @@ class HostSolverFDDP:
     def setCallbacks(self, callbacks):
         self.callbacks = list(callbacks)
 
+    def getCallbacks(self):
+        return list(self.callbacks)
+
+    # the reference's Python names of xreg_ / ureg_ (core/solver-base.cpp:100-126)
+    x_reg = property(lambda s: s.xreg, lambda s, v: setattr(s, "xreg", float(v)))
+    u_reg = property(lambda s: s.ureg, lambda s, v: setattr(s, "ureg", float(v)))
+
     # -- ddp.cpp -------------------------------------------------------------------
     def _increase_reg(self):
         self.xreg = min(self.xreg * self.regfactor, self.regmax)

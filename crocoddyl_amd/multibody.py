@@ -27,6 +27,7 @@ indices follow Pinocchio's (joint 0 / frame 0 = universe).
 import numpy as np
 
 from . import _abi
+from .models import _ControlLimits
 
 JOINT_REC = 27
 JOINT_REVOLUTE, JOINT_FREEFLYER = 0, 1
@@ -224,12 +225,25 @@ class RobotModel:
 
     @property
     def effortLimit(self):
-        """Model::effortLimit (nv; +inf where unset, as on the free-flyer's dofs)."""
+        """Model::effortLimit (nv; +inf where unset, as on the free-flyer's dofs). A copy,
+        as pinocchio's Python binding returns; write it back with the setter
+        (examples/bipedal_walk_ubound.py:16-18: lims = model.effortLimit; lims *= 0.5;
+        model.effortLimit = lims)."""
         out = np.full(self.nv, np.inf)
         for j, e in self._effort.items():
             if self.kinds[j] != JOINT_FREEFLYER:
                 out[self.idx_v(j)] = e
         return out
+
+    @effortLimit.setter
+    def effortLimit(self, lims):
+        lims = np.array(lims, np.float64).reshape(-1)
+        if lims.size != self.nv:
+            raise ValueError(f"Invalid argument: effortLimit has wrong dimension (it should be {self.nv})")
+        for j in range(1, self.njoints):
+            if self.kinds[j] != JOINT_FREEFLYER:
+                self._effort[j] = float(lims[self.idx_v(j)])
+        self._version += 1
 
     def _qlim(self, k, default):
         out = np.full(self.nq, default)
@@ -1109,7 +1123,7 @@ class CostModelSum:
         return recs
 
 
-class DifferentialActionModelFreeFwdDynamics:
+class DifferentialActionModelFreeFwdDynamics(_ControlLimits):
     """free-fwddyn.hxx:24-160: a = ABA(q, v, tau(u)) (or (M + diag(armature))^-1
     (tau - nle) once an armature is set), cost = costs.calc(x, u)."""
 
@@ -1137,11 +1151,7 @@ class DifferentialActionModelFreeFwdDynamics:
         self.nr = costs.nr
         self._armature = np.zeros(state.nv)
         self._arm_version = 0
-        self._u_lb = np.full(self.nu, -np.inf)
-        self._u_ub = np.full(self.nu, np.inf)
-
-    u_lb = property(lambda s: s._u_lb)
-    u_ub = property(lambda s: s._u_ub)
+        self._init_limits()
 
     @property
     def armature(self):
@@ -1336,6 +1346,10 @@ class DifferentialActionModelContactFwdDynamics(DifferentialActionModelFreeFwdDy
             raise ValueError(f"Invalid argument: Contacts doesn't have the same control dimension "
                              f"(it should be {actuation.nu})")
         self._init_dam(state, actuation, costs)
+        # the control limits start at the robot's torque limits on the actuated dofs
+        # (contact-fwddyn.hxx:51-52: set_u_lb(-effortLimit.tail(nu)), set_u_ub(+...))
+        lim = state.pinocchio.effortLimit[state.nv - self.nu:]
+        self.u_lb, self.u_ub = -lim, lim.copy()
         self.contacts = contacts
         self.JMinvJt_damping = abs(float(inv_damping))
         self.enable_force = bool(enable_force)

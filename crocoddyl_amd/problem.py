@@ -452,6 +452,8 @@ class SolverFDDP:
         self._prm = default_params()
         self._results = None
         self.callbacks = []
+        self.callbackMask = None
+        self._cb_error = None
 
     # -- helpers -----------------------------------------------------------
     @property
@@ -503,14 +505,46 @@ class SolverFDDP:
         self._push_params()
         reg = float("nan") if regInit is None else float(regInit)
         r = (_abi.Result * self.problem.B)()
-        check(lib().fddp_solve(self._ptr, int(maxiter), 1 if isFeasible else 0, reg, r))
+        ptr = self._ptr
+        if self.callbacks:
+            # every callback once per iteration of the loop (fddp.cpp:92-98), with the
+            # solver's getters reading that iteration's state
+            B = self.problem.B
+
+            def on_iter(_user, it, res, reported, _B):
+                snap = (_abi.Result * B)()
+                C.memmove(snap, res, C.sizeof(snap))
+                self._results = snap
+                self.callbackMask = np.ctypeslib.as_array(reported, (B,)).astype(bool)
+                if not self.problem.batched and not self.callbackMask[0]:
+                    return
+                try:
+                    for cb in self.callbacks:
+                        cb(self)
+                except BaseException as e:  # re-raised after fddp_solve returns
+                    self._cb_error = self._cb_error or e
+
+            self._cb_error = None
+            cfn = _abi.IterationCallback(on_iter)
+            check(lib().fddp_set_callback(ptr, cfn, None))
+            try:
+                check(lib().fddp_solve(ptr, int(maxiter), 1 if isFeasible else 0, reg, r))
+            finally:
+                check(lib().fddp_set_callback(ptr, _abi.IterationCallback(), None))
+                self.callbackMask = None
+            if self._cb_error is not None:
+                raise self._cb_error
+        else:
+            check(lib().fddp_solve(ptr, int(maxiter), 1 if isFeasible else 0, reg, r))
         self._results = r
         ok = np.array([x.status == _abi.STATUS_CONVERGED for x in r])
-        for cb in self.callbacks:
-            cb(self)
         return ok if self.problem.batched else bool(ok[0])
 
     def setCallbacks(self, callbacks):
+        """SolverAbstract::setCallbacks (solver-base.cpp:69-73): each callback is called
+        as cb(solver) once per iteration of solve(), after the regularisation update and
+        stoppingCriteria (fddp.cpp:92-98). When batched, the getters return the whole
+        batch and ``solver.callbackMask`` marks the elements that ran that iteration."""
         self.callbacks = list(callbacks)
 
     def getCallbacks(self):

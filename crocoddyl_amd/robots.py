@@ -77,9 +77,10 @@ def sample_talos():
         ("_1_joint", _Y, (0.0, 0.0, 0.4), 0.66, (0.0, 0.0, 0.02), (0.001, 0.001, 0.001)),
         ("_2_joint", _Z, (0.0, 0.0, 0.0), 1.16, (0.02, 0.0, 0.09), (0.006, 0.006, 0.005)),
     ], "head")
-    # effort limits (N m) of the Talos actuator classes, as the talos URDF's <limit effort>
-    # gives them (approximate: the URDF is not in this image); hips / knee / ankles,
-    # torso, shoulder / elbow / wrist, gripper, neck
+    # effort limits (N m) of the Talos actuator classes, standing in for the talos URDF's
+    # <limit effort> (approximate and PARITY UNPINNED: the URDF is not in this image, so
+    # box-limited workloads on these limits are not bipedal_walk_ubound.py parity);
+    # hips / knee / ankles, torso, shoulder / elbow / wrist, gripper, neck
     effort = {"leg_%s_1_joint": 100.0, "leg_%s_2_joint": 160.0, "leg_%s_3_joint": 160.0, "leg_%s_4_joint": 300.0,
               "leg_%s_5_joint": 160.0, "leg_%s_6_joint": 100.0, "arm_%s_1_joint": 44.64, "arm_%s_2_joint": 22.32,
               "arm_%s_3_joint": 22.32, "arm_%s_4_joint": 22.32, "arm_%s_5_joint": 3.0, "arm_%s_6_joint": 3.0,

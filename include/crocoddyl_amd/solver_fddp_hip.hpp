@@ -20,6 +20,7 @@
 #define CROCODDYL_AMD_SOLVER_FDDP_HIP_HPP_
 
 #include <cmath>
+#include <cstdio>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -248,6 +249,18 @@ class ShootingProblem {
   int nx_, ndx_, nu_max_, B_;
 };
 
+class SolverFDDP;
+
+// CallbackAbstract (solver-base.hpp:284-298): called once per iteration of solve(),
+// after the regularisation update and stoppingCriteria (fddp.cpp:92-98), with the
+// solver's getters reading that iteration's state (element 0 when batched;
+// get_results() / reported() give every element).
+class CallbackAbstract {
+ public:
+  virtual ~CallbackAbstract() {}
+  virtual void operator()(SolverFDDP& solver) = 0;
+};
+
 // SolverFDDP (fddp.hpp:50-101) on the GPU.
 class SolverFDDP {
  public:
@@ -281,9 +294,22 @@ class SolverFDDP {
     check(fddp_set_control_limits(h_.get(), lim ? lb.data() : nullptr, lim ? ub.data() : nullptr),
           "fddp_set_control_limits");
     check(fddp_set_params(h_.get(), &params_), "fddp_set_params");
-    check(fddp_solve(h_.get(), (int)maxiter, is_feasible ? 1 : 0, reginit, res_.data()), "fddp_solve");
+    check(fddp_set_callback(h_.get(), callbacks_.empty() ? nullptr : &SolverFDDP::on_iteration, this),
+          "fddp_set_callback");
+    cb_error_.clear();
+    const int rc = fddp_solve(h_.get(), (int)maxiter, is_feasible ? 1 : 0, reginit, res_.data());
+    fddp_set_callback(h_.get(), nullptr, nullptr);
+    reported_.clear();
+    check(rc, "fddp_solve");
+    if (!cb_error_.empty()) throw Exception("callback: " + cb_error_);
     return res_[0].status == FDDP_STATUS_CONVERGED;
   }
+
+  // SolverAbstract::setCallbacks / getCallbacks (solver-base.cpp:69-77)
+  void setCallbacks(const std::vector<std::shared_ptr<CallbackAbstract> >& callbacks) { callbacks_ = callbacks; }
+  const std::vector<std::shared_ptr<CallbackAbstract> >& getCallbacks() const { return callbacks_; }
+  // inside a callback: which elements ran the current iteration
+  const std::vector<int32_t>& reported() const { return reported_; }
 
   template <class V>
   void setCandidate(const std::vector<V>& xs_warm, const std::vector<V>& us_warm, bool is_feasible) {
@@ -331,6 +357,9 @@ class SolverFDDP {
   double get_ureg() const { return res_[0].ureg; }
   double get_steplength() const { return res_[0].steplength; }
   bool get_is_feasible() const { return res_[0].is_feasible != 0; }
+  double get_dV() const { return res_[0].dV; }
+  double get_dVexp() const { return res_[0].dVexp; }
+  std::vector<double> get_d() const { return {res_[0].d0, res_[0].d1}; }
 
   // thresholds with the reference setter validation (enforced by fddp_set_params)
   void set_th_stop(double v) { params_.th_stop = v; push(); }
@@ -358,6 +387,46 @@ class SolverFDDP {
   fddp_dims dims_;
   fddp_params params_;
   std::vector<fddp_result> res_;
+  std::vector<std::shared_ptr<CallbackAbstract> > callbacks_;
+  std::vector<int32_t> reported_;
+  std::string cb_error_;
+
+ private:
+  // fddp_iteration_callback: the C ABI calls it between iterations; no exception may
+  // cross the ABI, so one is kept and rethrown after fddp_solve returns
+  static void on_iteration(void* user, int, const fddp_result* results, const int32_t* reported, int B) {
+    SolverFDDP* self = static_cast<SolverFDDP*>(user);
+    if (!self->cb_error_.empty()) return;
+    self->res_.assign(results, results + B);
+    self->reported_.assign(reported, reported + B);
+    if (self->dims_.B == 1 && !reported[0]) return;
+    try {
+      for (const auto& cb : self->callbacks_) (*cb)(*self);
+    } catch (const std::exception& e) {
+      self->cb_error_ = e.what();
+    }
+  }
+};
+
+// CallbackVerbose (core/utils/callbacks.cpp:13-67): one table row per iteration,
+// a header every 10 iterations; level 2 adds dV-exp and dV.
+class CallbackVerbose : public CallbackAbstract {
+ public:
+  explicit CallbackVerbose(int level = 1, FILE* out = stdout) : level_(level), out_(out) {}
+  void operator()(SolverFDDP& s) override {
+    if (s.get_iter() % 10 == 0)
+      std::fprintf(out_, "iter \t cost \t      stop \t    grad \t  xreg \t      ureg \t step \t feas%s\n",
+                   level_ == 2 ? " \tdV-exp \t      dV" : "");
+    const fddp_result& r = s.get_results()[0];
+    std::fprintf(out_, "%4zu  %.5e  %.5e  %.5e  %.5e  %.5e   %.4f     %d", s.get_iter(), r.cost, r.stop, -r.d1, r.xreg,
+                 r.ureg, r.steplength, r.is_feasible ? 1 : 0);
+    if (level_ == 2) std::fprintf(out_, "  %.5e  %.5e", r.dVexp, r.dV);
+    std::fprintf(out_, "\n");
+  }
+
+ private:
+  int level_;
+  FILE* out_;
 };
 
 // SolverBoxFDDP (box-fddp.cpp:15-164): box-QP gains on limited knots once

@@ -232,6 +232,22 @@ int fddp_set_candidate_device(fddp_handle* h, const double* xs, const double* us
  * returns after the results are on the host. */
 int fddp_solve(fddp_handle* h, int maxiter, int is_feasible, double reg_init, fddp_result* out);
 
+/* Per-iteration callback of fddp_solve: the reference calls every
+ * CallbackAbstract once per loop body, after the regularisation update and
+ * stoppingCriteria and before the convergence test (fddp.cpp:92-98; an element
+ * that aborts at regmax returns before it, fddp.cpp:41-43,88-90). `iter` is the
+ * loop counter iter_ of that body; `results` the B elements' state at that point
+ * (results[b].iter == iter for the reported ones); reported[b] != 0 for the
+ * elements whose callbacks the reference would call in this body (the others
+ * have converged or aborted earlier, or aborted in it). Runs on the calling
+ * thread, between iterations (the device is idle): the callback may call the
+ * getters and the step API of the same handle, not fddp_solve. Setting a
+ * callback makes fddp_solve read the states back once per iteration. */
+typedef void (*fddp_iteration_callback)(void* user, int iter, const fddp_result* results, const int32_t* reported,
+                                        int B);
+/* NULL clears it. Replaces SolverAbstract::setCallbacks (solver-base.cpp:69-73). */
+int fddp_set_callback(fddp_handle* h, fddp_iteration_callback cb, void* user);
+
 /* Results of the last solve / current solver state per element. */
 int fddp_get_results(fddp_handle* h, fddp_result* out);
 /* xs: B*(T+1)*nx, us: B*T*nu_max. on_device != 0: `out` is a device pointer

@@ -10,6 +10,18 @@
 
 namespace croc = crocoddyl_amd;
 
+// a CallbackLogger-style recorder (bindings/python/crocoddyl/__init__.py:356-381)
+struct Logger : croc::CallbackAbstract {
+  struct Row {
+    std::size_t iter;
+    double cost, stop, step, xreg, grad;
+  };
+  std::vector<Row> rows;
+  void operator()(croc::SolverFDDP& s) override {
+    rows.push_back({s.get_iter(), s.get_cost(), s.get_stop(), s.get_steplength(), s.get_xreg(), -s.get_d()[1]});
+  }
+};
+
 int main(int argc, char** argv) {
   try {
     const int T = 100;
@@ -32,6 +44,14 @@ int main(int argc, char** argv) {
     const auto xs = usolver.get_xs();
     std::printf("unicycle converged=%d iter=%zu cost=%.12e xT=(%.3e %.3e %.3e)\n", uok, usolver.get_iter(),
                 usolver.get_cost(), xs.back()[0], xs.back()[1], xs.back()[2]);
+    // per-iteration callbacks (fddp.cpp:92-98): a logger and CallbackVerbose (to stderr)
+    auto logger = std::make_shared<Logger>();
+    croc::SolverFDDP lsolver(uprob);
+    lsolver.setCallbacks({logger, std::make_shared<croc::CallbackVerbose>(2, stderr)});
+    lsolver.solve();
+    for (const auto& r : logger->rows)
+      std::printf("trace%zu cost=%.17e stop=%.17e step=%.17e xreg=%.17e grad=%.17e\n", r.iter, r.cost, r.stop, r.step,
+                  r.xreg, r.grad);
     // control-limited LQR with SolverBoxFDDP (box-fddp.cpp)
     auto bmodel = std::make_shared<croc::ActionModelLQR>(24, 12, false);
     bmodel->set_u_lb(croc::VectorXd(12, -0.05));

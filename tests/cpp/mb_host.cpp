@@ -28,3 +28,20 @@ void mb_host_calc_diff(const double* P, int nx, int m, const double* x, const do
   knot_calc_diff_x(HostExec{e ? std::atoi(e) : kMbDiffNT}, P, nx, m, x, u, use_u != 0, w.data(), Fx, Fu, Lxx, Lxu, Luu, Lx, Lu, xnext, cost);
 }
 }
+
+extern "C" {
+// The calcDiff LDS plan of a knot block (doubles): the DiffLayout offsets in field
+// order, then total, nj, njac, nc, nrows, vcols.
+int mb_host_layout(const double* P, double* out) {
+  const Blk b = parse(P);
+  bool vc = false;
+  const int njac = count_jac_costs(b, &vc);
+  const int nu = b.nj - b.nun;
+  const int nrows = count_cost_rows(b, nu);
+  const DiffLayout l = diff_layout(b.nj, njac, b.nc, vc, nu, nrows);
+  const int64_t f[] = {l.wv, l.A, l.dtau, l.da, l.qp, l.vec, l.J, l.red, l.R, l.Jc, l.a0, l.lam, l.Y, l.H,
+                       l.Sx, l.da0, l.fx, l.zv, l.dfx, l.dfu, l.total, b.nj, njac, b.nc, nrows, vc ? 1 : 0};
+  for (int i = 0; i < (int)(sizeof(f) / sizeof(f[0])); ++i) out[i] = (double)f[i];
+  return (int)(sizeof(f) / sizeof(f[0]));
+}
+}

@@ -48,6 +48,21 @@ def test_facade_solves_on_gpu(tmp_path):
         cost = float(lines[key].split("cost=")[1].split()[0])
         assert abs(cost - r0.cost) <= 1e-6 * max(1, abs(r0.cost))
         assert f"iter={r0.iter}" in lines[key]
+    # per-iteration callbacks: the logger's rows == the oracle's per-iteration trace of
+    # the unicycle solve (cost, stop, steplength, xreg, grad = -d[1]), CallbackVerbose on stderr
+    model = ActionModelUnicycle()
+    knots, pool = pack_problem([model] * 30, model, 1)
+    o = oracle_lib.Oracle(_abi.Dims(3, 3, 2, 30, 1), knots, pool, np.array([[-1.0, -1.0, 1.0]]))
+    o.set_candidate(None, None, False)
+    o.solve(100)
+    tr = o.trace(0)
+    rows = [lines[f"trace{i}"] for i in range(len(tr))]
+    assert f"trace{len(tr)}" not in lines
+    for rec, row in zip(tr, rows):
+        got = {kv.split("=")[0]: float(kv.split("=")[1]) for kv in row.split()}
+        for key, want in (("cost", rec[0]), ("stop", rec[1]), ("step", rec[6]), ("xreg", rec[4]), ("grad", -rec[3])):
+            assert abs(got[key] - want) <= 1e-9 * max(1.0, abs(want)), (key, got[key], want)
+    assert r.stderr.count("iter") >= 1 and "dV-exp" in r.stderr
     # SolverBoxFDDP on the limited LQR
     assert "converged=1" in lines["box"] and "th_stop=5.0e-05" in lines["box"]
     model = ActionModelLQR(24, 12, False)

@@ -206,3 +206,20 @@ def test_mixed_horizon_matches_oracle_and_device_solve():
     assert full.solve([], [], 100)
     assert full.iter == solver.iter
     np.testing.assert_allclose(np.array(full.xs), np.array(solver.xs), atol=1e-9)
+
+
+def test_host_solver_callbacks_per_iteration():
+    """CallbackLogger / CallbackVerbose on the host path (Python-defined models): one
+    record per iteration (fddp.cpp:92-98), the last equal to the solve's final state."""
+    import io
+    m = UnicycleModelDerived()
+    problem = cr.ShootingProblem(np.array([-1.0, -1.0, 1.0]), [m] * 20, m)
+    solver = cr.SolverFDDP(problem)
+    log = cr.CallbackLogger()
+    buf = io.StringIO()
+    solver.setCallbacks([log, cr.CallbackVerbose(stream=buf)])
+    assert solver.solve([], [], 50)
+    assert log.iters == list(range(solver.iter + 1))
+    assert log.costs[-1] == solver.cost and log.x_regs[-1] == solver.x_reg
+    assert all(np.isfinite(log.grads)) and len(log.fs) == len(log.iters)
+    assert buf.getvalue().count("\n") == len(log.iters) + (len(log.iters) + 9) // 10
