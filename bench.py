@@ -91,7 +91,8 @@ def box_limits(config, nu):
 
 
 def box_text(config):
-    return ("u within the Talos effortLimit (bipedal_walk_ubound.py)" if config.startswith("C5")
+    return ("u within the code-built Talos effortLimit (the bipedal_walk_ubound.py pattern; limits parity unpinned)"
+            if config.startswith("C5")
             else f"|u| <= {BOX_LIMIT}")
 
 
@@ -160,7 +161,7 @@ def _cpu_baseline_child(cfg, T, seed, target_s, box, protocol):
 
     kind = synthetic.CONFIGS[cfg][0]
 
-    def run(Bs, steps, mode=2):
+    def make(Bs, mode=2):
         S = helpers.setup(cfg, T=T, B=Bs, seed=seed)
         d = S["dims"]
         o = oracle_lib.Oracle(S["dims"], S["knots"], S["pool"], S["x0s"], threads=threads, mode=mode)
@@ -174,24 +175,29 @@ def _cpu_baseline_child(cfg, T, seed, target_s, box, protocol):
             o.set_params(p)
         xs_w, us_w = warm_start_arrays(cfg, S["running"], S["x0s"], d)
         o.set_candidate(xs_w, us_w, False)
-        knots = list(S["knots"])
-        iters = 1
+        st = {"o": o, "knots": list(S["knots"]), "xs": xs_w, "us": us_w, "B": Bs}
         if protocol == "shift":
             o.solve(maxiter=5)
         if protocol == "feasible":
             o.solve(maxiter=BOX_PRESOLVE, reg_init=0.1)
-            xs_w, us_w = o.xs(), o.us()
+            st["xs"], st["us"] = o.xs(), o.us()
+        o.phase_times(reset=True)
+        return st
+
+    def timed(st, steps):
+        """element-iterations and seconds of `steps` benchmark steps (CLOCK_MONOTONIC)."""
+        o = st["o"]
         t0 = time.perf_counter()
         it = 0
         for _ in range(steps):
             if protocol == "shift":
-                knots = knots[1:T] + knots[:1] + knots[T:]
-                kd = (_abi.KnotDesc * len(knots))(*[_abi.KnotDesc(*k) for k in knots])
+                st["knots"] = st["knots"][1:T] + st["knots"][:1] + st["knots"][T:]
+                kd = (_abi.KnotDesc * len(st["knots"]))(*[_abi.KnotDesc(*k) for k in st["knots"]])
                 o.L.oracle_set_knots(o.h, kd, _abi.dptr(o.pool), o.pool.size)
                 o.mpc_shift()
             else:
-                o.set_candidate(xs_w, us_w, protocol == "feasible")
-            r = o.solve(maxiter=iters, is_feasible=protocol == "feasible", reg_init=0.1)
+                o.set_candidate(st["xs"], st["us"], protocol == "feasible")
+            r = o.solve(maxiter=1, is_feasible=protocol == "feasible", reg_init=0.1)
             it += sum(x.n_iter_run for x in r)
         return it, time.perf_counter() - t0
 
@@ -201,29 +207,49 @@ def _cpu_baseline_child(cfg, T, seed, target_s, box, protocol):
             cpu_model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), "")
     except OSError:
         pass
-    # batch-parallel (OpenMP over elements): the main figure
-    it, dt = run(threads, 1)
-    steps = 4
-    Bs = int(max(threads, min(1024, target_s * (it / max(dt, 1e-9)) / steps)))
+    # batch-parallel (OpenMP over elements): the main figure. A calibration solve sizes
+    # the batch so one repeat of `steps` steps takes ~target_s / (reps + 1); one warm-up
+    # repeat, then the median of `reps` timed repeats (median of >= 5)
+    reps, steps = 5, 2
+    cal = make(threads)
+    it, dt = timed(cal, 1)
+    Bs = int(max(threads, min(1024, target_s / (reps + 1) * (it / max(dt, 1e-9)) / steps)))
     Bs = max(threads, (Bs // threads) * threads)
-    it, dt = run(Bs, steps)
+    st = make(Bs)
+    timed(st, 1)  # warm-up
+    st["o"].phase_times(reset=True)
+    runs = [timed(st, steps) for _ in range(reps)]
+    rates = sorted(i / d for i, d in runs)
+    it, dt = sum(i for i, _ in runs), sum(d for _, d in runs)
+    ph = st["o"].phase_times(reset=True)
+    per_knot_us = {k: round(v / max(it, 1) / (T + 1) * 1e6, 3) for k, v in ph.items()}
     # reference-faithful (WITH_MULTITHREADING: OpenMP over knots inside calc / calcDiff,
-    # shooting.hxx:143-145,176-178; elements one after another) on a third of the budget
-    it1, dt1 = run(1, 1, mode=1)
-    B1 = int(max(1, min(256, target_s / 3 * (it1 / max(dt1, 1e-9)) / steps)))
-    it1, dt1 = run(B1, steps, mode=1)
-    v2, v1 = it / dt, it1 / dt1
+    # shooting.hxx:143-145,176-178; elements one after another): a smaller sample
+    cal1 = make(1, mode=1)
+    it1, dt1 = timed(cal1, 1)
+    B1 = int(max(1, min(256, target_s / 3 / 4 * (it1 / max(dt1, 1e-9)) / steps)))
+    st1 = make(B1, mode=1)
+    timed(st1, 1)
+    runs1 = [timed(st1, steps) for _ in range(3)]
+    rates1 = sorted(i / d for i, d in runs1)
+    v2, v1 = rates[len(rates) // 2], rates1[len(rates1) // 2]
     share = f"affinity {aff} CPUs, cgroup quota {'none' if quota is None else round(quota, 2)}"
     print(json.dumps({"value": max(v1, v2), "unit": "FDDP iterations/s", "cores": threads, "kind": "port",
                       "host_cpus": os.cpu_count(), "affinity_cpus": aff, "cgroup_cpu_quota": quota,
                       "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS"), "cpu_model": cpu_model,
                       "build": f"{flags} -fopenmp",
                       "modes": {"batch_parallel": round(v2, 2), "knot_parallel": round(v1, 2)},
-                      "sample": f"{cfg} T={T}, protocol {protocol}, solve(maxiter=1, reg_init=0.1) "
-                                f"per element per step: batch-parallel {Bs} elements x {steps} steps ({it} "
-                                f"element-iterations in {dt:.1f} s), knot-parallel {B1} elements x {steps} steps "
-                                f"({it1} in {dt1:.1f} s); value = the faster mode. oracle/fddp_oracle.cpp {flags} "
-                                f"-fopenmp, {threads} threads ({share}) of {os.cpu_count()} host CPUs ({cpu_model})"
+                      "repeats_it_per_s": {"batch_parallel": [round(r, 2) for r in rates],
+                                           "knot_parallel": [round(r, 2) for r in rates1]},
+                      "per_knot_thread_us": dict(per_knot_us, note="thread time per knot per FDDP iteration "
+                                                 "(forward: all line-search trials of the iteration), batch-parallel "
+                                                 "mode, summed over threads / (element-iterations x (T+1))"),
+                      "sample": f"{cfg} T={T}, protocol {protocol}, solve(maxiter=1, reg_init=0.1) per element per "
+                                f"step: batch-parallel {Bs} elements, 1 warm-up + {reps} timed repeats of {steps} "
+                                f"steps ({it} element-iterations in {dt:.1f} s; value = the median repeat), "
+                                f"knot-parallel {B1} elements, 1 warm-up + 3 repeats; value = the faster mode's "
+                                f"median. oracle/fddp_oracle.cpp {flags} -fopenmp, {threads} threads ({share}) of "
+                                f"{os.cpu_count()} host CPUs ({cpu_model})"
                                 f"{', SolverBoxFDDP ' + box_text(cfg) if box else ''}"}), flush=True)
 
 
@@ -356,8 +382,10 @@ def main():
     ap.add_argument("--batch", type=int, default=None, help="elements per GPU (default: the config's)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--solver", choices=["fddp", "boxfddp"], default="fddp",
-                    help="boxfddp: SolverBoxFDDP with control limits (C5: half the Talos effort limits), solve(maxiter=2) per MPC step so the "
-                         "box QP runs (iteration 1 is feasible)")
+                    help="boxfddp: SolverBoxFDDP with control limits (C5: the code-built Talos effortLimit on the "
+                         "actuated joints, parity unpinned; elsewhere |u| <= 1); default protocol 'feasible': an untimed "
+                         "solve(maxiter=20, regInit=0.1), then every step solve(xs_f, us_f, 1, isFeasible=true, 0.1) "
+                         "from that iterate, so the box QP runs on every knot")
     ap.add_argument("--protocol", choices=["fixed", "shift", "feasible"], default=None,
                     help="fixed: the reference benchmark's loop, solve(xs, us, 1, false, 0.1) from the same warm "
                          "start every step (bipedal_walk_optctrl.py:36-43); shift: receding horizon, gait knots "
@@ -411,9 +439,12 @@ def main():
     for _ in range(args.steps):
         step()
         iters += int(np.sum(solver.n_iter_run))
+    solver.synchronize()
+    t_solve = time.perf_counter() - t0
     # the solved trajectories and per-element results, device to device, then the
     # all-gathers (RCCL over xGMI): the only collectives of the batched solve
-    xs_all, us_all, res_all = cdist.gather_solution(solver, f"cuda:{dev}")
+    gstats = {}
+    xs_all, us_all, res_all = cdist.gather_solution(solver, f"cuda:{dev}", gstats)
     torch.cuda.synchronize(dev)
     if ws > 1:
         torch.distributed.barrier()
@@ -421,8 +452,19 @@ def main():
     solver.set_timing(False)
     timing = solver.get_timing()
     trials = line_search_trials(solver)  # of the last step
+    rank_elapsed = elapsed
     elapsed, total_iters = cdist.job_time_and_work(elapsed, iters, f"cuda:{dev}")
     assert xs_all.shape[0] == us_all.shape[0] == res_all.shape[0] == ws * B
+    # per-rank diagnostics (outside the timed region): the timed loop's own time, the
+    # gather's time and bytes, the rank's iterations; max/min imbalance per column
+    names = ["elapsed_s", "solve_s", "gather_s", "iterations", "mean_trials_last_step"]
+    rt = cdist.rank_table([rank_elapsed, t_solve, gstats["gather_s"], iters, float(np.mean(trials))], f"cuda:{dev}")
+    ranks = dict(cdist.rank_summary(rt, names), gather_bytes_sent_per_rank=gstats["gather_bytes_sent"],
+                 gather_bytes_received_per_rank=gstats["gather_bytes_received"],
+                 gather_GBps_received=round(gstats["gather_bytes_received"] / max(float(rt[:, 2].max()), 1e-12) / 1e9, 3)
+                 if ws > 1 else None,
+                 note="elapsed_s: this rank's barrier-to-barrier time (the job time is the max); solve_s: the timed "
+                      "solves alone; gather_s: the RCCL all-gathers of xs, us and results (device-synchronised)")
 
     box_bwd = None
     if box and ws == 1 and args.protocol == "feasible":
@@ -481,38 +523,60 @@ def main():
                     "algorithmic_flops_per_launch": F, "algorithmic_bytes_per_launch": Y,
                     "achieved_algorithmic_GBps": round(Y / avg_bwd_s / 1e9, 1),
                     "avg_launch_ms": round(avg_bwd_s * 1e3, 3), "timer": "HIP events on the solver stream"}
-        # the knot kernels: algorithmic HBM bytes (they are latency-bound recursions, far
-        # from either roof; the fraction says how far)
+        if Y / (HBM_PEAK_GBPS * 1e9) > F / (FP64_PEAK_TFLOPS * 1e12):  # the HBM floor binds (F/Y below the ridge)
+            gb = Y / avg_bwd_s / 1e9
+            roof_bwd.update(bound="hbm", achieved=round(gb, 1), peak=HBM_PEAK_GBPS, unit="GB/s",
+                            frac=round(gb / HBM_PEAK_GBPS, 4),
+                            fp64={"achieved": round(achieved, 3), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                                  "frac": round(achieved / FP64_PEAK_TFLOPS, 4)})
+        # the knot kernels: algorithmic HBM bytes and FP64 flops (crocoddyl_amd/opcount.py,
+        # the reference op sequence); the binding roof is the one with the larger time floor
         psz = mean_param_doubles(problem)
         rooflines = {"backward": (bwd_ms, roof_bwd)}
+        kfl = None
+        if kind in ("gait_biped", "gait_quadruped", "multibody", "multibody_contact"):
+            from crocoddyl_amd import opcount
+            kfl = opcount.horizon_flops(problem.runningModels, problem.terminalModel)
+        kpm = (pmc or {}).get("kernels", {})
+
+        def knot_roof(name, ms, n_launch, Y, F, traffic, extra):
+            t = ms / n_launch / 1e3
+            hb = Y / t / 1e9
+            r = {"kernel": name, "bound": "hbm", "achieved": round(hb, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                 "frac": round(hb / HBM_PEAK_GBPS, 5), "traffic": traffic, "algorithmic_bytes_per_launch": int(Y)}
+            if F:
+                fl = F / t / 1e12
+                r["fp64"] = {"achieved": round(fl, 3), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                             "frac": round(fl / FP64_PEAK_TFLOPS, 5), "algorithmic_flops_per_launch": int(F),
+                             "flop_model": "crocoddyl_amd/opcount.py (reference op sequence, spatial-algebra costs)"}
+                if F / (FP64_PEAK_TFLOPS * 1e12) > Y / (HBM_PEAK_GBPS * 1e9):  # FP64 floor binds
+                    hb_roof = {k: r[k] for k in ("achieved", "peak", "unit", "frac")}
+                    r.update(bound="fp64", achieved=r["fp64"]["achieved"], peak=FP64_PEAK_TFLOPS, unit="TFLOP/s",
+                             frac=r["fp64"]["frac"], hbm=hb_roof)
+            r.update(extra, avg_launch_ms=round(ms / n_launch, 3), timer="HIP events on the solver stream")
+            return r
+
         fw_ms, fw_n = timing["forward"]
-        fwd_pmc = ((pmc or {}).get("kernels", {}).get("forward") or None)
-        n_alphas = 10  # the reference's default alphas (solver-base.cpp: 2^-k, k < 10)
-        nv = n // 2
-        ls_par = int(os.environ.get("CROCODDYL_AMD_LS_PAR", "0")) or (4 if nv >= 24 else 1)
         if fw_n:
+            g, nl = solver.line_search_info()
             kt = float(np.sum(trials)) * (T + 1)  # knot-trials of one line search (last step's trials)
             Yf = rollout_bytes_per_knot_trial(nx, n, m, psz) * kt
-            a = Yf / (fw_ms / fw_n / 1e3) / 1e9
-            rooflines["forward"] = (fw_ms, {
-                "kernel": "line-search rollout (forward_kernel + ls_select_kernel, knot calc per trial)",
-                "bound": "hbm", "achieved": round(a, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                "frac": round(a / HBM_PEAK_GBPS, 5),
-                # HBM bytes per call: the PMC mean per group dispatch x the group dispatches of
-                # one line search (npar trials per group, as fddp_hip.hip chooses it)
-                "traffic": (fwd_pmc["hbm_bytes_per_launch"] * -(-n_alphas // ls_par) if fwd_pmc else None),
-                "algorithmic_bytes_per_launch": int(Yf),
-                "knot_trials_per_launch": int(kt), "avg_launch_ms": round(fw_ms / fw_n, 3),
-                "timer": "HIP events on the solver stream"})
+            fpm = kpm.get("forward") or {}
+            rooflines["forward"] = (fw_ms, knot_roof(
+                "line-search rollout: forward_kernel" + (f" x {nl} trial groups of {g} + ls_select_kernel"
+                                                         if g > 1 else " (serial line search, one dispatch)"),
+                fw_ms, fw_n, Yf, kfl[0] * kt if kfl else None,
+                # HBM bytes of one line search: every forward dispatch of a timed step (profiles/)
+                fpm.get("hbm_bytes_per_step"),
+                {"knot_trials_per_launch": int(kt), "trial_group_size": g, "dispatches_per_line_search": nl}))
         cd_ms, cd_n = timing["calcDiff"]
         if cd_n:
-            Yc = calc_diff_bytes_per_knot(nx, n, m, psz) * B * (T + 1)
-            a = Yc / (cd_ms / cd_n / 1e3) / 1e9
-            rooflines["calcDiff"] = (cd_ms, {
-                "kernel": "knot-parallel calcDiff (mb_knot_kernel / calc_diff_kernel)", "bound": "hbm",
-                "achieved": round(a, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(a / HBM_PEAK_GBPS, 5),
-                "traffic": ((pmc or {}).get("kernels", {}).get("mb_calc_diff") or {}).get("hbm_bytes_per_launch"), "algorithmic_bytes_per_launch": int(Yc), "avg_launch_ms": round(cd_ms / cd_n, 3),
-                "timer": "HIP events on the solver stream"})
+            nk = B * (T + 1)
+            Yc = calc_diff_bytes_per_knot(nx, n, m, psz) * nk
+            rooflines["calcDiff"] = (cd_ms, knot_roof(
+                "knot-parallel calcDiff (mb_knot_kernel / calc_diff_kernel) + gaps", cd_ms, cd_n, Yc,
+                kfl[1] * nk if kfl else None, (kpm.get("mb_calc_diff") or {}).get("hbm_bytes_per_step"),
+                {"knots_per_launch": nk}))
         dominant = max(rooflines, key=lambda k: rooflines[k][0])
         roof = dict(rooflines[dominant][1], dominant_of=sorted(rooflines))
         cpu = None
@@ -559,6 +623,9 @@ def main():
                        "solver": "SolverBoxFDDP" if box else "SolverFDDP"},
             "mpc_solves_per_s": round(B * ws * args.steps / elapsed, 2),
             "kernel_ms_per_step": {k: round(v[0] / max(args.steps, 1), 3) for k, v in timing.items()},
+            "per_knot_device_us": {k: round(v[0] / max(args.steps, 1) / (B * (T + 1)) * 1e3, 5)
+                                   for k, v in timing.items()},
+            "ranks": ranks,
             "line_search_trials_last_step": trials_summary(trials),
             "secondary_protocol": secondary,
             **({"box_backward": box_bwd} if box_bwd else {}),

@@ -104,6 +104,7 @@ PROTOS_GPU = {
     "device_bytes": (C.c_int64, [P]),
     "get_solver_kind": (C.c_int, [P, I32]),
     "set_callback": (C.c_int, [P, IterationCallback, C.c_void_p]),
+    "get_line_search_info": (C.c_int, [P, I32, I32]),
     "boxqp_default_params": (None, [C.POINTER(BoxQPParams)]),
     "boxqp_solve": (C.c_int, [C.c_int, C.c_int, C.c_int, D, D, D, D, D, C.POINTER(BoxQPParams), D, U64, U64, D, I32]),
 }

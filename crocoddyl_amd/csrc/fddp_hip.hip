@@ -319,6 +319,8 @@ struct fddp_handle_s {
   size_t mb_diff_smem = 0; // its dynamic LDS
   int mb_nj = 0;            // largest multibody tree (dofs)
   int bwd_variant = 0;  // 0 generic, else (NTL*10+MTL)*10+waves of the MFMA sweep
+  int ls_npar_last = 0;      // trial-group size of the last line search (1: serial)
+  int ls_launches_last = 0;  // rollout (forward_kernel) dispatches of the last line search
   fddp_iteration_callback cb = nullptr;  // per-iteration callback (fddp_set_callback)
   void* cb_user = nullptr;
   bool in_solve = false;
@@ -654,6 +656,8 @@ int launch_forward(fddp_handle* h, int mode, double alpha, int* count) {
     int rc;
     if ((rc = ensure_par_slots(h))) return rc;
     const int na = h->prm.n_alphas, G = (na + D.npar - 1) / D.npar;
+    h->ls_npar_last = D.npar;
+    h->ls_launches_last = G;
     for (int g = 0; g < G; ++g) {
       if (mb_rollout(h))
         hipLaunchKernelGGL((forward_kernel<kNT, false, true>), dim3(D.B, D.npar), dim3(kNT), h->fwd_smem, h->stream,
@@ -667,6 +671,10 @@ int launch_forward(fddp_handle* h, int mode, double alpha, int* count) {
       LAUNCH_CHECK();
     }
     return FDDP_OK;
+  }
+  if (mode == 0) {
+    h->ls_npar_last = 1;
+    h->ls_launches_last = 1;
   }
   if (h->fast)
     hipLaunchKernelGGL((forward_kernel<kNT, true>), dim3(D.B), dim3(kNT), h->fwd_fast_smem, h->stream, D,
@@ -1271,6 +1279,13 @@ int fddp_solve(fddp_handle* h, int maxiter, int is_feasible, double reg_init, fd
     fprintf(stderr, "fddp box stats: %llu QPs, %.3f Newton iterations and %.3f inverses per QP\n", bs[0],
             bs[0] ? (double)bs[1] / bs[0] : 0., bs[0] ? (double)bs[2] / bs[0] : 0.);
   }
+  return FDDP_OK;
+}
+
+int fddp_get_line_search_info(fddp_handle* h, int* group_size, int* launches) {
+  if (!h) return fail(FDDP_ERR_INVALID_ARG, "fddp_get_line_search_info: null handle");
+  if (group_size) *group_size = h->ls_npar_last;
+  if (launches) *launches = h->ls_launches_last;
   return FDDP_OK;
 }
 

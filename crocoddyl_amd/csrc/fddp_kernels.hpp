@@ -1009,26 +1009,32 @@ __global__ __launch_bounds__(NT) void ls_select_kernel(Dev D, Prm prm, int group
     }
   }
   if (group * D.npar + D.npar >= prm.n_alphas) exhausted = true;
-  if (acc_slot < 0 && !exhausted) {  // next group
-    if (tid == 0) *st = s;
-    return;
-  }
-  // the accepted slot's trajectories into the (new) current buffer; on an exhausted
-  // search the last trial's into the trial buffer, where the serial search (and the
-  // reference's xs_try_ / us_try_) leaves them
-  const int last_slot = prm.n_alphas - 1 - group * D.npar;
-  const int copy_slot = acc_slot >= 0 ? acc_slot : last_slot;
-  if (copy_slot > 0) {
-    // only the knots the trial wrote: a trial stopped by a forward_error leaves the
-    // rest of the buffer as it was, as in the serial search
-    const TrialOut src(D, 0, copy_slot), dst(D, acc_slot >= 0 ? s.cur : 1 - s.cur, 0);
-    const int64_t K1 = (int64_t)D.ptrial[((int64_t)b * D.npar + copy_slot) * 4 + 3];
+  // copy the knots slot p's trial wrote (a trial stopped by a forward_error leaves the
+  // rest of the buffer as it was, as in the serial search) into trajectory buffer `buf`
+  auto copy_slot = [&](int p, int buf) {
+    const TrialOut src(D, 0, p), dst(D, buf, 0);
+    const int64_t K1 = (int64_t)D.ptrial[((int64_t)b * D.npar + p) * 4 + 3];
     const int64_t K0 = K1 < D.T ? K1 : D.T;
     for (int64_t i = tid; i < K1 * D.sX; i += NT) dst.xs[D.knot(b, 0) * D.sX + i] = src.xs[D.knot(b, 0) * D.sX + i];
     for (int64_t i = tid; i < K0 * D.sM; i += NT) dst.us[D.run(b, 0) * D.sM + i] = src.us[D.run(b, 0) * D.sM + i];
     for (int64_t i = tid; i < K0 * D.sX; i += NT)
       dst.xnext[D.run(b, 0) * D.sX + i] = src.xnext[D.run(b, 0) * D.sX + i];
     for (int64_t i = tid; i < K1; i += NT) dst.kcost[D.knot(b, 0) + i] = src.kcost[D.knot(b, 0) + i];
+  };
+  if (acc_slot < 0) {
+    // no trial of this group accepted: its trials' outputs over the trial buffer in
+    // alpha order (slot 0 wrote it directly), so each knot holds the last trial that
+    // reached it, as the serial search leaves xs_try_ / us_try_ (fddp.cpp:149-225).
+    // A thread copies the same entries for every slot, so the order holds per entry.
+    const int np = prm.n_alphas - group * D.npar < D.npar ? prm.n_alphas - group * D.npar : D.npar;
+    for (int p = 1; p < np; ++p) copy_slot(p, 1 - s.cur);
+    if (!exhausted) {  // next group
+      if (tid == 0) *st = s;
+      return;
+    }
+  } else if (acc_slot > 0) {
+    // the accepted slot's trajectories into the new current buffer (ls_accept flipped cur)
+    copy_slot(acc_slot, s.cur);
   }
   ls_finish(prm, s, acc_slot >= 0);
   if (tid == 0) {

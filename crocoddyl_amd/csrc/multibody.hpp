@@ -36,6 +36,11 @@
 // gauss_jordan) is __host__ __device__, so the same arithmetic is unit-tested
 // on the CPU against the oracle (tests/test_multibody_host.py).
 #define MB_HD __host__ __device__
+#ifndef MB_DUMP
+// (tools/mb_probe: copies an LDS matrix, rows x cols at leading dimension ld, out of
+// the calcDiff for the parity diagnosis; every thread calls it between phases)
+#define MB_DUMP(slot, ptr, rows, cols, ld)
+#endif
 
 // On the device every multibody record (parameter block) and the work area live in
 // LDS; the record / work-area accessors re-assert it where the pointer is formed, so
@@ -1402,17 +1407,72 @@ MB_HD inline void w_joint_force(const Blk& b, const WVals& W, double* tau, int i
 // for the ancestors-or-self i < j of j (+ armature on the diagonal), the rows i < j split
 // in nw contiguous ranges, one per wave (the waves run side by side: the per-lane chain
 // of LDS loads is a quarter as long). A: ld lda, zeroed.
+// The column is formed about the point P = joint j's origin, not the world origin: the
+// subtree's composite inertia is summed from the bodies' offsets c_b - P, and the motion
+// subspaces are shifted to P (S_i at P: [w_i x (P - p_i); w_i], a prismatic dof [w_i; 0]).
+// About the world origin the entries of a light distal link (a gripper, 1e-4 kg m^2, 1 m
+// from the origin) are the difference of terms ~ m |c|^2 ~ 0.3, which cost ~3 digits of
+// M and, through cond(M) ~ 1e6, of M^-1 and Fu (the round-4 parity trace); at P the
+// lever arms are the link's own size.
 MB_HD inline void w_crba_column(const Blk& b, const WVals& W, int j, double* A, int lda, int w = 0, int nw = 1) {
-  double F[6];
-  comp_mul(W, j, W.S(j), F);
-  if (w == 0) A[(int64_t)j * lda + j] = dot6(W.S(j), F) + b.arm[j];
+  double P[3], m = 0., h[3] = {0., 0., 0.}, I[6] = {0., 0., 0., 0., 0., 0.};
+  for (int e = 0; e < 3; ++e) P[e] = W.op(j)[e];
+  // composite of j's subtree about P (every body read, the others weighted 0, as
+  // w_composite; each wave forms the whole sum: the loads are wave-uniform broadcasts)
+#pragma unroll 2
+  for (int k = b.ff ? 5 : 0; k < b.nj; ++k) {
+    const double sel = ((*W.anc(k) >> j) & 1ull) ? 1. : 0.;
+    const double mk = *W.m(k);
+    double c[3], Ic[6];
+    for (int e = 0; e < 3; ++e) c[e] = W.c(k)[e] - P[e];
+    for (int e = 0; e < 6; ++e) Ic[e] = W.Ic(k)[e];
+    const double cc = c[0] * c[0] + c[1] * c[1] + c[2] * c[2];
+    m += sel * mk;
+    for (int e = 0; e < 3; ++e) h[e] += sel * (mk * c[e]);
+    I[0] += sel * (Ic[0] + mk * (cc - c[0] * c[0]));
+    I[1] += sel * (Ic[1] + mk * (cc - c[1] * c[1]));
+    I[2] += sel * (Ic[2] + mk * (cc - c[2] * c[2]));
+    I[3] += sel * (Ic[3] - mk * c[0] * c[1]);
+    I[4] += sel * (Ic[4] - mk * c[0] * c[2]);
+    I[5] += sel * (Ic[5] - mk * c[1] * c[2]);
+  }
+  // S_i shifted to P: a revolute dof's axis w through p_i moves P at w x (P - p_i)
+  auto shifted = [&](int i, double* s) {
+    double wv[3], d[3];
+    const bool pr = dof_prismatic(b, i);
+    for (int e = 0; e < 3; ++e) {
+      wv[e] = W.S(i)[pr ? e : 3 + e];
+      d[e] = P[e] - W.op(i)[e];
+    }
+    if (pr) {
+      for (int e = 0; e < 3; ++e) {
+        s[e] = wv[e];
+        s[3 + e] = 0.;
+      }
+    } else {
+      cross3(wv, d, s);
+      for (int e = 0; e < 3; ++e) s[3 + e] = wv[e];
+    }
+  };
+  double Sj[6], F[6], t[3];
+  shifted(j, Sj);
+  // F = Ic_j S_j about P: (m v - h x w, I w + h x v)
+  cross3(h, Sj + 3, t);
+  for (int e = 0; e < 3; ++e) F[e] = m * Sj[e] - t[e];
+  cross3(h, Sj, t);
+  F[3] = I[0] * Sj[3] + I[3] * Sj[4] + I[4] * Sj[5] + t[0];
+  F[4] = I[3] * Sj[3] + I[1] * Sj[4] + I[5] * Sj[5] + t[1];
+  F[5] = I[4] * Sj[3] + I[5] * Sj[4] + I[2] * Sj[5] + t[2];
+  if (w == 0) A[(int64_t)j * lda + j] = dot6(Sj, F) + b.arm[j];
   const Mask am = *W.anc(j);
   const int ch = (j + nw - 1) / nw, i0 = w * ch, i1 = i0 + ch < j ? i0 + ch : j;
   // every i < j visited, the non-ancestors storing their zero (only lane j writes the
   // pair {i, j}), so the loop has no branch and the unrolled loads overlap
 #pragma unroll 2
   for (int i = i0; i < i1; ++i) {
-    const double d = dot6(W.S(i), F);
+    double Si[6];
+    shifted(i, Si);
+    const double d = dot6(Si, F);
     const double Mij = ((am >> i) & 1ull) ? d : 0.;
     A[(int64_t)j * lda + i] = Mij;
     A[(int64_t)i * lda + j] = Mij;
@@ -2908,6 +2968,12 @@ MB_HD __forceinline__ void knot_calc_diff_x(const X& ex, const double* P, int nx
         contact_a0_drift(b, W, C, a0 + row0);
       }
     });
+  MB_DUMP(0, A, nj, nj, lda);        // M (+ armature)
+  if (!imp) MB_DUMP(1, nle, nj, 1, nj);
+  if (nc > 0) {
+    MB_DUMP(2, Jc, nj, nc, nj);         // Jc^T (nj x nc)
+    MB_DUMP(3, a0, nc, 1, nc);
+  }
   double* pb = red + 8;
   double* Minv;  // column-major nj x nj (ld lda); with contacts: d a / d tau after the Schur step
   // The velocity-product maps of the derivatives (per-body N_b, h_b into the dtau area;
@@ -2939,6 +3005,7 @@ MB_HD __forceinline__ void knot_calc_diff_x(const X& ex, const double* P, int nx
   jac_side = vp > 0 && (ex.nt >> 6) - ((nj + 15) >> 4) >= 2;
   vp = imp ? 0 : (vp < 3 ? vp : 3);
   Minv = ex.lds(Minv);
+  MB_DUMP(4, Minv, nj, nj, lda);
   // z = (M + A)^-1 (tau - nle) (the acceleration without contacts); Y = Minv Jc^T
   ex.run([&](int lane) {
     if (lane < nj && imp) {
@@ -3009,6 +3076,13 @@ MB_HD __forceinline__ void knot_calc_diff_x(const X& ex, const double* P, int nx
         if (imp) zv[lane] = av[lane] - x[nq + lane];  // v+ - v
       }
     });
+  }
+  MB_DUMP(5, Minv, nj, nj, lda);  // Kinv top-left (with contacts)
+  MB_DUMP(6, av, nj, 1, nj);      // a
+  if (nc > 0) {
+    MB_DUMP(7, Y, nj, nc, nj);
+    MB_DUMP(8, Sx + (int64_t)nc * nc, nc, nc, nc);  // S^-1
+    MB_DUMP(9, H, nj, nc, nj);
   }
   // velocities, accelerations and forces at the solved a (the linearisation point
   // of computeABADerivatives / computeRNEADerivatives with fext)

@@ -7,7 +7,9 @@ solved trajectories at the end (RCCL over xGMI on the GPU box: backend
 "nccl"; gloo in the CPU tests).
 """
 import os
+import time
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -54,11 +56,14 @@ def gather_rows(local):
 RESULT_FIELDS = ("status", "iter", "is_feasible", "n_iter_run", "cost", "stop", "steplength")
 
 
-def gather_solution(solver, device):
+def gather_solution(solver, device, stats=None):
     """All-gather every rank's solved shard: (xs (B_all, T+1, nx), us (B_all, T, nu_max),
     results (B_all, len(RESULT_FIELDS))), rows in rank order. The trajectories are
     copied device to device from the solver (no host round trip); with the gloo
-    backend (CPU tests) the collective runs on host copies."""
+    backend (CPU tests) the collective runs on host copies. stats (a dict, optional):
+    receives the collectives' wall time on this rank ("gather_s", device-synchronised)
+    and bytes ("gather_bytes_sent" = this rank's rows, "gather_bytes_received" = the
+    other ranks' rows)."""
     p = solver.problem
     dev = torch.device(device) if not isinstance(device, torch.device) else device
     xs = torch.empty((p.B, p.T + 1, p.nx), dtype=torch.float64, device=dev)
@@ -70,7 +75,39 @@ def gather_solution(solver, device):
     solver.synchronize()
     if dist.is_initialized() and dist.get_backend() == "gloo":
         xs, us, res = xs.cpu(), us.cpu(), res.cpu()
-    return gather_rows(xs), gather_rows(us), gather_rows(res)
+    t0 = time.perf_counter()
+    out = gather_rows(xs), gather_rows(us), gather_rows(res)
+    if out[0].is_cuda:
+        torch.cuda.synchronize(out[0].device)
+    if stats is not None:
+        ws = dist.get_world_size() if dist.is_initialized() else 1
+        nbytes = sum(t.numel() * t.element_size() for t in (xs, us, res))
+        stats.update(gather_s=time.perf_counter() - t0, gather_bytes_sent=int(nbytes),
+                     gather_bytes_received=int(nbytes * (ws - 1)))
+    return out
+
+
+def rank_table(values, device):
+    """All-gather a short per-rank vector of floats: a (world_size, k) numpy array in
+    rank order (one row on a single process). Diagnostics only (bench.py's per-rank
+    times), outside the timed region."""
+    v = torch.tensor([float(x) for x in values], dtype=torch.float64, device=device)
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return v.cpu().numpy()[None]
+    if dist.get_backend() == "gloo":
+        v = v.cpu()
+    return gather_rows(v[None]).cpu().numpy()
+
+
+def rank_summary(table, names):
+    """{name: [per-rank values]} plus the max/min imbalance of each column."""
+    out = {}
+    for j, n in enumerate(names):
+        col = [float(x) for x in table[:, j]]
+        out[n] = [round(x, 6) for x in col]
+        lo = min(col)
+        out[n + "_max_over_min"] = round(max(col) / lo, 4) if lo > 0 else None
+    return out
 
 
 def job_time_and_work(elapsed_s, work, device):

@@ -750,6 +750,13 @@ class SolverFDDP:
     def synchronize(self):
         check(lib().fddp_synchronize(self._ptr))
 
+    def line_search_info(self):
+        """(trial-group size, rollout dispatches) of the last line search
+        (fddp_get_line_search_info; diagnostics)."""
+        g, n = C.c_int32(), C.c_int32()
+        check(lib().fddp_get_line_search_info(self._ptr, C.byref(g), C.byref(n)))
+        return g.value, n.value
+
 
 class SolverBoxFDDP(SolverFDDP):
     """SolverBoxFDDP (src/core/solvers/box-fddp.cpp:15-164) on the device:

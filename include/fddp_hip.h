@@ -248,6 +248,12 @@ typedef void (*fddp_iteration_callback)(void* user, int iter, const fddp_result*
 /* NULL clears it. Replaces SolverAbstract::setCallbacks (solver-base.cpp:69-73). */
 int fddp_set_callback(fddp_handle* h, fddp_iteration_callback cb, void* user);
 
+/* Diagnostics of the last line search of fddp_solve (for the bench's rollout
+ * accounting): the trial-group size it used (1: the serial search; g > 1: g alpha
+ * trials per element evaluated together, SolverFDDP's acceptance order kept) and
+ * the number of rollout dispatches it made. */
+int fddp_get_line_search_info(fddp_handle* h, int* group_size, int* launches);
+
 /* Results of the last solve / current solver state per element. */
 int fddp_get_results(fddp_handle* h, fddp_result* out);
 /* xs: B*(T+1)*nx, us: B*T*nu_max. on_device != 0: `out` is a device pointer

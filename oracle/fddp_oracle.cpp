@@ -22,6 +22,7 @@
 // calc/calcDiff as the reference's WITH_MULTITHREADING build (mode 1,
 // shooting.hxx:143-145,176-178).
 // ============================================================================
+#include <chrono>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -609,6 +610,12 @@ struct Solver {
   int status = FDDP_STATUS_RUNNING;
   int n_iter_run = 0;
   std::vector<TraceRec> trace;
+  // phase timers (CLOCK_MONOTONIC, as core/utils/timer.hpp:16-40): seconds spent in
+  // the iteration-0 calc, calcDiff + gaps, the backward pass, the forward passes
+  double ph[4] = {0., 0., 0., 0.};
+  static double now() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+  }
 
   void init(Problem* prob, const fddp_params& p) {
     P = prob;
@@ -700,7 +707,9 @@ struct Solver {
 
   // ddp.cpp:157-178
   double calcDiff() {
+    const double t0 = now();
     if (iter == 0) P->calc(xs, us);
+    const double t1 = now();
     cost = P->calcDiff(xs, us);
     const int T = P->T, ndx = P->ndx;
     if (!is_feasible) {
@@ -710,6 +719,8 @@ struct Solver {
     } else if (!was_feasible) {
       for (auto& f : fs) std::fill(f.begin(), f.end(), 0.);
     }
+    ph[0] += t1 - t0;
+    ph[1] += now() - t1;
     return cost;
   }
 
@@ -912,7 +923,10 @@ struct Solver {
   // ddp.cpp:120-125 ; false on backward_error
   bool computeDirection(bool recalc) {
     if (recalc) calcDiff();
-    return backwardPass();
+    const double t0 = now();
+    const bool ok = backwardPass();
+    ph[2] += now() - t0;
+    return ok;
   }
 
   // fddp.cpp:149-225 ; false on forward_error
@@ -963,7 +977,10 @@ struct Solver {
     return true;
   }
   bool tryStep(double alpha, double* dVout) {
-    if (!forwardPass(alpha)) return false;
+    const double t0 = now();
+    const bool ok = forwardPass(alpha);
+    ph[3] += now() - t0;
+    if (!ok) return false;
     *dVout = cost - cost_try;
     return true;
   }
@@ -1245,6 +1262,19 @@ int oracle_solve(oracle_handle* h, int maxiter, int is_feasible, double reg_init
   }
   if (out)
     for (int b = 0; b < B; ++b) fill_result(h->solvers[b], &out[b]);
+  return FDDP_OK;
+}
+
+// Phase times summed over the elements (seconds of thread time): the iteration-0 calc,
+// calcDiff + gaps, the backward passes, the forward passes (line-search trials);
+// reset != 0 zeroes them afterwards.
+int oracle_get_phase_times(oracle_handle* h, double* out, int reset) {
+  for (int i = 0; i < 4; ++i) out[i] = 0.;
+  for (auto& s : h->solvers)
+    for (int i = 0; i < 4; ++i) {
+      out[i] += s.ph[i];
+      if (reset) s.ph[i] = 0.;
+    }
   return FDDP_OK;
 }
 

@@ -5,6 +5,18 @@
 #include <cstdlib>
 #include <vector>
 
+// the calcDiff's LDS matrices (multibody.hpp MB_DUMP), column-major per slot, for the
+// parity diagnosis (tools/mb_dump_check.py --host)
+static double g_dump[12][4096];
+static int g_dump_shape[12][2];
+#define MB_DUMP(slot, ptr, rows, cols, ld)                                   \
+  do {                                                                       \
+    const double* p_ = (const double*)(ptr);                                 \
+    const int r_ = (rows), c_ = (cols), l_ = (ld);                           \
+    for (int e_ = 0; e_ < r_ * c_ && e_ < 4096; ++e_) g_dump[slot][e_] = p_[(e_ / r_) * l_ + e_ % r_]; \
+    g_dump_shape[slot][0] = r_;                                              \
+    g_dump_shape[slot][1] = c_;                                              \
+  } while (0)
 #include "../../crocoddyl_amd/csrc/multibody.hpp"
 
 using namespace fddp::mb;
@@ -43,5 +55,16 @@ int mb_host_layout(const double* P, double* out) {
                        l.Sx, l.da0, l.fx, l.zv, l.dfx, l.dfu, l.total, b.nj, njac, b.nc, nrows, vc ? 1 : 0};
   for (int i = 0; i < (int)(sizeof(f) / sizeof(f[0])); ++i) out[i] = (double)f[i];
   return (int)(sizeof(f) / sizeof(f[0]));
+}
+}
+
+extern "C" {
+// the MB_DUMP slots of the last mb_host_calc_diff: shapes (12 x 2 ints), values (12 x 4096)
+void mb_host_dump(int* shape, double* vals) {
+  for (int s = 0; s < 12; ++s) {
+    shape[2 * s] = g_dump_shape[s][0];
+    shape[2 * s + 1] = g_dump_shape[s][1];
+    for (int e = 0; e < 4096; ++e) vals[s * 4096 + e] = g_dump[s][e];
+  }
 }
 }

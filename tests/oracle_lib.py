@@ -66,6 +66,8 @@ def _bind(L):
         f.argtypes = [C.c_void_p, _abi.D]
     L.oracle_get_trace.restype = C.c_int
     L.oracle_get_trace.argtypes = [C.c_void_p, C.c_int, _abi.D, C.c_int]
+    L.oracle_get_phase_times.restype = C.c_int
+    L.oracle_get_phase_times.argtypes = [C.c_void_p, _abi.D, C.c_int]
     L.oracle_get_quu_inv.restype = C.c_int
     L.oracle_get_quu_inv.argtypes = [C.c_void_p, _abi.D]
     L.oracle_boxqp_solve.restype = C.c_int
@@ -152,6 +154,13 @@ class Oracle:
         a = np.zeros((self.dims.B, nk, per))
         self.L.oracle_get_quantity(self.h, which, _abi.dptr(a))
         return a
+
+    def phase_times(self, reset=True):
+        """Seconds of thread time per phase, summed over the elements: calc (iteration
+        0), calcDiff + gaps, backward, forward."""
+        a = np.zeros(4)
+        self.L.oracle_get_phase_times(self.h, _abi.dptr(a), int(reset))
+        return dict(zip(("calc", "calcDiff", "backward", "forward"), a.tolist()))
 
     def trace(self, b, maxn=1000):
         a = np.zeros((maxn, 8))

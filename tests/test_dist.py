@@ -46,8 +46,11 @@ def _worker(rank, ws, port, q):
     xs = torch.from_numpy(o.xs())
     allxs = cdist.gather_rows(xs)
     t, w = cdist.job_time_and_work(0.5 + rank, sum(x.n_iter_run for x in r), "cpu")
+    # bench.py's per-rank diagnostics table
+    rt = cdist.rank_table([0.5 + rank, 10.0 * (rank + 1)], "cpu")
+    summ = cdist.rank_summary(rt, ["elapsed_s", "iterations"])
     if rank == 0:
-        q.put((allxs.numpy(), t, w))
+        q.put((allxs.numpy(), t, w, rt, summ))
     torch.distributed.barrier()
     torch.distributed.destroy_process_group()
 
@@ -70,7 +73,7 @@ def test_world2_gloo_gather_matches_single_process():
     procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    allxs, t, w = q.get(timeout=120)
+    allxs, t, w, rt, summ = q.get(timeout=120)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -85,3 +88,6 @@ def test_world2_gloo_gather_matches_single_process():
     np.testing.assert_array_equal(allxs, np.concatenate(ref))
     assert t == pytest.approx(1.5)
     assert w == iters
+    np.testing.assert_array_equal(rt, [[0.5, 10.0], [1.5, 20.0]])
+    assert summ["elapsed_s"] == [0.5, 1.5] and summ["elapsed_s_max_over_min"] == 3.0
+    assert summ["iterations_max_over_min"] == 2.0

@@ -7,12 +7,33 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 // stamps inside the blocked Gauss-Jordan (multibody.hpp gj_mfma), thread 0 of workgroup 0
 __device__ unsigned long long g_gjst[32];
 #define MB_GJ_MARK(id)                                                            \
   do {                                                                            \
     if (threadIdx.x == 0 && blockIdx.x == 0) g_gjst[id] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+// LDS matrices of the calcDiff of workgroup 0 (multibody.hpp MB_DUMP), column-major
+// rows x cols per slot; the first launch fills them
+constexpr int kDumpSlots = 12, kDumpCap = 4096;
+__device__ double g_dump[kDumpSlots][kDumpCap];
+__device__ int g_dump_shape[kDumpSlots][2];
+#define MB_DUMP(slot, ptr, rows, cols, ld)                                                  \
+  do {                                                                                      \
+    __syncthreads();                                                                        \
+    if (blockIdx.x == 0) {                                                                  \
+      const double* p_ = (const double*)(ptr);                                              \
+      const int r_ = (rows), c_ = (cols), l_ = (ld);                                        \
+      for (int e_ = threadIdx.x; e_ < r_ * c_ && e_ < kDumpCap; e_ += blockDim.x)            \
+        g_dump[slot][e_] = p_[(e_ / r_) * l_ + e_ % r_];                                    \
+      if (threadIdx.x == 0) {                                                               \
+        g_dump_shape[slot][0] = r_;                                                         \
+        g_dump_shape[slot][1] = c_;                                                         \
+      }                                                                                     \
+    }                                                                                       \
+    __syncthreads();                                                                        \
   } while (0)
 #include "../crocoddyl_amd/csrc/multibody.hpp"
 
@@ -178,7 +199,8 @@ int main(int argc, char** argv) {
          (long)l.wv, (long)l.A, (long)l.dtau, (long)l.da, (long)l.qp, (long)l.vec, (long)l.J, (long)l.red, (long)l.Jc,
          (long)l.R, (long)l.total, njac, (int)vc, bk.nc, count_cost_rows(bk, bk.nj - bk.nun));
   fflush(stdout);
-  if (argc > 3) return 0;  // layout only
+  if (argc > 3 && std::string(argv[3]) != "dump") return 0;  // layout only
+  const bool dump = argc > 3;
   double *dP, *dx, *du, *dout;
   unsigned long long* dst;
   CK(hipMalloc(&dP, 8 * psz));
@@ -223,6 +245,22 @@ int main(int argc, char** argv) {
       CK(hipMemcpy(st.data(), dst, 8 * 256, hipMemcpyDeviceToHost));
       printf("%s nwg %d: %.3f ms (%.2f us per WG-knot at 256 CUs)\n", which == 0 ? "calcDiff" : "calc", nwg, ms,
              1e3 * ms / (nwg / 256.0 > 1 ? nwg / 256.0 : 1));
+      if (dump && which == 0 && rep == 0) {  // the LDS matrices and the output blocks
+        std::vector<double> dm((size_t)kDumpSlots * kDumpCap);
+        std::vector<int> sh(2 * kDumpSlots);
+        CK(hipMemcpyFromSymbol(dm.data(), HIP_SYMBOL(g_dump), 8 * dm.size()));
+        CK(hipMemcpyFromSymbol(sh.data(), HIP_SYMBOL(g_dump_shape), 4 * sh.size()));
+        std::vector<double> ob(so);
+        CK(hipMemcpy(ob.data(), dout, 8 * so, hipMemcpyDeviceToHost));
+        std::string path = std::string(argv[1]) + ".dump";
+        FILE* g = fopen(path.c_str(), "wb");
+        fwrite(sh.data(), 4, sh.size(), g);
+        fwrite(dm.data(), 8, dm.size(), g);
+        fwrite(&so, 8, 1, g);
+        fwrite(ob.data(), 8, ob.size(), g);
+        fclose(g);
+        printf("dumped %s\n", path.c_str());
+      }
       if (rep == 2) {
         unsigned long long prev = st[1];
         printf("  phases (s_memtime ticks; * = wave-0 phase):");

@@ -51,6 +51,7 @@ def main():
 
     def fresh():
         g = helpers.Gpu(d, S["knots"], S["pool"], S["x0s"], device=0)
+        g.set_debug(True)  # the Q / V blocks are stored only in debug mode
         o = oracle_lib.Oracle(d, S["knots"], S["pool"], S["x0s"], threads=4)
         for h in (g, o):
             h.set_candidate(xs, us, False)
