@@ -12,9 +12,11 @@
 //        G^T = Z^T Vxx' = Fx^T Vxx' as the reference forms it)
 //   Qx = Lx + Fx^T Vx', Qu = Lu + Fu^T Vx'  (VALU, folded into the G loop: the
 //        lane already holds the Z fragment)
-//   Quu^-1 by a symmetric sweep (Gauss-Jordan) on wave 0, overlapped with the
-//        Qxx/Qxu tiles of waves 1-3; a pivot <= 0 is the reference's LLT failure
-//   K  = Quu^-1 Qxu^T (MFMA), k = Quu^-1 Qu (VALU)
+//   C = Lc^-1, the inverse Cholesky factor of Quu (chol_inv_sweep) on wave 0,
+//        overlapped with the Qxx/Qxu tiles of waves 1-3; a pivot <= 0 is the
+//        reference's LLT failure
+//   K  = C^T (C Qxu^T) (two MFMA products), k = C^T (C Qu) (VALU): as accurate as
+//        the reference's LLT solves (an explicit Quu^-1 is not, on graded Quu)
 //   Vxx = Qxx - K^T Qxu^T (+ xreg I), written symmetric; the owner of x block
 //        i keeps its K(:, i) tiles in registers and finds its Qxx(i, :) tiles
 //        in the (dead) Vxx' buffer, updating them in place
@@ -270,6 +272,74 @@ __device__ __forceinline__ bool sym_sweep_inverse(const double* Quu, double* Qi,
   for (int r = 0; r < RPL; ++r) {
     const int i = h * RPL + r;
     Qi[i * LDQ + jc] = (i < m && jc < m) ? -A[r] : 0.;
+  }
+  return bad;
+}
+
+// The inverse Cholesky factor C = Lc^-1 of Quu = Lc Lc^T (the reference's LLT,
+// ddp.cpp:298-310) on one wave, in the lane layout of sym_sweep_inverse. Gaussian
+// elimination without pivoting (Quu = L D L^T, L unit lower) with the multipliers
+// applied to the identity in place: after pivot k, for every row i > k,
+//   A(i, j) -= l_ik A(k, j) (j != k),   A(i, k) = -l_ik,   l_ik = A(i, k) / d_k,
+// so the strictly lower part accumulates L^-1 (its row k holds L^-1(k, j < k), the
+// trailing block stays the symmetric Schur complement, which supplies A(i, k) from
+// the published row k) and the diagonal the pivots d_k; then C = D^-1/2 L^-1. The
+// gains are formed as K = C^T (C Qxu^T): on the C5 walk's Quu (cond 1e9 .. 5e10,
+// graded) the explicit inverse's product Quu^-1 Qxu^T was 200x further from the
+// LLT solves than the solves from each other (the round-4 parity trace: K 3e-8 vs
+// 1.5e-10), the two triangular products as close as the solves. A pivot <= 0 is the
+// LLT failure. C: lower triangular, zero above the diagonal and beyond m.
+template <int MP, int LDQ>
+__device__ __forceinline__ bool chol_inv_sweep(const double* Quu, double* C, double* rb, int m, int lane) {
+  constexpr int RPL = MP * MP / 64;
+  static_assert(MP * MP % 64 == 0 && 64 % MP == 0, "sweep lane layout");
+  const int jc = lane % MP, h = lane / MP;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  double A[RPL];
+#pragma unroll
+  for (int r = 0; r < RPL; ++r) A[r] = Quu[(h * RPL + r) * LDQ + jc];
+  bool bad = false;
+  rb[lane] = A[0];
+#pragma unroll
+  for (int k = 0; k < MP; ++k) {
+    if (k < m) {
+      const int hk = k / RPL;
+      const int r1 = (k + 1) % RPL;
+      asm volatile("" ::: "memory");
+      // row k (published by its lanes): the pivot, A(k, jc), and A(k, i) = A(i, k)
+      // for my rows i > k (the trailing block is symmetric)
+      const double d = rb[hk * MP + k];
+      const double akj = rb[hk * MP + jc];
+      double ak[RPL];
+#pragma unroll
+      for (int r = 0; r < RPL; ++r) ak[r] = rb[hk * MP + h * RPL + r];
+      bad |= !(d > 0.);
+      const bool colk = jc == k;
+      // next pivot row first (its product does not wait for 1/d), then published
+      const double p1 = ak[r1] * akj;
+      const double dinv = rcp_f64(d);
+      if (h * RPL + r1 > k) A[r1] = colk ? -ak[r1] * dinv : fma(-p1, dinv, A[r1]);
+      asm volatile("" ::: "memory");
+      rb[lane] = A[r1];
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int r = 0; r < RPL; ++r)
+        if (r != r1 && h * RPL + r > k) A[r] = colk ? -ak[r] * dinv : fma(-ak[r] * akj, dinv, A[r]);
+    }
+  }
+  // the pivots d_i, published by the diagonal's lanes; C(i, j) = L^-1(i, j) / sqrt(d_i)
+  asm volatile("" ::: "memory");
+#pragma unroll
+  for (int r = 0; r < RPL; ++r)
+    if (h * RPL + r == jc) rb[jc] = A[r];
+  asm volatile("" ::: "memory");
+#pragma unroll
+  for (int r = 0; r < RPL; ++r) {
+    const int i = h * RPL + r;
+    const double s = (i < m && rb[i] > 0.) ? 1. / sqrt(rb[i]) : 0.;
+    double v = 0.;
+    if (i < m && jc < m) v = i == jc ? s : (jc < i ? A[r] * s : 0.);
+    C[jc * LDQ + i] = v;  // (column-major: C(i, jc))
   }
   return bad;
 }
@@ -841,11 +911,8 @@ __device__ __forceinline__ bool bwd_knot(const Dev& D, const BwdLds& L, int b, i
     if (boxk) {
       if (!box_gains_wave<MP, LDQ>(D, L, b, t, cur, lane) && lane == 0) *L.flag = 1;
     } else {
-#ifdef FDDP_INV_BLK
-      const bool bad = sym_sweep_inverse_blk<MP, LDQ>(Quu, Qi, L.rowbuf, mu, lane);
-#else
-      const bool bad = sym_sweep_inverse<MP, LDQ>(Quu, Qi, L.rowbuf, mu, lane);
-#endif
+      // C = Lc^-1 into Qi (the gains as K = C^T (C Qxu^T), k = C^T (C Qu))
+      const bool bad = chol_inv_sweep<MP, LDQ>(Quu, Qi, L.rowbuf, mu, lane);
       if (bad && lane == 0) *L.flag = 1;
     }
   }
@@ -870,6 +937,24 @@ __device__ __forceinline__ bool bwd_knot(const Dev& D, const BwdLds& L, int b, i
           const double bq = Qxu[(4 * s + q) * LDV + 16 * i + c];
 #pragma unroll
           for (int it = 0; it < MTL; ++it) Kt[o][it] = mfma4(Qi[(4 * s + q) * LDQ + 16 * it + c], bq, Kt[o][it]);
+        }
+        if (!boxk) {
+          // Kt holds W = C Qxu^T; K = C^T W: W's accumulator register s' holds rows
+          // q + 4 s' of its 16-row tile, which is the B fragment of k-step s'. C is
+          // lower triangular, so C^T's tile (it, kt) vanishes for kt < it.
+          f64x4 Wt[MTL];
+#pragma unroll
+          for (int it = 0; it < MTL; ++it) {
+            Wt[it] = Kt[o][it];
+            Kt[o][it] = f64x4{0., 0., 0., 0.};
+          }
+#pragma unroll
+          for (int it = 0; it < MTL; ++it)
+#pragma unroll
+            for (int kt = it; kt < MTL; ++kt)
+#pragma unroll
+              for (int s = 0; s < 4; ++s)
+                Kt[o][it] = mfma4(Qi[(16 * it + c) * LDQ + 16 * kt + 4 * s + q], Wt[kt][s], Kt[o][it]);
         }
         const int C = 16 * i + c;
 #pragma unroll
@@ -930,6 +1015,7 @@ __device__ __forceinline__ bool bwd_knot(const Dev& D, const BwdLds& L, int b, i
       const int row = lane % MP, part = lane / MP;
       double a0 = 0., a1 = 0.;
       if (!boxk) {
+        // y = C Qu (into kv), then k = C^T y
         for (int k2 = part; k2 < mu; k2 += 2 * LPR) {
           a0 = fma(Qi[k2 * LDQ + row], L.qu[k2], a0);
           if (k2 + LPR < mu) a1 = fma(Qi[(k2 + LPR) * LDQ + row], L.qu[k2 + LPR], a1);
@@ -937,6 +1023,18 @@ __device__ __forceinline__ bool bwd_knot(const Dev& D, const BwdLds& L, int b, i
         double a = a0 + a1;
 #pragma unroll
         for (int o2 = MP; o2 < 64; o2 <<= 1) a += __shfl_xor(a, o2, 64);
+        if (part == 0) L.kv[row] = row < mu ? a : 0.;
+        asm volatile("" ::: "memory");
+        a0 = 0.;
+        a1 = 0.;
+        for (int k2 = part; k2 < mu; k2 += 2 * LPR) {
+          a0 = fma(Qi[row * LDQ + k2], L.kv[k2], a0);
+          if (k2 + LPR < mu) a1 = fma(Qi[row * LDQ + k2 + LPR], L.kv[k2 + LPR], a1);
+        }
+        a = a0 + a1;
+#pragma unroll
+        for (int o2 = MP; o2 < 64; o2 <<= 1) a += __shfl_xor(a, o2, 64);
+        asm volatile("" ::: "memory");
         if (part == 0) {
           if (row >= mu) a = 0.;
           L.kv[row] = a;

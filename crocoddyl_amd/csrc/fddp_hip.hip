@@ -25,6 +25,7 @@
 #include "fddp_kernels.hpp"
 #include "fast_path.hpp"
 #include "bwd_mfma.hpp"
+#include "bwd_wave.hpp"
 
 using namespace fddp;
 
@@ -319,6 +320,7 @@ struct fddp_handle_s {
   size_t mb_diff_smem = 0; // its dynamic LDS
   int mb_nj = 0;            // largest multibody tree (dofs)
   int bwd_variant = 0;  // 0 generic, else (NTL*10+MTL)*10+waves of the MFMA sweep
+  bool bwd_wave = false;  // small knots (n, m <= 16): the one-wave sweep (bwd_wave.hpp), FDDP only
   int ls_npar_last = 0;      // trial-group size of the last line search (1: serial)
   int ls_launches_last = 0;  // rollout (forward_kernel) dispatches of the last line search
   fddp_iteration_callback cb = nullptr;  // per-iteration callback (fddp_set_callback)
@@ -538,6 +540,12 @@ void launch_bwd_mfma(fddp_handle* h, int mode) {
 int launch_backward(fddp_handle* h, int mode) {
   Timed tm(h, 2);
   const Dev& D = h->D;
+  if (h->bwd_wave && !D.box) {  // (SolverBoxFDDP's box QP lives in the other sweeps)
+    hipLaunchKernelGGL(backward_wave_kernel, dim3((D.B + kWavesPerWg - 1) / kWavesPerWg), dim3(64 * kWavesPerWg),
+                       sizeof(double) * kWavesPerWg * bwd_wave_doubles(), h->stream, D, to_prm(h->prm), mode);
+    LAUNCH_CHECK();
+    return FDDP_OK;
+  }
   switch (h->bwd_variant) {
     case 528: launch_bwd_mfma<5, 2, 8>(h, mode); break;
     case 524: launch_bwd_mfma<5, 2, 4>(h, mode); break;
@@ -925,6 +933,13 @@ int apply_knots(fddp_handle* h, const fddp_knot_desc* knots, const double* param
       else if (ntl == 1 && mtl == 1) v = setup_bwd_mfma_nw<1, 1>(h, nw);
     }
     h->bwd_variant = v > 0 ? v : 0;
+    // small knots: the one-wave sweep unless a sweep is forced (FDDP_BACKWARD=generic / mfma)
+    if (!env && d.ndx <= kBwdWaveMax && d.nu_max <= kBwdWaveMax) {
+      if (hipFuncSetAttribute((const void*)backward_wave_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)(sizeof(double) * kWavesPerWg * bwd_wave_doubles())) != hipSuccess)
+        return fail(FDDP_ERR_RUNTIME, "hipFuncSetAttribute(dynamic LDS) of backward_wave_kernel");
+      h->bwd_wave = true;
+    }
   }
   return FDDP_OK;
 }

@@ -454,6 +454,7 @@ class SolverFDDP:
         self.callbacks = []
         self.callbackMask = None
         self._cb_error = None
+        self._cb_snap = None
 
     # -- helpers -----------------------------------------------------------
     @property
@@ -467,6 +468,8 @@ class SolverFDDP:
         return arr if self.problem.batched else arr[0]
 
     def _res(self):
+        if self._cb_snap is not None:  # inside a per-iteration callback: that iteration's state
+            return self._cb_snap
         if self._results is None:
             r = (_abi.Result * self.problem.B)()
             check(lib().fddp_get_results(self._ptr, r))
@@ -514,7 +517,7 @@ class SolverFDDP:
             def on_iter(_user, it, res, reported, _B):
                 snap = (_abi.Result * B)()
                 C.memmove(snap, res, C.sizeof(snap))
-                self._results = snap
+                self._cb_snap = snap
                 self.callbackMask = np.ctypeslib.as_array(reported, (B,)).astype(bool)
                 if not self.problem.batched and not self.callbackMask[0]:
                     return
@@ -532,6 +535,7 @@ class SolverFDDP:
             finally:
                 check(lib().fddp_set_callback(ptr, _abi.IterationCallback(), None))
                 self.callbackMask = None
+                self._cb_snap = None
             if self._cb_error is not None:
                 raise self._cb_error
         else:
