@@ -161,16 +161,25 @@ struct MfmaCfg {
   static constexpr int oKv = oLu + MP;  // kv + quuk: the sweep's 64-double row buffer (wave 0, P1)
   static constexpr int oQuuk = oKv + MP;
   static constexpr int oRed = oKv + (2 * MP > 64 ? 2 * MP : 64);  // 5 sums x up to 8 waves
-  static constexpr int oFlag = oRed + 40;  // flag; Quu-ready, G-done, P2-done counters (4 ints)
+  static constexpr int oFlag = oRed + 40;  // flag; Quu-ready, G-done, P2-done, H-done counters (5 ints)
   // Z column stride ZLD = NP - 2 (= 2 mod 4): the 16 lanes of a B fragment
   // read 16 columns at a stride of 2*ZLD = 4 (mod 8) banks, conflict-free
   // (a stride of NP was an 8-way conflict). k-steps past ZLD read the next
   // column's first rows (or the 2 zero doubles after the last column); they
   // only ever multiply the zero rows of Vxx' / G, so nothing changes.
   static constexpr int ZLD = NP - 2;
-  static constexpr int oZx = (oFlag + 2 + 1) & ~1;
+  static constexpr int oZx = (oFlag + 4 + 1) & ~1;
   static constexpr int oZu = oZx + NP * ZLD;
-  static constexpr int total = oZu + MP * ZLD + 2;
+  static constexpr int total0 = oZu + MP * ZLD + 2;
+  // C^T, the transposed inverse Cholesky factor (chol_inv_sweep), at the odd leading
+  // dimension LDT (its fragment reads step along it: conflict-free): its own area when
+  // it fits the 160 KB, else over Zu, which is dead from the H tiles of a knot until
+  // the next knot's LDS-DMA (issued after B2 by the 8-wave plan, see bwd_knot)
+  static constexpr int LDT = MP + 1;
+  static constexpr bool ct_own = sizeof(double) * (total0 + MP * LDT) <= 160 * 1024;
+  static constexpr int oCt = ct_own ? total0 : oZu;
+  static constexpr int total = ct_own ? total0 + MP * LDT : total0;
+  static_assert(ct_own || MP * LDT <= MP * ZLD, "C^T over Zu");
   static constexpr size_t bytes = sizeof(double) * total;
 };
 
@@ -289,8 +298,10 @@ __device__ __forceinline__ bool sym_sweep_inverse(const double* Quu, double* Qi,
 // LLT solves than the solves from each other (the round-4 parity trace: K 3e-8 vs
 // 1.5e-10), the two triangular products as close as the solves. A pivot <= 0 is the
 // LLT failure. C: lower triangular, zero above the diagonal and beyond m.
-template <int MP, int LDQ>
-__device__ __forceinline__ bool chol_inv_sweep(const double* Quu, double* C, double* rb, int m, int lane) {
+// Cx (may be null): C's transpose as well, C(i, j) at Cx[i * LDQ + j]; Ct null: no C^T.
+template <int MP, int LDQ, int LDT>
+__device__ __forceinline__ bool chol_inv_sweep(const double* Quu, double* C, double* Ct, double* rb, int m, int lane,
+                                               int* ct_ready, int ct_target, double* Cx = nullptr) {
   constexpr int RPL = MP * MP / 64;
   static_assert(MP * MP % 64 == 0 && 64 % MP == 0, "sweep lane layout");
   const int jc = lane % MP, h = lane / MP;
@@ -327,19 +338,97 @@ __device__ __forceinline__ bool chol_inv_sweep(const double* Quu, double* C, dou
         if (r != r1 && h * RPL + r > k) A[r] = colk ? -ak[r] * dinv : fma(-ak[r] * akj, dinv, A[r]);
     }
   }
-  // the pivots d_i, published by the diagonal's lanes; C(i, j) = L^-1(i, j) / sqrt(d_i)
+  // 1 / sqrt(d_i) by the diagonal's lanes (one each), published; C(i, j) = L^-1(i, j) / sqrt(d_i)
+  // into C (column-major, ld LDQ) and C^T (column-major, ld LDT)
   asm volatile("" ::: "memory");
 #pragma unroll
   for (int r = 0; r < RPL; ++r)
-    if (h * RPL + r == jc) rb[jc] = A[r];
+    if (h * RPL + r == jc) rb[jc] = (jc < m && A[r] > 0.) ? 1. / sqrt(A[r]) : 0.;
   asm volatile("" ::: "memory");
+  // C^T's area may still be read by other waves (ct_target > 0: wait for them)
+  if (Ct && ct_target > 0) {
+    while (__hip_atomic_load(ct_ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < ct_target)
+      __builtin_amdgcn_s_sleep(1);
+    asm volatile("" ::: "memory");
+  }
 #pragma unroll
   for (int r = 0; r < RPL; ++r) {
     const int i = h * RPL + r;
-    const double s = (i < m && rb[i] > 0.) ? 1. / sqrt(rb[i]) : 0.;
+    const double s = rb[i];
     double v = 0.;
     if (i < m && jc < m) v = i == jc ? s : (jc < i ? A[r] * s : 0.);
-    C[jc * LDQ + i] = v;  // (column-major: C(i, jc))
+    C[jc * LDQ + i] = v;
+    if (Ct) Ct[i * LDT + jc] = v;
+    if (Cx) Cx[i * LDQ + jc] = v;
+  }
+  return bad;
+}
+
+// The same factor for a 32-wide Quu (the C5 walk's m = 32) in 16-blocks, so that the
+// latency-bound sweeps run 2 x 16 light steps (4 rows per lane) instead of 32 steps of
+// 16 rows per lane: Quu = [A11 A21^T; A21 A22] = L L^T, C = L^-1 =
+// [C11 0; C21 C22]:
+//   C11 = chol_inv(A11);  G = C11 A21^T (= L21^T);  S = A22 - G^T G;
+//   C22 = chol_inv(S);    C21 = -C22 (L21 C11)
+// (the blocked right-looking Cholesky, the off-diagonal products on MFMA in registers:
+// the accumulator register s of G / T is the A and B fragment of k-step s). C as
+// chol_inv_sweep's (col-major, ld LDQ, zero above the diagonal and beyond m), then C^T
+// (ld LDT) once the other waves are done with its area.
+template <int LDQ, int LDT>
+__device__ __forceinline__ bool chol_inv_blocked2(const double* Quu, double* C, double* Ct, double* rb, int m, int lane,
+                                                  int* ct_ready, int ct_target) {
+  const int q = lane >> 4, c = lane & 15;
+  const int m1 = m < 16 ? m : 16, m2 = m - 16;
+  // C11, and its transpose in the lower-left block (free until C21 lands there)
+  bool bad = chol_inv_sweep<16, LDQ, LDT>(Quu, C, nullptr, rb, m1, lane, nullptr, 0, C + 16);
+  asm volatile("" ::: "memory");
+  if (m2 > 0) {
+    f64x4 G = {0., 0., 0., 0.}, T = {0., 0., 0., 0.}, S, X = {0., 0., 0., 0.};
+    // G = C11 A12: A(c, 4s+q) = C11(c, 4s+q); B(4s+q, c) = A12(4s+q, c) = Quu(16+c, 4s+q)
+#pragma unroll
+    for (int s = 0; s < 4; ++s) G = mfma4(C[(4 * s + q) * LDQ + c], Quu[(4 * s + q) * LDQ + 16 + c], G);
+    // S = A22 - G^T G, held as S(q+4r, c); staged (by symmetry) at (c, 16+q+4r), the
+    // upper-right block (zero in C, rewritten below)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) S[r] = Quu[(16 + q + 4 * r) * LDQ + 16 + c];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) S = mfma4(-G[s], G[s], S);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) C[(16 + q + 4 * r) * LDQ + c] = S[r];
+    // T = L21 C11: A(c, 4s+q) = L21(c, 4s+q) = G(4s+q, c); B(4s+q, c) = C11(4s+q, c),
+    // stored transposed at (16+c, 4s+q)
+#pragma unroll
+    for (int s = 0; s < 4; ++s) T = mfma4(G[s], C[(4 * s + q) * LDQ + 16 + c], T);
+    asm volatile("" ::: "memory");
+    bad = chol_inv_sweep<16, LDQ, LDT>(C + 16 * LDQ, C + 16 * LDQ + 16, nullptr, rb, m2, lane, nullptr, 0) || bad;
+    asm volatile("" ::: "memory");
+    // C21 = -C22 T: A(c, 4s+q) = C22(c, 4s+q) at (16+c, 16+4s+q); B = T's register s
+#pragma unroll
+    for (int s = 0; s < 4; ++s) X = mfma4(-C[(16 + 4 * s + q) * LDQ + 16 + c], T[s], X);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      C[c * LDQ + 16 + q + 4 * r] = X[r];
+      C[(16 + q + 4 * r) * LDQ + c] = 0.;  // the staging of S
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {  // rows 16..31 (C11^T's block too), then the upper-right block
+      const int e = lane + 64 * r, i = 16 + (e & 15), j = e >> 4;
+      C[j * LDQ + i] = 0.;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) C[(16 + q + 4 * r) * LDQ + c] = 0.;
+  }
+  asm volatile("" ::: "memory");
+  if (ct_target > 0) {
+    while (__hip_atomic_load(ct_ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < ct_target)
+      __builtin_amdgcn_s_sleep(1);
+    asm volatile("" ::: "memory");
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int e = lane + 64 * r, i = e & 31, j = e >> 5;
+    Ct[i * LDT + j] = C[j * LDQ + i];
   }
   return bad;
 }
@@ -470,7 +559,8 @@ __host__ __device__ constexpr int bwd_block_cost(int i) {
 template <int NTL, int MTL, int NW>
 struct BwdPlan {
   static constexpr int JT = NTL + MTL;
-  static_assert(NW == 4 || NW == 8, "4 or 8 waves");
+  static_assert(NW == 1 || NW == 4 || NW == 8, "1, 4 or 8 waves");
+  static_assert(NW != 1 || JT <= 8, "1-wave plan: at most 8 column blocks");
   static_assert(NW == 4 || JT <= 7, "8-wave plan: at most 7 column blocks");
   int nown[8];
   int blk[8][8];
@@ -483,7 +573,10 @@ struct BwdPlan {
   int xwaves;  // waves owning x blocks (the P3 consumers)
   constexpr BwdPlan() : nown{}, blk{}, ntile{}, tile{}, uwaves(0), gwaves(0), ndma(0), dmarank{}, xwaves(0) {
     int owner[16] = {};
-    if (NW == 4) {
+    if (NW == 1) {  // small knots: one wave owns every block (no partial barrier ever waits)
+      for (int u = 0; u < MTL; ++u) blk[0][nown[0]++] = NTL + u;
+      for (int i = 0; i < NTL; ++i) blk[0][nown[0]++] = i;
+    } else if (NW == 4) {
       for (int u = 0; u < MTL; ++u) {
         blk[0][nown[0]++] = NTL + u;
         owner[NTL + u] = 0;
@@ -549,7 +642,7 @@ struct BwdPlan {
     // hundred cycles, so in the 8-wave plan it goes to the waves that have no
     // x blocks (no P2 / P3 MFMA work); they skip B2 (see bwd_knot)
     for (int w = 0; w < NW; ++w) dmarank[w] = -1;
-    if (NW == 4) {
+    if (NW <= 4) {
       for (int w = 0; w < NW; ++w) dmarank[w] = ndma++;
     } else {  // the waves without x blocks: no MFMA work in P2 / P3
       for (int w = 0; w < NW; ++w)
@@ -597,7 +690,7 @@ __host__ __device__ constexpr int bwd_jstart(int i) {
 
 // LDS carve of one workgroup (see MfmaCfg).
 struct BwdLds {
-  double *V, *Qxu, *Quu, *Qi, *vx, *qx, *lxv, *fsb, *qu, *luv, *kv, *quuk, *rowbuf, *red, *Zx, *Zu;
+  double *V, *Qxu, *Quu, *Qi, *vx, *qx, *lxv, *fsb, *qu, *luv, *kv, *quuk, *rowbuf, *red, *Zx, *Zu, *Ct;
   int* flag;
 };
 
@@ -826,7 +919,7 @@ __device__ __forceinline__ bool bwd_knot(const Dev& D, const BwdLds& L, int b, i
   // run (any(j) is monotone in j, so the next column always exists). With two
   // waves per SIMD the partner wave covers that latency instead, and the
   // second buffer's registers are better spent elsewhere.
-  constexpr bool ZDB = NW == 4;
+  constexpr bool ZDB = NW <= 4;
   double zc[4 * NTL], zn[ZDB ? 4 * NTL : 1];
   bool first = true;
   auto zload = [&](double(&zz)[4 * NTL], int j) {
@@ -899,6 +992,10 @@ __device__ __forceinline__ bool bwd_knot(const Dev& D, const BwdLds& L, int b, i
     if (lane == 0) __hip_atomic_fetch_add(L.flag + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     __builtin_amdgcn_s_setprio(0);
   }
+  if constexpr (!Cfg::ct_own && NO > 0) {  // H done: its reads of Zu are over (C^T lands there)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (lane == 0) __hip_atomic_fetch_add(L.flag + 4, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
   stamp.mark(1);
   // ---- wave 0: Quu^-1 by the symmetric sweep (overlaps waves 1-3) ----------
   if constexpr (W == 0) {
@@ -912,7 +1009,15 @@ __device__ __forceinline__ bool bwd_knot(const Dev& D, const BwdLds& L, int b, i
       if (!box_gains_wave<MP, LDQ>(D, L, b, t, cur, lane) && lane == 0) *L.flag = 1;
     } else {
       // C = Lc^-1 into Qi (the gains as K = C^T (C Qxu^T), k = C^T (C Qu))
-      const bool bad = chol_inv_sweep<MP, LDQ>(Quu, Qi, L.rowbuf, mu, lane);
+      // (C^T over Zu: written once every wave's H tiles have read Zu)
+      const int htarget = Cfg::ct_own ? 0 : P.gwaves * (D.T - t);
+      __builtin_amdgcn_s_setprio(3);  // the sweeps' latency chain is the knot's critical path
+      bool bad;
+      if constexpr (MP == 32)
+        bad = chol_inv_blocked2<LDQ, Cfg::LDT>(Quu, Qi, L.Ct, L.rowbuf, mu, lane, L.flag + 4, htarget);
+      else
+        bad = chol_inv_sweep<MP, LDQ, Cfg::LDT>(Quu, Qi, L.Ct, L.rowbuf, mu, lane, L.flag + 4, htarget);
+      __builtin_amdgcn_s_setprio(0);
       if (bad && lane == 0) *L.flag = 1;
     }
   }
@@ -920,7 +1025,7 @@ __device__ __forceinline__ bool bwd_knot(const Dev& D, const BwdLds& L, int b, i
   dma_barrier();  // B1 (also retires the fs DMA issued at the end of the last knot)
   stamp.mark(3);
   if (*L.flag) return false;
-  if constexpr (NW == 4) issue_dma();
+  if constexpr (NW <= 4) issue_dma();
   // ---- P2: K(:, i) = Quu^-1 Qxu(i, :)^T ; Vxx(i, j) = Qxx(i, j) - K(:, i)^T Qxu(j, :)^T
   f64x4 Kt[NA][MTL];
   {
@@ -941,20 +1046,19 @@ __device__ __forceinline__ bool bwd_knot(const Dev& D, const BwdLds& L, int b, i
         if (!boxk) {
           // Kt holds W = C Qxu^T; K = C^T W: W's accumulator register s' holds rows
           // q + 4 s' of its 16-row tile, which is the B fragment of k-step s'. C is
-          // lower triangular, so C^T's tile (it, kt) vanishes for kt < it.
-          f64x4 Wt[MTL];
+          // lower triangular, so C^T's tile (it, kt) vanishes for kt < it: tile it of
+          // K reads W's tiles kt >= it only, so it replaces W's tile it in place
+          // (one extra tile of registers, not MTL)
 #pragma unroll
           for (int it = 0; it < MTL; ++it) {
-            Wt[it] = Kt[o][it];
-            Kt[o][it] = f64x4{0., 0., 0., 0.};
-          }
-#pragma unroll
-          for (int it = 0; it < MTL; ++it)
+            f64x4 kn = f64x4{0., 0., 0., 0.};
 #pragma unroll
             for (int kt = it; kt < MTL; ++kt)
 #pragma unroll
               for (int s = 0; s < 4; ++s)
-                Kt[o][it] = mfma4(Qi[(16 * it + c) * LDQ + 16 * kt + 4 * s + q], Wt[kt][s], Kt[o][it]);
+                kn = mfma4(L.Ct[(16 * kt + 4 * s + q) * Cfg::LDT + 16 * it + c], Kt[o][kt][s], kn);
+            Kt[o][it] = kn;
+          }
         }
         const int C = 16 * i + c;
 #pragma unroll
@@ -1028,8 +1132,8 @@ __device__ __forceinline__ bool bwd_knot(const Dev& D, const BwdLds& L, int b, i
         a0 = 0.;
         a1 = 0.;
         for (int k2 = part; k2 < mu; k2 += 2 * LPR) {
-          a0 = fma(Qi[row * LDQ + k2], L.kv[k2], a0);
-          if (k2 + LPR < mu) a1 = fma(Qi[row * LDQ + k2 + LPR], L.kv[k2 + LPR], a1);
+          a0 = fma(L.Ct[k2 * Cfg::LDT + row], L.kv[k2], a0);
+          if (k2 + LPR < mu) a1 = fma(L.Ct[(k2 + LPR) * Cfg::LDT + row], L.kv[k2 + LPR], a1);
         }
         a = a0 + a1;
 #pragma unroll
@@ -1173,6 +1277,8 @@ __device__ __forceinline__ bool bwd_sweep_mfma(const Dev& D, int b, bool feas, d
   L.flag = (int*)(sm + Cfg::oFlag);
   L.Zx = sm + Cfg::oZx;
   L.Zu = sm + Cfg::oZu;
+  L.Ct = sm + Cfg::oCt;
+  static_assert(Cfg::ct_own || NW == 8, "C^T over Zu needs the 8-wave plan's late LDS-DMA");
   double* V = L.V;
   const bool xr = !isnan(xreg);
   Stamp stamp(D.stamps ? D.stamps + ((int64_t)b * 8 + wid) * 8 : nullptr);
@@ -1182,6 +1288,7 @@ __device__ __forceinline__ bool bwd_sweep_mfma(const Dev& D, int b, bool feas, d
     L.flag[1] = 0;  // Quu-ready counter (8-wave plan)
     L.flag[2] = 0;  // G-done counter (partial B0)
     L.flag[3] = 0;  // P2-done counter (partial B2)
+    L.flag[4] = 0;  // H-done counter (C^T over Zu)
   }
   // ---- terminal: Vxx = Lxx_T (+ xreg I), Vx = Lx_T (+ Vxx fs_T) ------------
   {

@@ -548,13 +548,15 @@ int launch_backward(fddp_handle* h, int mode) {
   }
   switch (h->bwd_variant) {
     case 528: launch_bwd_mfma<5, 2, 8>(h, mode); break;
-    case 524: launch_bwd_mfma<5, 2, 4>(h, mode); break;
     case 318: launch_bwd_mfma<3, 1, 8>(h, mode); break;
     case 314: launch_bwd_mfma<3, 1, 4>(h, mode); break;
     case 218: launch_bwd_mfma<2, 1, 8>(h, mode); break;
     case 214: launch_bwd_mfma<2, 1, 4>(h, mode); break;
     case 118: launch_bwd_mfma<1, 1, 8>(h, mode); break;
     case 114: launch_bwd_mfma<1, 1, 4>(h, mode); break;
+    case 111: launch_bwd_mfma<1, 1, 1>(h, mode); break;
+    case 211: launch_bwd_mfma<2, 1, 1>(h, mode); break;
+    case 311: launch_bwd_mfma<3, 1, 1>(h, mode); break;
     default:
       hipLaunchKernelGGL(backward_kernel<kNT>, dim3(D.B), dim3(kNT), h->bwd_smem, h->stream, D, to_prm(h->prm), mode);
   }
@@ -575,7 +577,12 @@ int setup_bwd_mfma(fddp_handle* h) {
 }
 template <int NTL, int MTL>
 int setup_bwd_mfma_nw(fddp_handle* h, int nw) {
-  return nw == 4 ? setup_bwd_mfma<NTL, MTL, 4>(h) : setup_bwd_mfma<NTL, MTL, 8>(h);
+  if constexpr (NTL + MTL <= 4 && MTL == 1)
+    if (nw == 1) return setup_bwd_mfma<NTL, MTL, 1>(h);
+  // (C^T over Zu, when it needs that, only works with the 8-wave plan's late LDS-DMA)
+  if constexpr (MfmaCfg<NTL, MTL>::ct_own)
+    if (nw == 4) return setup_bwd_mfma<NTL, MTL, 4>(h);
+  return setup_bwd_mfma<NTL, MTL, 8>(h);
 }
 // slot buffers of the parallel line search (generic trials), allocated on first use
 static int ensure_par_slots(fddp_handle* h) {
@@ -925,16 +932,19 @@ int apply_knots(fddp_handle* h, const fddp_knot_desc* knots, const double* param
     const int ntl = (d.ndx + 15) / 16, mtl = (d.nu_max + 15) / 16;
     int v = -1;
     if (uniform_nu && !force_generic) {
+      // eight waves per element (measured round 4: one wave (C3) or four (C2) per element
+      // are slower, 12.1 / 1.06 ms against 3.6 / 0.89 ms); FDDP_BWD_WAVES=1|4 overrides
       const char* ew = std::getenv("FDDP_BWD_WAVES");
-      const int nw = (ew && ew[0] == '4') ? 4 : 8;
+      int nw = 8;
+      if (ew) nw = ew[0] == '1' ? 1 : (ew[0] == '4' ? 4 : 8);
       if (ntl == 5 && mtl == 2) v = setup_bwd_mfma_nw<5, 2>(h, nw);
       else if (ntl == 3 && mtl == 1) v = setup_bwd_mfma_nw<3, 1>(h, nw);
       else if (ntl == 2 && mtl == 1) v = setup_bwd_mfma_nw<2, 1>(h, nw);
       else if (ntl == 1 && mtl == 1) v = setup_bwd_mfma_nw<1, 1>(h, nw);
     }
     h->bwd_variant = v > 0 ? v : 0;
-    // small knots: the one-wave sweep unless a sweep is forced (FDDP_BACKWARD=generic / mfma)
-    if (!env && d.ndx <= kBwdWaveMax && d.nu_max <= kBwdWaveMax) {
+    // the one-wave VALU sweep (bwd_wave.hpp) on request (FDDP_BACKWARD=wave; A/B runs)
+    if (env && std::strcmp(env, "wave") == 0 && d.ndx <= kBwdWaveMax && d.nu_max <= kBwdWaveMax) {
       if (hipFuncSetAttribute((const void*)backward_wave_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)(sizeof(double) * kWavesPerWg * bwd_wave_doubles())) != hipSuccess)
         return fail(FDDP_ERR_RUNTIME, "hipFuncSetAttribute(dynamic LDS) of backward_wave_kernel");

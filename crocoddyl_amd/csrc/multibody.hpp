@@ -1136,7 +1136,8 @@ struct WVals {
 // leave the other waves idle in those phases.
 constexpr int kPartWaves = 4;
 MB_HD __forceinline__ int part_waves(int nt) { return (nt >> 6) < kPartWaves ? (nt >> 6) : kPartWaves; }
-MB_HD __forceinline__ int64_t part_doubles(int nj) { return (int64_t)kPartWaves * 6 * nj; }
+// (6 per dof for the RNEA sums, 10 for the composites)
+MB_HD __forceinline__ int64_t part_doubles(int nj) { return (int64_t)kPartWaves * 10 * nj; }
 
 // lane i < nj: local placement (buffer A starts as liMi), ancestor bits.
 MB_HD inline void w_joint_local(const Blk& b, const WVals& W, const double* q, int i) {
@@ -1255,66 +1256,12 @@ MB_HD inline void w_joint_world(const Blk& b, const WVals& W, int i, bool from_b
   o[5] = Iw[7];
 }
 
-// lane i < nj: composite inertia of the subtree of i in origin form
-// (m, h = m c, I_O = Ic + m (|c|^2 I - c c^T)): additive over the subtree.
 // wave w's contiguous share [w c, (w + 1) c), c = ceil(nj / nw), of nj dofs
 MB_HD __forceinline__ void k_range(int nj, int w, int nw, int& k0, int& k1) {
   const int c = (nj + nw - 1) / nw;
   k0 = w * c;
   k1 = k0 + c < nj ? k0 + c : nj;
 }
-MB_HD inline void w_composite(const Blk& b, const WVals& W, int i, int w = 0, int nw = 1) {
-  double m = 0., h[3] = {0., 0., 0.}, I[6] = {0., 0., 0., 0., 0., 0.};
-  // every body read, the ones outside the subtree weighted 0 (adds of +0: the sums are
-  // unchanged), so the unrolled iterations' LDS loads overlap instead of branching;
-  // nw > 1: wave w's share of the bodies into its partial (W.parts, 10 per dof)
-  int k0 = b.ff ? 5 : 0, k1 = b.nj;
-  if (nw > 1) k_range(b.nj, w, nw, k0, k1);
-  if (b.ff && k0 < 5) k0 = 5;
-#pragma unroll 2
-  for (int k = k0; k < k1; ++k) {
-    const double sel = ((*W.anc(k) >> i) & 1ull) ? 1. : 0.;
-    const double mk = *W.m(k);
-    double c[3], Ic[6];
-    for (int e = 0; e < 3; ++e) c[e] = W.c(k)[e];
-    for (int e = 0; e < 6; ++e) Ic[e] = W.Ic(k)[e];
-    const double cc = c[0] * c[0] + c[1] * c[1] + c[2] * c[2];
-    m += sel * mk;
-    for (int e = 0; e < 3; ++e) h[e] += sel * (mk * c[e]);
-    I[0] += sel * (Ic[0] + mk * (cc - c[0] * c[0]));
-    I[1] += sel * (Ic[1] + mk * (cc - c[1] * c[1]));
-    I[2] += sel * (Ic[2] + mk * (cc - c[2] * c[2]));
-    I[3] += sel * (Ic[3] - mk * c[0] * c[1]);
-    I[4] += sel * (Ic[4] - mk * c[0] * c[2]);
-    I[5] += sel * (Ic[5] - mk * c[1] * c[2]);
-  }
-  if (nw > 1) {
-    double* o = mb_lds(W.parts + 10 * ((int64_t)w * b.nj + i));
-    o[0] = m;
-    for (int e = 0; e < 3; ++e) o[1 + e] = h[e];
-    for (int e = 0; e < 6; ++e) o[4 + e] = I[e];
-    return;
-  }
-  *W.cm(i) = m;
-  for (int e = 0; e < 3; ++e) W.ch(i)[e] = h[e];
-  for (int e = 0; e < 6; ++e) W.cI(i)[e] = I[e];
-}
-// lane i: the composite of dof i from the nw wave partials (wave order); `store`: into W
-MB_HD inline void w_composite_combine(const WVals& W, int i, int nw, bool store) {
-  double v[10];
-  const double* p0 = mb_lds(W.parts + 10 * (int64_t)i);
-  for (int e = 0; e < 10; ++e) v[e] = p0[e];
-  for (int w = 1; w < nw; ++w) {
-    const double* p = mb_lds(W.parts + 10 * ((int64_t)w * W.nj + i));
-    for (int e = 0; e < 10; ++e) v[e] += p[e];
-  }
-  if (store) {
-    *W.cm(i) = v[0];
-    for (int e = 0; e < 3; ++e) W.ch(i)[e] = v[1 + e];
-    for (int e = 0; e < 6; ++e) W.cI(i)[e] = v[4 + e];
-  }
-}
-
 // composite inertia of dof i's subtree times a motion x: (m v - h x w, I_O w + h x v)
 MB_HD __forceinline__ void comp_mul(const WVals& W, int i, const double* x, double* o) {
   const double m = *W.cm(i);
@@ -1414,13 +1361,17 @@ MB_HD inline void w_joint_force(const Blk& b, const WVals& W, double* tau, int i
 // from the origin) are the difference of terms ~ m |c|^2 ~ 0.3, which cost ~3 digits of
 // M and, through cond(M) ~ 1e6, of M^-1 and Fu (the round-4 parity trace); at P the
 // lever arms are the link's own size.
-MB_HD inline void w_crba_column(const Blk& b, const WVals& W, int j, double* A, int lda, int w = 0, int nw = 1) {
+// Phase 1 (lane j of wave w < nw): wave w's share of j's subtree bodies into its
+// partial (W.parts, 10 per dof: m, h, I about P_j), as w_composite.
+MB_HD inline void w_crba_composite_part(const Blk& b, const WVals& W, int j, int w, int nw) {
   double P[3], m = 0., h[3] = {0., 0., 0.}, I[6] = {0., 0., 0., 0., 0., 0.};
   for (int e = 0; e < 3; ++e) P[e] = W.op(j)[e];
-  // composite of j's subtree about P (every body read, the others weighted 0, as
-  // w_composite; each wave forms the whole sum: the loads are wave-uniform broadcasts)
+  int k0 = b.ff ? 5 : 0, k1 = b.nj;
+  if (nw > 1) k_range(b.nj, w, nw, k0, k1);
+  if (b.ff && k0 < 5) k0 = 5;
+  // (every body of the share read, the others weighted 0: the loads overlap)
 #pragma unroll 2
-  for (int k = b.ff ? 5 : 0; k < b.nj; ++k) {
+  for (int k = k0; k < k1; ++k) {
     const double sel = ((*W.anc(k) >> j) & 1ull) ? 1. : 0.;
     const double mk = *W.m(k);
     double c[3], Ic[6];
@@ -1436,43 +1387,75 @@ MB_HD inline void w_crba_column(const Blk& b, const WVals& W, int j, double* A, 
     I[4] += sel * (Ic[4] - mk * c[0] * c[2]);
     I[5] += sel * (Ic[5] - mk * c[1] * c[2]);
   }
-  // S_i shifted to P: a revolute dof's axis w through p_i moves P at w x (P - p_i)
-  auto shifted = [&](int i, double* s) {
-    double wv[3], d[3];
-    const bool pr = dof_prismatic(b, i);
-    for (int e = 0; e < 3; ++e) {
-      wv[e] = W.S(i)[pr ? e : 3 + e];
-      d[e] = P[e] - W.op(i)[e];
+  double* o = mb_lds(W.parts + 10 * ((int64_t)w * b.nj + j));
+  o[0] = m;
+  for (int e = 0; e < 3; ++e) o[1 + e] = h[e];
+  for (int e = 0; e < 6; ++e) o[4 + e] = I[e];
+}
+// Phase 2 (lane j of wave w of nw): the partials of the npw waves combined in wave order,
+// F = Ic_j S_j about P_j, M_ij = S_i(P_j) . F for the ancestors-or-self i < j of j (+
+// armature on the diagonal), the rows i < j split in nw contiguous ranges, one per wave.
+// A: ld lda, zeroed.
+// store_world: wave 0 also stores the subtree composite about the world origin (W.cm /
+// ch / cI, the calcDiff's recursions): h_O = h + m P, I_O = I + 2 (h.P) 1 - (h P^T +
+// P h^T) + m (|P|^2 1 - P P^T) (the same terms as summing the bodies about the origin).
+MB_HD inline void w_crba_column(const Blk& b, const WVals& W, int j, double* A, int lda, int w, int nw, int npw,
+                                bool store_world = false) {
+  double P[3], v[10];
+  for (int e = 0; e < 3; ++e) P[e] = W.op(j)[e];
+  {
+    const double* p0 = mb_lds(W.parts + 10 * (int64_t)j);
+    for (int e = 0; e < 10; ++e) v[e] = p0[e];
+    for (int ww = 1; ww < npw; ++ww) {
+      const double* p = mb_lds(W.parts + 10 * ((int64_t)ww * b.nj + j));
+      for (int e = 0; e < 10; ++e) v[e] += p[e];
     }
-    if (pr) {
-      for (int e = 0; e < 3; ++e) {
-        s[e] = wv[e];
-        s[3 + e] = 0.;
-      }
-    } else {
-      cross3(wv, d, s);
-      for (int e = 0; e < 3; ++e) s[3 + e] = wv[e];
-    }
-  };
-  double Sj[6], F[6], t[3];
-  shifted(j, Sj);
+  }
+  const double m = v[0];
+  const double* h = v + 1;
+  const double* I = v + 4;
+  if (store_world && w == 0) {
+    const double hp = h[0] * P[0] + h[1] * P[1] + h[2] * P[2], pp = P[0] * P[0] + P[1] * P[1] + P[2] * P[2];
+    *W.cm(j) = m;
+    for (int e = 0; e < 3; ++e) W.ch(j)[e] = h[e] + m * P[e];
+    // (I ordering: xx, yy, zz, xy, xz, yz)
+    W.cI(j)[0] = I[0] + 2. * (hp - h[0] * P[0]) + m * (pp - P[0] * P[0]);
+    W.cI(j)[1] = I[1] + 2. * (hp - h[1] * P[1]) + m * (pp - P[1] * P[1]);
+    W.cI(j)[2] = I[2] + 2. * (hp - h[2] * P[2]) + m * (pp - P[2] * P[2]);
+    W.cI(j)[3] = I[3] - (h[0] * P[1] + P[0] * h[1]) - m * P[0] * P[1];
+    W.cI(j)[4] = I[4] - (h[0] * P[2] + P[0] * h[2]) - m * P[0] * P[2];
+    W.cI(j)[5] = I[5] - (h[1] * P[2] + P[1] * h[2]) - m * P[1] * P[2];
+  }
+  // S_i shifted to P: [S_i.lin + S_i.ang x P; S_i.ang] (a revolute dof's axis w through
+  // p_i moves P at w x (P - p_i) = S_i.lin + w x P; a prismatic dof has S_i.ang = 0).
+  // The products are dimension-one in the lever arms, so forming them from the world-origin
+  // S_i costs only the rounding of the placements (unlike the quadratic m |c|^2 terms).
+  // Scalars throughout: a shifted-S array written under a branch lands in scratch memory.
+  const double* Sjw = W.S(j);
+  const double sj3 = Sjw[3], sj4 = Sjw[4], sj5 = Sjw[5];
+  const double sj0 = Sjw[0] + (sj4 * P[2] - sj5 * P[1]);
+  const double sj1 = Sjw[1] + (sj5 * P[0] - sj3 * P[2]);
+  const double sj2 = Sjw[2] + (sj3 * P[1] - sj4 * P[0]);
   // F = Ic_j S_j about P: (m v - h x w, I w + h x v)
-  cross3(h, Sj + 3, t);
-  for (int e = 0; e < 3; ++e) F[e] = m * Sj[e] - t[e];
-  cross3(h, Sj, t);
-  F[3] = I[0] * Sj[3] + I[3] * Sj[4] + I[4] * Sj[5] + t[0];
-  F[4] = I[3] * Sj[3] + I[1] * Sj[4] + I[5] * Sj[5] + t[1];
-  F[5] = I[4] * Sj[3] + I[5] * Sj[4] + I[2] * Sj[5] + t[2];
-  if (w == 0) A[(int64_t)j * lda + j] = dot6(Sj, F) + b.arm[j];
+  const double F0 = m * sj0 - (h[1] * sj5 - h[2] * sj4);
+  const double F1 = m * sj1 - (h[2] * sj3 - h[0] * sj5);
+  const double F2 = m * sj2 - (h[0] * sj4 - h[1] * sj3);
+  const double F3 = I[0] * sj3 + I[3] * sj4 + I[4] * sj5 + (h[1] * sj2 - h[2] * sj1);
+  const double F4 = I[3] * sj3 + I[1] * sj4 + I[5] * sj5 + (h[2] * sj0 - h[0] * sj2);
+  const double F5 = I[4] * sj3 + I[5] * sj4 + I[2] * sj5 + (h[0] * sj1 - h[1] * sj0);
+  if (w == 0) A[(int64_t)j * lda + j] = (sj0 * F0 + sj1 * F1 + sj2 * F2) + (sj3 * F3 + sj4 * F4 + sj5 * F5) + b.arm[j];
   const Mask am = *W.anc(j);
   const int ch = (j + nw - 1) / nw, i0 = w * ch, i1 = i0 + ch < j ? i0 + ch : j;
   // every i < j visited, the non-ancestors storing their zero (only lane j writes the
   // pair {i, j}), so the loop has no branch and the unrolled loads overlap
 #pragma unroll 2
   for (int i = i0; i < i1; ++i) {
-    double Si[6];
-    shifted(i, Si);
-    const double d = dot6(Si, F);
+    const double* Si = W.S(i);
+    const double a3 = Si[3], a4 = Si[4], a5 = Si[5];
+    const double l0 = Si[0] + (a4 * P[2] - a5 * P[1]);
+    const double l1 = Si[1] + (a5 * P[0] - a3 * P[2]);
+    const double l2 = Si[2] + (a3 * P[1] - a4 * P[0]);
+    const double d = (l0 * F0 + l1 * F1 + l2 * F2) + (a3 * F3 + a4 * F4 + a5 * F5);
     const double Mij = ((am >> i) & 1ull) ? d : 0.;
     A[(int64_t)j * lda + i] = Mij;
     A[(int64_t)i * lda + j] = Mij;
@@ -2005,7 +1988,7 @@ MB_HD __attribute__((always_inline)) inline void contact_jac_lane(const Blk& b, 
 // the phase after the kinematics (nullptr-like no-op allowed).
 template <class X, class CostF>
 MB_HD inline void world_kinematics(const X& ex, const Blk& b, const WVals& W, const double* q, double* A, int lda,
-                                   CostF costs, bool split_composite = false) {
+                                   CostF costs, bool world_composite = false) {
   const int nj = b.nj;
   ex.run([&](int lane) {
     if (lane < nj) w_joint_local(b, W, q, lane);
@@ -2016,25 +1999,19 @@ MB_HD inline void world_kinematics(const X& ex, const Blk& b, const WVals& W, co
       w_joint_world(b, W, lane, false);
     }
   });
-  if (split_composite) {  // (no cost work alongside) the composites over the waves
-    const int nw = part_waves(ex.nt);
-    ex.run([&](int lane) {
-      const int w = lane >> 6, l = lane & 63;
-      if (l < nj && w < nw) w_composite(b, W, l, w, nw);
-    });
-    ex.run([&](int lane) {
-      if (lane < nj) w_composite_combine(W, lane, nw, true);
-    });
-  } else {
-    ex.run([&](int lane) {
-      const int wave = lane >> 6, l = lane & 63;
-      if (wave == 0 && l < nj) w_composite(b, W, l);
-      if (wave >= 1) costs(wave, l);
-    });
-  }
+  // CRBA about each column's joint: the subtree composites in wave partials (beside them,
+  // the cost records on waves >= 1), then the columns (rows split over all the waves); with
+  // `world_composite` (the calcDiff) the columns' lanes also store the subtree composites
+  // about the world origin
+  const int npw = part_waves(ex.nt);
   ex.run([&](int lane) {
     const int w = lane >> 6, j = lane & 63;
-    if (j < nj) w_crba_column(b, W, j, A, lda, w, ex.nt >> 6);
+    if (j < nj && w < npw) w_crba_composite_part(b, W, j, w, npw);
+    if (w >= 1) costs(w, j);
+  });
+  ex.run([&](int lane) {
+    const int w = lane >> 6, j = lane & 63;
+    if (j < nj) w_crba_column(b, W, j, A, lda, w, ex.nt >> 6, npw, world_composite);
   });
 }
 
