@@ -1168,7 +1168,11 @@ __device__ __forceinline__ bool bwd_knot(const Dev& D, const BwdLds& L, int b, i
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if (lane == 0) __hip_atomic_fetch_add(L.flag + 3, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
-  if constexpr (P.owns_x(W)) {
+  // With C^T over Zu (!ct_own) the next knot's LDS-DMA into Zu must also wait for every
+  // C^T read (the K products of the x-block owners, wave 0's k): the waves that only
+  // signal would otherwise issue it while those still run (a race seen as 1 in 256 solves
+  // differing between trial-group sizes)
+  if constexpr (P.owns_x(W) || (!Cfg::ct_own && NW == 8)) {
     const int target = (P.xwaves + (P.owns_x(0) ? 0 : 1)) * (D.T - t);
     while (__hip_atomic_load(L.flag + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target)
       __builtin_amdgcn_s_sleep(1);

@@ -268,16 +268,24 @@ __device__ __forceinline__ void mb_knot_body(const Dev& D, int sel_calc, int sel
   // the parameter block is read in every phase: stage it in LDS (D.mbp doubles, after the work area)
   const double* Pg = D.pblock(b, t);
   double* P = sm + D.mbd;
+  // this thread's x / u entries loaded beside the parameter block (the knot's first
+  // phase stores them: one global round trip fewer on its critical path)
+  double xu[2] = {0., 0.};
+  const bool pre = D.nx <= NT;
+  if (pre) {
+    if ((int)threadIdx.x < D.nx) xu[0] = xg[threadIdx.x];
+    if (ug && (int)threadIdx.x < D.m) xu[1] = ug[threadIdx.x];
+  }
   const int psz = (int)Pg[3];
   for (int e = threadIdx.x; e < psz; e += NT) P[e] = Pg[e];
   __syncthreads();
   if (do_diff)
     mb::knot_calc_diff<NT>(P, D.nx, D.m, xg, ug, running && kd.nu > 0, sm, D.Fx + kk * D.sNN, D.Fu + kk * D.sNM,
                        D.Lxx + kk * D.sNN, D.Lxu + kk * D.sNM, D.Luu + kk * D.sMM, D.Lx + kk * D.sN,
-                       D.Lu + kk * D.sM, xn, cost);
+                       D.Lu + kk * D.sM, xn, cost, pre ? xu : nullptr);
   else
     mb::knot_calc_diff<NT>(P, D.nx, D.m, xg, ug, running && kd.nu > 0, sm, nullptr, nullptr, nullptr, nullptr, nullptr,
-                       nullptr, nullptr, xn, cost);
+                       nullptr, nullptr, xn, cost, pre ? xu : nullptr);
 }
 // Two register budgets of the same kernel: 2 waves/EU (256 VGPRs, a few spills) lets two
 // workgroups share a CU where the LDS plan allows it (<= 80 KB: the trot, the arm); when

@@ -1986,12 +1986,14 @@ MB_HD __attribute__((always_inline)) inline void contact_jac_lane(const Blk& b, 
 // Placements, world quantities, composite inertias and M (into A, zeroed by
 // the caller) for configuration q; `costs(wave, l)` runs on waves >= 1 in
 // the phase after the kinematics (nullptr-like no-op allowed).
-template <class X, class CostF>
+// `early(wave, l)` runs on waves >= 1 beside the local placements (work on x / u only).
+template <class X, class EarlyF, class CostF>
 MB_HD inline void world_kinematics(const X& ex, const Blk& b, const WVals& W, const double* q, double* A, int lda,
-                                   CostF costs, bool world_composite = false) {
+                                   EarlyF early, CostF costs, bool world_composite = false) {
   const int nj = b.nj;
   ex.run([&](int lane) {
     if (lane < nj) w_joint_local(b, W, q, lane);
+    if (lane >= 64) early(lane >> 6, lane & 63);
   });
   ex.run([&](int lane) {
     if (lane < nj) {
@@ -2106,25 +2108,40 @@ MB_HD __forceinline__ double knot_calc_x(const X& ex, const double* P, int nx, c
     if (lane < nu) ub[lane] = use_u ? u[lane] : 0.;
     for (int e = lane; e < lda * ncol; e += ex.nt) A[e] = 0.;
   });
-  // once the placements exist: the wide records (state / control residuals) row-parallel
-  // on waves 3 and 1, their lane partials into pb (free until the Gauss-Jordan); the
-  // other records one per lane of wave 2
+  // the wide records (state / control residuals: x, u only) row-parallel on waves 3 and 1
+  // beside the local placements, their lane partials into pb (free until the
+  // Gauss-Jordan); once the placements exist, the other records one per lane of wave 2
   world_kinematics(ex, b, W, x, A, lda, [&](int wave, int l) {
     const double* cr = b.C;
-    int nn = 0, nw = 0;
+    int nw = 0;
     for (int k = 0; k < b.ncost; ++k) {
       const CRec C{cr};
       if (wide_cost(C, nw)) {
         if (wave == (nw == 0 ? 3 : 1)) pb[64 * nw + l] = cost_activation_part(b, C, x, ub, nu, l, 64);
         ++nw;
+      }
+      cr += C.size();
+    }
+  }, [&](int wave, int l) {
+    // the other records, then the contacts' position terms (log6 for the 6D ones): item
+    // i on lane i / 3 of wave 1 + i % 3, so that no wave runs two of them (a wave pays
+    // for the sum of its divergent lanes' paths)
+    if (wave > 3) return;
+    const int item = 3 * l + (wave - 1);
+    const double* cr = b.C;
+    int nn = 0, nw = 0;
+    for (int k = 0; k < b.ncost; ++k) {
+      const CRec C{cr};
+      if (wide_cost(C, nw)) {
+        ++nw;
       } else {
-        if (wave == 2 && l == nn) cv[k] = C.weight() * cost_activation(b, W, C, x, ub, nu, false);
+        if (item == nn) cv[k] = C.weight() * cost_activation(b, W, C, x, ub, nu, false);
         ++nn;
       }
       cr += C.size();
     }
-    const int kc = l - 32;  // contact position terms on the upper half of wave 2
-    if (!imp && wave == 2 && kc >= 0 && kc < b.ncon) {
+    const int kc = item - nn;
+    if (!imp && kc >= 0 && kc < b.ncon) {
       int row0;
       const CRec C{contact_rec(b, kc, &row0)};
       contact_a0_position(b, W, C, a0 + row0);
@@ -2864,14 +2881,23 @@ __device__ __forceinline__ void subtree_nh_mfma(const Blk& b, const WVals& W, co
     const int ti = tile / tc, tj = tile - ti * tc;
     const int j = 16 * ti + li, c = 16 * tj + li;
     mb_f64x4 acc = {0., 0., 0., 0.};
-#pragma unroll 2
-    for (int kb = 0; kb < nj; kb += 4) {
-      const int bb = kb + lk;
-      const bool bv_ok = bb < nj && c < 42;
-      const int bs = bb < nj ? bb : 0;
-      const double nv = nb[42 * bs + (c < 42 ? c : 0)];
-      const bool in = bb < nj && j < nj && carries_body(b, bs) && ((*W.anc(bs) >> j) & 1ull);
-      acc = mb_mfma(in ? 1. : 0., bv_ok ? nv : 0., acc);
+    // the k-steps in chunks of 8: every operand of a chunk loaded first, then its MFMA
+    // chain (one LDS round trip per chunk, not per k-step)
+#pragma unroll 1
+    for (int k0 = 0; k0 < nj; k0 += 32) {
+      double av[8], bv[8];
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        const int bb = k0 + 4 * s + lk;
+        const int bs = bb < nj ? bb : 0;
+        const double nv = nb[42 * bs + (c < 42 ? c : 0)];
+        const bool in = bb < nj && j < nj && carries_body(b, bs) && ((*W.anc(bs) >> j) & 1ull);
+        av[s] = in ? 1. : 0.;
+        bv[s] = bb < nj && c < 42 ? nv : 0.;
+      }
+#pragma unroll
+      for (int s = 0; s < 8; ++s)
+        if (k0 + 4 * s < nj) acc = mb_mfma(av[s], bv[s], acc);
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -2886,7 +2912,7 @@ template <class X>
 MB_HD __forceinline__ void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, const double* xg, const double* ug,
                                    bool use_u, double* w, double* Fx, double* Fu, double* Lxx, double* Lxu,
                                    double* Luu, double* Lx, double* Lu, double* xnext_out = nullptr,
-                                   double* cost_out = nullptr) {
+                                   double* cost_out = nullptr, const double* xu_pre = nullptr) {
   w = ex.lds(w);  // the work area and the parameter block live in LDS
   P = ex.lds(P);
   const Blk b = parse(P);
@@ -2925,15 +2951,22 @@ MB_HD __forceinline__ void knot_calc_diff_x(const X& ex, const double* P, int nx
   double* fx = w + l.fx;
   double* zv = w + l.zv;
   ex.run([&](int lane) {
-    for (int e = lane; e < nq + nj; e += ex.nt) x[e] = xg[e];
-    if (lane < nj) u[lane] = (use_u && lane < nu) ? ug[lane] : 0.;  // (impulse: a zero velocity)
+    // xu_pre (device, nq + nj <= nt): this thread's x[lane] / u[lane] loaded by the caller
+    // beside the parameter-block copy (one global round trip instead of two)
+    if (xu_pre) {
+      if (lane < nq + nj) x[lane] = xu_pre[0];
+      if (lane < nj) u[lane] = (use_u && lane < nu) ? xu_pre[1] : 0.;
+    } else {
+      for (int e = lane; e < nq + nj; e += ex.nt) x[e] = xg[e];
+      if (lane < nj) u[lane] = (use_u && lane < nu) ? ug[lane] : 0.;  // (impulse: a zero velocity)
+    }
     // the identity half of [M | I] (the CRBA writes every entry of M); the device
     // inverts M in place and needs none
     if (!mb_inv_inplace(ex))
       for (int e = lane; e < nj * lda; e += ex.nt) A[(int64_t)nj * lda + e] = e % lda == e / lda ? 1. : 0.;
   });
   // world-frame kinematics, M into the left half of [M | I], nle
-  world_kinematics(ex, b, W, x, A, lda, [](int, int) {}, true);
+  world_kinematics(ex, b, W, x, A, lda, [](int, int) {}, [](int, int) {}, true);
   if (!imp) world_rnea(ex, b, W, x + nq, nullptr, nle);
   if (nc > 0)  // contact rows at the drift (ddq = 0; ContactModelMultiple::calc)
     ex.run([&](int lane) {
@@ -3614,9 +3647,10 @@ MB_HD __forceinline__ void knot_calc_diff_x(const X& ex, const double* P, int nx
 template <int NT>
 __device__ __forceinline__ void knot_calc_diff(const double* P, int nx, int m, const double* xg, const double* ug, bool use_u,
                                       double* w, double* Fx, double* Fu, double* Lxx, double* Lxu, double* Luu,
-                                      double* Lx, double* Lu, double* xnext_out, double* cost_out) {
+                                      double* Lx, double* Lu, double* xnext_out, double* cost_out,
+                                      const double* xu_pre = nullptr) {
   static_assert(NT >= 128 && NT % 64 == 0, "the calcDiff phases take >= 2 waves");
-  knot_calc_diff_x(DevExec{NT}, P, nx, m, xg, ug, use_u, w, Fx, Fu, Lxx, Lxu, Luu, Lx, Lu, xnext_out, cost_out);
+  knot_calc_diff_x(DevExec{NT}, P, nx, m, xg, ug, use_u, w, Fx, Fu, Lxx, Lxu, Luu, Lx, Lu, xnext_out, cost_out, xu_pre);
 }
 
 }  // namespace mb

@@ -1,5 +1,7 @@
-// Micro-benchmark (diagnostic): cycles of one sym_sweep_inverse<32> (the
-// backward sweep's Quu^-1 on wave 0) in isolation, one wave per workgroup.
+// Micro-benchmark (diagnostic): cycles of the backward sweep's Quu factorisations on
+// wave 0 in isolation, one wave per workgroup: variant 0 sym_sweep_inverse<32> (the
+// explicit inverse, round 3), 1 chol_inv_sweep<32>, 2 chol_inv_blocked2 (round 4),
+// 3 chol_inv_sweep<16> on the leading 16 x 16 block.
 // Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -o tools/sweep_bench tools/sweep_bench.hip
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -7,19 +9,22 @@
 #include <cmath>
 #include "../crocoddyl_amd/csrc/bwd_mfma.hpp"
 
-__global__ void k_sweep(const double* Q, double* Qi_out, unsigned long long* cyc, int reps, int m) {
-  __shared__ double Quu[32 * 32], Qi[32 * 32], rb[64];
+__global__ void k_sweep(const double* Q, double* Qi_out, unsigned long long* cyc, int reps, int m, int variant) {
+  __shared__ double Quu[32 * 32], Qi[32 * 32], Ct[32 * 33], rb[64];
   const int lane = threadIdx.x;
   for (int e = lane; e < 1024; e += 64) Quu[e] = Q[e];
   __syncthreads();
   unsigned long long t0 = __builtin_amdgcn_s_memtime();
   bool bad = false;
   for (int r = 0; r < reps; ++r) {
-#ifdef SWEEP_BLK
-    bad |= fddp::sym_sweep_inverse_blk<32, 32>(Quu, Qi, rb, m, lane);
-#else
-    bad |= fddp::sym_sweep_inverse<32, 32>(Quu, Qi, rb, m, lane);
-#endif
+    if (variant == 0)
+      bad |= fddp::sym_sweep_inverse<32, 32>(Quu, Qi, rb, m, lane);
+    else if (variant == 1)
+      bad |= fddp::chol_inv_sweep<32, 32, 33>(Quu, Qi, Ct, rb, m, lane, nullptr, 0);
+    else if (variant == 2)
+      bad |= fddp::chol_inv_blocked2<32, 33>(Quu, Qi, Ct, rb, m, lane, nullptr, 0);
+    else
+      bad |= fddp::chol_inv_sweep<16, 32, 33>(Quu, Qi, Ct, rb, m < 16 ? m : 16, lane, nullptr, 0);
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   unsigned long long t1 = __builtin_amdgcn_s_memtime();
@@ -64,22 +69,30 @@ int main() {
   hipMalloc(&dQi, sizeof(double) * 1024 * 256);
   hipMalloc(&dc, 8 * 256);
   hipMemcpy(dQ, Q, sizeof(Q), hipMemcpyHostToDevice);
-  for (int blocks : {1, 256}) {
-    k_sweep<<<blocks, 64>>>(dQ, dQi, dc, 20, m);
-    hipDeviceSynchronize();
-    unsigned long long c[256];
-    hipMemcpy(c, dc, 8 * blocks, hipMemcpyDeviceToHost);
-    double Qi[1024];
-    hipMemcpy(Qi, dQi, sizeof(Qi), hipMemcpyDeviceToHost);
-    double err = 0;
-    for (int i = 0; i < m; ++i)
-      for (int j = 0; j < m; ++j) {
-        double s = 0;
-        for (int k = 0; k < m; ++k) s += Q[k * 32 + i] * Qi[j * 32 + k];
-        err = fmax(err, fabs(s - (i == j)));
-      }
-    printf("blocks=%d: %llu cycles per 32x32 inverse (%.0f per pivot), |Q Qi - I| = %.2e\n", blocks, c[0],
-           c[0] / 32.0, err);
-  }
+  for (int variant = 0; variant < 4; ++variant)
+    for (int blocks : {1, 256}) {
+      k_sweep<<<blocks, 64>>>(dQ, dQi, dc, 20, m, variant);
+      hipDeviceSynchronize();
+      unsigned long long c[256];
+      hipMemcpy(c, dc, 8 * blocks, hipMemcpyDeviceToHost);
+      double Qi[1024];
+      hipMemcpy(Qi, dQi, sizeof(Qi), hipMemcpyDeviceToHost);
+      // variant 0: |Q Qi - I|; 1, 2: |C Q C^T - I| (C = L^-1); 3: on the leading 16 block
+      const int mm = variant == 3 ? 16 : m;
+      double err = 0;
+      for (int i = 0; i < mm; ++i)
+        for (int j = 0; j < mm; ++j) {
+          double s = 0;
+          if (variant == 0) {
+            for (int k = 0; k < mm; ++k) s += Q[k * 32 + i] * Qi[j * 32 + k];
+          } else {
+            for (int k = 0; k < mm; ++k)
+              for (int l = 0; l < mm; ++l) s += Qi[k * 32 + i] * Q[l * 32 + k] * Qi[l * 32 + j];
+          }
+          err = fmax(err, fabs(s - (i == j)));
+        }
+      printf("variant %d blocks=%d: %llu cycles (%.0f per pivot), residual %.2e\n", variant, blocks, c[0],
+             c[0] / (double)mm, err);
+    }
   return 0;
 }
