@@ -1,10 +1,10 @@
-# round 3 closing profile of the C5 bench (fixed protocol): a rocprofv3 kernel trace of
+# closing profile of the C5 bench (fixed protocol): a rocprofv3 kernel trace of
 # exactly the timed steps (trace_window.py keeps the last STEPS solves), then the HBM
 # and MFMA counters in separate --pmc passes (FETCH_SIZE and WRITE_SIZE cannot share
 # one). Summarised into profiles/ by tools/prof_summary.py.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-O=gpurun_out/prof
+O=gpurun_out/prof${PROF_TAG:+_$PROF_TAG}
 rm -rf $O
 mkdir -p $O
 export TMPDIR=/tmp
