@@ -30,6 +30,8 @@
 // Parameter-block layout: include/fddp_hip.h (FDDP_KNOT_EULER_FREEFWD).
 #pragma once
 
+#include <type_traits>
+
 #include "fddp_device.hpp"
 
 // Everything except the workgroup drivers (knot_calc, knot_calc_diff,
@@ -507,6 +509,46 @@ __device__ __forceinline__ bool gauss_jordan_dev(double* A, int nr, int ld, int 
 }
 
 // v from lane l (uniform l) of the wave, as a scalar
+// lane n of every row of 16 lanes, to the whole row (DPP row_newbcast: a VALU move, no
+// LDS-crossbar round trip as __shfl's ds_bpermute); n a compile-time constant
+template <int N>
+__device__ __forceinline__ double row_bcast_d(double v) {
+  const long long bits = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)bits, 0x150 + N, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(bits >> 32), 0x150 + N, 0xf, 0xf, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+template <int I = 0>
+__device__ __forceinline__ double row_bcast_d(double v, int n) {  // n in [I, 16), unrolled
+  if constexpr (I < 15) {
+    if (n != I) return row_bcast_d<I + 1>(v, n);
+  }
+  return row_bcast_d<I>(v);
+}
+// row r (lanes 16 r .. 16 r + 15) of a wave to all four rows, lane for lane (= __shfl(v,
+// (lane & 15) + 16 r)) by two permlane swaps per half (gfx950 v_permlane16/32_swap: odd
+// rows of the first operand with even rows of the second; upper 32 lanes of the first
+// with lower 32 of the second)
+template <int R>
+__device__ __forceinline__ int row_to_all_i(int h) {
+  const auto a = __builtin_amdgcn_permlane16_swap(h, h, false, false);  // rows [0,0,2,2] | [1,1,3,3]
+  const int t = (R & 1) ? a[1] : a[0];
+  const auto c = __builtin_amdgcn_permlane32_swap(t, t, false, false);  // [t0,t1,t0,t1] | [t2,t3,t2,t3]
+  return (R & 2) ? c[1] : c[0];
+}
+template <int R>
+__device__ __forceinline__ double row_to_all_d(double v) {
+  const long long bits = __double_as_longlong(v);
+  const int lo = row_to_all_i<R>((int)bits), hi = row_to_all_i<R>((int)(bits >> 32));
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+template <int I = 0>
+__device__ __forceinline__ double row_to_all_d(double v, int r) {  // r in [I, 4), unrolled
+  if constexpr (I < 3) {
+    if (r != I) return row_to_all_d<I + 1>(v, r);
+  }
+  return row_to_all_d<I>(v);
+}
 __device__ __forceinline__ double readlane_d(double v, int l) {
   const long long bits = __double_as_longlong(v);
   const int lo = __builtin_amdgcn_readlane((int)bits, l);
@@ -657,6 +699,17 @@ __device__ __forceinline__ bool gj_mfma(double* A_, int nr, int ld, int nc, bool
     const double x = A[(v ? r : 0) + ld * (v ? c : 0)];
     return v ? x : 0.;
   };
+  // Without side work or the inverse's trailing column updates (mb_solve), the per-step
+  // workgroup barrier is replaced by a progress counter: step k + 1 needs tile k + 1 as
+  // updated by step k (its sweep reads the diagonal block, every wave's update its
+  // column), and nothing else another wave writes — a pivot tile is never written again
+  // once passed — so only its owner is waited for, and the other waves' updates of the
+  // later tiles overlap the next sweep.
+  constexpr bool kNoSide = std::is_same<Side, GjNoSide>::value;
+  const bool flagged = kNoSide && !inverse;
+  int* prog = flag + 1;   // diagonal block of tile k ready (its sweep may start)
+  int* prog2 = flag + 2;  // all of tile k ready (the updates may read it)
+  if (flagged && tid == 0) *prog = *prog2 = 0;
   __syncthreads();
   MB_GJ_MARK(0);
   bool bad = false;
@@ -689,6 +742,10 @@ __device__ __forceinline__ bool gj_mfma(double* A_, int nr, int ld, int nc, bool
   for (int k = 0; k < nbr; ++k) {
     const int r0 = 16 * k;
     double d[4] = {0., 0., 0., 0.};
+    if (flagged && k > 0 && wave < nct) {  // tile k updated through step k - 1
+      while (__hip_atomic_load(prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < k) __builtin_amdgcn_s_sleep(1);
+      asm volatile("" ::: "memory");
+    }
     // A: only the waves that own a column tile need N (one sweep per SIMD, not two);
     // the padding pivots beyond nr are skipped (their identity rows stay +1, which only
     // ever multiplies the zero-loaded padding)
@@ -704,10 +761,10 @@ __device__ __forceinline__ bool gj_mfma(double* A_, int nr, int ld, int nc, bool
         if (r0 + p < nr) {  // (uniform; the loop stays fully unrolled, d[] static)
           const int pq = p >> 2, pg = p & 3;
           const double app = readlane_d(d[pq], p + 16 * pg);
-          const double aip = __shfl(d[pq], li + 16 * pg);
+          const double aip = row_to_all_d(d[pq], pg);  // = __shfl(d[pq], li + 16 pg)
           double apc[4];
 #pragma unroll
-          for (int q = 0; q < 4; ++q) apc[q] = __shfl(d[q], p + 16 * lk);
+          for (int q = 0; q < 4; ++q) apc[q] = row_bcast_d(d[q], p);  // = __shfl(d[q], p + 16 lk)
           bad = bad || !(app > 0.);
           // 1 / app from v_rcp_f64 (relative error up to ~2^-23) corrected to working
           // precision in three dependent fmas: with e = 1 - app x0, x0 (1 + e + e^2) has
@@ -738,6 +795,10 @@ __device__ __forceinline__ bool gj_mfma(double* A_, int nr, int ld, int nc, bool
       }
     }
     MB_GJ_MARK(1 + 3 * k);
+    if (flagged && k > 0 && wave < nct) {  // all of tile k updated through step k - 1
+      while (__hip_atomic_load(prog2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < k) __builtin_amdgcn_s_sleep(1);
+      asm volatile("" ::: "memory");
+    }
 #pragma unroll 1
     for (int j = wave; j < nct; j += nw) {
       if (inverse && j == k - 1) col_update(j, Np);
@@ -746,8 +807,10 @@ __device__ __forceinline__ bool gj_mfma(double* A_, int nr, int ld, int nc, bool
       f64x4 R = {0., 0., 0., 0.};
 #pragma unroll
       for (int q = 0; q < 4; ++q) R = __builtin_amdgcn_mfma_f64_16x16x4f64(d[q], at(r0 + lk + 4 * q, pc), R, 0, 0, 0);
+      // row blocks from k + 1 on (rotated): the next pivot tile's diagonal block first
 #pragma unroll 1
-      for (int i = 0; i < nbr; ++i) {
+      for (int ii = 0; ii < nbr; ++ii) {
+        const int i = ii + k + 1 < nbr ? ii + k + 1 : ii + k + 1 - nbr;
         if (i == k) continue;
         f64x4 acc;
 #pragma unroll
@@ -762,18 +825,26 @@ __device__ __forceinline__ bool gj_mfma(double* A_, int nr, int ld, int nc, bool
           const int r = 16 * i + lk + 4 * q;
           if (r < nr && pc >= 0 && pc < nc) A[r + ld * pc] = acc[q];
         }
+        if (flagged && j == k + 1 && i == k + 1) {  // the next sweep's block is ready
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          if (lane == 0) __hip_atomic_store(prog, k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
       }
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int r = r0 + lk + 4 * q;
         if (r < nr && pc >= 0 && pc < nc) A[r + ld * pc] = -R[q];
       }
+      if (flagged && j == k + 1) {  // the whole next pivot tile is ready
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane == 0) __hip_atomic_store(prog2, k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) Np[q] = d[q];
     if (wave >= nct) side(k, tid - 64 * nct, (nw - nct) * 64);
     MB_GJ_MARK(2 + 3 * k);
-    __syncthreads();
+    if (!flagged) __syncthreads();
     MB_GJ_MARK(3 + 3 * k);
   }
   if (inverse)
@@ -1261,6 +1332,17 @@ MB_HD __forceinline__ void k_range(int nj, int w, int nw, int& k0, int& k1) {
   const int c = (nj + nw - 1) / nw;
   k0 = w * c;
   k1 = k0 + c < nj ? k0 + c : nj;
+}
+// Per-record work on one lane each, from the top of the workgroup down: record k on
+// lane nt - 1 - 64 (k mod W) - k / W (W waves), i.e. one record per wave before any wave
+// takes a second (a wave runs its divergent lanes' paths one after another).
+MB_HD __forceinline__ int spread_lane(int k, int nt) {
+  const int nwv = nt >> 6;
+  return nt - 1 - 64 * (k % nwv) - k / nwv;
+}
+MB_HD __forceinline__ int spread_item(int lane, int nt) {
+  const int u = nt - 1 - lane, nwv = nt >> 6;
+  return (u & 63) * nwv + (u >> 6);
 }
 // composite inertia of dof i's subtree times a motion x: (m v - h x w, I_O w + h x v)
 MB_HD __forceinline__ void comp_mul(const WVals& W, int i, const double* x, double* o) {
@@ -2971,7 +3053,9 @@ MB_HD __forceinline__ void knot_calc_diff_x(const X& ex, const double* P, int nx
   if (nc > 0)  // contact rows at the drift (ddq = 0; ContactModelMultiple::calc)
     ex.run([&](int lane) {
       if (lane < nj) contact_jac_lane(b, W, lane, Jc, nullptr);
-      for (int k = lane; k < (imp ? 0 : b.ncon); k += ex.nt) {
+      // the a0 terms on the next wave (not after the Jacobian columns on wave 0: a wave
+      // runs its divergent lanes' paths one after another)
+      for (int k = lane - 64; k >= 0 && k < (imp ? 0 : b.ncon); k += ex.nt) {
         int row0;
         const CRec C{contact_rec(b, k, &row0)};
         contact_a0_position(b, W, C, a0 + row0);
@@ -3267,10 +3351,16 @@ MB_HD __forceinline__ void knot_calc_diff_x(const X& ex, const double* P, int nx
     // the cost-derivative table: groups in cost (name) order, each the rows of one cost
     // with a dense residual Jacobian, or the diagonal of a state / control cost; per row
     // Arr (hess), and Ar as amul * aval (the quadratic kinds' (w, r), so the gradient
-    // keeps the order (X w) r of the reference's R^T (w r)). Cost k on lane nt-1-k
-    // (no da entries there), from its group / row / jac-cost offsets, prefix-counted.
+    // keeps the order (X w) r of the reference's R^T (w r)). Cost k on lane
+    // spread_lane(k) after the da tiles (host: lane nt-1-k, which has no da entries), from
+    // its group / row / jac-cost offsets, prefix-counted.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(MB_NO_MFMA_DA)
+    const int kk = spread_item(lane, ex.nt);  // (every lane ran the da tiles)
+    if (kk < (b.ncost > 0 ? b.ncost : 1)) {
+#else
     if (lane >= nl) {
       const int kk = ex.nt - 1 - lane;
+#endif
       int g = 0, row = 0, f = 0;
       const double* cr = b.C;
       for (int k = 0; k < kk; ++k) {  // offsets of record kk
@@ -3341,23 +3431,31 @@ MB_HD __forceinline__ void knot_calc_diff_x(const X& ex, const double* P, int nx
   // 16-B pairs of the column-major blocks (n even, blocks 16-B aligned); the lane's
   // (column, row pair) advances by nt pairs without a division.
   ex.run([&](int lane) {
+    // the operands re-asserted as LDS here: without it the inference lost them and they
+    // were flat loads, each waiting (vmcnt) for the output stores issued before it
+    const double* const daL = ex.lds(da);
+    const double* const MinvL = ex.lds(Minv);
+    const double* const HL = ex.lds(H);
+    const double* const JcL = ex.lds(Jc);
+    const double* const JeL = ex.lds(Je);
+    const double* const AiL = ex.lds(Ai);
     // Fx(i, c): Euler assembly (euler.hxx:100-112) with JintegrateTransport / Jintegrate
     auto fx_at = [&](int i, int c) -> double {
       if (imp) {  // [[I, 0], [-G dtau_dq - H dv0_dq, G M = I - H Jc]] (impulse-fwddyn.hxx:111-115)
         if (i < nj) return c == i ? 1. : 0.;
-        if (c < nj) return da[(int64_t)(i - nj) * Ld + c];
+        if (c < nj) return daL[(int64_t)(i - nj) * Ld + c];
         double s = 0.;
-        for (int k = 0; k < nc; ++k) s += H[(int64_t)k * nj + (i - nj)] * Jc[(int64_t)k * nj + (c - nj)];
+        for (int k = 0; k < nc; ++k) s += HL[(int64_t)k * nj + (i - nj)] * JcL[(int64_t)k * nj + (c - nj)];
         return ok ? (c - nj == i - nj ? 1. : 0.) - s : NAN;
       }
       if (!integ) return c == i ? 1. : 0.;
       if (i < nj && ffe && i < 6) {  // Jexp6(dq) (da dt^2 + [0 dt I]) + Ad(exp6(dq)^-1)
-        double s = c < 6 ? Ai[c * 6 + i] : 0.;
-        for (int r = 0; r < 6; ++r) s += Je[r * 6 + i] * (da[(int64_t)r * Ld + c] * dt2 + (c == nj + r ? dt : 0.));
+        double s = c < 6 ? AiL[c * 6 + i] : 0.;
+        for (int r = 0; r < 6; ++r) s += JeL[r * 6 + i] * (daL[(int64_t)r * Ld + c] * dt2 + (c == nj + r ? dt : 0.));
         return s;
       }
-      if (i < nj) return da[(int64_t)i * Ld + c] * dt2 + (c == nj + i ? dt : 0.) + (c == i ? 1. : 0.);
-      return da[(int64_t)(i - nj) * Ld + c] * dt + (c == i ? 1. : 0.);
+      if (i < nj) return daL[(int64_t)i * Ld + c] * dt2 + (c == nj + i ? dt : 0.) + (c == i ? 1. : 0.);
+      return daL[(int64_t)(i - nj) * Ld + c] * dt + (c == i ? 1. : 0.);
     };
     // Fu(i, c) = Kinv_tl(i mod nj, nun + c) dt^2 | dt (dtau/du = [0; I]), Jexp6 on
     // the free-flyer rows
@@ -3365,10 +3463,10 @@ MB_HD __forceinline__ void knot_calc_diff_x(const X& ex, const double* P, int nx
       if (!(integ && c < nu && !imp)) return 0.;
       if (i < nj && ffe && i < 6) {
         double s = 0.;
-        for (int r = 0; r < 6; ++r) s += Je[r * 6 + i] * Minv[(int64_t)(b.nun + c) * lda + r];
+        for (int r = 0; r < 6; ++r) s += JeL[r * 6 + i] * MinvL[(int64_t)(b.nun + c) * lda + r];
         return ok ? s * dt2 : NAN;
       }
-      const double mi = ok ? Minv[(int64_t)(b.nun + c) * lda + (i < nj ? i : i - nj)] : NAN;
+      const double mi = ok ? MinvL[(int64_t)(b.nun + c) * lda + (i < nj ? i : i - nj)] : NAN;
       return i < nj ? mi * dt2 : mi * dt;
     };
     // the free-flyer Euler rows (Jexp6 products, 6 terms each) on lanes of their own,
@@ -3581,7 +3679,7 @@ MB_HD __forceinline__ void knot_calc_diff_x(const X& ex, const double* P, int nx
       mb_gstore((isu ? Lu : Lx) + j, integ ? sc * acc : acc);
     }
     // the fused calc's cost (cost-sum.hxx:89-117): record k's weighted activation on
-    // lane nt-1-k (the lanes with the fewest GEMM tasks), into the dead pivot buffer
+    // lane spread_lane(k) (one record per wave first), into the dead pivot buffer
     // (pb[0, 64)); jac-cost residuals from the Jacobian phase.
     // The wide records (state / control, wide_cost) row-parallel instead: 32 lanes each
     // from lane 128 on (from lane 0 in a 128-thread workgroup), their partials into
@@ -3595,7 +3693,7 @@ MB_HD __forceinline__ void knot_calc_diff_x(const X& ex, const double* P, int nx
         const int t = C.type();
         const bool wide = wide_cost(C, nw);
         const int wl = lane - wbase - 32 * nw;  // this lane's share of wide record nw
-        if (wide ? (wl >= 0 && wl < 32) : lane == ex.nt - 1 - k) {
+        if (wide ? (wl >= 0 && wl < 32) : lane == spread_lane(k, ex.nt)) {
           const Act act = cost_act(b, C, nu);
           double a = 0.;
           if (jac_cost(b, t) && (!wide || wl == 0)) {
