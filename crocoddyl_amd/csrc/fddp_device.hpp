@@ -52,6 +52,55 @@ __device__ __forceinline__ T* lds_ptr(T* p) {
   return p;
 }
 
+// ---- register broadcasts within a wave (64 lanes = 4 rows of 16) -------------------
+// lane n of every row of 16 lanes, to the whole row (DPP row_newbcast: a VALU move, no
+// LDS-crossbar round trip as __shfl's ds_bpermute); n a compile-time constant
+template <int N>
+__device__ __forceinline__ double row_bcast_d(double v) {
+  const long long bits = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)bits, 0x150 + N, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(bits >> 32), 0x150 + N, 0xf, 0xf, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+template <int I = 0>
+__device__ __forceinline__ double row_bcast_d(double v, int n) {  // n in [I, 16), unrolled
+  if constexpr (I < 15) {
+    if (n != I) return row_bcast_d<I + 1>(v, n);
+  }
+  return row_bcast_d<I>(v);
+}
+// row r (lanes 16 r .. 16 r + 15) of a wave to all four rows, lane for lane (= __shfl(v,
+// (lane & 15) + 16 r)) by two permlane swaps per half (gfx950 v_permlane16/32_swap: odd
+// rows of the first operand with even rows of the second; upper 32 lanes of the first
+// with lower 32 of the second)
+template <int R>
+__device__ __forceinline__ int row_to_all_i(int h) {
+  const auto a = __builtin_amdgcn_permlane16_swap(h, h, false, false);  // rows [0,0,2,2] | [1,1,3,3]
+  const int t = (R & 1) ? a[1] : a[0];
+  const auto c = __builtin_amdgcn_permlane32_swap(t, t, false, false);  // [t0,t1,t0,t1] | [t2,t3,t2,t3]
+  return (R & 2) ? c[1] : c[0];
+}
+template <int R>
+__device__ __forceinline__ double row_to_all_d(double v) {
+  const long long bits = __double_as_longlong(v);
+  const int lo = row_to_all_i<R>((int)bits), hi = row_to_all_i<R>((int)(bits >> 32));
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+template <int I = 0>
+__device__ __forceinline__ double row_to_all_d(double v, int r) {  // r in [I, 4), unrolled
+  if constexpr (I < 3) {
+    if (r != I) return row_to_all_d<I + 1>(v, r);
+  }
+  return row_to_all_d<I>(v);
+}
+// lane l's value to every lane (v_readlane, a scalar)
+__device__ __forceinline__ double lane_read_d(double v, int l) {
+  const long long bits = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)bits, l);
+  const int hi = __builtin_amdgcn_readlane((int)(bits >> 32), l);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
 // fddp_boxqp_params on the device (BoxQP, box-qp.hpp:92-93)
 struct BoxQPCfg {
   int maxiter, n_alphas;

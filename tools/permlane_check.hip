@@ -4,7 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include "multibody.hpp"
-using namespace fddp::mb;
+using namespace fddp;
 __global__ void k(int* bad) {
   const int lane = threadIdx.x;
   const double v = 1000.0 * lane + 0.25;
