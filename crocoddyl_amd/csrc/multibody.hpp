@@ -68,6 +68,25 @@ MB_HD __forceinline__ void mb_gstore2(double* p, double v0, double v1) {
   p[1] = v1;
 #endif
 }
+// A fresh register copy of v (device: an empty asm the optimiser cannot see through), so
+// a value live across the whole kernel is reloaded from its spill slot once, here.
+template <class T>
+MB_HD __forceinline__ T mb_launder(T v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (sizeof(T) == 8) {
+    long long x;
+    __builtin_memcpy(&x, &v, 8);
+    asm volatile("" : "+v"(x));
+    __builtin_memcpy(&v, &x, 8);
+  } else {
+    int x;
+    __builtin_memcpy(&x, &v, 4);
+    asm volatile("" : "+v"(x));
+    __builtin_memcpy(&v, &x, 4);
+  }
+#endif
+  return v;
+}
 template <class T>
 MB_HD __forceinline__ T* mb_lds(T* p) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -3399,53 +3418,65 @@ MB_HD __forceinline__ void knot_calc_diff_x(const X& ex, const double* P, int nx
     const double* const JcL = ex.lds(Jc);
     const double* const JeL = ex.lds(Je);
     const double* const AiL = ex.lds(Ai);
+    // this phase's invariants laundered into fresh registers: kept in spill slots across
+    // the kernel they were reloaded in every iteration, and a scratch reload after an
+    // output store waits (vmcnt, in order) for that store to reach memory
+    const int NJ = mb_launder(nj), NC = mb_launder(nc), LD = mb_launder(Ld), NU = mb_launder(nu);
+    const int LDA = mb_launder(lda), NUN = mb_launder(b.nun), N = mb_launder(n), M = mb_launder(m);
+    const double DT = mb_launder(dt), DT2 = mb_launder(dt2);
+    const int flags = mb_launder((imp ? 1 : 0) | (integ ? 2 : 0) | (ffe ? 4 : 0) | (ok ? 8 : 0));
+    const bool IMP = flags & 1, INTEG = flags & 2, FFE = flags & 4, OK = flags & 8;
+    double* const FX = Fx;
+    double* const FU = Fu;
     // Fx(i, c): Euler assembly (euler.hxx:100-112) with JintegrateTransport / Jintegrate
-    auto fx_at = [&](int i, int c) -> double {
-      if (imp) {  // [[I, 0], [-G dtau_dq - H dv0_dq, G M = I - H Jc]] (impulse-fwddyn.hxx:111-115)
-        if (i < nj) return c == i ? 1. : 0.;
-        if (c < nj) return daL[(int64_t)(i - nj) * Ld + c];
+    // (both inlined, capturing copies: a closure left in scratch made every captured value a
+    // scratch load of its address and a flat load of the value)
+    auto fx_at = [=](int i, int c) __attribute__((always_inline)) -> double {
+      if (IMP) {  // [[I, 0], [-G dtau_dq - H dv0_dq, G M = I - H Jc]] (impulse-fwddyn.hxx:111-115)
+        if (i < NJ) return c == i ? 1. : 0.;
+        if (c < NJ) return daL[(int64_t)(i - NJ) * LD + c];
         double s = 0.;
-        for (int k = 0; k < nc; ++k) s += HL[(int64_t)k * nj + (i - nj)] * JcL[(int64_t)k * nj + (c - nj)];
-        return ok ? (c - nj == i - nj ? 1. : 0.) - s : NAN;
+        for (int k = 0; k < NC; ++k) s += HL[(int64_t)k * NJ + (i - NJ)] * JcL[(int64_t)k * NJ + (c - NJ)];
+        return OK ? (c - NJ == i - NJ ? 1. : 0.) - s : NAN;
       }
-      if (!integ) return c == i ? 1. : 0.;
-      if (i < nj && ffe && i < 6) {  // Jexp6(dq) (da dt^2 + [0 dt I]) + Ad(exp6(dq)^-1)
+      if (!INTEG) return c == i ? 1. : 0.;
+      if (i < NJ && FFE && i < 6) {  // Jexp6(dq) (da dt^2 + [0 dt I]) + Ad(exp6(dq)^-1)
         double s = c < 6 ? AiL[c * 6 + i] : 0.;
-        for (int r = 0; r < 6; ++r) s += JeL[r * 6 + i] * (daL[(int64_t)r * Ld + c] * dt2 + (c == nj + r ? dt : 0.));
+        for (int r = 0; r < 6; ++r) s += JeL[r * 6 + i] * (daL[(int64_t)r * LD + c] * DT2 + (c == NJ + r ? DT : 0.));
         return s;
       }
-      if (i < nj) return daL[(int64_t)i * Ld + c] * dt2 + (c == nj + i ? dt : 0.) + (c == i ? 1. : 0.);
-      return daL[(int64_t)(i - nj) * Ld + c] * dt + (c == i ? 1. : 0.);
+      if (i < NJ) return daL[(int64_t)i * LD + c] * DT2 + (c == NJ + i ? DT : 0.) + (c == i ? 1. : 0.);
+      return daL[(int64_t)(i - NJ) * LD + c] * DT + (c == i ? 1. : 0.);
     };
     // Fu(i, c) = Kinv_tl(i mod nj, nun + c) dt^2 | dt (dtau/du = [0; I]), Jexp6 on
     // the free-flyer rows
-    auto fu_at = [&](int i, int c) -> double {
-      if (!(integ && c < nu && !imp)) return 0.;
-      if (i < nj && ffe && i < 6) {
+    auto fu_at = [=](int i, int c) __attribute__((always_inline)) -> double {
+      if (!(INTEG && c < NU && !IMP)) return 0.;
+      if (i < NJ && FFE && i < 6) {
         double s = 0.;
-        for (int r = 0; r < 6; ++r) s += JeL[r * 6 + i] * MinvL[(int64_t)(b.nun + c) * lda + r];
-        return ok ? s * dt2 : NAN;
+        for (int r = 0; r < 6; ++r) s += JeL[r * 6 + i] * MinvL[(int64_t)(NUN + c) * LDA + r];
+        return OK ? s * DT2 : NAN;
       }
-      const double mi = ok ? MinvL[(int64_t)(b.nun + c) * lda + (i < nj ? i : i - nj)] : NAN;
-      return i < nj ? mi * dt2 : mi * dt;
+      const double mi = OK ? MinvL[(int64_t)(NUN + c) * LDA + (i < NJ ? i : i - NJ)] : NAN;
+      return i < NJ ? mi * DT2 : mi * DT;
     };
     // the free-flyer Euler rows (Jexp6 products, 6 terms each) on lanes of their own,
     // so the row pairs below all take the short path (a wave pays for its slowest lane)
-    const int r6 = ffe ? 6 : 0;
-    for (int e = lane; e < r6 * (n + m); e += ex.nt) {
+    const int r6 = FFE ? 6 : 0;
+    for (int e = lane; e < r6 * (N + M); e += ex.nt) {
       const int c = e / 6, i = e - 6 * c;
-      if (c < n)
-        mb_gstore(Fx + (int64_t)c * n + i, fx_at(i, c));
+      if (c < N)
+        mb_gstore(FX + (int64_t)c * N + i, fx_at(i, c));
       else
-        mb_gstore(Fu + (int64_t)(c - n) * n + i, fu_at(i, c - n));
+        mb_gstore(FU + (int64_t)(c - N) * N + i, fu_at(i, c - N));
     }
-    const int p0 = r6 >> 1, hp = (n >> 1) - p0, dq = ex.nt / hp, dr = ex.nt % hp;
-    for (int c = lane / hp, ip = lane % hp; c < n + m;) {
+    const int p0 = r6 >> 1, hp = (N >> 1) - p0, dq = ex.nt / hp, dr = ex.nt % hp;
+    for (int c = lane / hp, ip = lane % hp; c < N + M;) {
       const int i = 2 * (p0 + ip);
-      if (c < n)
-        mb_gstore2(Fx + (int64_t)c * n + i, fx_at(i, c), fx_at(i + 1, c));
+      if (c < N)
+        mb_gstore2(FX + (int64_t)c * N + i, fx_at(i, c), fx_at(i + 1, c));
       else
-        mb_gstore2(Fu + (int64_t)(c - n) * n + i, fu_at(i, c - n), fu_at(i + 1, c - n));
+        mb_gstore2(FU + (int64_t)(c - N) * N + i, fu_at(i, c - N), fu_at(i + 1, c - N));
       c += dq;
       ip += dr;
       if (ip >= hp) ip -= hp, ++c;
