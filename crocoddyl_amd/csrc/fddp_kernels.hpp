@@ -743,12 +743,14 @@ __device__ __forceinline__ bool fwd_trial(const Dev& D, int b, const ElemState& 
     const double* xs = D.xs[c] + kk * D.sX;
     double* xt = out.xs + kk * D.sX;
     // xs_try[t] = xnext  or  integrate(xnext, fs[t] * (alpha - 1))
+    // (the trial's outputs xs_try[t], us_try[t], xnext[t] are stored after the knot's calc,
+    // from LDS: a store before the calc made its first spill reloads wait (vmcnt, in
+    // order) for the store to reach memory)
     double pd = 0.;
     if (!ff) {
       for (int i = tid; i < nx; i += NT) {
         const double v = full ? xn[i] : xn[i] + fs[i] * (alpha - 1);
         xv[i] = v;
-        gstore(xt + i, v);
         if (!feas) pd += (v - xs[i]) * D.Vxxfs[kk * D.sN + i];  // -fs^T Vxx diff(xs_try, xs)
       }
       __syncthreads();
@@ -758,7 +760,6 @@ __device__ __forceinline__ bool fwd_trial(const Dev& D, int b, const ElemState& 
       else
         state_integrate_wg<NT>(D, xn, fs, alpha - 1, xv);
       __syncthreads();
-      for (int i = tid; i < nx; i += NT) gstore(xt + i, xv[i]);
       state_diff_wg<NT>(D, xs, xv, dxv);
       if (!feas) state_diff_wg<NT>(D, xv, xs, dxv + D.sN, kWave);
       __syncthreads();
@@ -773,7 +774,6 @@ __device__ __forceinline__ bool fwd_trial(const Dev& D, int b, const ElemState& 
       const double* us = D.us[c] + D.run(b, t) * D.sM;
       const double* K = D.K + D.run(b, t) * D.sNM;
       const double* kv = D.k + D.run(b, t) * D.sM;
-      double* ut = out.us + D.run(b, t) * D.sM;
       // us_try = us - k * alpha - K * dx ,  dx = diff(xs, xs_try)
       for (int i = tid; i < m; i += NT) {
         double v = 0.;
@@ -785,13 +785,15 @@ __device__ __forceinline__ bool fwd_trial(const Dev& D, int b, const ElemState& 
           if (D.box_knot(b, t)) v = std_min(std_max(v, D.ulb[D.run(b, t) * D.sM + i]), D.uub[D.run(b, t) * D.sM + i]);
         }
         uv[i] = v;
-        gstore(ut + i, v);
       }
       __syncthreads();
     }
     const double ct = knot_calc<NT, MB>(kd, P, nx, xv, uv, running, xn, red, mbw);
     bool bad = false;
+    for (int i = tid; i < nx; i += NT) gstore(xt + i, xv[i]);
     if (running) {
+      double* ut = out.us + D.run(b, t) * D.sM;
+      for (int i = tid; i < m; i += NT) gstore(ut + i, uv[i]);
       double* xo = out.xnext + D.run(b, t) * D.sX;
       for (int i = tid; i < nx; i += NT) {
         gstore(xo + i, xn[i]);
