@@ -148,6 +148,7 @@ struct Dev {
   // npar workgroups; trial slot 0 writes the other trajectory buffer, slots
   // 1..npar-1 their own copies (same [b][t] layout), accepted ones are copied back
   int npar;                        // trials per element evaluated together (1: serial line search)
+  const int* ls_order;             // [B] rollout workgroup -> element (longest line search first), or null
   double *pxs, *pus, *pxnext, *pkcost, *pdvp;  // slots 1..npar-1: [slot][B][T+1|T][...]
   double* ptrial;                  // [B][npar][4]: ok, cost_try, dv, -
   int* ls_done;                    // [B] line search decided in an earlier group of this iteration

@@ -322,6 +322,7 @@ struct fddp_handle_s {
   int bwd_variant = 0;  // 0 generic, else (NTL*10+MTL)*10+waves of the MFMA sweep
   bool bwd_wave = false;  // small knots (n, m <= 16): the one-wave sweep (bwd_wave.hpp), FDDP only
   int ls_npar_last = 0;      // trial-group size of the last line search (1: serial)
+  std::vector<int> h_order;  // host copy of D.ls_order (kept alive for the async upload)
   int ls_launches_last = 0;  // rollout (forward_kernel) dispatches of the last line search
   fddp_iteration_callback cb = nullptr;  // per-iteration callback (fddp_set_callback)
   void* cb_user = nullptr;
@@ -660,6 +661,42 @@ static void choose_npar(fddp_handle* h, const std::vector<ElemState>& st) {
     if (g == 1 || time < best) best = time, best_g = g;
   }
   h->D.npar = best_g;
+}
+
+// Longest-processing-time-first dispatch of the next line search: the rollout's
+// workgroups map to the elements in descending order of their last line search's trial
+// count (the fixed MPC protocol repeats it exactly; a heuristic otherwise). Each element's
+// work is unchanged, so are its results. A simulation of the C5 walk's trial histogram on
+// 512 resident workgroups: 8 trial-lengths in element order, 6 longest-first (ideal 5.1).
+static int update_ls_order(fddp_handle* h, const std::vector<ElemState>& st) {
+  Dev& D = h->D;
+  const int B = D.B, na = h->prm.n_alphas;
+  if (B < 2 || h->fast) return FDDP_OK;
+  if (!D.ls_order) {
+    double* p = nullptr;
+    int rc;
+    if ((rc = dalloc(h, &p, (B + 1) / 2))) return rc;
+    D.ls_order = (const int*)p;
+  }
+  std::vector<int> key(B);
+  for (int b = 0; b < B; ++b) {
+    const ElemState& s = st[b];
+    int k = 0;
+    if (s.n_iter_run > 0) {
+      k = na;
+      for (int a = 0; a < na; ++a)
+        if (s.steplength == h->prm.alphas[a]) {
+          k = a + 1;
+          break;
+        }
+    }
+    key[b] = k;
+  }
+  h->h_order.resize(B);
+  for (int b = 0; b < B; ++b) h->h_order[b] = b;
+  std::stable_sort(h->h_order.begin(), h->h_order.end(), [&](int x, int y) { return key[x] > key[y]; });
+  HIP_TRY(hipMemcpyAsync((void*)D.ls_order, h->h_order.data(), sizeof(int) * B, hipMemcpyHostToDevice, h->stream));
+  return FDDP_OK;
 }
 
 int launch_forward(fddp_handle* h, int mode, double alpha, int* count) {
@@ -1022,6 +1059,7 @@ int fddp_create(const fddp_dims* dims, const fddp_knot_desc* knots, const double
   // path: the same trials and the same choice as the serial search, fewer serial
   // rollouts for the elements that backtrack (CROCODDYL_AMD_LS_PAR = 1 is serial)
   D.npar = 1;
+  D.ls_order = nullptr;
   if (const char* e = std::getenv("CROCODDYL_AMD_LS_PAR")) D.npar = h->npar_env = std::max(1, std::min(16, std::atoi(e)));
   const int64_t B = d.B, K1 = (int64_t)d.T + 1, K0 = d.T;
   {  // SolverBoxFDDP's qp_(nu, 100, 0.1, 1e-5, 0.) (box-fddp.cpp:16); unused until BOXFDDP
@@ -1295,6 +1333,7 @@ int fddp_solve(fddp_handle* h, int maxiter, int is_feasible, double reg_init, fd
     if ((rc = download_states(h, st))) return rc;
     for (int b = 0; b < D.B; ++b) fill_result(st[b], &out[b]);
     choose_npar(h, st);
+    if ((rc = update_ls_order(h, st))) return rc;
   } else {
     HIP_TRY(hipStreamSynchronize(h->stream));
   }

@@ -910,7 +910,9 @@ __device__ __forceinline__ void ls_finish(const Prm& prm, ElemState& s, bool acc
 template <int NT, bool FAST, bool MB = false>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((FAST || MB) ? FDDP_FWD_WPE : 1))) void forward_kernel(Dev D, Prm prm, int mode, double alpha1, int* active_count,
                                                      int64_t pcap, int group = 0) {
-  const int b = blockIdx.x;
+  // (workgroups are dispatched roughly in index order: the elements whose last line
+  // search took the most trials start first, so they do not trail the launch)
+  const int b = D.ls_order ? D.ls_order[blockIdx.x] : (int)blockIdx.x;
   ElemState* st = D.st + b;
   if (mode != 1 && !st->active) return;
   const int slot = mode == 2 ? (int)blockIdx.y : 0;
