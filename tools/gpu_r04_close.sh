@@ -1,7 +1,7 @@
 # closing run: GPU suite, smoke, bench lines with the CPU port (C5 default, C2, C3, C4), C5 + C2 profiles
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-O=gpurun_out/r04close
+O=gpurun_out/r04close2
 mkdir -p $O
 timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests -m gpu > $O/gpu_tests.log 2>&1 || { tail -30 $O/gpu_tests.log; exit 1; }
 timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit 1
