@@ -70,11 +70,20 @@ def test_fullsize_fixed_protocol_vs_oracle(cfg):
     step = bench.FixedWarmStart(solver, 0)
     spots = np.array([0, B // 2, B - 1])
     o, _ = _oracle_spots(solver, spots)
+    first = None
     for k in range(2):  # every step starts from the same warm start: same result twice
         step(1)
         o.set_candidate(*[None if a is None else a[spots] for a in solver.warm], False)
         o.solve(maxiter=1, is_feasible=False, reg_init=0.1)
         _compare(solver, o, spots, f"{cfg} fixed step {k}")
+        # (step 1's rollout dispatches the elements longest line search first, from step 0's
+        # trial counts: the same solves to the last bit)
+        cur = (np.asarray(solver.xs).copy(), np.asarray(solver.cost).copy(), np.asarray(solver.stepLength).copy())
+        if first is None:
+            first = cur
+        else:
+            for a, b2 in zip(first, cur):
+                np.testing.assert_array_equal(a, b2)
     trials = bench.line_search_trials(solver)
     assert trials.min() >= 1 and trials.max() <= 10
 
