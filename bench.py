@@ -11,10 +11,12 @@ reference's benchmark unit. Two protocols:
 Each step runs exactly one FDDP iteration per element (calc, calcDiff + gaps,
 backward Riccati sweep, line search), so FDDP iterations/s == MPC solves/s.
 
-Multi-GPU: one process per GPU (torchrun), the batch axis is sharded (each
-rank owns B independent problems: weak scaling, no collective inside the
-solve), and the solved trajectories are collected with one RCCL all-gather at
-the end of the timed region (crocoddyl_amd/dist.py).
+Multi-GPU: one process per GPU, the batch axis is sharded (each rank owns B
+independent problems: weak scaling, no collective inside the solve), and the
+solved trajectories are collected with one RCCL all-gather at the end of the
+timed region (crocoddyl_amd/dist.py). Under torchrun the ranks come from its
+environment; `python bench.py --gpus N` without one starts the N ranks itself
+(launch_ranks) and relays rank 0's line.
 
 Prints one JSON line (rank 0).
 """
@@ -369,6 +371,89 @@ def trials_summary(trials):
             "hist": np.bincount(trials.astype(int), minlength=11)[1:].tolist()}
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n, argv, timeout=None):
+    """`bench.py --gpus N` without a torchrun environment: start N fresh worker
+    processes of this script, one per GPU (RANK / LOCAL_RANK / WORLD_SIZE /
+    LOCAL_WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT in their environment), wait
+    for all of them, and relay rank 0's stdout (the JSON line). The parent touches no
+    GPU (nothing here imports torch) and execs nothing: the ranks are children. Ranks
+    other than 0 have their stdout sent to stderr, as do rank 0's non-JSON lines, so
+    the job's stdout is the one line. If a rank
+    fails, the others are stopped (by their own PIDs) and its exit code is returned."""
+    import subprocess
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
+                                      stdout=subprocess.PIPE if r == 0 else sys.stderr.fileno(), text=True))
+    t0 = time.time()
+    out = []
+    import threading
+
+    def pump():  # relay rank 0's stdout as it comes: its JSON line to stdout, the rest (library chatter) to stderr
+        for line in procs[0].stdout:
+            out.append(line)
+            dst = sys.stdout if line.startswith("{") else sys.stderr
+            dst.write(line)
+            dst.flush()
+    th = threading.Thread(target=pump, daemon=True)
+    th.start()
+    rc = 0
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [c for c in codes if c not in (None, 0)]
+        if bad or (timeout and time.time() - t0 > timeout):
+            rc = bad[0] if bad else 124
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            for p in procs:
+                try:
+                    p.wait(timeout=30)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+            break
+        if all(c == 0 for c in codes):
+            break
+        time.sleep(0.2)
+    th.join(timeout=10)
+    if rc == 0 and not any(ln.startswith("{") for ln in out):
+        sys.stderr.write("bench.py: rank 0 printed no JSON line\n")
+        rc = 1
+    return rc
+
+
+def _launch_selftest(args):
+    """--launch-selftest: the N-rank launch path without a GPU (gloo, no solve): every
+    rank joins the process group, and rank 0 prints the job's line with the per-rank
+    table bench.py records (device, world size), for the CPU launcher test."""
+    import torch.distributed as tdist
+
+    from crocoddyl_amd import dist as cdist
+    ws, rank, local_rank = cdist.world()
+    assert ws == args.gpus, f"world size {ws} != --gpus {args.gpus}"
+    cdist.init("gloo")
+    rt = cdist.rank_table([local_rank, tdist.get_world_size() if tdist.is_initialized() else 1, os.getpid()], "cpu")
+    t, w = cdist.job_time_and_work(0.1 * (rank + 1), 10 * (rank + 1), "cpu")
+    if rank == 0:
+        print(json.dumps({"n_gpus": ws, "job_time_s": t, "work": w,
+                          "ranks": cdist.rank_summary(rt, ["device", "world_size", "pid"])}), flush=True)
+    if ws > 1:
+        tdist.barrier()
+        tdist.destroy_process_group()
+
+
 def main():
     if len(sys.argv) > 1 and sys.argv[1] == "--cpu-baseline-child":
         a = sys.argv[2:]
@@ -392,10 +477,16 @@ def main():
                          "rotated (circularAppend) + device shift of x0/xs/us, then the warm-started solve")
     ap.add_argument("--secondary-steps", type=int, default=5,
                     help="steps of the other protocol, reported beside the headline (1 GPU only; 0: off)")
+    ap.add_argument("--launch-selftest", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
     box = args.solver == "boxfddp"
     if args.protocol is None:
         args.protocol = "feasible" if box else "fixed"
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no torchrun environment: this process becomes the launcher of N ranks
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if args.launch_selftest:
+        return _launch_selftest(args)
 
     import torch
 
@@ -403,8 +494,14 @@ def main():
     from crocoddyl_amd import dist as cdist
 
     ws, rank, local_rank = cdist.world()
-    cdist.init("nccl", local_rank)
-    dev = local_rank
+    assert ws == args.gpus, f"world size {ws} (WORLD_SIZE) != --gpus {args.gpus}"
+    # one rank per GPU; on a lease with fewer GPUs than ranks (a rehearsal of the N-GPU
+    # job) ranks share devices and the collectives run on gloo (RCCL refuses two ranks
+    # on one device)
+    ndev = torch.cuda.device_count()
+    dev = local_rank % max(ndev, 1)
+    backend = os.environ.get("CROCODDYL_AMD_DIST_BACKEND") or ("nccl" if ndev >= ws else "gloo")
+    cdist.init(backend, dev)
 
     kind, d1, nu, T, B0, dt = synthetic.CONFIGS[args.config]
     B = args.batch or B0
@@ -457,14 +554,19 @@ def main():
     assert xs_all.shape[0] == us_all.shape[0] == res_all.shape[0] == ws * B
     # per-rank diagnostics (outside the timed region): the timed loop's own time, the
     # gather's time and bytes, the rank's iterations; max/min imbalance per column
-    names = ["elapsed_s", "solve_s", "gather_s", "iterations", "mean_trials_last_step"]
-    rt = cdist.rank_table([rank_elapsed, t_solve, gstats["gather_s"], iters, float(np.mean(trials))], f"cuda:{dev}")
-    ranks = dict(cdist.rank_summary(rt, names), gather_bytes_sent_per_rank=gstats["gather_bytes_sent"],
+    names = ["elapsed_s", "solve_s", "gather_s", "iterations", "mean_trials_last_step", "device", "world_size"]
+    gws = torch.distributed.get_world_size() if torch.distributed.is_initialized() else 1
+    rt = cdist.rank_table([rank_elapsed, t_solve, gstats["gather_s"], iters, float(np.mean(trials)), dev, gws],
+                          f"cuda:{dev}")
+    ranks = dict(cdist.rank_summary(rt, names), backend=cdist.backend(),
+                 gather_bytes_sent_per_rank=gstats["gather_bytes_sent"],
                  gather_bytes_received_per_rank=gstats["gather_bytes_received"],
                  gather_GBps_received=round(gstats["gather_bytes_received"] / max(float(rt[:, 2].max()), 1e-12) / 1e9, 3)
                  if ws > 1 else None,
                  note="elapsed_s: this rank's barrier-to-barrier time (the job time is the max); solve_s: the timed "
-                      "solves alone; gather_s: the RCCL all-gathers of xs, us and results (device-synchronised)")
+                      "solves alone; gather_s: the all-gathers of xs, us and results (device-synchronised; RCCL "
+                      "when every rank has its own GPU, gloo over host copies when ranks share one); device: the "
+                      "rank's GPU; world_size: dist.get_world_size() seen by the rank")
 
     box_bwd = None
     if box and ws == 1 and args.protocol == "feasible":

@@ -11,6 +11,7 @@ FDDP_ERR_INVALID_ARG = -1
 FDDP_ERR_RUNTIME = -2
 FDDP_ERR_UNSUPPORTED = -3
 FDDP_ERR_NO_DEVICE = -4
+FDDP_ERR_CALLBACK_ABORT = -5
 
 STATUS_RUNNING, STATUS_CONVERGED, STATUS_REGMAX = 0, 1, 2
 
@@ -58,7 +59,7 @@ I32 = C.POINTER(C.c_int32)
 U64 = C.POINTER(C.c_uint64)
 
 # fddp_iteration_callback(void* user, int iter, const fddp_result* results, const int32_t* reported, int B)
-IterationCallback = C.CFUNCTYPE(None, C.c_void_p, C.c_int, C.POINTER(Result), I32, C.c_int)
+IterationCallback = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.POINTER(Result), I32, C.c_int)
 
 # name -> (restype, argtypes); `h` is an opaque handle pointer
 PROTOS = {

@@ -30,7 +30,8 @@ class VerboseLevel:
 class CallbackVerbose(CallbackAbstract):
     """One table row per iteration (iter, cost, stop, grad = -d[1], xreg, ureg, step,
     feas; level 2 adds dV-exp and dV), a header every 10 iterations. Batched solvers
-    print element 0's row."""
+    print the row of the first element that ran the iteration (``solver.callbackMask``),
+    so a finished element 0 does not repeat its last row under later iterations."""
 
     def __init__(self, level=VerboseLevel._1, stream=None):
         self.level = level
@@ -38,12 +39,20 @@ class CallbackVerbose(CallbackAbstract):
 
     def __call__(self, solver):
         out = self.stream or sys.stdout
-        first = (lambda v: np.asarray(v).reshape(-1)[0])
+        mask = getattr(solver, "callbackMask", None)
+        e = 0
+        if mask is not None and np.size(mask) > 1:
+            ran = np.flatnonzero(np.asarray(mask))
+            if ran.size == 0:
+                return
+            e = int(ran[0])
+        first = (lambda v: np.asarray(v).reshape(-1)[e] if np.size(v) > e else np.asarray(v).reshape(-1)[0])
         it = int(first(solver.iter))
         if it % 10 == 0:
             out.write("iter \t cost \t      stop \t    grad \t  xreg \t      ureg \t step \t feas"
                       + (" \tdV-exp \t      dV" if self.level == VerboseLevel._2 else "") + "\n")
-        d = np.asarray(solver.d).reshape(-1, 2)[0]
+        d = np.asarray(solver.d).reshape(-1, 2)
+        d = d[e] if d.shape[0] > e else d[0]
         row = (f"{it:4d}  {first(solver.cost):.5e}  {first(solver.stop):.5e}  {-d[1]:.5e}  "
                f"{first(solver.x_reg):.5e}  {first(solver.u_reg):.5e}   {first(solver.stepLength):.4f}     "
                f"{int(bool(first(solver.isFeasible)))}")

@@ -10,6 +10,8 @@
 //   forward_kernel (line search, update) fddp.cpp:49-103
 // Elements that converge or abort drop out (masked); the host only reads one
 // counter per iteration to stop early.
+// (the large kernels are compiled in the k_*.hip objects and reached through ktab.hpp)
+#define FDDP_TU_MAIN 1
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -25,16 +27,50 @@
 #include "fddp_kernels.hpp"
 #include "fast_path.hpp"
 #include "bwd_mfma.hpp"
-#include "bwd_wave.hpp"
+#include "ktab.hpp"
 
 using namespace fddp;
+
+// ---- kernel-table dispatchers (ktab.hpp): variant -> the object that compiled it ----
+namespace fddp {
+namespace ktab {
+int mb_knot_threads(int v) {
+  return v == MB_W1 ? mb_knot_threads_1() : v == MB_X2 ? mb_knot_threads_2() : v == MB_X8 ? mb_knot_threads_3()
+                                                                                        : mb_knot_threads_0();
+}
+const void* mb_knot_fn(int v) {
+  return v == MB_W1 ? mb_knot_fn_1() : v == MB_X2 ? mb_knot_fn_2() : v == MB_X8 ? mb_knot_fn_3() : mb_knot_fn_0();
+}
+hipError_t mb_knot(int v, dim3 grid, size_t smem, hipStream_t s, const Dev& D, int sel_calc, int sel_diff) {
+  switch (v) {
+    case MB_W1: return mb_knot_1(grid, smem, s, D, sel_calc, sel_diff);
+    case MB_X2: return mb_knot_2(grid, smem, s, D, sel_calc, sel_diff);
+    case MB_X8: return mb_knot_3(grid, smem, s, D, sel_calc, sel_diff);
+    default: return mb_knot_0(grid, smem, s, D, sel_calc, sel_diff);
+  }
+}
+const void* forward_fn(int v) { return v == FWD_MB ? forward_fn_1() : forward_fn_0(v); }
+hipError_t forward(int v, dim3 grid, size_t smem, hipStream_t s, const Dev& D, const Prm& prm, int mode, double alpha,
+                   int* count, int64_t pcap, int group) {
+  if (v == FWD_MB) return forward_1(grid, smem, s, D, prm, mode, alpha, count, pcap, group);
+  return forward_0(v, grid, smem, s, D, prm, mode, alpha, count, pcap, group);
+}
+int backward_mfma_setup(int ntl, int mtl, int nw, int n) {
+  const int v = backward_mfma_setup_0(ntl, mtl, nw, n);
+  return v != -2 ? v : backward_mfma_setup_1(ntl, mtl, nw, n);
+}
+hipError_t backward_mfma(int code, dim3 grid, hipStream_t s, const Dev& D, const Prm& prm, int mode) {
+  return code == 528 ? backward_mfma_0(code, grid, s, D, prm, mode) : backward_mfma_1(code, grid, s, D, prm, mode);
+}
+}  // namespace ktab
+}  // namespace fddp
 
 namespace {
 
 thread_local std::string g_err;
 
-constexpr int kNT = 256;
-constexpr int kNTF = 512;  // fused calc/calcDiff: 8 waves per CU keep the derivative stores streaming
+using ktab::kNT;
+using ktab::kNTF;
 
 int fail(int code, const std::string& msg) {
   g_err = msg;
@@ -51,6 +87,13 @@ int fail(int code, const std::string& msg) {
 #define LAUNCH_CHECK()                                                                          \
   do {                                                                                          \
     hipError_t e_ = hipGetLastError();                                                          \
+    if (e_ != hipSuccess) return fail(FDDP_ERR_RUNTIME, std::string("launch: ") + hipGetErrorString(e_)); \
+  } while (0)
+
+// a launch through the kernel table (ktab.hpp), which returns the launch's error
+#define KLAUNCH(expr)                                                                           \
+  do {                                                                                          \
+    hipError_t e_ = (expr);                                                                     \
     if (e_ != hipSuccess) return fail(FDDP_ERR_RUNTIME, std::string("launch: ") + hipGetErrorString(e_)); \
   } while (0)
 
@@ -320,7 +363,6 @@ struct fddp_handle_s {
   size_t mb_diff_smem = 0; // its dynamic LDS
   int mb_nj = 0;            // largest multibody tree (dofs)
   int bwd_variant = 0;  // 0 generic, else (NTL*10+MTL)*10+waves of the MFMA sweep
-  bool bwd_wave = false;  // small knots (n, m <= 16): the one-wave sweep (bwd_wave.hpp), FDDP only
   int ls_npar_last = 0;      // trial-group size of the last line search (1: serial)
   std::vector<int> h_order;  // host copy of D.ls_order (kept alive for the async upload)
   int ls_launches_last = 0;  // rollout (forward_kernel) dispatches of the last line search
@@ -421,9 +463,7 @@ BoxQPCfg to_boxcfg(const fddp_boxqp_params& p) {
 int launch_fused(fddp_handle* h, int sel_calc, int sel_diff, int gaps) {
   Timed tm(h, sel_diff >= 0 ? 1 : 0);
   const Dev& D = h->D;
-  hipLaunchKernelGGL(calc_tiled_kernel<kNTF>, dim3(D.B), dim3(kNTF), h->fused_smem, h->stream, D, sel_calc, sel_diff,
-                     gaps, h->pcap);
-  LAUNCH_CHECK();
+  KLAUNCH(ktab::calc_tiled(dim3(D.B), h->fused_smem, h->stream, D, sel_calc, sel_diff, gaps, h->pcap));
   return FDDP_OK;
 }
 // The knot-parallel kernel's LDS plan leaves room for one workgroup per CU: take the
@@ -455,19 +495,8 @@ static bool mb_x2(const fddp_handle* h) {
 // Multibody knots (knot-parallel): calc for sel_calc, calcDiff for sel_diff (-1: none).
 int launch_mb(fddp_handle* h, int sel_calc, int sel_diff) {
   const Dev& D = h->D;
-  if (mb_x2(h))
-    hipLaunchKernelGGL(mb_knot_kernel_x2, dim3(D.T + 1, D.B), dim3(mb::kMbDiffNT / 2), h->mb_diff_smem, h->stream, D,
-                       sel_calc, sel_diff);
-  else if (mb_x8(h))
-    hipLaunchKernelGGL(mb_knot_kernel_x8, dim3(D.T + 1, D.B), dim3(2 * mb::kMbDiffNT), h->mb_diff_smem, h->stream, D,
-                       sel_calc, sel_diff);
-  else if (mb_one_per_cu(h))
-    hipLaunchKernelGGL(mb_knot_kernel_w1, dim3(D.T + 1, D.B), dim3(mb::kMbDiffNT), h->mb_diff_smem, h->stream, D, sel_calc,
-                       sel_diff);
-  else
-    hipLaunchKernelGGL(mb_knot_kernel, dim3(D.T + 1, D.B), dim3(mb::kMbDiffNT), h->mb_diff_smem, h->stream, D, sel_calc,
-                       sel_diff);
-  LAUNCH_CHECK();
+  const int v = mb_x2(h) ? ktab::MB_X2 : (mb_x8(h) ? ktab::MB_X8 : (mb_one_per_cu(h) ? ktab::MB_W1 : ktab::MB_W2));
+  KLAUNCH(ktab::mb_knot(v, dim3(D.T + 1, D.B), h->mb_diff_smem, h->stream, D, sel_calc, sel_diff));
   return FDDP_OK;
 }
 int launch_calc(fddp_handle* h, int sel) {
@@ -477,12 +506,10 @@ int launch_calc(fddp_handle* h, int sel) {
   if (h->has_mb) {
     int rc;
     if ((rc = launch_mb(h, sel, -1))) return rc;
-    if (!h->all_mb)
-      hipLaunchKernelGGL(calc_kernel<kNT>, dim3(D.B), dim3(kNT), h->calc_smem, h->stream, D, sel, h->pcap, 1);
+    if (!h->all_mb) KLAUNCH(ktab::calc(dim3(D.B), h->calc_smem, h->stream, D, sel, h->pcap, 1));
   } else {
-    hipLaunchKernelGGL(calc_kernel<kNT>, dim3(D.B), dim3(kNT), h->calc_smem, h->stream, D, sel, h->pcap, 0);
+    KLAUNCH(ktab::calc(dim3(D.B), h->calc_smem, h->stream, D, sel, h->pcap, 0));
   }
-  LAUNCH_CHECK();
   return FDDP_OK;
 }
 int launch_cost_sum(fddp_handle* h, int sel, double* out) {
@@ -499,8 +526,7 @@ int launch_calc_diff(fddp_handle* h, int sel, int gaps) {
     int rc;
     if ((rc = launch_mb(h, -1, sel))) return rc;
   }
-  hipLaunchKernelGGL(calc_diff_kernel<kNT>, dim3(D.B), dim3(kNT), h->cdiff_smem, h->stream, D, sel, gaps, h->pcap);
-  LAUNCH_CHECK();
+  KLAUNCH(ktab::calc_diff(dim3(D.B), h->cdiff_smem, h->stream, D, sel, gaps, h->pcap));
   return FDDP_OK;
 }
 // problem.calc (sel_calc) + cost_ = sum of knot costs, then problem.calcDiff
@@ -517,74 +543,25 @@ int launch_calc_then_diff(fddp_handle* h, int sel_calc, int sel_calc_sum, int se
     Timed tm(h, 1);
     const Dev& D = h->D;
     if ((rc = launch_mb(h, sel_calc, sel_diff))) return rc;
-    if (!h->all_mb) {
-      hipLaunchKernelGGL(calc_kernel<kNT>, dim3(D.B), dim3(kNT), h->calc_smem, h->stream, D, sel_calc, h->pcap, 1);
-      LAUNCH_CHECK();
-    }
+    if (!h->all_mb) KLAUNCH(ktab::calc(dim3(D.B), h->calc_smem, h->stream, D, sel_calc, h->pcap, 1));
     if ((rc = launch_cost_sum(h, sel_calc_sum, nullptr))) return rc;
-    hipLaunchKernelGGL(calc_diff_kernel<kNT>, dim3(D.B), dim3(kNT), h->cdiff_smem, h->stream, D, sel_diff, gaps,
-                       h->pcap);
-    LAUNCH_CHECK();
+    KLAUNCH(ktab::calc_diff(dim3(D.B), h->cdiff_smem, h->stream, D, sel_diff, gaps, h->pcap));
     return FDDP_OK;
   }
   if ((rc = launch_calc(h, sel_calc))) return rc;
   if ((rc = launch_cost_sum(h, sel_calc_sum, nullptr))) return rc;
   return launch_calc_diff(h, sel_diff, gaps);
 }
-template <int NTL, int MTL, int NW>
-void launch_bwd_mfma(fddp_handle* h, int mode) {
-  const Dev& D = h->D;
-  backward_mfma_kernel<NTL, MTL, NW><<<dim3(D.B), dim3(NW * 64), MfmaCfg<NTL, MTL>::bytes, h->stream>>>(
-      D, to_prm(h->prm), mode);
-}
-
 int launch_backward(fddp_handle* h, int mode) {
   Timed tm(h, 2);
   const Dev& D = h->D;
-  if (h->bwd_wave && !D.box) {  // (SolverBoxFDDP's box QP lives in the other sweeps)
-    hipLaunchKernelGGL(backward_wave_kernel, dim3((D.B + kWavesPerWg - 1) / kWavesPerWg), dim3(64 * kWavesPerWg),
-                       sizeof(double) * kWavesPerWg * bwd_wave_doubles(), h->stream, D, to_prm(h->prm), mode);
-    LAUNCH_CHECK();
-    return FDDP_OK;
-  }
-  switch (h->bwd_variant) {
-    case 528: launch_bwd_mfma<5, 2, 8>(h, mode); break;
-    case 318: launch_bwd_mfma<3, 1, 8>(h, mode); break;
-    case 314: launch_bwd_mfma<3, 1, 4>(h, mode); break;
-    case 218: launch_bwd_mfma<2, 1, 8>(h, mode); break;
-    case 214: launch_bwd_mfma<2, 1, 4>(h, mode); break;
-    case 118: launch_bwd_mfma<1, 1, 8>(h, mode); break;
-    case 114: launch_bwd_mfma<1, 1, 4>(h, mode); break;
-    case 111: launch_bwd_mfma<1, 1, 1>(h, mode); break;
-    case 211: launch_bwd_mfma<2, 1, 1>(h, mode); break;
-    case 311: launch_bwd_mfma<3, 1, 1>(h, mode); break;
-    default:
-      hipLaunchKernelGGL(backward_kernel<kNT>, dim3(D.B), dim3(kNT), h->bwd_smem, h->stream, D, to_prm(h->prm), mode);
-  }
-  LAUNCH_CHECK();
+  if (h->bwd_variant)
+    KLAUNCH(ktab::backward_mfma(h->bwd_variant, dim3(D.B), h->stream, D, to_prm(h->prm), mode));
+  else
+    KLAUNCH(ktab::backward_generic(dim3(D.B), h->bwd_smem, h->stream, D, to_prm(h->prm), mode));
   return FDDP_OK;
 }
 
-template <int NTL, int MTL, int NW>
-int setup_bwd_mfma(fddp_handle* h) {
-  using Cfg = MfmaCfg<NTL, MTL>;
-  const size_t lds = Cfg::bytes;
-  if (lds > 160 * 1024 || h->D.n > Cfg::ZLD) return -1;
-  if (hipFuncSetAttribute((const void*)backward_mfma_kernel<NTL, MTL, NW>,
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-    return -1;
-  // column-block ownership per wave is static (BwdPlan in bwd_mfma.hpp)
-  return (NTL * 10 + MTL) * 10 + NW;
-}
-template <int NTL, int MTL>
-int setup_bwd_mfma_nw(fddp_handle* h, int nw) {
-  if constexpr (NTL + MTL <= 4 && MTL == 1)
-    if (nw == 1) return setup_bwd_mfma<NTL, MTL, 1>(h);
-  // (C^T over Zu, when it needs that, only works with the 8-wave plan's late LDS-DMA)
-  if constexpr (MfmaCfg<NTL, MTL>::ct_own)
-    if (nw == 4) return setup_bwd_mfma<NTL, MTL, 4>(h);
-  return setup_bwd_mfma<NTL, MTL, 8>(h);
-}
 // slot buffers of the parallel line search (generic trials), allocated on first use
 static int ensure_par_slots(fddp_handle* h) {
   Dev& D = h->D;
@@ -623,7 +600,7 @@ static void choose_npar(fddp_handle* h, const std::vector<ElemState>& st) {
   if (h->ls_slots <= 0.) {
     int dev_cus = 0, per_cu = 0;
     (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, h->device);
-    const void* k = mb_rollout(h) ? (const void*)forward_kernel<kNT, false, true> : (const void*)forward_kernel<kNT, false>;
+    const void* k = ktab::forward_fn(mb_rollout(h) ? ktab::FWD_MB : ktab::FWD_GENERIC);
     (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, kNT, h->fwd_smem);
     h->ls_slots = (double)std::max(1, dev_cus) * std::max(1, per_cu);
   }
@@ -710,17 +687,11 @@ int launch_forward(fddp_handle* h, int mode, double alpha, int* count) {
     const int na = h->prm.n_alphas, G = (na + D.npar - 1) / D.npar;
     h->ls_npar_last = D.npar;
     h->ls_launches_last = G;
+    const int v = mb_rollout(h) ? ktab::FWD_MB : ktab::FWD_GENERIC;
     for (int g = 0; g < G; ++g) {
-      if (mb_rollout(h))
-        hipLaunchKernelGGL((forward_kernel<kNT, false, true>), dim3(D.B, D.npar), dim3(kNT), h->fwd_smem, h->stream,
-                           D, to_prm(h->prm), 2, 1., nullptr, h->pcap, g);
-      else
-        hipLaunchKernelGGL((forward_kernel<kNT, false>), dim3(D.B, D.npar), dim3(kNT), h->fwd_smem, h->stream, D,
-                           to_prm(h->prm), 2, 1., nullptr, h->pcap, g);
-      LAUNCH_CHECK();
-      hipLaunchKernelGGL((ls_select_kernel<kNT>), dim3(D.B), dim3(kNT), 0, h->stream, D, to_prm(h->prm), g,
-                         g == G - 1 ? 1 : 0, count);
-      LAUNCH_CHECK();
+      KLAUNCH(ktab::forward(v, dim3(D.B, D.npar), h->fwd_smem, h->stream, D, to_prm(h->prm), 2, 1., nullptr, h->pcap,
+                            g));
+      KLAUNCH(ktab::ls_select(dim3(D.B), h->stream, D, to_prm(h->prm), g, g == G - 1 ? 1 : 0, count));
     }
     return FDDP_OK;
   }
@@ -729,15 +700,11 @@ int launch_forward(fddp_handle* h, int mode, double alpha, int* count) {
     h->ls_launches_last = 1;
   }
   if (h->fast)
-    hipLaunchKernelGGL((forward_kernel<kNT, true>), dim3(D.B), dim3(kNT), h->fwd_fast_smem, h->stream, D,
-                       to_prm(h->prm), mode, alpha, count, h->pcap);
-  else if (mb_rollout(h))
-    hipLaunchKernelGGL((forward_kernel<kNT, false, true>), dim3(D.B), dim3(kNT), h->fwd_smem, h->stream, D,
-                       to_prm(h->prm), mode, alpha, count, h->pcap);
+    KLAUNCH(ktab::forward(ktab::FWD_FAST, dim3(D.B), h->fwd_fast_smem, h->stream, D, to_prm(h->prm), mode, alpha,
+                          count, h->pcap, 0));
   else
-    hipLaunchKernelGGL((forward_kernel<kNT, false>), dim3(D.B), dim3(kNT), h->fwd_smem, h->stream, D,
-                       to_prm(h->prm), mode, alpha, count, h->pcap);
-  LAUNCH_CHECK();
+    KLAUNCH(ktab::forward(mb_rollout(h) ? ktab::FWD_MB : ktab::FWD_GENERIC, dim3(D.B), h->fwd_smem, h->stream, D,
+                          to_prm(h->prm), mode, alpha, count, h->pcap, 0));
   return FDDP_OK;
 }
 
@@ -938,17 +905,17 @@ int apply_knots(fddp_handle* h, const fddp_knot_desc* knots, const double* param
       bool use;
       const char* name;
     } reqs[] = {
-        {(const void*)backward_kernel<kNT>, h->bwd_smem, true, "backward_kernel"},
-        {(const void*)forward_kernel<kNT, false>, h->fwd_smem, true, "forward_kernel"},
-        {(const void*)forward_kernel<kNT, true>, h->fwd_fast_smem, true, "forward_kernel<fast>"},
-        {(const void*)forward_kernel<kNT, false, true>, h->fwd_smem, h->has_mb, "forward_kernel<multibody>"},
-        {(const void*)calc_tiled_kernel<kNTF>, h->fused_smem, true, "calc_tiled_kernel"},
-        {(const void*)calc_kernel<kNT>, h->calc_smem, true, "calc_kernel"},
-        {(const void*)calc_diff_kernel<kNT>, h->cdiff_smem, true, "calc_diff_kernel"},
-        {(const void*)mb_knot_kernel, h->mb_diff_smem, h->has_mb, "mb_knot_kernel"},
-        {(const void*)mb_knot_kernel_w1, h->mb_diff_smem, h->has_mb, "mb_knot_kernel_w1"},
-        {(const void*)mb_knot_kernel_x8, h->mb_diff_smem, h->has_mb, "mb_knot_kernel_x8"},
-        {(const void*)mb_knot_kernel_x2, h->mb_diff_smem, h->has_mb, "mb_knot_kernel_x2"},
+        {ktab::backward_generic_fn(), h->bwd_smem, true, "backward_kernel"},
+        {ktab::forward_fn(ktab::FWD_GENERIC), h->fwd_smem, true, "forward_kernel"},
+        {ktab::forward_fn(ktab::FWD_FAST), h->fwd_fast_smem, true, "forward_kernel<fast>"},
+        {ktab::forward_fn(ktab::FWD_MB), h->fwd_smem, h->has_mb, "forward_kernel<multibody>"},
+        {ktab::calc_tiled_fn(), h->fused_smem, true, "calc_tiled_kernel"},
+        {ktab::calc_fn(), h->calc_smem, true, "calc_kernel"},
+        {ktab::calc_diff_fn(), h->cdiff_smem, true, "calc_diff_kernel"},
+        {ktab::mb_knot_fn(ktab::MB_W2), h->mb_diff_smem, h->has_mb, "mb_knot_kernel"},
+        {ktab::mb_knot_fn(ktab::MB_W1), h->mb_diff_smem, h->has_mb, "mb_knot_kernel_w1"},
+        {ktab::mb_knot_fn(ktab::MB_X8), h->mb_diff_smem, h->has_mb, "mb_knot_kernel_x8"},
+        {ktab::mb_knot_fn(ktab::MB_X2), h->mb_diff_smem, h->has_mb, "mb_knot_kernel_x2"},
     };
     for (const Req& r : reqs) {
       if (!r.use) continue;
@@ -974,19 +941,17 @@ int apply_knots(fddp_handle* h, const fddp_knot_desc* knots, const double* param
       const char* ew = std::getenv("FDDP_BWD_WAVES");
       int nw = 8;
       if (ew) nw = ew[0] == '1' ? 1 : (ew[0] == '4' ? 4 : 8);
-      if (ntl == 5 && mtl == 2) v = setup_bwd_mfma_nw<5, 2>(h, nw);
-      else if (ntl == 3 && mtl == 1) v = setup_bwd_mfma_nw<3, 1>(h, nw);
-      else if (ntl == 2 && mtl == 1) v = setup_bwd_mfma_nw<2, 1>(h, nw);
-      else if (ntl == 1 && mtl == 1) v = setup_bwd_mfma_nw<1, 1>(h, nw);
+      // one-wave plans exist for the small shapes (NTL + MTL <= 4, MTL = 1); four-wave
+      // plans where C^T has its own LDS area (else C^T over Zu needs the 8-wave plan's
+      // late LDS-DMA); everything else runs eight waves (ktab::backward_mfma_setup)
+      const bool known = (ntl == 5 && mtl == 2) || (mtl == 1 && ntl >= 1 && ntl <= 3);
+      if (known) {
+        if (nw == 1 && !(ntl + mtl <= 4 && mtl == 1)) nw = 8;
+        v = ktab::backward_mfma_setup(ntl, mtl, nw, d.ndx);
+        if (v < 0 && nw == 4) v = ktab::backward_mfma_setup(ntl, mtl, 8, d.ndx);
+      }
     }
     h->bwd_variant = v > 0 ? v : 0;
-    // the one-wave VALU sweep (bwd_wave.hpp) on request (FDDP_BACKWARD=wave; A/B runs)
-    if (env && std::strcmp(env, "wave") == 0 && d.ndx <= kBwdWaveMax && d.nu_max <= kBwdWaveMax) {
-      if (hipFuncSetAttribute((const void*)backward_wave_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)(sizeof(double) * kWavesPerWg * bwd_wave_doubles())) != hipSuccess)
-        return fail(FDDP_ERR_RUNTIME, "hipFuncSetAttribute(dynamic LDS) of backward_wave_kernel");
-      h->bwd_wave = true;
-    }
   }
   return FDDP_OK;
 }
@@ -1314,13 +1279,18 @@ int fddp_solve(fddp_handle* h, int maxiter, int is_feasible, double reg_init, fd
       int any = 0;
       for (int b = 0; b < D.B; ++b) {
         fill_result(cbst[b], &cbres[b]);
-        cbres[b].iter = it;
         cbrep[b] = (cbst[b].n_iter_run > cbrun[b] && cbst[b].status != FDDP_STATUS_REGMAX) ? 1 : 0;
+        if (cbrep[b]) cbres[b].iter = it;  // the loop counter of this body; finished elements keep theirs
         cbrun[b] = cbst[b].n_iter_run;
         any |= cbrep[b];
       }
-      if (any) h->cb(h->cb_user, it, cbres.data(), cbrep.data(), D.B);
+      const int stop = any ? h->cb(h->cb_user, it, cbres.data(), cbrep.data(), D.B) : 0;
       (void)hipSetDevice(h->device);  // (the callback may have switched devices)
+      if (stop) {  // the reference's exception out of the loop body: the state stays at this iteration
+        if (out) std::copy(cbres.begin(), cbres.end(), out);
+        return fail(FDDP_ERR_CALLBACK_ABORT, "fddp_solve: stopped by the iteration callback at iteration " +
+                                                 std::to_string(it));
+      }
     }
     if (it + 1 < maxiter) {
       HIP_TRY(hipMemcpyAsync(h->h_count, h->d_count, sizeof(int), hipMemcpyDeviceToHost, h->stream));

@@ -9,6 +9,9 @@
 
 namespace fddp {
 
+// Non-template kernels are compiled in one translation unit each: FDDP_TU_MAIN
+// (fddp_hip.hip) or FDDP_TU_MB = the multibody variant (k_mb.hip, ktab.hpp).
+
 // Doubles in a knot's parameter block (layouts in include/fddp_hip.h); the
 // multibody block carries its size in its header (g: the block).
 __device__ inline int64_t block_doubles_dev(int kind, int nx, int nu, const double* g = nullptr) {
@@ -175,6 +178,7 @@ __global__ __launch_bounds__(NT) void calc_kernel(Dev D, int sel, int64_t pcap, 
 }
 
 // cost_ = sum of data[t].cost in knot order, terminal last (shooting.hxx:155-160).
+#if defined(FDDP_TU_MAIN)
 __global__ void cost_sum_kernel(Dev D, int sel, double* out) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= D.B) return;
@@ -187,6 +191,8 @@ __global__ void cost_sum_kernel(Dev D, int sel, double* out) {
   s.cost = c;
   if (out) out[b] = c;
 }
+#endif
+
 
 // ---------------------------------------------------------------------------
 // ShootingProblem::calcDiff (shooting.hxx:164-195) fused with the gap
@@ -291,25 +297,37 @@ __device__ __forceinline__ void mb_knot_body(const Dev& D, int sel_calc, int sel
 // workgroups share a CU where the LDS plan allows it (<= 80 KB: the trot, the arm); when
 // the plan leaves room for one workgroup per CU anyway (Talos: ~140 KB) the 1-wave/EU
 // build gets the whole register file (VGPRs + AGPRs) and nothing spills.
+#if defined(FDDP_TU_MB) && FDDP_TU_MB == 0
 __global__ __launch_bounds__(mb::kMbDiffNT) __attribute__((amdgpu_waves_per_eu(2))) void mb_knot_kernel(Dev D, int sel_calc, int sel_diff) {
   mb_knot_body<mb::kMbDiffNT>(D, sel_calc, sel_diff);
 }
+#endif
+
+#if defined(FDDP_TU_MB) && FDDP_TU_MB == 1
 __global__ __launch_bounds__(mb::kMbDiffNT) __attribute__((amdgpu_waves_per_eu(1, 1))) void mb_knot_kernel_w1(Dev D, int sel_calc,
                                                                                                    int sel_diff) {
   mb_knot_body<mb::kMbDiffNT>(D, sel_calc, sel_diff);
 }
+#endif
+
 // Two waves per (knot, element) workgroup, for the small trees (the arm: nv = 7), whose
 // phases leave most lanes of four waves idle: four workgroups per CU under the same
 // register budget.
+#if defined(FDDP_TU_MB) && FDDP_TU_MB == 2
 __global__ __launch_bounds__(mb::kMbDiffNT / 2) __attribute__((amdgpu_waves_per_eu(2))) void mb_knot_kernel_x2(Dev D, int sel_calc, int sel_diff) {
   mb_knot_body<mb::kMbDiffNT / 2>(D, sel_calc, sel_diff);
 }
+#endif
+
 // Eight waves per (knot, element) workgroup: one workgroup per CU on the large LDS plans
 // still puts two waves on every SIMD, and the phases' independent work (Gauss-Jordan
 // slabs, MFMA tiles, the output blocks) spreads over twice the waves.
+#if defined(FDDP_TU_MB) && FDDP_TU_MB == 3
 __global__ __launch_bounds__(2 * mb::kMbDiffNT) void mb_knot_kernel_x8(Dev D, int sel_calc, int sel_diff) {
   mb_knot_body<2 * mb::kMbDiffNT>(D, sel_calc, sel_diff);
 }
+#endif
+
 
 // ---------------------------------------------------------------------------
 // Backward Riccati sweep — SolverDDP::backwardPass + computeGains
@@ -1082,6 +1100,7 @@ __global__ __launch_bounds__(NT) void mpc_shift_kernel(Dev D) {
 }
 
 // Solve prologue: per-element state (fddp.cpp:21-31, solver-base.cpp:66).
+#if defined(FDDP_TU_MAIN)
 __global__ void init_state_kernel(Dev D, int is_feasible, double xreg) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= D.B) return;
@@ -1101,8 +1120,11 @@ __global__ void init_state_kernel(Dev D, int is_feasible, double xreg) {
   // stale one (a failed launch between groups would otherwise skip a line search)
   if (D.ls_done) D.ls_done[b] = 0;
 }
+#endif
+
 
 // Copy xs/us of the current buffer of every element into a dense output.
+#if defined(FDDP_TU_MAIN)
 __global__ void gather_traj_kernel(Dev D, int which, double* out) {
   const int b = blockIdx.y;
   const int c = D.st[b].cur;
@@ -1114,7 +1136,10 @@ __global__ void gather_traj_kernel(Dev D, int which, double* out) {
   for (int64_t e = blockIdx.x * blockDim.x + threadIdx.x; e < rows * w; e += (int64_t)gridDim.x * blockDim.x)
     dst[e] = src[(e / w) * sw + e % w];
 }
+#endif
 
+
+#if defined(FDDP_TU_MAIN)
 __global__ void scatter_traj_kernel(Dev D, int which, const double* in, int use_zero) {
   const int b = blockIdx.y;
   const int c = D.st[b].cur;
@@ -1128,12 +1153,15 @@ __global__ void scatter_traj_kernel(Dev D, int which, const double* in, int use_
   for (int64_t e = blockIdx.x * blockDim.x + threadIdx.x; e < rows * w; e += (int64_t)gridDim.x * blockDim.x)
     dst[(e / w) * sw + e % w] = use_zero ? ((e % w) == qw ? 1. : 0.) : src[e];
 }
+#endif
+
 
 
 // ---------------------------------------------------------------------------
 // Standalone batched box QP (fddp_boxqp_solve): BoxQP::solve (box-qp.cpp:
 // 51-182), one wave per problem, H and the free-Hessian inverse in LDS.
 // ---------------------------------------------------------------------------
+#if defined(FDDP_TU_MAIN)
 __global__ __launch_bounds__(64) void boxqp_kernel(int nx, const double* H, const double* q, const double* lb,
                                                    const double* ub, const double* xinit, BoxQPCfg c, double* x,
                                                    uint64_t* free_mask, uint64_t* inv_mask, double* Hinv,
@@ -1163,5 +1191,7 @@ __global__ __launch_bounds__(64) void boxqp_kernel(int nx, const double* H, cons
     status[b] = ok ? 0 : 1;
   }
 }
+#endif
+
 
 }  // namespace fddp

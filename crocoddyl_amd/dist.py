@@ -34,6 +34,11 @@ def init(backend, local_rank=None):
     return ws, rank
 
 
+def backend():
+    """The default group's backend ("nccl" = RCCL on ROCm, "gloo"), or None on one process."""
+    return dist.get_backend() if dist.is_initialized() else None
+
+
 def shard(b_global, ws, rank):
     """Contiguous block of batch elements owned by `rank`: (start, count)."""
     base, rem = divmod(b_global, ws)
@@ -114,6 +119,8 @@ def job_time_and_work(elapsed_s, work, device):
     """Whole-job numbers: the slowest rank's time, the sum of the work."""
     if not dist.is_initialized() or dist.get_world_size() == 1:
         return float(elapsed_s), float(work)
+    if dist.get_backend() == "gloo":
+        device = "cpu"
     t = torch.tensor([float(elapsed_s)], dtype=torch.float64, device=device)
     w = torch.tensor([float(work)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)

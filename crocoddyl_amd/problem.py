@@ -520,24 +520,30 @@ class SolverFDDP:
                 self._cb_snap = snap
                 self.callbackMask = np.ctypeslib.as_array(reported, (B,)).astype(bool)
                 if not self.problem.batched and not self.callbackMask[0]:
-                    return
+                    return 0
                 try:
                     for cb in self.callbacks:
                         cb(self)
-                except BaseException as e:  # re-raised after fddp_solve returns
-                    self._cb_error = self._cb_error or e
+                except BaseException as e:  # stops fddp_solve after this iteration; re-raised below
+                    self._cb_error = e
+                    return 1
+                return 0
 
             self._cb_error = None
             cfn = _abi.IterationCallback(on_iter)
             check(lib().fddp_set_callback(ptr, cfn, None))
             try:
-                check(lib().fddp_solve(ptr, int(maxiter), 1 if isFeasible else 0, reg, r))
+                rc = lib().fddp_solve(ptr, int(maxiter), 1 if isFeasible else 0, reg, r)
             finally:
                 check(lib().fddp_set_callback(ptr, _abi.IterationCallback(), None))
                 self.callbackMask = None
                 self._cb_snap = None
-            if self._cb_error is not None:
+            if rc == _abi.FDDP_ERR_CALLBACK_ABORT and self._cb_error is not None:
+                # the reference's exception leaves solve() in that iteration (fddp.cpp:92-98):
+                # iter / xs / us / regularisation stay there
+                self._results = r
                 raise self._cb_error
+            check(rc)
         else:
             check(lib().fddp_solve(ptr, int(maxiter), 1 if isFeasible else 0, reg, r))
         self._results = r

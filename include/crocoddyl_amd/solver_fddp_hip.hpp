@@ -300,8 +300,10 @@ class SolverFDDP {
     const int rc = fddp_solve(h_.get(), (int)maxiter, is_feasible ? 1 : 0, reginit, res_.data());
     fddp_set_callback(h_.get(), nullptr, nullptr);
     reported_.clear();
+    // a callback that threw stopped the solve after its iteration (fddp.cpp:92-98):
+    // res_ holds that iteration's results
+    if (rc == FDDP_ERR_CALLBACK_ABORT && !cb_error_.empty()) throw Exception("callback: " + cb_error_);
     check(rc, "fddp_solve");
-    if (!cb_error_.empty()) throw Exception("callback: " + cb_error_);
     return res_[0].status == FDDP_STATUS_CONVERGED;
   }
 
@@ -393,18 +395,20 @@ class SolverFDDP {
 
  private:
   // fddp_iteration_callback: the C ABI calls it between iterations; no exception may
-  // cross the ABI, so one is kept and rethrown after fddp_solve returns
-  static void on_iteration(void* user, int, const fddp_result* results, const int32_t* reported, int B) {
+  // cross the ABI, so one is kept, fddp_solve is told to stop (return 1) and the
+  // exception is rethrown after it returns
+  static int on_iteration(void* user, int, const fddp_result* results, const int32_t* reported, int B) {
     SolverFDDP* self = static_cast<SolverFDDP*>(user);
-    if (!self->cb_error_.empty()) return;
     self->res_.assign(results, results + B);
     self->reported_.assign(reported, reported + B);
-    if (self->dims_.B == 1 && !reported[0]) return;
+    if (self->dims_.B == 1 && !reported[0]) return 0;
     try {
       for (const auto& cb : self->callbacks_) (*cb)(*self);
     } catch (const std::exception& e) {
       self->cb_error_ = e.what();
+      return 1;
     }
+    return 0;
   }
 };
 
@@ -413,12 +417,19 @@ class SolverFDDP {
 class CallbackVerbose : public CallbackAbstract {
  public:
   explicit CallbackVerbose(int level = 1, FILE* out = stdout) : level_(level), out_(out) {}
+  // batched: the row of the first element that ran this iteration (reported()), so a
+  // finished element 0 does not repeat its last row under later iterations
   void operator()(SolverFDDP& s) override {
-    if (s.get_iter() % 10 == 0)
+    std::size_t e = 0;
+    const std::vector<int32_t>& rep = s.reported();
+    while (e < rep.size() && !rep[e]) ++e;
+    if (!rep.empty() && e == rep.size()) return;
+    if (rep.empty()) e = 0;
+    const fddp_result& r = s.get_results()[e];
+    if (r.iter % 10 == 0)
       std::fprintf(out_, "iter \t cost \t      stop \t    grad \t  xreg \t      ureg \t step \t feas%s\n",
                    level_ == 2 ? " \tdV-exp \t      dV" : "");
-    const fddp_result& r = s.get_results()[0];
-    std::fprintf(out_, "%4zu  %.5e  %.5e  %.5e  %.5e  %.5e   %.4f     %d", s.get_iter(), r.cost, r.stop, -r.d1, r.xreg,
+    std::fprintf(out_, "%4d  %.5e  %.5e  %.5e  %.5e  %.5e   %.4f     %d", r.iter, r.cost, r.stop, -r.d1, r.xreg,
                  r.ureg, r.steplength, r.is_feasible ? 1 : 0);
     if (level_ == 2) std::fprintf(out_, "  %.5e  %.5e", r.dVexp, r.dV);
     std::fprintf(out_, "\n");

@@ -37,6 +37,9 @@ extern "C" {
 #define FDDP_ERR_RUNTIME (-2)       /* HIP runtime failure */
 #define FDDP_ERR_UNSUPPORTED (-3)   /* knot kind / size the device path does not cover */
 #define FDDP_ERR_NO_DEVICE (-4)     /* no usable gfx950 device */
+#define FDDP_ERR_CALLBACK_ABORT (-5) /* an iteration callback returned nonzero: fddp_solve stopped after that
+                                        iteration (out = that iteration's results); reference: an exception
+                                        thrown by a CallbackAbstract leaves solve() there (fddp.cpp:92-98) */
 
 /* ---- per-element solve status (fddp_result.status) ----------------------- */
 #define FDDP_STATUS_RUNNING 0       /* maxiter reached without convergence (solve returned false) */
@@ -242,9 +245,13 @@ int fddp_solve(fddp_handle* h, int maxiter, int is_feasible, double reg_init, fd
  * have converged or aborted earlier, or aborted in it). Runs on the calling
  * thread, between iterations (the device is idle): the callback may call the
  * getters and the step API of the same handle, not fddp_solve. Setting a
- * callback makes fddp_solve read the states back once per iteration. */
-typedef void (*fddp_iteration_callback)(void* user, int iter, const fddp_result* results, const int32_t* reported,
-                                        int B);
+ * callback makes fddp_solve read the states back once per iteration.
+ * Returns 0 to go on; nonzero stops fddp_solve after this iteration (the
+ * reference's exception leaving solve() inside the loop body): fddp_solve then
+ * fills `out` with this iteration's results (iter, xs, us, regularisation stay
+ * where that body left them) and returns FDDP_ERR_CALLBACK_ABORT. */
+typedef int (*fddp_iteration_callback)(void* user, int iter, const fddp_result* results, const int32_t* reported,
+                                       int B);
 /* NULL clears it. Replaces SolverAbstract::setCallbacks (solver-base.cpp:69-73). */
 int fddp_set_callback(fddp_handle* h, fddp_iteration_callback cb, void* user);
 

@@ -142,9 +142,90 @@ class Gpu:
 
 
 def rel_err(a, b):
+    """One max-abs error over the whole array / max(1, max|b|). Coarse: small components
+    hide behind large ones. Solve-level parity uses elem_err."""
     a = np.asarray(a, float)
     b = np.asarray(b, float)
     return float(np.max(np.abs(a - b)) / max(1.0, float(np.max(np.abs(b)))))
+
+
+def elem_err(a, b, floor=1e-3):
+    """Element-wise parity error: max_i |a_i − b_i| / max(|b_i|, s_c(i)).
+
+    s_c is the scale of element i's component c (the last axis: the state / control
+    coordinate): max |b[..., c]| over every other axis (the knots of a trajectory, the
+    elements of a batch), so each coordinate is compared at its own magnitude and a small
+    joint velocity is not hidden behind the base height. Coordinates that are (nearly)
+    zero everywhere fall back to `floor` × the array's max |b|. For a 1-D array (costs of
+    a batch) every entry is its own component: plain relative error. NaN anywhere → NaN
+    (which fails every `<=` bar)."""
+    a = np.asarray(a, float)
+    b = np.asarray(b, float)
+    if b.size == 0:
+        return 0.0
+    if b.ndim == 1:
+        s = np.zeros_like(b)
+    else:
+        s = np.max(np.abs(b).reshape(-1, b.shape[-1]), axis=0)
+    big = float(np.max(np.abs(b))) if np.all(np.isfinite(b)) else np.nan
+    s = np.maximum(s, floor * big)
+    d = np.abs(a - b) / np.maximum(np.maximum(np.abs(b), s), 1e-300)
+    return float(np.nan if np.any(np.isnan(d)) else np.max(d))
+
+
+def ulp_perturbed(pool, rng):
+    """The parameter pool with every non-integer entry (masses, inertias, placements,
+    cost weights, references, dt ...; not the structure: counts, kinds, parents) moved by
+    one ulp, relative ±2^-52 with random signs."""
+    p = np.array(pool, dtype=np.float64, copy=True)
+    m = p != np.round(p)
+    p[m] *= 1.0 + np.finfo(np.float64).eps * rng.choice([-1.0, 1.0], size=int(m.sum()))
+    return p
+
+
+def ulp_floor(run, pool, reps=3, seed=0):
+    """Conditioning floor of a solve protocol: run(pool) -> tuple of output arrays
+    (xs, us, costs ...) of the CPU oracle. Returns (run(pool), floors) where floors[i] is
+    the largest elem_err of output i over `reps` runs on ulp_perturbed pools: how far the
+    reference algorithm itself moves when its inputs carry one rounding error. Two
+    correct fp64 implementations (different operation orders) cannot be expected to
+    agree closer than this; on the ill-conditioned gait solves (cond(Quu) up to 5e10,
+    cost ~1e7) it grows with every FDDP iteration (C5 smoke, T = 8: 2.2e-9 after one
+    iteration, 2.4e-8 after three)."""
+    base = run(pool)
+    rng = np.random.default_rng(seed)
+    floors = [0.0] * len(base)
+    for _ in range(reps):
+        out = run(ulp_perturbed(pool, rng))
+        floors = [max(f, elem_err(o, b)) for f, o, b in zip(floors, out, base)]
+    return base, floors
+
+
+FLOOR_FACTOR = 4.0  # parity bar = max(tol, FLOOR_FACTOR x the conditioning floor)
+
+_LOGGED = []
+
+
+def parity(name, a, b, tol, floor=None, scale_floor=1e-3):
+    """elem_err(a, b) <= bar, recorded: printed and appended as a JSON line to
+    $CROCODDYL_AMD_PARITY_LOG when set (so a GPU run leaves every achieved error behind,
+    not only the failures). bar = tol, or max(tol, FLOOR_FACTOR * floor) when the
+    oracle's conditioning floor (ulp_floor) of the same protocol is given."""
+    import json
+    import os
+    e = elem_err(a, b, scale_floor)
+    bar = tol if floor is None else max(tol, FLOOR_FACTOR * floor)
+    test = os.environ.get("PYTEST_CURRENT_TEST", "").split(" ")[0]
+    rec = {"test": test, "check": name, "elem_err": e, "tol": tol, "floor": floor, "bar": bar, "ok": bool(e <= bar)}
+    _LOGGED.append(rec)
+    print(f"parity {name}: {e:.3e} (bar {bar:.3g}" + ("" if floor is None else f", oracle floor {floor:.3g}") + ")")
+    path = os.environ.get("CROCODDYL_AMD_PARITY_LOG")
+    if path:
+        with open(path, "a") as f:
+            f.write(json.dumps(rec) + "\n")
+    if os.environ.get("CROCODDYL_AMD_PARITY_MEASURE") != "1":  # measuring runs log every bar, assert none
+        assert e <= bar, (name, e, bar, floor)
+    return e
 
 
 def results_dict(r):

@@ -17,7 +17,7 @@ from test_gpu import backward_variant  # noqa: F401  (autouse: every device code
 
 pytestmark = pytest.mark.gpu
 
-RTOL = 1e-6  # north_star: xs/us/cost within 1e-6 relative
+RTOL = 1e-8  # element-wise (helpers.elem_err); north_star: xs/us/cost within 1e-6 relative
 
 
 def _gpu_box(S, maxiter=100, th_stop=5e-5, debug=False):
@@ -37,8 +37,8 @@ def _gpu_box(S, maxiter=100, th_stop=5e-5, debug=False):
 def _assert_same(rg, ro, g, o):
     for f in ("status", "iter", "n_iter_run", "is_feasible", "xreg"):
         np.testing.assert_array_equal(rg[f], ro[f], err_msg=f)
-    assert helpers.rel_err(g.xs(), o.xs()) < RTOL
-    assert helpers.rel_err(g.us(), o.us()) < RTOL
+    helpers.parity("xs", g.xs(), o.xs(), RTOL)
+    helpers.parity("us", g.us(), o.us(), RTOL)
     assert float(np.max(np.abs(rg["cost"] - ro["cost"]) / np.maximum(1, np.abs(ro["cost"])))) < RTOL
     assert float(np.max(np.abs(rg["stop"] - ro["stop"]) / np.maximum(1, np.abs(ro["stop"])))) < RTOL
 
@@ -171,5 +171,5 @@ def test_boxfddp_facade_single_problem():
     o, ro = _oracle_box(S)
     assert done and ro["status"][0] == 1
     assert solver.iter == ro["iter"][0]
-    assert helpers.rel_err(np.array(solver.us), o.us()[0]) < RTOL
-    assert helpers.rel_err(np.array(solver.xs), o.xs()[0]) < RTOL
+    helpers.parity("us", np.array(solver.us), o.us()[0], RTOL)
+    helpers.parity("xs", np.array(solver.xs), o.xs()[0], RTOL)

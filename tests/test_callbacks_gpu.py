@@ -3,7 +3,7 @@ CallbackLogger (bindings/python/crocoddyl/__init__.py:356-381) records one entry
 iteration, and its cost / stop / steplength / xreg / ureg / grad traces equal the
 C++ oracle's per-iteration trace (recorded at the same point of the loop body).
 Batched: every element's trace through ``solver.callbackMask``. The bar is the
-solver bar (1e-9 relative for the LQ / unicycle problems, the C5 knots' 1e-6)."""
+solver bar (1e-9 relative for the LQ / unicycle problems, 1e-8 element-wise on the C5 knots)."""
 import io
 
 import numpy as np
@@ -101,6 +101,7 @@ def test_callbacks_c5_walk_trace():
     def on_iter(_u, it, res, rep, B):
         got.append((it, [(res[b].cost, res[b].stop, res[b].steplength, res[b].xreg, res[b].d1) for b in range(B)],
                     [rep[b] for b in range(B)]))
+        return 0
 
     cfn = _abi.IterationCallback(on_iter)
     g._ok(g.L.fddp_set_callback(g.h, cfn, None))
@@ -112,7 +113,7 @@ def test_callbacks_c5_walk_trace():
         assert len(mine) == len(traces[b])
         for (it, (cost, stop, sl, xr, d1)), rec in zip(mine, traces[b]):
             assert sl == rec[6] and xr == rec[4]
-            assert _close(cost, rec[0], 1e-6) and _close(stop, rec[1], 1e-6) and _close(d1, rec[3], 1e-6)
+            helpers.parity(f"C5 callback trace b{b} it{it}", [cost, stop, d1], [rec[0], rec[1], rec[3]], 1e-8)
 
 
 def test_callback_exception_propagates():
@@ -120,11 +121,54 @@ def test_callback_exception_propagates():
     model = crocoddyl.ActionModelUnicycle()
     solver = crocoddyl.SolverFDDP(crocoddyl.ShootingProblem(np.array([-1.0, -1.0, 1.0]), [model] * 10, model))
 
-    def boom(_s):
-        raise KeyError("from callback")
+    calls = []
+
+    def boom(s):
+        calls.append(int(s.iter))
+        if s.iter == 2:
+            raise KeyError("from callback")
 
     solver.setCallbacks([boom])
     with pytest.raises(KeyError):
         solver.solve()
+    # the exception left solve() in the iteration that raised (fddp.cpp:92-98): no
+    # further iterations ran or called back, and the solver's state is that iteration's
+    assert calls == [0, 1, 2]
+    assert solver.iter == 2
+    cost_at_2 = solver.cost
+    ref = crocoddyl.SolverFDDP(crocoddyl.ShootingProblem(np.array([-1.0, -1.0, 1.0]), [model] * 10, model))
+    ref.solve([], [], 3)
+    assert cost_at_2 == ref.cost  # (ref.iter is 3: its loop ran to maxiter)
+    np.testing.assert_array_equal(np.asarray(solver.xs), np.asarray(ref.xs))
     solver.setCallbacks([])
     assert solver.solve()
+
+
+def test_c_abi_callback_abort():
+    """fddp_iteration_callback returning nonzero stops fddp_solve after that iteration:
+    FDDP_ERR_CALLBACK_ABORT, `out` holding that iteration's results (iter, cost), and
+    the trajectories equal a solve that stopped there by maxiter."""
+    S = helpers.setup("C1_unicycle", T=30, B=3, seed=5)
+    d = S["dims"]
+    g = helpers.Gpu(d, S["knots"], S["pool"], S["x0s"])
+    g.set_candidate(None, None, False)
+    seen = []
+
+    def on_iter(_u, it, res, rep, B):
+        seen.append(it)
+        return 1 if it == 1 else 0
+
+    cfn = _abi.IterationCallback(on_iter)
+    g._ok(g.L.fddp_set_callback(g.h, cfn, None))
+    r = (_abi.Result * d.B)()
+    rc = g.L.fddp_solve(g.h, 100, 0, 1e-9, r)
+    g._ok(g.L.fddp_set_callback(g.h, _abi.IterationCallback(), None))
+    assert rc == _abi.FDDP_ERR_CALLBACK_ABORT
+    assert seen == [0, 1]
+    assert [x.iter for x in r] == [1] * d.B
+    xs_abort = g.xs()
+    g2 = helpers.Gpu(d, S["knots"], S["pool"], S["x0s"])
+    g2.set_candidate(None, None, False)
+    r2 = g2.solve(maxiter=2)
+    np.testing.assert_array_equal(xs_abort, g2.xs())
+    assert [x.cost for x in r] == [x.cost for x in r2]

@@ -17,6 +17,7 @@ from crocoddyl_amd.problem import pack_problem
 from oracle import fddp_np
 
 pytestmark = pytest.mark.gpu
+SOLVE_TOL = 1e-8  # element-wise (helpers.elem_err), solves vs the numpy oracle
 
 
 def _mixed(T, B, seed=0):
@@ -117,13 +118,13 @@ def test_solve_vs_oracle(case):
         conv = o.solve([x0s[b]] * (T + 1), None, maxiter=30, is_feasible=False, reg_init=1e-9)
         assert r["iter"][b] == o.iter, (b, r["iter"][b], o.iter)
         assert bool(r["status"][b] == _abi.STATUS_CONVERGED) == bool(conv)
-        assert abs(r["cost"][b] - o.cost) <= 1e-6 * abs(o.cost)
-        assert helpers.rel_err(xs_g[b], np.array(o.xs)) < 1e-6
+        helpers.parity(f"contact case {case} b{b} cost", [r["cost"][b]], [o.cost], SOLVE_TOL)
+        helpers.parity(f"contact case {case} b{b} xs", xs_g[b], np.array(o.xs), SOLVE_TOL)
         us_o = np.zeros_like(us_g[b])
         for t in range(T):
             u = np.asarray(o.us[t])
             us_o[t, :u.size] = u
-        assert helpers.rel_err(us_g[b], us_o) < 1e-6
+        helpers.parity(f"contact case {case} b{b} us", us_g[b], us_o, SOLVE_TOL)
 
 
 def test_facade_contact_solve():

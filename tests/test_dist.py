@@ -55,6 +55,39 @@ def _worker(rank, ws, port, q):
     torch.distributed.destroy_process_group()
 
 
+@pytest.mark.parametrize("n", [2, 3])
+def test_bench_launches_n_ranks(n):
+    """`python bench.py --gpus N` with no torchrun environment starts N rank processes
+    itself (bench.launch_ranks: RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set per child)
+    and relays rank 0's one JSON line; here on gloo without a GPU (--launch-selftest)."""
+    import json
+    import subprocess
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--launch-selftest"],
+                       env=env, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, p.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == n
+    r = out["ranks"]
+    assert r["world_size"] == [float(n)] * n
+    assert r["device"] == [float(i) for i in range(n)]
+    assert len(set(r["pid"])) == n
+    assert out["job_time_s"] == pytest.approx(0.1 * n)
+    assert out["work"] == 10 * n * (n + 1) / 2
+
+
+def test_bench_rank_refuses_world_size_mismatch():
+    """A rank whose WORLD_SIZE disagrees with --gpus stops instead of reporting n_gpus wrong."""
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--launch-selftest"],
+                       env=env, capture_output=True, text=True, timeout=120)
+    assert p.returncode != 0 and "--gpus 2" in p.stderr
+
+
 def test_shard_bounds():
     from crocoddyl_amd.dist import shard
     for bg in (1, 7, 8, 1024, 8192):

@@ -10,7 +10,11 @@ bench's steps on the GPU:
 Spot elements {0, B/2, B-1} are replayed on the C++ oracle (oracle/floating_oracle.hpp)
 from the same x0 and warm start with the same knot rotation: identical status,
 iteration count and step length (every branch decision of the line search), xs / us /
-cost within 1e-6 relative (north_star's bar).
+cost element-wise (helpers.elem_err: each coordinate at its own scale) within 1e-8, or
+within 4x the oracle's own spread under one-ulp noise in the model parameters where the
+protocol's conditioning is worse than that (helpers.ulp_floor: the five-iteration
+presolve of the shift protocol); north_star's bar is 1e-6 relative. The achieved
+errors and floors are printed and logged.
 
 The parallel line search (groups of 4 trials, the default on Talos) is also compared
 with the serial one on the same problems: identical to the last bit, including
@@ -33,34 +37,54 @@ import bench  # noqa: E402
 pytestmark = pytest.mark.gpu
 
 FULL = {"C5_talos_walk": (100, 1024), "C4_solo12_trot": (60, 1024)}
+TOL = 1e-8  # element-wise (helpers.elem_err); north_star's bar is 1e-6 relative
 
 
-def _oracle_spots(solver, spots, threads=3):
+def _oracle_spots(solver, spots, pool=None, threads=3):
     p = solver.problem
-    knots, pool = p._packed()
+    knots, pool0 = p._packed()
     d = _abi.Dims(p.nx, p.ndx, p.nu_max, p.T, len(spots))
-    o = oracle_lib.Oracle(d, knots, pool, p.x0[spots], threads=threads)
+    o = oracle_lib.Oracle(d, knots, pool0 if pool is None else pool, p.x0[spots], threads=threads)
     xs, us = solver.warm
     o.set_candidate(None if xs is None else xs[spots], None if us is None else us[spots], False)
     return o, knots
 
 
-def _compare(solver, o, spots, what):
+def _live_us(solver, us):
+    """controls of the knots' own nu (the rows of nu = 0 impulse knots carry no control)"""
+    live = np.zeros(us.shape[-2:], bool)
+    for t, m in enumerate(solver.problem.runningModels):
+        live[t, :m.nu] = True
+    return np.where(live, us, 0.0)
+
+
+def _snap(o):
+    return helpers.results_dict(o.results()), o.xs(), o.us()
+
+
+def _compare(solver, spots, what, ref, floors):
+    """ref = the oracle's (results, xs, us) of the spot elements; floors = its
+    conditioning floors (helpers.ulp_floor) of (cost, xs, us) for this protocol point."""
+    ro, xo, uo = ref
     r = helpers.results_dict(solver._res())
-    ro = helpers.results_dict(o.results())
     xs, us = np.asarray(solver.xs), np.asarray(solver.us)
-    xo, uo = o.xs(), o.us()
     for i, b in enumerate(spots):
         for f in ("status", "iter", "n_iter_run", "steplength", "is_feasible"):
             assert r[f][b] == ro[f][i], (what, b, f, r[f][b], ro[f][i])
-        assert abs(r["cost"][b] - ro["cost"][i]) <= 1e-6 * abs(ro["cost"][i]), (what, b, r["cost"][b], ro["cost"][i])
-        assert helpers.rel_err(xs[b], xo[i]) < 1e-6, (what, b, helpers.rel_err(xs[b], xo[i]))
-        # controls of the knots' own nu (the rows of nu = 0 impulse knots carry no control)
-        nus = [m.nu for m in solver.problem.runningModels]
-        ug = np.concatenate([us[b, t, :nu] for t, nu in enumerate(nus)])
-        uc = np.concatenate([uo[i, t, :nu] for t, nu in enumerate(nus)])
-        assert helpers.rel_err(ug, uc) < 1e-6, (what, b, helpers.rel_err(ug, uc))
+    # element-wise, each state / control coordinate at its own scale (helpers.elem_err)
+    helpers.parity(f"{what} cost", r["cost"][spots], ro["cost"], TOL, floors[0])
+    helpers.parity(f"{what} xs", xs[spots], xo, TOL, floors[1])
+    helpers.parity(f"{what} us", _live_us(solver, us[spots]), _live_us(solver, uo), TOL, floors[2])
     assert np.all(np.isfinite(xs)) and np.all(np.isfinite(r["cost"])), what
+
+
+def _with_floors(run, pool):
+    """run(pool) -> list of oracle snapshots (results, xs, us); the snapshots at the
+    unperturbed pool and, per snapshot, the floors of (cost, xs, us) (helpers.ulp_floor)"""
+    flat = lambda p: tuple(a for r, x, u in run(p) for a in (r["cost"], x, u))  # noqa: E731
+    base = run(pool)
+    _, fl = helpers.ulp_floor(flat, pool)
+    return base, [fl[3 * k:3 * k + 3] for k in range(len(base))]
 
 
 @pytest.mark.parametrize("cfg", list(FULL))
@@ -69,13 +93,17 @@ def test_fullsize_fixed_protocol_vs_oracle(cfg):
     solver = bench.make_shard_solver(cfg, B, 0, 0, presolve=False)
     step = bench.FixedWarmStart(solver, 0)
     spots = np.array([0, B // 2, B - 1])
-    o, _ = _oracle_spots(solver, spots)
+
+    def run(pool):
+        o, _ = _oracle_spots(solver, spots, pool)
+        o.solve(maxiter=1, is_feasible=False, reg_init=0.1)
+        return [_snap(o)]
+
+    (ref,), (floors,) = _with_floors(run, solver.problem._packed()[1])
     first = None
     for k in range(2):  # every step starts from the same warm start: same result twice
         step(1)
-        o.set_candidate(*[None if a is None else a[spots] for a in solver.warm], False)
-        o.solve(maxiter=1, is_feasible=False, reg_init=0.1)
-        _compare(solver, o, spots, f"{cfg} fixed step {k}")
+        _compare(solver, spots, f"{cfg} fixed step {k}", ref, floors)
         # (step 1's rollout dispatches the elements longest line search first, from step 0's
         # trial counts: the same solves to the last bit)
         cur = (np.asarray(solver.xs).copy(), np.asarray(solver.cost).copy(), np.asarray(solver.stepLength).copy())
@@ -93,17 +121,25 @@ def test_fullsize_shift_protocol_vs_oracle(cfg):
     T, B = FULL[cfg]
     solver = bench.make_shard_solver(cfg, B, 0, 0, presolve=True)
     spots = np.array([0, B // 2, B - 1])
-    o, knots = _oracle_spots(solver, spots)
-    o.solve(maxiter=5)
-    _compare(solver, o, spots, f"{cfg} presolve")
+
+    def run(pool):  # presolve, then two receding-horizon steps with the knot rotation
+        o, knots = _oracle_spots(solver, spots, pool)
+        o.solve(maxiter=5)
+        out = [_snap(o)]
+        for k in range(2):
+            knots = knots[1:T] + knots[:1] + knots[T:]
+            kd = (_abi.KnotDesc * len(knots))(*[_abi.KnotDesc(*x) for x in knots])
+            assert o.L.oracle_set_knots(o.h, kd, _abi.dptr(o.pool), o.pool.size) == 0
+            o.mpc_shift()
+            o.solve(maxiter=1, is_feasible=False, reg_init=0.1)
+            out.append(_snap(o))
+        return out
+
+    refs, floors = _with_floors(run, solver.problem._packed()[1])
+    _compare(solver, spots, f"{cfg} presolve", refs[0], floors[0])
     for k in range(2):
         bench.mpc_step(solver, 1, rotate=True)
-        knots = knots[1:T] + knots[:1] + knots[T:]
-        kd = (_abi.KnotDesc * len(knots))(*[_abi.KnotDesc(*x) for x in knots])
-        assert o.L.oracle_set_knots(o.h, kd, _abi.dptr(o.pool), o.pool.size) == 0
-        o.mpc_shift()
-        o.solve(maxiter=1, is_feasible=False, reg_init=0.1)
-        _compare(solver, o, spots, f"{cfg} shift step {k}")
+        _compare(solver, spots, f"{cfg} shift step {k}", refs[k + 1], floors[k + 1])
     q = np.linalg.norm(np.asarray(solver.xs)[..., 3:7], axis=-1)
     np.testing.assert_allclose(q, 1.0, atol=1e-9)
 

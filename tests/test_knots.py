@@ -17,7 +17,7 @@ from crocoddyl_amd import _abi, synthetic
 from crocoddyl_amd.problem import pack_problem
 from oracle import fddp_np
 
-RTOL = 1e-6
+RTOL = 1e-8  # element-wise (helpers.elem_err); north_star: xs/us/cost within 1e-6 relative
 
 
 def hetero_setup(name, T, B, **kw):
@@ -47,11 +47,11 @@ def _live(us, knots):
 def _same(rg, ro, g, o, knots=None):
     for f in ("status", "iter", "n_iter_run", "is_feasible", "xreg"):
         np.testing.assert_array_equal(rg[f], ro[f], err_msg=f)
-    assert helpers.rel_err(g.xs(), o.xs()) < RTOL
+    helpers.parity("xs", g.xs(), o.xs(), RTOL)
     if knots is None:
-        assert helpers.rel_err(g.us(), o.us()) < RTOL
+        helpers.parity("us", g.us(), o.us(), RTOL)
     else:
-        assert helpers.rel_err(_live(g.us(), knots), _live(o.us(), knots)) < RTOL
+        helpers.parity("us (live)", _live(g.us(), knots), _live(o.us(), knots), RTOL)
     assert float(np.max(np.abs(rg["cost"] - ro["cost"]) / np.maximum(1, np.abs(ro["cost"])))) < RTOL
 
 
