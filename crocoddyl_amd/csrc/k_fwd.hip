@@ -1,6 +1,12 @@
 // Line-search rollout kernels (fddp_kernels.hpp forward_kernel, ls_select_kernel).
 // FDDP_TU_FWD = 0: the generic and dense fast-path variants + ls_select; 1: the
 // multibody-only variant (the large one), so the two compile in parallel.
+// The rollout's knot calc solves [M | Jc^T | tau - nle] by the dense blocked Gauss-Jordan
+// (multibody.hpp MB_CALC_DENSE): measured on the C5 walk, the tree-sparse LTDL with the
+// cost records on its idle waves has to be called out of line here (the backend's register
+// alignment check trips on it inlined at the 256-VGPR cap), and the calls cost the rollout
+// 6 % (29.9 -> 31.8 ms per step), more than the solve gains.
+#define MB_CALC_DENSE 1
 #include "fast_path.hpp"
 #include "fddp_kernels.hpp"
 #include "ktab.hpp"

@@ -2046,6 +2046,550 @@ MB_HD __attribute__((always_inline)) inline void contact_jac_lane(const Blk& b, 
 // the caller) for configuration q; `costs(wave, l)` runs on waves >= 1 in
 // the phase after the kinematics (nullptr-like no-op allowed).
 // `early(wave, l)` runs on waves >= 1 beside the local placements (work on x / u only).
+#if defined(__HIP_DEVICE_COMPILE__)
+// ---- fp64 matrix-core products (v_mfma_f64_16x16x4_f64) ---------------------------
+// Fragment maps (MI355X guide, f64 16x16x4): A[i = lane & 15][k = lane >> 4],
+// B[k = lane >> 4][j = lane & 15], C/D col = lane & 15, row = (lane >> 4) + 4 reg.
+// Every wave of the workgroup takes 16 x 16 output tiles round-robin; loads outside
+// the operands read as exact zeros, so padded rows / columns stay zero.
+typedef double mb_f64x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ mb_f64x4 mb_mfma(double a, double b, mb_f64x4 c) {
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+typedef __attribute__((address_space(3))) double mb_lds_d;
+#endif
+
+// ---- tree-sparse LTDL of the joint-space inertia (RBDA 6.3) ------------------------
+// M (nj x nj, column-major at ld lda, both triangles as the CRBA writes them) has the
+// branch-induced sparsity of the kinematic tree: M_ij != 0 only when i is an ancestor-
+// or-self of j or j of i, in the dof tree whose parent of d is chain_parent(b, d) (the
+// free-flyer's six dofs form a chain). Featherstone's LTDL factorisation M = L^T D L
+// keeps L (unit lower triangular) on that pattern, and the reference's solvers reach
+// M^-1 through Pinocchio's sparse Cholesky of M (contact-fwddyn.hxx:94,132: forwardDynamics
+// / getKKTContactDynamicMatrixInverse; free-fwddyn.hxx:64: aba). A dof's row is final once
+// all its descendants are eliminated, and dofs of one depth are never ancestor and
+// descendant of each other, so a whole depth level is eliminated in one step, deepest
+// first: the chain of dependent steps is the tree depth (16 on Talos) instead of the nj (38)
+// pivots of a dense factorisation, and each step is one FMA per pattern entry.
+// G = L^-1 (same pattern) follows level by level from the root, and
+//   M^-1 = G D^-1 G^T,   M^-1 B = G (D^-1 (G^T B)),
+// whose sums run over common ancestors only.
+// Storage: L, then G, in place of M's lower triangle on the pattern, D on the diagonal;
+// M's upper triangle is left as it was. The factorisation and G run on wave 0 alone
+// (run_w0 steps, one wave-level fence per level); the products on the whole workgroup.
+struct TreeWork {
+  Mask* cm;      // nj: chain ancestors-or-self of each dof (index order = depth order)
+  Mask* dsc;     // nj: strict descendants
+  Mask* lev;     // 64: the dofs of each depth
+  double* dinv;  // nj: 1 / D
+  int* bad;      // set on a non-positive D (the LLT failure)
+};
+MB_HD __forceinline__ Mask chain_mask(const Blk& b, const WVals& W, int d) {
+  return (b.ff && d < 6) ? ((Mask(2) << d) - 1) : *W.anc(d);
+}
+MB_HD __forceinline__ int mask_depth(Mask m) { return __builtin_popcountll(m) - 1; }
+MB_HD __forceinline__ int mask_low(Mask m) { return __builtin_ctzll(m); }
+// 1 / d to working precision: v_rcp_f64 corrected by x0 (1 + e + e^2), e = 1 - d x0
+// (relative error e^3, as the blocked Gauss-Jordan's pivots)
+MB_HD __forceinline__ double mb_recip(double d) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const double x0 = __builtin_amdgcn_rcp(d);
+  const double e = __builtin_fma(-d, x0, 1.);
+  return __builtin_fma(x0, __builtin_fma(e, e, e), x0);
+#else
+  return 1. / d;
+#endif
+}
+// the tree's depth (uniform: every thread computes it from the ancestor masks)
+MB_HD inline int tree_depth(const Blk& b, const WVals& W) {
+  int md = 0;
+  for (int k = 0; k < b.nj; ++k) {
+    const int d = mask_depth(chain_mask(b, W, k));
+    md = d > md ? d : md;
+  }
+  return md;
+}
+// M -> (L, D) in place, then L -> G = L^-1 in place; tw.dinv = 1 / D. md: tree_depth.
+// The level steps as executor phases (the host emulation; the device for trees deeper
+// than its register fast path, tree_ltdl_wave).
+template <class X>
+MB_HD inline void tree_ltdl_steps(const X& ex, const Blk& b, const WVals& W, double* A_, int lda, const TreeWork& tw,
+                                  int md) {
+  const int nj = b.nj;
+  double* A = ex.lds(A_);
+  ex.run_w0([&](int lane) {
+    if (lane < nj) {
+      const Mask c = chain_mask(b, W, lane);
+      Mask d = 0;
+      for (int k = lane + 1; k < nj; ++k) d |= ((chain_mask(b, W, k) >> lane) & 1ull) << k;
+      tw.cm[lane] = c;
+      tw.dsc[lane] = d;
+    }
+    Mask lv = 0;  // lane l: the dofs at depth l
+    for (int k = 0; k < nj; ++k) lv |= Mask(mask_depth(chain_mask(b, W, k)) == lane ? 1 : 0) << k;
+    tw.lev[lane] = lv;
+    if (lane == 0) *tw.bad = 0;
+  });
+  // Level L, deepest first: (a) every row i above level L takes the contributions of its
+  // descendants k at depth L (rows final since the deeper levels), H_ij -= H_ki H_kj / D_k
+  // for j in the ancestors-or-self of i; (b) the rows of level L + 1 (final now) are
+  // scaled to L_kj = H_kj / D_k. (a) reads the rows of level L and writes rows above it,
+  // (b) rewrites the rows of level L + 1: no lane reads what another writes.
+#pragma unroll 1
+  for (int L = md; L >= -1; --L)
+    ex.run_w0([&](int i) {
+      if (i >= nj) return;
+      const Mask ci = tw.cm[i];
+      const int di = mask_depth(ci);
+      if (di < L) {
+        Mask km = tw.dsc[i] & tw.lev[L];
+        while (km) {
+          const int k = mask_low(km);
+          km &= km - 1;
+          const double f = A[k + lda * i] * mb_recip(A[k + lda * k]);
+          Mask jm = ci;
+          while (jm) {
+            const int j = mask_low(jm);
+            jm &= jm - 1;
+            A[i + lda * j] -= f * A[k + lda * j];
+          }
+        }
+      } else if (di == L + 1) {
+        const double d = A[i + lda * i];
+        const double inv = mb_recip(d);
+        if (!(d > 0.)) *tw.bad = 1;
+        tw.dinv[i] = inv;
+        Mask jm = ci & ~(Mask(1) << i);
+        while (jm) {
+          const int j = mask_low(jm);
+          jm &= jm - 1;
+          A[i + lda * j] *= inv;
+        }
+      }
+    });
+  // G = L^-1: G_k = e_k - sum_{m in anc(k)} L_km G_m, level L from the root: row k (deeper
+  // than L) takes the term of its ancestor m at depth L, whose row is final; position (k, m)
+  // holds L_km until this step and G_km from it on.
+#pragma unroll 1
+  for (int L = 0; L < md; ++L)
+    ex.run_w0([&](int k) {
+      if (k >= nj) return;
+      const Mask ck = tw.cm[k];
+      if (mask_depth(ck) <= L) return;
+      const int m = mask_low(ck & tw.lev[L]);
+      const double l = A[k + lda * m];
+      Mask im = ck & ((Mask(1) << m) - 1);
+      while (im) {
+        const int i = mask_low(im);
+        im &= im - 1;
+        A[k + lda * i] -= l * A[m + lda * i];
+      }
+      A[k + lda * m] = -l;
+    });
+  ex.sync();
+}
+#if defined(__HIP_DEVICE_COMPILE__)
+// Device fast path of tree_ltdl for trees of depth < kTreeKD, on wave 0 in one phase:
+// lane i holds row i of the factor in registers, path-indexed (entry s = the column of
+// i's ancestor at depth s; s = depth(i) the diagonal), so every update is a static-index
+// register FMA; the rows other lanes need (a level's rows, then G's rows) go through LDS
+// (PR: nj x kTreeKD), the levels and descendant sets are wave ballots, and one wave-level
+// fence separates the levels. Same results as the generic steps up to the summation order
+// of a row's contributions.
+constexpr int kTreeKD = 16;
+#ifndef MB_GJ_MARK
+#define MB_GJ_MARK(id)  // (tools/mb_probe: phase stamps)
+#endif
+typedef __attribute__((address_space(3))) Mask mb_lds_mask;
+typedef __attribute__((address_space(3))) int mb_lds_int;
+__device__ __forceinline__ void tree_wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+// (the LDS operands arrive typed as LDS; the own row lives in registers during the
+// elimination, then L in the row's LDS copy, so only G's row is in registers after it)
+// (MB_TREE_NOINLINE builds it out of line: inlined into the rollout kernel at its
+// 256-VGPR cap, the register allocation trips the backend's "even aligned vector
+// registers" check; the rollout takes the dense solve instead, k_fwd.hip MB_CALC_DENSE.)
+#ifdef MB_TREE_NOINLINE
+#define MB_TREE_INL __attribute__((noinline))
+#else
+#define MB_TREE_INL __forceinline__
+#endif
+__device__ __forceinline__ Mask readlane_mask(Mask v, int l) {
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)v, l);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v >> 32), l);
+  return (Mask(hi) << 32) | lo;
+}
+__device__ MB_TREE_INL void tree_ltdl_wave(const mb_lds_mask* anc, int ff, int nj, mb_lds_d* A, int lda,
+                                           int md, mb_lds_d* PR, mb_lds_d* dinv_out, mb_lds_int* bad_out) {
+  // Written for the instruction stream of one wave: every register array index is static
+  // (the levels are unrolled, so level L touches only the path entries s < L), the
+  // level's dofs are a uniform (scalar) loop with their rows read as LDS broadcasts, and
+  // every LDS access is unconditional within its lanes.
+  constexpr int KD = kTreeKD;
+  const int pld = md + 1;  // PR row stride (a row has depth + 1 <= md + 1 entries)
+  MB_GJ_MARK(0);
+  const int lane = (int)threadIdx.x & 63;
+  const bool act = lane < nj;
+  const int rl = act ? lane : 0;  // (inactive lanes read row 0 and store nothing)
+  const Mask cmi = act ? ((ff && lane < 6) ? ((Mask(2) << lane) - 1) : anc[lane]) : Mask(1);
+  const int di = act ? mask_depth(cmi) : -1;
+  // the ancestors by depth (col[s], s <= di; col[di] = the dof itself; beyond: the dof)
+  int col[KD];
+  {
+    Mask cur = cmi;
+#pragma unroll
+    for (int s = 0; s < KD; ++s) {
+      const int c = (int)__builtin_ctzll(cur | (Mask(1) << 63));
+      col[s] = c < nj ? c : rl;
+      cur &= cur - 1;
+    }
+  }
+  // row i of M, path-indexed (entries beyond the diagonal are never read)
+  double R[KD];
+#pragma unroll
+  for (int s = 0; s < KD; ++s) R[s] = A[rl + lda * col[s]];
+  mb_lds_d* pr = PR + pld * rl;
+  MB_GJ_MARK(1);
+  double dinv = 0.;
+  bool bad = false;
+  // the rows of depth L are final: stored for the level that reads them, with 1 / D
+  // (L static: the diagonal is R[L], and the row has L + 1 entries)
+  auto finalize = [&](auto Lc) __attribute__((always_inline)) {
+    constexpr int L = decltype(Lc)::value;
+    if (act && di == L) {
+#pragma unroll
+      for (int s = 0; s <= L; ++s) pr[s] = R[s];
+      const double d = R[L];
+      dinv = mb_recip(d);
+      bad = bad || !(d > 0.);
+      dinv_out[lane] = dinv;
+    }
+  };
+  // (the deepest level: every row of depth md is final from the start)
+#pragma unroll
+  for (int s = 0; s < KD; ++s)
+    if (act && di == md && s <= md) pr[s] = R[s];
+  if (act && di == md) {
+    double d = 0.;
+#pragma unroll
+    for (int s = 0; s < KD; ++s) d = s == di ? R[s] : d;
+    dinv = mb_recip(d);
+    bad = bad || !(d > 0.);
+    dinv_out[lane] = dinv;
+  }
+  tree_wave_sync();
+  MB_GJ_MARK(2);
+  // elimination, deepest level first: row i takes the contributions of its descendants k
+  // at depth L, H_is -= (H_ki / D_k) H_ks over the path entries s <= depth(i) < L
+  auto level = [&](auto Lc) __attribute__((always_inline)) {
+    constexpr int L = decltype(Lc)::value;
+    if (L > md) return;
+    Mask lev = __ballot(act && di == L);  // the dofs at depth L (uniform)
+    const bool mine = act && di < L;
+    while (lev) {
+      const int k = mask_low(lev);
+      lev &= lev - 1;
+      const Mask ck = readlane_mask(cmi, k);
+      if (mine && ((ck >> lane) & 1ull)) {
+        const mb_lds_d* pk = PR + pld * k;
+        const double f = pk[di] * dinv_out[k];
+#pragma unroll
+        for (int s = 0; s < L; ++s) R[s] = __builtin_fma(-f, pk[s], R[s]);
+      }
+    }
+    finalize(std::integral_constant<int, L - 1>{});
+    tree_wave_sync();
+    MB_GJ_MARK(3 + md - L);
+  };
+  static_assert(KD == 16, "the levels below are unrolled for kTreeKD = 16");
+  level(std::integral_constant<int, 15>{});
+  level(std::integral_constant<int, 14>{});
+  level(std::integral_constant<int, 13>{});
+  level(std::integral_constant<int, 12>{});
+  level(std::integral_constant<int, 11>{});
+  level(std::integral_constant<int, 10>{});
+  level(std::integral_constant<int, 9>{});
+  level(std::integral_constant<int, 8>{});
+  level(std::integral_constant<int, 7>{});
+  level(std::integral_constant<int, 6>{});
+  level(std::integral_constant<int, 5>{});
+  level(std::integral_constant<int, 4>{});
+  level(std::integral_constant<int, 3>{});
+  level(std::integral_constant<int, 2>{});
+  level(std::integral_constant<int, 1>{});
+  MB_GJ_MARK(19);
+  // L = row i / D_i below the diagonal (registers; the final row values are in R)
+  double Lr[KD];
+#pragma unroll
+  for (int s = 0; s < KD; ++s) Lr[s] = R[s] * dinv;
+  // G = L^-1 from the root: row k takes the term of its ancestor at depth t (whose G row,
+  // final after step t - 1, is read from PR); the rows of depth t + 1 are final after step t
+  double Gr[KD];
+#pragma unroll
+  for (int s = 0; s < KD; ++s) Gr[s] = 0.;
+  tree_wave_sync();
+#pragma unroll
+  for (int t = 0; t < KD - 1; ++t) {
+    if (t < md) {
+      if (act && di > t) {
+        const mb_lds_d* pm = PR + pld * col[t];
+        double g[KD];
+#pragma unroll
+        for (int s = 0; s < t; ++s) g[s] = pm[s];
+        const double l = Lr[t];
+#pragma unroll
+        for (int s = 0; s < t; ++s) Gr[s] = __builtin_fma(-l, g[s], Gr[s]);
+        Gr[t] = -l;
+        if (di == t + 1)
+#pragma unroll
+          for (int s = 0; s <= t; ++s) pr[s] = Gr[s];
+      }
+      tree_wave_sync();
+    }
+  }
+  MB_GJ_MARK(20);
+  // G below the diagonal into A's pattern entries (D stays on the diagonal)
+  if (act)
+#pragma unroll
+    for (int s = 0; s < KD - 1; ++s)
+      if (s < di) A[lane + lda * col[s]] = Gr[s];
+  if (lane == 0) *bad_out = 0;
+  tree_wave_sync();
+  if (bad) *bad_out = 1;
+  MB_GJ_MARK(21);
+}
+#endif
+#if defined(__HIP_DEVICE_COMPILE__)
+// G's entry (r, m) from the dense storage tree_ltdl leaves (G below the diagonal on the
+// pattern, exact zeros elsewhere below it, D on the diagonal: G_rr = 1), zero above the
+// diagonal and outside nj
+__device__ __forceinline__ double tree_gd(const mb_lds_d* A, int lda, int nj, int r, int m) {
+  const bool in = r < nj && m < nj;
+  const double v = A[in ? r + lda * m : 0];
+  return (!in || m > r) ? 0. : (m == r ? 1. : v);
+}
+// Minv = G D^-1 G^T on the matrix cores: the upper 16 x 16 tiles, each entry with r <= c
+// stored at (r, c) and (c, r) (exactly symmetric); a tile's k-range stops at the smaller
+// block (G is lower triangular)
+__device__ __forceinline__ void tree_minv_mfma(const double* A_, int lda, int nj, const double* dinv_, double* Mi_) {
+  const mb_lds_d* A = (const mb_lds_d*)lds_ptr(A_);
+  const mb_lds_d* dinv = (const mb_lds_d*)lds_ptr(dinv_);
+  mb_lds_d* Mi = (mb_lds_d*)lds_ptr(Mi_);
+  const int lane = (int)threadIdx.x & 63, wave = (int)threadIdx.x >> 6, nw = (int)blockDim.x >> 6;
+  const int li = lane & 15, lk = lane >> 4, nt = (nj + 15) >> 4, ntiles = nt * (nt + 1) / 2;
+#pragma unroll 1
+  for (int tile = wave; tile < ntiles; tile += nw) {
+    int ti = 0, rem = tile;
+    while (rem >= nt - ti) {
+      rem -= nt - ti;
+      ++ti;
+    }
+    const int tj = ti + rem;
+    const int r = 16 * ti + li, c = 16 * tj + li;
+    const int kmax = 16 * ti + 16 < nj ? 16 * ti + 16 : nj;
+    mb_f64x4 acc0 = {0., 0., 0., 0.}, acc1 = {0., 0., 0., 0.};  // two chains (even / odd k-steps)
+#pragma unroll 2
+    for (int kb = 0; kb < kmax; kb += 8) {
+      const int m0 = kb + lk, m1 = kb + 4 + lk;
+      const double w0 = m0 < nj ? dinv[m0] : 0., w1 = m1 < nj ? dinv[m1] : 0.;
+      acc0 = mb_mfma(tree_gd(A, lda, nj, r, m0), tree_gd(A, lda, nj, c, m0) * w0, acc0);
+      if (kb + 4 < kmax) acc1 = mb_mfma(tree_gd(A, lda, nj, r, m1), tree_gd(A, lda, nj, c, m1) * w1, acc1);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int row = 16 * ti + lk + 4 * q, col = 16 * tj + li;
+      const double v = acc0[q] + acc1[q];
+      if (row < nj && col < nj && row <= col) {
+        Mi[row + lda * col] = v;
+        Mi[col + lda * row] = v;
+      }
+    }
+  }
+}
+// The right-hand sides B (nj x nb at A + lda nj) -> M^-1 B in place on the matrix cores:
+// T = D^-1 G^T B (T: nj x nb, ld nj), a workgroup barrier, X = G T. Every thread calls.
+__device__ __forceinline__ void tree_solve_mfma(const double* A_, int lda, int nj, int nb, const double* dinv_,
+                                                double* T_) {
+  const mb_lds_d* A = (const mb_lds_d*)lds_ptr(A_);
+  const mb_lds_d* dinv = (const mb_lds_d*)lds_ptr(dinv_);
+  mb_lds_d* T = (mb_lds_d*)lds_ptr(T_);
+  mb_lds_d* B = (mb_lds_d*)lds_ptr(A_ + (int64_t)lda * nj);
+  const int lane = (int)threadIdx.x & 63, wave = (int)threadIdx.x >> 6, nw = (int)blockDim.x >> 6;
+  const int li = lane & 15, lk = lane >> 4, tr = (nj + 15) >> 4, tc = (nb + 15) >> 4;
+  // T tile (tm, tcc): rows m, k over r >= 16 tm
+#pragma unroll 1
+  for (int tile = wave; tile < tr * tc; tile += nw) {
+    const int tm = tile / tc, tcc = tile - tm * tc;
+    const int m = 16 * tm + li, c = 16 * tcc + li;
+    mb_f64x4 acc0 = {0., 0., 0., 0.}, acc1 = {0., 0., 0., 0.};
+#pragma unroll 2
+    for (int kb = 16 * tm; kb < nj; kb += 8) {
+      const int r0 = kb + lk, r1 = kb + 4 + lk;
+      const double b0 = (r0 < nj && c < nb) ? B[r0 + lda * c] : 0.;
+      const double b1 = (r1 < nj && c < nb) ? B[r1 + lda * c] : 0.;
+      acc0 = mb_mfma(tree_gd(A, lda, nj, r0, m), b0, acc0);
+      if (kb + 4 < nj) acc1 = mb_mfma(tree_gd(A, lda, nj, r1, m), b1, acc1);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int row = 16 * tm + lk + 4 * q, col = 16 * tcc + li;
+      if (row < nj && col < nb) T[row + nj * col] = (acc0[q] + acc1[q]) * dinv[row];
+    }
+  }
+  __syncthreads();
+  // X tile (tr_, tcc): rows r, k over m <= 16 tr_ + 15
+#pragma unroll 1
+  for (int tile = wave; tile < tr * tc; tile += nw) {
+    const int ti = tile / tc, tcc = tile - ti * tc;
+    const int r = 16 * ti + li, c = 16 * tcc + li;
+    const int kmax = 16 * ti + 16 < nj ? 16 * ti + 16 : nj;
+    mb_f64x4 acc0 = {0., 0., 0., 0.}, acc1 = {0., 0., 0., 0.};
+#pragma unroll 2
+    for (int kb = 0; kb < kmax; kb += 8) {
+      const int m0 = kb + lk, m1 = kb + 4 + lk;
+      const double t0 = (m0 < nj && c < nb) ? T[m0 + nj * c] : 0.;
+      const double t1 = (m1 < nj && c < nb) ? T[m1 + nj * c] : 0.;
+      acc0 = mb_mfma(tree_gd(A, lda, nj, r, m0), t0, acc0);
+      if (kb + 4 < kmax) acc1 = mb_mfma(tree_gd(A, lda, nj, r, m1), t1, acc1);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int row = 16 * ti + lk + 4 * q, col = 16 * tcc + li;
+      if (row < nj && col < nb) B[row + lda * col] = acc0[q] + acc1[q];
+    }
+  }
+  __syncthreads();
+}
+#endif
+// M -> (L, D) -> G = L^-1 in place, tw.dinv = 1 / D (tree_ltdl_steps / tree_ltdl_wave).
+// PR: (md + 1) * nj doubles of scratch (the device fast path's rows; the generic steps
+// use tw.cm / tw.dsc instead, so the two may share their space).
+// Independent work of the caller for the waves the factorisation leaves idle: side(slot,
+// lane, nlanes) on waves >= 1 (lane counted from wave 1), slots 0 .. nslots - 1 one after
+// another, the side waves meeting at an LDS counter (ctr, zeroed by the caller in an
+// earlier phase) between slots. Without the device fast path the slots run afterwards as
+// ordinary phases.
+struct TreeNoSide {
+  MB_HD void operator()(int, int, int) const {}
+};
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ __forceinline__ void tree_side_barrier(int* ctr_, int target) {
+  mb_lds_int* ctr = (mb_lds_int*)lds_ptr(ctr_);
+  if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  while (__hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < target) __builtin_amdgcn_s_sleep(1);
+}
+#endif
+template <class X, class Side = TreeNoSide>
+MB_HD __forceinline__ void tree_ltdl(const X& ex, const Blk& b, const WVals& W, double* A, int lda, const TreeWork& tw,
+                                     int md, double* PR, Side side = Side{}, int nslots = 0, int* ctr = nullptr) {
+#if defined(__HIP_DEVICE_COMPILE__)
+#ifndef MB_TREE_NO_WAVE
+  if (md < kTreeKD) {
+    double* const Al = ex.lds(A);
+    double* const PRl = ex.lds(PR);
+    ex.run([&](int tid) {
+      if (tid < 64) {
+        tree_ltdl_wave((const mb_lds_mask*)ex.lds(W.anc(0)), b.ff ? 1 : 0, b.nj, (mb_lds_d*)Al, lda, md,
+                       (mb_lds_d*)PRl, (mb_lds_d*)ex.lds(tw.dinv), (mb_lds_int*)ex.lds(tw.bad));
+      } else if (nslots > 0) {
+        const int sl = tid - 64, snt = ex.nt - 64;
+#pragma unroll 1
+        for (int slot = 0; slot < nslots; ++slot) {
+          if (slot > 0) tree_side_barrier(ctr, (snt >> 6) * slot);
+          side(slot, sl, snt);
+        }
+      }
+    });
+    return;
+  }
+#endif
+#endif
+  (void)PR;
+  tree_ltdl_steps(ex, b, W, A, lda, tw, md);
+  for (int slot = 0; slot < nslots; ++slot)
+    ex.run([&](int lane) {
+      if (lane >= 64) side(slot, lane - 64, ex.nt - 64);
+    });
+}
+// G's entry (r, m), m an ancestor-or-self of r (the diagonal holds D: G_rr = 1)
+MB_HD __forceinline__ double tree_g(const double* A, int lda, int r, int m) { return m == r ? 1. : A[r + lda * m]; }
+// Minv (ld lda) = G D^-1 G^T from tree_ltdl, exactly symmetric (the sum for (r, c) and
+// (c, r) has the same terms in the same order). Returns false on a non-positive pivot.
+// (device: on the matrix cores, tree_minv_mfma)
+template <class X>
+MB_HD inline bool tree_minv(const X& ex, const Blk& b, const double* A_, int lda, const TreeWork& tw, double* Mi_) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  ex.run([&](int) { tree_minv_mfma(A_, lda, b.nj, tw.dinv, Mi_); });
+  return *tw.bad == 0;
+#endif
+  const int nj = b.nj;
+  const double* A = ex.lds(A_);
+  double* Mi = ex.lds(Mi_);
+  ex.run([&](int lane) {
+    for (int e = lane; e < nj * nj; e += ex.nt) {
+      const int c = e / nj, r = e - nj * c;
+      Mask mm = tw.cm[r] & tw.cm[c];
+      double s = 0.;
+      while (mm) {
+        const int m = mask_low(mm);
+        mm &= mm - 1;
+        s += (tree_g(A, lda, r, m) * tree_g(A, lda, c, m)) * tw.dinv[m];
+      }
+      Mi[r + lda * c] = s;
+    }
+  });
+  return *tw.bad == 0;
+}
+// B (nj x nb at A + lda nj, ld lda: the right-hand sides beside M) -> M^-1 B in place,
+// through T = D^-1 G^T B (nj x nb, ld nj). Returns false on a non-positive pivot.
+template <class X>
+MB_HD inline bool tree_solve(const X& ex, const Blk& b, double* A_, int lda, int nb, const TreeWork& tw, double* T_) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  ex.run([&](int) { tree_solve_mfma(A_, lda, b.nj, nb, tw.dinv, T_); });
+  return *tw.bad == 0;
+#endif
+  const int nj = b.nj;
+  double* A = ex.lds(A_);
+  double* T = ex.lds(T_);
+  double* B = A + (int64_t)lda * nj;
+  ex.run([&](int lane) {
+    for (int e = lane; e < nj * nb; e += ex.nt) {
+      const int c = e / nj, m = e - nj * c;
+      const double* bc = B + (int64_t)lda * c;
+      Mask rm = tw.dsc[m];
+      double s0 = bc[m], s1 = 0.;  // (two partial sums: the root's row has nj terms)
+      while (rm) {
+        const int r = mask_low(rm);
+        rm &= rm - 1;
+        s0 += A[r + lda * m] * bc[r];
+        if (!rm) break;
+        const int r2 = mask_low(rm);
+        rm &= rm - 1;
+        s1 += A[r2 + lda * m] * bc[r2];
+      }
+      T[m + nj * c] = (s0 + s1) * tw.dinv[m];
+    }
+  });
+  ex.run([&](int lane) {
+    for (int e = lane; e < nj * nb; e += ex.nt) {
+      const int c = e / nj, r = e - nj * c;
+      const double* tc = T + (int64_t)nj * c;
+      Mask mm = tw.cm[r] & ~(Mask(1) << r);
+      double s = tc[r];
+      while (mm) {
+        const int m = mask_low(mm);
+        mm &= mm - 1;
+        s += A[r + lda * m] * tc[m];
+      }
+      B[r + (int64_t)lda * c] = s;
+    }
+  });
+  return *tw.bad == 0;
+}
+
 template <class X, class EarlyF, class CostF>
 MB_HD inline void world_kinematics(const X& ex, const Blk& b, const WVals& W, const double* q, double* A, int lda,
                                    EarlyF early, CostF costs, bool world_composite = false) {
@@ -2132,6 +2676,44 @@ MB_HD inline int64_t calc_work_doubles(int nj, int nc = 0) {
          (int64_t)nc * (nc + 1) + 128 + part_doubles(nj);
 }
 
+// The calc's cost records other than the wide ones (knot_calc_x): record item i on lane
+// i / 3 of side wave i % 3 (sl: the lane counted from the first side wave, snt: the side
+// lanes), each record's weighted value into cv[k]. It rebuilds the block's views from the
+// LDS pointers, so it can be built out of line (MB_TREE_NOINLINE, as tree_ltdl_wave).
+#if defined(__HIP_DEVICE_COMPILE__) && defined(MB_TREE_NOINLINE)
+__device__ __attribute__((noinline))
+#else
+MB_HD __forceinline__
+#endif
+void calc_cost_records(const double* P_, double* w_, double* parts_, const double* x_, const double* ub_, double* cv_,
+                       int sl, int snt) {
+  const double* P = mb_lds(P_);
+  const Blk b = parse(P);
+  const WVals W{mb_lds(w_), b.nj, mb_lds(parts_)};
+  const double* x = mb_lds(x_);
+  const double* ub = mb_lds(ub_);
+  double* cv = mb_lds(cv_);
+  const int nu = b.nj - b.nun, nc = b.nc;
+  const bool imp = b.impulse;
+  const int nsw = snt >> 6, item = nsw * (sl & 63) + (sl >> 6);
+  const double* cr = b.C;
+  int nn = 0, nw = 0;
+  for (int k = 0; k < b.ncost; ++k) {
+    const CRec C{cr};
+    if (wide_cost(C, nw)) {
+      ++nw;
+    } else {
+      if (item == nn) {
+        double v = C.type() == C_FRAME_VELOCITY && imp ? 0. : cost_activation(b, W, C, x, ub, nu);
+        if (force_cost(C.type()) && nc == 0) v = force_cost_activation(b, C, nullptr, nu);
+        cv[k] = C.weight() * v;
+      }
+      ++nn;
+    }
+    cr += C.size();
+  }
+}
+
 // model->calc(data, x, u) for the Euler∘FreeFwdDynamics knot (euler.hxx:41-80,
 // free-fwddyn.hxx:44-79): a = (M + diag(armature))^-1 (u - nle) in world frame;
 // with contacts, Euler∘ContactFwdDynamics (contact-fwddyn.hxx:59-104):
@@ -2169,7 +2751,7 @@ MB_HD __forceinline__ double knot_calc_x(const X& ex, const double* P, int nx, c
   });
   // the wide records (state / control residuals: x, u only) row-parallel on waves 3 and 1
   // beside the local placements, their lane partials into pb (free until the
-  // Gauss-Jordan); once the placements exist, the other records one per lane of wave 2
+  // factorisation); the other records on the waves the factorisation leaves idle (below)
   world_kinematics(ex, b, W, x, A, lda, [&](int wave, int l) {
     const double* cr = b.C;
     int nw = 0;
@@ -2182,23 +2764,28 @@ MB_HD __forceinline__ double knot_calc_x(const X& ex, const double* P, int nx, c
       cr += C.size();
     }
   }, [&](int wave, int l) {
-    // the other records, then the contacts' position terms (log6 for the 6D ones): item
-    // i on lane i / 3 of wave 1 + i % 3, so that no wave runs two of them (a wave pays
-    // for the sum of its divergent lanes' paths)
+    // (dense solve: the other records but the frame velocities first,) the contacts'
+    // position terms (log6 for the 6D ones): item i on lane i / 3 of wave 1 + i % 3, so
+    // that no wave runs two of them (a wave pays for the sum of its divergent lanes' paths)
     if (wave > 3) return;
     const int item = 3 * l + (wave - 1);
-    const double* cr = b.C;
-    int nn = 0, nw = 0;
-    for (int k = 0; k < b.ncost; ++k) {
-      const CRec C{cr};
-      if (wide_cost(C, nw)) {
-        ++nw;
-      } else {
-        if (item == nn) cv[k] = C.weight() * cost_activation(b, W, C, x, ub, nu, false);
-        ++nn;
+    int nn = 0;
+#ifdef MB_CALC_DENSE
+    {
+      const double* cr = b.C;
+      int nw = 0;
+      for (int k = 0; k < b.ncost; ++k) {
+        const CRec C{cr};
+        if (wide_cost(C, nw)) {
+          ++nw;
+        } else {
+          if (item == nn) cv[k] = C.weight() * cost_activation(b, W, C, x, ub, nu, false);
+          ++nn;
+        }
+        cr += C.size();
       }
-      cr += C.size();
     }
+#endif
     const int kc = item - nn;
     if (!imp && kc >= 0 && kc < b.ncon) {
       int row0;
@@ -2218,8 +2805,8 @@ MB_HD __forceinline__ double knot_calc_x(const X& ex, const double* P, int nx, c
       const CRec C{contact_rec(b, lane - 64, &row0)};
       contact_a0_drift(b, W, C, a0 + row0);
     }
-    if (lane == 128) {
-      double total = 0.;
+    if (lane == 128) {  // the wide records' values from their lane partials (pb is the
+                        // factorisation's scratch next)
       const double* cr = b.C;
       int nw = 0;
       for (int k = 0; k < b.ncost; ++k) {
@@ -2227,21 +2814,41 @@ MB_HD __forceinline__ double knot_calc_x(const X& ex, const double* P, int nx, c
         if (wide_cost(C, nw)) {
           double a = 0.;
           for (int l = 0; l < 64; ++l) a += pb[64 * nw + l];
-          total += C.weight() * (0.5 * a);
+          cv[k] = C.weight() * (0.5 * a);
           ++nw;
-        } else {
-          total += cv[k];
         }
-        // force costs without active contact rows (lambda = 0)
-        if (force_cost(C.type()) && nc == 0) total += C.weight() * force_cost_activation(b, C, nullptr, nu);
-        // frame velocities, now that the body velocities exist (impulse knots: rejected by the host)
-        if (C.type() == C_FRAME_VELOCITY && !imp) total += C.weight() * cost_activation(b, W, C, x, ub, nu);
+#ifdef MB_CALC_DENSE
+        // force costs without active contact rows (lambda = 0); frame velocities, now
+        // that the body velocities exist (impulse knots: rejected by the host)
+        if (force_cost(C.type()) && nc == 0) cv[k] = C.weight() * force_cost_activation(b, C, nullptr, nu);
+        if (C.type() == C_FRAME_VELOCITY && !imp) cv[k] = C.weight() * cost_activation(b, W, C, x, ub, nu);
+#endif
         cr += C.size();
       }
-      red[0] = total;
     }
   });
+  // Every other record's weighted value into cv[k], on the waves the factorisation leaves
+  // idle: record item i on lane i / 3 of side wave i % 3 (the frame placements / CoM are
+  // long serial evaluations, which would otherwise sit on the knot's critical path); the
+  // force costs without active contact rows (lambda = 0) here, with contacts after the
+  // Schur solve; frame velocities with the body velocities (impulse knots: rejected by the
+  // host). The knot cost is their sum in record order (cost-sum.hxx:89-117), at the end.
+  auto cost_side = [&](int, int sl, int snt) { calc_cost_records(P, w, W.parts, x, ub, cv, sl, snt); };
+  // [Y | z] = M^-1 [Jc^T | tau - nle] by the tree-sparse LTDL of M; its scratch: the depth
+  // levels in pb, the dof masks, 1 / D and the intermediate D^-1 G^T B in the recursions'
+  // per-wave partials (dead from here on)
+  double* const tp = ex.lds(W.parts);
+  const TreeWork tw{(Mask*)tp, (Mask*)tp + nj, (Mask*)ex.lds(pb), tp + 2 * nj, ex.lds(flag)};
+  // (the device fast path's rows, then D^-1 G^T B, both after the masks and 1 / D)
+#ifdef MB_CALC_DENSE
+  // (the dense factorisation: the blocked Gauss-Jordan on [M | Jc^T | tau - nle])
+  (void)cost_side;
+  (void)tw;
   bool ok = mb_solve(ex, A, nj, lda, ncol, flag, pb);
+#else
+  tree_ltdl(ex, b, W, A, lda, tw, tree_depth(b, W), tp + 3 * nj, cost_side, 1);
+  bool ok = tree_solve(ex, b, A, lda, ncol - nj, tw, tp + 3 * nj);
+#endif
   // z, then a (impulse: v+, in tau's slot; z = M^-1 M v = v)
   double* a = imp ? tau : A + (int64_t)lda * (nj + nc);
   if (nc > 0) {
@@ -2258,20 +2865,17 @@ MB_HD __forceinline__ double knot_calc_x(const X& ex, const double* P, int nx, c
     ok = gauss_jordan<1>(ex, S, nc, nc, nc + 1, flag, pb) && ok;
     ex.run([&](int lane) {
       // contact-force costs (lambda = -S^-1 r, in S's last column, negated): record k's
-      // term on lane 64 + k into cv[k] (dead since the cost total), summed in record
-      // order with the next phase
+      // value on lane 64 + k into cv[k], summed in record order with the next phase
       const int kf = lane - 64;
       if (kf >= 0 && kf < b.ncost && !imp) {
         const double* cr = b.C;
         for (int k = 0; k < kf; ++k) cr += CRec{cr}.size();
         const CRec C{cr};
-        double term = 0.;
         if (force_cost(C.type())) {
           double lamv[kMaxNc];
           for (int k = 0; k < nc; ++k) lamv[k] = -S[(int64_t)nc * nc + k];
-          term = C.weight() * force_cost_activation(b, C, lamv, nu);
+          cv[kf] = C.weight() * force_cost_activation(b, C, lamv, nu);
         }
-        cv[kf] = term;
       }
       if (lane >= nj) return;
       double s = imp ? x[nq + lane] : a[lane];
@@ -2285,15 +2889,10 @@ MB_HD __forceinline__ double knot_calc_x(const X& ex, const double* P, int nx, c
       if (i < nj) a[i] = NAN;
     });
   ex.run([&](int i) {
-    if (i == 64 && nc > 0 && !imp) {  // the contact-force terms, in record order
-      double add = 0.;
-      const double* cr = b.C;
-      for (int k = 0; k < b.ncost; ++k) {
-        const CRec C{cr};
-        if (force_cost(C.type())) add += cv[k];
-        cr += C.size();
-      }
-      red[0] += add;
+    if (i == 64) {  // the knot cost: the records' values in record order
+      double total = 0.;
+      for (int k = 0; k < b.ncost; ++k) total += cv[k];
+      red[0] = total;
     }
     if (i >= nj) return;
     if (imp) {  // impulse-fwddyn.hxx:80-81: xnext = (q, v+)
@@ -2809,16 +3408,7 @@ MB_HD inline void jac_lane(const Blk& b, const WVals& W, const double* x, int j,
 // Fx == nullptr: calc only (no derivative block is written).
 #if defined(__HIP_DEVICE_COMPILE__)
 // ---- fp64 matrix-core products of the calcDiff (v_mfma_f64_16x16x4_f64) -------
-// Fragment maps (MI355X guide, f64 16x16x4): A[i = lane & 15][k = lane >> 4],
-// B[k = lane >> 4][j = lane & 15], C/D col = lane & 15, row = (lane >> 4) + 4 reg.
-// Every wave of the workgroup takes 16 x 16 output tiles round-robin; loads outside
-// the operands read as exact zeros, so padded rows / columns stay zero.
-typedef double mb_f64x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ mb_f64x4 mb_mfma(double a, double b, mb_f64x4 c) {
-  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
-}
-
-typedef __attribute__((address_space(3))) double mb_lds_d;
+// (fragment maps and mb_mfma: with the tree-sparse LTDL above)
 __device__ __attribute__((noinline)) void da_mfma_lds(const mb_lds_d* Minv, int lda, const mb_lds_d* H,
                                                       const mb_lds_d* dtau, const mb_lds_d* da0, int nj, int nc, int L,
                                                       int Ld, double mul_v, int vcols, mb_lds_d* da,
@@ -3012,6 +3602,7 @@ MB_HD __forceinline__ void knot_calc_diff_x(const X& ex, const double* P, int nx
   ex.run([&](int lane) {
     // xu_pre (device, nq + nj <= nt): this thread's x[lane] / u[lane] loaded by the caller
     // beside the parameter-block copy (one global round trip instead of two)
+    if (lane == 0) *(int*)(red + 5) = 0;  // the factorisation's side-work counter
     if (xu_pre) {
       if (lane < nq + nj) x[lane] = xu_pre[0];
       if (lane < nj) u[lane] = (use_u && lane < nu) ? xu_pre[1] : 0.;
@@ -3019,10 +3610,6 @@ MB_HD __forceinline__ void knot_calc_diff_x(const X& ex, const double* P, int nx
       for (int e = lane; e < nq + nj; e += ex.nt) x[e] = xg[e];
       if (lane < nj) u[lane] = (use_u && lane < nu) ? ug[lane] : 0.;  // (impulse: a zero velocity)
     }
-    // the identity half of [M | I] (the CRBA writes every entry of M); the device
-    // inverts M in place and needs none
-    if (!mb_inv_inplace(ex))
-      for (int e = lane; e < nj * lda; e += ex.nt) A[(int64_t)nj * lda + e] = e % lda == e / lda ? 1. : 0.;
   });
   // world-frame kinematics, M into the left half of [M | I], nle
   world_kinematics(ex, b, W, x, A, lda, [](int, int) {}, [](int, int) {}, true);
@@ -3046,16 +3633,15 @@ MB_HD __forceinline__ void knot_calc_diff_x(const X& ex, const double* P, int nx
     MB_DUMP(3, a0, nc, 1, nc);
   }
   double* pb = red + 8;
-  double* Minv;  // column-major nj x nj (ld lda); with contacts: d a / d tau after the Schur step
+  // M^-1 by the tree-sparse LTDL of M (tree_ltdl), into the second half of the A area
+  // (column-major nj x nj, ld lda); with contacts: d a / d tau after the Schur step.
+  double* Minv = A + (int64_t)lda * nj;
   // The velocity-product maps of the derivatives (per-body N_b, h_b into the dtau area;
-  // their subtree sums into the da area; P_k, Q_k) need the velocities and composite
-  // inertias only: the waves the blocked Gauss-Jordan leaves idle build them meanwhile,
-  // one map per barrier interval (vp: how many are done when it returns)
+  // their subtree sums into the da area; P_k, Q_k) and the cost-Jacobian columns need the
+  // velocities and composite inertias only: on the device the waves the factorisation
+  // leaves idle build them meanwhile, one map per slot (vp: how many are built), the
+  // Jacobian columns beside the body maps when the idle waves are at least two (jac_side).
   double* nsub = da;  // (unused by impulse knots)
-  // The cost-Jacobian columns (one (dof, jac cost) item per lane, jac_lane) need the
-  // kinematics only as well: beside the body maps in the first slot, when the idle
-  // waves are at least two (jac_side).
-  bool jac_side = false;
   auto vp_side = [&](int slot, int sl, int snt) {
     if (slot == 0) {
       if (!imp)
@@ -3071,10 +3657,25 @@ MB_HD __forceinline__ void knot_calc_diff_x(const X& ex, const double* P, int nx
       for (int j = sl; j < nj; j += snt) qp_lane_ns(W, j, nsub, qp);
     }
   };
-  int vp = 0;
-  bool ok = mb_invert(ex, A, nj, lda, flag, pb, &Minv, vp_side, &vp);
-  jac_side = vp > 0 && (ex.nt >> 6) - ((nj + 15) >> 4) >= 2;
-  vp = imp ? 0 : (vp < 3 ? vp : 3);
+#if defined(__HIP_DEVICE_COMPILE__)
+  // scratch of the factorisation: the depth levels and 1 / D in pb; in the M^-1 area (free
+  // until tree_minv, nj lda >= nj^2 doubles) the fast path's rows ((md + 1) nj) or the
+  // generic steps' dof masks (2 nj), which never run together
+  const int md = tree_depth(b, W);
+  const int vp = (md < kTreeKD && ex.nt >= 128) ? 3 : 0;
+  const bool jac_side = vp > 0 && ex.nt - 64 >= 128;
+  double* const tp = ex.lds(Minv);
+  const TreeWork tw{(Mask*)tp, (Mask*)tp + nj, (Mask*)ex.lds(pb), ex.lds(pb) + 64, ex.lds(flag)};
+  tree_ltdl(ex, b, W, A, lda, tw, md, tp, vp_side, vp, (int*)(red + 5));
+#else
+  // (host emulation: the scratch in the recursions' per-wave partials, no side work)
+  const int vp = 0;
+  const bool jac_side = false;
+  double* const tp = ex.lds(W.parts);
+  const TreeWork tw{(Mask*)tp, (Mask*)tp + nj, (Mask*)ex.lds(pb), tp + 2 * nj, ex.lds(flag)};
+  tree_ltdl(ex, b, W, A, lda, tw, tree_depth(b, W), tp + 3 * nj);
+#endif
+  bool ok = tree_minv(ex, b, A, lda, tw, Minv);
   Minv = ex.lds(Minv);
   MB_DUMP(4, Minv, nj, nj, lda);
   // z = (M + A)^-1 (tau - nle) (the acceleration without contacts); Y = Minv Jc^T

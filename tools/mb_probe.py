@@ -1,6 +1,6 @@
 """Diagnostic (not a test): writes one knot of a config (block, x, u) for
 tools/mb_probe and runs it. Usage: python tools/mb_probe.py <config> <knot> <nwg>
-(PROBE_COSTS=a,b keeps only those cost records active; PROBE_COSTS= none; a 4th
+(PROBE_BIN: another probe build; PROBE_COSTS=a,b keeps only those cost records active; PROBE_COSTS= none; a 4th
 argument "layout" prints the LDS plan only, no GPU needed).
 """
 import os
@@ -36,4 +36,4 @@ with open(path, "wb") as f:
     blk.tofile(f)
     x.astype(np.float64).tofile(f)
     u.astype(np.float64).tofile(f)
-sys.exit(subprocess.call([os.path.join(ROOT, "tools", "mb_probe"), path, nwg] + sys.argv[4:]))
+sys.exit(subprocess.call([os.environ.get("PROBE_BIN", os.path.join(ROOT, "tools", "mb_probe")), path, nwg] + sys.argv[4:]))
