@@ -255,11 +255,33 @@ def _cpu_baseline_child(cfg, T, seed, target_s, box, protocol):
                                 f"{', SolverBoxFDDP ' + box_text(cfg) if box else ''}"}), flush=True)
 
 
-def load_pmc(cfg):
+def lib_sha256():
+    """sha256 (first 16 hex digits) of the libfddp_hip.so this process runs"""
+    import hashlib
+    from crocoddyl_amd._lib import LIB_PATH
+    with open(LIB_PATH, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
+def load_pmc(cfg, lib_hash):
+    """The HBM / MFMA counters of `cfg` in profiles/pmc_backward.json (tools/prof_summary.py),
+    used only when they were collected on this very library build: the entry's lib_sha256
+    must equal the running library's (and its tag CROCODDYL_AMD_PMC_TAG, when set).
+    Returns (entry or None, provenance dict for the roofline)."""
+    want_tag = os.environ.get("CROCODDYL_AMD_PMC_TAG")
     try:
-        return json.load(open(os.path.join(ROOT, "profiles", "pmc_backward.json"))).get(cfg)
+        e = json.load(open(os.path.join(ROOT, "profiles", "pmc_backward.json"))).get(cfg)
     except Exception:
-        return None
+        e = None
+    prov = {"source": "profiles/pmc_backward.json", "lib_sha256": lib_hash}
+    if e is None:
+        return None, dict(prov, status="absent: no counters for this config")
+    prov.update(tag=e.get("tag"), profiled_lib_sha256=e.get("lib_sha256"))
+    if e.get("lib_sha256") != lib_hash:
+        return None, dict(prov, status="refused: counters collected on another library build (traffic = null)")
+    if want_tag and e.get("tag") != want_tag:
+        return None, dict(prov, status=f"refused: tag {e.get('tag')} != CROCODDYL_AMD_PMC_TAG={want_tag}")
+    return e, dict(prov, status="matched")
 
 
 def warm_start_arrays(config, running, x0s, dims):
@@ -618,7 +640,8 @@ def main():
         F = backward_flops_per_knot(n, m) * B * T
         Y = backward_bytes_per_knot(n, m) * B * T
         achieved = F / avg_bwd_s / 1e12
-        pmc = load_pmc(args.config)
+        lib_hash = lib_sha256()
+        pmc, pmc_prov = load_pmc(args.config, lib_hash)
         roof_bwd = {"kernel": "backward Riccati sweep (bwd_mfma.hpp)", "bound": "mfma", "achieved": round(achieved, 3),
                     "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / FP64_PEAK_TFLOPS, 4),
                     "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
@@ -680,7 +703,7 @@ def main():
                 kfl[1] * nk if kfl else None, (kpm.get("mb_calc_diff") or {}).get("hbm_bytes_per_step"),
                 {"knots_per_launch": nk}))
         dominant = max(rooflines, key=lambda k: rooflines[k][0])
-        roof = dict(rooflines[dominant][1], dominant_of=sorted(rooflines))
+        roof = dict(rooflines[dominant][1], dominant_of=sorted(rooflines), pmc=pmc_prov)
         cpu = None
         if ws == 1 and not args.no_cpu_baseline:
             try:
@@ -731,6 +754,7 @@ def main():
             "line_search_trials_last_step": trials_summary(trials),
             "secondary_protocol": secondary,
             **({"box_backward": box_bwd} if box_bwd else {}),
+            "lib_sha256": lib_hash,
             "roofline": roof,
             "rooflines": {k: v[1] for k, v in rooflines.items()},
             "cpu_baseline": cpu,

@@ -144,6 +144,7 @@ struct Dev {
   BoxQPCfg boxcfg;                 // qp_(nu, 100, 0.1, 1e-5, 0.) (box-fddp.cpp:16)
   int64_t mbw;                     // LDS doubles of the multibody calc scratch (0: no multibody knots)
   int64_t mbd;                     // LDS doubles of the multibody calcDiff work area (its parameter block follows)
+  int mbspill;                     // its plan's spill flags (multibody.hpp diff_spill)
   // parallel line search (generic trials): npar trials of one element run in
   // npar workgroups; trial slot 0 writes the other trajectory buffer, slots
   // 1..npar-1 their own copies (same [b][t] layout), accepted ones are copied back

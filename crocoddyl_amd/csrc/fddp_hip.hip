@@ -35,17 +35,25 @@ using namespace fddp;
 namespace fddp {
 namespace ktab {
 int mb_knot_threads(int v) {
-  return v == MB_W1 ? mb_knot_threads_1() : v == MB_X2 ? mb_knot_threads_2() : v == MB_X8 ? mb_knot_threads_3()
-                                                                                        : mb_knot_threads_0();
+  return v == MB_W1   ? mb_knot_threads_1()
+         : v == MB_X2 ? mb_knot_threads_2()
+         : v == MB_X8 ? mb_knot_threads_3()
+         : v == MB_S2 ? mb_knot_threads_4()
+                      : mb_knot_threads_0();
 }
 const void* mb_knot_fn(int v) {
-  return v == MB_W1 ? mb_knot_fn_1() : v == MB_X2 ? mb_knot_fn_2() : v == MB_X8 ? mb_knot_fn_3() : mb_knot_fn_0();
+  return v == MB_W1   ? mb_knot_fn_1()
+         : v == MB_X2 ? mb_knot_fn_2()
+         : v == MB_X8 ? mb_knot_fn_3()
+         : v == MB_S2 ? mb_knot_fn_4()
+                      : mb_knot_fn_0();
 }
 hipError_t mb_knot(int v, dim3 grid, size_t smem, hipStream_t s, const Dev& D, int sel_calc, int sel_diff) {
   switch (v) {
     case MB_W1: return mb_knot_1(grid, smem, s, D, sel_calc, sel_diff);
     case MB_X2: return mb_knot_2(grid, smem, s, D, sel_calc, sel_diff);
     case MB_X8: return mb_knot_3(grid, smem, s, D, sel_calc, sel_diff);
+    case MB_S2: return mb_knot_4(grid, smem, s, D, sel_calc, sel_diff);
     default: return mb_knot_0(grid, smem, s, D, sel_calc, sel_diff);
   }
 }
@@ -495,7 +503,8 @@ static bool mb_x2(const fddp_handle* h) {
 // Multibody knots (knot-parallel): calc for sel_calc, calcDiff for sel_diff (-1: none).
 int launch_mb(fddp_handle* h, int sel_calc, int sel_diff) {
   const Dev& D = h->D;
-  const int v = mb_x2(h) ? ktab::MB_X2 : (mb_x8(h) ? ktab::MB_X8 : (mb_one_per_cu(h) ? ktab::MB_W1 : ktab::MB_W2));
+  const int v = D.mbspill ? ktab::MB_S2
+                           : mb_x2(h) ? ktab::MB_X2 : (mb_x8(h) ? ktab::MB_X8 : (mb_one_per_cu(h) ? ktab::MB_W1 : ktab::MB_W2));
   KLAUNCH(ktab::mb_knot(v, dim3(D.T + 1, D.B), h->mb_diff_smem, h->stream, D, sel_calc, sel_diff));
   return FDDP_OK;
 }
@@ -844,7 +853,18 @@ int apply_knots(fddp_handle* h, const fddp_knot_desc* knots, const double* param
         for (int b = 0; b < nb; ++b)
           mb_pmax = std::max<int64_t>(mb_pmax, (int64_t)params[knots[t].param_offset + (int64_t)b * knots[t].param_stride + 3]);
       }
-    D.mbd = h->has_mb ? pad2(fddp::mb::diff_layout(mb_nj, mb_njac, mb_nc, mb_vcols, mb_nu, mb_nrows).total) : 0;
+    // the calcDiff's LDS plan: spilled to the output blocks where the all-LDS plan would
+    // leave room for one workgroup per CU only (multibody.hpp diff_spill; FDDP_MB_SPILL=0
+    // forces the all-LDS plan, for A/B runs)
+    static const int spill_env = [] {
+      const char* e = std::getenv("FDDP_MB_SPILL");
+      return e ? std::atoi(e) : -1;
+    }();
+    D.mbspill = h->has_mb && spill_env != 0
+                    ? fddp::mb::diff_spill(mb_nj, mb_njac, mb_nc, mb_vcols, mb_nu, mb_nrows, mb_pmax, D.m)
+                    : 0;
+    D.mbd = h->has_mb ? pad2(fddp::mb::diff_layout(mb_nj, mb_njac, mb_nc, mb_vcols, mb_nu, mb_nrows, D.mbspill).total)
+                      : 0;
     h->mb_diff_smem = h->has_mb ? sizeof(double) * (D.mbd + pad2(mb_pmax)) : 0;
     const int64_t budget = (150 * 1024) / 8 - (2 * D.sX + D.sM + 2 * D.sN + 5 * (kNT / kWave) + 16) - D.mbw;
     // LDS-staged parameter blocks up to pcap doubles; larger (dense) blocks are read from
@@ -916,6 +936,7 @@ int apply_knots(fddp_handle* h, const fddp_knot_desc* knots, const double* param
         {ktab::mb_knot_fn(ktab::MB_W1), h->mb_diff_smem, h->has_mb, "mb_knot_kernel_w1"},
         {ktab::mb_knot_fn(ktab::MB_X8), h->mb_diff_smem, h->has_mb, "mb_knot_kernel_x8"},
         {ktab::mb_knot_fn(ktab::MB_X2), h->mb_diff_smem, h->has_mb, "mb_knot_kernel_x2"},
+        {ktab::mb_knot_fn(ktab::MB_S2), h->mb_diff_smem, h->has_mb, "mb_knot_kernel_s2"},
     };
     for (const Req& r : reqs) {
       if (!r.use) continue;

@@ -254,7 +254,7 @@ __global__ __launch_bounds__(NT) void calc_diff_kernel(Dev D, int sel, int gaps,
 // (derivative blocks) for those selected by sel_diff (-1: none), fused: the
 // calcDiff evaluates the dynamics the calc needs anyway. The gaps of these
 // knots are written by calc_diff_kernel as for any knot.
-template <int NT>
+template <int NT, int SP = 0>
 __device__ __forceinline__ void mb_knot_body(const Dev& D, int sel_calc, int sel_diff) {
   const int t = blockIdx.x, b = blockIdx.y;
   const fddp_knot_desc kd = D.knots[t];
@@ -286,12 +286,12 @@ __device__ __forceinline__ void mb_knot_body(const Dev& D, int sel_calc, int sel
   for (int e = threadIdx.x; e < psz; e += NT) P[e] = Pg[e];
   __syncthreads();
   if (do_diff)
-    mb::knot_calc_diff<NT>(P, D.nx, D.m, xg, ug, running && kd.nu > 0, sm, D.Fx + kk * D.sNN, D.Fu + kk * D.sNM,
+    mb::knot_calc_diff<NT, SP>(P, D.nx, D.m, xg, ug, running && kd.nu > 0, sm, D.Fx + kk * D.sNN, D.Fu + kk * D.sNM,
                        D.Lxx + kk * D.sNN, D.Lxu + kk * D.sNM, D.Luu + kk * D.sMM, D.Lx + kk * D.sN,
-                       D.Lu + kk * D.sM, xn, cost, pre ? xu : nullptr);
+                       D.Lu + kk * D.sM, xn, cost, pre ? xu : nullptr, D.mbspill);
   else
-    mb::knot_calc_diff<NT>(P, D.nx, D.m, xg, ug, running && kd.nu > 0, sm, nullptr, nullptr, nullptr, nullptr, nullptr,
-                       nullptr, nullptr, xn, cost, pre ? xu : nullptr);
+    mb::knot_calc_diff<NT, SP>(P, D.nx, D.m, xg, ug, running && kd.nu > 0, sm, nullptr, nullptr, nullptr, nullptr, nullptr,
+                       nullptr, nullptr, xn, cost, pre ? xu : nullptr, D.mbspill);
 }
 // Two register budgets of the same kernel: 2 waves/EU (256 VGPRs, a few spills) lets two
 // workgroups share a CU where the LDS plan allows it (<= 80 KB: the trot, the arm); when
@@ -316,6 +316,14 @@ __global__ __launch_bounds__(mb::kMbDiffNT) __attribute__((amdgpu_waves_per_eu(1
 #if defined(FDDP_TU_MB) && FDDP_TU_MB == 2
 __global__ __launch_bounds__(mb::kMbDiffNT / 2) __attribute__((amdgpu_waves_per_eu(2))) void mb_knot_kernel_x2(Dev D, int sel_calc, int sel_diff) {
   mb_knot_body<mb::kMbDiffNT / 2>(D, sel_calc, sel_diff);
+}
+#endif
+
+// The spilled plan (multibody.hpp diff_spill: the large trees, whose all-LDS plan leaves
+// room for one workgroup per CU): two 256-thread workgroups per CU.
+#if defined(FDDP_TU_MB) && FDDP_TU_MB == 4
+__global__ __launch_bounds__(mb::kMbDiffNT) __attribute__((amdgpu_waves_per_eu(2))) void mb_knot_kernel_s2(Dev D, int sel_calc, int sel_diff) {
+  mb_knot_body<mb::kMbDiffNT, 1>(D, sel_calc, sel_diff);
 }
 #endif
 

@@ -1,5 +1,5 @@
 // Multibody knot kernels (fddp_kernels.hpp mb_knot_kernel*), one variant per object:
-// the Makefile compiles this file once per FDDP_TU_MB = ktab::MB_W2 .. MB_X8.
+// the Makefile compiles this file once per FDDP_TU_MB = ktab::MB_W2 .. MB_S2.
 #include "fddp_kernels.hpp"
 #include "ktab.hpp"
 
@@ -23,10 +23,14 @@ const void* const kFn = (const void*)mb_knot_kernel_w1;
 constexpr int kThreads = mb::kMbDiffNT / 2;
 const void* const kFn = (const void*)mb_knot_kernel_x2;
 #define MB_KERNEL mb_knot_kernel_x2
-#else
+#elif FDDP_TU_MB == 3
 constexpr int kThreads = 2 * mb::kMbDiffNT;
 const void* const kFn = (const void*)mb_knot_kernel_x8;
 #define MB_KERNEL mb_knot_kernel_x8
+#else
+constexpr int kThreads = mb::kMbDiffNT;
+const void* const kFn = (const void*)mb_knot_kernel_s2;
+#define MB_KERNEL mb_knot_kernel_s2
 #endif
 }  // namespace
 

@@ -18,8 +18,9 @@ constexpr int kNTF = 512;  // fused calc/calcDiff: 8 waves per CU keep the deriv
 
 // Multibody knot calc/calcDiff, one workgroup per (knot, element) (k_mb.hip):
 //   MB_W2 256 threads at 2 waves/EU, MB_W1 256 threads at 1 wave/EU,
-//   MB_X2 128 threads (small trees), MB_X8 512 threads (the one-per-CU plans)
-enum { MB_W2 = 0, MB_W1 = 1, MB_X2 = 2, MB_X8 = 3, MB_NVAR = 4 };
+//   MB_X2 128 threads (small trees), MB_X8 512 threads (the one-per-CU plans),
+//   MB_S2 256 threads at 2 waves/EU on the spilled plan (multibody.hpp diff_spill)
+enum { MB_W2 = 0, MB_W1 = 1, MB_X2 = 2, MB_X8 = 3, MB_S2 = 4, MB_NVAR = 5 };
 int mb_knot_threads(int v);
 const void* mb_knot_fn(int v);
 hipError_t mb_knot(int v, dim3 grid, size_t smem, hipStream_t s, const Dev& D, int sel_calc, int sel_diff);
@@ -61,14 +62,17 @@ int mb_knot_threads_0();
 int mb_knot_threads_1();
 int mb_knot_threads_2();
 int mb_knot_threads_3();
+int mb_knot_threads_4();
 const void* mb_knot_fn_0();
 const void* mb_knot_fn_1();
 const void* mb_knot_fn_2();
 const void* mb_knot_fn_3();
+const void* mb_knot_fn_4();
 hipError_t mb_knot_0(dim3 grid, size_t smem, hipStream_t s, const Dev& D, int sel_calc, int sel_diff);
 hipError_t mb_knot_1(dim3 grid, size_t smem, hipStream_t s, const Dev& D, int sel_calc, int sel_diff);
 hipError_t mb_knot_2(dim3 grid, size_t smem, hipStream_t s, const Dev& D, int sel_calc, int sel_diff);
 hipError_t mb_knot_3(dim3 grid, size_t smem, hipStream_t s, const Dev& D, int sel_calc, int sel_diff);
+hipError_t mb_knot_4(dim3 grid, size_t smem, hipStream_t s, const Dev& D, int sel_calc, int sel_diff);
 const void* forward_fn_0(int v);
 hipError_t forward_0(int v, dim3 grid, size_t smem, hipStream_t s, const Dev& D, const Prm& prm, int mode,
                      double alpha, int* count, int64_t pcap, int group);

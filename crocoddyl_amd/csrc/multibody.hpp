@@ -1144,9 +1144,9 @@ MB_HD inline void jlog6_col(const double* R, const double* p, int k, double* col
 // which each lane evaluates for its own dof: no serial chain through LDS.
 // anc(i) holds every dof of the ancestor-or-self bodies (all six free-flyer
 // dofs for the base), so v_k is the full body velocity. The placements
-// oMi = oMparent * liMi are composed by pointer jumping (ceil(log2 nj) rounds).
+// oMi = oMparent * liMi are composed by each lane walking its ancestors (w_walk).
 // ---------------------------------------------------------------------------
-constexpr int kWPerJoint = 96;
+constexpr int kWPerJoint = 80;
 constexpr int kMaxCosts = 64;
 struct WVals {
   double* base;
@@ -1154,7 +1154,7 @@ struct WVals {
   double* parts;  // per-wave partial sums of the recursions: 4 x 6 per dof (kPartDoubles)
   MB_HD double* R(int i) const { return mb_lds(base + kWPerJoint * i); }  // liMi rotation
   MB_HD double* p(int i) const { return R(i) + 9; }
-  MB_HD double* oR(int i) const { return R(i) + 12; }  // oMi (also pointer-jumping buffer A)
+  MB_HD double* oR(int i) const { return R(i) + 12; }  // oMi
   MB_HD double* op(int i) const { return R(i) + 21; }
   MB_HD double* S(int i) const { return R(i) + 24; }   // dof motion subspace (world)
   MB_HD double* m(int i) const { return R(i) + 30; }   // body mass (0 on the massless free-flyer dofs)
@@ -1167,11 +1167,7 @@ struct WVals {
   MB_HD double* ch(int i) const { return R(i) + 59; }
   MB_HD double* cI(int i) const { return R(i) + 62; }
   MB_HD double* cq(int i) const { return R(i) + 68; }  // S_i qdd_i + v_i x S_i qd_i
-  MB_HD double* Rb(int i) const { return R(i) + 74; }  // pointer-jumping buffer B
-  MB_HD double* pb(int i) const { return R(i) + 83; }
-  MB_HD double* jA(int i) const { return R(i) + 86; }  // jump targets of buffers A / B
-  MB_HD double* jB(int i) const { return R(i) + 87; }
-  MB_HD double* fb(int i) const { return R(i) + 90; }  // body force I a + v x* I v
+  MB_HD double* fb(int i) const { return R(i) + 74; }  // body force I a + v x* I v
   // per-wave partial sums of the ancestor / subtree recursions (wave w's share of the dofs)
   MB_HD double* part(int w, int i) const { return mb_lds(parts + 6 * ((int64_t)w * nj + i)); }
   MB_HD Mask* anc(int i) const { return (Mask*)(base + kWPerJoint * nj) + i; }  // ancestors-or-self dofs
@@ -1218,7 +1214,6 @@ MB_HD inline void w_joint_local(const Blk& b, const WVals& W, const double* q, i
     W.p(i)[e] = p[e];
     W.op(i)[e] = p[e];
   }
-  *W.jA(i) = (double)chain_parent(b, i);
   if (i == 0) {
     for (int e = 0; e < 6; ++e) W.root_a()[e] = e < 3 ? -b.g[e] : 0.;
   }
@@ -1251,16 +1246,11 @@ MB_HD inline void w_walk(const Blk& b, const WVals& W, int i) {
   for (int e = 0; e < 3; ++e) W.op(i)[e] = p[e];
 }
 
-// lane i < nj: oMi into oR/op (from buffer B after an odd number of rounds),
-// world motion subspace and body inertia.
-MB_HD inline void w_joint_world(const Blk& b, const WVals& W, int i, bool from_b) {
+// lane i < nj: world motion subspace and body inertia from oMi (oR/op).
+MB_HD inline void w_joint_world(const Blk& b, const WVals& W, int i) {
   double oR[9], op[3], w[3], ax[3];
-  for (int e = 0; e < 9; ++e) oR[e] = from_b ? W.Rb(i)[e] : W.oR(i)[e];
-  for (int e = 0; e < 3; ++e) op[e] = from_b ? W.pb(i)[e] : W.op(i)[e];
-  if (from_b) {
-    for (int e = 0; e < 9; ++e) W.oR(i)[e] = oR[e];
-    for (int e = 0; e < 3; ++e) W.op(i)[e] = op[e];
-  }
+  for (int e = 0; e < 9; ++e) oR[e] = W.oR(i)[e];
+  for (int e = 0; e < 3; ++e) op[e] = W.op(i)[e];
   dof_axis(b, i, ax);
   matvec3(oR, ax, w);
   if (dof_prismatic(b, i)) {
@@ -2188,6 +2178,7 @@ MB_HD inline void tree_ltdl_steps(const X& ex, const Blk& b, const WVals& W, dou
     });
   ex.sync();
 }
+constexpr int kTreeKD = 16;  // depth bound of the device fast path (below)
 #if defined(__HIP_DEVICE_COMPILE__)
 // Device fast path of tree_ltdl for trees of depth < kTreeKD, on wave 0 in one phase:
 // lane i holds row i of the factor in registers, path-indexed (entry s = the column of
@@ -2196,7 +2187,6 @@ MB_HD inline void tree_ltdl_steps(const X& ex, const Blk& b, const WVals& W, dou
 // (PR: nj x kTreeKD), the levels and descendant sets are wave ballots, and one wave-level
 // fence separates the levels. Same results as the generic steps up to the summation order
 // of a row's contributions.
-constexpr int kTreeKD = 16;
 #ifndef MB_GJ_MARK
 #define MB_GJ_MARK(id)  // (tools/mb_probe: phase stamps)
 #endif
@@ -2601,7 +2591,7 @@ MB_HD inline void world_kinematics(const X& ex, const Blk& b, const WVals& W, co
   ex.run([&](int lane) {
     if (lane < nj) {
       w_walk(b, W, lane);
-      w_joint_world(b, W, lane, false);
+      w_joint_world(b, W, lane);
     }
   });
   // CRBA about each column's joint: the subtree composites in wave partials (beside them,
@@ -2950,7 +2940,24 @@ struct DiffLayout {
   // contact area (nc > 0): Jc nc x nj, a0 nc, lambda nc, Y = Minv Jc^T and
   // H = Y S^-1 (nj x nc each), [S | I | r] nc x (2nc + 1), da0/dx nc x L, fx 6 nj
   int64_t Jc, a0, lam, Y, H, Sx, da0, fx, zv, dfx, dfu;
+  // the per-wave partials of the recursions (kinematics / the RNEA at the solved a), the
+  // per-body velocity-product maps and their subtree sums; half: doubles per half of A
+  int64_t pk, pr, nb, ns, half;
+  int spill;       // kSpill* flags the plan was made with
+  int64_t ht;      // host emulation: its factorisation scratch (70 nj)
+  int64_t htotal;  // host emulation: total plus its own areas (da, the factorisation scratch)
 };
+// The spilled calcDiff plan (the Talos-size trees): the LDS plan keeps what the phases read
+// at random, and the arrays each written once and streamed once go to the knot's own
+// output blocks in global memory, dead there until the blocks are written (after their
+// last read): dtau/dx into Lxx (read by the da product, the Gauss-Newton blocks write Lxx
+// after it), the body maps and their subtree sums into Fx (read up to the tangent
+// directions; the da product writes Fx), the jac-cost Jacobians into Lxu (kSpillJ: read by
+// the residual rows, before the Gauss-Newton blocks), d lambda / dx, du into Fu (kSpillF:
+// read by the residual rows; Fu is written last). The product's epilogue writes Fx
+// itself, so da needs no area; Minv and the contact arrays share the factorisation's A
+// area. Two workgroups share a CU under it (<= 80 KB with the parameter block).
+constexpr int kSpillBlocks = 1, kSpillJ = 2, kSpillF = 4;
 // vec area: x (nq + nj <= 2 nj + 1), u (nj), nle / z / a / tau (3 nj), jac-cost
 // residuals (6 per cost), Jexp6 / Ad(exp6^-1) (72)
 // Cost-derivative area (doubles) for nrows stacked residual rows over L + nu columns.
@@ -2963,46 +2970,213 @@ MB_HD __forceinline__ int64_t cost_area_doubles(int nj, int nu, int nrows) {
   return cost_table_doubles() + kMaxCostCols + (int64_t)nrows * cost_rows_ld(nj, nu);
 }
 __host__ __device__ inline DiffLayout diff_layout(int nj, int njac, int nc = 0, bool vel_cols = false, int nu = 0,
-                                                  int nrows = 0) {
+                                                  int nrows = 0, int spill = 0) {
   const int L = 2 * nj;
   DiffLayout l;
-  // dtau [k][L] (first the per-body N_b, h_b: 42 per dof); da = -Kinv (dtau; da0) [r][L]
-  // (first the subtree sums Nsub, Hsub)
-  // (da rows at the odd stride L + 1: the Fx assembly reads a column of it per wave)
-  const int64_t dsz = pad2((int64_t)nj * (L + 1) > 42 * (int64_t)nj ? (int64_t)nj * (L + 1) : 42 * (int64_t)nj);
-  // the world values, then dtau: both dead after the da phase, so the cost-derivative
-  // area can run over both
+  l.spill = spill;
+  const int64_t jsz = (int64_t)6 * (vel_cols ? L : nj) * (njac > 0 ? njac : 1);  // jac-cost Jacobians [cost][6][jw]
+  const int64_t ca = cost_area_doubles(nj, nu, nrows);
+  const int64_t wvs = pad2(WVals::doubles(nj));
+  if (!(spill & kSpillBlocks)) {
+    // dtau [k][L] (first the per-body N_b, h_b: 42 per dof); the da area (first the subtree
+    // sums Nsub, Hsub; da itself on the host: the device's product writes Fx directly)
+    // (da rows at the odd stride L + 1: the Fx assembly reads a column of it per wave)
+    const int64_t dsz = pad2((int64_t)nj * (L + 1) > 42 * (int64_t)nj ? (int64_t)nj * (L + 1) : 42 * (int64_t)nj);
+    // the world values, then dtau: both dead after the da phase, so the cost-derivative
+    // area can run over both
+    l.wv = 0;
+    l.dtau = l.wv + wvs;
+    l.half = pad2((int64_t)lda_of(nj) * nj);
+    l.A = l.dtau + dsz;  // [M | Minv], ld lda_of(nj)
+    l.da = l.A + 2 * l.half;
+    l.pk = l.pr = l.nb = l.dtau;
+    l.ns = l.da;
+    l.qp = l.da + dsz;
+    l.vec = l.qp + (int64_t)12 * nj;      // Q_k, P_k
+    l.J = l.vec + pad2(6 * nj + 1 + 6 * kMaxJacCosts + 72);
+    l.red = l.J + jsz;
+    l.total = l.red + 8 + 128;  // reductions, Gauss-Jordan pivot-column buffer
+    l.Jc = l.total;
+    l.a0 = l.Jc + (int64_t)nc * nj;
+    l.lam = l.a0 + nc;
+    l.Y = l.lam + nc;
+    l.H = l.Y + (int64_t)nj * nc;
+    l.Sx = l.H + (int64_t)nj * nc;
+    l.da0 = l.Sx + (int64_t)nc * (2 * nc + 1);
+    l.fx = l.da0 + (int64_t)nc * L;
+    l.zv = l.fx + 6 * nj;  // impulse: v+ - v
+    l.dfx = l.zv + nj;     // d lambda / dx (nc x L), d lambda / du (nc x nj): CostModelContactForce
+    l.dfu = l.dfx + (int64_t)nc * L;
+    l.total = nc > 0 ? l.dfu + (int64_t)nc * nj : l.total;
+    // the table (written on spare lanes during the da phase, beside the dtau reads) within
+    // the world values; the diagonal terms and R rows (written after it) also over dtau
+    if (cost_table_doubles() <= wvs && ca <= wvs + dsz) {
+      l.R = l.wv;
+    } else {
+      l.R = pad2(l.total);
+      l.total = l.R + ca;
+    }
+    l.ht = pad2(l.total);  // host: the factorisation scratch
+    l.htotal = l.ht + pad2((int64_t)70 * nj);
+    return l;
+  }
+  // spilled plan; live ranges (phases of knot_calc_diff_x):
+  //   world values        kinematics .. tangent directions; then the cost area
+  //   A, first half       M and its factors .. M^-1; then Y (z / Y .. Kinv), the partials
+  //                       of the RNEA at the solved a, then da0 / dlambda/dx, du (tangent
+  //                       directions .. residual rows) when they fit, else their own area
+  //   A, second half      the recursions' partials (kinematics), the factorisation's
+  //                       scratch, then M^-1 / Kinv top-left .. Fu
+  //   contact area        Jc, a0, lambda, H, [S | I | r], joint forces, v+ - v
+  l.half = pad2(lda_of(nj) * (int64_t)nj > part_doubles(nj) ? lda_of(nj) * (int64_t)nj : part_doubles(nj));
   l.wv = 0;
-  l.dtau = l.wv + pad2(WVals::doubles(nj));
-  l.A = l.dtau + dsz;  // [M | I] -> [. | Minv], ld lda_of(nj)
-  l.da = l.A + pad2((int64_t)lda_of(nj) * 2 * nj);
-  l.qp = l.da + dsz;
-  l.vec = l.qp + (int64_t)12 * nj;      // Q_k, P_k
-  l.J = l.vec + pad2(6 * nj + 1 + 6 * kMaxJacCosts + 72);
-  l.red = l.J + (int64_t)6 * (vel_cols ? L : nj) * (njac > 0 ? njac : 1);  // jac-cost Jacobians [cost][6][jw]
-  l.total = l.red + 8 + 128;  // reductions, Gauss-Jordan pivot-column buffer
+  l.A = wvs;
+  l.pk = l.A + l.half;
+  l.pr = l.A;
+  l.dtau = l.nb = l.ns = -1;  // in the output blocks
+  l.qp = l.A + 2 * l.half;
+  l.vec = l.qp + (int64_t)12 * nj;
+  l.red = l.vec + pad2(6 * nj + 1 + 6 * kMaxJacCosts + 72);
+  l.total = l.red + 8 + 128;
+  l.J = -1;
+  if (!(spill & kSpillJ)) {
+    l.J = l.total;
+    l.total = pad2(l.J + jsz);
+  }
   l.Jc = l.total;
   l.a0 = l.Jc + (int64_t)nc * nj;
   l.lam = l.a0 + nc;
-  l.Y = l.lam + nc;
-  l.H = l.Y + (int64_t)nj * nc;
+  l.H = l.lam + nc;
   l.Sx = l.H + (int64_t)nj * nc;
-  l.da0 = l.Sx + (int64_t)nc * (2 * nc + 1);
-  l.fx = l.da0 + (int64_t)nc * L;
-  l.zv = l.fx + 6 * nj;  // impulse: v+ - v
-  l.dfx = l.zv + nj;     // d lambda / dx (nc x L), d lambda / du (nc x nj): CostModelContactForce
-  l.dfu = l.dfx + (int64_t)nc * L;
-  l.total = nc > 0 ? l.dfu + (int64_t)nc * nj : l.total;
-  // the table (written on spare lanes during the da phase, beside the dtau reads) within
-  // the world values; the diagonal terms and R rows (written after it) also over dtau
-  const int64_t ca = cost_area_doubles(nj, nu, nrows);
-  if (cost_table_doubles() <= pad2(WVals::doubles(nj)) && ca <= pad2(WVals::doubles(nj)) + dsz) {
+  l.fx = l.Sx + (int64_t)nc * (2 * nc + 1);
+  l.zv = l.fx + 6 * nj;
+  if (nc > 0) l.total = pad2(l.zv + nj);
+  const int64_t ysz = (int64_t)nj * nc, d0 = pad2((int64_t)nc * L), dfs = pad2((int64_t)nc * L) + (int64_t)nc * nj;
+  l.Y = ysz <= l.half ? l.A : l.total;
+  if (nc > 0 && l.Y == l.total) l.total = pad2(l.total + ysz);
+  l.da0 = d0 <= l.half ? l.A : l.total;
+  if (nc > 0 && l.da0 == l.total) l.total = pad2(l.total + d0);
+  // d lambda / dx, du: the knot's Fu block (kSpillF: written after the residual rows read
+  // them), else after da0 when both fit the half, else their own area
+  if (spill & kSpillF) {
+    l.dfx = l.dfu = -1;
+  } else {
+    l.dfx = (l.da0 == l.A && d0 + dfs <= l.half) ? l.A + d0 : l.total;
+    if (nc > 0 && l.dfx == l.total) l.total = pad2(l.total + dfs);
+    l.dfu = l.dfx + pad2((int64_t)nc * L);
+  }
+  // the cost area over the world values and the first half of A (contiguous; dead from the
+  // da phase on, the table written during it within the world values; not over the half
+  // when d lambda / dx, du sit there: the residual rows read them)
+  const bool f_in_half = nc > 0 && l.dfx >= l.A && l.dfx < l.A + l.half;
+  if (cost_table_doubles() + kMaxCostCols <= wvs && ca <= wvs + (f_in_half ? 0 : l.half)) {
     l.R = l.wv;
   } else {
     l.R = pad2(l.total);
     l.total = l.R + ca;
   }
+  // host emulation: the da area and the factorisation's scratch of its own
+  l.da = pad2(l.total);
+  l.ht = l.da + pad2((int64_t)nj * (L + 1));
+  l.htotal = l.ht + pad2((int64_t)70 * nj);
   return l;
+}
+// The spill flags of a handle's plan: spill when the all-LDS plan (with the parameter block
+// of psz doubles) exceeds half the CU's LDS, the tree is large enough for the body maps
+// and their sums (84 nj doubles) to fit in the Fx block (4 nj^2); the Jacobians go to
+// Lxu (2 nj m), d lambda / dx, du to Fu (2 nj m) when they fit.
+MB_HD inline int diff_spill(int nj, int njac, int nc, bool vcols, int nu, int nrows, int64_t psz, int m) {
+  const DiffLayout a = diff_layout(nj, njac, nc, vcols, nu, nrows, 0);
+  if ((pad2(a.total) + pad2(psz)) * 8 <= 80 * 1024 || 84 * (int64_t)nj > 4 * (int64_t)nj * nj) return 0;
+  const int64_t jsz = (int64_t)6 * (vcols ? 2 * nj : nj) * (njac > 0 ? njac : 1);
+  const int64_t fsz = pad2((int64_t)nc * 2 * nj) + (int64_t)nc * nj;
+  return kSpillBlocks | (jsz <= (int64_t)2 * nj * m ? kSpillJ : 0) | (nc > 0 && fsz <= (int64_t)2 * nj * m ? kSpillF : 0);
+}
+
+// Live ranges of the calcDiff's LDS arrays (knot_calc_diff_x's phases, in order), for the
+// static check of its plans (diff_layout_check): arrays whose areas overlap must not be
+// live in a common phase.
+enum DiffPhase {
+  DP_INIT, DP_KIN, DP_CONTACT, DP_FACTOR, DP_MINV, DP_ZY, DP_SX, DP_SGJ, DP_LAMH, DP_KINV, DP_RNEA2, DP_CALC,
+  DP_QPJAC, DP_TANG, DP_DA, DP_RROWS, DP_GN, DP_END
+};
+struct DiffRegion {
+  const char* name;
+  int64_t off, size;
+  int first, last;
+};
+// The regions of plan l (host emulation areas excluded); returns their count (<= 40).
+MB_HD inline int diff_layout_regions(const DiffLayout& l, int nj, int njac, int nc, bool vcols, int nu, int nrows,
+                                     DiffRegion* r) {
+  const int L = 2 * nj;
+  const bool sp = l.spill & kSpillBlocks;
+  const int64_t wvs = WVals::doubles(nj), jsz = (int64_t)6 * (vcols ? L : nj) * (njac > 0 ? njac : 1);
+  int k = 0;
+  auto add = [&](const char* n, int64_t off, int64_t size, int first, int last) {
+    if (off >= 0 && size > 0) r[k++] = DiffRegion{n, off, size, first, last};
+  };
+  add("world values", l.wv, wvs, DP_INIT, DP_TANG);
+  add("M / its factors", l.A, (int64_t)lda_of(nj) * nj, DP_KIN, DP_MINV);
+  // (the fast path's rows, or the generic steps' masks; then the recursions' partials are
+  // dead, and M^-1 is written)
+  // ((depth + 1) nj <= min(kTreeKD, nj) nj doubles, or 2 nj)
+  const int64_t fs = (int64_t)nj * (kTreeKD < nj ? kTreeKD : nj);
+  add("factorisation scratch", l.A + l.half, fs > 2 * nj ? fs : 2 * nj, DP_FACTOR, DP_FACTOR);
+  add("Minv / Kinv", l.A + l.half, (int64_t)lda_of(nj) * nj, DP_MINV, DP_END);
+  add("partials (kinematics)", l.pk, part_doubles(nj), DP_KIN, DP_KIN);
+  add("partials (RNEA at a)", l.pr, part_doubles(nj), DP_RNEA2, DP_RNEA2);
+  add("qp", l.qp, (int64_t)12 * nj, DP_FACTOR, DP_TANG);
+  add("vec", l.vec, 6 * nj + 1 + 6 * kMaxJacCosts + 72, DP_INIT, DP_END);
+  add("red / pivots", l.red, 8 + 128, DP_INIT, DP_END);
+  if (!(l.spill & kSpillJ)) add("jac-cost Jacobians", l.J, jsz, DP_FACTOR, DP_RROWS);
+  if (!sp) {
+    // (built beside the factorisation, or after the RNEA at a when no wave is idle then)
+    add("body maps (side)", l.nb, (int64_t)42 * nj, DP_FACTOR, DP_FACTOR);
+    add("body maps", l.nb, (int64_t)42 * nj, DP_QPJAC, DP_QPJAC);
+    add("subtree sums", l.ns, (int64_t)42 * nj, DP_FACTOR, DP_TANG);
+    add("dtau", l.dtau, (int64_t)nj * L, DP_TANG, DP_DA);
+  }
+  if (nc > 0) {
+    add("Jc", l.Jc, (int64_t)nc * nj, DP_CONTACT, DP_DA);
+    add("a0", l.a0, nc, DP_CONTACT, DP_SX);
+    add("lambda", l.lam, nc, DP_LAMH, DP_END);
+    add("Y", l.Y, (int64_t)nj * nc, DP_ZY, DP_KINV);
+    add("H", l.H, (int64_t)nj * nc, DP_LAMH, DP_DA);
+    add("[S | I | r]", l.Sx, (int64_t)nc * (2 * nc + 1), DP_SX, DP_DA);
+    add("da0", l.da0, (int64_t)nc * L, DP_TANG, DP_DA);
+    add("contact joint forces", l.fx, 6 * nj, DP_KINV, DP_RNEA2);
+    add("v+ - v", l.zv, nj, DP_KINV, DP_RNEA2);
+    if (!(l.spill & kSpillF)) {
+      add("d lambda / dx", l.dfx, (int64_t)nc * L, DP_DA, DP_RROWS);
+      add("d lambda / du", l.dfu, (int64_t)nc * nj, DP_DA, DP_RROWS);
+    }
+  }
+  add("cost table", l.R, cost_table_doubles(), DP_DA, DP_END);
+  add("cost diagonal / rows", l.R + cost_table_doubles(), cost_area_doubles(nj, nu, nrows) - cost_table_doubles(),
+      DP_RROWS, DP_END);
+  return k;
+}
+// 0 when no two regions of the plan overlap in both LDS and live range (and all lie in
+// [0, total)); else the index + 1 of the first region in conflict (a, b: the pair).
+MB_HD inline int diff_layout_check(const DiffLayout& l, int nj, int njac, int nc, bool vcols, int nu, int nrows,
+                                   int* a = nullptr, int* b = nullptr) {
+  DiffRegion r[40];
+  const int n = diff_layout_regions(l, nj, njac, nc, vcols, nu, nrows, r);
+  for (int i = 0; i < n; ++i) {
+    if (r[i].off + r[i].size > l.total) {
+      if (a) *a = i, *b = i;
+      return i + 1;
+    }
+    for (int j = i + 1; j < n; ++j) {
+      const bool mem = r[i].off < r[j].off + r[j].size && r[j].off < r[i].off + r[i].size;
+      const bool live = r[i].first <= r[j].last && r[j].first <= r[i].last;
+      if (mem && live) {
+        if (a) *a = i, *b = j;
+        return i + 1;
+      }
+    }
+  }
+  return 0;
 }
 
 // The velocity-product terms of the derivatives are linear maps of the subtree
@@ -3409,56 +3583,91 @@ MB_HD inline void jac_lane(const Blk& b, const WVals& W, const double* x, int j,
 #if defined(__HIP_DEVICE_COMPILE__)
 // ---- fp64 matrix-core products of the calcDiff (v_mfma_f64_16x16x4_f64) -------
 // (fragment maps and mb_mfma: with the tree-sparse LTDL above)
-__device__ __attribute__((noinline)) void da_mfma_lds(const mb_lds_d* Minv, int lda, const mb_lds_d* H,
-                                                      const mb_lds_d* dtau, const mb_lds_d* da0, int nj, int nc, int L,
-                                                      int Ld, double mul_v, int vcols, mb_lds_d* da,
-                                                      const mb_lds_d* Sinv, int nfd, mb_lds_d* dfx) {
+typedef __attribute__((address_space(1))) double mb_glb_d;
+// The Fx block (euler.hxx:100-112 with JintegrateTransport / Jintegrate;
+// impulse-fwddyn.hxx:111-115) straight from the da product's accumulators:
+// da = -(Kinv_tl dtau + H da0) (contact-fwddyn.hxx:127-140 as computeABADerivatives / the
+// KKT inverse), computed transposed, tile rows = the tangent directions c, tile columns =
+// the dofs i: a lane's accumulators are da(i, c) for one i and four c, and the 16 lanes of
+// a row group store 16 consecutive rows of a column of the column-major Fx. With the
+// contact-force costs (nfd = nc) the same product's rows nj + k' ([H^T | -S^-1]) give
+// d lambda / dx (contact-fwddyn.hxx:131-137), row-major nc x L into dfx (LDS, or the Fu
+// block in the spilled plan: a generic pointer).
+// mode: bit 0 impulse, 1 integrated (dt != 0), 2 free-flyer Euler (Jexp6 rows), 3 ok.
+// DT: the address space of dtau (LDS, or the knot's Lxx block in the spilled plan).
+template <class DT>
+__device__ __attribute__((noinline)) void da_fx_mfma(const mb_lds_d* Minv, int lda, const mb_lds_d* H, const DT* dtau,
+                                                     const mb_lds_d* da0, int nj, int nc, int L, int mode, double dt,
+                                                     const mb_lds_d* Sinv, int nfd, double* dfx, const mb_lds_d* Je,
+                                                     const mb_lds_d* Ai, const mb_lds_d* Jc, double* Fx) {
   const int lane = (int)threadIdx.x & 63, wave = (int)threadIdx.x >> 6, nw = (int)blockDim.x >> 6;
   const int li = lane & 15, lk = lane >> 4;
-  const int NR = nj + nfd, tr = (NR + 15) >> 4, tc = (L + 15) >> 4, K = nj + nc;
+  const int NR = nj + nfd, tr = (NR + 15) >> 4, tc = (L + 15) >> 4, K = nj + nc, N = 2 * nj;
+  const bool imp = mode & 1, integ = mode & 2, ffe = mode & 4, ok = mode & 8;
+  const double mul_v = ok ? -1. : (double)NAN, dt2 = dt * dt;
+  const int vcols = imp ? nj : L;  // impulse knots: the v columns of da are zero
+  mb_glb_d* const F = (mb_glb_d*)Fx;
 #pragma unroll 1
   for (int tile = wave; tile < tr * tc; tile += nw) {
     const int ti = tile / tc, tj = tile - ti * tc;
-    const int r = 16 * ti + li, c = 16 * tj + li;
-    const bool rv = r < nj, rf = !rv && r < NR, cvld = c < L;
+    const int i = 16 * ti + li, ca = 16 * tj + li;
+    const bool rv = i < nj, rf = !rv && i < NR, cv = ca < L;
     mb_f64x4 acc = {0., 0., 0., 0.};
 #pragma unroll 1
     for (int kb = 0; kb < K; kb += 4) {
       const int k = kb + lk;
       const bool km = k < nj, kh = !km && k < K;
-      // rows < nj: [Kinv_tl | H]; the force rows nj + k': [H^T | -S^-1] (S symmetric)
-      double a = 0.;
+      // A(c, k) = [dtau; da0](k, c); B(k, i) = [Kinv_tl | H](i, k), the force rows nj + k':
+      // [H^T | -S^-1](k', k) (S symmetric)
+      const double a = (cv && km) ? dtau[k * L + ca] : ((cv && kh) ? da0[(k - nj) * L + ca] : 0.);
+      double bv = 0.;
       if (rv)
-        a = km ? Minv[k * lda + r] : (kh ? H[(k - nj) * nj + r] : 0.);
+        bv = km ? Minv[k * lda + i] : (kh ? H[(k - nj) * nj + i] : 0.);
       else if (rf)
-        a = km ? H[(r - nj) * nj + k] : (kh ? -Sinv[(k - nj) * nc + (r - nj)] : 0.);
-      const double bv = (cvld && km) ? dtau[k * L + c] : ((cvld && kh) ? da0[(k - nj) * L + c] : 0.);
+        bv = km ? H[(i - nj) * nj + k] : (kh ? -Sinv[(k - nj) * nc + (i - nj)] : 0.);
       acc = mb_mfma(a, bv, acc);
     }
-    // (impulse knots: the v columns (>= vcols) are zero; a failed factorisation: NaN)
-    const int jc = 16 * tj + li;
-    const double mul = jc >= vcols ? 0. * mul_v : mul_v;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int i = 16 * ti + lk + 4 * q;
-      if (i < nj && jc < L) da[i * Ld + jc] = acc[q] * mul;
-      if (i >= nj && i < NR && jc < L) dfx[(i - nj) * L + jc] = acc[q];
+      const int c = 16 * tj + lk + 4 * q;
+      // da(i, c) (a failed factorisation: NaN; impulse: 0 in the v columns)
+      const double dav = acc[q] * (c >= vcols ? 0. * mul_v : mul_v);
+      // the free-flyer Euler rows i < 6 mix da(0..5, c): lanes li = 0..5 of this row group
+      double d6[6];
+      if (ffe && ti == 0)
+#pragma unroll
+        for (int r = 0; r < 6; ++r) d6[r] = __shfl(dav, (lane & 48) | r);
+      if (i >= nj && i < NR && c < L) dfx[(i - nj) * L + c] = acc[q];
+      if (i >= nj || c >= L) continue;
+      double fq, fv;  // Fx(i, c), Fx(nj + i, c)
+      if (imp) {  // [[I, 0], [-G dtau_dq - H dv0_dq, G M = I - H Jc]]
+        fq = c == i ? 1. : 0.;
+        if (c < nj) {
+          fv = dav;
+        } else {
+          double s = 0.;
+          for (int k = 0; k < nc; ++k) s += H[k * nj + i] * Jc[k * nj + (c - nj)];
+          fv = ok ? (c - nj == i ? 1. : 0.) - s : (double)NAN;
+        }
+      } else if (!integ) {
+        fq = c == i ? 1. : 0.;
+        fv = c == nj + i ? 1. : 0.;
+      } else {
+        if (ffe && i < 6) {  // Jexp6(dq) (da dt^2 + [0 dt I]) + Ad(exp6(dq)^-1)
+          double s2 = c < 6 ? Ai[c * 6 + i] : 0.;
+#pragma unroll
+          for (int r = 0; r < 6; ++r) s2 += Je[r * 6 + i] * (d6[r] * dt2 + (c == nj + r ? dt : 0.));
+          fq = s2;
+        } else {
+          fq = dav * dt2 + (c == nj + i ? dt : 0.) + (c == i ? 1. : 0.);
+        }
+        fv = dav * dt + (c == nj + i ? 1. : 0.);
+      }
+      F[(int64_t)c * N + i] = fq;
+      F[(int64_t)c * N + nj + i] = fv;
     }
   }
 }
-// da = -(Kinv_tl dtau + H da0) (contact-fwddyn.hxx:127-140 as computeABADerivatives /
-// the KKT inverse): [Kinv_tl | H] (nj x (nj + nc)) times [dtau; da0] ((nj + nc) x L),
-// rows of da at stride Ld; impulse knots keep only the q columns. With the contact-force
-// costs (nfd = nc) the same product's extra rows [H^T | -S^-1] give d lambda / dx
-// (contact-fwddyn.hxx:131-137), row-major nc x L into dfx.
-__device__ __forceinline__ void da_mfma(const double* Minv, int lda, const double* H, const double* dtau,
-                                        const double* da0, int nj, int nc, int L, int Ld, bool imp, bool ok,
-                                        double* da, const double* Sinv, int nfd, double* dfx) {
-  da_mfma_lds((const mb_lds_d*)lds_ptr(Minv), lda, (const mb_lds_d*)lds_ptr(H), (const mb_lds_d*)lds_ptr(dtau),
-              (const mb_lds_d*)lds_ptr(da0), nj, nc, L, Ld, ok ? -1. : (double)NAN, imp ? nj : L,
-              (mb_lds_d*)lds_ptr(da), (const mb_lds_d*)lds_ptr(Sinv), nfd, (mb_lds_d*)lds_ptr(dfx));
-}
-
 // The Gauss-Newton blocks sc * (R^T diag(w h) R + the diagonal state / control terms)
 // (cost-sum.hxx:122-160) over the combined column space [x tangent (L) | u (m)]: the
 // upper-triangle 16 x 16 tiles (bi <= bj) of the (L + m)^2 product; Lxx and Luu are
@@ -3519,10 +3728,12 @@ __device__ __forceinline__ void gn_blocks_mfma(const double* Rm, int ldR, const 
 // Nsub (nj x 42) = T nb with the subtree indicator T[j][b] = 1 when dof j is an ancestor-
 // or-self of b and b carries a body; waves w of nw (the caller's numbering) take the
 // 16 x 16 output tiles round-robin. (The sums' association changes, not their terms.)
+// (AS: the address space of the maps and sums, LDS or the spilled plan's Fx block)
+template <class AS>
 __device__ __forceinline__ void subtree_nh_mfma(const Blk& b, const WVals& W, const double* nb_, double* ns_, int w,
                                                 int nw) {
-  const mb_lds_d* nb = (const mb_lds_d*)lds_ptr(nb_);
-  mb_lds_d* ns = (mb_lds_d*)lds_ptr(ns_);
+  const AS* nb = (const AS*)(std::is_same<AS, mb_lds_d>::value ? lds_ptr(nb_) : nb_);
+  AS* ns = (AS*)(std::is_same<AS, mb_lds_d>::value ? lds_ptr(ns_) : ns_);
   const int lane = (int)threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
   const int nj = b.nj, tr = (nj + 15) >> 4, tc = 3;  // 42 components in 3 tiles
 #pragma unroll 1
@@ -3557,11 +3768,13 @@ __device__ __forceinline__ void subtree_nh_mfma(const Blk& b, const WVals& W, co
 }
 #endif
 
-template <class X>
+// SP: the spilled plan fixed at compile time (0 / 1: the device kernels, one variant per
+// plan) or taken from `spill` (-1: the host emulation)
+template <class X, int SP = -1>
 MB_HD __forceinline__ void knot_calc_diff_x(const X& ex, const double* P, int nx, int m, const double* xg, const double* ug,
                                    bool use_u, double* w, double* Fx, double* Fu, double* Lxx, double* Lxu,
                                    double* Luu, double* Lx, double* Lu, double* xnext_out = nullptr,
-                                   double* cost_out = nullptr, const double* xu_pre = nullptr) {
+                                   double* cost_out = nullptr, const double* xu_pre = nullptr, int spill = 0) {
   w = ex.lds(w);  // the work area and the parameter block live in LDS
   P = ex.lds(P);
   const Blk b = parse(P);
@@ -3572,13 +3785,21 @@ MB_HD __forceinline__ void knot_calc_diff_x(const X& ex, const double* P, int nx
   const int njac = count_jac_costs(b, &vcols);
   const int jw = vcols ? L : nj;  // columns of the stored jac-cost Jacobians
   const int nrows = count_cost_rows(b, nu);
-  const DiffLayout l = diff_layout(nj, njac, nc, vcols, nu, nrows);
-  // the recursions' per-wave partials in the dtau area (free until the tangent directions)
-  const WVals W{w + l.wv, nj, w + l.dtau};
+  // (calc only, Fx == nullptr: the same plan; it ends before any spilled array is used)
+  if (SP == 0) spill = 0;
+  if (SP == 1) spill |= kSpillBlocks;
+  const DiffLayout l = diff_layout(nj, njac, nc, vcols, nu, nrows, spill);
+  const bool spilled = SP >= 0 ? SP == 1 : (spill & kSpillBlocks) != 0;
+  // the recursions' per-wave partials (free areas of their phases: DiffLayout)
+  const WVals W{w + l.wv, nj, w + l.pk};
   double* A = w + l.A;
-  double* dtau = w + l.dtau;
-  double* da = w + l.da;
-  const int Ld = L + 1;  // row stride of da (odd: conflict-free column reads)
+  // dtau/dx, the body maps and their subtree sums: LDS, or (spilled) the knot's Lxx / Fx
+  // blocks, written there after their last read (DiffLayout)
+  double* dtau = spilled ? Lxx : w + l.dtau;
+  double* nbm = spilled ? Fx : w + l.nb;
+  double* nsub = spilled ? Fx + pad2((int64_t)42 * nj) : w + l.ns;
+  double* da = w + l.da;  // (host emulation only)
+  const int Ld = L + 1;   // row stride of da (odd: conflict-free column reads)
   double* qp = w + l.qp;
   double* x = w + l.vec;
   double* u = x + nq + nj;
@@ -3587,7 +3808,7 @@ MB_HD __forceinline__ void knot_calc_diff_x(const X& ex, const double* P, int nx
   double* rf = av + nj;   // jac-cost residuals, 6 per cost
   double* Je = rf + 6 * kMaxJacCosts;  // Jexp6(dq) 6x6
   double* Ai = Je + 36;                // Ad(exp6(dq)^-1) 6x6
-  double* Jf = w + l.J;
+  double* Jf = (spill & kSpillJ) ? Lxu : w + l.J;
   double* red = w + l.red;
   int* flag = (int*)(red + 4);
   double* Jc = w + l.Jc;
@@ -3635,23 +3856,26 @@ MB_HD __forceinline__ void knot_calc_diff_x(const X& ex, const double* P, int nx
   double* pb = red + 8;
   // M^-1 by the tree-sparse LTDL of M (tree_ltdl), into the second half of the A area
   // (column-major nj x nj, ld lda); with contacts: d a / d tau after the Schur step.
-  double* Minv = A + (int64_t)lda * nj;
+  double* Minv = A + l.half;
   // The velocity-product maps of the derivatives (per-body N_b, h_b into the dtau area;
   // their subtree sums into the da area; P_k, Q_k) and the cost-Jacobian columns need the
   // velocities and composite inertias only: on the device the waves the factorisation
   // leaves idle build them meanwhile, one map per slot (vp: how many are built), the
   // Jacobian columns beside the body maps when the idle waves are at least two (jac_side).
-  double* nsub = da;  // (unused by impulse knots)
+  // (unused by impulse knots)
   auto vp_side = [&](int slot, int sl, int snt) {
     if (slot == 0) {
       if (!imp)
-        for (int d = sl; d < nj; d += 64) body_nh_lane(b, W, d, dtau);
+        for (int d = sl; d < nj; d += 64) body_nh_lane(b, W, d, nbm);
       if (snt >= 128)
         for (int id = sl - 64; id >= 0 && id < nj * njac; id += snt - 64)
           jac_lane(b, W, x, id % nj, Jf, jw, rf, nullptr, nullptr, nullptr, id / nj);
     } else if (slot == 1 && !imp) {
 #if defined(__HIP_DEVICE_COMPILE__)
-      subtree_nh_mfma(b, W, dtau, nsub, sl >> 6, snt >> 6);
+      if (spilled)
+        subtree_nh_mfma<mb_glb_d>(b, W, nbm, nsub, sl >> 6, snt >> 6);
+      else
+        subtree_nh_mfma<mb_lds_d>(b, W, nbm, nsub, sl >> 6, snt >> 6);
 #endif
     } else if (slot == 2 && !imp) {
       for (int j = sl; j < nj; j += snt) qp_lane_ns(W, j, nsub, qp);
@@ -3662,16 +3886,17 @@ MB_HD __forceinline__ void knot_calc_diff_x(const X& ex, const double* P, int nx
   // until tree_minv, nj lda >= nj^2 doubles) the fast path's rows ((md + 1) nj) or the
   // generic steps' dof masks (2 nj), which never run together
   const int md = tree_depth(b, W);
-  const int vp = (md < kTreeKD && ex.nt >= 128) ? 3 : 0;
+  // (calc only: no derivative work beside the factorisation)
+  const int vp = (md < kTreeKD && ex.nt >= 128 && Fx) ? 3 : 0;
   const bool jac_side = vp > 0 && ex.nt - 64 >= 128;
   double* const tp = ex.lds(Minv);
   const TreeWork tw{(Mask*)tp, (Mask*)tp + nj, (Mask*)ex.lds(pb), ex.lds(pb) + 64, ex.lds(flag)};
   tree_ltdl(ex, b, W, A, lda, tw, md, tp, vp_side, vp, (int*)(red + 5));
 #else
-  // (host emulation: the scratch in the recursions' per-wave partials, no side work)
+  // (host emulation: the factorisation's scratch in an area of its own, no side work)
   const int vp = 0;
   const bool jac_side = false;
-  double* const tp = ex.lds(W.parts);
+  double* const tp = w + l.ht;
   const TreeWork tw{(Mask*)tp, (Mask*)tp + nj, (Mask*)ex.lds(pb), tp + 2 * nj, ex.lds(flag)};
   tree_ltdl(ex, b, W, A, lda, tw, tree_depth(b, W), tp + 3 * nj);
 #endif
@@ -3759,7 +3984,8 @@ MB_HD __forceinline__ void knot_calc_diff_x(const X& ex, const double* P, int nx
   // velocities, accelerations and forces at the solved a (the linearisation point
   // of computeABADerivatives / computeRNEADerivatives with fext)
   // (impulse: RNEA(q, 0, v+ - v) without gravity, impulse-fwddyn.hxx:102-104)
-  world_rnea(ex, b, W, imp ? u : x + nq, imp ? zv : av, nle, nc > 0 ? fx : nullptr);
+  // (the partials in the first half of A in the spilled plan: M is dead, Y too)
+  world_rnea(ex, b, WVals{W.base, nj, w + l.pr}, imp ? u : x + nq, imp ? zv : av, nle, nc > 0 ? fx : nullptr);
   if (xnext_out || cost_out) {  // the knot's calc, fused (iteration 0 of a solve, or calc only)
     ex.run([&](int lane) {
       const double dt = b.dt;
@@ -3794,25 +4020,27 @@ MB_HD __forceinline__ void knot_calc_diff_x(const X& ex, const double* P, int nx
   const bool ffe = b.ff && integ && !imp;  // Euler on the free-flyer: Jexp6 / Ad(exp6^-1)
   // per-dof Q_k, P_k (lanes < nj) and the jac-cost Jacobians / residuals; the
   // free-flyer Euler step's Jexp6 and Ad(exp6(dq)^-1) (dq = v dt + a dt^2)
-  // per-body velocity-product maps (in the dtau area, free until the dtau phase), then
-  // their subtree sums (in the da area, free until the da phase)
-  // (the maps the Gauss-Jordan's idle waves did not build)
+  // per-body velocity-product maps, then their subtree sums (DiffLayout nb / ns)
+  // (the maps the factorisation's idle waves did not build)
   if (!imp && vp < 1)
     ex.run([&](int lane) {
-      if (lane < nj) body_nh_lane(b, W, lane, dtau);
+      if (lane < nj) body_nh_lane(b, W, lane, nbm);
     });
   if (!imp && vp < 2)
     ex.run([&](int lane) {
       const int w = lane >> 6, j = lane & 63;
 #if defined(__HIP_DEVICE_COMPILE__)
       (void)j;
-      subtree_nh_mfma(b, W, dtau, nsub, w, ex.nt >> 6);
+      if (spilled)
+        subtree_nh_mfma<mb_glb_d>(b, W, nbm, nsub, w, ex.nt >> 6);
+      else
+        subtree_nh_mfma<mb_lds_d>(b, W, nbm, nsub, w, ex.nt >> 6);
 #else
       if (j < nj) {
         if (ex.nt >= 512)
-          subtree_nh_lane<6>(b, W, j, dtau, nsub, w, ex.nt >> 6);
+          subtree_nh_lane<6>(b, W, j, nbm, nsub, w, ex.nt >> 6);
         else
-          subtree_nh_lane<11>(b, W, j, dtau, nsub, w, ex.nt >> 6);
+          subtree_nh_lane<11>(b, W, j, nbm, nsub, w, ex.nt >> 6);
       }
 #endif
     });
@@ -3866,8 +4094,9 @@ MB_HD __forceinline__ void knot_calc_diff_x(const X& ex, const double* P, int nx
   // d lambda / dx, d lambda / du for CostModelContactForce (contact-fwddyn.hxx:131-137, with
   // enable_force): Kinv bottom-left = H^T, bottom-right = -S^-1; dtau/du = [0; I]
   const bool fd = b.enable_force && nc > 0 && !imp;
-  double* dfx = w + l.dfx;
-  double* dfu = w + l.dfu;
+  // (kSpillF: in the knot's Fu block, written last)
+  double* dfx = (spill & kSpillF) ? Fu : w + l.dfx;
+  double* dfu = (spill & kSpillF) ? Fu + pad2((int64_t)nc * L) : w + l.dfu;
   const double sc = integ ? dt : 1.;
   // cost-derivative area (layout: group table 4 kMaxCosts | Arr, Ar mul, Ar val,
   // source per row | R rows)
@@ -3885,10 +4114,25 @@ MB_HD __forceinline__ void knot_calc_diff_x(const X& ex, const double* P, int nx
   // the world-value area, dead since the tangent-direction phase)
   ex.run([&](int lane) {
     const int nl = ex.nt - (b.ncost > 0 ? b.ncost : 1);
-#if defined(__HIP_DEVICE_COMPILE__) && !defined(MB_NO_MFMA_DA)
-    // on the matrix cores, every wave (the whole workgroup is converged here)
-    da_mfma(Minv, lda, H, dtau, da0, nj, nc, L, Ld, imp, ok, da, Sx + (int64_t)nc * nc, fd ? nc : 0, dfx);
+#if defined(__HIP_DEVICE_COMPILE__)
+    // on the matrix cores, every wave (the whole workgroup is converged here), the product's
+    // epilogue writing the Fx block
+    {
+      const int mode = (imp ? 1 : 0) | (integ ? 2 : 0) | (ffe ? 4 : 0) | (ok ? 8 : 0);
+      const mb_lds_d* SiL = (const mb_lds_d*)lds_ptr(Sx + (int64_t)nc * nc);
+      if (spilled)
+        da_fx_mfma<mb_glb_d>((const mb_lds_d*)lds_ptr(Minv), lda, (const mb_lds_d*)lds_ptr(H), (const mb_glb_d*)dtau,
+                             (const mb_lds_d*)lds_ptr(da0), nj, nc, L, mode, dt, SiL, fd ? nc : 0,
+                             dfx, (const mb_lds_d*)lds_ptr(Je), (const mb_lds_d*)lds_ptr(Ai),
+                             (const mb_lds_d*)lds_ptr(Jc), Fx);
+      else
+        da_fx_mfma<mb_lds_d>((const mb_lds_d*)lds_ptr(Minv), lda, (const mb_lds_d*)lds_ptr(H),
+                             (const mb_lds_d*)lds_ptr(dtau), (const mb_lds_d*)lds_ptr(da0), nj, nc, L, mode, dt, SiL,
+                             fd ? nc : 0, dfx, (const mb_lds_d*)lds_ptr(Je),
+                             (const mb_lds_d*)lds_ptr(Ai), (const mb_lds_d*)lds_ptr(Jc), Fx);
+    }
     constexpr bool dfx_done = true;
+    (void)nl;
 #else
     constexpr bool dfx_done = false;
     // two entries per lane at a time: two independent dot-product chains, so the LDS
@@ -3932,7 +4176,7 @@ MB_HD __forceinline__ void knot_calc_diff_x(const X& ex, const double* P, int nx
     // keeps the order (X w) r of the reference's R^T (w r)). Cost k on lane
     // spread_lane(k) after the da tiles (host: lane nt-1-k, which has no da entries), from
     // its group / row / jac-cost offsets, prefix-counted.
-#if defined(__HIP_DEVICE_COMPILE__) && !defined(MB_NO_MFMA_DA)
+#if defined(__HIP_DEVICE_COMPILE__)
     const int kk = spread_item(lane, ex.nt);  // (every lane ran the da tiles)
     if (kk < (b.ncost > 0 ? b.ncost : 1)) {
 #else
@@ -4007,8 +4251,10 @@ MB_HD __forceinline__ void knot_calc_diff_x(const X& ex, const double* P, int nx
   });
   // Output blocks in row pairs over all lanes: consecutive lanes write consecutive
   // 16-B pairs of the column-major blocks (n even, blocks 16-B aligned); the lane's
-  // (column, row pair) advances by nt pairs without a division.
-  ex.run([&](int lane) {
+  // (column, row pair) advances by nt pairs without a division. Columns c0.. of [Fx | Fu],
+  // after the residual rows (DiffLayout kSpillF): the host's last phase writes both; on the
+  // device the da product wrote Fx, and Fu is written at the end of the last phase.
+  auto assemble = [&](int lane, int c0) __attribute__((always_inline)) {
     // the operands re-asserted as LDS here: without it the inference lost them and they
     // were flat loads, each waiting (vmcnt) for the output stores issued before it
     const double* const daL = ex.lds(da);
@@ -4062,7 +4308,7 @@ MB_HD __forceinline__ void knot_calc_diff_x(const X& ex, const double* P, int nx
     // the free-flyer Euler rows (Jexp6 products, 6 terms each) on lanes of their own,
     // so the row pairs below all take the short path (a wave pays for its slowest lane)
     const int r6 = FFE ? 6 : 0;
-    for (int e = lane; e < r6 * (N + M); e += ex.nt) {
+    for (int e = lane + r6 * c0; e < r6 * (N + M); e += ex.nt) {
       const int c = e / 6, i = e - 6 * c;
       if (c < N)
         mb_gstore(FX + (int64_t)c * N + i, fx_at(i, c));
@@ -4070,7 +4316,7 @@ MB_HD __forceinline__ void knot_calc_diff_x(const X& ex, const double* P, int nx
         mb_gstore(FU + (int64_t)(c - N) * N + i, fu_at(i, c - N));
     }
     const int p0 = r6 >> 1, hp = (N >> 1) - p0, dq = ex.nt / hp, dr = ex.nt % hp;
-    for (int c = lane / hp, ip = lane % hp; c < N + M;) {
+    for (int c = c0 + lane / hp, ip = lane % hp; c < N + M;) {
       const int i = 2 * (p0 + ip);
       if (c < N)
         mb_gstore2(FX + (int64_t)c * N + i, fx_at(i, c), fx_at(i + 1, c));
@@ -4080,7 +4326,7 @@ MB_HD __forceinline__ void knot_calc_diff_x(const X& ex, const double* P, int nx
       ip += dr;
       if (ip >= hp) ip -= hp, ++c;
     }
-  });
+  };
   // the stacked residual Jacobians R (nrows x (L + nu), ld ldR): jac-cost rows from
   // their q (or x) columns, force-cost rows from d lambda / dx, du
   const int ngr = (int)cg[4 * kMaxCosts - 1];
@@ -4268,6 +4514,11 @@ MB_HD __forceinline__ void knot_calc_diff_x(const X& ex, const double* P, int nx
       }
       mb_gstore((isu ? Lu : Lx) + j, integ ? sc * acc : acc);
     }
+#if defined(__HIP_DEVICE_COMPILE__)
+    assemble(lane, n);  // Fu
+#else
+    (void)lane;
+#endif
     // the fused calc's cost (cost-sum.hxx:89-117): record k's weighted activation on
     // lane spread_lane(k) (one record per wave first), into the dead pivot buffer
     // (pb[0, 64)); jac-cost residuals from the Jacobian phase.
@@ -4329,16 +4580,20 @@ MB_HD __forceinline__ void knot_calc_diff_x(const X& ex, const double* P, int nx
       }
       *cost_out = integ ? dt * total : total;
     });
+#if !defined(__HIP_DEVICE_COMPILE__)
+  ex.run([&](int lane) { assemble(lane, 0); });  // Fx, Fu (after the residual rows: kSpillF)
+#endif
   (void)nx;
 }
 
-template <int NT>
+template <int NT, int SP>
 __device__ __forceinline__ void knot_calc_diff(const double* P, int nx, int m, const double* xg, const double* ug, bool use_u,
                                       double* w, double* Fx, double* Fu, double* Lxx, double* Lxu, double* Luu,
                                       double* Lx, double* Lu, double* xnext_out, double* cost_out,
-                                      const double* xu_pre = nullptr) {
+                                      const double* xu_pre = nullptr, int spill = 0) {
   static_assert(NT >= 128 && NT % 64 == 0, "the calcDiff phases take >= 2 waves");
-  knot_calc_diff_x(DevExec{NT}, P, nx, m, xg, ug, use_u, w, Fx, Fu, Lxx, Lxu, Luu, Lx, Lu, xnext_out, cost_out, xu_pre);
+  knot_calc_diff_x<DevExec, SP>(DevExec{NT}, P, nx, m, xg, ug, use_u, w, Fx, Fu, Lxx, Lxu, Luu, Lx, Lu, xnext_out,
+                                cost_out, xu_pre, spill);
 }
 
 }  // namespace mb

@@ -2,6 +2,7 @@
 // crocoddyl_amd/csrc/multibody.hpp compiled for the host and run with the
 // sequential-lane executor, so tests/test_multibody_host.py can check the
 // exact device arithmetic against the numpy oracle without a GPU.
+#include <cstdio>
 #include <cstdlib>
 #include <vector>
 
@@ -33,28 +34,69 @@ void mb_host_calc_diff(const double* P, int nx, int m, const double* x, const do
                        double* Fu, double* Lxx, double* Lxu, double* Luu, double* Lx, double* Lu, double* xnext,
                        double* cost) {
   const Blk b = parse(P);
-  std::vector<double> w(diff_layout(b.nj, kMaxJacCosts, b.nc, true, b.nj - b.nun, count_cost_rows(b, b.nj - b.nun)).total, 0.);
+  bool vc = false;
+  const int njac = count_jac_costs(b, &vc);
+  const int nu = b.nj - b.nun, nrows = count_cost_rows(b, nu);
+  // the device's plan for this block (spilled to the output blocks on the large trees);
+  // MB_HOST_SPILL=0 forces the all-LDS plan
+  const char* sp = std::getenv("MB_HOST_SPILL");
+  const int spill = sp && sp[0] == '0' ? 0 : diff_spill(b.nj, njac, b.nc, vc, nu, nrows, (int64_t)P[3], m);
+  std::vector<double> w(diff_layout(b.nj, njac, b.nc, vc, nu, nrows, spill).htotal, 0.);
   // MB_HOST_NT: the workgroup size the lanes emulate (128 / 256 / 512: the device's
   // small-tree, default and 8-wave calcDiff kernels)
   const char* e = std::getenv("MB_HOST_NT");
-  knot_calc_diff_x(HostExec{e ? std::atoi(e) : kMbDiffNT}, P, nx, m, x, u, use_u != 0, w.data(), Fx, Fu, Lxx, Lxu, Luu, Lx, Lu, xnext, cost);
+  knot_calc_diff_x(HostExec{e ? std::atoi(e) : kMbDiffNT}, P, nx, m, x, u, use_u != 0, w.data(), Fx, Fu, Lxx, Lxu, Luu,
+                   Lx, Lu, xnext, cost, nullptr, spill);
 }
 }
 
 extern "C" {
 // The calcDiff LDS plan of a knot block (doubles): the DiffLayout offsets in field
-// order, then total, nj, njac, nc, nrows, vcols.
-int mb_host_layout(const double* P, double* out) {
+// order, then total, nj, njac, nc, nrows, vcols, spill flags, half, block size.
+// (m: nu_max of the plan, diff_spill)
+int mb_host_layout(const double* P, int m, double* out) {
   const Blk b = parse(P);
   bool vc = false;
   const int njac = count_jac_costs(b, &vc);
   const int nu = b.nj - b.nun;
   const int nrows = count_cost_rows(b, nu);
-  const DiffLayout l = diff_layout(b.nj, njac, b.nc, vc, nu, nrows);
+  const int spill = diff_spill(b.nj, njac, b.nc, vc, nu, nrows, (int64_t)P[3], m);
+  const DiffLayout l = diff_layout(b.nj, njac, b.nc, vc, nu, nrows, spill);
   const int64_t f[] = {l.wv, l.A, l.dtau, l.da, l.qp, l.vec, l.J, l.red, l.R, l.Jc, l.a0, l.lam, l.Y, l.H,
-                       l.Sx, l.da0, l.fx, l.zv, l.dfx, l.dfu, l.total, b.nj, njac, b.nc, nrows, vc ? 1 : 0};
+                       l.Sx, l.da0, l.fx, l.zv, l.dfx, l.dfu, l.total, b.nj, njac, b.nc, nrows, vc ? 1 : 0,
+                       spill, l.half, (int64_t)P[3]};
   for (int i = 0; i < (int)(sizeof(f) / sizeof(f[0])); ++i) out[i] = (double)f[i];
   return (int)(sizeof(f) / sizeof(f[0]));
+}
+}
+
+extern "C" {
+// The device's calcDiff plan for a block at nu_max m: the spill flags (diff_spill) and
+// the LDS bytes of the plan with the parameter block.
+int mb_host_plan(const double* P, int m, int64_t* lds_bytes) {
+  const Blk b = parse(P);
+  bool vc = false;
+  const int njac = count_jac_costs(b, &vc);
+  const int nu = b.nj - b.nun, nrows = count_cost_rows(b, nu);
+  const int spill = diff_spill(b.nj, njac, b.nc, vc, nu, nrows, (int64_t)P[3], m);
+  *lds_bytes = 8 * (fddp::pad2(diff_layout(b.nj, njac, b.nc, vc, nu, nrows, spill).total) + fddp::pad2((int64_t)P[3]));
+  return spill;
+}
+}
+
+extern "C" {
+// The static check of a calcDiff plan (multibody.hpp diff_layout_check): 0, or 1 with the
+// conflicting pair's names in msg.
+int mb_host_layout_check(int nj, int njac, int nc, int vcols, int nu, int nrows, int spill, char* msg, int cap) {
+  const DiffLayout l = diff_layout(nj, njac, nc, vcols != 0, nu, nrows, spill);
+  int a = 0, b = 0;
+  if (!diff_layout_check(l, nj, njac, nc, vcols != 0, nu, nrows, &a, &b)) return 0;
+  DiffRegion r[40];
+  diff_layout_regions(l, nj, njac, nc, vcols != 0, nu, nrows, r);
+  std::snprintf(msg, cap, "%s [%lld, +%lld) phases %d-%d / %s [%lld, +%lld) phases %d-%d (total %lld)", r[a].name,
+                (long long)r[a].off, (long long)r[a].size, r[a].first, r[a].last, r[b].name, (long long)r[b].off,
+                (long long)r[b].size, r[b].first, r[b].last, (long long)l.total);
+  return 1;
 }
 }
 

@@ -144,3 +144,39 @@ def test_talos_active_friction_cones(lib, talos_walk, t):  # noqa: F811
         hit += sum(int(np.any(c.a_hess(np.real(r)) > 0)) for c, r in zip(k.costs, res) if c.type == onp.FRICTION_CONE)
         _check_knot(lib, m, x, u, tol=1e-8)
     assert hit > 0
+
+
+@pytest.mark.parametrize("t", [0, 1, 49, 99])
+def test_talos_spilled_plan_equals_lds_plan(lib, talos_walk, t, monkeypatch):  # noqa: F811
+    """The spilled calcDiff plan (multibody.hpp diff_spill: dtau/dx, the body maps and
+    their subtree sums, the jac-cost Jacobians, d lambda / dx in the knot's own output
+    blocks; the Talos
+    knots fit two workgroups per CU under it) computes the all-LDS plan's blocks bit for
+    bit: only where the arrays live changes."""
+    import ctypes as C
+    g, models = talos_walk
+    model = models[t]
+    kind, nu, blk = model.pack()
+    blk = np.ascontiguousarray(blk[0])
+    nx, n, m = model.state.nx, model.state.ndx, max(nu, 1)
+    lib.mb_host_plan.argtypes = [C.POINTER(C.c_double), C.c_int, C.POINTER(C.c_int64)]
+    lds = C.c_int64(0)
+    flags = lib.mb_host_plan(_p(blk), m, C.byref(lds))
+    assert flags & 3 == 3, flags  # blocks and Jacobians spilled (and d lambda / dx with contacts)
+    assert lds.value <= 80 * 1024, lds.value
+    rng = np.random.default_rng(t)
+    x0 = g.rmodel.defaultState
+    x = g.state.integrate(x0, np.concatenate([rng.uniform(-0.05, 0.05, g.state.nv), rng.uniform(-0.3, 0.3, g.state.nv)]))
+    u = model.quasiStatic(None, x0) + rng.uniform(-2, 2, nu)
+    outs = []
+    for spill in (None, "0"):
+        if spill is None:
+            monkeypatch.delenv("MB_HOST_SPILL", raising=False)
+        else:
+            monkeypatch.setenv("MB_HOST_SPILL", spill)
+        o = [np.zeros(s) for s in (n * n, n * m, n * n, n * m, m * m, n, m, nx, 1)]
+        lib.mb_host_calc_diff(_p(blk), nx, m, _p(x), _p(u), 1 if nu else 0, *[_p(a) for a in o])
+        outs.append(o)
+    for a, b in zip(*outs):
+        np.testing.assert_array_equal(a, b)
+

@@ -168,3 +168,27 @@ def test_impulse_device_code_vs_oracle(lib, case):
             got = out[q].reshape(n, n).T if q == "Lxx" else out[q]
             assert float(np.max(np.abs(got - ref[q]))) / max(1.0, float(np.max(np.abs(ref[q])))) < 1e-10, q
         assert not out["Fu"].any() and not out["Lxu"].any() and not out["Luu"].any() and not out["Lu"].any()
+
+
+def test_calc_diff_lds_plans_have_no_live_overlap(lib):
+    """The calcDiff's LDS plans (multibody.hpp diff_layout: the all-LDS plan and the
+    spilled one, whose arrays share areas by live range) checked statically: any two
+    arrays whose LDS areas overlap have disjoint live ranges over the calcDiff's phases
+    (diff_layout_regions / diff_layout_check), and every array lies inside the plan."""
+    msg = C.create_string_buffer(512)
+    lib.mb_host_layout_check.argtypes = [C.c_int] * 7 + [C.c_char_p, C.c_int]
+    n = 0
+    for nj in (3, 6, 7, 12, 18, 21, 24, 30, 38, 48, 64):
+        for nc in (0, 3, 6, 12, 24):
+            for njac in (0, 1, 3, 8):
+                for vcols in (0, 1):
+                    for nu in {nj, max(nj - 6, 1)}:
+                        for nrows in (0, 20, 64):
+                            for spill in (0, 1, 3, 5, 7):
+                                if spill and 84 * nj > 4 * nj * nj:
+                                    continue  # (diff_spill: the maps must fit the Fx block)
+                                rc = lib.mb_host_layout_check(nj, njac, nc, vcols, nu, nrows, spill, msg, 512)
+                                assert rc == 0, (nj, nc, njac, vcols, nu, nrows, spill, msg.value.decode())
+                                n += 1
+    assert n > 5000
+

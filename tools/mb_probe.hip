@@ -11,6 +11,11 @@
 #include <vector>
 // stamps inside the blocked Gauss-Jordan (multibody.hpp gj_mfma), thread 0 of workgroup 0
 __device__ unsigned long long g_gjst[32];
+// phase labels (first stamped launch only): the source location of each phase's lambda,
+// cut from the executor method's __PRETTY_FUNCTION__ ("... (lambda at FILE:LINE:COL) ...")
+constexpr int kLabelLen = 48;
+__device__ char g_labels[256][kLabelLen];
+__device__ int g_label_on;
 #define MB_GJ_MARK(id)                                                            \
   do {                                                                            \
     if (threadIdx.x == 0 && blockIdx.x == 0) g_gjst[id] = __builtin_amdgcn_s_memtime(); \
@@ -47,7 +52,7 @@ struct StampExec {
   __device__ __forceinline__ void run(F f) const {
     [[clang::always_inline]] f((int)threadIdx.x);
     __syncthreads();
-    mark();
+    mark(__PRETTY_FUNCTION__);
   }
   template <class F>
   __device__ __forceinline__ void run_w0(F f) const {
@@ -60,6 +65,7 @@ struct StampExec {
     if (threadIdx.x == 0) {
       unsigned long long i = st[0]++;
       if (i < 254) st[2 + i] = __builtin_amdgcn_s_memtime() | (1ull << 63);
+      label(i, __PRETTY_FUNCTION__);
     }
   }
   __device__ __forceinline__ void sync() const {
@@ -70,11 +76,23 @@ struct StampExec {
   __device__ __forceinline__ T* lds(T* p) const {
     return fddp::lds_ptr(p);
   }
-  __device__ __forceinline__ void mark() const {
+  __device__ __forceinline__ void mark(const char* who = "sync / solver") const {
     if (threadIdx.x == 0) {
       unsigned long long i = st[0]++;
       if (i < 254) st[2 + i] = __builtin_amdgcn_s_memtime();
+      label(i, who);
     }
+  }
+  // (after the stamp: the copy is not timed in the phase it names)
+  __device__ __forceinline__ void label(unsigned long long i, const char* who) const {
+    if (!g_label_on || blockIdx.x != 0 || i >= 254) return;
+    const char* s = who;
+    for (const char* q = who; *q; ++q)
+      if (q[0] == 'a' && q[1] == 't' && q[2] == ' ' && q > who && q[-1] == ' ') s = q + 3;
+    int k = 0;
+    for (const char* q = s; *q && k < kLabelLen - 1; ++q)  // keep "file:line" past the last '/'
+      if (*q == '/') k = 0; else if (*q == ')') break; else g_labels[i][k++] = *q;
+    g_labels[i][k] = 0;
   }
 };
 
@@ -100,16 +118,18 @@ __device__ inline bool mb_invert(const StampExec& ex, double* A, int nr, int ld,
   return ok;
 }
 
+// (2 waves / EU as the library's mb_knot_kernel / _s2: two 256-thread workgroups per CU
+// when the LDS plan allows it)
 template <int NT>
-__global__ __launch_bounds__(NT) void probe_diff(const double* Pg, int nx, int m, const double* xg,
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2))) void probe_diff(const double* Pg, int nx, int m, const double* xg,
                                                         const double* ug, int use_u, double* out, int64_t so,
-                                                        unsigned long long* stamps, int mode) {
+                                                        unsigned long long* stamps, int mode, int spill) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
   const int psz = (int)Pg[3];
   const Blk bk = parse(Pg);
   bool vc;
   const int njac = count_jac_costs(bk, &vc);
-  const DiffLayout l = diff_layout(bk.nj, njac, bk.nc, vc, bk.nj - bk.nun, count_cost_rows(bk, bk.nj - bk.nun));
+  const DiffLayout l = diff_layout(bk.nj, njac, bk.nc, vc, bk.nj - bk.nun, count_cost_rows(bk, bk.nj - bk.nun), spill);
   double* P = sm + pad2(l.total);
   unsigned long long* st = (unsigned long long*)(P + pad2(psz));
   for (int e = threadIdx.x; e < psz; e += NT) P[e] = Pg[e];
@@ -126,7 +146,8 @@ __global__ __launch_bounds__(NT) void probe_diff(const double* Pg, int nx, int m
   if (mode == 0)
     knot_calc_diff_x(ex, P, nx, m, xg, ug, use_u != 0, sm, o, o + n * n, o + n * n + n * m, o + 2 * n * n + n * m,
                      o + 2 * n * n + 2 * n * m, o + 2 * n * n + 2 * n * m + m * m, o + 2 * n * n + 2 * n * m + m * m + n,
-                     o + 2 * n * n + 2 * n * m + m * m + n + m, o + 2 * n * n + 2 * n * m + m * m + n + m + nx);
+                     o + 2 * n * n + 2 * n * m + m * m + n + m, o + 2 * n * n + 2 * n * m + m * m + n + m + nx,
+                     nullptr, spill);
   else  // without the fused calc's outputs (next state, cost)
     knot_calc_diff_x(ex, P, nx, m, xg, ug, use_u != 0, sm, o, o + n * n, o + n * n + n * m, o + 2 * n * n + n * m,
                      o + 2 * n * n + 2 * n * m, o + 2 * n * n + 2 * n * m + m * m, o + 2 * n * n + 2 * n * m + m * m + n,
@@ -191,13 +212,18 @@ int main(int argc, char** argv) {
   const Blk bk = parse(P.data());
   bool vc;
   const int njac = count_jac_costs(bk, &vc);
-  const DiffLayout l = diff_layout(nj, njac, bk.nc, vc, bk.nj - bk.nun, count_cost_rows(bk, bk.nj - bk.nun));
+  // the library's plan (spilled on the large trees; PROBE_SPILL=0 forces the all-LDS plan)
+  const int spill = getenv("PROBE_SPILL") && getenv("PROBE_SPILL")[0] == '0'
+                        ? 0
+                        : diff_spill(nj, njac, bk.nc, vc, bk.nj - bk.nun, count_cost_rows(bk, bk.nj - bk.nun), psz, m);
+  const DiffLayout l = diff_layout(nj, njac, bk.nc, vc, bk.nj - bk.nun, count_cost_rows(bk, bk.nj - bk.nun), spill);
   const size_t smd = 8 * (pad2(l.total) + pad2(psz) + 256);
   const size_t smc = 8 * (pad2(calc_work_doubles(nj, bk.nc)) + pad2(psz) + 256);
   printf("nj %d nx %d nu %d m %d psz %d lds diff %zu calc %zu\n", nj, nx, nu, m, psz, smd, smc);
-  printf("  layout: wv %ld A %ld dtau %ld da %ld qp %ld vec %ld J %ld red %ld Jc %ld R %ld total %ld (njac %d vcols %d nc %d nrows %d)\n",
-         (long)l.wv, (long)l.A, (long)l.dtau, (long)l.da, (long)l.qp, (long)l.vec, (long)l.J, (long)l.red, (long)l.Jc,
-         (long)l.R, (long)l.total, njac, (int)vc, bk.nc, count_cost_rows(bk, bk.nj - bk.nun));
+  printf("  layout (spill %d): wv %ld A %ld half %ld dtau %ld da %ld qp %ld vec %ld J %ld red %ld Jc %ld Y %ld da0 %ld R %ld total %ld (njac %d vcols %d nc %d nrows %d)\n",
+         spill, (long)l.wv, (long)l.A, (long)l.half, (long)l.dtau, (long)l.da, (long)l.qp, (long)l.vec, (long)l.J,
+         (long)l.red, (long)l.Jc, (long)l.Y, (long)l.da0, (long)l.R, (long)l.total, njac, (int)vc, bk.nc,
+         count_cost_rows(bk, bk.nj - bk.nun));
   fflush(stdout);
   if (argc > 3 && std::string(argv[3]) != "dump") return 0;  // layout only
   const bool dump = argc > 3;
@@ -219,8 +245,13 @@ int main(int argc, char** argv) {
   CK(hipFuncSetAttribute((const void*)probe_diff<512>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smd));
   CK(hipFuncSetAttribute((const void*)probe_calc, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smc));
   std::vector<unsigned long long> st(256);
+  std::vector<char> labels(256 * kLabelLen, 0);
   for (int which = 0; which < 2; ++which) {
-    for (int rep = 0; rep < 3; ++rep) {
+    for (int rep = 0; rep < 4; ++rep) {
+      {  // the last launch records the phase labels (its times are not reported)
+        const int on = rep == 3;
+        CK(hipMemcpyToSymbol(HIP_SYMBOL(g_label_on), &on, sizeof(int)));
+      }
       hipEvent_t e0, e1;
       CK(hipEventCreate(&e0));
       CK(hipEventCreate(&e1));
@@ -228,13 +259,13 @@ int main(int argc, char** argv) {
       if (which == 0) {
         if (pnt == 128)
           hipLaunchKernelGGL(probe_diff<128>, dim3(nwg), dim3(128), smd, 0, dP, nx, m, dx, du, nu > 0 ? 1 : 0, dout, so,
-                             dst, getenv("PROBE_DIFF_NOCOST") ? 1 : 0);
+                             dst, getenv("PROBE_DIFF_NOCOST") ? 1 : 0, spill);
         else if (pnt == 512)
           hipLaunchKernelGGL(probe_diff<512>, dim3(nwg), dim3(512), smd, 0, dP, nx, m, dx, du, nu > 0 ? 1 : 0, dout, so,
-                             dst, getenv("PROBE_DIFF_NOCOST") ? 1 : 0);
+                             dst, getenv("PROBE_DIFF_NOCOST") ? 1 : 0, spill);
         else
           hipLaunchKernelGGL(probe_diff<256>, dim3(nwg), dim3(256), smd, 0, dP, nx, m, dx, du, nu > 0 ? 1 : 0, dout, so,
-                             dst, getenv("PROBE_DIFF_NOCOST") ? 1 : 0);
+                             dst, getenv("PROBE_DIFF_NOCOST") ? 1 : 0, spill);
       } else {
         hipLaunchKernelGGL(probe_calc, dim3(nwg), dim3(256), smc, 0, dP, nx, dx, du, nu > 0 ? 1 : 0, dout, dst);
       }
@@ -243,7 +274,7 @@ int main(int argc, char** argv) {
       float ms;
       CK(hipEventElapsedTime(&ms, e0, e1));
       CK(hipMemcpy(st.data(), dst, 8 * 256, hipMemcpyDeviceToHost));
-      printf("%s nwg %d: %.3f ms (%.2f us per WG-knot at 256 CUs)\n", which == 0 ? "calcDiff" : "calc", nwg, ms,
+      if (rep < 3) printf("%s nwg %d: %.3f ms (%.2f us per WG-knot at 256 CUs)\n", which == 0 ? "calcDiff" : "calc", nwg, ms,
              1e3 * ms / (nwg / 256.0 > 1 ? nwg / 256.0 : 1));
       if (dump && which == 0 && rep == 0) {  // the LDS matrices and the output blocks
         std::vector<double> dm((size_t)kDumpSlots * kDumpCap);
@@ -260,6 +291,12 @@ int main(int argc, char** argv) {
         fwrite(ob.data(), 8, ob.size(), g);
         fclose(g);
         printf("dumped %s\n", path.c_str());
+      }
+      if (rep == 3) {
+        CK(hipMemcpyFromSymbol(labels.data(), HIP_SYMBOL(g_labels), labels.size()));
+        printf("  phase labels:");
+        for (unsigned long long i = 0; i < st[0] && i < 254; ++i) printf(" [%llu %s]", i, &labels[i * kLabelLen]);
+        printf("\n");
       }
       if (rep == 2) {
         unsigned long long prev = st[1];

@@ -110,9 +110,18 @@ def main():
             c["mfma_f64_flops"] = c["SQ_INSTS_VALU_MFMA_F64"] * 16 * 16 * 4 * 2  # v_mfma_f64_16x16x4
             d["counters"] = c
         out[key] = d
+    # the library build the counters belong to: the lib_sha256 of the profiled bench runs'
+    # own JSON lines (bench.py uses the entry only when its running library has that hash)
+    hashes = set()
+    for log in glob.glob(os.path.join(src, "*.json")) + glob.glob(os.path.join(src, "pmc_*.log")):
+        for line in open(log, errors="replace"):
+            if line.startswith("{") and '"lib_sha256"' in line:
+                hashes.add(json.loads(line)["lib_sha256"])
+    if len(hashes) != 1:
+        raise SystemExit(f"prof_summary: expected one library hash over the profiled runs, found {sorted(hashes)}")
     path = os.path.join(prof, "pmc_backward.json")
     data = json.load(open(path)) if os.path.exists(path) else {}
-    data[cfg] = dict(out.get("backward", {}), kernels=out, tag=tag, steps=steps,
+    data[cfg] = dict(out.get("backward", {}), kernels=out, tag=tag, steps=steps, lib_sha256=hashes.pop(),
                      note="dispatches of the last `steps` solves only (the timed steps); FETCH_SIZE x2 (gfx950 "
                           "streaming-read correction) + WRITE_SIZE, KiB -> bytes; per launch = mean per dispatch, "
                           "per step = sum over the step's dispatches")
