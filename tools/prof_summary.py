@@ -107,6 +107,9 @@ def main():
                 c[n] = s[0] if s else 0.0
             clk = c["GRBM_GUI_ACTIVE"] / 8.0  # per-XCD GPU cycles of the dispatch
             c["mfma_busy_frac"] = c["SQ_VALU_MFMA_BUSY_CYCLES"] / max(clk * 256 * 4, 1.0)  # per SIMD
+            # mean resident waves per CU over the dispatch (SQ_WAVE_CYCLES counts quad-cycles,
+            # MI355X_MICROARCH.md; the per-XCD clock as above)
+            c["resident_waves_per_cu"] = 4.0 * c["SQ_WAVE_CYCLES"] / max(clk * 256, 1.0)
             c["mfma_f64_flops"] = c["SQ_INSTS_VALU_MFMA_F64"] * 16 * 16 * 4 * 2  # v_mfma_f64_16x16x4
             d["counters"] = c
         out[key] = d
