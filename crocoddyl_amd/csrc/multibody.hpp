@@ -2943,6 +2943,9 @@ struct DiffLayout {
   // the per-wave partials of the recursions (kinematics / the RNEA at the solved a), the
   // per-body velocity-product maps and their subtree sums; half: doubles per half of A
   int64_t pk, pr, nb, ns, half;
+  // the cost table's diagonal terms and residual rows (after the table, or apart from it),
+  // and the LDS copy of dtau the da product reads (the spilled plan: over the world values)
+  int64_t Rr, dts;
   int spill;       // kSpill* flags the plan was made with
   int64_t ht;      // host emulation: its factorisation scratch (70 nj)
   int64_t htotal;  // host emulation: total plus its own areas (da, the factorisation scratch)
@@ -3016,6 +3019,8 @@ __host__ __device__ inline DiffLayout diff_layout(int nj, int njac, int nc = 0, 
       l.R = pad2(l.total);
       l.total = l.R + ca;
     }
+    l.Rr = l.R + cost_table_doubles();
+    l.dts = l.dtau;
     l.ht = pad2(l.total);  // host: the factorisation scratch
     l.htotal = l.ht + pad2((int64_t)70 * nj);
     return l;
@@ -3065,15 +3070,26 @@ __host__ __device__ inline DiffLayout diff_layout(int nj, int njac, int nc = 0, 
     if (nc > 0 && l.dfx == l.total) l.total = pad2(l.total + dfs);
     l.dfu = l.dfx + pad2((int64_t)nc * L);
   }
-  // the cost area over the world values and the first half of A (contiguous; dead from the
-  // da phase on, the table written during it within the world values; not over the half
-  // when d lambda / dx, du sit there: the residual rows read them)
+  // The cost area: where the world values are dead (from the da phase on). With room in
+  // the first half of A after da0 (and d lambda / dx, du not there) the table (written
+  // during the da phase) goes there, and the da phase reads dtau from an LDS copy over the
+  // world values (dts: its loads then never wait behind the Fx stores, as global loads
+  // do); the diagonal terms and the rows (from the next phase on) over the world values.
+  // Else the whole area over the world values and the first half, when it fits.
   const bool f_in_half = nc > 0 && l.dfx >= l.A && l.dfx < l.A + l.half;
-  if (cost_table_doubles() + kMaxCostCols <= wvs && ca <= wvs + (f_in_half ? 0 : l.half)) {
+  const int64_t tab0 = (nc > 0 ? d0 : 0), rsz = ca - cost_table_doubles();
+  l.dts = -1;
+  if (!f_in_half && tab0 + cost_table_doubles() <= l.half && (int64_t)nj * L <= wvs && rsz <= wvs) {
+    l.R = l.A + tab0;
+    l.Rr = l.wv;
+    l.dts = l.wv;
+  } else if (cost_table_doubles() + kMaxCostCols <= wvs && ca <= wvs + (f_in_half ? 0 : l.half)) {
     l.R = l.wv;
+    l.Rr = l.R + cost_table_doubles();
   } else {
     l.R = pad2(l.total);
     l.total = l.R + ca;
+    l.Rr = l.R + cost_table_doubles();
   }
   // host emulation: the da area and the factorisation's scratch of its own
   l.da = pad2(l.total);
@@ -3152,8 +3168,8 @@ MB_HD inline int diff_layout_regions(const DiffLayout& l, int nj, int njac, int 
     }
   }
   add("cost table", l.R, cost_table_doubles(), DP_DA, DP_END);
-  add("cost diagonal / rows", l.R + cost_table_doubles(), cost_area_doubles(nj, nu, nrows) - cost_table_doubles(),
-      DP_RROWS, DP_END);
+  add("cost diagonal / rows", l.Rr, cost_area_doubles(nj, nu, nrows) - cost_table_doubles(), DP_RROWS, DP_END);
+  if (sp && l.dts >= 0) add("dtau (LDS copy)", l.dts, (int64_t)nj * L, DP_DA, DP_DA);
   return k;
 }
 // 0 when no two regions of the plan overlap in both LDS and live range (and all lie in
@@ -3594,12 +3610,16 @@ typedef __attribute__((address_space(1))) double mb_glb_d;
 // d lambda / dx (contact-fwddyn.hxx:131-137), row-major nc x L into dfx (LDS, or the Fu
 // block in the spilled plan: a generic pointer).
 // mode: bit 0 impulse, 1 integrated (dt != 0), 2 free-flyer Euler (Jexp6 rows), 3 ok.
-// DT: the address space of dtau (LDS, or the knot's Lxx block in the spilled plan).
-template <class DT>
-__device__ __attribute__((noinline)) void da_fx_mfma(const mb_lds_d* Minv, int lda, const mb_lds_d* H, const DT* dtau,
-                                                     const mb_lds_d* da0, int nj, int nc, int L, int mode, double dt,
-                                                     const mb_lds_d* Sinv, int nfd, double* dfx, const mb_lds_d* Je,
-                                                     const mb_lds_d* Ai, const mb_lds_d* Jc, double* Fx) {
+// dtau: read from LDS at dts; in the spilled plan dtg is its global copy (the knot's Lxx
+// block) and each wave first copies the direction blocks of its tiles into dts (so the
+// tiles' loads are LDS loads, which never wait behind the Fx stores); dtg == nullptr:
+// dtau is in LDS already. dts == nullptr: the product reads dtg (global) directly.
+template <bool GA>  // GA: the A operand read from global memory (dtg) instead of the LDS copy
+__device__ __attribute__((noinline)) void da_fx_mfma(const mb_lds_d* Minv, int lda, const mb_lds_d* H,
+                                                     const double* dtg, mb_lds_d* dts, const mb_lds_d* da0, int nj,
+                                                     int nc, int L, int mode, double dt, const mb_lds_d* Sinv, int nfd,
+                                                     double* dfx, const mb_lds_d* Je, const mb_lds_d* Ai,
+                                                     const mb_lds_d* Jc, double* Fx, const mb_lds_d* Z) {
   const int lane = (int)threadIdx.x & 63, wave = (int)threadIdx.x >> 6, nw = (int)blockDim.x >> 6;
   const int li = lane & 15, lk = lane >> 4;
   const int NR = nj + nfd, tr = (NR + 15) >> 4, tc = (L + 15) >> 4, K = nj + nc, N = 2 * nj;
@@ -3607,25 +3627,119 @@ __device__ __attribute__((noinline)) void da_fx_mfma(const mb_lds_d* Minv, int l
   const double mul_v = ok ? -1. : (double)NAN, dt2 = dt * dt;
   const int vcols = imp ? nj : L;  // impulse knots: the v columns of da are zero
   mb_glb_d* const F = (mb_glb_d*)Fx;
+  const mb_glb_d* const G = (const mb_glb_d*)dtg;
+  // tiles direction-block major, a contiguous range per wave: its tiles share their A
+  // operands (at most two direction blocks)
+  MB_GJ_MARK(22);
+  const int per = (tr * tc + nw - 1) / nw, t0 = wave * per;
+  const int t1 = (wave + 1) * per < tr * tc ? (wave + 1) * per : tr * tc;
+  if (!GA && G && t0 < t1) {  // this wave's direction blocks of dtau into LDS (loads first)
+    const int j0 = t0 / tr, j1 = (t1 - 1) / tr;
+    for (int tj = j0; tj <= j1; ++tj) {
+      const int c = 16 * tj + li;
+      // (nj <= 40: the copy's area, 2 nj^2 doubles, fits the world values' only then)
+      double v[10];
+#pragma unroll
+      for (int s = 0; s < 10; ++s) {
+        const int k = 4 * s + lk;
+        v[s] = (k < nj && c < L) ? (double)G[k * L + c] : 0.;
+      }
+#pragma unroll
+      for (int s = 0; s < 10; ++s) {
+        const int k = 4 * s + lk;
+        if (k < nj && c < L) dts[k * L + c] = v[s];
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  MB_GJ_MARK(25);
 #pragma unroll 1
-  for (int tile = wave; tile < tr * tc; tile += nw) {
-    const int ti = tile / tc, tj = tile - ti * tc;
+  for (int tile = t0; tile < t1; ++tile) {
+    const int tj = tile / tr, ti = tile - tj * tr;
     const int i = 16 * ti + li, ca = 16 * tj + li;
     const bool rv = i < nj, rf = !rv && i < NR, cv = ca < L;
     mb_f64x4 acc = {0., 0., 0., 0.};
+    // operands from clamped addresses, every load unconditional, then selected (a load
+    // under a lane-dependent condition becomes a branch that waits for it: one LDS round
+    // trip per k-step); the k-steps in chunks of 8, the chunk's loads first
+    const int cac = ca < L ? ca : L - 1;
+    const int ic = i < nj ? i : nj - 1, ir = i - nj < 0 ? 0 : (i - nj < nfd ? i - nj : (nfd > 0 ? nfd - 1 : 0));
+    if constexpr (!GA) {
+      // two k-ranges, each with one operand source per lane and a per-lane stride (no
+      // per-step address selects, which became branches): k < nj (A = dtau, B = Kinv_tl
+      // rows / H^T columns), then k' = k - nj < nc (A = da0, B = H rows / -S^-1); the
+      // padding k-steps masked; loads of 4 k-steps first, then their MFMAs
+      const mb_lds_d* pa = dts + (lk * L + cac);
+      const mb_lds_d* pb = rv ? Minv + (lk * lda + ic) : (rf ? H + (ir * nj + lk) : Z);
+      const int sb = rv ? 4 * lda : (rf ? 4 : 0);
 #pragma unroll 1
-    for (int kb = 0; kb < K; kb += 4) {
-      const int k = kb + lk;
-      const bool km = k < nj, kh = !km && k < K;
-      // A(c, k) = [dtau; da0](k, c); B(k, i) = [Kinv_tl | H](i, k), the force rows nj + k':
-      // [H^T | -S^-1](k', k) (S symmetric)
-      const double a = (cv && km) ? dtau[k * L + ca] : ((cv && kh) ? da0[(k - nj) * L + ca] : 0.);
-      double bv = 0.;
-      if (rv)
-        bv = km ? Minv[k * lda + i] : (kh ? H[(k - nj) * nj + i] : 0.);
-      else if (rf)
-        bv = km ? H[(i - nj) * nj + k] : (kh ? -Sinv[(k - nj) * nc + (i - nj)] : 0.);
-      acc = mb_mfma(a, bv, acc);
+      for (int k0 = 0; k0 < nj; k0 += 16) {
+        double av[4], bw[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          av[s] = pa[(k0 + 4 * s) * L];
+          bw[s] = pb[(k0 / 4 + s) * sb];
+        }
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int k = k0 + 4 * s + lk;
+          if (k0 + 4 * s < nj) acc = mb_mfma(cv && k < nj ? av[s] : 0., rv || rf ? bw[s] : 0., acc);
+        }
+      }
+      const mb_lds_d* qa = da0 + (lk * L + cac);
+      const mb_lds_d* qb = rv ? H + (lk * nj + ic) : (rf ? Sinv + (lk * nc + ir) : Z);
+      const int sq = rv ? 4 * nj : (rf ? 4 * nc : 0);
+      const double sg = rf ? -1. : 1.;
+#pragma unroll 1
+      for (int k0 = 0; k0 < nc; k0 += 16) {
+        double av[4], bw[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          av[s] = qa[(k0 + 4 * s) * L];
+          bw[s] = qb[(k0 / 4 + s) * sq];
+        }
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int k = k0 + 4 * s + lk;
+          if (k0 + 4 * s < nc) acc = mb_mfma(cv && k < nc ? av[s] : 0., rv || rf ? sg * bw[s] : 0., acc);
+        }
+      }
+    } else {
+    // (chunks of 4 k-steps: the chunk's 24 loads issued, pinned by one empty asm that
+    // consumes them all, then selected: sunk into the selects' conditions the loads became
+    // branches that each wait for their load)
+#pragma unroll 1
+    for (int k0 = 0; k0 < K; k0 += 16) {
+      double x1[4], x2[4], m1[4], h1[4], h2[4], s2[4];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int k = k0 + 4 * s + lk;
+        const int kc = k < nj ? k : nj - 1, kn = k - nj < 0 ? 0 : (k - nj < nc ? k - nj : (nc > 0 ? nc - 1 : 0));
+        // A(c, k) = [dtau; da0](k, c)
+        x1[s] = GA ? (double)G[kc * L + cac] : (double)dts[kc * L + cac];
+        x2[s] = da0[kn * L + cac];
+        // B(k, i) = [Kinv_tl | H](i, k), the force rows nj + k': [H^T | -S^-1](k', k) (S symmetric)
+        m1[s] = Minv[kc * lda + ic];
+        h1[s] = H[kn * nj + ic];
+        h2[s] = H[ir * nj + kc];
+        s2[s] = Sinv[kn * nc + ir];
+      }
+      asm volatile(""
+                   : "+v"(x1[0]), "+v"(x1[1]), "+v"(x1[2]), "+v"(x1[3]), "+v"(x2[0]), "+v"(x2[1]), "+v"(x2[2]),
+                     "+v"(x2[3]), "+v"(m1[0]), "+v"(m1[1]), "+v"(m1[2]), "+v"(m1[3]), "+v"(h1[0]), "+v"(h1[1]),
+                     "+v"(h1[2]), "+v"(h1[3]), "+v"(h2[0]), "+v"(h2[1]), "+v"(h2[2]), "+v"(h2[3]), "+v"(s2[0]),
+                     "+v"(s2[1]), "+v"(s2[2]), "+v"(s2[3]));
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int k = k0 + 4 * s + lk;
+        const bool km = k < nj, kh = !km && k < K;
+        const double av = !cv ? 0. : (km ? x1[s] : (kh ? x2[s] : 0.));
+        const double bw = rv ? (km ? m1[s] : (kh ? h1[s] : 0.)) : (rf ? (km ? h2[s] : (kh ? -s2[s] : 0.)) : 0.);
+        if (k0 + 4 * s < K) acc = mb_mfma(av, bw, acc);
+      }
+    }
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -3667,6 +3781,7 @@ __device__ __attribute__((noinline)) void da_fx_mfma(const mb_lds_d* Minv, int l
       F[(int64_t)c * N + nj + i] = fv;
     }
   }
+  MB_GJ_MARK(23);
 }
 // The Gauss-Newton blocks sc * (R^T diag(w h) R + the diagonal state / control terms)
 // (cost-sum.hxx:122-160) over the combined column space [x tangent (L) | u (m)]: the
@@ -3691,19 +3806,21 @@ __device__ __forceinline__ void gn_blocks_mfma(const double* Rm, int ldR, const 
     }
     const int bj = bi + rem;
     const int ca = 16 * bi + li, cb = 16 * bj + li;
+    // (clamped addresses, unconditional loads, then selects: a lane-dependent condition
+    // around a load becomes a branch that waits for it)
+    const int cac = ca < ldR ? ca : ldR - 1, cbc = cb < ldR ? cb : ldR - 1;
     mb_f64x4 acc = {0., 0., 0., 0.};
-#pragma unroll 2
+#pragma unroll 4
     for (int kb = 0; kb < nrows; kb += 4) {
-      const int r = kb + lk;
-      double a = 0., bv = 0.;
-      if (r < nrows) {
-        const double* Rr = Rm + (int64_t)r * ldR;
-        // (the tile's transpose: the accumulator rows run over bj, its columns over bi,
-        // so lane li holds row 16 bi + li and the 16 lanes of a column store 128
-        // contiguous bytes of the column-major blocks)
-        a = cb < cv ? Rr[cb] : 0.;
-        bv = ca < cv ? Rr[ca] * wrow[r] : 0.;
-      }
+      const int r = kb + lk, rc = r < nrows ? r : nrows - 1;
+      const double* Rr = Rm + (int64_t)rc * ldR;
+      // (the tile's transpose: the accumulator rows run over bj, its columns over bi,
+      // so lane li holds row 16 bi + li and the 16 lanes of a column store 128
+      // contiguous bytes of the column-major blocks)
+      double x = Rr[cbc], y = Rr[cac], wr = wrow[rc];
+      asm volatile("" : "+v"(x), "+v"(y), "+v"(wr));  // (loads pinned: not sunk into branches)
+      const double a = (r < nrows && cb < cv) ? x : 0.;
+      const double bv = (r < nrows && ca < cv) ? y * wr : 0.;
       acc = mb_mfma(a, bv, acc);
     }
 #pragma unroll
@@ -3824,6 +3941,7 @@ MB_HD __forceinline__ void knot_calc_diff_x(const X& ex, const double* P, int nx
     // xu_pre (device, nq + nj <= nt): this thread's x[lane] / u[lane] loaded by the caller
     // beside the parameter-block copy (one global round trip instead of two)
     if (lane == 0) *(int*)(red + 5) = 0;  // the factorisation's side-work counter
+    if (lane == 1) red[7] = 0.;           // an LDS zero (the da product's padding operand)
     if (xu_pre) {
       if (lane < nq + nj) x[lane] = xu_pre[0];
       if (lane < nj) u[lane] = (use_u && lane < nu) ? xu_pre[1] : 0.;
@@ -4068,10 +4186,11 @@ MB_HD __forceinline__ void knot_calc_diff_x(const X& ex, const double* P, int nx
       for (int e = 0; e < 6; ++e) qp[12 * lane + 6 + e] = 0.;
     });
   }
-  // tangent directions: dtau/dx (impulse: q only) and da0/dx
-  // (dtau on the lower half of the workgroup, da0 on the upper half, side by side)
+  // tangent directions: dtau/dx (impulse: q only) and da0/dx side by side: one lane per
+  // da0 direction (at most half the workgroup), the rest for dtau
   ex.run([&](int lane) {
-    const int h = ex.nt / 2;
+    const int hc = (nc > 0 && !imp) ? (L < ex.nt / 2 ? L : ex.nt / 2) : 0;
+    const int h = ex.nt - hc;
     if (lane < h) {
       // (direction, row part) per lane: a direction's rows split over up to 3 lanes when
       // the half-workgroup has the lanes for it
@@ -4079,8 +4198,8 @@ MB_HD __forceinline__ void knot_calc_diff_x(const X& ex, const double* P, int nx
       const int np = h >= 3 * nd ? 3 : (h >= 2 * nd ? 2 : 1);
       for (int id = lane; id < nd * np; id += h)
         dtau_direction(b, W, qp, id % nd, L, dtau, imp ? nullptr : nsub, id / nd, np);
-    } else if (nc > 0 && !imp) {
-      for (int dd = lane - h; dd < L; dd += h) contact_direction(b, W, dd, L, da0);
+    } else {
+      for (int dd = lane - h; dd < L; dd += hc) contact_direction(b, W, dd, L, da0);
     }
   });
   if (imp && nc > 0) {  // velocities at v+, then d(Jc v+)/dq
@@ -4106,7 +4225,7 @@ MB_HD __forceinline__ void knot_calc_diff_x(const X& ex, const double* P, int nx
   double* cav = cam + kMaxCostRows;
   double* csrc = cav + kMaxCostRows;
   double* cgi = csrc + kMaxCostRows;  // group of each row
-  double* cdg = cgi + kMaxCostRows;   // device: the state / control diagonal terms per column
+  double* cdg = w + l.Rr;             // device: the state / control diagonal terms per column
   double* Rm = cdg + kMaxCostCols;
   const int ldR = cost_rows_ld(nj, nu);
   // da = -Kinv_tl dtau - H da0 (impulse: -G dtau_dq - H dv0_dq on the q columns) on all
@@ -4120,16 +4239,23 @@ MB_HD __forceinline__ void knot_calc_diff_x(const X& ex, const double* P, int nx
     {
       const int mode = (imp ? 1 : 0) | (integ ? 2 : 0) | (ffe ? 4 : 0) | (ok ? 8 : 0);
       const mb_lds_d* SiL = (const mb_lds_d*)lds_ptr(Sx + (int64_t)nc * nc);
-      if (spilled)
-        da_fx_mfma<mb_glb_d>((const mb_lds_d*)lds_ptr(Minv), lda, (const mb_lds_d*)lds_ptr(H), (const mb_glb_d*)dtau,
-                             (const mb_lds_d*)lds_ptr(da0), nj, nc, L, mode, dt, SiL, fd ? nc : 0,
-                             dfx, (const mb_lds_d*)lds_ptr(Je), (const mb_lds_d*)lds_ptr(Ai),
-                             (const mb_lds_d*)lds_ptr(Jc), Fx);
+      // dtau: LDS (all-LDS plan), or the Lxx block copied into the LDS staging area / read
+      // in place (spilled plan without room for the copy)
+      // (an explicit flag: the copy's area may sit at LDS address 0)
+      const double* dtg = spilled ? dtau : nullptr;
+      const bool staged = !spilled || l.dts >= 0;
+      mb_lds_d* dts = !spilled ? (mb_lds_d*)lds_ptr(dtau) : (mb_lds_d*)lds_ptr(w + (l.dts >= 0 ? l.dts : 0));
+      const mb_lds_d* Z = (const mb_lds_d*)lds_ptr(red + 7);  // (0, set in the first phase)
+      if (staged)
+        da_fx_mfma<false>((const mb_lds_d*)lds_ptr(Minv), lda, (const mb_lds_d*)lds_ptr(H), dtg, dts,
+                          (const mb_lds_d*)lds_ptr(da0), nj, nc, L, mode, dt, SiL, fd ? nc : 0, dfx,
+                          (const mb_lds_d*)lds_ptr(Je), (const mb_lds_d*)lds_ptr(Ai), (const mb_lds_d*)lds_ptr(Jc),
+                          Fx, Z);
       else
-        da_fx_mfma<mb_lds_d>((const mb_lds_d*)lds_ptr(Minv), lda, (const mb_lds_d*)lds_ptr(H),
-                             (const mb_lds_d*)lds_ptr(dtau), (const mb_lds_d*)lds_ptr(da0), nj, nc, L, mode, dt, SiL,
-                             fd ? nc : 0, dfx, (const mb_lds_d*)lds_ptr(Je),
-                             (const mb_lds_d*)lds_ptr(Ai), (const mb_lds_d*)lds_ptr(Jc), Fx);
+        da_fx_mfma<true>((const mb_lds_d*)lds_ptr(Minv), lda, (const mb_lds_d*)lds_ptr(H), dtg, dts,
+                         (const mb_lds_d*)lds_ptr(da0), nj, nc, L, mode, dt, SiL, fd ? nc : 0, dfx,
+                         (const mb_lds_d*)lds_ptr(Je), (const mb_lds_d*)lds_ptr(Ai), (const mb_lds_d*)lds_ptr(Jc),
+                         Fx, Z);
     }
     constexpr bool dfx_done = true;
     (void)nl;
@@ -4248,6 +4374,9 @@ MB_HD __forceinline__ void knot_calc_diff_x(const X& ex, const double* P, int nx
       }
       if (kk == (b.ncost > 0 ? b.ncost - 1 : 0)) cg[4 * kMaxCosts - 1] = g;  // the group count
     }
+#if defined(__HIP_DEVICE_COMPILE__)
+    MB_GJ_MARK(24);
+#endif
   });
   // Output blocks in row pairs over all lanes: consecutive lanes write consecutive
   // 16-B pairs of the column-major blocks (n even, blocks 16-B aligned); the lane's
@@ -4331,7 +4460,9 @@ MB_HD __forceinline__ void knot_calc_diff_x(const X& ex, const double* P, int nx
   // their q (or x) columns, force-cost rows from d lambda / dx, du
   const int ngr = (int)cg[4 * kMaxCosts - 1];
   ex.run([&](int lane) {
-    for (int e = lane; e < nrows * ldR; e += ex.nt) {
+    // entry e of the rows (the Jacobians and d lambda / dx, du may be in global memory:
+    // four entries' loads issued before their stores)
+    auto rentry = [&](int e) __attribute__((always_inline)) -> double {
       const int row = e / ldR, c = e % ldR;
       const int src = (int)csrc[row];
       double v = 0.;
@@ -4349,14 +4480,27 @@ MB_HD __forceinline__ void knot_calc_diff_x(const X& ex, const double* P, int nx
         else if (c - L < nu)
           v = force_jac(C, dfu + (c - L), nj, e2);
       }
-      Rm[e] = c < L + nu ? v : 0.;
+      return c < L + nu ? v : 0.;
+    };
+    const int ne = nrows * ldR;
+    for (int e0 = lane; e0 < ne; e0 += 2 * ex.nt) {
+      double v4[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) v4[u] = e0 + u * ex.nt < ne ? rentry(e0 + u * ex.nt) : 0.;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int e = e0 + u * ex.nt;
+        if (e >= ne) break;
+        Rm[e] = v4[u];
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(MB_NO_MFMA_GN)
-      // the matrix-core GEMM takes each row's weight times its activation Hessian (w h)
-      if (c == 0) {
-        const CRec C{P + (int64_t)cg[4 * (int)cgi[row] + 2]};
-        ch[row] *= C.weight();
-      }
+        // the matrix-core GEMM takes each row's weight times its activation Hessian (w h)
+        if (e % ldR == 0) {
+          const int row = e / ldR;
+          const CRec C{P + (int64_t)cg[4 * (int)cgi[row] + 2]};
+          ch[row] *= C.weight();
+        }
 #endif
+      }
     }
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(MB_NO_MFMA_GN)
     // the diagonal terms of the state / control costs (beyond the free-flyer block), per
