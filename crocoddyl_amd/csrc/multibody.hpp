@@ -3788,9 +3788,10 @@ __device__ __attribute__((noinline)) void da_fx_mfma(const mb_lds_d* Minv, int l
 // upper-triangle 16 x 16 tiles (bi <= bj) of the (L + m)^2 product; Lxx and Luu are
 // written from the upper triangle and mirrored, Lxu from the x-row / u-column tiles.
 // wrow[r]: the row's weight times its activation Hessian (w h).
-__device__ __forceinline__ void gn_blocks_mfma(const double* Rm, int ldR, const double* wrow, int nrows, int L,
-                                               int nu, int m, double sc, double* Lxx, double* Lxu, double* Luu,
-                                               const double* diag) {
+// (noinline: its registers apart from the kernel body's, which is at the VGPR cap here)
+__device__ __attribute__((noinline)) void gn_blocks_mfma(const double* Rm, int ldR, const double* wrow, int nrows,
+                                                         int L, int nu, int m, double sc, double* Lxx, double* Lxu,
+                                                         double* Luu, const double* diag) {
   const int lane = (int)threadIdx.x & 63, wave = (int)threadIdx.x >> 6, nw = (int)blockDim.x >> 6;
   const int li = lane & 15, lk = lane >> 4;
   const int NC = L + m, cv = L + nu, NT = (NC + 15) >> 4, ntiles = NT * (NT + 1) / 2, n = L;
@@ -3810,18 +3811,31 @@ __device__ __forceinline__ void gn_blocks_mfma(const double* Rm, int ldR, const 
     // around a load becomes a branch that waits for it)
     const int cac = ca < ldR ? ca : ldR - 1, cbc = cb < ldR ? cb : ldR - 1;
     mb_f64x4 acc = {0., 0., 0., 0.};
-#pragma unroll 4
-    for (int kb = 0; kb < nrows; kb += 4) {
-      const int r = kb + lk, rc = r < nrows ? r : nrows - 1;
-      const double* Rr = Rm + (int64_t)rc * ldR;
-      // (the tile's transpose: the accumulator rows run over bj, its columns over bi,
-      // so lane li holds row 16 bi + li and the 16 lanes of a column store 128
-      // contiguous bytes of the column-major blocks)
-      double x = Rr[cbc], y = Rr[cac], wr = wrow[rc];
-      asm volatile("" : "+v"(x), "+v"(y), "+v"(wr));  // (loads pinned: not sunk into branches)
-      const double a = (r < nrows && cb < cv) ? x : 0.;
-      const double bv = (r < nrows && ca < cv) ? y * wr : 0.;
-      acc = mb_mfma(a, bv, acc);
+    // (the tile's transpose: the accumulator rows run over bj, its columns over bi, so
+    // lane li holds row 16 bi + li and the 16 lanes of a column store 128 contiguous
+    // bytes of the column-major blocks); chunks of 4 k-steps, the chunk's 12 loads issued
+    // first and pinned by one empty asm (not sunk into the selects' branches)
+#pragma unroll 1
+    for (int k0 = 0; k0 < nrows; k0 += 16) {
+      double x[4], y[4], wr[4];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int r = k0 + 4 * s + lk, rc = r < nrows ? r : nrows - 1;
+        const mb_lds_d* Rr = (const mb_lds_d*)Rm + (int64_t)rc * ldR;
+        x[s] = Rr[cbc];
+        y[s] = Rr[cac];
+        wr[s] = ((const mb_lds_d*)wrow)[rc];
+      }
+      asm volatile(""
+                   : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(y[0]), "+v"(y[1]), "+v"(y[2]), "+v"(y[3]),
+                     "+v"(wr[0]), "+v"(wr[1]), "+v"(wr[2]), "+v"(wr[3]));
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int r = k0 + 4 * s + lk;
+        const double a = (r < nrows && cb < cv) ? x[s] : 0.;
+        const double bv = (r < nrows && ca < cv) ? y[s] * wr[s] : 0.;
+        if (k0 + 4 * s < nrows) acc = mb_mfma(a, bv, acc);
+      }
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -4536,6 +4550,7 @@ MB_HD __forceinline__ void knot_calc_diff_x(const X& ex, const double* P, int nx
     const double* const u = ex.lds(u_);
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(MB_NO_MFMA_GN)
     gn_blocks_mfma(Rm, ldR, ch, nrows, L, nu, m, sc, Lxx, Lxu, Luu, cdg_);
+    MB_GJ_MARK(26);
 #else
     const int n4 = (n + 3) / 4, m4 = (m + 3) / 4;
     // Lxx is symmetric: only its row blocks i0 <= j are tasks (column j has j / 4 + 1 of
@@ -4659,7 +4674,9 @@ MB_HD __forceinline__ void knot_calc_diff_x(const X& ex, const double* P, int nx
       mb_gstore((isu ? Lu : Lx) + j, integ ? sc * acc : acc);
     }
 #if defined(__HIP_DEVICE_COMPILE__)
+    MB_GJ_MARK(27);
     assemble(lane, n);  // Fu
+    MB_GJ_MARK(28);
 #else
     (void)lane;
 #endif
