@@ -801,16 +801,44 @@ __device__ __forceinline__ bool fwd_trial(const Dev& D, int b, const ElemState& 
       const double* K = D.K + D.run(b, t) * D.sNM;
       const double* kv = D.k + D.run(b, t) * D.sM;
       // us_try = us - k * alpha - K * dx ,  dx = diff(xs, xs_try)
-      for (int i = tid; i < m; i += NT) {
-        double v = 0.;
-        if (i < nu) {
-          const double kd2 = ff ? gains_dot(K, m, i, n, [&](int j) { return dxv[j]; })
-                                : gains_dot(K, m, i, n, [&](int j) { return xv[j] - xs[j]; });
-          v = (us[i] - kv[i] * alpha) - kd2;
-          // SolverBoxFDDP::forwardPass: cwiseMax(u_lb).cwiseMin(u_ub) (box-fddp.cpp:100-102)
-          if (D.box_knot(b, t)) v = std_min(std_max(v, D.ulb[D.run(b, t) * D.sM + i]), D.uub[D.run(b, t) * D.sM + i]);
+      // K (HBM) is read by the whole workgroup: control i's dot product split into np
+      // contiguous j-ranges of one load batch each (np = NT / m), their partials (in the
+      // knot calc's LDS scratch, free between knots) summed in range order by lane i: one
+      // round trip to HBM instead of one per 8 entries of a 32-lane chain
+      const int np = m > 0 && m <= NT ? (NT / m < 8 ? NT / m : 8) : 1;
+      if (np > 1 && D.mbw >= (int64_t)np * m) {
+        const int i = tid % m, pp = tid / m, len = (n + np - 1) / np, j0 = pp * len;
+        double ps = 0.;
+        if (pp < np && i < nu) {
+          const int j1 = j0 + len < n ? j0 + len : n;
+          ps = ff ? gains_dot(K + (int64_t)j0 * m, m, i, j1 - j0, [&](int j) { return dxv[j0 + j]; })
+                  : gains_dot(K + (int64_t)j0 * m, m, i, j1 - j0, [&](int j) { return xv[j0 + j] - xs[j0 + j]; });
         }
-        uv[i] = v;
+        if (pp < np) mbw[pp * m + i] = ps;
+        __syncthreads();
+        if (tid < m) {
+          double v = 0.;
+          if (tid < nu) {
+            double kd2 = 0.;
+            for (int q = 0; q < np; ++q) kd2 += mbw[q * m + tid];
+            v = (us[tid] - kv[tid] * alpha) - kd2;
+            // SolverBoxFDDP::forwardPass: cwiseMax(u_lb).cwiseMin(u_ub) (box-fddp.cpp:100-102)
+            if (D.box_knot(b, t))
+              v = std_min(std_max(v, D.ulb[D.run(b, t) * D.sM + tid]), D.uub[D.run(b, t) * D.sM + tid]);
+          }
+          uv[tid] = v;
+        }
+      } else {
+        for (int i = tid; i < m; i += NT) {
+          double v = 0.;
+          if (i < nu) {
+            const double kd2 = ff ? gains_dot(K, m, i, n, [&](int j) { return dxv[j]; })
+                                  : gains_dot(K, m, i, n, [&](int j) { return xv[j] - xs[j]; });
+            v = (us[i] - kv[i] * alpha) - kd2;
+            if (D.box_knot(b, t)) v = std_min(std_max(v, D.ulb[D.run(b, t) * D.sM + i]), D.uub[D.run(b, t) * D.sM + i]);
+          }
+          uv[i] = v;
+        }
       }
       __syncthreads();
     }
@@ -965,13 +993,18 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((FAST || MB)
     red = xn + D.sX;
     flag = (int*)(red + 5 * (NT / kWave) + 8);
   }
-  ElemState s = *st;
+  // The element's solver state lives in LDS during the line search: a register copy
+  // would be held across every trial's rollout (the knot calc runs at the VGPR cap); the
+  // threads take a copy after each trial, and thread 0 writes the changes back.
+  __shared__ ElemState ss;
+  if (threadIdx.x == 0) ss = *st;
+  __syncthreads();
   int nwr = D.T + 1;
   auto trial = [&](double alpha, double& ct, double& dv) {
     if constexpr (FAST)
-      return fwd_trial_fast<NT, true>(D, b, s, alpha, xv, dxv, xn, pa, pdyn, red, flag, ct, dv, pl, pcap, cached);
+      return fwd_trial_fast<NT, true>(D, b, ss, alpha, xv, dxv, xn, pa, pdyn, red, flag, ct, dv, pl, pcap, cached);
     else
-      return fwd_trial<NT, MB>(D, b, s, alpha, xv, uv, xn, red, flag, ct, dv, pl, pcap, cached, (double*)flag + 2 + 2 * D.sN,
+      return fwd_trial<NT, MB>(D, b, ss, alpha, xv, uv, xn, red, flag, ct, dv, pl, pcap, cached, (double*)flag + 2 + 2 * D.sN,
                            (double*)flag + 2, slot, &nwr);
   };
   // line search (fddp.cpp:53-81). One call site of the trial, so it is inlined (its
@@ -987,7 +1020,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((FAST || MB)
       if (threadIdx.x == 0) {
         st->fwd_fail = ok ? 0 : 1;
         st->cost_try = ct;
-        st->dV = s.cost - ct;
+        st->dV = ss.cost - ct;
         st->dv = ok ? dv : 0.;
       }
       return;
@@ -1002,13 +1035,18 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((FAST || MB)
       }
       return;
     }
+    ElemState s = ss;
     s.steplength = alpha;
-    if (!ok) continue;
-    if (ls_accept(prm, s, alpha, ct, dv)) {
+    const bool acc = ok && ls_accept(prm, s, alpha, ct, dv);
+    __syncthreads();  // (every thread has read ss)
+    if (threadIdx.x == 0) ss = s;
+    __syncthreads();
+    if (acc) {
       accepted = true;
       break;
     }
   }
+  ElemState s = ss;
   ls_finish(prm, s, accepted);
   if (threadIdx.x == 0) {
     *st = s;
