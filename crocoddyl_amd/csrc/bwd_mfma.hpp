@@ -347,9 +347,7 @@ __device__ __forceinline__ bool chol_inv_sweep(const double* Quu, double* C, dou
   asm volatile("" ::: "memory");
   // C^T's area may still be read by other waves (ct_target > 0: wait for them)
   if (Ct && ct_target > 0) {
-    while (__hip_atomic_load(ct_ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < ct_target)
-      __builtin_amdgcn_s_sleep(1);
-    asm volatile("" ::: "memory");
+    lds_wait_ge(ct_ready, ct_target);
   }
 #pragma unroll
   for (int r = 0; r < RPL; ++r) {
@@ -421,9 +419,7 @@ __device__ __forceinline__ bool chol_inv_blocked2(const double* Quu, double* C, 
   }
   asm volatile("" ::: "memory");
   if (ct_target > 0) {
-    while (__hip_atomic_load(ct_ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < ct_target)
-      __builtin_amdgcn_s_sleep(1);
-    asm volatile("" ::: "memory");
+    lds_wait_ge(ct_ready, ct_target);
   }
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
@@ -902,13 +898,11 @@ __device__ __forceinline__ bool bwd_knot(const Dev& D, const BwdLds& L, int b, i
   // The u-block owners only write Quu and go on (their Quu rows are what the
   // inversion waits for); the inversion wave does not read V' at all.
   if constexpr (NO > 0) {
-    if (lane == 0) __hip_atomic_fetch_add(L.flag + 2, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (lane == 0) lds_signal(L.flag + 2);
   }
   if constexpr (P.owns_x(W)) {
     const int target = P.gwaves * (D.T - t);
-    while (__hip_atomic_load(L.flag + 2, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < target)
-      __builtin_amdgcn_s_sleep(1);
-    asm volatile("" ::: "memory");
+    lds_wait_ge(L.flag + 2, target);
   }
   // H(i, j) = G_i^T Z_j (+ Lxu / Luu + ureg I), j >= jstart(i). Qxx(i, j) goes to the
   // dead V' buffer at the mirrored position (R, C) -> V[R * LDV + C]
@@ -987,20 +981,18 @@ __device__ __forceinline__ bool bwd_knot(const Dev& D, const BwdLds& L, int b, i
     __builtin_amdgcn_sched_barrier(0);
   }
   if constexpr (W != 0 && P.owns_u(W)) {  // this wave's Quu rows are stored: tell wave 0
-    if (lane == 0) __hip_atomic_fetch_add(L.flag + 1, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (lane == 0) lds_signal(L.flag + 1);
     __builtin_amdgcn_s_setprio(0);
   }
   if constexpr (!Cfg::ct_own && NO > 0) {  // H done: its reads of Zu are over (C^T lands there)
-    if (lane == 0) __hip_atomic_fetch_add(L.flag + 4, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (lane == 0) lds_signal(L.flag + 4);
   }
   stamp.mark(1);
   // ---- wave 0: Quu^-1 by the symmetric sweep (overlaps waves 1-3) ----------
   if constexpr (W == 0) {
     if constexpr (P.uwaves > 0) {  // wait for the other u-block owners' Quu rows
       const int target = P.uwaves * (D.T - t);
-      while (__hip_atomic_load(L.flag + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < target)
-        __builtin_amdgcn_s_sleep(1);
-      asm volatile("" ::: "memory");
+      lds_wait_ge(L.flag + 1, target);
     }
     if (boxk) {
       if (!box_gains_wave<MP, LDQ>(D, L, b, t, cur, lane) && lane == 0) *L.flag = 1;
@@ -1162,7 +1154,7 @@ __device__ __forceinline__ bool bwd_knot(const Dev& D, const BwdLds& L, int b, i
   // and wave 0's Quu k; the other waves only signal (when they produced
   // something) and go on issuing the DMA.
   if constexpr (W == 0 || P.owns_x(W)) {
-    if (lane == 0) __hip_atomic_fetch_add(L.flag + 3, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (lane == 0) lds_signal(L.flag + 3);
   }
   // With C^T over Zu (!ct_own) the next knot's LDS-DMA into Zu must also wait for every
   // C^T read (the K products of the x-block owners, wave 0's k): the waves that only
@@ -1170,9 +1162,7 @@ __device__ __forceinline__ bool bwd_knot(const Dev& D, const BwdLds& L, int b, i
   // differing between trial-group sizes)
   if constexpr (P.owns_x(W) || (!Cfg::ct_own && NW == 8)) {
     const int target = (P.xwaves + (P.owns_x(0) ? 0 : 1)) * (D.T - t);
-    while (__hip_atomic_load(L.flag + 3, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < target)
-      __builtin_amdgcn_s_sleep(1);
-    asm volatile("" ::: "memory");
+    lds_wait_ge(L.flag + 3, target);
   }
   if constexpr (NW == 8) issue_dma();
   // ---- P3: Vx = Qx + K^T Quuk - 2 K^T Qu (+ Vxx fs), reduction terms -------

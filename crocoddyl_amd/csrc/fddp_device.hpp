@@ -52,6 +52,25 @@ __device__ __forceinline__ T* lds_ptr(T* p) {
   return p;
 }
 
+// ---- LDS progress counters between the waves of a workgroup ------------------------
+// For data exchanged through LDS only: the fences order LDS accesses alone (an LDS-only
+// s_waitcnt lgkmcnt(0)). A generic workgroup release would also wait for every vector
+// memory operation in flight (vmcnt(0)): the backward sweep's LDS-DMA of the next knot's
+// operands, which the counters are meant to overlap. Data in global memory needs the
+// generic fences instead (multibody.hpp tree_side_barrier).
+__device__ __forceinline__ void lds_signal(int* ctr) {  // after this wave's LDS writes / reads
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_publish(int* ctr, int v) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __hip_atomic_store(ctr, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_wait_ge(int* ctr, int target) {  // before the LDS accesses it guards
+  while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target) __builtin_amdgcn_s_sleep(1);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // ---- register broadcasts within a wave (64 lanes = 4 rows of 16) -------------------
 // lane n of every row of 16 lanes, to the whole row (DPP row_newbcast: a VALU move, no
 // LDS-crossbar round trip as __shfl's ds_bpermute); n a compile-time constant

@@ -722,7 +722,7 @@ __device__ __forceinline__ bool gj_mfma(double* A_, int nr, int ld, int nc, bool
     const int r0 = 16 * k;
     double d[4] = {0., 0., 0., 0.};
     if (flagged && k > 0 && wave < nct) {  // tile k updated through step k - 1
-      while (__hip_atomic_load(prog, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < k) __builtin_amdgcn_s_sleep(1);
+      lds_wait_ge(prog, k);
       asm volatile("" ::: "memory");
     }
     // A: only the waves that own a column tile need N (one sweep per SIMD, not two);
@@ -775,7 +775,7 @@ __device__ __forceinline__ bool gj_mfma(double* A_, int nr, int ld, int nc, bool
     }
     MB_GJ_MARK(1 + 3 * k);
     if (flagged && k > 0 && wave < nct) {  // all of tile k updated through step k - 1
-      while (__hip_atomic_load(prog2, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < k) __builtin_amdgcn_s_sleep(1);
+      lds_wait_ge(prog2, k);
       asm volatile("" ::: "memory");
     }
 #pragma unroll 1
@@ -805,7 +805,7 @@ __device__ __forceinline__ bool gj_mfma(double* A_, int nr, int ld, int nc, bool
           if (r < nr && pc >= 0 && pc < nc) A[r + ld * pc] = acc[q];
         }
         if (flagged && j == k + 1 && i == k + 1) {  // the next sweep's block is ready
-          if (lane == 0) __hip_atomic_store(prog, k + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+          if (lane == 0) lds_publish(prog, k + 1);
         }
       }
 #pragma unroll
@@ -814,7 +814,7 @@ __device__ __forceinline__ bool gj_mfma(double* A_, int nr, int ld, int nc, bool
         if (r < nr && pc >= 0 && pc < nc) A[r + ld * pc] = -R[q];
       }
       if (flagged && j == k + 1) {  // the whole next pivot tile is ready
-        if (lane == 0) __hip_atomic_store(prog2, k + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (lane == 0) lds_publish(prog2, k + 1);
       }
     }
 #pragma unroll
