@@ -1397,6 +1397,7 @@ __global__ __launch_bounds__(NW * 64) void backward_mfma_kernel(Dev D, Prm prm, 
   const bool feas = st->is_feasible != 0;
   double xreg = st->xreg, ureg = st->ureg;
   bool ok;
+  int tries = 0;
   for (;;) {
     ok = bwd_sweep_mfma<NTL, MTL, NW>(D, b, feas, xreg, ureg, st->cur, sm);
     __syncthreads();
@@ -1404,7 +1405,9 @@ __global__ __launch_bounds__(NW * 64) void backward_mfma_kernel(Dev D, Prm prm, 
     xreg *= prm.regfactor;  // increaseRegularization (ddp.cpp:312-318)
     if (xreg > prm.regmax) xreg = prm.regmax;
     ureg = xreg;
-    if (xreg == prm.regmax) break;
+    // (as the reference: at regmax; also on a NaN xreg or a regfactor <= 1, which would
+    // never reach it: every wave of the workgroup must leave the loop)
+    if (!(xreg < prm.regmax) || ++tries >= kMaxRegRetries) break;
   }
   if (threadIdx.x == 0) {
     st->xreg = xreg;

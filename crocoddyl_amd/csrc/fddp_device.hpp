@@ -40,6 +40,10 @@ struct ElemState {
 
 static_assert(sizeof(ElemState) % 8 == 0, "ElemState alignment");
 
+// Bound on the backward kernels' regularisation retries within one sweep (the
+// reference's loop ends at regmax: 1e-9 * 10^k reaches the default 1e9 in 18 steps).
+constexpr int kMaxRegRetries = 64;
+
 __host__ __device__ inline int64_t pad2(int64_t v) { return (v + 1) & ~int64_t(1); }
 
 // A pointer known to address LDS: the assumption lets the address-space inference

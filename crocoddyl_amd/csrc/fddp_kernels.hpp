@@ -641,6 +641,7 @@ __global__ __launch_bounds__(NT) void backward_kernel(Dev D, Prm prm, int mode) 
   const bool feas = st->is_feasible != 0;
   double xreg = st->xreg, ureg = st->ureg;
   bool ok;
+  int tries = 0;
   for (;;) {
     if (threadIdx.x == 0) *S.flag = 0;
     __syncthreads();
@@ -651,7 +652,9 @@ __global__ __launch_bounds__(NT) void backward_kernel(Dev D, Prm prm, int mode) 
     xreg *= prm.regfactor;
     if (xreg > prm.regmax) xreg = prm.regmax;
     ureg = xreg;
-    if (xreg == prm.regmax) break;
+    // (as the reference: at regmax; also on a NaN xreg or a regfactor <= 1, which would
+    // never reach it: every wave of the workgroup must leave the loop)
+    if (!(xreg < prm.regmax) || ++tries >= kMaxRegRetries) break;
   }
   if (threadIdx.x == 0) {
     st->xreg = xreg;
