@@ -178,7 +178,19 @@ struct MfmaCfg {
   static constexpr int LDT = MP + 1;
   static constexpr bool ct_own = sizeof(double) * (total0 + MP * LDT) <= 160 * 1024;
   static constexpr int oCt = ct_own ? total0 : oZu;
-  static constexpr int total = ct_own ? total0 + MP * LDT : total0;
+  // the prefetch plan's second operand buffers (BwdPlan::prefetch; C^T in its own area):
+  // Z, then lx, lu, fs
+  static constexpr int oZx2 = (total0 + MP * LDT + 1) & ~1;
+  static constexpr int oZu2 = oZx2 + NP * ZLD;
+  static constexpr int oLx2 = oZu2 + MP * ZLD + 2;
+  static constexpr int oLu2 = oLx2 + NP;
+  static constexpr int oFs2 = oLu2 + MP;
+  // and the cost blocks Lxx | Lxu | Luu of a knot (n x n, n x m, m x m, column-major as in
+  // HBM), twice: the prefetch plan stages them with the knot's other operands
+  static constexpr int CB = NP * NP + NP * MP + MP * MP;
+  static constexpr int oCb = (oFs2 + NP + 1) & ~1;
+  static constexpr bool pre_fits = ct_own && sizeof(double) * (oCb + 2 * CB) <= 160 * 1024;
+  static constexpr int total = pre_fits ? oCb + 2 * CB : (ct_own ? total0 + MP * LDT : total0);
   static_assert(ct_own || MP * LDT <= MP * ZLD, "C^T over Zu");
   static constexpr size_t bytes = sizeof(double) * total;
 };
@@ -567,7 +579,9 @@ struct BwdPlan {
   int ndma;    // waves issuing the LDS-DMA of the next knot's operands
   int dmarank[8];
   int xwaves;  // waves owning x blocks (the P3 consumers)
-  constexpr BwdPlan() : nown{}, blk{}, ntile{}, tile{}, uwaves(0), gwaves(0), ndma(0), dmarank{}, xwaves(0) {
+  bool prefetch;  // double-buffered operands, DMA at the knot's start (see below)
+  constexpr BwdPlan()
+      : nown{}, blk{}, ntile{}, tile{}, uwaves(0), gwaves(0), ndma(0), dmarank{}, xwaves(0), prefetch(false) {
     int owner[16] = {};
     if (NW == 1) {  // small knots: one wave owns every block (no partial barrier ever waits)
       for (int u = 0; u < MTL; ++u) blk[0][nown[0]++] = NTL + u;
@@ -638,7 +652,16 @@ struct BwdPlan {
     // hundred cycles, so in the 8-wave plan it goes to the waves that have no
     // x blocks (no P2 / P3 MFMA work); they skip B2 (see bwd_knot)
     for (int w = 0; w < NW; ++w) dmarank[w] = -1;
-    if (NW <= 4) {
+    // Prefetch plan (C^T in its own area, some wave other than 0 owns no block): the
+    // operands are double-buffered and those idle waves issue knot t-1's DMA at the start
+    // of knot t, a whole knot before B3 waits for it (and B1 waits for LDS only)
+    int idle = 0;
+    for (int w = 1; w < NW; ++w) idle += nown[w] == 0 ? 1 : 0;
+    prefetch = MfmaCfg<NTL, MTL>::pre_fits && idle >= 1;
+    if (prefetch) {
+      for (int w = 1; w < NW; ++w)
+        if (nown[w] == 0) dmarank[w] = ndma++;
+    } else if (NW <= 4) {
       for (int w = 0; w < NW; ++w) dmarank[w] = ndma++;
     } else {  // the waves without x blocks: no MFMA work in P2 / P3
       for (int w = 0; w < NW; ++w)
@@ -684,9 +707,18 @@ __host__ __device__ constexpr int bwd_jstart(int i) {
   return i < NTL ? i : NTL;
 }
 
+// A knot descriptor's nu by a scalar (constant address space) load: the descriptors do
+// not change during a kernel.
+__device__ __forceinline__ int knot_nu_const(const Dev& D, int t) {
+  typedef const __attribute__((address_space(4))) fddp_knot_desc* const_knot_ptr;
+  return ((const_knot_ptr)(uintptr_t)D.knots)[t].nu;
+}
+
 // LDS carve of one workgroup (see MfmaCfg).
 struct BwdLds {
   double *V, *Qxu, *Quu, *Qi, *vx, *qx, *lxv, *fsb, *qu, *luv, *kv, *quuk, *rowbuf, *red, *Zx, *Zu, *Ct;
+  double *Zx2, *Zu2, *lxv2, *luv2, *fsb2;  // the prefetch plan's second buffers (else = the first)
+  double *cb0, *cb1;                       // the prefetch plan's cost-block buffers
   int* flag;
 };
 
@@ -740,7 +772,7 @@ __device__ __forceinline__ bool box_gains_wave(const Dev& D, const BwdLds& L, in
 // with their own W; the barriers inside line up one to one).
 template <int NTL, int MTL, int NW, int W>
 __device__ __forceinline__ bool bwd_knot(const Dev& D, const BwdLds& L, int b, int t, bool feas, double xreg,
-                                         double ureg, int cur, Stamp& stamp) {
+                                         double ureg, int cur, Stamp& stamp, double (&red5)[5]) {
   using Cfg = MfmaCfg<NTL, MTL>;
   constexpr int NP = Cfg::NP, MP = Cfg::MP, JT = Cfg::JT, LDV = Cfg::LDV, LDQ = Cfg::LDQ, ZLD = Cfg::ZLD;
   constexpr BwdPlan<NTL, MTL, NW> P{};
@@ -754,7 +786,9 @@ __device__ __forceinline__ bool bwd_knot(const Dev& D, const BwdLds& L, int b, i
   // impulse knot has none: Quu_inv, K and k vanish, Vx = Qx, Vxx = Qxx as the reference's
   // backwardPass does for nu = 0, ddp.cpp:229-253); the blocks' columns beyond mu are
   // not read
-  int lane = threadIdx.x & 63, n = D.n, m = D.m, mu = D.knots[t].nu;
+  // (the knot's nu by a scalar load through the constant address space: a vector load
+  // would wait, in-order, behind the previous knot's stores still in flight)
+  int lane = threadIdx.x & 63, n = D.n, m = D.m, mu = knot_nu_const(D, t);
   asm volatile("" : "+v"(lane));
   asm volatile("" : "+s"(n), "+s"(m));
   mu = __builtin_amdgcn_readfirstlane(mu);
@@ -764,23 +798,42 @@ __device__ __forceinline__ bool bwd_knot(const Dev& D, const BwdLds& L, int b, i
   const bool boxk = feas && mu > 0 && D.box_knot(b, t);  // SolverBoxFDDP gains on this knot (box-fddp.cpp:47)
   if constexpr (W != 0 && P.owns_u(W)) __builtin_amdgcn_s_setprio(2);  // Quu first: the inversion waits on it
   // the next knot's operands (LDS-DMA; lands during P2 / P3)
+  // this knot's operand buffers (prefetch plan: by the knot's parity) and knot t-1's
+  constexpr bool pre = P.prefetch;
+  const bool odd = pre && (t & 1);
+  double* const Zx = odd ? L.Zx2 : L.Zx;
+  double* const Zu = odd ? L.Zu2 : L.Zu;
+  const double* const lxv = odd ? L.lxv2 : L.lxv;
+  const double* const luv = odd ? L.luv2 : L.luv;
+  const double* const fsb = odd ? L.fsb2 : L.fsb;
   auto issue_dma = [&]() {
   if constexpr (P.dmarank[W] >= 0) {
-    if (t > 0) {  // operands of knot t-1 land during P2/P3
+    if (t > 0) {  // operands of knot t-1 (prefetch plan: into the other buffers, with fs)
       constexpr int ND = P.ndma, RK = P.dmarank[W];
       const int64_t k1 = kk - 1;
+      const bool nb = pre && !odd;
+      double* const nZx = nb ? L.Zx2 : L.Zx;
+      double* const nZu = nb ? L.Zu2 : L.Zu;
       if ((n & 1) == 0 && ZLD - n <= 2 * 64) {
-        dma_cols_full<ND, ZLD>(L.Zx, D.Fx + k1 * D.sNN, n, n, D.zero16, RK, lane);
-        dma_cols_full<ND, ZLD>(L.Zu, D.Fu + k1 * D.sNM, n, m, D.zero16, RK, lane);
+        dma_cols_full<ND, ZLD>(nZx, D.Fx + k1 * D.sNN, n, n, D.zero16, RK, lane);
+        dma_cols_full<ND, ZLD>(nZu, D.Fu + k1 * D.sNM, n, m, D.zero16, RK, lane);
       } else {
-        dma_cols<ND>(L.Zx, ZLD, D.Fx + k1 * D.sNN, n, n, RK, lane);
-        dma_cols<ND>(L.Zu, ZLD, D.Fu + k1 * D.sNM, n, m, RK, lane);
+        dma_cols<ND>(nZx, ZLD, D.Fx + k1 * D.sNN, n, n, RK, lane);
+        dma_cols<ND>(nZu, ZLD, D.Fu + k1 * D.sNM, n, m, RK, lane);
       }
-      dma_vec<ND>(L.lxv, D.Lx + k1 * D.sN, n, RK, lane);
-      dma_vec<ND>(L.luv, D.Lu + k1 * D.sM, m, RK, lane);
+      dma_vec<ND>(nb ? L.lxv2 : L.lxv, D.Lx + k1 * D.sN, n, RK, lane);
+      dma_vec<ND>(nb ? L.luv2 : L.luv, D.Lu + k1 * D.sM, m, RK, lane);
+      if constexpr (pre) {
+        dma_vec<ND>(nb ? L.fsb2 : L.fsb, D.fs + k1 * D.sN, n, RK, lane);
+        double* const cb = nb ? L.cb1 : L.cb0;
+        dma_vec<ND>(cb, D.Lxx + k1 * D.sNN, n * n, RK, lane);
+        dma_vec<ND>(cb + n * n + (n * n & 1), D.Lxu + k1 * D.sNM, n * m, RK, lane);
+        dma_vec<ND>(cb + n * n + (n * n & 1) + n * m + (n * m & 1), D.Luu + k1 * D.sMM, m * m, RK, lane);
+      }
     }
   }
   };
+  if constexpr (pre) issue_dma();
   double* V = L.V;
   double* Qxu = L.Qxu;
   double* Quu = L.Quu;
@@ -797,9 +850,12 @@ __device__ __forceinline__ bool bwd_knot(const Dev& D, const BwdLds& L, int b, i
   double Lv[NVT][4][2];
   double Lq[NA][MTL][4];
   {
-    const double* Lxx = D.Lxx + kk * D.sNN;
-    const double* Lxu = D.Lxu + kk * D.sNM;
-    const double* Luu = D.Luu + kk * D.sMM;
+    // (the prefetch plan: from their LDS copies, staged a knot ahead)
+    const double* const cbk = odd ? L.cb1 : L.cb0;
+    const int o1 = n * n + (n * n & 1), o2 = o1 + n * m + (n * m & 1);
+    const double* Lxx = pre ? cbk : D.Lxx + kk * D.sNN;
+    const double* Lxu = pre ? cbk + o1 : D.Lxu + kk * D.sNM;
+    const double* Luu = pre ? cbk + o2 : D.Luu + kk * D.sMM;
 #pragma unroll
     for (int k3 = 0; k3 < P.ntile[W]; ++k3) {
       const int i = P.tile[W][k3][0], j = P.tile[W][k3][1];
@@ -853,7 +909,7 @@ __device__ __forceinline__ bool bwd_knot(const Dev& D, const BwdLds& L, int b, i
 #pragma unroll
     for (int o = 0; o < NO; ++o) {
       const int i = P.blk[W][o];
-      zf[buf][o] = i < NTL ? L.Zx[(16 * i + c) * ZLD + row] : L.Zu[(16 * (i - NTL) + c) * ZLD + row];
+      zf[buf][o] = i < NTL ? Zx[(16 * i + c) * ZLD + row] : Zu[(16 * (i - NTL) + c) * ZLD + row];
     }
   };
   // (rows >= n of V' are exactly zero, so the padded k-steps add nothing;
@@ -885,10 +941,10 @@ __device__ __forceinline__ bool bwd_knot(const Dev& D, const BwdLds& L, int b, i
     if (q == 0) {
       if (i < NTL) {
         const int R = 16 * i + c;
-        L.qx[R] = R < n ? L.lxv[R] + v : 0.;
+        L.qx[R] = R < n ? lxv[R] + v : 0.;
       } else {
         const int Ru = 16 * (i - NTL) + c;
-        L.qu[Ru] = Ru < mu ? L.luv[Ru] + v : 0.;
+        L.qu[Ru] = Ru < mu ? luv[Ru] + v : 0.;
       }
     }
   }
@@ -918,7 +974,7 @@ __device__ __forceinline__ bool bwd_knot(const Dev& D, const BwdLds& L, int b, i
   auto zload = [&](double(&zz)[4 * NTL], int j) {
 #pragma unroll
     for (int s = 0; s < 4 * NTL; ++s)
-      zz[s] = j < NTL ? L.Zx[(16 * j + c) * ZLD + 4 * s + q] : L.Zu[(16 * (j - NTL) + c) * ZLD + 4 * s + q];
+      zz[s] = j < NTL ? Zx[(16 * j + c) * ZLD + 4 * s + q] : Zu[(16 * (j - NTL) + c) * ZLD + 4 * s + q];
   };
 #pragma unroll
   for (int j = 0; j < JT; ++j) {
@@ -1011,15 +1067,59 @@ __device__ __forceinline__ bool bwd_knot(const Dev& D, const BwdLds& L, int b, i
     }
   }
   stamp.mark(2);
-  dma_barrier();  // B1 (also retires the fs DMA issued at the end of the last knot)
+  // B1 (without the prefetch plan it also retires the fs DMA issued at the end of the
+  // last knot; with it, the knot's DMA in flight stays in flight)
+  if constexpr (pre)
+    lds_barrier();
+  else
+    dma_barrier();
   stamp.mark(3);
   if (*L.flag) return false;
-  if constexpr (NW <= 4) issue_dma();
+  // the next knot's operands: right after B1, except in the 8-wave plan with C^T over Zu
+  // (after B2, once every C^T read is done)
+  constexpr bool early_dma = NW <= 4 || Cfg::ct_own;
+  if constexpr (early_dma && !pre) issue_dma();
   // ---- P2: K(:, i) = Quu^-1 Qxu(i, :)^T ; Vxx(i, j) = Qxx(i, j) - K(:, i)^T Qxu(j, :)^T
   f64x4 Kt[NA][MTL];
+  double kst = 0.;   // wave 0: k(row) (lanes part == 0)
+  double vfs[NA];    // Vxx fs (lanes q == 0 of the x blocks)
+  // This knot's K, k and Vxx fs to HBM. With C^T in its own area (the small shapes) after
+  // B3: their stores would otherwise hold B3's vmcnt wait, and they drain while the next
+  // knot's G runs. The C5 shape stores them where they are formed (measured: deferring
+  // costs its spilling kernel 3 %).
+  constexpr bool defer = Cfg::ct_own;
+  auto store_K = [&]() {
+    double* Kg = D.K + rr * D.sNM;
+#pragma unroll
+    for (int o = 0; o < NO; ++o) {
+      const int i = P.blk[W][o];
+      if (i < NTL) {
+        const int C = 16 * i + c;
+#pragma unroll
+        for (int it = 0; it < MTL; ++it)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int R = 16 * it + q + 4 * r;
+            if (R < m && C < n) Kg[(int64_t)C * m + R] = Kt[o][it][r];
+          }
+      }
+    }
+  };
+  auto store_fs = [&]() {
+#pragma unroll
+    for (int o = 0; o < NO; ++o) {
+      const int C = 16 * P.blk[W][o] + c;
+      if (P.blk[W][o] < NTL && !feas && q == 0 && C < n) D.Vxxfs[kk * D.sN + C] = vfs[o];
+    }
+  };
+  auto store_k = [&]() {
+    if constexpr (W == 0) {
+      const int row = lane % MP, part = lane / MP;
+      if (!boxk && part == 0 && row < m) D.k[rr * D.sM + row] = kst;
+    }
+  };
   {
     bool bad = false;
-    double* Kg = D.K + rr * D.sNM;
 #pragma unroll
     for (int o = 0; o < NO; ++o) {
       const int i = P.blk[W][o];
@@ -1049,16 +1149,9 @@ __device__ __forceinline__ bool bwd_knot(const Dev& D, const BwdLds& L, int b, i
             Kt[o][it] = kn;
           }
         }
-        const int C = 16 * i + c;
-#pragma unroll
-        for (int it = 0; it < MTL; ++it)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int R = 16 * it + q + 4 * r;
-            if (R < m && C < n) Kg[(int64_t)C * m + R] = Kt[o][it][r];
-          }
       }
     }
+    if constexpr (!defer) store_K();
     stamp.mark(4);
     // this wave's V tiles (i, j), i <= j: with K(:, i) when it owns block i
     // ("row" form, V(i, j) = Qxx(i, j) - K(:, i)^T Qxu(j, :)^T), else with
@@ -1131,8 +1224,9 @@ __device__ __forceinline__ bool bwd_knot(const Dev& D, const BwdLds& L, int b, i
         if (part == 0) {
           if (row >= mu) a = 0.;
           L.kv[row] = a;
-          if (row < m) D.k[rr * D.sM + row] = a;
+          kst = a;
         }
+        if constexpr (!defer) store_k();
       }
       asm volatile("" ::: "memory");
       double a;
@@ -1164,14 +1258,15 @@ __device__ __forceinline__ bool bwd_knot(const Dev& D, const BwdLds& L, int b, i
     const int target = (P.xwaves + (P.owns_x(0) ? 0 : 1)) * (D.T - t);
     lds_wait_ge(L.flag + 3, target);
   }
-  if constexpr (NW == 8) issue_dma();
+  if constexpr (!early_dma) issue_dma();
   // ---- P3: Vx = Qx + K^T Quuk - 2 K^T Qu (+ Vxx fs), reduction terms -------
   {
-    const double* fsv = L.fsb;
+    const double* fsv = fsb;
     bool bad = false;
     double pv[5] = {0., 0., 0., 0., 0.};
 #pragma unroll
     for (int o = 0; o < NO; ++o) {
+      if constexpr (defer) vfs[o] = 0.;
       const int i = P.blk[W][o];
       if (i < NTL) {
         const int R = 16 * i + c;
@@ -1207,7 +1302,10 @@ __device__ __forceinline__ bool bwd_knot(const Dev& D, const BwdLds& L, int b, i
           if (R < n) {
             v = ur ? (L.qx[R] + a) - 2 * c2 : L.qx[R] - c2;
             if (!feas) {
-              D.Vxxfs[kk * D.sN + R] = f;
+              if constexpr (defer)
+                vfs[o] = f;
+              else
+                D.Vxxfs[kk * D.sN + R] = f;
               v += f;
               pv[2] += v * fsv[R];
               pv[3] += fsv[R] * f;
@@ -1225,25 +1323,39 @@ __device__ __forceinline__ bool bwd_knot(const Dev& D, const BwdLds& L, int b, i
         pv[4] = L.qu[lane] * L.qu[lane];
       }
     }
+    // the expected-improvement / stopping terms. Small shapes: per-lane running sums over
+    // the knots, reduced over the workgroup once at the end of the sweep; the C5 shape
+    // (its kernel at the register cap): per-knot wave sums into D.part
+    if constexpr (defer) {
 #pragma unroll
-    for (int j = 0; j < 5; ++j) {
-      const double s = wave_sum(pv[j]);
-      if (lane == 0) L.red[j * NW + W] = s;
+      for (int j = 0; j < 5; ++j) red5[j] += pv[j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < 5; ++j) {
+        const double s = wave_sum(pv[j]);
+        if (lane == 0) L.red[j * NW + W] = s;
+      }
     }
     if (bad) *L.flag = 1;
   }
   stamp.mark(6);
   dma_barrier();  // B3: knot t-1 operands resident
   // fs of knot t-1 (read in its P3; landed by the vmcnt(0) of its B1)
-  if constexpr (P.dmarank[W] >= 0) {
+  if constexpr (P.dmarank[W] >= 0 && !pre) {
     if (t > 0) dma_vec<P.ndma>(L.fsb, D.fs + (kk - 1) * D.sN, n, P.dmarank[W], lane);
+  }
+  if constexpr (defer) {
+    store_K();
+    store_fs();
+    store_k();
   }
   return true;
 }
 
 template <int NTL, int MTL, int NW>
 __device__ __forceinline__ bool bwd_sweep_mfma(const Dev& D, int b, bool feas, double xreg, double ureg, int cur,
-                                               double* sm) {
+                                               double* sm, double (&ei)[3]) {
+  double red5[5] = {0., 0., 0., 0., 0.};  // running sums (C^T in its own area: the small shapes)
   using Cfg = MfmaCfg<NTL, MTL>;
   constexpr int NP = Cfg::NP, MP = Cfg::MP, LDV = Cfg::LDV, LDQ = Cfg::LDQ;
   constexpr int NT = NW * 64;
@@ -1268,6 +1380,14 @@ __device__ __forceinline__ bool bwd_sweep_mfma(const Dev& D, int b, bool feas, d
   L.Zx = sm + Cfg::oZx;
   L.Zu = sm + Cfg::oZu;
   L.Ct = sm + Cfg::oCt;
+  constexpr bool pre = BwdPlan<NTL, MTL, NW>{}.prefetch;
+  L.Zx2 = pre ? sm + Cfg::oZx2 : L.Zx;
+  L.Zu2 = pre ? sm + Cfg::oZu2 : L.Zu;
+  L.lxv2 = pre ? sm + Cfg::oLx2 : L.lxv;
+  L.luv2 = pre ? sm + Cfg::oLu2 : L.luv;
+  L.fsb2 = pre ? sm + Cfg::oFs2 : L.fsb;
+  L.cb0 = sm + Cfg::oCb;
+  L.cb1 = sm + Cfg::oCb + Cfg::CB;
   static_assert(Cfg::ct_own || NW == 8, "C^T over Zu needs the 8-wave plan's late LDS-DMA");
   double* V = L.V;
   const bool xr = !isnan(xreg);
@@ -1300,6 +1420,9 @@ __device__ __forceinline__ bool bwd_sweep_mfma(const Dev& D, int b, bool feas, d
     for (int i = tid; i < NP; i += NT) L.lxv[i] = 0.;
     for (int i = tid; i < MP; i += NT) L.luv[i] = 0.;
     for (int e = tid; e < (NP + MP) * Cfg::ZLD + 2; e += NT) L.Zx[e] = 0.;
+    if constexpr (pre) {  // the second buffers: Z, lx, lu, fs (contiguous)
+      for (int e = tid; e < (NP + MP) * Cfg::ZLD + 2 + 2 * NP + MP; e += NT) L.Zx2[e] = 0.;
+    }
     __syncthreads();
     double pv[2] = {0., 0.};
     for (int i = tid; i < NP; i += NT) {
@@ -1315,10 +1438,15 @@ __device__ __forceinline__ bool bwd_sweep_mfma(const Dev& D, int b, bool feas, d
       }
       L.vx[i] = v;
     }
-    wg_sums<NT, 2>(pv, L.red);
-    if (tid == 0) {
-      double* p = D.part + kk * 8;
-      p[0] = 0.; p[1] = 0.; p[2] = pv[0]; p[3] = pv[1]; p[4] = 0.;
+    if constexpr (Cfg::ct_own) {
+      red5[2] += pv[0];
+      red5[3] += pv[1];
+    } else {
+      wg_sums<NT, 2>(pv, L.red);
+      if (tid == 0) {
+        double* p = D.part + kk * 8;
+        p[0] = 0.; p[1] = 0.; p[2] = pv[0]; p[3] = pv[1]; p[4] = 0.;
+      }
     }
     if (D.dVxx) {
       for (int e = tid; e < n * n; e += NT) {
@@ -1328,13 +1456,20 @@ __device__ __forceinline__ bool bwd_sweep_mfma(const Dev& D, int b, bool feas, d
       for (int i = tid; i < n; i += NT) D.dVx[kk * D.sN + i] = L.vx[i];
     }
     __syncthreads();
-    if (T > 0) {  // operands of knot T-1
+    if (T > 0) {  // operands of knot T-1 (prefetch plan: into the buffers of its parity)
       const int64_t k1 = kk - 1;
-      dma_cols<NW>(L.Zx, Cfg::ZLD, D.Fx + k1 * D.sNN, n, n, wid, lane);
-      dma_cols<NW>(L.Zu, Cfg::ZLD, D.Fu + k1 * D.sNM, n, m, wid, lane);
-      dma_vec<NW>(L.lxv, D.Lx + k1 * D.sN, n, wid, lane);
-      dma_vec<NW>(L.luv, D.Lu + k1 * D.sM, m, wid, lane);
-      dma_vec<NW>(L.fsb, D.fs + k1 * D.sN, n, wid, lane);
+      const bool o1 = pre && ((T - 1) & 1);
+      dma_cols<NW>(o1 ? L.Zx2 : L.Zx, Cfg::ZLD, D.Fx + k1 * D.sNN, n, n, wid, lane);
+      dma_cols<NW>(o1 ? L.Zu2 : L.Zu, Cfg::ZLD, D.Fu + k1 * D.sNM, n, m, wid, lane);
+      dma_vec<NW>(o1 ? L.lxv2 : L.lxv, D.Lx + k1 * D.sN, n, wid, lane);
+      dma_vec<NW>(o1 ? L.luv2 : L.luv, D.Lu + k1 * D.sM, m, wid, lane);
+      dma_vec<NW>(o1 ? L.fsb2 : L.fsb, D.fs + k1 * D.sN, n, wid, lane);
+      if constexpr (pre) {
+        double* const cb = o1 ? L.cb1 : L.cb0;
+        dma_vec<NW>(cb, D.Lxx + k1 * D.sNN, n * n, wid, lane);
+        dma_vec<NW>(cb + n * n + (n * n & 1), D.Lxu + k1 * D.sNM, n * m, wid, lane);
+        dma_vec<NW>(cb + n * n + (n * n & 1) + n * m + (n * m & 1), D.Luu + k1 * D.sMM, m * m, wid, lane);
+      }
     }
     dma_barrier();
   }
@@ -1345,27 +1480,29 @@ __device__ __forceinline__ bool bwd_sweep_mfma(const Dev& D, int b, bool feas, d
     stamp.mark(7);
     bool ok = false;
     switch (wid) {
-      case 0: ok = bwd_knot<NTL, MTL, NW, 0>(D, L, b, t, feas, xreg, ureg, cur, stamp); break;
-      case 1: ok = bwd_knot<NTL, MTL, NW, 1>(D, L, b, t, feas, xreg, ureg, cur, stamp); break;
-      case 2: ok = bwd_knot<NTL, MTL, NW, 2>(D, L, b, t, feas, xreg, ureg, cur, stamp); break;
-      case 3: ok = bwd_knot<NTL, MTL, NW, 3>(D, L, b, t, feas, xreg, ureg, cur, stamp); break;
-      case 4: if constexpr (NW > 4) ok = bwd_knot<NTL, MTL, NW, 4>(D, L, b, t, feas, xreg, ureg, cur, stamp); break;
-      case 5: if constexpr (NW > 4) ok = bwd_knot<NTL, MTL, NW, 5>(D, L, b, t, feas, xreg, ureg, cur, stamp); break;
-      case 6: if constexpr (NW > 4) ok = bwd_knot<NTL, MTL, NW, 6>(D, L, b, t, feas, xreg, ureg, cur, stamp); break;
-      default: if constexpr (NW > 4) ok = bwd_knot<NTL, MTL, NW, 7>(D, L, b, t, feas, xreg, ureg, cur, stamp); break;
+      case 0: ok = bwd_knot<NTL, MTL, NW, 0>(D, L, b, t, feas, xreg, ureg, cur, stamp, red5); break;
+      case 1: ok = bwd_knot<NTL, MTL, NW, 1>(D, L, b, t, feas, xreg, ureg, cur, stamp, red5); break;
+      case 2: ok = bwd_knot<NTL, MTL, NW, 2>(D, L, b, t, feas, xreg, ureg, cur, stamp, red5); break;
+      case 3: ok = bwd_knot<NTL, MTL, NW, 3>(D, L, b, t, feas, xreg, ureg, cur, stamp, red5); break;
+      case 4: if constexpr (NW > 4) ok = bwd_knot<NTL, MTL, NW, 4>(D, L, b, t, feas, xreg, ureg, cur, stamp, red5); break;
+      case 5: if constexpr (NW > 4) ok = bwd_knot<NTL, MTL, NW, 5>(D, L, b, t, feas, xreg, ureg, cur, stamp, red5); break;
+      case 6: if constexpr (NW > 4) ok = bwd_knot<NTL, MTL, NW, 6>(D, L, b, t, feas, xreg, ureg, cur, stamp, red5); break;
+      default: if constexpr (NW > 4) ok = bwd_knot<NTL, MTL, NW, 7>(D, L, b, t, feas, xreg, ureg, cur, stamp, red5); break;
     }
     if (!ok) {  // the factorisation failed (every wave saw the flag)
       stamp.flush();
       return false;
     }
-    if (tid == 0) {
-      double* p = D.part + kk * 8;
-      const double* red = L.red;
+    if constexpr (!Cfg::ct_own) {
+      if (tid == 0) {
+        double* p = D.part + kk * 8;
+        const double* red = L.red;
 #pragma unroll
-      for (int j = 0; j < 5; ++j) {
-        double a = 0.;
-        for (int w = 0; w < NW; ++w) a += red[j * NW + w];
-        p[j] = a;
+        for (int j = 0; j < 5; ++j) {
+          double a = 0.;
+          for (int w = 0; w < NW; ++w) a += red[j * NW + w];
+          p[j] = a;
+        }
       }
     }
     if (D.dQxx) {
@@ -1385,6 +1522,14 @@ __device__ __forceinline__ bool bwd_sweep_mfma(const Dev& D, int b, bool feas, d
     }
   }
   stamp.flush();
+  // updateExpectedImprovement / stoppingCriteria (fddp.cpp:126-146, ddp.cpp:132-142):
+  // ei = {dg, dq, stop}, in thread 0
+  if constexpr (Cfg::ct_own) {  // the running sums over the workgroup
+    wg_sums<NT, 5>(red5, L.red);
+    ei[0] = feas ? red5[0] : red5[0] - red5[2];
+    ei[1] = feas ? -red5[1] : red5[3] - red5[1];
+    ei[2] = red5[4];
+  }  // (else: the per-knot sums in D.part, summed by the kernel's epilogue)
   return true;
 }
 
@@ -1398,8 +1543,9 @@ __global__ __launch_bounds__(NW * 64) void backward_mfma_kernel(Dev D, Prm prm, 
   double xreg = st->xreg, ureg = st->ureg;
   bool ok;
   int tries = 0;
+  double ei[3];  // dg, dq, stop (thread 0)
   for (;;) {
-    ok = bwd_sweep_mfma<NTL, MTL, NW>(D, b, feas, xreg, ureg, st->cur, sm);
+    ok = bwd_sweep_mfma<NTL, MTL, NW>(D, b, feas, xreg, ureg, st->cur, sm, ei);
     __syncthreads();
     if (ok || mode == 1) break;
     xreg *= prm.regfactor;  // increaseRegularization (ddp.cpp:312-318)
@@ -1419,25 +1565,30 @@ __global__ __launch_bounds__(NW * 64) void backward_mfma_kernel(Dev D, Prm prm, 
       st->n_iter_run += 1;
     }
     if (ok) {
-      const double* p = D.part + D.knot(b, 0) * 8;
-      const int T = D.T;
-      double dg = 0., dq = 0., stop = 0.;
-      if (!feas) {
-        dg -= p[T * 8 + 2];
-        dq += p[T * 8 + 3];
-      }
-      for (int t = 0; t < T; ++t) {
-        dg += p[t * 8 + 0];
-        dq -= p[t * 8 + 1];
-        stop += p[t * 8 + 4];
+      if constexpr (!MfmaCfg<NTL, MTL>::ct_own) {  // the per-knot sums, in knot order
+        const double* p = D.part + D.knot(b, 0) * 8;
+        const int T = D.T;
+        double dg = 0., dq = 0., stop = 0.;
         if (!feas) {
-          dg -= p[t * 8 + 2];
-          dq += p[t * 8 + 3];
+          dg -= p[T * 8 + 2];
+          dq += p[T * 8 + 3];
         }
+        for (int t = 0; t < T; ++t) {
+          dg += p[t * 8 + 0];
+          dq -= p[t * 8 + 1];
+          stop += p[t * 8 + 4];
+          if (!feas) {
+            dg -= p[t * 8 + 2];
+            dq += p[t * 8 + 3];
+          }
+        }
+        ei[0] = dg;
+        ei[1] = dq;
+        ei[2] = stop;
       }
-      st->dg = dg;
-      st->dq = dq;
-      st->stop = stop;
+      st->dg = ei[0];
+      st->dq = ei[1];
+      st->stop = ei[2];
     }
   }
 }

@@ -63,9 +63,9 @@ hipError_t forward(int v, dim3 grid, size_t smem, hipStream_t s, const Dev& D, c
   if (v == FWD_MB) return forward_1(grid, smem, s, D, prm, mode, alpha, count, pcap, group);
   return forward_0(v, grid, smem, s, D, prm, mode, alpha, count, pcap, group);
 }
-int backward_mfma_setup(int ntl, int mtl, int nw, int n) {
-  const int v = backward_mfma_setup_0(ntl, mtl, nw, n);
-  return v != -2 ? v : backward_mfma_setup_1(ntl, mtl, nw, n);
+int backward_mfma_setup(int ntl, int mtl, int nw, int n, int* per_cu) {
+  const int v = backward_mfma_setup_0(ntl, mtl, nw, n, per_cu);
+  return v != -2 ? v : backward_mfma_setup_1(ntl, mtl, nw, n, per_cu);
 }
 hipError_t backward_mfma(int code, dim3 grid, hipStream_t s, const Dev& D, const Prm& prm, int mode) {
   return code == 528 ? backward_mfma_0(code, grid, s, D, prm, mode) : backward_mfma_1(code, grid, s, D, prm, mode);
@@ -957,8 +957,13 @@ int apply_knots(fddp_handle* h, const fddp_knot_desc* knots, const double* param
     const int ntl = (d.ndx + 15) / 16, mtl = (d.nu_max + 15) / 16;
     int v = -1;
     if (uniform_nu && !force_generic) {
-      // eight waves per element (measured round 4: one wave (C3) or four (C2) per element
-      // are slower, 12.1 / 1.06 ms against 3.6 / 0.89 ms); FDDP_BWD_WAVES=1|4 overrides
+      // eight waves per element, the fastest knot (measured round 4: one wave (C3) or four
+      // (C2) per element are slower, 12.1 / 1.06 ms against 3.6 / 0.89 ms), unless the
+      // four-wave plan keeps more elements resident: the sweep is a serial chain per
+      // element, so its time goes with the rounds of resident workgroups, ceil(B / slots),
+      // and a four-wave knot takes ~1.15x an eight-wave one (C3, B = 512 on 256 CUs: two
+      // four-wave workgroups per CU, one round, 3.20 -> 2.16 ms; C4 and C2 keep eight).
+      // FDDP_BWD_WAVES=1|4|8 overrides.
       const char* ew = std::getenv("FDDP_BWD_WAVES");
       int nw = 8;
       if (ew) nw = ew[0] == '1' ? 1 : (ew[0] == '4' ? 4 : 8);
@@ -968,8 +973,19 @@ int apply_knots(fddp_handle* h, const fddp_knot_desc* knots, const double* param
       const bool known = (ntl == 5 && mtl == 2) || (mtl == 1 && ntl >= 1 && ntl <= 3);
       if (known) {
         if (nw == 1 && !(ntl + mtl <= 4 && mtl == 1)) nw = 8;
-        v = ktab::backward_mfma_setup(ntl, mtl, nw, d.ndx);
-        if (v < 0 && nw == 4) v = ktab::backward_mfma_setup(ntl, mtl, 8, d.ndx);
+        int occ = 0;
+        v = ktab::backward_mfma_setup(ntl, mtl, nw, d.ndx, &occ);
+        if (v < 0 && nw == 4) v = ktab::backward_mfma_setup(ntl, mtl, 8, d.ndx, &occ);
+        if (!ew && v > 0 && mtl == 1) {
+          int cus = 0, occ4 = 0;
+          (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device);
+          const int v4 = ktab::backward_mfma_setup(ntl, mtl, 4, d.ndx, &occ4);
+          if (v4 > 0 && cus > 0 && occ > 0 && occ4 > 0) {
+            const int64_t r8 = (d.B + (int64_t)cus * occ - 1) / ((int64_t)cus * occ);
+            const int64_t r4 = (d.B + (int64_t)cus * occ4 - 1) / ((int64_t)cus * occ4);
+            if (1.2 * (double)r4 < (double)r8) v = v4;
+          }
+        }
       }
     }
     h->bwd_variant = v > 0 ? v : 0;

@@ -14,13 +14,14 @@ namespace ktab {
 
 namespace {
 template <int NTL, int MTL, int NW>
-int setup_one(int n) {
+int setup_one(int n, int* per_cu) {
   using Cfg = MfmaCfg<NTL, MTL>;
   const size_t lds = Cfg::bytes;
   if (lds > 160 * 1024 || n > Cfg::ZLD) return -1;
-  if (hipFuncSetAttribute((const void*)backward_mfma_kernel<NTL, MTL, NW>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)lds) != hipSuccess)
-    return -1;
+  const void* f = (const void*)backward_mfma_kernel<NTL, MTL, NW>;
+  if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return -1;
+  // resident workgroups per CU (registers and LDS): the plan choice weighs it
+  if (per_cu && hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, f, NW * 64, lds) != hipSuccess) *per_cu = 1;
   // column-block ownership per wave is static (BwdPlan in bwd_mfma.hpp)
   return (NTL * 10 + MTL) * 10 + NW;
 }
@@ -31,8 +32,8 @@ void launch_one(dim3 grid, hipStream_t s, const Dev& D, const Prm& prm, int mode
 }  // namespace
 
 #if FDDP_TU_BWD == 0
-int backward_mfma_setup_0(int ntl, int mtl, int nw, int n) {
-  return (ntl == 5 && mtl == 2 && nw == 8) ? setup_one<5, 2, 8>(n) : -2;
+int backward_mfma_setup_0(int ntl, int mtl, int nw, int n, int* per_cu) {
+  return (ntl == 5 && mtl == 2 && nw == 8) ? setup_one<5, 2, 8>(n, per_cu) : -2;
 }
 hipError_t backward_mfma_0(int code, dim3 grid, hipStream_t s, const Dev& D, const Prm& prm, int mode) {
   if (code != 528) return hipErrorInvalidDeviceFunction;
@@ -40,9 +41,9 @@ hipError_t backward_mfma_0(int code, dim3 grid, hipStream_t s, const Dev& D, con
   return hipGetLastError();
 }
 #else
-int backward_mfma_setup_1(int ntl, int mtl, int nw, int n) {  // -1: no such variant or it does not fit
+int backward_mfma_setup_1(int ntl, int mtl, int nw, int n, int* per_cu) {  // -1: no such variant or it does not fit
 #define FDDP_BWD_CASE(A, B, W) \
-  if (ntl == A && mtl == B && nw == W) return setup_one<A, B, W>(n);
+  if (ntl == A && mtl == B && nw == W) return setup_one<A, B, W>(n, per_cu);
   FDDP_BWD_CASE(3, 1, 8) FDDP_BWD_CASE(3, 1, 4) FDDP_BWD_CASE(3, 1, 1)
   FDDP_BWD_CASE(2, 1, 8) FDDP_BWD_CASE(2, 1, 4) FDDP_BWD_CASE(2, 1, 1)
   FDDP_BWD_CASE(1, 1, 8) FDDP_BWD_CASE(1, 1, 4) FDDP_BWD_CASE(1, 1, 1)

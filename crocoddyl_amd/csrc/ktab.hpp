@@ -36,7 +36,7 @@ hipError_t ls_select(dim3 grid, hipStream_t s, const Dev& D, const Prm& prm, int
 // Riccati sweep (k_bwd.hip). MFMA variants are named (NTL*10+MTL)*10+NW (n, m in
 // 16-tiles, waves per element). backward_mfma_setup: the variant for (NTL, MTL, NW)
 // with its dynamic LDS set, or -1 if the shape does not fit (n > its padded width, LDS).
-int backward_mfma_setup(int ntl, int mtl, int nw, int n);
+int backward_mfma_setup(int ntl, int mtl, int nw, int n, int* per_cu = nullptr);
 hipError_t backward_mfma(int code, dim3 grid, hipStream_t s, const Dev& D, const Prm& prm, int mode);
 const void* backward_generic_fn();
 hipError_t backward_generic(dim3 grid, size_t smem, hipStream_t s, const Dev& D, const Prm& prm, int mode);
@@ -79,8 +79,8 @@ hipError_t forward_0(int v, dim3 grid, size_t smem, hipStream_t s, const Dev& D,
 const void* forward_fn_1();
 hipError_t forward_1(dim3 grid, size_t smem, hipStream_t s, const Dev& D, const Prm& prm, int mode, double alpha,
                      int* count, int64_t pcap, int group);
-int backward_mfma_setup_0(int ntl, int mtl, int nw, int n);  // -2: not in this object
-int backward_mfma_setup_1(int ntl, int mtl, int nw, int n);
+int backward_mfma_setup_0(int ntl, int mtl, int nw, int n, int* per_cu);  // -2: not in this object
+int backward_mfma_setup_1(int ntl, int mtl, int nw, int n, int* per_cu);
 hipError_t backward_mfma_0(int code, dim3 grid, hipStream_t s, const Dev& D, const Prm& prm, int mode);
 hipError_t backward_mfma_1(int code, dim3 grid, hipStream_t s, const Dev& D, const Prm& prm, int mode);
 }  // namespace ktab
