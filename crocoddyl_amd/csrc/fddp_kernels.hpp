@@ -314,7 +314,10 @@ __global__ __launch_bounds__(mb::kMbDiffNT) __attribute__((amdgpu_waves_per_eu(1
 // phases leave most lanes of four waves idle: four workgroups per CU under the same
 // register budget.
 #if defined(FDDP_TU_MB) && FDDP_TU_MB == 2
-__global__ __launch_bounds__(mb::kMbDiffNT / 2) __attribute__((amdgpu_waves_per_eu(2))) void mb_knot_kernel_x2(Dev D, int sel_calc, int sel_diff) {
+#ifndef FDDP_X2_WPE
+#define FDDP_X2_WPE 3
+#endif
+__global__ __launch_bounds__(mb::kMbDiffNT / 2) __attribute__((amdgpu_waves_per_eu(FDDP_X2_WPE))) void mb_knot_kernel_x2(Dev D, int sel_calc, int sel_diff) {
   mb_knot_body<mb::kMbDiffNT / 2>(D, sel_calc, sel_diff);
 }
 #endif
