@@ -341,6 +341,7 @@ struct fddp_handle_s {
   int npar_env = 0;    // CROCODDYL_AMD_LS_PAR (0: chosen per problem)
   int npar_alloc = 1;  // trial slots allocated for the parallel line search
   bool npar_adapt = false;  // trial-group size re-chosen after every solve (choose_npar)
+  bool npar_chosen = false;  // choose_npar has set D.npar
   double ls_slots = 0.;     // rollout workgroups resident on the device at once
   hipStream_t stream = nullptr;
   std::vector<fddp_knot_desc> knots;
@@ -626,6 +627,8 @@ static void choose_npar(fddp_handle* h, const std::vector<ElemState>& st) {
     t.push_back(k);
   }
   if (t.empty()) return;
+  // (in whole rounds of resident workgroups: a launch with one workgroup more than the
+  // slots takes two trial-times)
   const double S = h->ls_slots;
   double best = 0.;
   int best_g = 1;
@@ -635,18 +638,19 @@ static void choose_npar(fddp_handle* h, const std::vector<ElemState>& st) {
       double w = 0.;
       int tmax = 0;
       for (int v : t) w += v, tmax = std::max(tmax, v);
-      time = std::max(w / S, (double)tmax);
+      time = std::max(std::ceil(w / S), (double)tmax);
     } else {
       for (int k0 = 0; k0 < na; k0 += g) {
         const int slots = std::min(g, na - k0);
         double u = 0.;
         for (int v : t) u += v > k0 ? slots : 0;
-        if (u > 0.) time += std::max(u / S, 1.);
+        if (u > 0.) time += std::ceil(u / S);
       }
     }
     if (g == 1 || time < best) best = time, best_g = g;
   }
   h->D.npar = best_g;
+  h->npar_chosen = true;
 }
 
 // Longest-processing-time-first dispatch of the next line search: the rollout's
@@ -844,7 +848,11 @@ int apply_knots(fddp_handle* h, const fddp_knot_desc* knots, const double* param
     // parallel line-search trials: they pay on the large trees (C5 Talos, nv = 38:
     // forward -12 %), where one rollout keeps a CU busy longest; on small ones (C4
     // Solo12, nv = 18) the extra trials cost more than the shorter chains save
-    D.npar = h->npar_env ? h->npar_env : (h->has_mb && mb_nj >= 24 ? 4 : 1);
+    // (a re-application of the knots — fddp_set_knots, the MPC loop's circularAppend —
+    // keeps the size chosen from the last line search's trial counts: resetting it every
+    // step cost the C5 shift protocol's rollout 52.3 -> 65.8 ms)
+    if (!(h->npar_chosen && h->has_mb && !h->npar_env))
+      D.npar = h->npar_env ? h->npar_env : (h->has_mb && mb_nj >= 24 ? 4 : 1);
     h->npar_adapt = !h->npar_env && h->has_mb;
     int64_t mb_pmax = 0;  // largest multibody parameter block (staged in LDS by mb_knot_kernel)
     for (int t = 0; t <= d.T; ++t)
