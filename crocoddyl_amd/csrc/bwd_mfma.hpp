@@ -1533,8 +1533,21 @@ __device__ __forceinline__ bool bwd_sweep_mfma(const Dev& D, int b, bool feas, d
   return true;
 }
 
+// LDS bytes of a plan: the prefetch plan's second buffers only where the plan uses them
+// (a four-wave plan with every wave owning blocks keeps the smaller carve, so two of its
+// workgroups fit a CU)
 template <int NTL, int MTL, int NW>
-__global__ __launch_bounds__(NW * 64) void backward_mfma_kernel(Dev D, Prm prm, int mode) {
+constexpr size_t bwd_lds_bytes() {
+  using Cfg = MfmaCfg<NTL, MTL>;
+  return BwdPlan<NTL, MTL, NW>{}.prefetch ? Cfg::bytes
+                                          : sizeof(double) * (Cfg::ct_own ? Cfg::total0 + Cfg::MP * Cfg::LDT : Cfg::total0);
+}
+
+// (the four-wave plans at two waves per SIMD: two workgroups per CU, which is what the
+// residency-based plan choice counts on)
+template <int NTL, int MTL, int NW>
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 4 ? 2 : 1))) void backward_mfma_kernel(
+    Dev D, Prm prm, int mode) {
   const int b = blockIdx.x;
   ElemState* st = D.st + b;
   if (mode == 0 && !st->active) return;

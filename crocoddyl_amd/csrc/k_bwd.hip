@@ -16,7 +16,7 @@ namespace {
 template <int NTL, int MTL, int NW>
 int setup_one(int n, int* per_cu) {
   using Cfg = MfmaCfg<NTL, MTL>;
-  const size_t lds = Cfg::bytes;
+  const size_t lds = bwd_lds_bytes<NTL, MTL, NW>();
   if (lds > 160 * 1024 || n > Cfg::ZLD) return -1;
   const void* f = (const void*)backward_mfma_kernel<NTL, MTL, NW>;
   if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return -1;
@@ -27,7 +27,7 @@ int setup_one(int n, int* per_cu) {
 }
 template <int NTL, int MTL, int NW>
 void launch_one(dim3 grid, hipStream_t s, const Dev& D, const Prm& prm, int mode) {
-  backward_mfma_kernel<NTL, MTL, NW><<<grid, dim3(NW * 64), MfmaCfg<NTL, MTL>::bytes, s>>>(D, prm, mode);
+  backward_mfma_kernel<NTL, MTL, NW><<<grid, dim3(NW * 64), bwd_lds_bytes<NTL, MTL, NW>(), s>>>(D, prm, mode);
 }
 }  // namespace
 
