@@ -500,6 +500,9 @@ def main():
     ap.add_argument("--secondary-steps", type=int, default=5,
                     help="steps of the other protocol, reported beside the headline (1 GPU only; 0: off)")
     ap.add_argument("--launch-selftest", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--rehearsal", action="store_true",
+                    help="allow more ranks than GPUs (ranks share devices, gloo collectives): a rehearsal of the "
+                         "N-GPU job, marked as such in the JSON line, n_gpus = the distinct devices used")
     args = ap.parse_args()
     box = args.solver == "boxfddp"
     if args.protocol is None:
@@ -521,6 +524,10 @@ def main():
     # job) ranks share devices and the collectives run on gloo (RCCL refuses two ranks
     # on one device)
     ndev = torch.cuda.device_count()
+    if ndev < ws and not args.rehearsal:
+        sys.stderr.write(f"bench.py: {ws} ranks but {ndev} GPU(s): one rank per GPU is required (pass --rehearsal "
+                         "to run the ranks on shared devices, reported as a rehearsal)\n")
+        sys.exit(2)
     dev = local_rank % max(ndev, 1)
     backend = os.environ.get("CROCODDYL_AMD_DIST_BACKEND") or ("nccl" if ndev >= ws else "gloo")
     cdist.init(backend, dev)
@@ -711,7 +718,7 @@ def main():
             except Exception as e:  # reported, never fatal for the GPU number
                 cpu = {"error": repr(e)}
         out = {
-            "metric": METRIC, "value": round(value, 2), "unit": "FDDP iterations/s", "n_gpus": ws,
+            "metric": METRIC, "value": round(value, 2), "unit": "FDDP iterations/s", "n_gpus": min(ws, max(ndev, 1)),
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
             "data": ("synthetic: the reference's Talos walking gait (utils/biped.py createWalkingProblem: 6D foot "
@@ -761,6 +768,10 @@ def main():
         }
         if cpu and "value" in cpu:
             out["speedup_vs_cpu"] = round(value / cpu["value"], 2)
+        if ndev < ws:  # (--rehearsal) not an N-GPU measurement
+            out["rehearsal"] = {"ranks": ws, "physical_gpus": ndev,
+                                "note": "ranks share GPUs (gloo collectives): a rehearsal of the sharded job, "
+                                        "not a multi-GPU throughput"}
         print(json.dumps(out), flush=True)
     if ws > 1:
         torch.distributed.destroy_process_group()

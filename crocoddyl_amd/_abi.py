@@ -6,6 +6,8 @@ which exports the same functions with an ``oracle_`` prefix.
 """
 import ctypes as C
 
+ABI_VERSION = 3  # FDDP_ABI_VERSION of include/fddp_hip.h this binding was written against
+
 FDDP_OK = 0
 FDDP_ERR_INVALID_ARG = -1
 FDDP_ERR_RUNTIME = -2
@@ -53,6 +55,23 @@ class Result(C.Structure):
                 ("d1", C.c_double)]
 
 
+# numpy view of a (Result * B) array: the per-element fields as arrays without a Python loop
+RESULT_DTYPE = None
+
+
+def result_array(r):
+    """Structured numpy view of a ctypes (Result * B) array (no copy)."""
+    global RESULT_DTYPE
+    if RESULT_DTYPE is None:
+        import numpy as np
+        RESULT_DTYPE = np.dtype({"names": [f for f, _ in Result._fields_],
+                                 "formats": ["<i4" if t is C.c_int32 else "<f8" for _, t in Result._fields_],
+                                 "offsets": [getattr(Result, f).offset for f, _ in Result._fields_],
+                                 "itemsize": C.sizeof(Result)})
+    import numpy as np
+    return np.frombuffer(r, dtype=RESULT_DTYPE)
+
+
 P = C.c_void_p
 D = C.POINTER(C.c_double)
 I32 = C.POINTER(C.c_int32)
@@ -74,6 +93,9 @@ PROTOS = {
     "problem_calc": (C.c_int, [P, D]),
     "problem_calc_diff": (C.c_int, [P, D]),
     "compute_direction": (C.c_int, [P, C.c_int, I32]),
+    "calc_diff": (C.c_int, [P, D]),
+    "backward_pass": (C.c_int, [P, I32]),
+    "forward_pass": (C.c_int, [P, C.c_double, D, I32]),
     "update_expected_improvement": (C.c_int, [P]),
     "try_step": (C.c_int, [P, C.c_double, D, I32]),
     "expected_improvement": (C.c_int, [P, D]),
@@ -88,6 +110,7 @@ PROTOS = {
 
 # product-only entry points (libfddp_hip)
 PROTOS_GPU = {
+    "abi_version": (C.c_int, []),
     "create": (C.c_int, [C.POINTER(Dims), C.POINTER(KnotDesc), D, C.c_int64, C.c_int, C.POINTER(P)]),
     "set_model_params": (C.c_int, [P, D, C.c_int64]),
     "set_candidate_device": (C.c_int, [P, D, D, C.c_int]),

@@ -45,6 +45,10 @@ def lib():
         L = C.CDLL(LIB_PATH)
         _abi.bind(L, "fddp_", _abi.PROTOS)
         _abi.bind(L, "fddp_", _abi.PROTOS_GPU)
+        v = L.fddp_abi_version()
+        if v != _abi.ABI_VERSION:
+            raise ImportError(f"crocoddyl_amd: {LIB_PATH} has C ABI version {v}, this binding needs "
+                              f"{_abi.ABI_VERSION} (rebuild it)")
         _lib = L
     return _lib
 

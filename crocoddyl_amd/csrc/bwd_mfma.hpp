@@ -48,7 +48,6 @@
 namespace fddp {
 
 typedef double f64x4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) void* lds_void_ptr;
 
 // 1/d from v_rcp_f64 and Newton steps (the IEEE division sequence is ~3x
 // longer on the sweep's critical path; dependent f64 FMA latency is 32 cycles)
@@ -67,28 +66,6 @@ __device__ __forceinline__ f64x4 mfma4(double a, double b, f64x4 c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
 
-// Barrier that waits only for this wave's LDS traffic: an LDS-DMA in flight
-// stays in flight across it (a __syncthreads() would add vmcnt(0)).
-__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-// Barrier after which every LDS-DMA issued by the workgroup has landed.
-__device__ __forceinline__ void dma_barrier() {
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-}
-
-// Asynchronous copy global -> LDS by LDS-DMA (global_load_lds: the LDS
-// destination of one wave instruction is a wave-uniform base + lane * size).
-// dma_vec: nd contiguous doubles (16-B aligned both sides) over the 4 waves;
-// an odd tail double moves as two 4-byte DMAs.
-template <int NW>  // NW participating waves, wid = this wave's rank among them
-__device__ __forceinline__ void dma_vec(double* lds, const double* g, int nd, int wid, int lane) {
-  const int nch = nd >> 1;
-  for (int base = wid * 64; base < nch; base += NW * 64) {
-    const int ch = base + lane;
-    if (ch < nch) __builtin_amdgcn_global_load_lds(g + 2 * ch, (lds_void_ptr)(lds + 2 * base), 16, 0, 0);
-  }
-  if ((nd & 1) && wid == NW - 1 && lane < 2)
-    __builtin_amdgcn_global_load_lds((const char*)(g + nd - 1) + 4 * lane, (lds_void_ptr)(lds + nd - 1), 4, 0, 0);
-}
 // dma_cols: ncols columns of nr doubles (global ld nr) into LDS columns of
 // stride ld (a multiple of 2); one column per wave instruction (16-B chunks
 // when nr is even, else 4-byte pieces). Rows [nr, ld) are left untouched.
@@ -1556,6 +1533,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 4
   double xreg = st->xreg, ureg = st->ureg;
   bool ok;
   int tries = 0;
+  const int max_tries = reg_retry_bound(prm, xreg);
   double ei[3];  // dg, dq, stop (thread 0)
   for (;;) {
     ok = bwd_sweep_mfma<NTL, MTL, NW>(D, b, feas, xreg, ureg, st->cur, sm, ei);
@@ -1564,9 +1542,9 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 4
     xreg *= prm.regfactor;  // increaseRegularization (ddp.cpp:312-318)
     if (xreg > prm.regmax) xreg = prm.regmax;
     ureg = xreg;
-    // (as the reference: at regmax; also on a NaN xreg or a regfactor <= 1, which would
-    // never reach it: every wave of the workgroup must leave the loop)
-    if (!(xreg < prm.regmax) || ++tries >= kMaxRegRetries) break;
+    // (as the reference: at regmax; a NaN / zero xreg never reaches it: the bound
+    // reg_retry_bound makes every wave of the workgroup leave the loop)
+    if (!(xreg < prm.regmax) || ++tries >= max_tries) break;
   }
   if (threadIdx.x == 0) {
     st->xreg = xreg;

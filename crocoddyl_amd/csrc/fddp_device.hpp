@@ -40,9 +40,6 @@ struct ElemState {
 
 static_assert(sizeof(ElemState) % 8 == 0, "ElemState alignment");
 
-// Bound on the backward kernels' regularisation retries within one sweep (the
-// reference's loop ends at regmax: 1e-9 * 10^k reaches the default 1e9 in 18 steps).
-constexpr int kMaxRegRetries = 64;
 
 __host__ __device__ inline int64_t pad2(int64_t v) { return (v + 1) & ~int64_t(1); }
 
@@ -75,6 +72,30 @@ __device__ __forceinline__ void lds_wait_ge(int* ctr, int target) {  // before t
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
+typedef __attribute__((address_space(3))) void* lds_void_ptr;
+
+// Barrier that waits only for this wave's LDS traffic: an LDS-DMA in flight
+// stays in flight across it (a __syncthreads() would add vmcnt(0)).
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+// Barrier after which every LDS-DMA issued by the workgroup has landed.
+__device__ __forceinline__ void dma_barrier() {
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// Asynchronous copy global -> LDS by LDS-DMA (global_load_lds: the LDS
+// destination of one wave instruction is a wave-uniform base + lane * size).
+// dma_vec: nd contiguous doubles (16-B aligned both sides) over the 4 waves;
+// an odd tail double moves as two 4-byte DMAs.
+template <int NW>  // NW participating waves, wid = this wave's rank among them
+__device__ __forceinline__ void dma_vec(double* lds, const double* g, int nd, int wid, int lane) {
+  const int nch = nd >> 1;
+  for (int base = wid * 64; base < nch; base += NW * 64) {
+    const int ch = base + lane;
+    if (ch < nch) __builtin_amdgcn_global_load_lds(g + 2 * ch, (lds_void_ptr)(lds + 2 * base), 16, 0, 0);
+  }
+  if ((nd & 1) && wid == NW - 1 && lane < 2)
+    __builtin_amdgcn_global_load_lds((const char*)(g + nd - 1) + 4 * lane, (lds_void_ptr)(lds + nd - 1), 4, 0, 0);
+}
 // ---- register broadcasts within a wave (64 lanes = 4 rows of 16) -------------------
 // lane n of every row of 16 lanes, to the whole row (DPP row_newbcast: a VALU move, no
 // LDS-crossbar round trip as __shfl's ds_bpermute); n a compile-time constant
@@ -192,6 +213,17 @@ struct Prm {
   int n_alphas;
   double alphas[16];
 };
+
+// Bound on the backward kernels' regularisation retries within one sweep. The reference
+// retries until xreg reaches regmax (fddp.cpp:35-47): from a positive xreg that is
+// ceil(log(regmax / xreg) / log(regfactor)) increases (set_regfactor rejects <= 1); two
+// more absorb the rounding of the products. A zero / NaN xreg never reaches regmax (the
+// reference would not stop): one try, then the element stops at regmax.
+__host__ __device__ inline int reg_retry_bound(const Prm& prm, double xreg) {
+  if (!(xreg > 0.) || !(prm.regfactor > 1.) || !(xreg < prm.regmax)) return 1;
+  const double k = ceil(log(prm.regmax / xreg) / log(prm.regfactor));
+  return k < 1e6 ? (int)k + 2 : 1000000;
+}
 
 // Which batch elements a launch works on (host-side selectors).
 enum Sel { SEL_ACTIVE = 0, SEL_ALL = 1, SEL_ITER0 = 2, SEL_RECALC = 3 };

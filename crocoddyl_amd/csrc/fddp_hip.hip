@@ -1451,6 +1451,43 @@ int fddp_compute_direction(fddp_handle* h, int recalc, int32_t* status) {
   return FDDP_OK;
 }
 
+// SolverDDP::calcDiff (ddp.cpp:157-178): the first half of computeDirection(true)
+int fddp_calc_diff(fddp_handle* h, double* cost) {
+  if (!h) return fail(FDDP_ERR_INVALID_ARG, "fddp_calc_diff: null handle");
+  DeviceGuard g(h->device);
+  int rc;
+  if ((rc = launch_calc_then_diff(h, SEL_ITER0, SEL_ITER0, SEL_ALL, 1))) return rc;
+  if ((rc = launch_cost_sum(h, SEL_ALL, h->d_out))) return rc;
+  if (cost) HIP_TRY(hipMemcpyAsync(cost, h->d_out, sizeof(double) * h->dims.B, hipMemcpyDeviceToHost, h->stream));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  return FDDP_OK;
+}
+
+// SolverDDP::backwardPass (ddp.cpp:180-253): the second half of computeDirection
+int fddp_backward_pass(fddp_handle* h, int32_t* status) {
+  if (!h) return fail(FDDP_ERR_INVALID_ARG, "fddp_backward_pass: null handle");
+  return fddp_compute_direction(h, 0, status);
+}
+
+// SolverFDDP::forwardPass (fddp.cpp:149-225): tryStep without the cost difference
+int fddp_forward_pass(fddp_handle* h, double step_length, double* cost_try, int32_t* status) {
+  if (!h) return fail(FDDP_ERR_INVALID_ARG, "fddp_forward_pass: null handle");
+  if (step_length > 1. || step_length < 0.)
+    return fail(FDDP_ERR_INVALID_ARG, "invalid step length, value is between 0. to 1.");  // fddp.cpp:150-153
+  DeviceGuard g(h->device);
+  int rc;
+  if ((rc = launch_forward(h, 1, step_length, nullptr))) return rc;
+  std::vector<ElemState> st;
+  if ((rc = download_states(h, st))) return rc;
+  for (int b = 0; b < h->dims.B; ++b) {
+    if (cost_try) cost_try[b] = st[b].cost_try;
+    if (status) status[b] = st[b].fwd_fail;
+  }
+  return FDDP_OK;
+}
+
+int fddp_abi_version(void) { return FDDP_ABI_VERSION; }
+
 int fddp_update_expected_improvement(fddp_handle* h) {
   // dg/dq are reduced inside the backward kernel (same terms, same order).
   if (!h) return fail(FDDP_ERR_INVALID_ARG, "null handle");

@@ -645,6 +645,7 @@ __global__ __launch_bounds__(NT) void backward_kernel(Dev D, Prm prm, int mode) 
   double xreg = st->xreg, ureg = st->ureg;
   bool ok;
   int tries = 0;
+  const int max_tries = reg_retry_bound(prm, xreg);
   for (;;) {
     if (threadIdx.x == 0) *S.flag = 0;
     __syncthreads();
@@ -655,9 +656,9 @@ __global__ __launch_bounds__(NT) void backward_kernel(Dev D, Prm prm, int mode) 
     xreg *= prm.regfactor;
     if (xreg > prm.regmax) xreg = prm.regmax;
     ureg = xreg;
-    // (as the reference: at regmax; also on a NaN xreg or a regfactor <= 1, which would
-    // never reach it: every wave of the workgroup must leave the loop)
-    if (!(xreg < prm.regmax) || ++tries >= kMaxRegRetries) break;
+    // (as the reference: at regmax; a NaN / zero xreg never reaches it: the bound
+    // reg_retry_bound makes every wave of the workgroup leave the loop)
+    if (!(xreg < prm.regmax) || ++tries >= max_tries) break;
   }
   if (threadIdx.x == 0) {
     st->xreg = xreg;
@@ -738,7 +739,7 @@ __device__ __forceinline__ double gains_dot(const double* K, int m, int i, int n
       d[q] = dx(j + q);
     }
 #pragma unroll
-    for (int q = 0; q < 8; ++q) s += k[q] * d[q];
+    for (int q = 0; q < 8; ++q) s = fma(k[q], d[q], s);
   }
   if (j < n) {  // the tail as one guarded batch
     double k[8], d[8];
@@ -749,7 +750,7 @@ __device__ __forceinline__ double gains_dot(const double* K, int m, int i, int n
     }
 #pragma unroll
     for (int q = 0; q < 8; ++q)
-      if (j + q < n) s += k[q] * d[q];
+      if (j + q < n) s = fma(k[q], d[q], s);
   }
   return s;
 }
@@ -807,27 +808,34 @@ __device__ __forceinline__ bool fwd_trial(const Dev& D, int b, const ElemState& 
       const double* K = D.K + D.run(b, t) * D.sNM;
       const double* kv = D.k + D.run(b, t) * D.sM;
       // us_try = us - k * alpha - K * dx ,  dx = diff(xs, xs_try)
-      // K (HBM) is read by the whole workgroup: control i's dot product split into np
-      // contiguous j-ranges of one load batch each (np = NT / m), their partials (in the
-      // knot calc's LDS scratch, free between knots) summed in range order by lane i: one
-      // round trip to HBM instead of one per 8 entries of a 32-lane chain
-      const int np = m > 0 && m <= NT ? (NT / m < 8 ? NT / m : 8) : 1;
-      if (np > 1 && D.mbw >= (int64_t)np * m) {
-        const int i = tid % m, pp = tid / m, len = (n + np - 1) / np, j0 = pp * len;
-        double ps = 0.;
-        if (pp < np && i < nu) {
-          const int j1 = j0 + len < n ? j0 + len : n;
-          ps = ff ? gains_dot(K + (int64_t)j0 * m, m, i, j1 - j0, [&](int j) { return dxv[j0 + j]; })
-                  : gains_dot(K + (int64_t)j0 * m, m, i, j1 - j0, [&](int j) { return xv[j0 + j] - xs[j0 + j]; });
-        }
-        if (pp < np) mbw[pp * m + i] = ps;
-        __syncthreads();
+      // K (HBM) moves into the knot calc's LDS scratch (free between knots) by LDS-DMA
+      // issued by the whole workgroup: one round trip to HBM, no registers. Control i's
+      // product is then one FMA chain in j order on lane i, the summation order of the
+      // reference's GEMV row (fddp.cpp:199) and of the oracle (gain_row_dot), so us_try
+      // rounds as theirs. (Round 5 split the row into 8 partial sums over the workgroup:
+      // the reordered sums moved the C5 smoke's xs after 3 iterations 2.4e-8 -> 3.8e-8.)
+      if (m <= NT && D.mbw >= (int64_t)m * n) {
+        if (!ff)
+          for (int j = tid; j < n; j += NT) dxv[j] = xv[j] - xs[j];
+        dma_vec<NT / kWave>(mbw, K, m * n, tid / kWave, tid & (kWave - 1));
+        dma_barrier();
         if (tid < m) {
           double v = 0.;
           if (tid < nu) {
+            const double* Kl = lds_ptr(mbw) + tid;
+            const double* dl = lds_ptr(dxv);
             double kd2 = 0.;
-            for (int q = 0; q < np; ++q) kd2 += mbw[q * m + tid];
-            v = (us[tid] - kv[tid] * alpha) - kd2;
+            int j = 0;
+#pragma unroll 1
+            for (; j + 8 <= n; j += 8) {  // 8 LDS loads in flight, then their chain
+              double kq[8], dq[8];
+#pragma unroll
+              for (int q = 0; q < 8; ++q) kq[q] = Kl[(j + q) * m], dq[q] = dl[j + q];
+#pragma unroll
+              for (int q = 0; q < 8; ++q) kd2 = fma(kq[q], dq[q], kd2);
+            }
+            for (; j < n; ++j) kd2 = fma(Kl[j * m], dl[j], kd2);
+            v = fma(-kv[tid], alpha, us[tid]) - kd2;
             // SolverBoxFDDP::forwardPass: cwiseMax(u_lb).cwiseMin(u_ub) (box-fddp.cpp:100-102)
             if (D.box_knot(b, t))
               v = std_min(std_max(v, D.ulb[D.run(b, t) * D.sM + tid]), D.uub[D.run(b, t) * D.sM + tid]);
@@ -840,7 +848,7 @@ __device__ __forceinline__ bool fwd_trial(const Dev& D, int b, const ElemState& 
           if (i < nu) {
             const double kd2 = ff ? gains_dot(K, m, i, n, [&](int j) { return dxv[j]; })
                                   : gains_dot(K, m, i, n, [&](int j) { return xv[j] - xs[j]; });
-            v = (us[i] - kv[i] * alpha) - kd2;
+            v = fma(-kv[i], alpha, us[i]) - kd2;
             if (D.box_knot(b, t)) v = std_min(std_max(v, D.ulb[D.run(b, t) * D.sM + i]), D.uub[D.run(b, t) * D.sM + i]);
           }
           uv[i] = v;

@@ -477,8 +477,7 @@ class SolverFDDP:
         return self._results
 
     def _field(self, name, conv=float):
-        r = self._res()
-        arr = np.array([conv(getattr(x, name)) for x in r])
+        arr = _abi.result_array(self._res())[name].astype(conv)
         return arr if self.problem.batched else arr[0]
 
     # -- SolverAbstract::setCandidate / solve --------------------------------
@@ -505,10 +504,10 @@ class SolverFDDP:
 
     def solve_from_candidate(self, maxiter=100, isFeasible=False, regInit=1e-9):
         """solve() without re-uploading a warm start (device-resident MPC loops)."""
-        self._push_params()
+        ptr = self._ptr
+        check(lib().fddp_set_params(ptr, C.byref(self._prm)))
         reg = float("nan") if regInit is None else float(regInit)
         r = (_abi.Result * self.problem.B)()
-        ptr = self._ptr
         if self.callbacks:
             # every callback once per iteration of the loop (fddp.cpp:92-98), with the
             # solver's getters reading that iteration's state
@@ -547,7 +546,7 @@ class SolverFDDP:
         else:
             check(lib().fddp_solve(ptr, int(maxiter), 1 if isFeasible else 0, reg, r))
         self._results = r
-        ok = np.array([x.status == _abi.STATUS_CONVERGED for x in r])
+        ok = _abi.result_array(r)["status"] == _abi.STATUS_CONVERGED
         return ok if self.problem.batched else bool(ok[0])
 
     def setCallbacks(self, callbacks):
@@ -571,6 +570,58 @@ class SolverFDDP:
         if not self.problem.batched and st[0]:
             raise FDDPError("backward_error")
         return st.astype(bool) if self.problem.batched else None
+
+    def calcDiff(self):
+        """SolverDDP::calcDiff (ddp.cpp:157-178): problem.calc at iter 0, problem.calcDiff,
+        the gaps. Returns the cost (an array when batched)."""
+        c = np.zeros(self.problem.B)
+        check(lib().fddp_calc_diff(self._ptr, _abi.dptr(c)))
+        self._results = None
+        return self._scalar(c)
+
+    def backwardPass(self):
+        """SolverDDP::backwardPass (ddp.cpp:180-253) on the last calcDiff's derivatives.
+        Raises on backward_error (single problem); returns the per-element failure flags
+        when batched."""
+        self._push_params()
+        st = np.zeros(self.problem.B, dtype=np.int32)
+        check(lib().fddp_backward_pass(self._ptr, st.ctypes.data_as(_abi.I32)))
+        self._results = None
+        if not self.problem.batched and st[0]:
+            raise FDDPError("backward_error")
+        return st.astype(bool) if self.problem.batched else None
+
+    def forwardPass(self, stepLength=1.0):
+        """SolverFDDP::forwardPass (fddp.cpp:149-225): rolls the policy out into
+        xs_try / us_try (properties xs_try, us_try) and cost_try. Raises on
+        forward_error (single problem); the per-element flags when batched."""
+        ct = np.zeros(self.problem.B)
+        st = np.zeros(self.problem.B, dtype=np.int32)
+        check(lib().fddp_forward_pass(self._ptr, float(stepLength), _abi.dptr(ct), st.ctypes.data_as(_abi.I32)))
+        self._results = None
+        self._cost_try = ct
+        if not self.problem.batched and st[0]:
+            raise FDDPError("forward_error")
+        return st.astype(bool) if self.problem.batched else None
+
+    @property
+    def cost_try(self):
+        """cost_try_ of the last forwardPass / tryStep."""
+        return self._scalar(self._cost_try) if getattr(self, "_cost_try", None) is not None else None
+
+    @property
+    def xs_try(self):
+        p = self.problem
+        a = np.zeros((p.B, p.T + 1, p.nx))
+        check(lib().fddp_get_xs_try(self._ptr, _abi.dptr(a)))
+        return p._out_x(a)
+
+    @property
+    def us_try(self):
+        p = self.problem
+        a = np.zeros((p.B, p.T, p.nu_max))
+        check(lib().fddp_get_us_try(self._ptr, _abi.dptr(a)))
+        return p._out_u(a)
 
     def tryStep(self, stepLength=1.0):
         """ddp.cpp:127-130; returns cost - cost_try."""
@@ -682,8 +733,8 @@ class SolverFDDP:
 
     @property
     def d(self):
-        r = self._res()
-        a = np.array([[x.d0, x.d1] for x in r])
+        r = _abi.result_array(self._res())
+        a = np.stack([r["d0"], r["d1"]], axis=1)
         return a if self.problem.batched else a[0]
 
     # thresholds with the reference setter validation (via fddp_set_params)

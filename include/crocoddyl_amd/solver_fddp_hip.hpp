@@ -21,6 +21,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <exception>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -276,6 +277,9 @@ class SolverFDDP {
     d.B = problem->get_B();
     dims_ = d;
     fddp_handle* h = nullptr;
+    if (fddp_abi_version() != FDDP_ABI_VERSION)
+      throw Exception("libfddp_hip C ABI version " + std::to_string(fddp_abi_version()) + ", this header is " +
+                      std::to_string(FDDP_ABI_VERSION));
     check(fddp_create(&d, knots.data(), pool.data(), (int64_t)pool.size(), device, &h), "fddp_create");
     h_.reset(h, fddp_destroy);
     fddp_default_params(&params_);
@@ -296,15 +300,106 @@ class SolverFDDP {
     check(fddp_set_params(h_.get(), &params_), "fddp_set_params");
     check(fddp_set_callback(h_.get(), callbacks_.empty() ? nullptr : &SolverFDDP::on_iteration, this),
           "fddp_set_callback");
-    cb_error_.clear();
+    cb_error_ = nullptr;
     const int rc = fddp_solve(h_.get(), (int)maxiter, is_feasible ? 1 : 0, reginit, res_.data());
     fddp_set_callback(h_.get(), nullptr, nullptr);
     reported_.clear();
     // a callback that threw stopped the solve after its iteration (fddp.cpp:92-98):
-    // res_ holds that iteration's results
-    if (rc == FDDP_ERR_CALLBACK_ABORT && !cb_error_.empty()) throw Exception("callback: " + cb_error_);
+    // res_ holds that iteration's results, and the callback's exception is rethrown as is
+    if (rc == FDDP_ERR_CALLBACK_ABORT && cb_error_) {
+      std::exception_ptr e = cb_error_;
+      cb_error_ = nullptr;
+      std::rethrow_exception(e);
+    }
     check(rc, "fddp_solve");
     return res_[0].status == FDDP_STATUS_CONVERGED;
+  }
+
+  // ---- the solver's phases one at a time (SolverDDP / SolverFDDP methods) --------------
+  // SolverDDP::calcDiff (ddp.cpp:157-178): problem.calc at iter 0, problem.calcDiff, the
+  // gaps; returns cost_ (element 0; get_costs() every element)
+  double calcDiff() {
+    costs_.assign(dims_.B, 0.);
+    check(fddp_calc_diff(h_.get(), costs_.data()), "fddp_calc_diff");
+    return costs_[0];
+  }
+  // SolverDDP::backwardPass (ddp.cpp:180-253); throws "backward_error" as the reference
+  // (batched: when any element fails; get_step_status() says which)
+  void backwardPass() {
+    check(fddp_set_params(h_.get(), &params_), "fddp_set_params");
+    step_status_.assign(dims_.B, 0);
+    check(fddp_backward_pass(h_.get(), step_status_.data()), "fddp_backward_pass");
+    for (int32_t v : step_status_)
+      if (v) throw Exception("backward_error");
+  }
+  // SolverDDP::computeDirection (ddp.cpp:120-125)
+  void computeDirection(bool recalc = true) {
+    if (recalc) calcDiff();
+    backwardPass();
+  }
+  // SolverFDDP::forwardPass (fddp.cpp:149-225): xs_try / us_try / cost_try; throws
+  // "forward_error" as the reference; stepLength outside [0, 1] is an invalid argument
+  void forwardPass(double steplength) {
+    costs_try_.assign(dims_.B, 0.);
+    step_status_.assign(dims_.B, 0);
+    check(fddp_forward_pass(h_.get(), steplength, costs_try_.data(), step_status_.data()), "fddp_forward_pass");
+    for (int32_t v : step_status_)
+      if (v) throw Exception("forward_error");
+  }
+  // SolverDDP::tryStep (ddp.cpp:127-130): cost_ - cost_try_
+  double tryStep(double steplength = 1.) {
+    std::vector<double> dv(dims_.B, 0.);
+    step_status_.assign(dims_.B, 0);
+    check(fddp_try_step(h_.get(), steplength, dv.data(), step_status_.data()), "fddp_try_step");
+    for (int32_t v : step_status_)
+      if (v) throw Exception("forward_error");
+    return dv[0];
+  }
+  // SolverDDP::stoppingCriteria (ddp.cpp:132-142)
+  double stoppingCriteria() {
+    std::vector<double> s(dims_.B, 0.);
+    check(fddp_stopping_criteria(h_.get(), s.data()), "fddp_stopping_criteria");
+    return s[0];
+  }
+  // SolverFDDP::updateExpectedImprovement / expectedImprovement (fddp.cpp:107-147)
+  void updateExpectedImprovement() { check(fddp_update_expected_improvement(h_.get()), "fddp_update_expected_improvement"); }
+  std::vector<double> expectedImprovement() {
+    std::vector<double> d(2 * (size_t)dims_.B, 0.);
+    check(fddp_expected_improvement(h_.get(), d.data()), "fddp_expected_improvement");
+    return {d[0], d[1]};
+  }
+  double get_cost_try() const { return costs_try_.empty() ? 0. : costs_try_[0]; }
+  const std::vector<double>& get_costs() const { return costs_; }
+  const std::vector<double>& get_costs_try() const { return costs_try_; }
+  const std::vector<int32_t>& get_step_status() const { return step_status_; }
+  // SolverDDP getters (ddp.hpp:60-271), element 0: K_[t] (nu x ndx, column-major), k_[t],
+  // fs_[t]; Vxx / Vx / Q* need set_debug(true) before the backward pass (device stores)
+  std::vector<VectorXd> get_K() const { return quantity(FDDP_Q_K, dims_.T, (size_t)dims_.nu_max * dims_.ndx); }
+  std::vector<VectorXd> get_k() const { return quantity(FDDP_Q_KV, dims_.T, dims_.nu_max); }
+  std::vector<VectorXd> get_fs() const { return quantity(FDDP_Q_FS, dims_.T + 1, dims_.ndx); }
+  std::vector<VectorXd> get_Vxx() const { return quantity(FDDP_Q_VXX, dims_.T + 1, (size_t)dims_.ndx * dims_.ndx); }
+  std::vector<VectorXd> get_Vx() const { return quantity(FDDP_Q_VX, dims_.T + 1, dims_.ndx); }
+  std::vector<VectorXd> get_Quu() const { return quantity(FDDP_Q_QUU, dims_.T, (size_t)dims_.nu_max * dims_.nu_max); }
+  std::vector<VectorXd> get_Qu() const { return quantity(FDDP_Q_QU, dims_.T, dims_.nu_max); }
+  void set_debug(bool on) { check(fddp_set_debug(h_.get(), on ? 1 : 0), "fddp_set_debug"); }
+  std::vector<VectorXd> get_xs_try() const {
+    VectorXd a((size_t)dims_.B * (dims_.T + 1) * dims_.nx);
+    check(fddp_get_xs_try(h_.get(), a.data()), "fddp_get_xs_try");
+    std::vector<VectorXd> out;
+    for (int t = 0; t <= dims_.T; ++t) out.push_back(VectorXd(a.begin() + t * dims_.nx, a.begin() + (t + 1) * dims_.nx));
+    return out;
+  }
+  std::vector<VectorXd> get_us_try() const {
+    VectorXd a((size_t)dims_.B * dims_.T * dims_.nu_max);
+    check(fddp_get_us_try(h_.get(), a.data()), "fddp_get_us_try");
+    std::vector<VectorXd> out;
+    for (int t = 0; t < dims_.T; ++t)
+      out.push_back(VectorXd(a.begin() + t * dims_.nu_max, a.begin() + (t + 1) * dims_.nu_max));
+    return out;
+  }
+  // the solver members the phases read (a fresh solver: iter 0, xreg = ureg = NaN)
+  void set_solver_state(int iter, double xreg, double ureg, bool was_feasible) {
+    check(fddp_set_solver_state(h_.get(), iter, xreg, ureg, was_feasible ? 1 : 0), "fddp_set_solver_state");
   }
 
   // SolverAbstract::setCallbacks / getCallbacks (solver-base.cpp:69-77)
@@ -391,7 +486,18 @@ class SolverFDDP {
   std::vector<fddp_result> res_;
   std::vector<std::shared_ptr<CallbackAbstract> > callbacks_;
   std::vector<int32_t> reported_;
-  std::string cb_error_;
+  std::exception_ptr cb_error_;
+  std::vector<double> costs_, costs_try_;
+  std::vector<int32_t> step_status_;
+
+  // per-knot blocks of element 0 (fddp_get_quantity: [b][t][per])
+  std::vector<VectorXd> quantity(int which, int nk, size_t per) const {
+    VectorXd a((size_t)dims_.B * nk * per);
+    check(fddp_get_quantity(h_.get(), which, a.data()), "fddp_get_quantity");
+    std::vector<VectorXd> out;
+    for (int t = 0; t < nk; ++t) out.push_back(VectorXd(a.begin() + t * per, a.begin() + (t + 1) * per));
+    return out;
+  }
 
  private:
   // fddp_iteration_callback: the C ABI calls it between iterations; no exception may
@@ -404,8 +510,8 @@ class SolverFDDP {
     if (self->dims_.B == 1 && !reported[0]) return 0;
     try {
       for (const auto& cb : self->callbacks_) (*cb)(*self);
-    } catch (const std::exception& e) {
-      self->cb_error_ = e.what();
+    } catch (...) {  // any exception: kept, rethrown by solve() after fddp_solve returns
+      self->cb_error_ = std::current_exception();
       return 1;
     }
     return 0;

@@ -31,6 +31,15 @@
 extern "C" {
 #endif
 
+/* ---- ABI version ----------------------------------------------------------
+ * Bumped on every incompatible change of a declaration below; a caller compiled
+ * against this header checks fddp_abi_version() == FDDP_ABI_VERSION at start-up.
+ *   1  rounds 1-4
+ *   2  fddp_iteration_callback returns int (nonzero stops fddp_solve)
+ *   3  fddp_calc_diff / fddp_backward_pass / fddp_forward_pass */
+#define FDDP_ABI_VERSION 3
+int fddp_abi_version(void);
+
 /* ---- status codes -------------------------------------------------------- */
 #define FDDP_OK 0
 #define FDDP_ERR_INVALID_ARG (-1)   /* reference: throw_pretty("Invalid argument") */
@@ -280,6 +289,25 @@ int fddp_problem_calc_diff(fddp_handle* h, double* cost);
  * iter==0 calc and the gaps, ddp.cpp:157-178) + backwardPass (ddp.cpp:180-253).
  * status: B ints, 0 ok / 1 backward_error (may be NULL). */
 int fddp_compute_direction(fddp_handle* h, int recalc, int32_t* status);
+/* The three phases of computeDirection / tryStep one at a time, as the reference's
+ * SolverDDP exposes them (bindings/python/crocoddyl/core/solvers/ddp.cpp:70-82) and its
+ * timing harness calls them (benchmark/arm-kinova-codegen.cpp:260-285).
+ * SolverDDP::calcDiff (ddp.cpp:157-178): problem.calc when iter_ == 0, problem.calcDiff,
+ * then the gaps fs (or zero gaps when the candidate just became feasible). cost: B
+ * doubles (cost_, the return value), may be NULL. */
+int fddp_calc_diff(fddp_handle* h, double* cost);
+/* SolverDDP::backwardPass (ddp.cpp:180-253) with computeGains (ddp.cpp:298-310) and the
+ * sums of SolverFDDP::updateExpectedImprovement (fddp.cpp:126-147), on the derivatives of
+ * the last calc_diff. K, k, Vx, Vxx, Q* are read with fddp_get_quantity (Vx, Vxx, Q* in
+ * debug mode). status: B ints, 0 ok / 1 backward_error (the reference throws; here the
+ * element keeps the blocks of the failed sweep), may be NULL. */
+int fddp_backward_pass(fddp_handle* h, int32_t* status);
+/* SolverFDDP::forwardPass(stepLength) (fddp.cpp:149-225): the rollout of the current
+ * policy into xs_try / us_try (fddp_get_xs_try / us_try) and cost_try, without the
+ * cost difference tryStep returns. stepLength outside [0, 1] is an argument error
+ * (fddp.cpp:150-153). cost_try: B doubles, status: B ints (1 forward_error); either
+ * may be NULL. */
+int fddp_forward_pass(fddp_handle* h, double step_length, double* cost_try, int32_t* status);
 /* SolverFDDP::updateExpectedImprovement (fddp.cpp:126-147). */
 int fddp_update_expected_improvement(fddp_handle* h);
 /* SolverDDP::tryStep / SolverFDDP::forwardPass (ddp.cpp:127-130, fddp.cpp:149-225).

@@ -84,6 +84,21 @@ static inline void gemv(const double* A, int r, int c, const double* x, double* 
 static inline void gemvT(const double* A, int r, int c, const double* x, double* y) {
   for (int j = 0; j < c; ++j) y[j] = dot(A + (size_t)j * r, x, r);
 }
+// sum_j K(i, j) dx_j of the forward pass's feedback term (fddp.cpp:199 K_[t] * dx_[t]):
+// one chain in j order, as Eigen's column-major GEMV accumulates a row, and as the
+// device's rollout (fddp_kernels.hpp fwd_trial). Built without reassociation: with
+// -fassociative-math gcc would split this reduction over vector lanes (two partial sums).
+#if defined(__GNUC__) && !defined(__clang__)
+__attribute__((optimize("no-associative-math")))
+#endif
+static double gain_row_dot(const double* K, int ld, int i, const double* dx, int n) {
+  double s = 0.;
+#if defined(__clang__)
+#pragma clang loop vectorize(disable)
+#endif
+  for (int j = 0; j < n; ++j) s = std::fma(K[(size_t)j * ld + i], dx[j], s);
+  return s;
+}
 
 // ---------------------------------------------------------------------------
 // Knot models. One ActionData per knot (core/action-base.hpp:101-142).
@@ -946,10 +961,8 @@ struct Solver {
       P->diff(xs[t].data(), xs_try[t].data(), dx[t].data());  // diff(xs, xs_try)
       if (m.nu != 0) {
         for (int i = 0; i < m.nu; ++i) {
-          double v = us[t][i] - k[t][i] * alpha;
-          double kd = 0.;
-          for (int j = 0; j < n; ++j) kd += K[t](i, j) * dx[t][j];
-          us_try[t][i] = v - kd;
+          const double v = std::fma(-k[t][i], alpha, us[t][i]);  // us - k alpha (contracted, as the device)
+          us_try[t][i] = v - gain_row_dot(K[t].a.data(), K[t].r, i, dx[t].data(), n);
           // SolverBoxFDDP::forwardPass clamps (box-fddp.cpp:100-102):
           // cwiseMax(u_lb).cwiseMin(u_ub)
           if (box && haslim[t]) us_try[t][i] = std::min(std::max(us_try[t][i], ulb[t][i]), uub[t][i]);
@@ -1341,6 +1354,35 @@ int oracle_set_solver_state(oracle_handle* h, int iter, double xreg, double ureg
 int oracle_compute_direction(oracle_handle* h, int recalc, int32_t* status) {
   for (int b = 0; b < h->dims.B; ++b) {
     bool ok = h->solvers[b].computeDirection(recalc != 0);
+    if (status) status[b] = ok ? 0 : 1;
+  }
+  return FDDP_OK;
+}
+// SolverDDP::calcDiff (ddp.cpp:157-178)
+int oracle_calc_diff(oracle_handle* h, double* cost) {
+  for (int b = 0; b < h->dims.B; ++b) {
+    const double c = h->solvers[b].calcDiff();
+    if (cost) cost[b] = c;
+  }
+  return FDDP_OK;
+}
+// SolverDDP::backwardPass (ddp.cpp:180-253)
+int oracle_backward_pass(oracle_handle* h, int32_t* status) {
+  for (int b = 0; b < h->dims.B; ++b) {
+    const bool ok = h->solvers[b].backwardPass();
+    if (status) status[b] = ok ? 0 : 1;
+  }
+  return FDDP_OK;
+}
+// SolverFDDP::forwardPass (fddp.cpp:149-225)
+int oracle_forward_pass(oracle_handle* h, double alpha, double* cost_try, int32_t* status) {
+  if (alpha > 1. || alpha < 0.) {  // fddp.cpp:150-153
+    g_err = "invalid step length, value is between 0. to 1.";
+    return FDDP_ERR_INVALID_ARG;
+  }
+  for (int b = 0; b < h->dims.B; ++b) {
+    const bool ok = h->solvers[b].forwardPass(alpha);
+    if (cost_try) cost_try[b] = h->solvers[b].cost_try;
     if (status) status[b] = ok ? 0 : 1;
   }
   return FDDP_OK;

@@ -110,6 +110,24 @@ class Gpu:
     def update_expected_improvement(self):
         self._ok(self.L.fddp_update_expected_improvement(self.h))
 
+    # SolverDDP's phases one at a time (fddp_calc_diff / fddp_backward_pass / fddp_forward_pass)
+    def ddp_calc_diff(self):
+        c = np.zeros(self.dims.B)
+        self._ok(self.L.fddp_calc_diff(self.h, _abi.dptr(c)))
+        return c
+
+    def backward_pass(self):
+        st = np.zeros(self.dims.B, dtype=np.int32)
+        self._ok(self.L.fddp_backward_pass(self.h, st.ctypes.data_as(_abi.I32)))
+        return st
+
+    def forward_pass(self, alpha):
+        """(rc, cost_try, status); rc != 0 on an argument error (no exception)."""
+        ct = np.zeros(self.dims.B)
+        st = np.zeros(self.dims.B, dtype=np.int32)
+        rc = self.L.fddp_forward_pass(self.h, alpha, _abi.dptr(ct), st.ctypes.data_as(_abi.I32))
+        return rc, ct, st
+
     def try_step(self, alpha):
         dV = np.zeros(self.dims.B)
         st = np.zeros(self.dims.B, dtype=np.int32)

@@ -189,6 +189,23 @@ class Oracle:
     def update_expected_improvement(self):
         self.L.oracle_update_expected_improvement(self.h)
 
+    # SolverDDP's phases one at a time (ddp.cpp:157-253, fddp.cpp:149-225)
+    def ddp_calc_diff(self):
+        c = np.zeros(self.dims.B)
+        self.L.oracle_calc_diff(self.h, _abi.dptr(c))
+        return c
+
+    def backward_pass(self):
+        st = np.zeros(self.dims.B, dtype=np.int32)
+        self.L.oracle_backward_pass(self.h, st.ctypes.data_as(_abi.I32))
+        return st
+
+    def forward_pass(self, alpha):
+        ct = np.zeros(self.dims.B)
+        st = np.zeros(self.dims.B, dtype=np.int32)
+        rc = self.L.oracle_forward_pass(self.h, alpha, _abi.dptr(ct), st.ctypes.data_as(_abi.I32))
+        return rc, ct, st
+
     def try_step(self, alpha):
         dV = np.zeros(self.dims.B)
         st = np.zeros(self.dims.B, dtype=np.int32)
