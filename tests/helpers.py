@@ -219,7 +219,7 @@ def ulp_floor(run, pool, reps=3, seed=0):
     return base, floors
 
 
-FLOOR_FACTOR = 4.0  # parity bar = max(tol, FLOOR_FACTOR x the conditioning floor)
+FLOOR_FACTOR = 3.0  # parity bar = max(tol, FLOOR_FACTOR x the conditioning floor) (round 6: 4 -> 3)
 
 _LOGGED = []
 
