@@ -172,31 +172,6 @@ struct MfmaCfg {
   static constexpr size_t bytes = sizeof(double) * total;
 };
 
-// Diagnostic phase timer (built with -DFDDP_STAMPS_BUILD, enabled by
-// FDDP_STAMPS=1): per wave, core cycles spent per phase, accumulated in
-// registers (a global read-modify-write per mark would drain the LDS-DMA in
-// flight) and flushed at the end of the sweep. Compiled out otherwise.
-struct Stamp {
-#ifdef FDDP_STAMPS_BUILD
-  unsigned long long* out;
-  unsigned long long t0;
-  unsigned long long acc[8];
-  __device__ Stamp(unsigned long long* o) : out(o), t0(__builtin_amdgcn_s_memtime()), acc{} {}
-  __device__ __forceinline__ void mark(int ph) {
-    const unsigned long long t = __builtin_amdgcn_s_memtime();
-    acc[ph] += t - t0;
-    t0 = t;
-  }
-  __device__ __forceinline__ void flush() {
-    if (out && (threadIdx.x & 63) == 0)
-      for (int i = 0; i < 8; ++i) out[i] += acc[i];
-  }
-#else
-  __device__ Stamp(unsigned long long*) {}
-  __device__ __forceinline__ void mark(int) {}
-  __device__ __forceinline__ void flush() {}
-#endif
-};
 
 // Quu^-1 by the symmetric sweep operator on one wave (Gauss-Jordan without
 // pivoting, which SPD matrices do not need). Pivot k is the k-th Schur

@@ -613,7 +613,7 @@ __device__ __forceinline__ bool fwd_trial_fast(const Dev& D, int b, const ElemSt
   for (int t = 0; t <= T; ++t) {
     const int64_t kk = D.knot(b, t);
     const bool running = t < T;
-    const fddp_knot_desc kd = D.knots[t];
+    const fddp_knot_desc kd = knot_desc_s(D, t);  // scalar loads: no wait behind the prefetches
     const int nu = kd.nu;
     const double cxs = pxs[0], cfs = pfs[0], cvf = pvf[0], cus = pus[0], ckv = pkv[0], clb = plb[0], cub = pub[0];
     double cK[KMAX];
@@ -646,7 +646,7 @@ __device__ __forceinline__ bool fwd_trial_fast(const Dev& D, int b, const ElemSt
       pd = wave_sum(pd);
       if (lane == 0) red[8 + wid] = pd;
     }
-    stage_params_batched<NT>(D.pblock(b, t), block_doubles_dev(kd.kind, nx, nu), pl, cached);
+    stage_params_batched<NT>(D.params + kd.param_offset + (int64_t)b * kd.param_stride, block_doubles_dev(kd.kind, nx, nu), pl, cached);
     const double* P = pl;
     __syncthreads();
     if (running) {

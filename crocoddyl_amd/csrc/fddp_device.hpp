@@ -68,7 +68,12 @@ __device__ __forceinline__ void lds_publish(int* ctr, int v) {
   __hip_atomic_store(ctr, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 __device__ __forceinline__ void lds_wait_ge(int* ctr, int target) {  // before the LDS accesses it guards
+#ifdef FDDP_SPIN_POLL  // diagnostic build (make spin): busy polls, no s_sleep between them
+  while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target) {
+  }
+#else
   while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target) __builtin_amdgcn_s_sleep(1);
+#endif
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
@@ -96,6 +101,32 @@ __device__ __forceinline__ void dma_vec(double* lds, const double* g, int nd, in
   if ((nd & 1) && wid == NW - 1 && lane < 2)
     __builtin_amdgcn_global_load_lds((const char*)(g + nd - 1) + 4 * lane, (lds_void_ptr)(lds + nd - 1), 4, 0, 0);
 }
+// Diagnostic phase timer (built with -DFDDP_STAMPS_BUILD, enabled by
+// FDDP_STAMPS=1): per wave, core cycles spent per phase, accumulated in
+// registers (a global read-modify-write per mark would drain the LDS-DMA in
+// flight) and flushed at the end of the sweep. Compiled out otherwise.
+struct Stamp {
+#ifdef FDDP_STAMPS_BUILD
+  unsigned long long* out;
+  unsigned long long t0;
+  unsigned long long acc[8];
+  __device__ Stamp(unsigned long long* o) : out(o), t0(__builtin_amdgcn_s_memtime()), acc{} {}
+  __device__ __forceinline__ void mark(int ph) {
+    const unsigned long long t = __builtin_amdgcn_s_memtime();
+    acc[ph] += t - t0;
+    t0 = t;
+  }
+  __device__ __forceinline__ void flush() {
+    if (out && (threadIdx.x & 63) == 0)
+      for (int i = 0; i < 8; ++i) out[i] += acc[i];
+  }
+#else
+  __device__ Stamp(unsigned long long*) {}
+  __device__ __forceinline__ void mark(int) {}
+  __device__ __forceinline__ void flush() {}
+#endif
+};
+
 // ---- register broadcasts within a wave (64 lanes = 4 rows of 16) -------------------
 // lane n of every row of 16 lanes, to the whole row (DPP row_newbcast: a VALU move, no
 // LDS-crossbar round trip as __shfl's ds_bpermute); n a compile-time constant

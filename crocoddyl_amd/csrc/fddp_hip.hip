@@ -1127,7 +1127,7 @@ int fddp_create(const fddp_dims* dims, const fddp_knot_desc* knots, const double
   if (const char* e = std::getenv("FDDP_STAMPS")) {
     if (e[0] == '1') {
       double* p2 = nullptr;
-      if ((rc = dalloc(h, &p2, (int64_t)d.B * 128))) return bail(rc);
+      if ((rc = dalloc(h, &p2, (int64_t)d.B * 136))) return bail(rc);
       D.stamps = (unsigned long long*)p2;
     }
   }
@@ -1141,7 +1141,7 @@ void fddp_destroy(fddp_handle* h) {
   DeviceGuard g(h->device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   if (h->D.stamps) {  // diagnostic summary: mean cycles per element per wave and phase
-    std::vector<unsigned long long> v((size_t)h->dims.B * 128);
+    std::vector<unsigned long long> v((size_t)h->dims.B * 136);
     if (hipMemcpy(v.data(), h->D.stamps, v.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
       const char* names[8] = {"p1_G", "p1_H", "p1_inv", "b1_dma", "p2_K", "p2_Vupd", "b2_p3", "b3_wait"};
       std::fprintf(stderr, "[fddp stamps] mean cycles per element (variant %d):\n", h->bwd_variant);
@@ -1151,6 +1151,16 @@ void fddp_destroy(fddp_handle* h) {
           double s2 = 0;
           for (int b = 0; b < h->dims.B; ++b) s2 += (double)v[((size_t)b * 8 + w) * 8 + ph];
           std::fprintf(stderr, " %s=%.0f", names[ph], s2 / h->dims.B);
+        }
+        std::fprintf(stderr, "\n");
+      }
+      if (h->has_mb) {
+        const char* mn[5] = {"state", "params", "gains", "calc", "stores_checks"};
+        std::fprintf(stderr, "[fddp stamps] multibody rollout, mean cycles per element summed over waves (all trials):");
+        for (int ph = 0; ph < 5; ++ph) {
+          double s2 = 0;
+          for (int b = 0; b < h->dims.B; ++b) s2 += (double)v[(size_t)h->dims.B * 128 + (size_t)b * 8 + ph];
+          std::fprintf(stderr, " %s=%.0f", mn[ph], s2 / h->dims.B);
         }
         std::fprintf(stderr, "\n");
       }

@@ -769,6 +769,8 @@ __device__ __forceinline__ bool fwd_trial(const Dev& D, int b, const ElemState& 
   for (int i = tid; i < nx; i += NT) xn[i] = x0[i];
   cost_try = 0.;
   double* dvp = out.dvp + D.knot(b, 0);
+  // (diagnostic phase timer, FDDP_STAMPS=1 on the stamps build: per wave, summed)
+  Stamp stamp(D.stamps ? D.stamps + (int64_t)D.B * 128 + (int64_t)b * 8 : nullptr);
   __syncthreads();
   for (int t = 0; t <= T; ++t) {
     const int64_t kk = D.knot(b, t);
@@ -801,7 +803,9 @@ __device__ __forceinline__ bool fwd_trial(const Dev& D, int b, const ElemState& 
     }
     const bool running = t < T;
     const fddp_knot_desc kd = D.knots[t];
+    stamp.mark(0);
     const double* P = stage_params<NT>(D.pblock(b, t), block_doubles_dev(kd.kind, nx, kd.nu, D.pblock(b, t)), pl, pcap, cached);
+    stamp.mark(1);
     if (running) {
       const int nu = kd.nu;
       const double* us = D.us[c] + D.run(b, t) * D.sM;
@@ -856,7 +860,9 @@ __device__ __forceinline__ bool fwd_trial(const Dev& D, int b, const ElemState& 
       }
       __syncthreads();
     }
+    stamp.mark(2);
     const double ct = knot_calc<NT, MB>(kd, P, nx, xv, uv, running, xn, red, mbw);
+    stamp.mark(3);
     bool bad = false;
     for (int i = tid; i < nx; i += NT) gstore(xt + i, xv[i]);
     if (running) {
@@ -877,9 +883,12 @@ __device__ __forceinline__ bool fwd_trial(const Dev& D, int b, const ElemState& 
     bad |= raise_if_nan(cost_try);
     if (wg_any(bad, flag)) {
       if (nwritten) *nwritten = t + 1;  // the knots of the trial buffers this trial wrote
+      stamp.flush();
       return false;
     }
+    stamp.mark(4);
   }
+  stamp.flush();
   if (nwritten) *nwritten = T + 1;
   // dv: terminal first, then t = 0..T-1 (fddp.cpp:110-119). Summed by the
   // thread that stored the terms (program order), broadcast through LDS.
