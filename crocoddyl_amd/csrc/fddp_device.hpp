@@ -268,6 +268,26 @@ __device__ inline bool selected(const ElemState& s, int sel) {
   }
 }
 
+// Knot descriptors and segment ends through the constant address space:
+// scalar loads (lgkmcnt), which do not queue behind the global stores in
+// flight the way vector loads do (loads and stores share vmcnt, in order).
+__device__ __forceinline__ fddp_knot_desc knot_desc_s(const Dev& D, int t) {
+  typedef __attribute__((address_space(4))) const fddp_knot_desc* cptr;
+  const cptr p = (cptr)D.knots + t;
+  fddp_knot_desc k;
+  k.kind = p->kind;
+  k.nu = p->nu;
+  k.param_offset = p->param_offset;
+  k.param_stride = p->param_stride;
+  return k;
+}
+// A parameter-pool double through the constant address space (the pool does not change
+// during a kernel): a scalar load
+__device__ __forceinline__ double param_s(const double* p) {
+  typedef __attribute__((address_space(4))) const double* cptr;
+  return *(cptr)p;
+}
+
 // raiseIfNaN — src/core/solver-base.cpp:175-181
 __device__ inline bool raise_if_nan(double v) { return isnan(v) || isinf(v) || v >= 1e30; }
 // |x| value that trips raiseIfNaN(lpNorm<Infinity>) for an element of a vector
