@@ -758,7 +758,12 @@ __device__ __forceinline__ bool bwd_knot(const Dev& D, const BwdLds& L, int b, i
   const double* const lxv = odd ? L.lxv2 : L.lxv;
   const double* const luv = odd ? L.luv2 : L.luv;
   const double* const fsb = odd ? L.fsb2 : L.fsb;
-  auto issue_dma = [&]() {
+  // part 1: Fx (the Zx buffer: no reader after P1) by the DMA waves other than 0, so it can
+  // go right after B1 even where C^T lives over Zu; part 2: the rest (Fu into Zu, Lx, Lu and
+  // the prefetch plan's blocks); 3: everything
+  constexpr int NDX = P.ndma - (P.dmarank[0] >= 0 ? 1 : 0);
+  constexpr int RKX = P.dmarank[W] - (P.dmarank[0] >= 0 && P.dmarank[W] > P.dmarank[0] ? 1 : 0);
+  auto issue_dma = [&](int part) {
   if constexpr (P.dmarank[W] >= 0) {
     if (t > 0) {  // operands of knot t-1 (prefetch plan: into the other buffers, with fs)
       constexpr int ND = P.ndma, RK = P.dmarank[W];
@@ -766,11 +771,26 @@ __device__ __forceinline__ bool bwd_knot(const Dev& D, const BwdLds& L, int b, i
       const bool nb = pre && !odd;
       double* const nZx = nb ? L.Zx2 : L.Zx;
       double* const nZu = nb ? L.Zu2 : L.Zu;
-      if ((n & 1) == 0 && ZLD - n <= 2 * 64) {
-        dma_cols_full<ND, ZLD>(nZx, D.Fx + k1 * D.sNN, n, n, D.zero16, RK, lane);
+      const bool full = (n & 1) == 0 && ZLD - n <= 2 * 64;
+      if (part == 3) {
+        if (full) {
+          dma_cols_full<ND, ZLD>(nZx, D.Fx + k1 * D.sNN, n, n, D.zero16, RK, lane);
+        } else {
+          dma_cols<ND>(nZx, ZLD, D.Fx + k1 * D.sNN, n, n, RK, lane);
+        }
+      } else if (part == 1) {
+        if constexpr (W != 0 && NDX > 0) {
+          if (full) {
+            dma_cols_full<NDX, ZLD>(nZx, D.Fx + k1 * D.sNN, n, n, D.zero16, RKX, lane);
+          } else {
+            dma_cols<NDX>(nZx, ZLD, D.Fx + k1 * D.sNN, n, n, RKX, lane);
+          }
+        }
+        return;
+      }
+      if (full) {
         dma_cols_full<ND, ZLD>(nZu, D.Fu + k1 * D.sNM, n, m, D.zero16, RK, lane);
       } else {
-        dma_cols<ND>(nZx, ZLD, D.Fx + k1 * D.sNN, n, n, RK, lane);
         dma_cols<ND>(nZu, ZLD, D.Fu + k1 * D.sNM, n, m, RK, lane);
       }
       dma_vec<ND>(nb ? L.lxv2 : L.lxv, D.Lx + k1 * D.sN, n, RK, lane);
@@ -785,7 +805,7 @@ __device__ __forceinline__ bool bwd_knot(const Dev& D, const BwdLds& L, int b, i
     }
   }
   };
-  if constexpr (pre) issue_dma();
+  if constexpr (pre) issue_dma(3);
   double* V = L.V;
   double* Qxu = L.Qxu;
   double* Quu = L.Quu;
@@ -1030,7 +1050,10 @@ __device__ __forceinline__ bool bwd_knot(const Dev& D, const BwdLds& L, int b, i
   // the next knot's operands: right after B1, except in the 8-wave plan with C^T over Zu
   // (after B2, once every C^T read is done)
   constexpr bool early_dma = NW <= 4 || Cfg::ct_own;
-  if constexpr (early_dma && !pre) issue_dma();
+  // (with C^T over Zu: the Fx part now, the rest after B2)
+  constexpr bool split_dma = !early_dma && !pre && NDX > 0;
+  if constexpr (early_dma && !pre) issue_dma(3);
+  if constexpr (split_dma) issue_dma(1);
   // ---- P2: K(:, i) = Quu^-1 Qxu(i, :)^T ; Vxx(i, j) = Qxx(i, j) - K(:, i)^T Qxu(j, :)^T
   f64x4 Kt[NA][MTL];
   double kst = 0.;   // wave 0: k(row) (lanes part == 0)
@@ -1210,7 +1233,7 @@ __device__ __forceinline__ bool bwd_knot(const Dev& D, const BwdLds& L, int b, i
     const int target = (P.xwaves + (P.owns_x(0) ? 0 : 1)) * (D.T - t);
     lds_wait_ge(L.flag + 3, target);
   }
-  if constexpr (!early_dma) issue_dma();
+  if constexpr (!early_dma) issue_dma(split_dma ? 2 : 3);
   // ---- P3: Vx = Qx + K^T Quuk - 2 K^T Qu (+ Vxx fs), reduction terms -------
   {
     const double* fsv = fsb;
