@@ -762,6 +762,7 @@ __device__ __forceinline__ bool bwd_knot(const Dev& D, const BwdLds& L, int b, i
   // go right after B1 even where C^T lives over Zu; part 2: the rest (Fu into Zu, Lx, Lu and
   // the prefetch plan's blocks); 3: everything
   constexpr int NDX = P.ndma - (P.dmarank[0] >= 0 ? 1 : 0);
+  constexpr int CTC = (MP * Cfg::LDT + ZLD - 1) / ZLD;  // Zu columns C^T covers (when it lies over Zu)
   constexpr int RKX = P.dmarank[W] - (P.dmarank[0] >= 0 && P.dmarank[W] > P.dmarank[0] ? 1 : 0);
   auto issue_dma = [&](int part) {
   if constexpr (P.dmarank[W] >= 0) {
@@ -779,19 +780,27 @@ __device__ __forceinline__ bool bwd_knot(const Dev& D, const BwdLds& L, int b, i
           dma_cols<ND>(nZx, ZLD, D.Fx + k1 * D.sNN, n, n, RK, lane);
         }
       } else if (part == 1) {
+        // (and the columns of Fu past the ones C^T lies over: CTC Zu columns hold C^T)
         if constexpr (W != 0 && NDX > 0) {
+          const int c0 = CTC < m ? CTC : m;
           if (full) {
             dma_cols_full<NDX, ZLD>(nZx, D.Fx + k1 * D.sNN, n, n, D.zero16, RKX, lane);
+            if (c0 < m)
+              dma_cols_full<NDX, ZLD>(nZu + c0 * ZLD, D.Fu + k1 * D.sNM + (int64_t)c0 * n, n, m - c0, D.zero16, RKX,
+                                      lane);
           } else {
             dma_cols<NDX>(nZx, ZLD, D.Fx + k1 * D.sNN, n, n, RKX, lane);
+            if (c0 < m) dma_cols<NDX>(nZu + c0 * ZLD, ZLD, D.Fu + k1 * D.sNM + (int64_t)c0 * n, n, m - c0, RKX, lane);
           }
         }
         return;
       }
+      // part 2 of a split: only the Fu columns under C^T
+      const int mu2 = part == 2 ? (CTC < m ? CTC : m) : m;
       if (full) {
-        dma_cols_full<ND, ZLD>(nZu, D.Fu + k1 * D.sNM, n, m, D.zero16, RK, lane);
+        dma_cols_full<ND, ZLD>(nZu, D.Fu + k1 * D.sNM, n, mu2, D.zero16, RK, lane);
       } else {
-        dma_cols<ND>(nZu, ZLD, D.Fu + k1 * D.sNM, n, m, RK, lane);
+        dma_cols<ND>(nZu, ZLD, D.Fu + k1 * D.sNM, n, mu2, RK, lane);
       }
       dma_vec<ND>(nb ? L.lxv2 : L.lxv, D.Lx + k1 * D.sN, n, RK, lane);
       dma_vec<ND>(nb ? L.luv2 : L.luv, D.Lu + k1 * D.sM, m, RK, lane);
