@@ -1146,7 +1146,16 @@ MB_HD inline void jlog6_col(const double* R, const double* p, int k, double* col
 // dofs for the base), so v_k is the full body velocity. The placements
 // oMi = oMparent * liMi are composed by each lane walking its ancestors (w_walk).
 // ---------------------------------------------------------------------------
-constexpr int kWPerJoint = 80;
+// Doubles per dof in the world values: 80 used, 2 of padding. The workgroup's lanes read
+// and write their own dof's record (lane stride kWPerJoint): at 80 doubles (160 dwords)
+// every lane of a 64-bit access maps to banks 0-1 or 32-33 (16-way conflicts in a 32-lane
+// group), at 82 (164 dwords) to 16 bank pairs (2-way) with the records 16-byte aligned.
+// Measured on the C5 walk: rollout 28.55 -> 26.81 ms, calcDiff 25.60 -> 25.26 ms (81:
+// conflict-free 64-bit accesses but 8-byte aligned records, calcDiff 26.11 ms).
+#ifndef MB_WPJ
+#define MB_WPJ 82
+#endif
+constexpr int kWPerJoint = MB_WPJ;
 constexpr int kMaxCosts = 64;
 struct WVals {
   double* base;
