@@ -218,6 +218,8 @@ struct Dev {
   unsigned long long* box_stats;   // diagnostics (FDDP_BOX_STATS=1): box QPs, Newton iterations, inverses
   BoxQPCfg boxcfg;                 // qp_(nu, 100, 0.1, 1e-5, 0.) (box-fddp.cpp:16)
   int64_t mbw;                     // LDS doubles of the multibody calc scratch (0: no multibody knots)
+  int64_t mbw_fwd;                 // ... of the forward kernels' calc (mb::calc_dense_doubles)
+  int dxv_mbw;                     // forward kernels: dx (2 sN) in the tail of that scratch (dead during the calc)
   int64_t mbd;                     // LDS doubles of the multibody calcDiff work area (its parameter block follows)
   int mbspill;                     // its plan's spill flags (multibody.hpp diff_spill)
   // parallel line search (generic trials): npar trials of one element run in

@@ -613,6 +613,9 @@ static void choose_npar(fddp_handle* h, const std::vector<ElemState>& st) {
     const void* k = ktab::forward_fn(mb_rollout(h) ? ktab::FWD_MB : ktab::FWD_GENERIC);
     (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, kNT, h->fwd_smem);
     h->ls_slots = (double)std::max(1, dev_cus) * std::max(1, per_cu);
+    if (std::getenv("FDDP_STAMPS"))  // (diagnostic runs: the rollout's residency)
+      std::fprintf(stderr, "[fddp] rollout: %d workgroups per CU x %d CUs (LDS %zu B per workgroup)\n", per_cu, dev_cus,
+                   h->fwd_smem);
   }
   std::vector<int> t;
   t.reserve(st.size());
@@ -844,6 +847,7 @@ int apply_knots(fddp_handle* h, const fddp_knot_desc* knots, const double* param
     h->all_mb = true;
     for (int t = 0; t <= d.T; ++t) h->all_mb = h->all_mb && is_mb_kind(knots[t].kind);
     D.mbw = h->has_mb ? pad2(fddp::mb::calc_work_doubles(mb_nj, mb_nc)) : 0;
+    D.mbw_fwd = h->has_mb ? pad2(fddp::mb::calc_dense_doubles(mb_nj, mb_nc)) : 0;
     h->mb_nj = mb_nj;
     // parallel line-search trials: they pay on the large trees (C5 Talos, nv = 38:
     // forward -12 %), where one rollout keeps a CU busy longest; on small ones (C4
@@ -882,7 +886,12 @@ int apply_knots(fddp_handle* h, const fddp_knot_desc* knots, const double* param
     if (h->has_mb && h->pcap < pad2(mb_pmax))
       return fail(FDDP_ERR_INVALID_ARG, "multibody parameter blocks exceed the LDS budget of the calc / rollout kernels");
   }
-  h->fwd_smem = sizeof(double) * (h->pcap + fwd_lds_doubles<kNT, false>(D.sX, D.sN, D.sM) + D.mbw);
+  // (dx in the tail of the calc's scratch when the gains' K staging leaves room: on the C5 walk
+  // that takes the rollout's LDS to 52.6 KB, three workgroups per CU; the LDS is allocated in
+  // 2 KB granules (measured: tools/occ_probe.hip), which the occupancy API does not model)
+  D.dxv_mbw = D.mbw_fwd >= (int64_t)D.m * D.n + 2 * D.sN ? 1 : 0;
+  h->fwd_smem = sizeof(double) * (h->pcap + fwd_lds_doubles<kNT, false>(D.sX, D.sN, D.sM) - (D.dxv_mbw ? 2 * D.sN : 0) +
+                                  D.mbw_fwd);
   h->calc_smem = sizeof(double) * (h->pcap + 2 * D.sX + D.sM + 5 * (kNT / kWave) + 16 + D.mbw);
   h->cdiff_smem = sizeof(double) * (h->pcap + D.sX + D.sM);
   {  // dense-knot fast path: every knot LQR / Euler∘DiffLQR, block LDS-resident
@@ -1127,7 +1136,7 @@ int fddp_create(const fddp_dims* dims, const fddp_knot_desc* knots, const double
   if (const char* e = std::getenv("FDDP_STAMPS")) {
     if (e[0] == '1') {
       double* p2 = nullptr;
-      if ((rc = dalloc(h, &p2, (int64_t)d.B * 136))) return bail(rc);
+      if ((rc = dalloc(h, &p2, (int64_t)d.B * 140))) return bail(rc);
       D.stamps = (unsigned long long*)p2;
     }
   }
@@ -1141,7 +1150,7 @@ void fddp_destroy(fddp_handle* h) {
   DeviceGuard g(h->device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   if (h->D.stamps) {  // diagnostic summary: mean cycles per element per wave and phase
-    std::vector<unsigned long long> v((size_t)h->dims.B * 136);
+    std::vector<unsigned long long> v((size_t)h->dims.B * 140);
     if (hipMemcpy(v.data(), h->D.stamps, v.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
       const char* names[8] = {"p1_G", "p1_H", "p1_inv", "b1_dma", "p2_K", "p2_Vupd", "b2_p3", "b3_wait"};
       std::fprintf(stderr, "[fddp stamps] mean cycles per element (variant %d):\n", h->bwd_variant);
@@ -1163,6 +1172,49 @@ void fddp_destroy(fddp_handle* h) {
           std::fprintf(stderr, " %s=%.0f", mn[ph], s2 / h->dims.B);
         }
         std::fprintf(stderr, "\n");
+      }
+      {  // the rollout's residency: per workgroup (element) of its last launch, the real-time
+         // start / end (100 MHz) and the CU it ran on (HW_ID, XCC_ID); the most workgroups one
+         // CU held at once, and the mean over the launch
+        struct Ev {
+          unsigned long long t;
+          int d;
+        };
+        std::vector<std::pair<unsigned long long, std::vector<Ev>>> cus;
+        std::vector<std::pair<unsigned long long, std::vector<Ev>>>* pc = &cus;
+        unsigned long long t0 = ~0ull, t1 = 0;
+        int n = 0;
+        for (int b = 0; b < h->dims.B; ++b) {
+          const unsigned long long* r = &v[(size_t)h->dims.B * 136 + (size_t)b * 4];
+          if (r[0] == 0 || r[2] == 0) continue;
+          const unsigned long long hw = r[1];
+          // cu: HW_ID cu_id [11:8], sh_id [12], se_id [15:13]; XCC_ID in the high word
+          const unsigned long long key = ((hw >> 32) << 16) | ((hw >> 8) & 0xff);
+          size_t i = 0;
+          while (i < pc->size() && (*pc)[i].first != key) ++i;
+          if (i == pc->size()) pc->push_back({key, {}});
+          (*pc)[i].second.push_back({r[0], 1});
+          (*pc)[i].second.push_back({r[2], -1});
+          t0 = std::min(t0, r[0]);
+          t1 = std::max(t1, r[2]);
+          ++n;
+        }
+        int most = 0;
+        double area = 0.;
+        for (auto& c : cus) {
+          std::sort(c.second.begin(), c.second.end(), [](const Ev& a, const Ev& b) { return a.t < b.t || (a.t == b.t && a.d < b.d); });
+          int cur = 0;
+          for (size_t k = 0; k < c.second.size(); ++k) {
+            cur += c.second[k].d;
+            most = std::max(most, cur);
+            if (k + 1 < c.second.size()) area += (double)cur * (double)(c.second[k + 1].t - c.second[k].t);
+          }
+        }
+        if (n > 0)
+          std::fprintf(stderr,
+                       "[fddp stamps] rollout residency: %d workgroups on %zu CUs, at most %d on one CU, mean %.2f per used "
+                       "CU over the launch (%.3f ms)\n",
+                       n, cus.size(), most, area / ((double)(t1 - t0) * (double)cus.size()), (t1 - t0) * 1e-5);
       }
       if (h->fast) {
         const char* fn[8] = {"stage", "compute", "-", "-", "-", "blocks", "-", "-"};

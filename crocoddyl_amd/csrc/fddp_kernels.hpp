@@ -827,7 +827,7 @@ __device__ __forceinline__ bool fwd_trial(const Dev& D, int b, const ElemState& 
       // reference's GEMV row (fddp.cpp:199) and of the oracle (gain_row_dot), so us_try
       // rounds as theirs. (Round 5 split the row into 8 partial sums over the workgroup:
       // the reordered sums moved the C5 smoke's xs after 3 iterations 2.4e-8 -> 3.8e-8.)
-      if (m <= NT && D.mbw >= (int64_t)m * n) {
+      if (m <= NT && D.mbw_fwd - (D.dxv_mbw ? 2 * D.sN : 0) >= (int64_t)m * n) {
         if (!ff)
           for (int j = tid; j < n; j += NT) dxv[j] = xv[j] - xs[j];
         dma_vec<NT / kWave>(mbw, K, m * n, tid / kWave, tid & (kWave - 1));
@@ -922,7 +922,7 @@ __device__ __forceinline__ bool fwd_trial_fast(const Dev& D, int b, const ElemSt
                                                const double*& cached);
 
 // Forward-pass LDS beyond the parameter block (doubles): generic trial
-// [xv sX | uv sM | xn sX | red 5*NW+8 | flag 2 | dxv 2 sN | multibody scratch D.mbw], fast trial
+// [xv sX | uv sM | xn sX | red 5*NW+8 | flag 2 | dxv 2 sN | multibody scratch D.mbw_fwd], fast trial
 // [xu sX+sM | dxv sN | xn sX | pa NT | pdyn NT | red 24 | flag].
 template <int NT, bool FAST>
 __host__ __device__ inline int64_t fwd_lds_doubles(int64_t sX, int64_t sN, int64_t sM) {
@@ -991,10 +991,15 @@ __device__ __forceinline__ void ls_finish(const Prm& prm, ElemState& s, bool acc
 #ifndef FDDP_FWD_WPE
 #define FDDP_FWD_WPE 2
 #endif
+// the multibody rollout at three workgroups per CU (its LDS, knot_calc_dense_x, allows it on
+// the C5 walk): 168 VGPRs
+#ifndef FDDP_FWD_WPE_MB
+#define FDDP_FWD_WPE_MB 3
+#endif
 // (the generic variant, for horizons that mix multibody and dense knots, gets the
 // whole register file: under the 2-waves cap its spills trip a backend error)
 template <int NT, bool FAST, bool MB = false>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((FAST || MB) ? FDDP_FWD_WPE : 1))) void forward_kernel(Dev D, Prm prm, int mode, double alpha1, int* active_count,
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MB ? FDDP_FWD_WPE_MB : FAST ? FDDP_FWD_WPE : 1))) void forward_kernel(Dev D, Prm prm, int mode, double alpha1, int* active_count,
                                                      int64_t pcap, int group = 0) {
   // (workgroups are dispatched roughly in index order: the elements whose last line
   // search took the most trials start first, so they do not trail the launch)
@@ -1030,14 +1035,27 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((FAST || MB)
   // threads take a copy after each trial, and thread 0 writes the changes back.
   __shared__ ElemState ss;
   if (threadIdx.x == 0) ss = *st;
+#ifdef FDDP_STAMPS_BUILD
+  // (diagnostic: this workgroup's residency, real time and hardware ids; fddp_destroy)
+  unsigned long long* rs = D.stamps ? D.stamps + (int64_t)D.B * 136 + (int64_t)b * 4 : nullptr;
+  if (rs && threadIdx.x == 0) {
+    rs[0] = __builtin_amdgcn_s_memrealtime();
+    rs[1] = (unsigned long long)(unsigned)__builtin_amdgcn_s_getreg(4 | (31 << 11)) |
+            ((unsigned long long)(unsigned)__builtin_amdgcn_s_getreg(20 | (31 << 11)) << 32);
+  }
+#endif
   __syncthreads();
   int nwr = D.T + 1;
+  // (generic trial) the knot calc's scratch, and dx: its own 2 sN doubles before the scratch,
+  // or (D.dxv_mbw) the scratch's last 2 sN doubles: dx is dead once the gains are applied, and
+  // the gains' K staging stays below it (fddp_create checks the room)
+  double* const mbw = (double*)flag + 2 + (D.dxv_mbw ? 0 : 2 * D.sN);
+  double* const dxv_ = D.dxv_mbw ? mbw + D.mbw_fwd - 2 * D.sN : (double*)flag + 2;
   auto trial = [&](double alpha, double& ct, double& dv) {
     if constexpr (FAST)
       return fwd_trial_fast<NT, true>(D, b, ss, alpha, xv, dxv, xn, pa, pdyn, red, flag, ct, dv, pl, pcap, cached);
     else
-      return fwd_trial<NT, MB>(D, b, ss, alpha, xv, uv, xn, red, flag, ct, dv, pl, pcap, cached, (double*)flag + 2 + 2 * D.sN,
-                           (double*)flag + 2, slot, &nwr);
+      return fwd_trial<NT, MB>(D, b, ss, alpha, xv, uv, xn, red, flag, ct, dv, pl, pcap, cached, mbw, dxv_, slot, &nwr);
   };
   // line search (fddp.cpp:53-81). One call site of the trial, so it is inlined (its
   // LDS pointers keep their address space).
@@ -1080,6 +1098,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((FAST || MB)
   }
   ElemState s = ss;
   ls_finish(prm, s, accepted);
+#ifdef FDDP_STAMPS_BUILD
+  if (rs && threadIdx.x == 0) rs[2] = __builtin_amdgcn_s_memrealtime();
+#endif
   if (threadIdx.x == 0) {
     *st = s;
     if (s.active && active_count) atomicAdd(active_count, 1);

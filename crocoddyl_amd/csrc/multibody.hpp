@@ -668,6 +668,12 @@ __device__ __forceinline__ bool gj_mfma(double* A_, int nr, int ld, int nc, bool
   typedef __attribute__((address_space(3))) double lds_d;
   typedef double f64x4 __attribute__((ext_vector_type(4)));
   lds_d* A = (lds_d*)lds_ptr(A_);
+  // the shape in scalar registers (the callers read it from the LDS parameter block, i.e.
+  // into vector registers): the sweep's `r0 + p < nr` then skips the padding pivots of the
+  // last block by a scalar branch instead of running all 16 under a lane mask
+  nr = __builtin_amdgcn_readfirstlane(nr);
+  ld = __builtin_amdgcn_readfirstlane(ld);
+  nc = __builtin_amdgcn_readfirstlane(nc);
   const int tid = (int)threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = (int)(blockDim.x >> 6);
   const int li = lane & 15, lk = lane >> 4;
   const int nrp = (nr + 15) & ~15, nbr = nrp >> 4, nct = (nrp + nc - nr + 15) >> 4;
@@ -1146,42 +1152,52 @@ MB_HD inline void jlog6_col(const double* R, const double* p, int k, double* col
 // dofs for the base), so v_k is the full body velocity. The placements
 // oMi = oMparent * liMi are composed by each lane walking its ancestors (w_walk).
 // ---------------------------------------------------------------------------
-// Doubles per dof in the world values: 80 used, 2 of padding. The workgroup's lanes read
-// and write their own dof's record (lane stride kWPerJoint): at 80 doubles (160 dwords)
-// every lane of a 64-bit access maps to banks 0-1 or 32-33 (16-way conflicts in a 32-lane
-// group), at 82 (164 dwords) to 16 bank pairs (2-way) with the records 16-byte aligned.
-// Measured on the C5 walk: rollout 28.55 -> 26.81 ms, calcDiff 25.60 -> 25.26 ms (81:
-// conflict-free 64-bit accesses but 8-byte aligned records, calcDiff 26.11 ms).
-#ifndef MB_WPJ
-#define MB_WPJ 82
-#endif
-constexpr int kWPerJoint = MB_WPJ;
+// The world values of a dof in two records of kWRec doubles (40 used, 2 of padding): the
+// L record holds what outlives the recursions (placement oMi, motion subspace, velocity,
+// acceleration, composite inertia), the D record what the recursions alone use (the local
+// placement, body mass / CoM / inertia, the RNEA's forces and terms). The workgroup's lanes
+// read and write their own dof's records (lane stride kWRec): at a multiple of 32 doubles
+// every lane of a 64-bit access would map to the same bank pair; at 42 (84 dwords) the lanes
+// spread over 16 bank pairs (2-way) with the records 16-byte aligned. (One 80-double record
+// per dof, its round-5 layout, was a 16-way conflict: C5 rollout 28.55 -> 26.81 ms,
+// calcDiff 25.60 -> 25.26 ms when padded.) The D records may lie apart from the L records
+// (`aux`): the rollout's calc puts its factorisation over them once the recursions are done
+// (knot_calc_dense_x); by default they follow the L records, the ancestor masks and root_a.
+constexpr int kWRec = 42;
 constexpr int kMaxCosts = 64;
 struct WVals {
   double* base;
   int nj;
   double* parts;  // per-wave partial sums of the recursions: 4 x 6 per dof (kPartDoubles)
-  MB_HD double* R(int i) const { return mb_lds(base + kWPerJoint * i); }  // liMi rotation
-  MB_HD double* p(int i) const { return R(i) + 9; }
-  MB_HD double* oR(int i) const { return R(i) + 12; }  // oMi
-  MB_HD double* op(int i) const { return R(i) + 21; }
-  MB_HD double* S(int i) const { return R(i) + 24; }   // dof motion subspace (world)
-  MB_HD double* m(int i) const { return R(i) + 30; }   // body mass (0 on the massless free-flyer dofs)
-  MB_HD double* c(int i) const { return R(i) + 31; }   // body CoM (world)
-  MB_HD double* Ic(int i) const { return R(i) + 34; }  // body inertia about its CoM, world axes (6)
-  MB_HD double* v(int i) const { return R(i) + 40; }
-  MB_HD double* a(int i) const { return R(i) + 46; }
-  MB_HD double* F(int i) const { return R(i) + 52; }   // body force, then accumulated joint force
-  MB_HD double* cm(int i) const { return R(i) + 58; }  // composite inertia, origin form: m, h = m c, I_O (6)
-  MB_HD double* ch(int i) const { return R(i) + 59; }
-  MB_HD double* cI(int i) const { return R(i) + 62; }
-  MB_HD double* cq(int i) const { return R(i) + 68; }  // S_i qdd_i + v_i x S_i qd_i
-  MB_HD double* fb(int i) const { return R(i) + 74; }  // body force I a + v x* I v
+  double* aux;    // the D records
+  MB_HD WVals(double* b, int n, double* p, double* a = nullptr)
+      : base(b), nj(n), parts(p), aux(a ? a : b + lsize(n)) {}
+  MB_HD double* L(int i) const { return mb_lds(base + kWRec * i); }
+  MB_HD double* Dr(int i) const { return mb_lds(aux + kWRec * i); }
+  MB_HD double* oR(int i) const { return L(i); }  // oMi
+  MB_HD double* op(int i) const { return L(i) + 9; }
+  MB_HD double* S(int i) const { return L(i) + 12; }   // dof motion subspace (world)
+  MB_HD double* v(int i) const { return L(i) + 18; }
+  MB_HD double* a(int i) const { return L(i) + 24; }
+  MB_HD double* cm(int i) const { return L(i) + 30; }  // composite inertia, origin form: m, h = m c, I_O (6)
+  MB_HD double* ch(int i) const { return L(i) + 31; }
+  MB_HD double* cI(int i) const { return L(i) + 34; }
+  MB_HD double* R(int i) const { return Dr(i); }  // liMi rotation
+  MB_HD double* p(int i) const { return Dr(i) + 9; }
+  MB_HD double* m(int i) const { return Dr(i) + 12; }   // body mass (0 on the massless free-flyer dofs)
+  MB_HD double* c(int i) const { return Dr(i) + 13; }   // body CoM (world)
+  MB_HD double* Ic(int i) const { return Dr(i) + 16; }  // body inertia about its CoM, world axes (6)
+  MB_HD double* F(int i) const { return Dr(i) + 22; }   // body force, then accumulated joint force
+  MB_HD double* cq(int i) const { return Dr(i) + 28; }  // S_i qdd_i + v_i x S_i qd_i
+  MB_HD double* fb(int i) const { return Dr(i) + 34; }  // body force I a + v x* I v
   // per-wave partial sums of the ancestor / subtree recursions (wave w's share of the dofs)
   MB_HD double* part(int w, int i) const { return mb_lds(parts + 6 * ((int64_t)w * nj + i)); }
-  MB_HD Mask* anc(int i) const { return (Mask*)(base + kWPerJoint * nj) + i; }  // ancestors-or-self dofs
-  MB_HD double* root_a() const { return mb_lds(base + kWPerJoint * nj + nj); }
-  MB_HD static int64_t doubles(int nj) { return (int64_t)kWPerJoint * nj + nj + 6; }
+  MB_HD Mask* anc(int i) const { return (Mask*)(base + kWRec * nj) + i; }  // ancestors-or-self dofs
+  MB_HD double* root_a() const { return mb_lds(base + kWRec * nj + nj); }
+  // the L records, the masks and root_a; the D records
+  MB_HD static int64_t lsize(int nj) { return pad2((int64_t)kWRec * nj + nj + 6); }
+  MB_HD static int64_t dsize(int nj) { return (int64_t)kWRec * nj; }
+  MB_HD static int64_t doubles(int nj) { return lsize(nj) + dsize(nj); }
 };
 
 // The per-wave partial sums (RNEA recursions: 6 per dof, composites: 10 per dof) come
@@ -1457,17 +1473,27 @@ MB_HD inline void w_crba_composite_part(const Blk& b, const WVals& W, int j, int
 // store_world: wave 0 also stores the subtree composite about the world origin (W.cm /
 // ch / cI, the calcDiff's recursions): h_O = h + m P, I_O = I + 2 (h.P) 1 - (h P^T +
 // P h^T) + m (|P|^2 1 - P P^T) (the same terms as summing the bodies about the origin).
+// (the partials of the npw waves combined in wave order)
+MB_HD __forceinline__ void w_crba_combine(const WVals& W, int nj, int j, int npw, double* v) {
+  const double* p0 = mb_lds(W.parts + 10 * (int64_t)j);
+  for (int e = 0; e < 10; ++e) v[e] = p0[e];
+  for (int ww = 1; ww < npw; ++ww) {
+    const double* p = mb_lds(W.parts + 10 * ((int64_t)ww * nj + j));
+    for (int e = 0; e < 10; ++e) v[e] += p[e];
+  }
+}
+// combined: the composite about P_j already in W.cm / ch / cI (w_crba_store_local; the
+// partials may be overwritten meanwhile)
 MB_HD inline void w_crba_column(const Blk& b, const WVals& W, int j, double* A, int lda, int w, int nw, int npw,
-                                bool store_world = false) {
+                                bool store_world = false, bool combined = false) {
   double P[3], v[10];
   for (int e = 0; e < 3; ++e) P[e] = W.op(j)[e];
-  {
-    const double* p0 = mb_lds(W.parts + 10 * (int64_t)j);
-    for (int e = 0; e < 10; ++e) v[e] = p0[e];
-    for (int ww = 1; ww < npw; ++ww) {
-      const double* p = mb_lds(W.parts + 10 * ((int64_t)ww * b.nj + j));
-      for (int e = 0; e < 10; ++e) v[e] += p[e];
-    }
+  if (combined) {
+    v[0] = *W.cm(j);
+    for (int e = 0; e < 3; ++e) v[1 + e] = W.ch(j)[e];
+    for (int e = 0; e < 6; ++e) v[4 + e] = W.cI(j)[e];
+  } else {
+    w_crba_combine(W, b.nj, j, npw, v);
   }
   const double m = v[0];
   const double* h = v + 1;
@@ -1518,6 +1544,16 @@ MB_HD inline void w_crba_column(const Blk& b, const WVals& W, int j, double* A, 
     A[(int64_t)j * lda + i] = Mij;
     A[(int64_t)i * lda + j] = Mij;
   }
+}
+
+// lane j: the subtree composite about P_j (the combined partials) into W.cm / ch / cI, so
+// that the columns can overwrite the partials (the rollout's calc, knot_calc_dense_x)
+MB_HD inline void w_crba_store_local(const WVals& W, int nj, int j, int npw) {
+  double v[10];
+  w_crba_combine(W, nj, j, npw, v);
+  *W.cm(j) = v[0];
+  for (int e = 0; e < 3; ++e) W.ch(j)[e] = v[1 + e];
+  for (int e = 0; e < 6; ++e) W.cI(j)[e] = v[4 + e];
 }
 
 // ---- the RNEA recursions split over the waves ---------------------------------
@@ -2768,24 +2804,7 @@ MB_HD __forceinline__ double knot_calc_x(const X& ex, const double* P, int nx, c
     // that no wave runs two of them (a wave pays for the sum of its divergent lanes' paths)
     if (wave > 3) return;
     const int item = 3 * l + (wave - 1);
-    int nn = 0;
-#ifdef MB_CALC_DENSE
-    {
-      const double* cr = b.C;
-      int nw = 0;
-      for (int k = 0; k < b.ncost; ++k) {
-        const CRec C{cr};
-        if (wide_cost(C, nw)) {
-          ++nw;
-        } else {
-          if (item == nn) cv[k] = C.weight() * cost_activation(b, W, C, x, ub, nu, false);
-          ++nn;
-        }
-        cr += C.size();
-      }
-    }
-#endif
-    const int kc = item - nn;
+    const int kc = item;
     if (!imp && kc >= 0 && kc < b.ncon) {
       int row0;
       const CRec C{contact_rec(b, kc, &row0)};
@@ -2816,12 +2835,6 @@ MB_HD __forceinline__ double knot_calc_x(const X& ex, const double* P, int nx, c
           cv[k] = C.weight() * (0.5 * a);
           ++nw;
         }
-#ifdef MB_CALC_DENSE
-        // force costs without active contact rows (lambda = 0); frame velocities, now
-        // that the body velocities exist (impulse knots: rejected by the host)
-        if (force_cost(C.type()) && nc == 0) cv[k] = C.weight() * force_cost_activation(b, C, nullptr, nu);
-        if (C.type() == C_FRAME_VELOCITY && !imp) cv[k] = C.weight() * cost_activation(b, W, C, x, ub, nu);
-#endif
         cr += C.size();
       }
     }
@@ -2839,15 +2852,8 @@ MB_HD __forceinline__ double knot_calc_x(const X& ex, const double* P, int nx, c
   double* const tp = ex.lds(W.parts);
   const TreeWork tw{(Mask*)tp, (Mask*)tp + nj, (Mask*)ex.lds(pb), tp + 2 * nj, ex.lds(flag)};
   // (the device fast path's rows, then D^-1 G^T B, both after the masks and 1 / D)
-#ifdef MB_CALC_DENSE
-  // (the dense factorisation: the blocked Gauss-Jordan on [M | Jc^T | tau - nle])
-  (void)cost_side;
-  (void)tw;
-  bool ok = mb_solve(ex, A, nj, lda, ncol, flag, pb);
-#else
   tree_ltdl(ex, b, W, A, lda, tw, tree_depth(b, W), tp + 3 * nj, cost_side, 1);
   bool ok = tree_solve(ex, b, A, lda, ncol - nj, tw, tp + 3 * nj);
-#endif
   // z, then a (impulse: v+, in tau's slot; z = M^-1 M v = v)
   double* a = imp ? tau : A + (int64_t)lda * (nj + nc);
   if (nc > 0) {
@@ -2914,11 +2920,214 @@ MB_HD __forceinline__ double knot_calc_x(const X& ex, const double* P, int nx, c
   return dt != 0. ? dt * cc : cc;
 }
 
+// LDS (doubles) of the rollout's calc (knot_calc_dense_x): the L records, the small arrays,
+// then one region that first holds the D records and the recursions' partials and, from the
+// CRBA columns on, [M | Jc^T | tau - nle], Jc and the Schur block.
+MB_HD inline int64_t calc_dense_doubles(int nj, int nc = 0) {
+  const int64_t small = 2 * nj + kMaxCosts + 8 + nc + 128;
+  const int64_t rec = WVals::dsize(nj) + part_doubles(nj);
+  const int64_t fac = (int64_t)lda_of(nj) * (nj + nc + 1) + (int64_t)nc * nj + (int64_t)nc * (nc + 1);
+  return WVals::lsize(nj) + pad2(small) + pad2(rec > fac ? rec : fac);
+}
+
+// model->calc as knot_calc_x, with the dense factorisation (the blocked Gauss-Jordan of
+// gj_mfma on [M | Jc^T | tau - nle]) and a smaller LDS footprint: the rollout's workgroups
+// share a CU three at a time on the C5 walk (calc_dense_doubles: 40 KB against
+// calc_work_doubles' 60 KB). The phases run in the order
+//   local placements | walk, world frames | RNEA (tau = nle) | CRBA composites + cost records |
+//   composites stored | CRBA columns into A | Jc, a0, tau column | solve | Schur | a, xnext
+// so that the D records and the partials are dead when the columns write A over them.
+// Every value is formed by the same arithmetic as in knot_calc_x's dense solve of round 5.
+template <class X>
+MB_HD __forceinline__ double knot_calc_dense_x(const X& ex, const double* P, int nx, const double* x, const double* u,
+                                               bool use_u, double* xnext, double* w) {
+  w = ex.lds(w);
+  P = ex.lds(P);
+  const Blk b = parse(P);
+  const bool imp = b.impulse;  // impulse: [M | Jc^T] only, z = v
+  const int nj = b.nj, nq = b.nq, nc = b.nc, nu = nj - b.nun, ncol = imp ? nj + nc : nj + nc + 1;
+  const int lda = lda_of(nj);
+  double* tau = w + WVals::lsize(nj);
+  double* ub = tau + nj;  // u (zero if !use_u)
+  double* cv = ub + nj;   // per-cost activations
+  double* red = cv + kMaxCosts;
+  int* flag = (int*)(red + 2);
+  double* a0 = red + 8;     // nc
+  double* pb = a0 + nc;     // the wide records' lane partials; the Schur block's pivot buffer
+  double* R2 = w + WVals::lsize(nj) + pad2(2 * nj + kMaxCosts + 8 + nc + 128);
+  const WVals W{w, nj, R2 + WVals::dsize(nj), R2};
+  double* A = R2;                          // from the columns on: nj x ncol, ld lda
+  double* Jc = A + (int64_t)lda * ncol;    // nc x nj
+  double* S = Jc + (int64_t)nc * nj;       // nc x (nc + 1), ld nc: [S | Jc z + a0]
+  const int npw = part_waves(ex.nt);
+  ex.run([&](int lane) {
+    if (lane < nu) ub[lane] = use_u ? u[lane] : 0.;
+  });
+  // local placements; the wide records (state / control residuals: x, u only) row-parallel
+  // on waves 3 and 1, their lane partials into pb
+  ex.run([&](int lane) {
+    if (lane < nj) w_joint_local(b, W, x, lane);
+    if (lane >= 64) {
+      const int wave = lane >> 6, l = lane & 63;
+      const double* cr = b.C;
+      int nw = 0;
+      for (int k = 0; k < b.ncost; ++k) {
+        const CRec C{cr};
+        if (wide_cost(C, nw)) {
+          if (wave == (nw == 0 ? 3 : 1)) pb[64 * nw + l] = cost_activation_part(b, C, x, ub, nu, l, 64);
+          ++nw;
+        }
+        cr += C.size();
+      }
+    }
+  });
+  ex.run([&](int lane) {
+    if (lane < nj) {
+      w_walk(b, W, lane);
+      w_joint_world(b, W, lane);
+    }
+  });
+  if (!imp) world_rnea(ex, b, W, x + nq, nullptr, tau);
+  // CRBA composites in wave partials; beside them, on waves 1-3, the other cost records
+  // (force costs without active contact rows: lambda = 0; frame velocities: impulse knots
+  // skip them, as the host rejects them there) and the contacts' position terms (log6 for the
+  // 6D ones): item i on lane i / 3 of wave 1 + i % 3, so that no wave runs two of them
+  ex.run([&](int lane) {
+    const int wave = lane >> 6, l = lane & 63;
+    if (l < nj && wave < npw) w_crba_composite_part(b, W, l, wave, npw);
+    if (wave < 1 || wave > 3) return;
+    const int item = 3 * l + (wave - 1);
+    int nn = 0;
+    const double* cr = b.C;
+    int nw = 0;
+    for (int k = 0; k < b.ncost; ++k) {
+      const CRec C{cr};
+      if (wide_cost(C, nw)) {
+        ++nw;
+      } else {
+        if (item == nn) {
+          double v = cost_activation(b, W, C, x, ub, nu, !imp);
+          if (force_cost(C.type()) && nc == 0) v = force_cost_activation(b, C, nullptr, nu);
+          cv[k] = C.weight() * v;
+        }
+        ++nn;
+      }
+      cr += C.size();
+    }
+    const int kc = item - nn;
+    if (!imp && kc >= 0 && kc < b.ncon) {
+      int row0;
+      const CRec C{contact_rec(b, kc, &row0)};
+      contact_a0_position(b, W, C, a0 + row0);
+    }
+  });
+  ex.run([&](int lane) {
+    if (lane < nj) w_crba_store_local(W, nj, lane, npw);
+  });
+  // (from here on the D records and the partials are dead: A, Jc, S over them)
+  ex.run([&](int lane) {
+    const int wv = lane >> 6, j = lane & 63;
+    if (j < nj) w_crba_column(b, W, j, A, lda, wv, ex.nt >> 6, npw, false, true);
+  });
+  ex.run([&](int lane) {
+    if (lane < nj) {
+      const double ti = lane < b.nun ? 0. : ub[lane - b.nun];  // ActuationModelFloatingBase: tau = [0; u]
+      if (!imp) A[(int64_t)lda * (nj + nc) + lane] = ti - tau[lane];
+      if (nc) contact_jac_lane(b, W, lane, Jc, A, lda);
+    }
+    if (!imp && lane >= 64 && lane < 64 + b.ncon) {
+      int row0;
+      const CRec C{contact_rec(b, lane - 64, &row0)};
+      contact_a0_drift(b, W, C, a0 + row0);
+    }
+    if (lane == 128) {  // the wide records' values from their lane partials
+      const double* cr = b.C;
+      int nw = 0;
+      for (int k = 0; k < b.ncost; ++k) {
+        const CRec C{cr};
+        if (wide_cost(C, nw)) {
+          double a = 0.;
+          for (int l = 0; l < 64; ++l) a += pb[64 * nw + l];
+          cv[k] = C.weight() * (0.5 * a);
+          ++nw;
+        }
+        cr += C.size();
+      }
+    }
+  });
+  bool ok = mb_solve(ex, A, nj, lda, ncol, flag, pb);
+  // z, then a (impulse: v+, in tau's slot; z = M^-1 M v = v)
+  double* a = imp ? tau : A + (int64_t)lda * (nj + nc);
+  if (nc > 0) {
+    ex.run([&](int lane) {
+      for (int e = lane; e < nc * (nc + 1); e += ex.nt) {
+        const int col = e / nc, row = e % nc;
+        const double* yc = (imp && col == nc) ? x + nq : A + (int64_t)lda * (nj + col);
+        double s = 0.;
+        for (int i = 0; i < nj; ++i) s += Jc[(int64_t)row * nj + i] * yc[i];
+        S[e] = col < nc ? s + (row == col ? b.damping : 0.) : (imp ? (1. + b.r_coeff) * s : s + a0[row]);
+      }
+    });
+    ok = gauss_jordan<1>(ex, S, nc, nc, nc + 1, flag, pb) && ok;
+    ex.run([&](int lane) {
+      const int kf = lane - 64;
+      if (kf >= 0 && kf < b.ncost && !imp) {
+        const double* cr = b.C;
+        for (int k = 0; k < kf; ++k) cr += CRec{cr}.size();
+        const CRec C{cr};
+        if (force_cost(C.type())) {
+          double lamv[kMaxNc];
+          for (int k = 0; k < nc; ++k) lamv[k] = -S[(int64_t)nc * nc + k];
+          cv[kf] = C.weight() * force_cost_activation(b, C, lamv, nu);
+        }
+      }
+      if (lane >= nj) return;
+      double s = imp ? x[nq + lane] : a[lane];
+      for (int k = 0; k < nc; ++k) s -= A[(int64_t)lda * (nj + k) + lane] * S[(int64_t)nc * nc + k];
+      a[lane] = s;
+    });
+  }
+  const double dt = b.dt;
+  if (!ok)
+    ex.run([&](int i) {
+      if (i < nj) a[i] = NAN;
+    });
+  ex.run([&](int i) {
+    if (i == 64) {
+      double total = 0.;
+      for (int k = 0; k < b.ncost; ++k) total += cv[k];
+      red[0] = total;
+    }
+    if (i >= nj) return;
+    if (imp) {
+      xnext[nq + i] = nc > 0 ? a[i] : x[nq + i];
+      if (!ok) xnext[nq + i] = NAN;
+      xnext[i] = x[i];
+      if (i == nj - 1 && b.ff) xnext[nq - 1] = x[nq - 1];
+      return;
+    }
+    if (dt != 0.) {
+      euler_step(b, x, a, dt, xnext, i);
+    } else {
+      xnext[i] = x[i];
+      xnext[nq + i] = x[nq + i];
+      if (i == nj - 1 && b.ff) xnext[nq - 1] = x[nq - 1];
+    }
+  });
+  const double cc = red[0];
+  (void)nx;
+  return dt != 0. ? dt * cc : cc;
+}
+
 template <int NT>
 __device__ __forceinline__ double knot_calc(const double* P, int nx, const double* x, const double* u, bool use_u, double* xnext,
                                    double* w) {
   static_assert(NT >= 256, "the multibody calc splits its phases over 4 waves");
+#ifdef MB_CALC_DENSE
+  return knot_calc_dense_x(DevExec{NT}, P, nx, x, u, use_u, xnext, w);
+#else
   return knot_calc_x(DevExec{NT}, P, nx, x, u, use_u, xnext, w);
+#endif
 }
 
 // ---------------------------------------------------------------------------

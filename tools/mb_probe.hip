@@ -165,7 +165,11 @@ __global__ __launch_bounds__(256) void probe_calc(const double* Pg, int nx, cons
                                                   int use_u, double* out, unsigned long long* stamps) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
   const int psz = (int)Pg[3];
+#ifdef MB_CALC_DENSE
+  const int64_t w = pad2(calc_dense_doubles((int)Pg[1], parse(Pg).nc));
+#else
   const int64_t w = pad2(calc_work_doubles((int)Pg[1], parse(Pg).nc));
+#endif
   double* P = sm + w;
   unsigned long long* st = (unsigned long long*)(P + pad2(psz));
   for (int e = threadIdx.x; e < psz; e += 256) P[e] = Pg[e];
@@ -175,7 +179,11 @@ __global__ __launch_bounds__(256) void probe_calc(const double* Pg, int nx, cons
   }
   __syncthreads();
   StampExec ex{256, st};
+#ifdef MB_CALC_DENSE
+  const double c = knot_calc_dense_x(ex, P, nx, xg, ug, use_u != 0, out + (int64_t)blockIdx.x * (nx + 1), sm);
+#else
   const double c = knot_calc_x(ex, P, nx, xg, ug, use_u != 0, out + (int64_t)blockIdx.x * (nx + 1), sm);
+#endif
   if (threadIdx.x == 0) out[(int64_t)blockIdx.x * (nx + 1) + nx] = c;
   __syncthreads();
   if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -218,7 +226,11 @@ int main(int argc, char** argv) {
                         : diff_spill(nj, njac, bk.nc, vc, bk.nj - bk.nun, count_cost_rows(bk, bk.nj - bk.nun), psz, m);
   const DiffLayout l = diff_layout(nj, njac, bk.nc, vc, bk.nj - bk.nun, count_cost_rows(bk, bk.nj - bk.nun), spill);
   const size_t smd = 8 * (pad2(l.total) + pad2(psz) + 256);
+#ifdef MB_CALC_DENSE
+  const size_t smc = 8 * (pad2(calc_dense_doubles(nj, bk.nc)) + pad2(psz) + 256);
+#else
   const size_t smc = 8 * (pad2(calc_work_doubles(nj, bk.nc)) + pad2(psz) + 256);
+#endif
   printf("nj %d nx %d nu %d m %d psz %d lds diff %zu calc %zu\n", nj, nx, nu, m, psz, smd, smc);
   printf("  layout (spill %d): wv %ld A %ld half %ld dtau %ld da %ld qp %ld vec %ld J %ld red %ld Jc %ld Y %ld da0 %ld R %ld total %ld (njac %d vcols %d nc %d nrows %d)\n",
          spill, (long)l.wv, (long)l.A, (long)l.half, (long)l.dtau, (long)l.da, (long)l.qp, (long)l.vec, (long)l.J,
