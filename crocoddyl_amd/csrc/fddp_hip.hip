@@ -57,10 +57,13 @@ hipError_t mb_knot(int v, dim3 grid, size_t smem, hipStream_t s, const Dev& D, i
     default: return mb_knot_0(grid, smem, s, D, sel_calc, sel_diff);
   }
 }
-const void* forward_fn(int v) { return v == FWD_MB ? forward_fn_1() : forward_fn_0(v); }
+const void* forward_fn(int v) {
+  return v == FWD_MB ? forward_fn_1() : v == FWD_MB2 ? forward_fn_2() : forward_fn_0(v);
+}
 hipError_t forward(int v, dim3 grid, size_t smem, hipStream_t s, const Dev& D, const Prm& prm, int mode, double alpha,
                    int* count, int64_t pcap, int group) {
   if (v == FWD_MB) return forward_1(grid, smem, s, D, prm, mode, alpha, count, pcap, group);
+  if (v == FWD_MB2) return forward_2(grid, smem, s, D, prm, mode, alpha, count, pcap, group);
   return forward_0(v, grid, smem, s, D, prm, mode, alpha, count, pcap, group);
 }
 int backward_mfma_setup(int ntl, int mtl, int nw, int n, int* per_cu) {
@@ -343,6 +346,7 @@ struct fddp_handle_s {
   bool npar_adapt = false;  // trial-group size re-chosen after every solve (choose_npar)
   bool npar_chosen = false;  // choose_npar has set D.npar
   double ls_slots = 0.;     // rollout workgroups resident on the device at once
+  int fwd_mb_variant = -1;  // rollout_variant's choice (-1: not yet made; reset by apply_knots)
   hipStream_t stream = nullptr;
   std::vector<fddp_knot_desc> knots;
   int64_t n_params = 0;
@@ -599,6 +603,37 @@ static bool mb_rollout(const fddp_handle* h) {
   return h->all_mb && !off;
 }
 
+// Workgroups of `fn` one CU holds at once with `smem` bytes of dynamic LDS: the occupancy
+// API's answer, capped by the LDS allocated in 2 KB granules (measured on gfx950,
+// tools/occ_probe.hip: 53,248 B per workgroup fit three per CU, 53,776 B two, where the API
+// still says three).
+static int resident_per_cu(const void* fn, size_t smem) {
+  int per_cu = 0;
+  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kNT, smem);
+  hipFuncAttributes fa{};
+  (void)hipFuncGetAttributes(&fa, fn);
+  const size_t g = 2048, lds = ((smem + fa.sharedSizeBytes + g - 1) / g) * g;
+  const int by_lds = lds > 0 ? (int)((160 * 1024) / lds) : per_cu;
+  return std::max(1, std::min(per_cu, by_lds));
+}
+// The rollout variant: the generic one for mixed horizons; for multibody-only horizons the
+// three-workgroups-per-CU build (168 VGPRs, spills) when its LDS allows three per CU and the
+// batch needs more than two per CU, else the 256-VGPR build (FDDP_FWD_MBW=2|3 forces one).
+static int rollout_variant(fddp_handle* h) {
+  if (!mb_rollout(h)) return ktab::FWD_GENERIC;
+  if (h->fwd_mb_variant >= 0) return h->fwd_mb_variant;
+  static const int env = [] {
+    const char* e = std::getenv("FDDP_FWD_MBW");
+    return e ? std::atoi(e) : 0;
+  }();
+  int dev_cus = 0;
+  (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, h->device);
+  const bool three = resident_per_cu(ktab::forward_fn(ktab::FWD_MB), h->fwd_smem) >= 3;
+  const bool take3 = env ? env == 3 : (three && h->D.B > 2 * std::max(1, dev_cus));
+  h->fwd_mb_variant = take3 ? ktab::FWD_MB : ktab::FWD_MB2;
+  return h->fwd_mb_variant;
+}
+
 // Trial-group size of the next line searches from the trial counts of the last one
 // (the results are bit-identical for every size; only the work and the number of
 // sequential launches change). With S rollout workgroups resident at once and t_b the
@@ -608,10 +643,9 @@ static void choose_npar(fddp_handle* h, const std::vector<ElemState>& st) {
   if (!h->npar_adapt || h->fast) return;
   const int na = h->prm.n_alphas;
   if (h->ls_slots <= 0.) {
-    int dev_cus = 0, per_cu = 0;
+    int dev_cus = 0;
     (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, h->device);
-    const void* k = ktab::forward_fn(mb_rollout(h) ? ktab::FWD_MB : ktab::FWD_GENERIC);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, kNT, h->fwd_smem);
+    const int per_cu = resident_per_cu(ktab::forward_fn(rollout_variant(h)), h->fwd_smem);
     h->ls_slots = (double)std::max(1, dev_cus) * std::max(1, per_cu);
     if (std::getenv("FDDP_STAMPS"))  // (diagnostic runs: the rollout's residency)
       std::fprintf(stderr, "[fddp] rollout: %d workgroups per CU x %d CUs (LDS %zu B per workgroup)\n", per_cu, dev_cus,
@@ -703,7 +737,7 @@ int launch_forward(fddp_handle* h, int mode, double alpha, int* count) {
     const int na = h->prm.n_alphas, G = (na + D.npar - 1) / D.npar;
     h->ls_npar_last = D.npar;
     h->ls_launches_last = G;
-    const int v = mb_rollout(h) ? ktab::FWD_MB : ktab::FWD_GENERIC;
+    const int v = rollout_variant(h);
     for (int g = 0; g < G; ++g) {
       KLAUNCH(ktab::forward(v, dim3(D.B, D.npar), h->fwd_smem, h->stream, D, to_prm(h->prm), 2, 1., nullptr, h->pcap,
                             g));
@@ -719,7 +753,7 @@ int launch_forward(fddp_handle* h, int mode, double alpha, int* count) {
     KLAUNCH(ktab::forward(ktab::FWD_FAST, dim3(D.B), h->fwd_fast_smem, h->stream, D, to_prm(h->prm), mode, alpha,
                           count, h->pcap, 0));
   else
-    KLAUNCH(ktab::forward(mb_rollout(h) ? ktab::FWD_MB : ktab::FWD_GENERIC, dim3(D.B), h->fwd_smem, h->stream, D,
+    KLAUNCH(ktab::forward(rollout_variant(h), dim3(D.B), h->fwd_smem, h->stream, D,
                           to_prm(h->prm), mode, alpha, count, h->pcap, 0));
   return FDDP_OK;
 }
@@ -826,6 +860,15 @@ int apply_knots(fddp_handle* h, const fddp_knot_desc* knots, const double* param
     int mb_nj = 0, mb_njac = 0, mb_nc = 0;
     bool mb_vcols = false;
     int mb_nu = 0, mb_nrows = 0;
+    // each multibody block's own shape: the device lays out a knot's calcDiff LDS from its
+    // own block, so the plan to allocate is the largest knot's, not the plan of the largest
+    // value of every parameter (on the Solo12 trot those come from different knots: 82.2 KB,
+    // one workgroup per CU, against the largest knot's 79.6 KB)
+    struct MbShape {
+      int nj, njac, nc, nu, nrows;
+      bool vcols;
+    };
+    std::vector<MbShape> shapes;
     h->has_mb = false;
     for (int t = 0; t <= d.T; ++t) {
       int64_t sz;
@@ -836,8 +879,20 @@ int apply_knots(fddp_handle* h, const fddp_knot_desc* knots, const double* param
         for (int b = 0; b < nb; ++b) {  // validated by check_knots
           const int64_t off = knots[t].param_offset + (int64_t)b * knots[t].param_stride;
           std::string why;
-          sz = std::max(sz, mb_block_check(params + off, n_params - off, knots[t].kind, d.nx, knots[t].nu, why, &mb_nj,
-                                           &mb_njac, &mb_nc, &mb_vcols, &mb_nu, &mb_nrows));
+          MbShape k{0, 0, 0, 0, 0, false};
+          sz = std::max(sz, mb_block_check(params + off, n_params - off, knots[t].kind, d.nx, knots[t].nu, why, &k.nj,
+                                           &k.njac, &k.nc, &k.vcols, &k.nu, &k.nrows));
+          mb_nj = std::max(mb_nj, k.nj);
+          mb_njac = std::max(mb_njac, k.njac);
+          mb_nc = std::max(mb_nc, k.nc);
+          mb_vcols = mb_vcols || k.vcols;
+          mb_nu = std::max(mb_nu, k.nu);
+          mb_nrows = std::max(mb_nrows, k.nrows);
+          bool seen = false;
+          for (const MbShape& q : shapes)
+            seen = seen || (q.nj == k.nj && q.njac == k.njac && q.nc == k.nc && q.nu == k.nu && q.nrows == k.nrows &&
+                            q.vcols == k.vcols);
+          if (!seen) shapes.push_back(k);
         }
       } else {
         sz = block_doubles(knots[t].kind, d.nx, knots[t].nu);
@@ -872,11 +927,18 @@ int apply_knots(fddp_handle* h, const fddp_knot_desc* knots, const double* param
       const char* e = std::getenv("FDDP_MB_SPILL");
       return e ? std::atoi(e) : -1;
     }();
-    D.mbspill = h->has_mb && spill_env != 0
+    auto plan_doubles = [&](int spill) {  // the largest knot's plan under spill flags `spill`
+      int64_t mx = 0;
+      for (const MbShape& q : shapes)
+        mx = std::max<int64_t>(mx, pad2(fddp::mb::diff_layout(q.nj, q.njac, q.nc, q.vcols, q.nu, q.nrows, spill).total));
+      return mx;
+    };
+    // (the spill flags themselves from the largest value of every parameter: the spilled
+    // arrays must fit their output blocks on every knot)
+    D.mbspill = h->has_mb && spill_env != 0 && (plan_doubles(0) + pad2(mb_pmax)) * 8 > 80 * 1024
                     ? fddp::mb::diff_spill(mb_nj, mb_njac, mb_nc, mb_vcols, mb_nu, mb_nrows, mb_pmax, D.m)
                     : 0;
-    D.mbd = h->has_mb ? pad2(fddp::mb::diff_layout(mb_nj, mb_njac, mb_nc, mb_vcols, mb_nu, mb_nrows, D.mbspill).total)
-                      : 0;
+    D.mbd = h->has_mb ? plan_doubles(D.mbspill) : 0;
     h->mb_diff_smem = h->has_mb ? sizeof(double) * (D.mbd + pad2(mb_pmax)) : 0;
     const int64_t budget = (150 * 1024) / 8 - (2 * D.sX + D.sM + 2 * D.sN + 5 * (kNT / kWave) + 16) - D.mbw;
     // LDS-staged parameter blocks up to pcap doubles; larger (dense) blocks are read from
@@ -892,6 +954,8 @@ int apply_knots(fddp_handle* h, const fddp_knot_desc* knots, const double* param
   D.dxv_mbw = D.mbw_fwd >= (int64_t)D.m * D.n + 2 * D.sN ? 1 : 0;
   h->fwd_smem = sizeof(double) * (h->pcap + fwd_lds_doubles<kNT, false>(D.sX, D.sN, D.sM) - (D.dxv_mbw ? 2 * D.sN : 0) +
                                   D.mbw_fwd);
+  h->fwd_mb_variant = -1;  // (re-chosen with the new LDS size)
+  h->ls_slots = 0.;
   h->calc_smem = sizeof(double) * (h->pcap + 2 * D.sX + D.sM + 5 * (kNT / kWave) + 16 + D.mbw);
   h->cdiff_smem = sizeof(double) * (h->pcap + D.sX + D.sM);
   {  // dense-knot fast path: every knot LQR / Euler∘DiffLQR, block LDS-resident
@@ -946,6 +1010,7 @@ int apply_knots(fddp_handle* h, const fddp_knot_desc* knots, const double* param
         {ktab::forward_fn(ktab::FWD_GENERIC), h->fwd_smem, true, "forward_kernel"},
         {ktab::forward_fn(ktab::FWD_FAST), h->fwd_fast_smem, true, "forward_kernel<fast>"},
         {ktab::forward_fn(ktab::FWD_MB), h->fwd_smem, h->has_mb, "forward_kernel<multibody>"},
+        {ktab::forward_fn(ktab::FWD_MB2), h->fwd_smem, h->has_mb, "forward_kernel<multibody, 2 waves/EU>"},
         {ktab::calc_tiled_fn(), h->fused_smem, true, "calc_tiled_kernel"},
         {ktab::calc_fn(), h->calc_smem, true, "calc_kernel"},
         {ktab::calc_diff_fn(), h->cdiff_smem, true, "calc_diff_kernel"},

@@ -998,8 +998,10 @@ __device__ __forceinline__ void ls_finish(const Prm& prm, ElemState& s, bool acc
 #endif
 // (the generic variant, for horizons that mix multibody and dense knots, gets the
 // whole register file: under the 2-waves cap its spills trip a backend error)
-template <int NT, bool FAST, bool MB = false>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MB ? FDDP_FWD_WPE_MB : FAST ? FDDP_FWD_WPE : 1))) void forward_kernel(Dev D, Prm prm, int mode, double alpha1, int* active_count,
+// MBW: waves per EU of the multibody variant (3: three workgroups per CU where the LDS
+// allows it, at 168 VGPRs; 2: the 256-VGPR build for batches that fit two per CU anyway)
+template <int NT, bool FAST, bool MB = false, int MBW = FDDP_FWD_WPE_MB>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MB ? MBW : FAST ? FDDP_FWD_WPE : 1))) void forward_kernel(Dev D, Prm prm, int mode, double alpha1, int* active_count,
                                                      int64_t pcap, int group = 0) {
   // (workgroups are dispatched roughly in index order: the elements whose last line
   // search took the most trials start first, so they do not trail the launch)

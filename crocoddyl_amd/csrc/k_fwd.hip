@@ -1,6 +1,7 @@
 // Line-search rollout kernels (fddp_kernels.hpp forward_kernel, ls_select_kernel).
-// FDDP_TU_FWD = 0: the generic and dense fast-path variants + ls_select; 1: the
-// multibody-only variant (the large one), so the two compile in parallel.
+// FDDP_TU_FWD = 0: the generic and dense fast-path variants + ls_select; 1 / 2: the
+// multibody-only variants at three / two waves per EU (the large ones), so they compile in
+// parallel.
 // The rollout's knot calc solves [M | Jc^T | tau - nle] by the dense blocked Gauss-Jordan
 // (multibody.hpp MB_CALC_DENSE): measured on the C5 walk, the tree-sparse LTDL with the
 // cost records on its idle waves has to be called out of line here (the backend's register
@@ -12,7 +13,7 @@
 #include "ktab.hpp"
 
 #ifndef FDDP_TU_FWD
-#error "k_fwd.hip is compiled with -DFDDP_TU_FWD=0|1"
+#error "k_fwd.hip is compiled with -DFDDP_TU_FWD=0|1|2"
 #endif
 
 namespace fddp {
@@ -32,6 +33,14 @@ hipError_t forward_0(int v, dim3 grid, size_t smem, hipStream_t s, const Dev& D,
 }
 hipError_t ls_select(dim3 grid, hipStream_t s, const Dev& D, const Prm& prm, int group, int last, int* count) {
   hipLaunchKernelGGL((ls_select_kernel<kNT>), grid, dim3(kNT), 0, s, D, prm, group, last, count);
+  return hipGetLastError();
+}
+#elif FDDP_TU_FWD == 2
+const void* forward_fn_2() { return (const void*)forward_kernel<kNT, false, true, 2>; }
+hipError_t forward_2(dim3 grid, size_t smem, hipStream_t s, const Dev& D, const Prm& prm, int mode, double alpha,
+                     int* count, int64_t pcap, int group) {
+  hipLaunchKernelGGL((forward_kernel<kNT, false, true, 2>), grid, dim3(kNT), smem, s, D, prm, mode, alpha, count, pcap,
+                     group);
   return hipGetLastError();
 }
 #else

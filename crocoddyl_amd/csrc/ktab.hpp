@@ -26,8 +26,9 @@ const void* mb_knot_fn(int v);
 hipError_t mb_knot(int v, dim3 grid, size_t smem, hipStream_t s, const Dev& D, int sel_calc, int sel_diff);
 
 // Line-search rollout (k_fwd.hip): FWD_GENERIC any knot mix, FWD_FAST the dense-knot
-// fast path, FWD_MB multibody-only horizons
-enum { FWD_GENERIC = 0, FWD_FAST = 1, FWD_MB = 2 };
+// fast path, FWD_MB multibody-only horizons at three workgroups per CU (168 VGPRs),
+// FWD_MB2 the same at two (256 VGPRs)
+enum { FWD_GENERIC = 0, FWD_FAST = 1, FWD_MB = 2, FWD_MB2 = 3 };
 const void* forward_fn(int v);
 hipError_t forward(int v, dim3 grid, size_t smem, hipStream_t s, const Dev& D, const Prm& prm, int mode, double alpha,
                    int* count, int64_t pcap, int group);
@@ -78,6 +79,9 @@ hipError_t forward_0(int v, dim3 grid, size_t smem, hipStream_t s, const Dev& D,
                      double alpha, int* count, int64_t pcap, int group);
 const void* forward_fn_1();
 hipError_t forward_1(dim3 grid, size_t smem, hipStream_t s, const Dev& D, const Prm& prm, int mode, double alpha,
+                     int* count, int64_t pcap, int group);
+const void* forward_fn_2();
+hipError_t forward_2(dim3 grid, size_t smem, hipStream_t s, const Dev& D, const Prm& prm, int mode, double alpha,
                      int* count, int64_t pcap, int group);
 int backward_mfma_setup_0(int ntl, int mtl, int nw, int n, int* per_cu);  // -2: not in this object
 int backward_mfma_setup_1(int ntl, int mtl, int nw, int n, int* per_cu);
