@@ -562,9 +562,13 @@ __device__ __forceinline__ bool fwd_trial_fast(const Dev& D, int b, const ElemSt
   constexpr int KMAX = 16;
   const int kcols = rk.on ? (n - rk.g + rk.G - 1) / rk.G : 0;
   const bool kreg = (n + rk.G - 1) / rk.G <= KMAX;
-  // knots t+1..t+PD in flight in registers (rotating window; deeper windows
-  // measured slower: register pressure)
-  constexpr int PD = 1;
+  // knots t+1..t+PD in flight in registers (rotating window). Two knots ahead: C2's knot
+  // 13.5k -> 12.6k cycles (phase stamps, wave 0), rollout 0.60 -> 0.57 ms, at 256 VGPRs
+  // and 2 spills; deeper windows measured slower (register pressure)
+#ifndef FDDP_FAST_PD
+#define FDDP_FAST_PD 2
+#endif
+  constexpr int PD = FDDP_FAST_PD;
   double pK[PD][KMAX];
   double pxs[PD], pfs[PD], pvf[PD], pus[PD], pkv[PD], plb[PD], pub[PD];
   auto fetch = [&](int t, int q) {
@@ -597,6 +601,8 @@ __device__ __forceinline__ bool fwd_trial_fast(const Dev& D, int b, const ElemSt
   };
 #pragma unroll
   for (int q = 0; q < PD; ++q) fetch(q, q);
+  // (diagnostic phase timer, FDDP_STAMPS=1 on the stamps build: per wave, summed)
+  Stamp stamp(D.stamps && wid == 0 ? D.stamps + (int64_t)D.B * 128 + (int64_t)b * 8 : nullptr);  // (wave 0's)
   __syncthreads();
   for (int t = 0; t <= T; ++t) {
     const int64_t kk = D.knot(b, t);
@@ -634,9 +640,11 @@ __device__ __forceinline__ bool fwd_trial_fast(const Dev& D, int b, const ElemSt
       pd = wave_sum(pd);
       if (lane == 0) red[8 + wid] = pd;
     }
+    stamp.mark(0);
     stage_params_batched<NT>(D.params + kd.param_offset + (int64_t)b * kd.param_stride, block_doubles_dev(kd.kind, nx, nu), pl, cached);
     const double* P = pl;
     __syncthreads();
+    stamp.mark(1);
     if (running) {
       // us_try = us - k * alpha - K * dx
       if (rk.on) {
@@ -665,6 +673,7 @@ __device__ __forceinline__ bool fwd_trial_fast(const Dev& D, int b, const ElemSt
       }
       __syncthreads();
     }
+    stamp.mark(2);
     const DenseKnot K(kd.kind, P, nx, nu);
     double cp = dense_partials<NT>(K, nx, nu, running && nu > 0, xu, running, false, false, true, pdyn, nullptr,
                                    nullptr, tid);
@@ -684,11 +693,14 @@ __device__ __forceinline__ bool fwd_trial_fast(const Dev& D, int b, const ElemSt
       D.dvp[kk] = feas ? 0. : p2;
     }
     __syncthreads();  // xn complete; red / pa / pdyn free
+    stamp.mark(3);
     if (running && tid < nx) {
       D.xnext[o][D.run(b, t) * D.sX + tid] = xn[tid];
       bad |= bad_entry(xn[tid]);
     }
+    stamp.mark(4);
   }
+  stamp.flush();
   // cost_try in knot order with raiseIfNaN on every partial sum (fddp.cpp:
   // 189-196); dv: terminal first, then t = 0..T-1 (fddp.cpp:110-119)
   __syncthreads();

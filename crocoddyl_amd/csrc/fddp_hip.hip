@@ -1228,9 +1228,10 @@ void fddp_destroy(fddp_handle* h) {
         }
         std::fprintf(stderr, "\n");
       }
-      if (h->has_mb) {
+      if (h->has_mb || h->fast) {
         const char* mn[5] = {"state", "params", "gains", "calc", "stores_checks"};
-        std::fprintf(stderr, "[fddp stamps] multibody rollout, mean cycles per element summed over waves (all trials):");
+        std::fprintf(stderr, "[fddp stamps] %s rollout, wave 0's mean cycles per element (all trials):",
+                     h->fast ? "dense fast-path" : "multibody");
         for (int ph = 0; ph < 5; ++ph) {
           double s2 = 0;
           for (int b = 0; b < h->dims.B; ++b) s2 += (double)v[(size_t)h->dims.B * 128 + (size_t)b * 8 + ph];

@@ -779,7 +779,7 @@ __device__ __forceinline__ bool fwd_trial(const Dev& D, int b, const ElemState& 
   cost_try = 0.;
   double* dvp = out.dvp + D.knot(b, 0);
   // (diagnostic phase timer, FDDP_STAMPS=1 on the stamps build: per wave, summed)
-  Stamp stamp(D.stamps ? D.stamps + (int64_t)D.B * 128 + (int64_t)b * 8 : nullptr);
+  Stamp stamp(D.stamps && tid < kWave ? D.stamps + (int64_t)D.B * 128 + (int64_t)b * 8 : nullptr);  // (wave 0's)
   __syncthreads();
   for (int t = 0; t <= T; ++t) {
     const int64_t kk = D.knot(b, t);
