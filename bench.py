@@ -712,7 +712,8 @@ def main():
             Yc = calc_diff_bytes_per_knot(nx, n, m, psz) * nk
             rooflines["calcDiff"] = (cd_ms, knot_roof(
                 "knot-parallel calcDiff (mb_knot_kernel / calc_diff_kernel) + gaps", cd_ms, cd_n, Yc,
-                kfl[1] * nk if kfl else None, (kpm.get("mb_calc_diff") or {}).get("hbm_bytes_per_step"),
+                kfl[1] * nk if kfl else None,
+                (kpm.get("mb_calc_diff") or kpm.get("calc_fused") or {}).get("hbm_bytes_per_step"),
                 {"knots_per_launch": nk}))
         dominant = max(rooflines, key=lambda k: rooflines[k][0])
         roof = dict(rooflines[dominant][1], dominant_of=sorted(rooflines), pmc=pmc_prov)

@@ -34,7 +34,7 @@ CLASSES = {  # bench.py's rooflines keys -> kernel name fragments
     "backward": ("backward_mfma_kernel", "backward_kernel"),
     "forward": ("forward_kernel",),
     "mb_calc_diff": ("mb_knot_kernel",),
-    "calc_fused": ("calc_fused_kernel",),
+    "calc_fused": ("calc_tiled_kernel", "calc_diff_kernel"),  # the dense knots' calc / calcDiff
 }
 
 
