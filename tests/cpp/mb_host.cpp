@@ -85,6 +85,20 @@ int mb_host_plan(const double* P, int m, int64_t* lds_bytes) {
 }
 
 extern "C" {
+// The multibody rollout's dynamic LDS per workgroup for a block (fddp_hip.hip apply_knots):
+// the staged parameter block, the trial's vectors (x, u, next x, the sums, the flag; dx in
+// the knot calc's scratch) and the dense knot calc's scratch (calc_dense_doubles, also in
+// *dense); in *work the tree calc's scratch (calc_work_doubles), for comparison.
+int64_t mb_host_rollout_lds(const double* P, int nx, int nu_max, int64_t* dense, int64_t* work) {
+  const Blk b = parse(P);
+  const int64_t sX = fddp::pad2(nx), sM = fddp::pad2(nu_max);
+  *dense = fddp::pad2(calc_dense_doubles(b.nj, b.nc));
+  *work = fddp::pad2(calc_work_doubles(b.nj, b.nc));
+  return 8 * (fddp::pad2((int64_t)P[3]) + 2 * sX + sM + 5 * 4 + 8 + 2 + *dense);
+}
+}
+
+extern "C" {
 // The static check of a calcDiff plan (multibody.hpp diff_layout_check): 0, or 1 with the
 // conflicting pair's names in msg.
 int mb_host_layout_check(int nj, int njac, int nc, int vcols, int nu, int nrows, int spill, char* msg, int cap) {

@@ -180,3 +180,28 @@ def test_talos_spilled_plan_equals_lds_plan(lib, talos_walk, t, monkeypatch):  #
     for a, b in zip(*outs):
         np.testing.assert_array_equal(a, b)
 
+
+
+def test_talos_rollout_fits_three_workgroups_per_cu(lib, talos_walk):  # noqa: F811
+    """The multibody rollout's LDS on the C5 walk's knots (the dense knot calc of
+    multibody.hpp knot_calc_dense_x, its factorisation over the dead recursion records,
+    and dx in that scratch's tail): at most 53,248 B per workgroup with 256 B to spare for
+    the kernel's static LDS, i.e. three workgroups per CU with the LDS allocated in 2 KB
+    granules (tools/occ_probe.hip: 53,248 B fit three, 53,776 B two); the dense calc's
+    scratch is smaller than the tree calc's."""
+    import ctypes as C
+    g, models = talos_walk
+    lib.mb_host_rollout_lds.restype = C.c_int64
+    lib.mb_host_rollout_lds.argtypes = [C.POINTER(C.c_double), C.c_int, C.c_int, C.POINTER(C.c_int64),
+                                        C.POINTER(C.c_int64)]
+    nu_max = max(m.nu for m in models)
+    worst = 0
+    for model in models:
+        kind, nu, blk = model.pack()
+        blk = np.ascontiguousarray(blk[0])
+        dense, work = C.c_int64(0), C.c_int64(0)
+        lds = lib.mb_host_rollout_lds(_p(blk), model.state.nx, nu_max, C.byref(dense), C.byref(work))
+        assert dense.value < work.value, (dense.value, work.value)
+        worst = max(worst, lds)
+    granule = 2048
+    assert 3 * (-(-(worst + 256) // granule) * granule) <= 160 * 1024, worst
